@@ -1,0 +1,129 @@
+"""In-tree native build (no JIT cache, no hipify, no setuptools CUDAExtension).
+
+Compiles every ``csrc/**/*.hip`` with ``hipcc --offload-arch=gfx950`` (device
+kernels + their host launchers, no torch headers -> seconds per file) and every
+``csrc/**/*.cpp`` (torch/pybind11 bindings, C++ runtime: communicator, reducer,
+engine) with hipcc as host C++, then links ONE shared object
+``cs744_pytorch_distributed_tutorial_amd/_C.so`` against the HIP/RCCL/torch
+libraries that ship inside the installed torch wheel (so the process has exactly
+one HIP runtime and one RCCL, SURVEY.md §5.8 "Library pitfall").
+
+Incremental: an object is rebuilt when its source or any header under
+``csrc/`` is newer. Usage: ``python -m cs744_pytorch_distributed_tutorial_amd._build [-j N] [--force]``.
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import glob
+import os
+import subprocess
+import sys
+import sysconfig
+import time
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG_DIR)
+CSRC = os.path.join(ROOT, "csrc")
+BUILD = os.path.join(ROOT, "build", "obj")
+OUT = os.path.join(PKG_DIR, "_C.so")
+ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+HIPCC = os.path.join(ROCM, "bin", "hipcc")
+
+
+def _torch_paths():
+    import torch
+    tdir = os.path.dirname(torch.__file__)
+    inc = [os.path.join(tdir, "include"), os.path.join(tdir, "include", "torch", "csrc", "api", "include")]
+    return tdir, inc, os.path.join(tdir, "lib")
+
+
+def _sources():
+    hip = sorted(glob.glob(os.path.join(CSRC, "**", "*.hip"), recursive=True))
+    cpp = sorted(glob.glob(os.path.join(CSRC, "**", "*.cpp"), recursive=True))
+    return hip, cpp
+
+
+def _headers_mtime() -> float:
+    hs = glob.glob(os.path.join(CSRC, "**", "*.h"), recursive=True) + \
+        glob.glob(os.path.join(CSRC, "**", "*.hpp"), recursive=True) + \
+        glob.glob(os.path.join(CSRC, "**", "*.cuh"), recursive=True)
+    return max([os.path.getmtime(h) for h in hs] + [0.0])
+
+
+def _obj_path(src: str) -> str:
+    rel = os.path.relpath(src, CSRC).replace(os.sep, "__")
+    return os.path.join(BUILD, rel + ".o")
+
+
+def _common_flags():
+    return ["-O3", "-std=c++17", "-fPIC", f"-I{CSRC}", "-D__HIP_PLATFORM_AMD__", "-Wno-unused-result",
+            "-Wno-unused-command-line-argument"]
+
+
+def _compile_cmd(src: str, obj: str):
+    if src.endswith(".hip"):
+        return [HIPCC, f"--offload-arch={ARCH}", "-munsafe-fp-atomics", *_common_flags(), "-c", src, "-o", obj]
+    _, tinc, _ = _torch_paths()
+    py_inc = sysconfig.get_paths()["include"]
+    incs = [f"-I{p}" for p in tinc] + [f"-I{py_inc}", f"-I{ROCM}/include"]
+    return [HIPCC, *_common_flags(), *incs, "-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H",
+            "-D_GLIBCXX_USE_CXX11_ABI=1", "-DUSE_ROCM=1", "-x", "c++", "-c", src, "-o", obj]
+
+
+def _link_cmd(objs):
+    _, _, tlib = _torch_paths()
+    return [HIPCC, "-shared", f"--offload-arch={ARCH}", "-fgpu-rdc" if False else "-fPIC", "-o", OUT, *objs,
+            f"-L{tlib}", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-lc10", "-lc10_hip", "-ltorch_python",
+            "-l:libamdhip64.so", "-l:librccl.so", f"-Wl,-rpath,{tlib}", "-Wl,--no-as-needed"]
+
+
+def build(jobs: int = 0, force: bool = False, verbose: bool = False) -> str:
+    os.makedirs(BUILD, exist_ok=True)
+    hip, cpp = _sources()
+    hdr = _headers_mtime()
+    todo = []
+    objs = []
+    for s in hip + cpp:
+        o = _obj_path(s)
+        objs.append(o)
+        if force or not os.path.exists(o) or os.path.getmtime(o) < max(os.path.getmtime(s), hdr):
+            todo.append((s, o))
+    jobs = jobs or min(8, os.cpu_count() or 4)
+    t0 = time.time()
+    if todo:
+        def run(so):
+            s, o = so
+            cmd = _compile_cmd(s, o)
+            if verbose:
+                print(" ".join(cmd), flush=True)
+            r = subprocess.run(cmd, capture_output=True, text=True)
+            if r.returncode != 0:
+                raise RuntimeError(f"compile failed: {os.path.relpath(s, ROOT)}\n{r.stdout}\n{r.stderr}")
+            return s
+        with cf.ThreadPoolExecutor(jobs) as ex:
+            for s in ex.map(run, todo):
+                print(f"[build] compiled {os.path.relpath(s, ROOT)}", flush=True)
+    if todo or not os.path.exists(OUT) or any(os.path.getmtime(o) > os.path.getmtime(OUT) for o in objs):
+        cmd = _link_cmd(objs)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+        print(f"[build] linked {os.path.relpath(OUT, ROOT)} ({len(objs)} objects, {time.time() - t0:.1f}s)",
+              flush=True)
+    return OUT
+
+
+def main(argv=None) -> int:
+    p = argparse.ArgumentParser()
+    p.add_argument("-j", "--jobs", type=int, default=0)
+    p.add_argument("--force", action="store_true")
+    p.add_argument("-v", "--verbose", action="store_true")
+    a = p.parse_args(argv)
+    build(a.jobs, a.force, a.verbose)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,1 @@
+from .vgg import CFG, VGG, VGG11, VGG13, VGG16, VGG19, block_specs, make_layers  # noqa: F401

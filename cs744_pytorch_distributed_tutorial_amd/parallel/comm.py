@@ -1,0 +1,94 @@
+"""Communicator backends used by the gradient-sync engines.
+
+``Comm`` is the small interface the bucketed reducer needs — asynchronous
+average-all-reduce of a contiguous buffer plus broadcast — with two
+implementations:
+
+* ``TorchComm`` — ``torch.distributed`` (ProcessGroupNCCL = RCCL on GPU
+  tensors, gloo on CPU tensors). RCCL work is enqueued on the process group's
+  internal stream after an event wait on the caller's current stream, so a call
+  issued right after a layer's weight-gradient kernel overlaps the rest of the
+  backward pass; ``wait()`` only makes the current stream wait (no host block).
+* ``RcclComm`` (``parallel.rccl``) — the native C++ communicator: one
+  ``ncclComm_t`` built from a TCPStore-shared unique id, a dedicated high-priority
+  comm stream, HIP events between compute and comm streams, ``ncclAvg`` so the
+  1/N costs no extra kernel. Stream-ordered and host-sync-free, so it can be
+  captured into a hipGraph together with the compute kernels.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from .. import distributed as D
+
+
+class Handle:
+    def wait(self) -> None:  # pragma: no cover - interface
+        raise NotImplementedError
+
+
+class _TorchHandle(Handle):
+    def __init__(self, work):
+        self.work = work
+
+    def wait(self) -> None:
+        if self.work is not None:
+            self.work.wait()
+
+
+class Comm:
+    rank: int = 0
+    world_size: int = 1
+
+    def all_reduce_avg(self, buf: torch.Tensor, async_op: bool = True) -> Handle:
+        raise NotImplementedError
+
+    def all_reduce_sum(self, buf: torch.Tensor, async_op: bool = True) -> Handle:
+        raise NotImplementedError
+
+    def broadcast(self, buf: torch.Tensor, src: int = 0) -> None:
+        raise NotImplementedError
+
+    def all_gather_int64(self, values: torch.Tensor) -> torch.Tensor:
+        raise NotImplementedError
+
+
+class TorchComm(Comm):
+    def __init__(self, group=None):
+        self.group = group
+        self.rank = D.get_rank(group)
+        self.world_size = D.get_world_size(group)
+
+    def all_reduce_avg(self, buf: torch.Tensor, async_op: bool = True) -> Handle:
+        if self.world_size == 1:
+            return _TorchHandle(None)
+        return _TorchHandle(D.all_reduce(buf, op=D.ReduceOp.AVG, group=self.group, async_op=async_op))
+
+    def all_reduce_sum(self, buf: torch.Tensor, async_op: bool = True) -> Handle:
+        if self.world_size == 1:
+            return _TorchHandle(None)
+        return _TorchHandle(D.all_reduce(buf, op=D.ReduceOp.SUM, group=self.group, async_op=async_op))
+
+    def broadcast(self, buf: torch.Tensor, src: int = 0) -> None:
+        if self.world_size > 1:
+            D.broadcast(buf, src=src, group=self.group)
+
+    def all_gather_int64(self, values: torch.Tensor) -> torch.Tensor:
+        if self.world_size == 1:
+            return values.reshape(1, -1)
+        out = [torch.zeros_like(values) for _ in range(self.world_size)]
+        D.all_gather(out, values, group=self.group)
+        return torch.stack(out)
+
+
+def make_comm(kind: Optional[str] = None, group=None) -> Comm:
+    """``kind``: ``"torch"`` (default) or ``"rccl"`` (native C++ communicator)."""
+    kind = kind or "torch"
+    if kind == "torch":
+        return TorchComm(group)
+    if kind == "rccl":
+        from .rccl import RcclComm
+        return RcclComm.from_process_group(group)
+    raise ValueError(f"unknown comm kind {kind!r}")

@@ -1,0 +1,141 @@
+"""Logging, timing and metrics.
+
+Keeps the reference's human-readable line formats exactly
+(`master/part1/part1.py:40,44,60-62`):
+
+* ``"{i} loss:  {x}"`` every 20 iterations (``print(batch_idx, "loss: ", loss)``),
+* ``"average time:  {s}"`` — the reference formula (iterations 1..10 divided by
+  9, +11 % bias) is reproduced *and* the true per-iteration mean is reported next
+  to it,
+* ``"Test set: Average loss: {:.4f}, Accuracy: {}/{} ({:.0f}%)"``.
+
+Adds a rank-0 filter (the reference prints on every rank), JSONL metrics and
+device-side timing with HIP events (no host sync inside the hot loop).
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import time
+from typing import Any, Dict, List, Optional
+
+import torch
+
+
+class RankLogger:
+    def __init__(self, rank: int = 0, all_ranks: bool = False, jsonl_path: Optional[str] = None,
+                 stream=None):
+        self.rank, self.all_ranks = rank, all_ranks
+        self.stream = stream or sys.stdout
+        self.jsonl_path = jsonl_path
+        if jsonl_path and rank == 0:
+            os.makedirs(os.path.dirname(os.path.abspath(jsonl_path)), exist_ok=True)
+
+    @property
+    def active(self) -> bool:
+        return self.all_ranks or self.rank == 0
+
+    def print(self, *args) -> None:
+        if self.active:
+            print(*args, file=self.stream, flush=True)
+
+    def loss_line(self, batch_idx: int, loss: float) -> None:
+        # reference: print(batch_idx, "loss: ", train_loss.item())
+        self.print(batch_idx, "loss: ", loss)
+
+    def average_time_line(self, seconds: float) -> None:
+        self.print("average time: ", seconds)
+
+    def test_line(self, avg_loss: float, correct: int, total: int) -> None:
+        self.print('Test set: Average loss: {:.4f}, Accuracy: {}/{} ({:.0f}%)\n'.format(
+            avg_loss, correct, total, 100.0 * correct / max(total, 1)))
+
+    def metric(self, **kv: Any) -> None:
+        if self.rank != 0:
+            return
+        kv.setdefault("ts", time.time())
+        if self.jsonl_path:
+            with open(self.jsonl_path, "a") as f:
+                f.write(json.dumps(kv) + "\n")
+
+
+class IterTimer:
+    """Wall-clock per-iteration timer that reproduces the reference's print.
+
+    The reference takes ``now`` at batch 0 and ``later`` at batch 10 and divides
+    by 9 (`master/part1/part1.py:41-44`); ``reference_formula()`` returns that
+    value, ``true_mean()`` the honest mean over the same window.
+    """
+
+    def __init__(self, sync_cuda: bool = True):
+        self.sync_cuda = sync_cuda and torch.cuda.is_available()
+        self.stamps: List[float] = []
+
+    def stamp(self) -> None:
+        if self.sync_cuda:
+            torch.cuda.synchronize()
+        self.stamps.append(time.perf_counter())
+
+    def reference_formula(self) -> Optional[float]:
+        if len(self.stamps) < 11:
+            return None
+        return (self.stamps[10] - self.stamps[0]) / 9
+
+    def true_mean(self, first: int = 1) -> Optional[float]:
+        if len(self.stamps) <= first + 1:
+            return None
+        d = self.stamps[-1] - self.stamps[first]
+        return d / (len(self.stamps) - 1 - first)
+
+
+class PhaseTimer:
+    """Device-side phase timing with HIP events (fwd / bwd / comm-wait / opt).
+
+    Events are recorded on the current stream and only resolved in ``summary()``
+    so the hot loop never blocks on the host.
+    """
+
+    def __init__(self, enabled: bool = True):
+        self.enabled = enabled and torch.cuda.is_available()
+        self._events: Dict[str, List] = {}
+        self._host: Dict[str, List[float]] = {}
+        self._open: Dict[str, Any] = {}
+
+    def start(self, name: str) -> None:
+        if self.enabled:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            self._open[name] = e
+        else:
+            self._open[name] = time.perf_counter()
+
+    def stop(self, name: str) -> None:
+        s = self._open.pop(name, None)
+        if s is None:
+            return
+        if self.enabled:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            self._events.setdefault(name, []).append((s, e))
+        else:
+            self._host.setdefault(name, []).append(time.perf_counter() - s)
+
+    def summary(self) -> Dict[str, float]:
+        out: Dict[str, float] = {}
+        if self.enabled:
+            torch.cuda.synchronize()
+            for k, pairs in self._events.items():
+                out[k + "_ms"] = sum(a.elapsed_time(b) for a, b in pairs) / max(len(pairs), 1)
+        for k, v in self._host.items():
+            out[k + "_ms"] = 1e3 * sum(v) / max(len(v), 1)
+        return out
+
+
+def roctx_range(name: str):
+    """Context manager emitting a roctx range (visible in rocprofv3 marker traces)."""
+    try:
+        return torch.cuda.nvtx.range(name)  # maps to roctx on ROCm builds
+    except Exception:  # pragma: no cover - no GPU profiler
+        import contextlib
+        return contextlib.nullcontext()

@@ -1,0 +1,153 @@
+// torch bindings for the gfx950 kernels (module name: cs744_pytorch_distributed_tutorial_amd._C).
+// Every op checks device/dtype/shape on the host BEFORE launching, so a bad call
+// fails loudly in Python instead of faulting the GPU.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/hip/HIPGuard.h>
+
+#include "kernels/launchers.h"
+
+namespace {
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+#define CS_CHECK_CUDA(t) TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor")
+#define CS_CHECK_F32(t) TORCH_CHECK((t).scalar_type() == at::kFloat, #t " must be float32")
+#define CS_CHECK_CONTIG(t) TORCH_CHECK((t).is_contiguous(), #t " must be contiguous")
+#define CS_LAUNCH(expr)                                                                  \
+  do {                                                                                   \
+    hipError_t _e = (expr);                                                              \
+    TORCH_CHECK(_e == hipSuccess, "kernel launch failed: ", hipGetErrorString(_e));      \
+  } while (0)
+
+const float kMean[3] = {125.3f / 255.f, 123.0f / 255.f, 113.9f / 255.f};
+const float kStd[3] = {63.0f / 255.f, 62.1f / 255.f, 66.7f / 255.f};
+
+torch::Tensor augment(torch::Tensor data, torch::Tensor idx, torch::Tensor params, bool nhwc, int64_t cstride) {
+  CS_CHECK_CUDA(data); CS_CHECK_CUDA(idx); CS_CHECK_CUDA(params);
+  TORCH_CHECK(data.scalar_type() == at::kByte && data.dim() == 4 && data.size(1) == 32 && data.size(2) == 32 &&
+              data.size(3) == 3, "data must be uint8 [N,32,32,3]");
+  TORCH_CHECK(idx.scalar_type() == at::kLong && idx.dim() == 1, "idx must be int64 [B]");
+  TORCH_CHECK(params.scalar_type() == at::kInt && params.dim() == 2 && params.size(1) == 3 &&
+              params.size(0) == data.size(0), "params must be int32 [N,3]");
+  CS_CHECK_CONTIG(data); CS_CHECK_CONTIG(idx); CS_CHECK_CONTIG(params);
+  TORCH_CHECK(cstride == 3 || cstride == 4, "cstride must be 3 or 4");
+  const int64_t B = idx.size(0);
+  // bounds check of the gather indices on the host side of the call (cheap: B values)
+  if (B > 0) {
+    auto mm = at::aminmax(idx);
+    TORCH_CHECK(std::get<0>(mm).item<int64_t>() >= 0 && std::get<1>(mm).item<int64_t>() < data.size(0),
+                "augment: index out of range");
+  }
+  c10::hip::HIPGuard g(data.device());
+  auto out = nhwc ? torch::empty({B, 32, 32, cstride}, data.options().dtype(at::kFloat))
+                  : torch::empty({B, 3, 32, 32}, data.options().dtype(at::kFloat));
+  CS_LAUNCH(cs_augment(data.data_ptr<uint8_t>(), idx.data_ptr<int64_t>(), params.data_ptr<int32_t>(),
+                       out.data_ptr<float>(), (int)B, nhwc ? 1 : 0, (int)cstride, kMean, kStd, cur_stream()));
+  return out;
+}
+
+void sgd_flat(torch::Tensor p, torch::Tensor g, torch::Tensor m, double lr, double mom, double wd, double damp,
+              double scale, bool first) {
+  for (auto* t : {&p, &g, &m}) { CS_CHECK_CUDA(*t); CS_CHECK_F32(*t); CS_CHECK_CONTIG(*t); }
+  TORCH_CHECK(p.numel() == g.numel() && p.numel() == m.numel(), "sgd_flat: size mismatch");
+  c10::hip::HIPGuard gd(p.device());
+  CS_LAUNCH(cs_sgd_flat(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), p.numel(), (float)lr,
+                        (float)mom, (float)wd, (float)damp, (float)scale, first ? 1 : 0, cur_stream()));
+}
+
+// Builds the device table {p,g,m,n} + chunk prefix once per distinct pointer set; returns it
+// as an int64 tensor the caller caches. Layout: [ntens*4 entries | ntens chunk starts | nchunks].
+torch::Tensor sgd_multi_table(std::vector<torch::Tensor> ps, std::vector<torch::Tensor> gs,
+                              std::vector<torch::Tensor> ms) {
+  TORCH_CHECK(ps.size() == gs.size() && ps.size() == ms.size() && !ps.empty(), "sgd_multi_table: list sizes");
+  const int64_t nt = ps.size();
+  auto host = torch::empty({nt * 4 + nt + 1}, torch::kLong);
+  int64_t* h = host.data_ptr<int64_t>();
+  int64_t chunks = 0;
+  for (int64_t i = 0; i < nt; ++i) {
+    for (auto* t : {&ps[i], &gs[i], &ms[i]}) { CS_CHECK_CUDA(*t); CS_CHECK_F32(*t); CS_CHECK_CONTIG(*t); }
+    TORCH_CHECK(ps[i].numel() == gs[i].numel() && ps[i].numel() == ms[i].numel(), "sgd_multi_table: numel");
+    h[i * 4 + 0] = (int64_t)ps[i].data_ptr<float>();
+    h[i * 4 + 1] = (int64_t)gs[i].data_ptr<float>();
+    h[i * 4 + 2] = (int64_t)ms[i].data_ptr<float>();
+    h[i * 4 + 3] = ps[i].numel();
+    h[nt * 4 + i] = chunks;
+    chunks += (ps[i].numel() + 4095) / 4096;
+  }
+  h[nt * 5] = chunks;
+  return host.to(ps[0].device());
+}
+
+void sgd_multi(torch::Tensor table, int64_t ntens, int64_t nchunks, double lr, double mom, double wd, double damp,
+               double scale, bool first) {
+  CS_CHECK_CUDA(table);
+  TORCH_CHECK(table.scalar_type() == at::kLong && table.numel() == ntens * 5 + 1, "sgd_multi: bad table");
+  c10::hip::HIPGuard gd(table.device());
+  const int64_t* t = table.data_ptr<int64_t>();
+  CS_LAUNCH(cs_sgd_multi(reinterpret_cast<const CsTensorEntry*>(t), (int)ntens, t + ntens * 4, (int)nchunks,
+                         (float)lr, (float)mom, (float)wd, (float)damp, (float)scale, first ? 1 : 0, cur_stream()));
+}
+
+std::vector<torch::Tensor> linear_xent(torch::Tensor feat, torch::Tensor W, torch::Tensor bias, torch::Tensor labels,
+                                       double gscale, bool backward) {
+  for (auto* t : {&feat, &W, &bias}) { CS_CHECK_CUDA(*t); CS_CHECK_F32(*t); CS_CHECK_CONTIG(*t); }
+  CS_CHECK_CUDA(labels);
+  TORCH_CHECK(labels.scalar_type() == at::kLong && labels.dim() == 1, "labels int64 [B]");
+  TORCH_CHECK(feat.dim() == 2 && W.dim() == 2 && bias.dim() == 1 && feat.size(1) == W.size(1) &&
+              W.size(0) == bias.size(0) && labels.size(0) == feat.size(0), "linear_xent: shapes");
+  const int B = feat.size(0), K = feat.size(1), C = W.size(0);
+  TORCH_CHECK(C <= 16 && 2 * B * C + 16 <= 40960, "linear_xent: C<=16 and B*C small enough for LDS");
+  c10::hip::HIPGuard gd(feat.device());
+  auto loss = torch::empty({}, feat.options());
+  auto correct = torch::empty({}, feat.options().dtype(at::kInt));
+  auto logits = torch::empty({B, C}, feat.options());
+  auto pred = torch::empty({B}, feat.options().dtype(at::kLong));
+  torch::Tensor dW, db, dfeat;
+  if (backward) {
+    dW = torch::empty_like(W);
+    db = torch::empty_like(bias);
+    dfeat = torch::empty_like(feat);
+  }
+  CS_LAUNCH(cs_linear_xent(feat.data_ptr<float>(), W.data_ptr<float>(), bias.data_ptr<float>(),
+                           labels.data_ptr<int64_t>(), B, K, C, (float)gscale, loss.data_ptr<float>(),
+                           correct.data_ptr<int>(), logits.data_ptr<float>(),
+                           backward ? dW.data_ptr<float>() : nullptr, backward ? db.data_ptr<float>() : nullptr,
+                           backward ? dfeat.data_ptr<float>() : nullptr, pred.data_ptr<int64_t>(), cur_stream()));
+  if (backward) return {loss, correct, logits, dW, db, dfeat, pred};
+  return {loss, correct, logits, pred};
+}
+
+std::vector<torch::Tensor> softmax_xent(torch::Tensor logits, torch::Tensor labels, double gscale) {
+  CS_CHECK_CUDA(logits); CS_CHECK_F32(logits); CS_CHECK_CONTIG(logits); CS_CHECK_CUDA(labels);
+  TORCH_CHECK(logits.dim() == 2 && labels.dim() == 1 && labels.size(0) == logits.size(0) &&
+              labels.scalar_type() == at::kLong, "softmax_xent: shapes");
+  TORCH_CHECK(logits.size(1) <= 16, "softmax_xent: C <= 16");
+  c10::hip::HIPGuard gd(logits.device());
+  auto loss = torch::empty({}, logits.options());
+  auto dl = torch::empty_like(logits);
+  auto correct = torch::empty({}, logits.options().dtype(at::kInt));
+  CS_LAUNCH(cs_softmax_xent(logits.data_ptr<float>(), labels.data_ptr<int64_t>(), logits.size(0), logits.size(1),
+                            (float)gscale, loss.data_ptr<float>(), dl.data_ptr<float>(), correct.data_ptr<int>(),
+                            cur_stream()));
+  return {loss, dl, correct};
+}
+
+}  // namespace
+
+void register_conv_ops(pybind11::module& m);
+void register_bn_ops(pybind11::module& m);
+void register_runtime(pybind11::module& m);
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "gfx950 (MI355X) kernels + native runtime for cs744_pytorch_distributed_tutorial_amd";
+  m.def("augment", &augment, "fused CIFAR gather+crop+flip+normalize");
+  m.def("sgd_flat", &sgd_flat, "fused SGD on flat buffers");
+  m.def("sgd_multi_table", &sgd_multi_table, "build the multi-tensor SGD table");
+  m.def("sgd_multi", &sgd_multi, "multi-tensor fused SGD");
+  m.def("linear_xent", &linear_xent, "fused Linear + softmax cross-entropy fwd(+bwd)");
+  m.def("softmax_xent", &softmax_xent, "softmax cross-entropy fwd+bwd");
+  register_conv_ops(m);
+  register_bn_ops(m);
+  register_runtime(m);
+}

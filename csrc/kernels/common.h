@@ -1,0 +1,61 @@
+// Shared helpers for the gfx950 (MI355X / CDNA4) kernels.
+// Wave size is 64 on CDNA: every lane/wave constant below is written for 64.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define CS_WAVE 64
+
+#define CS_HIP_CHECK(expr)                                                             \
+  do {                                                                                 \
+    hipError_t _e = (expr);                                                            \
+    if (_e != hipSuccess) {                                                            \
+      fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(_e), __FILE__,      \
+              __LINE__);                                                               \
+      return _e;                                                                       \
+    }                                                                                  \
+  } while (0)
+
+namespace cs {
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
+  return v;
+}
+
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// Block-wide sum for blockDim.x a multiple of 64 (<= 1024). `red` needs 16 floats.
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  float r = (threadIdx.x < (unsigned)nw) ? red[threadIdx.x] : 0.f;
+  if (wid == 0) r = wave_sum(r);
+  if (threadIdx.x == 0) red[0] = r;
+  __syncthreads();
+  return red[0];
+}
+
+// XCD-aware bijective block remap (cdna_hip_programming.md §5, "XCD swizzle must be
+// bijective"): blocks b and b+8 share an XCD, so hand each XCD a contiguous range.
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+  const int base = (xcd < r) ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + (orig >> 3);
+}
+
+}  // namespace cs
