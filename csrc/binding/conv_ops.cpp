@@ -1,2 +1,142 @@
-#include <torch/extension.h>
-void register_conv_ops(pybind11::module& m) {}
+// torch bindings: implicit-GEMM conv (fwd / dgrad / wgrad) and the fused BN kernels.
+// All shapes are validated on the host before any launch.
+#include "binding/torch_util.h"
+#include "kernels/launchers.h"
+
+namespace {
+
+using csb::cur_stream;
+using csb::DevGuard;
+
+const float* cptr(const c10::optional<torch::Tensor>& t) {
+  return (t.has_value() && t->defined()) ? t->data_ptr<float>() : nullptr;
+}
+float* mptr(const c10::optional<torch::Tensor>& t) {
+  return (t.has_value() && t->defined()) ? t->data_ptr<float>() : nullptr;
+}
+
+void check_t(const c10::optional<torch::Tensor>& t, int64_t numel, const char* name) {
+  if (!t.has_value() || !t->defined()) return;
+  TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->is_contiguous(), name,
+              ": must be a contiguous float32 GPU tensor");
+  TORCH_CHECK(t->numel() >= numel, name, ": has ", t->numel(), " elements, kernel needs ", numel);
+}
+
+bool pow2(int64_t v) { return v > 0 && (v & (v - 1)) == 0; }
+
+// returns the number of rows per FWD statistics tile
+int64_t conv_gemm(int64_t mode, c10::optional<torch::Tensor> x, c10::optional<torch::Tensor> w,
+                  c10::optional<torch::Tensor> dz, c10::optional<torch::Tensor> bias, torch::Tensor out,
+                  c10::optional<torch::Tensor> ws, c10::optional<torch::Tensor> stats, int64_t B, int64_t H, int64_t W,
+                  int64_t Cin, int64_t Cout, bool w_oihw, int64_t bm, int64_t bn, int64_t splits) {
+  TORCH_CHECK(mode >= 0 && mode <= 2, "conv_gemm: bad mode");
+  TORCH_CHECK(pow2(H) && pow2(W) && pow2(Cin) && pow2(Cout) && Cin >= 4 && Cout >= 64 && B > 0,
+              "conv_gemm: H, W, Cin, Cout must be powers of two (Cin>=4, Cout>=64)");
+  TORCH_CHECK((bm == 64 || bm == 128) && (bn == 64 || bn == 128) && splits >= 1, "conv_gemm: bad tiling");
+  TORCH_CHECK(!w_oihw || Cin == 4, "conv_gemm: OIHW weights only for the padded conv0 (Cin=4)");
+  if (mode == CS_CONV_DGRAD) TORCH_CHECK(Cin >= 64 && !w_oihw, "conv_gemm: dgrad needs Cin >= 64");
+  const int64_t pix = B * H * W;
+  const int64_t wnum = w_oihw ? Cout * 27 : Cout * 9 * Cin;
+  CsConvArgs a{};
+  a.B = B; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout; a.w_oihw = w_oihw ? 1 : 0;
+  cs_conv_fill_dims(&a, (int)mode);
+  if (mode == CS_CONV_FWD) {
+    TORCH_CHECK(x.has_value() && w.has_value(), "conv fwd needs x and w");
+    check_t(x, pix * Cin, "x"); check_t(w, wnum, "w"); check_t(bias, Cout, "bias");
+    check_t(out, pix * Cout, "out");
+    const int64_t R = splits > 1 ? 64 : bm;
+    check_t(stats, ((pix + R - 1) / R) * Cout * 2, "stats");
+  } else if (mode == CS_CONV_DGRAD) {
+    TORCH_CHECK(dz.has_value() && w.has_value(), "conv dgrad needs dz and w");
+    check_t(dz, pix * Cout, "dz"); check_t(w, wnum, "w"); check_t(out, pix * Cin, "out");
+  } else {
+    TORCH_CHECK(dz.has_value() && x.has_value(), "conv wgrad needs dz and x");
+    check_t(dz, pix * Cout, "dz"); check_t(x, pix * Cin, "x"); check_t(out, wnum, "out");
+  }
+  const int64_t ksteps = (a.K + 15) / 16;
+  const int64_t sp = std::min<int64_t>(splits, ksteps);
+  if (sp > 1) {
+    TORCH_CHECK(ws.has_value() && ws->defined(), "conv_gemm: split-K needs a workspace");
+    check_t(ws, sp * (int64_t)a.M * a.N, "ws");
+  }
+  DevGuard g(out.device());
+  a.x = cptr(x); a.w = cptr(w); a.dz = cptr(dz); a.bias = cptr(bias);
+  a.out = out.data_ptr<float>(); a.ws = mptr(ws); a.stats = mptr(stats);
+  CS_LAUNCH(cs_conv_gemm(a, (int)mode, (int)bm, (int)bn, (int)splits, cur_stream()));
+  return splits > 1 ? 64 : bm;
+}
+
+void bn_finalize(torch::Tensor part, int64_t T, int64_t R, int64_t M, torch::Tensor gamma, torch::Tensor beta,
+                 c10::optional<torch::Tensor> running_mean, c10::optional<torch::Tensor> running_var,
+                 c10::optional<torch::Tensor> nbt, double momentum, double eps, torch::Tensor scale,
+                 torch::Tensor shift, torch::Tensor save_mean, torch::Tensor save_invstd) {
+  const int64_t C = gamma.numel();
+  check_t(part, T * C * 2, "part");
+  TORCH_CHECK(T == (M + R - 1) / R, "bn_finalize: T must be ceil(M/R)");
+  for (auto* t : {&beta, &scale, &shift, &save_mean, &save_invstd}) check_t(*t, C, "bn vec");
+  check_t(running_mean, C, "running_mean"); check_t(running_var, C, "running_var");
+  int64_t* nb = nullptr;
+  if (nbt.has_value() && nbt->defined()) {
+    TORCH_CHECK(nbt->scalar_type() == at::kLong && nbt->is_cuda(), "num_batches_tracked must be int64 GPU");
+    nb = nbt->data_ptr<int64_t>();
+  }
+  DevGuard g(part.device());
+  CS_LAUNCH(cs_bn_finalize(part.data_ptr<float>(), T, R, M, C, gamma.data_ptr<float>(), beta.data_ptr<float>(),
+                           mptr(running_mean), mptr(running_var), nb, (float)momentum, (float)eps,
+                           scale.data_ptr<float>(), shift.data_ptr<float>(), save_mean.data_ptr<float>(),
+                           save_invstd.data_ptr<float>(), cur_stream()));
+}
+
+void bn_eval_coeffs(torch::Tensor gamma, torch::Tensor beta, torch::Tensor rm, torch::Tensor rv, double eps,
+                    torch::Tensor scale, torch::Tensor shift) {
+  const int64_t C = gamma.numel();
+  for (auto* t : {&beta, &rm, &rv, &scale, &shift}) check_t(*t, C, "bn vec");
+  DevGuard g(gamma.device());
+  CS_LAUNCH(cs_bn_eval_coeffs(gamma.data_ptr<float>(), beta.data_ptr<float>(), rm.data_ptr<float>(),
+                              rv.data_ptr<float>(), C, (float)eps, scale.data_ptr<float>(), shift.data_ptr<float>(),
+                              cur_stream()));
+}
+
+void bn_apply(torch::Tensor y, torch::Tensor scale, torch::Tensor shift, torch::Tensor out, int64_t B, int64_t H,
+              int64_t W, int64_t C, bool pool) {
+  TORCH_CHECK(C % 4 == 0 && (!pool || (H % 2 == 0 && W % 2 == 0)), "bn_apply: shape");
+  check_t(y, B * H * W * C, "y"); check_t(scale, C, "scale"); check_t(shift, C, "shift");
+  check_t(out, B * (pool ? H / 2 : H) * (pool ? W / 2 : W) * C, "out");
+  DevGuard g(y.device());
+  CS_LAUNCH(cs_bn_apply(y.data_ptr<float>(), scale.data_ptr<float>(), shift.data_ptr<float>(), out.data_ptr<float>(),
+                        B, H, W, C, pool ? 1 : 0, cur_stream()));
+}
+
+int64_t bn_bwd_blocks(int64_t B, int64_t H, int64_t W, int64_t C, bool pool) {
+  return cs_bn_bwd_blocks(B, H, W, C, pool ? 1 : 0);
+}
+
+void bn_bwd(torch::Tensor y, torch::Tensor G, int64_t B, int64_t H, int64_t W, int64_t C, bool pool,
+            torch::Tensor scale, torch::Tensor shift, torch::Tensor mean, torch::Tensor invstd, torch::Tensor gamma,
+            torch::Tensor part, torch::Tensor coef, c10::optional<torch::Tensor> dgamma,
+            c10::optional<torch::Tensor> dbeta, c10::optional<torch::Tensor> dbias, torch::Tensor dz) {
+  TORCH_CHECK(C % 4 == 0 && C <= 1024 && (!pool || (H % 2 == 0 && W % 2 == 0)), "bn_bwd: shape");
+  check_t(y, B * H * W * C, "y");
+  check_t(G, B * (pool ? H / 2 : H) * (pool ? W / 2 : W) * C, "G");
+  for (auto* t : {&scale, &shift, &mean, &invstd, &gamma}) check_t(*t, C, "bn vec");
+  check_t(part, (int64_t)cs_bn_bwd_blocks(B, H, W, C, pool) * C * 3, "part");
+  check_t(coef, C * 3, "coef");
+  check_t(dgamma, C, "dgamma"); check_t(dbeta, C, "dbeta"); check_t(dbias, C, "dbias");
+  check_t(dz, B * H * W * C, "dz");
+  DevGuard g(y.device());
+  CS_LAUNCH(cs_bn_bwd(y.data_ptr<float>(), G.data_ptr<float>(), B, H, W, C, pool ? 1 : 0, scale.data_ptr<float>(),
+                      shift.data_ptr<float>(), mean.data_ptr<float>(), invstd.data_ptr<float>(),
+                      gamma.data_ptr<float>(), part.data_ptr<float>(), coef.data_ptr<float>(), mptr(dgamma),
+                      mptr(dbeta), mptr(dbias), dz.data_ptr<float>(), cur_stream()));
+}
+
+}  // namespace
+
+void register_conv_ops(pybind11::module& m) {
+  m.def("conv_gemm", &conv_gemm, "implicit-GEMM 3x3 conv (mode 0 fwd / 1 dgrad / 2 wgrad), fp32 MFMA");
+  m.def("bn_finalize", &bn_finalize);
+  m.def("bn_eval_coeffs", &bn_eval_coeffs);
+  m.def("bn_apply", &bn_apply);
+  m.def("bn_bwd_blocks", &bn_bwd_blocks);
+  m.def("bn_bwd", &bn_bwd);
+}

@@ -1,24 +1,13 @@
 // torch bindings for the gfx950 kernels (module name: cs744_pytorch_distributed_tutorial_amd._C).
 // Every op checks device/dtype/shape on the host BEFORE launching, so a bad call
 // fails loudly in Python instead of faulting the GPU.
-#include <torch/extension.h>
-#include <c10/hip/HIPStream.h>
-#include <c10/hip/HIPGuard.h>
-
+#include "binding/torch_util.h"
 #include "kernels/launchers.h"
 
 namespace {
 
-hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
-
-#define CS_CHECK_CUDA(t) TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor")
-#define CS_CHECK_F32(t) TORCH_CHECK((t).scalar_type() == at::kFloat, #t " must be float32")
-#define CS_CHECK_CONTIG(t) TORCH_CHECK((t).is_contiguous(), #t " must be contiguous")
-#define CS_LAUNCH(expr)                                                                  \
-  do {                                                                                   \
-    hipError_t _e = (expr);                                                              \
-    TORCH_CHECK(_e == hipSuccess, "kernel launch failed: ", hipGetErrorString(_e));      \
-  } while (0)
+using csb::cur_stream;
+using csb::DevGuard;
 
 const float kMean[3] = {125.3f / 255.f, 123.0f / 255.f, 113.9f / 255.f};
 const float kStd[3] = {63.0f / 255.f, 62.1f / 255.f, 66.7f / 255.f};
@@ -39,7 +28,7 @@ torch::Tensor augment(torch::Tensor data, torch::Tensor idx, torch::Tensor param
     TORCH_CHECK(std::get<0>(mm).item<int64_t>() >= 0 && std::get<1>(mm).item<int64_t>() < data.size(0),
                 "augment: index out of range");
   }
-  c10::hip::HIPGuard g(data.device());
+  DevGuard g(data.device());
   auto out = nhwc ? torch::empty({B, 32, 32, cstride}, data.options().dtype(at::kFloat))
                   : torch::empty({B, 3, 32, 32}, data.options().dtype(at::kFloat));
   CS_LAUNCH(cs_augment(data.data_ptr<uint8_t>(), idx.data_ptr<int64_t>(), params.data_ptr<int32_t>(),
@@ -51,7 +40,7 @@ void sgd_flat(torch::Tensor p, torch::Tensor g, torch::Tensor m, double lr, doub
               double scale, bool first) {
   for (auto* t : {&p, &g, &m}) { CS_CHECK_CUDA(*t); CS_CHECK_F32(*t); CS_CHECK_CONTIG(*t); }
   TORCH_CHECK(p.numel() == g.numel() && p.numel() == m.numel(), "sgd_flat: size mismatch");
-  c10::hip::HIPGuard gd(p.device());
+  DevGuard gd(p.device());
   CS_LAUNCH(cs_sgd_flat(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), p.numel(), (float)lr,
                         (float)mom, (float)wd, (float)damp, (float)scale, first ? 1 : 0, cur_stream()));
 }
@@ -83,7 +72,7 @@ void sgd_multi(torch::Tensor table, int64_t ntens, int64_t nchunks, double lr, d
                double scale, bool first) {
   CS_CHECK_CUDA(table);
   TORCH_CHECK(table.scalar_type() == at::kLong && table.numel() == ntens * 5 + 1, "sgd_multi: bad table");
-  c10::hip::HIPGuard gd(table.device());
+  DevGuard gd(table.device());
   const int64_t* t = table.data_ptr<int64_t>();
   CS_LAUNCH(cs_sgd_multi(reinterpret_cast<const CsTensorEntry*>(t), (int)ntens, t + ntens * 4, (int)nchunks,
                          (float)lr, (float)mom, (float)wd, (float)damp, (float)scale, first ? 1 : 0, cur_stream()));
@@ -98,7 +87,7 @@ std::vector<torch::Tensor> linear_xent(torch::Tensor feat, torch::Tensor W, torc
               W.size(0) == bias.size(0) && labels.size(0) == feat.size(0), "linear_xent: shapes");
   const int B = feat.size(0), K = feat.size(1), C = W.size(0);
   TORCH_CHECK(C <= 16 && 2 * B * C + 16 <= 40960, "linear_xent: C<=16 and B*C small enough for LDS");
-  c10::hip::HIPGuard gd(feat.device());
+  DevGuard gd(feat.device());
   auto loss = torch::empty({}, feat.options());
   auto correct = torch::empty({}, feat.options().dtype(at::kInt));
   auto logits = torch::empty({B, C}, feat.options());
@@ -123,7 +112,7 @@ std::vector<torch::Tensor> softmax_xent(torch::Tensor logits, torch::Tensor labe
   TORCH_CHECK(logits.dim() == 2 && labels.dim() == 1 && labels.size(0) == logits.size(0) &&
               labels.scalar_type() == at::kLong, "softmax_xent: shapes");
   TORCH_CHECK(logits.size(1) <= 16, "softmax_xent: C <= 16");
-  c10::hip::HIPGuard gd(logits.device());
+  DevGuard gd(logits.device());
   auto loss = torch::empty({}, logits.options());
   auto dl = torch::empty_like(logits);
   auto correct = torch::empty({}, logits.options().dtype(at::kInt));

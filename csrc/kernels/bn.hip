@@ -1,0 +1,301 @@
+// BatchNorm2d (training statistics, eps 1e-5, momentum 0.1) + ReLU + optional
+// MaxPool2d(2,2), forward and backward, NHWC fp32 — the reference block
+// Conv -> BatchNorm2d -> ReLU(inplace) [-> MaxPool2d] (master/part1/model.py:16-25;
+// SURVEY.md §2.2 N4-N7).
+//
+// Forward:  the conv GEMM epilogue already produced per-row-tile (mean, M2) partials;
+//   bn_finalize combines them with Chan's parallel update (numerically robust,
+//   deterministic), updates running_mean / running_var (unbiased) /
+//   num_batches_tracked, and emits per-channel scale/shift; bn_apply then computes
+//   relu(y*scale+shift) and the 2x2 max in ONE pass (the un-pooled activation is
+//   never written).
+// Backward: bn_bwd_reduce recomputes z = relu(bn(y)) and the pool argmax (first
+//   maximum in window scan order, as ATen) from y, routes the incoming gradient,
+//   and accumulates per-channel (sum g, sum g*xhat, sum xhat); bn_bwd_finalize
+//   emits dgamma, dbeta, the conv-bias gradient (exact chain rule:
+//   sum_m dZ = -gamma*invstd*mean(g*xhat)*sum(xhat)) and the dZ coefficients;
+//   bn_bwd_apply writes dZ = gamma*invstd*(g - mean(g) - xhat*mean(g*xhat)).
+#include "common.h"
+#include "launchers.h"
+
+namespace {
+
+__device__ __forceinline__ void chan_combine(float& n, float& m, float& M2, float nb, float mb, float M2b) {
+  if (nb == 0.f) return;
+  if (n == 0.f) {
+    n = nb; m = mb; M2 = M2b;
+    return;
+  }
+  const float nn = n + nb, d = mb - m;
+  m = m + d * (nb / nn);
+  M2 = M2 + M2b + d * d * (n * nb / nn);
+  n = nn;
+}
+
+// 256 threads = 16 channels x 16 tile-lanes
+__global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restrict__ part, int T, int R, int M, int C,
+                                                          const float* __restrict__ gamma,
+                                                          const float* __restrict__ beta, float* running_mean,
+                                                          float* running_var, int64_t* nbt, float momentum, float eps,
+                                                          float* __restrict__ scale, float* __restrict__ shift,
+                                                          float* __restrict__ save_mean,
+                                                          float* __restrict__ save_invstd) {
+  const int cl = threadIdx.x >> 4, tl = threadIdx.x & 15;
+  const int c = blockIdx.x * 16 + cl;
+  float n = 0.f, m = 0.f, M2 = 0.f;
+  if (c < C) {
+    for (int t = tl; t < T; t += 16) {
+      const int cnt = (M - t * R) < R ? (M - t * R) : R;
+      chan_combine(n, m, M2, (float)cnt, part[((size_t)t * C + c) * 2], part[((size_t)t * C + c) * 2 + 1]);
+    }
+  }
+#pragma unroll
+  for (int off = 8; off > 0; off >>= 1) {
+    const float nb = __shfl_xor(n, off, 64), mb = __shfl_xor(m, off, 64), M2b = __shfl_xor(M2, off, 64);
+    chan_combine(n, m, M2, nb, mb, M2b);
+  }
+  if (tl == 0 && c < C) {
+    const float var = M2 / n;
+    const float inv = 1.0f / sqrtf(var + eps);
+    const float g = gamma[c], b = beta[c];
+    scale[c] = g * inv;
+    shift[c] = b - m * g * inv;
+    save_mean[c] = m;
+    save_invstd[c] = inv;
+    if (running_mean != nullptr) {
+      const float unb = n > 1.f ? M2 / (n - 1.f) : var;
+      running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * m;
+      running_var[c] = (1.f - momentum) * running_var[c] + momentum * unb;
+    }
+  }
+  if (nbt != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *nbt += 1;
+}
+
+__global__ void bn_eval_coeffs_kernel(const float* gamma, const float* beta, const float* rm, const float* rv, int C,
+                                      float eps, float* scale, float* shift) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < C) {
+    const float inv = 1.0f / sqrtf(rv[c] + eps);
+    scale[c] = gamma[c] * inv;
+    shift[c] = beta[c] - rm[c] * gamma[c] * inv;
+  }
+}
+
+__device__ __forceinline__ float4 bnrelu4(float4 y, float4 s, float4 t) {
+  return make_float4(fmaxf(y.x * s.x + t.x, 0.f), fmaxf(y.y * s.y + t.y, 0.f), fmaxf(y.z * s.z + t.z, 0.f),
+                     fmaxf(y.w * s.w + t.w, 0.f));
+}
+
+// one thread per (output position, 4 channels)
+__global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__ y, const float* __restrict__ scale,
+                                                       const float* __restrict__ shift, float* __restrict__ out,
+                                                       int B, int H, int W, int C, int pool) {
+  const int C4 = C >> 2;
+  const int Ho = pool ? H >> 1 : H, Wo = pool ? W >> 1 : W;
+  const int total = B * Ho * Wo * C4;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= total) return;
+  const int cq = t % C4, pos = t / C4;
+  const float4 s = reinterpret_cast<const float4*>(scale)[cq];
+  const float4 sh = reinterpret_cast<const float4*>(shift)[cq];
+  float4 r;
+  if (!pool) {
+    r = bnrelu4(reinterpret_cast<const float4*>(y)[t], s, sh);
+  } else {
+    const int wo = pos % Wo, ho = (pos / Wo) % Ho, b = pos / (Wo * Ho);
+    const size_t base = (((size_t)b * H + 2 * ho) * W + 2 * wo) * C4 + cq;
+    const float4* y4 = reinterpret_cast<const float4*>(y);
+    const float4 a0 = bnrelu4(y4[base], s, sh), a1 = bnrelu4(y4[base + C4], s, sh);
+    const float4 a2 = bnrelu4(y4[base + (size_t)W * C4], s, sh), a3 = bnrelu4(y4[base + (size_t)W * C4 + C4], s, sh);
+    r = make_float4(fmaxf(fmaxf(a0.x, a1.x), fmaxf(a2.x, a3.x)), fmaxf(fmaxf(a0.y, a1.y), fmaxf(a2.y, a3.y)),
+                    fmaxf(fmaxf(a0.z, a1.z), fmaxf(a2.z, a3.z)), fmaxf(fmaxf(a0.w, a1.w), fmaxf(a2.w, a3.w)));
+  }
+  reinterpret_cast<float4*>(out)[t] = r;
+}
+
+// ------------------------------------------------------------------ backward
+// Visit every full-resolution element once: unit = a 2x2 window (pool) or a pixel.
+// APPLY = false: accumulate per-channel partials; APPLY = true: write dZ.
+template <bool APPLY, bool POOL>
+__device__ __forceinline__ void bwd_visit(const float* __restrict__ y, const float* __restrict__ G, int B, int H,
+                                          int W, int C, int cq, int unit, const float* scale, const float* shift,
+                                          const float* mean, const float* invstd, const float* coef, float* dz,
+                                          float (&acc)[3][4]) {
+  const int C4 = C >> 2;
+  float sc[4], sh[4], mu[4], is[4], k1[4], k2[4], k3[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int c = 4 * cq + q;
+    sc[q] = scale[c]; sh[q] = shift[c]; mu[q] = mean[c]; is[q] = invstd[c];
+    if (APPLY) { k1[q] = coef[3 * c]; k2[q] = coef[3 * c + 1]; k3[q] = coef[3 * c + 2]; }
+  }
+  const float4 g4 = reinterpret_cast<const float4*>(G)[(size_t)unit * C4 + cq];
+  const float gin[4] = {g4.x, g4.y, g4.z, g4.w};
+  constexpr int NP = POOL ? 4 : 1;
+  size_t off[NP];
+  if (POOL) {
+    const int Wo = W >> 1, Ho = H >> 1;
+    const int wo = unit % Wo, ho = (unit / Wo) % Ho, b = unit / (Wo * Ho);
+    const size_t base = (((size_t)b * H + 2 * ho) * W + 2 * wo) * C4 + cq;
+    off[0] = base;
+    if (POOL) {
+      off[1 % NP] = base + C4;
+      off[2 % NP] = base + (size_t)W * C4;
+      off[3 % NP] = base + (size_t)W * C4 + C4;
+    }
+  } else {
+    off[0] = (size_t)unit * C4 + cq;
+  }
+  float yv[NP][4];
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const float4 v = reinterpret_cast<const float4*>(y)[off[p]];
+    yv[p][0] = v.x; yv[p][1] = v.y; yv[p][2] = v.z; yv[p][3] = v.w;
+  }
+  float out[NP][4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    float z[NP];
+    int am = 0;
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      z[p] = fmaxf(yv[p][q] * sc[q] + sh[q], 0.f);
+      if (p > 0 && z[p] > z[am]) am = p;
+    }
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      const float g = (p == am && z[p] > 0.f) ? gin[q] : 0.f;
+      const float xh = (yv[p][q] - mu[q]) * is[q];
+      if (APPLY) {
+        out[p][q] = k1[q] * (g - k2[q] - xh * k3[q]);
+      } else {
+        acc[0][q] += g;
+        acc[1][q] += g * xh;
+        acc[2][q] += xh;
+      }
+    }
+  }
+  if (APPLY) {
+#pragma unroll
+    for (int p = 0; p < NP; ++p)
+      reinterpret_cast<float4*>(dz)[off[p]] = make_float4(out[p][0], out[p][1], out[p][2], out[p][3]);
+  }
+}
+
+template <bool APPLY, bool POOL>
+__global__ __launch_bounds__(256) void bn_bwd_kernel(const float* __restrict__ y, const float* __restrict__ G, int B,
+                                                     int H, int W, int C, const float* __restrict__ scale,
+                                                     const float* __restrict__ shift, const float* __restrict__ mean,
+                                                     const float* __restrict__ invstd, const float* __restrict__ coef,
+                                                     float* __restrict__ dz, float* __restrict__ part) {
+  extern __shared__ __attribute__((aligned(16))) float red[];  // [rows][C][3] (reduce only)
+  const int C4 = C >> 2;
+  const int rows = 256 / C4;  // C <= 1024
+  const int cq = threadIdx.x % C4, rl = threadIdx.x / C4;
+  const int units = POOL ? B * (H >> 1) * (W >> 1) : B * H * W;
+  float acc[3][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  if (rl < rows) {
+    for (int u = blockIdx.x * rows + rl; u < units; u += gridDim.x * rows)
+      bwd_visit<APPLY, POOL>(y, G, B, H, W, C, cq, u, scale, shift, mean, invstd, coef, dz, acc);
+  }
+  if (APPLY) return;
+  if (rl < rows) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) red[((size_t)rl * C + 4 * cq + q) * 3 + k] = acc[k][q];
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < C * 3; e += blockDim.x) {
+    float s = 0.f;
+    for (int r = 0; r < rows; ++r) s += red[(size_t)r * C * 3 + e];
+    part[(size_t)blockIdx.x * C * 3 + e] = s;
+  }
+}
+
+__global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int P, int C, int M,
+                                       const float* __restrict__ gamma, const float* __restrict__ invstd,
+                                       float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                       float* __restrict__ dbias, float* __restrict__ coef) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float sg = 0.f, sgx = 0.f, sx = 0.f;
+  for (int p = 0; p < P; ++p) {
+    const float* q = part + ((size_t)p * C + c) * 3;
+    sg += q[0];
+    sgx += q[1];
+    sx += q[2];
+  }
+  const float k1 = gamma[c] * invstd[c], k2 = sg / (float)M, k3 = sgx / (float)M;
+  if (dgamma) dgamma[c] = sgx;
+  if (dbeta) dbeta[c] = sg;
+  if (dbias) dbias[c] = -k1 * k3 * sx;
+  coef[3 * c] = k1;
+  coef[3 * c + 1] = k2;
+  coef[3 * c + 2] = k3;
+}
+
+}  // namespace
+
+int cs_bn_bwd_blocks(int B, int H, int W, int C, int pool) {
+  const int units = pool ? B * (H / 2) * (W / 2) : B * H * W;
+  const int rows = 256 / (C / 4);
+  int blocks = (units + rows - 1) / rows;
+  return blocks < 256 ? blocks : 256;
+}
+
+hipError_t cs_bn_finalize(const float* part, int T, int R, int M, int C, const float* gamma, const float* beta,
+                          float* running_mean, float* running_var, int64_t* nbt, float momentum, float eps,
+                          float* scale, float* shift, float* save_mean, float* save_invstd, hipStream_t stream) {
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, stream, part, T, R, M, C, gamma, beta,
+                     running_mean, running_var, nbt, momentum, eps, scale, shift, save_mean, save_invstd);
+  return hipGetLastError();
+}
+
+hipError_t cs_bn_eval_coeffs(const float* gamma, const float* beta, const float* rm, const float* rv, int C, float eps,
+                             float* scale, float* shift, hipStream_t stream) {
+  hipLaunchKernelGGL(bn_eval_coeffs_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, gamma, beta, rm, rv, C, eps,
+                     scale, shift);
+  return hipGetLastError();
+}
+
+hipError_t cs_bn_apply(const float* y, const float* scale, const float* shift, float* out, int B, int H, int W, int C,
+                       int pool, hipStream_t stream) {
+  if (C % 4 != 0 || (pool && ((H | W) & 1))) return hipErrorInvalidValue;
+  const int total = B * (pool ? H / 2 : H) * (pool ? W / 2 : W) * (C / 4);
+  if (total == 0) return hipSuccess;
+  hipLaunchKernelGGL(bn_apply_kernel, dim3((total + 255) / 256), dim3(256), 0, stream, y, scale, shift, out, B, H, W,
+                     C, pool);
+  return hipGetLastError();
+}
+
+hipError_t cs_bn_bwd(const float* y, const float* G, int B, int H, int W, int C, int pool, const float* scale,
+                     const float* shift, const float* mean, const float* invstd, const float* gamma, float* part,
+                     float* coef, float* dgamma, float* dbeta, float* dbias, float* dz, hipStream_t stream) {
+  if (C % 4 != 0 || C > 1024 || (pool && ((H | W) & 1))) return hipErrorInvalidValue;
+  const int P = cs_bn_bwd_blocks(B, H, W, C, pool);
+  const int rows = 256 / (C / 4);
+  const size_t lds = (size_t)rows * C * 3 * sizeof(float);
+  const int M = B * H * W;
+  if (pool) {
+    hipLaunchKernelGGL((bn_bwd_kernel<false, true>), dim3(P), dim3(256), lds, stream, y, G, B, H, W, C, scale, shift,
+                       mean, invstd, nullptr, nullptr, part);
+  } else {
+    hipLaunchKernelGGL((bn_bwd_kernel<false, false>), dim3(P), dim3(256), lds, stream, y, G, B, H, W, C, scale, shift,
+                       mean, invstd, nullptr, nullptr, part);
+  }
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, part, P, C, M, gamma, invstd,
+                     dgamma, dbeta, dbias, coef);
+  // the apply pass is sized for bandwidth, independent of the reduce's P
+  const int units = pool ? B * (H / 2) * (W / 2) : B * H * W;
+  int blocks = (units + rows - 1) / rows;
+  if (blocks > 2048) blocks = 2048;
+  if (pool) {
+    hipLaunchKernelGGL((bn_bwd_kernel<true, true>), dim3(blocks), dim3(256), 0, stream, y, G, B, H, W, C, scale, shift,
+                       mean, invstd, coef, dz, nullptr);
+  } else {
+    hipLaunchKernelGGL((bn_bwd_kernel<true, false>), dim3(blocks), dim3(256), 0, stream, y, G, B, H, W, C, scale,
+                       shift, mean, invstd, coef, dz, nullptr);
+  }
+  return hipGetLastError();
+}

@@ -1,0 +1,503 @@
+// 3x3 / stride 1 / pad 1 convolution as implicit GEMM on CDNA4 fp32 MFMA
+// (v_mfma_f32_32x32x2_f32: exact f32, 64 FLOP/clk/SIMD), NHWC activations.
+// Replaces ATen conv2d forward / backward-data / backward-weight of the reference
+// (nn.Conv2d at master/part1/model.py:18-23; SURVEY.md §2.2 N1-N3, §2.4 shapes).
+//
+//   FWD  : Y [M=B*H*W][N=Cout]  = im2col(X)[M][K=9*Cin] . W^T      (+bias, +BN tile stats)
+//   DGRAD: dX[M=B*H*W][N=Cin]   = shift(dZ)[M][K=9*Cout] . W        (flipped taps)
+//   WGRAD: dW[M=Cout][N=9*Cin]  = dZ^T[Cout][K=B*H*W] . im2col(X)
+//
+// Tiling: 256 threads = 4 waves (2x2), block tile BMxBN, BK = 16, wave tile
+// (BM/2)x(BN/2) built from 32x32 MFMA tiles. Global -> registers -> LDS double
+// buffer with one barrier per K-step; the next K-step's global loads are issued
+// before the current step's MFMAs so HBM/L2 latency hides under matrix work.
+// K is permuted inside a K-step so each lane's 8 A (and B) values are contiguous
+// in LDS: lane-half h feeds k = 8h + s at MFMA sub-step s (s = 0..7), turning the
+// operand fetch into two ds_read_b128 per tile ([row][16+4] padded rows are
+// bank-conflict free for the ds_read_b128 lane groups), or 8 conflict-free
+// ds_read_b32 for operands that are staged K-major ([k][rows+4]).
+// Split-K over blockIdx.z writes fp32 slabs that `splitk_reduce` sums in a fixed
+// order (deterministic, no float atomics). Tiles are dealt to XCDs in contiguous
+// ranges (common.h xcd_remap) so neighbouring tiles share an L2.
+#include "common.h"
+#include "launchers.h"
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+constexpr int BK = 16;
+
+__device__ __forceinline__ void pix_decode(int p, const CsConvArgs& a, int& b, int& h, int& w) {
+  w = p & (a.W - 1);
+  h = (p >> a.lgW) & (a.H - 1);
+  b = p >> (a.lgW + a.lgH);
+}
+
+template <int MODE>
+struct Traits;
+template <>
+struct Traits<CS_CONV_FWD> {
+  static constexpr bool A_KC = true, B_KC = true;
+};
+template <>
+struct Traits<CS_CONV_DGRAD> {
+  static constexpr bool A_KC = true, B_KC = false;
+};
+template <>
+struct Traits<CS_CONV_WGRAD> {
+  static constexpr bool A_KC = false, B_KC = false;
+};
+
+template <int BM, int BN, int MODE>
+struct Tile {
+  static constexpr bool A_KC = Traits<MODE>::A_KC, B_KC = Traits<MODE>::B_KC;
+  static constexpr int A_ELEMS = A_KC ? BM * (BK + 4) : BK * (BM + 4);
+  static constexpr int B_ELEMS = B_KC ? BN * (BK + 4) : BK * (BN + 4);
+  static constexpr int STAGE = A_ELEMS + B_ELEMS;
+  static constexpr int AC = BM / 64;  // float4 chunks per thread per stage
+  static constexpr int BC = BN / 64;
+  static constexpr int WM = BM / 2, WN = BN / 2, RM = WM / 32, RN = WN / 32;
+};
+
+template <int BM, int BN, int MODE>
+struct Loader {
+  using T = Tile<BM, BN, MODE>;
+  // per-thread precomputed row info for K-contiguous A rows (FWD/DGRAD: pixel rows)
+  int a_b[T::AC], a_h[T::AC], a_w[T::AC];
+  bool a_ok[T::AC];
+  float4 ra[T::AC], rb[T::BC];
+
+  __device__ void init(const CsConvArgs& a, int m0) {
+    if constexpr (T::A_KC) {
+#pragma unroll
+      for (int i = 0; i < T::AC; ++i) {
+        const int q = threadIdx.x + 256 * i, row = q >> 2, m = m0 + row;
+        a_ok[i] = m < a.M;
+        pix_decode(a_ok[i] ? m : 0, a, a_b[i], a_h[i], a_w[i]);
+      }
+    }
+  }
+
+  __device__ void load(const CsConvArgs& a, int m0, int n0, int k0) {
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    // ---------------- A operand
+#pragma unroll
+    for (int i = 0; i < T::AC; ++i) {
+      const int q = threadIdx.x + 256 * i;
+      float4 v = z4;
+      if constexpr (MODE == CS_CONV_FWD || MODE == CS_CONV_DGRAD) {
+        const int c = q & 3, kk = k0 + 4 * c;
+        const int lgC = (MODE == CS_CONV_FWD) ? a.lgCin : a.lgCout;
+        const int tap = kk >> lgC, ch = kk & ((1 << lgC) - 1);
+        if (a_ok[i] && tap < 9) {
+          const int t3 = tap / 3, dh = t3 - 1, dw = tap - 3 * t3 - 1;
+          const int hh = (MODE == CS_CONV_FWD) ? a_h[i] + dh : a_h[i] - dh;
+          const int ww = (MODE == CS_CONV_FWD) ? a_w[i] + dw : a_w[i] - dw;
+          if ((unsigned)hh < (unsigned)a.H && (unsigned)ww < (unsigned)a.W) {
+            const float* src = (MODE == CS_CONV_FWD) ? a.x : a.dz;
+            v = *reinterpret_cast<const float4*>(src + ((((size_t)a_b[i] * a.H + hh) * a.W + ww) << lgC) + ch);
+          }
+        }
+      } else {  // WGRAD: A[k = pixel][m' = cout]  (K-major staging)
+        constexpr int CPR = BM / 4;
+        const int kr = q / CPR, c = q - kr * CPR, p = k0 + kr;
+        if (p < a.K && m0 + 4 * c < a.M)
+          v = *reinterpret_cast<const float4*>(a.dz + ((size_t)p << a.lgCout) + m0 + 4 * c);
+      }
+      ra[i] = v;
+    }
+    // ---------------- B operand
+#pragma unroll
+    for (int i = 0; i < T::BC; ++i) {
+      const int q = threadIdx.x + 256 * i;
+      float4 v = z4;
+      if constexpr (MODE == CS_CONV_FWD) {
+        const int row = q >> 2, c = q & 3, n = n0 + row, kk = k0 + 4 * c;
+        if (n < a.N && kk < a.K) {
+          if (!a.w_oihw) {
+            v = *reinterpret_cast<const float4*>(a.w + (size_t)n * a.K + kk);
+          } else {  // conv0: OIHW [Cout][3][3x3], K = 9 taps x 4 (padded) channels
+            const int tap = kk >> 2;
+            const float* wr = a.w + (size_t)n * 27 + tap;
+            v = make_float4(wr[0], wr[9], wr[18], 0.f);
+          }
+        }
+      } else if constexpr (MODE == CS_CONV_DGRAD) {  // B[k = (tap, cout)][n = cin]
+        constexpr int CPR = BN / 4;
+        const int kr = q / CPR, c = q - kr * CPR, kk = k0 + kr;
+        const int tap = kk >> a.lgCout, co = kk & (a.Cout - 1);
+        if (kk < a.K && n0 + 4 * c < a.N)
+          v = *reinterpret_cast<const float4*>(a.w + ((size_t)co * 9 + tap) * a.Cin + n0 + 4 * c);
+      } else {  // WGRAD: B[k = pixel][n' = (tap, cin)]
+        constexpr int CPR = BN / 4;
+        const int kr = q / CPR, c = q - kr * CPR, p = k0 + kr, nn = n0 + 4 * c;
+        const int tap = nn >> a.lgCin, ci = nn & (a.Cin - 1);
+        if (p < a.K && nn < a.N && tap < 9) {
+          int b, h, w;
+          pix_decode(p, a, b, h, w);
+          const int t3 = tap / 3, hh = h + t3 - 1, ww = w + (tap - 3 * t3) - 1;
+          if ((unsigned)hh < (unsigned)a.H && (unsigned)ww < (unsigned)a.W)
+            v = *reinterpret_cast<const float4*>(a.x + ((((size_t)b * a.H + hh) * a.W + ww) << a.lgCin) + ci);
+        }
+      }
+      rb[i] = v;
+    }
+  }
+
+  __device__ void store(float* As, float* Bs) const {
+#pragma unroll
+    for (int i = 0; i < T::AC; ++i) {
+      const int q = threadIdx.x + 256 * i;
+      if constexpr (T::A_KC) {
+        *reinterpret_cast<float4*>(As + (q >> 2) * (BK + 4) + 4 * (q & 3)) = ra[i];
+      } else {
+        constexpr int CPR = BM / 4;
+        const int kr = q / CPR, c = q - kr * CPR;
+        *reinterpret_cast<float4*>(As + kr * (BM + 4) + 4 * c) = ra[i];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < T::BC; ++i) {
+      const int q = threadIdx.x + 256 * i;
+      if constexpr (T::B_KC) {
+        *reinterpret_cast<float4*>(Bs + (q >> 2) * (BK + 4) + 4 * (q & 3)) = rb[i];
+      } else {
+        constexpr int CPR = BN / 4;
+        const int kr = q / CPR, c = q - kr * CPR;
+        *reinterpret_cast<float4*>(Bs + kr * (BN + 4) + 4 * c) = rb[i];
+      }
+    }
+  }
+};
+
+template <int BM, int BN, int MODE>
+__global__ __launch_bounds__(256) void conv_gemm_kernel(CsConvArgs a) {
+  using T = Tile<BM, BN, MODE>;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int ntn = (a.N + BN - 1) / BN;
+  const int ntiles = ((a.M + BM - 1) / BM) * ntn;
+  const int tile = cs::xcd_remap(blockIdx.x, ntiles);
+  const int mt = tile / ntn, nt = tile - mt * ntn;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int split = blockIdx.z;
+  const int ks_begin = split * a.ksteps_per_split;
+  int ks_end = ks_begin + a.ksteps_per_split;
+  if (ks_end > a.total_ksteps) ks_end = a.total_ksteps;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1, r = lane & 31, hh = lane >> 5;
+
+  f32x16 acc[T::RM][T::RN];
+#pragma unroll
+  for (int i = 0; i < T::RM; ++i)
+#pragma unroll
+    for (int j = 0; j < T::RN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  Loader<BM, BN, MODE> ld;
+  ld.init(a, m0);
+  float* stage0 = smem;
+  float* stage1 = smem + T::STAGE;
+  if (ks_begin < ks_end) {
+    ld.load(a, m0, n0, ks_begin * BK);
+    ld.store(stage0, stage0 + T::A_ELEMS);
+  }
+  __syncthreads();
+  int cur = 0;
+  for (int ks = ks_begin; ks < ks_end; ++ks) {
+    const bool more = ks + 1 < ks_end;
+    if (more) ld.load(a, m0, n0, (ks + 1) * BK);
+    const float* As = cur ? stage1 : stage0;
+    const float* Bs = As + T::A_ELEMS;
+    float af[T::RM][8], bf[T::RN][8];
+#pragma unroll
+    for (int i = 0; i < T::RM; ++i) {
+      const int row = wm * T::WM + i * 32 + r;
+      if constexpr (T::A_KC) {
+        const float4 lo = *reinterpret_cast<const float4*>(As + row * (BK + 4) + 8 * hh);
+        const float4 hi = *reinterpret_cast<const float4*>(As + row * (BK + 4) + 8 * hh + 4);
+        af[i][0] = lo.x; af[i][1] = lo.y; af[i][2] = lo.z; af[i][3] = lo.w;
+        af[i][4] = hi.x; af[i][5] = hi.y; af[i][6] = hi.z; af[i][7] = hi.w;
+      } else {
+#pragma unroll
+        for (int s = 0; s < 8; ++s) af[i][s] = As[(8 * hh + s) * (BM + 4) + row];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < T::RN; ++j) {
+      const int col = wn * T::WN + j * 32 + r;
+      if constexpr (T::B_KC) {
+        const float4 lo = *reinterpret_cast<const float4*>(Bs + col * (BK + 4) + 8 * hh);
+        const float4 hi = *reinterpret_cast<const float4*>(Bs + col * (BK + 4) + 8 * hh + 4);
+        bf[j][0] = lo.x; bf[j][1] = lo.y; bf[j][2] = lo.z; bf[j][3] = lo.w;
+        bf[j][4] = hi.x; bf[j][5] = hi.y; bf[j][6] = hi.z; bf[j][7] = hi.w;
+      } else {
+#pragma unroll
+        for (int s = 0; s < 8; ++s) bf[j][s] = Bs[(8 * hh + s) * (BN + 4) + col];
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+#pragma unroll
+      for (int i = 0; i < T::RM; ++i)
+#pragma unroll
+        for (int j = 0; j < T::RN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][s], bf[j][s], acc[i][j], 0, 0, 0);
+    if (more) ld.store(cur ? stage0 : stage1, (cur ? stage0 : stage1) + T::A_ELEMS);
+    __syncthreads();
+    cur ^= 1;
+  }
+
+  // ------------------------------------------------------------------ epilogue
+  // C/D map (32x32 f32 MFMA): col = lane & 31, row = (reg&3) + 8*(reg>>2) + 4*(lane>>5)
+  const bool slab = gridDim.z > 1;
+  if (slab) {
+    float* dst = a.ws + (size_t)split * a.M * a.N;
+#pragma unroll
+    for (int i = 0; i < T::RM; ++i)
+#pragma unroll
+      for (int j = 0; j < T::RN; ++j) {
+        const int n = n0 + wn * T::WN + j * 32 + r;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int m = m0 + wm * T::WM + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * hh;
+          if (m < a.M && n < a.N) dst[(size_t)m * a.N + n] = acc[i][j][e];
+        }
+      }
+    return;
+  }
+  if constexpr (MODE == CS_CONV_WGRAD) {
+#pragma unroll
+    for (int i = 0; i < T::RM; ++i)
+#pragma unroll
+      for (int j = 0; j < T::RN; ++j) {
+        const int n = n0 + wn * T::WN + j * 32 + r;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int m = m0 + wm * T::WM + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * hh;
+          if (m < a.M && n < a.N) {
+            if (!a.w_oihw) {
+              a.out[(size_t)m * a.N + n] = acc[i][j][e];
+            } else {
+              const int tap = n >> 2, ci = n & 3;
+              if (ci < 3) a.out[(size_t)m * 27 + ci * 9 + tap] = acc[i][j][e];
+            }
+          }
+        }
+      }
+    return;
+  }
+  if constexpr (MODE == CS_CONV_DGRAD) {
+#pragma unroll
+    for (int i = 0; i < T::RM; ++i)
+#pragma unroll
+      for (int j = 0; j < T::RN; ++j) {
+        const int n = n0 + wn * T::WN + j * 32 + r;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int m = m0 + wm * T::WM + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * hh;
+          if (m < a.M && n < a.N) a.out[(size_t)m * a.N + n] = acc[i][j][e];
+        }
+      }
+    return;
+  }
+  if constexpr (MODE == CS_CONV_FWD) {
+    // bias, store, and this tile's per-channel (mean, M2) for the BN statistics
+    float* red = smem;  // [2][BN] after the main loop's final barrier
+    const int cnt = (a.M - m0) < BM ? (a.M - m0) : BM;
+    float colsum[T::RN];
+#pragma unroll
+    for (int j = 0; j < T::RN; ++j) {
+      const int n = n0 + wn * T::WN + j * 32 + r;
+      const float bv = (a.bias != nullptr && n < a.N) ? a.bias[n] : 0.f;
+      float s = 0.f;
+#pragma unroll
+      for (int i = 0; i < T::RM; ++i)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int m = m0 + wm * T::WM + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * hh;
+          const float v = acc[i][j][e] + bv;
+          acc[i][j][e] = v;
+          if (m < a.M) {
+            s += v;
+            if (n < a.N) a.out[(size_t)m * a.N + n] = v;
+          }
+        }
+      colsum[j] = s + __shfl_xor(s, 32, 64);
+    }
+    if (a.stats == nullptr) return;
+#pragma unroll
+    for (int j = 0; j < T::RN; ++j)
+      if (hh == 0) red[wm * BN + wn * T::WN + j * 32 + r] = colsum[j];
+    __syncthreads();
+    float mean[T::RN];
+#pragma unroll
+    for (int j = 0; j < T::RN; ++j) {
+      const int c = wn * T::WN + j * 32 + r;
+      mean[j] = (red[c] + red[BN + c]) / (float)cnt;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < T::RN; ++j) {
+      float s = 0.f;
+#pragma unroll
+      for (int i = 0; i < T::RM; ++i)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int m = m0 + wm * T::WM + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * hh;
+          const float d = acc[i][j][e] - mean[j];
+          if (m < a.M) s += d * d;
+        }
+      s += __shfl_xor(s, 32, 64);
+      if (hh == 0) red[wm * BN + wn * T::WN + j * 32 + r] = s;
+    }
+    __syncthreads();
+    if (wm == 0 && hh == 0) {
+#pragma unroll
+      for (int j = 0; j < T::RN; ++j) {
+        const int c = wn * T::WN + j * 32 + r, n = n0 + c;
+        if (n < a.N) {
+          a.stats[((size_t)mt * a.N + n) * 2 + 0] = mean[j];
+          a.stats[((size_t)mt * a.N + n) * 2 + 1] = red[c] + red[BN + c];
+        }
+      }
+    }
+  }
+}
+
+// Deterministic split-K combine: out = sum_z ws[z] (+bias, +BN tile stats for FWD;
+// OIHW scatter for the conv0 weight gradient). Tile = 64 rows x 64 columns.
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(CsConvArgs a, int mode, int splits) {
+  __shared__ float red[16][64];
+  __shared__ float meanv[64];
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const int ntn = (a.N + 63) / 64;
+  const int mt = blockIdx.x / ntn, nt = blockIdx.x - mt * ntn;
+  const int m0 = mt * 64, n0 = nt * 64, n = n0 + 4 * tx;
+  const size_t slab = (size_t)a.M * a.N;
+  float4 v[4];
+  float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (mode == CS_CONV_FWD && a.bias != nullptr && n < a.N) bv = *reinterpret_cast<const float4*>(a.bias + n);
+  float4 s1 = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    const int m = m0 + ty + 16 * rr;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (m < a.M && n < a.N) {
+      const float* p = a.ws + (size_t)m * a.N + n;
+      for (int z = 0; z < splits; ++z) {
+        const float4 t = *reinterpret_cast<const float4*>(p + z * slab);
+        acc.x += t.x; acc.y += t.y; acc.z += t.z; acc.w += t.w;
+      }
+      acc.x += bv.x; acc.y += bv.y; acc.z += bv.z; acc.w += bv.w;
+      if (mode == CS_CONV_WGRAD && a.w_oihw) {
+        const float vals[4] = {acc.x, acc.y, acc.z, acc.w};
+        for (int q = 0; q < 4; ++q) {
+          const int nn = n + q, tap = nn >> 2, ci = nn & 3;
+          if (ci < 3) a.out[(size_t)m * 27 + ci * 9 + tap] = vals[q];
+        }
+      } else {
+        *reinterpret_cast<float4*>(a.out + (size_t)m * a.N + n) = acc;
+      }
+      s1.x += acc.x; s1.y += acc.y; s1.z += acc.z; s1.w += acc.w;
+    }
+    v[rr] = acc;
+  }
+  if (mode != CS_CONV_FWD || a.stats == nullptr) return;
+  const int cnt = (a.M - m0) < 64 ? (a.M - m0) : 64;
+  red[ty][4 * tx + 0] = s1.x; red[ty][4 * tx + 1] = s1.y; red[ty][4 * tx + 2] = s1.z; red[ty][4 * tx + 3] = s1.w;
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    float s = 0.f;
+    for (int k = 0; k < 16; ++k) s += red[k][threadIdx.x];
+    meanv[threadIdx.x] = s / (float)cnt;
+  }
+  __syncthreads();
+  const float mx = meanv[4 * tx], my = meanv[4 * tx + 1], mz = meanv[4 * tx + 2], mw = meanv[4 * tx + 3];
+  float4 s2 = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    const int m = m0 + ty + 16 * rr;
+    if (m < a.M && n < a.N) {
+      const float dx = v[rr].x - mx, dy = v[rr].y - my, dz = v[rr].z - mz, dw = v[rr].w - mw;
+      s2.x += dx * dx; s2.y += dy * dy; s2.z += dz * dz; s2.w += dw * dw;
+    }
+  }
+  __syncthreads();
+  red[ty][4 * tx + 0] = s2.x; red[ty][4 * tx + 1] = s2.y; red[ty][4 * tx + 2] = s2.z; red[ty][4 * tx + 3] = s2.w;
+  __syncthreads();
+  if (threadIdx.x < 64 && n0 + (int)threadIdx.x < a.N) {
+    float s = 0.f;
+    for (int k = 0; k < 16; ++k) s += red[k][threadIdx.x];
+    a.stats[((size_t)mt * a.N + n0 + threadIdx.x) * 2 + 0] = meanv[threadIdx.x];
+    a.stats[((size_t)mt * a.N + n0 + threadIdx.x) * 2 + 1] = s;
+  }
+}
+
+template <int BM, int BN, int MODE>
+hipError_t launch_gemm(const CsConvArgs& a, int splits, hipStream_t stream) {
+  using T = Tile<BM, BN, MODE>;
+  const int ntiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
+  const size_t lds = 2 * T::STAGE * sizeof(float);
+  hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, MODE>), dim3(ntiles, 1, splits), dim3(256), lds, stream, a);
+  return hipGetLastError();
+}
+
+int ilog2(int v) {
+  int l = 0;
+  while ((1 << l) < v) ++l;
+  return l;
+}
+
+}  // namespace
+
+int cs_conv_lg(int v) { return ilog2(v); }
+
+void cs_conv_fill_dims(CsConvArgs* a, int mode) {
+  a->lgH = ilog2(a->H);
+  a->lgW = ilog2(a->W);
+  a->lgCin = ilog2(a->Cin);
+  a->lgCout = ilog2(a->Cout);
+  const int pix = a->B * a->H * a->W;
+  if (mode == CS_CONV_FWD) {
+    a->M = pix;
+    a->N = a->Cout;
+    a->K = 9 * a->Cin;
+  } else if (mode == CS_CONV_DGRAD) {
+    a->M = pix;
+    a->N = a->Cin;
+    a->K = 9 * a->Cout;
+  } else {
+    a->M = a->Cout;
+    a->N = 9 * a->Cin;
+    a->K = pix;
+  }
+}
+
+hipError_t cs_conv_gemm(CsConvArgs a, int mode, int bm, int bn, int splits, hipStream_t stream) {
+  cs_conv_fill_dims(&a, mode);
+  a.total_ksteps = (a.K + BK - 1) / BK;
+  if (splits < 1) splits = 1;
+  if (splits > a.total_ksteps) splits = a.total_ksteps;
+  a.ksteps_per_split = (a.total_ksteps + splits - 1) / splits;
+  splits = (a.total_ksteps + a.ksteps_per_split - 1) / a.ksteps_per_split;
+  if (splits > 1 && a.ws == nullptr) return hipErrorInvalidValue;
+#define CS_DISPATCH(BM_, BN_)                                                   \
+  if (bm == BM_ && bn == BN_) {                                                 \
+    hipError_t e;                                                               \
+    if (mode == CS_CONV_FWD) e = launch_gemm<BM_, BN_, CS_CONV_FWD>(a, splits, stream);          \
+    else if (mode == CS_CONV_DGRAD) e = launch_gemm<BM_, BN_, CS_CONV_DGRAD>(a, splits, stream); \
+    else e = launch_gemm<BM_, BN_, CS_CONV_WGRAD>(a, splits, stream);                            \
+    if (e != hipSuccess || splits == 1) return e;                               \
+    const int nt = ((a.M + 63) / 64) * ((a.N + 63) / 64);                        \
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(nt), dim3(256), 0, stream, a, mode, splits); \
+    return hipGetLastError();                                                   \
+  }
+  CS_DISPATCH(64, 64)
+  CS_DISPATCH(128, 64)
+  CS_DISPATCH(64, 128)
+  CS_DISPATCH(128, 128)
+#undef CS_DISPATCH
+  return hipErrorInvalidValue;
+}

@@ -27,3 +27,39 @@ hipError_t cs_linear_xent(const float* feat, const float* W, const float* bias, 
                           float* db, float* dfeat, int64_t* pred_out, hipStream_t stream);
 hipError_t cs_softmax_xent(const float* logits, const int64_t* labels, int B, int C, float gscale, float* loss_out,
                            float* dlogits, int* correct_out, hipStream_t stream);
+
+// ---------------------------------------------------------------- conv (implicit GEMM, fp32 MFMA)
+enum { CS_CONV_FWD = 0, CS_CONV_DGRAD = 1, CS_CONV_WGRAD = 2 };
+
+struct CsConvArgs {
+  const float* x;     // FWD / WGRAD: conv input, NHWC [B,H,W,Cin] (Cin = 4 for the padded conv0 input)
+  const float* w;     // FWD / DGRAD: weights, OHWI [Cout][9][Cin]; conv0 (w_oihw=1): OIHW [Cout][3][9]
+  const float* dz;    // DGRAD / WGRAD: gradient w.r.t. conv output, NHWC [B,H,W,Cout]
+  const float* bias;  // FWD: [Cout] or null
+  float* out;         // FWD: y [M][Cout]; DGRAD: dx [M][Cin]; WGRAD: dW (OHWI, or OIHW for conv0)
+  float* ws;          // split-K slabs [splits][M][N] (required when splits > 1)
+  float* stats;       // FWD: per-row-tile BN partials [tiles][Cout][2] = (mean, M2); may be null
+  int B, H, W, Cin, Cout;
+  int w_oihw;
+  // filled by the launcher:
+  int lgH, lgW, lgCin, lgCout, M, N, K, ksteps_per_split, total_ksteps;
+};
+
+void cs_conv_fill_dims(CsConvArgs* a, int mode);
+// bm, bn in {64, 128}; splits >= 1 (split-K over blockIdx.z + deterministic reduce).
+// FWD stats tiles have `bm` rows when splits == 1 and 64 rows otherwise.
+hipError_t cs_conv_gemm(CsConvArgs a, int mode, int bm, int bn, int splits, hipStream_t stream);
+
+// ---------------------------------------------------------------- BatchNorm + ReLU (+ 2x2 max-pool), NHWC
+hipError_t cs_bn_finalize(const float* part, int T, int R, int M, int C, const float* gamma, const float* beta,
+                          float* running_mean, float* running_var, int64_t* nbt, float momentum, float eps,
+                          float* scale, float* shift, float* save_mean, float* save_invstd, hipStream_t stream);
+hipError_t cs_bn_eval_coeffs(const float* gamma, const float* beta, const float* rm, const float* rv, int C, float eps,
+                             float* scale, float* shift, hipStream_t stream);
+hipError_t cs_bn_apply(const float* y, const float* scale, const float* shift, float* out, int B, int H, int W, int C,
+                       int pool, hipStream_t stream);
+int cs_bn_bwd_blocks(int B, int H, int W, int C, int pool);
+// part: [cs_bn_bwd_blocks][C][3] scratch; coef: [C][3] scratch; dgamma/dbeta/dbias may be null.
+hipError_t cs_bn_bwd(const float* y, const float* G, int B, int H, int W, int C, int pool, const float* scale,
+                     const float* shift, const float* mean, const float* invstd, const float* gamma, float* part,
+                     float* coef, float* dgamma, float* dbeta, float* dbias, float* dz, hipStream_t stream);
