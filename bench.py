@@ -42,15 +42,16 @@ def parse(argv=None):
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--batch-size", type=int, default=64, help="per-GPU batch")
     p.add_argument("--model", type=str, default="VGG11")
-    p.add_argument("--engine", type=str, default=os.environ.get("CS744_BENCH_ENGINE", "torch"),
+    p.add_argument("--engine", type=str, default=os.environ.get("CS744_BENCH_ENGINE", "native"),
                    choices=["torch", "native"])
     p.add_argument("--sync", type=str, default="ddp",
                    choices=["ddp", "allreduce", "gather_scatter", "p2p", "flat"])
-    p.add_argument("--comm", type=str, default="torch", choices=["torch", "rccl"])
-    p.add_argument("--bucket-mb", type=float, default=4.0)
+    p.add_argument("--comm", type=str, default="rccl", choices=["torch", "rccl"])
+    p.add_argument("--bucket-mb", type=float, default=9.0)
     p.add_argument("--bucket-policy", type=str, default="layer", choices=["size", "layer", "single"])
     p.add_argument("--dtype", type=str, default="fp32", choices=["fp32", "bf16"])
     p.add_argument("--no-graph", action="store_true", help="native engine: disable hipGraph capture")
+    p.add_argument("--graph", type=str, default="auto", choices=["auto", "full", "segments", "none"])
     p.add_argument("--json-out", type=str, default=None)
     return p.parse_args(argv)
 

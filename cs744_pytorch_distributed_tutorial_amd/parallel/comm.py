@@ -54,6 +54,26 @@ class Comm:
     def all_gather_int64(self, values: torch.Tensor) -> torch.Tensor:
         raise NotImplementedError
 
+    # flat-buffer primitives used by ``parallel.flat_sync`` (blocking w.r.t. the caller's stream)
+    def all_reduce(self, buf: torch.Tensor, op: str = "sum") -> None:
+        raise NotImplementedError
+
+    def gather_flat(self, buf: torch.Tensor, out: Optional[torch.Tensor], dst: int = 0) -> None:
+        """``out`` (on ``dst`` only) receives ``world * buf.numel()`` elements, rank-major."""
+        raise NotImplementedError
+
+    def send(self, buf: torch.Tensor, dst: int) -> None:
+        raise NotImplementedError
+
+    def recv(self, buf: torch.Tensor, src: int) -> None:
+        raise NotImplementedError
+
+    def join(self) -> None:
+        """Make the caller's current stream wait for all communication issued so far."""
+
+
+_OPS = {"sum": D.ReduceOp.SUM, "avg": D.ReduceOp.AVG, "max": D.ReduceOp.MAX, "min": D.ReduceOp.MIN}
+
 
 class TorchComm(Comm):
     def __init__(self, group=None):
@@ -81,6 +101,24 @@ class TorchComm(Comm):
         out = [torch.zeros_like(values) for _ in range(self.world_size)]
         D.all_gather(out, values, group=self.group)
         return torch.stack(out)
+
+    def all_reduce(self, buf: torch.Tensor, op: str = "sum") -> None:
+        if self.world_size > 1:
+            D.all_reduce(buf, op=_OPS[op], group=self.group)  # the facade maps AVG to SUM+scale on gloo
+
+    def gather_flat(self, buf: torch.Tensor, out: Optional[torch.Tensor], dst: int = 0) -> None:
+        if self.world_size == 1:
+            if out is not None:
+                out.copy_(buf.reshape(-1))
+            return
+        lst = list(out.view(self.world_size, -1).unbind(0)) if self.rank == dst else None
+        D.gather(buf, lst, dst=dst, group=self.group)
+
+    def send(self, buf: torch.Tensor, dst: int) -> None:
+        D.isend(buf, dst, group=self.group).wait()
+
+    def recv(self, buf: torch.Tensor, src: int) -> None:
+        D.irecv(buf, src, group=self.group).wait()
 
 
 def make_comm(kind: Optional[str] = None, group=None) -> Comm:

@@ -1,0 +1,101 @@
+"""Gradient synchronisation on a FLAT gradient buffer (the native engine's layout).
+
+Same four strategies as ``parallel.sync`` (which works on ``param.grad``
+tensors for the autograd path), expressed over ``(offset, numel)`` ranges of
+one flat buffer, so the native engine can run every mode of the tutorial with
+either communicator (``TorchComm``: ProcessGroupNCCL/gloo; ``RcclComm``: the
+native C++ RCCL communicator):
+
+==================  =========================================================  ==============================
+mode                reference                                                  pattern here
+==================  =========================================================  ==============================
+``gather_scatter``  part2a (`master/part2a/part2a.py:42-52`)                   per tensor: gather to rank 0,
+                                                                               mean on rank 0, send the mean
+                                                                               back (a scatter of N identical
+                                                                               shards == a broadcast)
+``p2p``             part2a_extra (`master/part2a/part2a_extra.py:41-58`)       per tensor star: rank 0 recvs
+                                                                               from 1..N-1, averages, sends
+                                                                               back; every message waited
+``allreduce``       part2b (`master/part2b/part2b.py:43-45`)                   per tensor all_reduce(AVG)
+                                                                               (AVG == the reference's /N then
+                                                                               SUM, one pass fewer)
+``flat``            — (extension)                                              ONE all_reduce(AVG) of the
+                                                                               whole buffer
+``ddp``             part3 (`master/part3/part3.py:116`)                        per bucket all_reduce(AVG),
+                                                                               launched by the engine during
+                                                                               backward (not here)
+==================  =========================================================  ==============================
+
+Ranges are visited in the reference's ``model.parameters()`` order. Runs on
+CPU tensors over gloo too, which is how the multi-rank logic is unit-tested
+without GPUs.
+"""
+from __future__ import annotations
+
+from typing import List, Sequence, Tuple
+
+import torch
+
+from .comm import Comm
+
+FLAT_MODES = ("gather_scatter", "p2p", "allreduce", "flat", "ddp", "none")
+
+
+class FlatGradSync:
+    def __init__(self, mode: str, comm: Comm, ranges: Sequence[Tuple[int, int]], total: int, root: int = 0):
+        if mode not in FLAT_MODES:
+            raise ValueError(f"unknown sync mode {mode!r}; choose from {FLAT_MODES}")
+        self.mode, self.comm, self.root = mode, comm, root
+        self.ranges: List[Tuple[int, int]] = list(ranges)
+        self.total = total
+        self._scratch = None
+
+    def _tmp(self, n: int, like: torch.Tensor) -> torch.Tensor:
+        if self._scratch is None or self._scratch.numel() < n or self._scratch.device != like.device:
+            self._scratch = torch.empty(max(n, 1), dtype=like.dtype, device=like.device)
+        return self._scratch[:n]
+
+    def __call__(self, flat_grad: torch.Tensor) -> None:
+        w = self.comm.world_size
+        if w == 1 or self.mode in ("none", "ddp"):
+            return
+        if self.mode == "flat":
+            self.comm.all_reduce(flat_grad[:self.total], "avg")
+        elif self.mode == "allreduce":
+            for off, n in self.ranges:
+                self.comm.all_reduce(flat_grad[off:off + n], "avg")
+        elif self.mode == "gather_scatter":
+            self._gather_scatter(flat_grad)
+        elif self.mode == "p2p":
+            self._p2p(flat_grad)
+        self.comm.join()
+
+    def _gather_scatter(self, flat_grad: torch.Tensor) -> None:
+        w, r = self.comm.world_size, self.comm.rank
+        maxn = max(n for _, n in self.ranges)
+        for off, n in self.ranges:
+            g = flat_grad[off:off + n]
+            out = self._tmp(w * maxn, g)[:w * n] if r == self.root else None
+            self.comm.gather_flat(g, out, self.root)
+            if r == self.root:
+                torch.mean(out.view(w, n), 0, out=g)
+            self.comm.broadcast(g, self.root)
+
+    def _p2p(self, flat_grad: torch.Tensor) -> None:
+        w, r = self.comm.world_size, self.comm.rank
+        for off, n in self.ranges:
+            g = flat_grad[off:off + n]
+            if r == self.root:
+                tmp = self._tmp(n, g)
+                for src in range(w):
+                    if src == self.root:
+                        continue
+                    self.comm.recv(tmp, src)
+                    g.add_(tmp)
+                g.div_(w)
+                for dst in range(w):
+                    if dst != self.root:
+                        self.comm.send(g, dst)
+            else:
+                self.comm.send(g, self.root)
+                self.comm.recv(g, self.root)

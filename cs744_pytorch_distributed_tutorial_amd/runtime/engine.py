@@ -1,0 +1,476 @@
+"""Native training engine: VGG on MI355X through the C++ ``VggEngine`` + hipGraphs.
+
+This is the MI355X-first replacement for the reference's whole training loop
+(`master/part1/part1.py:31-38`, `master/part2b/part2b.py:35-46`,
+`master/part3/part3.py:24-48`): no autograd, no nn.Module dispatch, no per-step
+host work beyond one index copy and graph replays.
+
+* ``FlatLayout`` — parameters / gradients / momentum live in three flat fp32
+  buffers in *backward-ready* order (fc1, then conv blocks last -> first), each
+  tensor 256-B aligned; conv weights are OHWI (conv0 keeps OIHW). It converts
+  to / from the reference ``state_dict`` (58 keys for VGG-11),
+  so checkpoints load into the reference ``_VGG`` unchanged.
+* ``NativeTrainer`` — owns the engine, the device-resident synthetic CIFAR-10,
+  the DistributedSampler shard, the communicator and the gradient-sync mode:
+  ``ddp`` (bucketed all-reduce(AVG) launched as soon as a bucket's backward
+  completes, overlapped with the rest of backward), or the faithful modes
+  ``allreduce`` / ``gather_scatter`` / ``p2p`` / ``flat`` run after backward.
+  Graph modes: ``full`` (the whole step, RCCL included, is ONE hipGraph),
+  ``segments`` (one graph per bucket segment, collectives issued eagerly
+  between them — the default with >1 rank), ``none`` (eager).
+"""
+from __future__ import annotations
+
+import math
+import os
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+
+from .. import distributed as D
+from ..models.vgg import VGG, block_specs, CFG
+from ..ops import native
+from ..parallel.flat_sync import FlatGradSync
+from ..utils import data as dm
+
+ALIGN = 64  # floats (256 B)
+
+
+def _align(n: int) -> int:
+    return (n + ALIGN - 1) // ALIGN * ALIGN
+
+
+class FlatLayout:
+    """Offsets of every VGG tensor inside the engine's flat buffers."""
+
+    def __init__(self, model_name: str = "VGG11", feat: int = 512, ncls: int = 10):
+        self.model_name = model_name
+        self.specs = block_specs(CFG[model_name])
+        self.L = len(self.specs)
+        self.feat, self.ncls = feat, ncls
+        off = 0
+        self.entries: Dict[str, Tuple[int, Tuple[int, ...], str]] = {}  # name -> (offset, torch shape, kind)
+        self.order: List[str] = []
+
+        def add(name, shape, kind):
+            nonlocal off
+            n = int(math.prod(shape))
+            self.entries[name] = (off, tuple(shape), kind)
+            self.order.append(name)
+            off = _align(off + n)
+
+        add("fc1.weight", (ncls, feat), "plain")
+        add("fc1.bias", (ncls,), "plain")
+        self.block_start: List[int] = [0] * self.L
+        self.block_end: List[int] = [0] * self.L
+        for l in range(self.L - 1, -1, -1):
+            s = self.specs[l]
+            self.block_start[l] = off
+            add(f"layers.{s.conv_idx}.weight", (s.cout, s.cin, 3, 3), "oihw" if l == 0 else "ohwi")
+            add(f"layers.{s.conv_idx}.bias", (s.cout,), "plain")
+            add(f"layers.{s.bn_idx}.weight", (s.cout,), "plain")
+            add(f"layers.{s.bn_idx}.bias", (s.cout,), "plain")
+            self.block_end[l] = off
+        self.total = off
+        boff = 0
+        self.buf_entries: Dict[str, Tuple[int, int]] = {}
+        for l, s in enumerate(self.specs):
+            for nm in ("running_mean", "running_var"):
+                self.buf_entries[f"layers.{s.bn_idx}.{nm}"] = (boff, s.cout)
+                boff = _align(boff + s.cout)
+        self.buf_total = boff
+        # the reference's parameter order (model.parameters()): used by the faithful sync modes
+        ref = VGG(model_name)
+        self.param_names = [n for n, _ in ref.named_parameters()]
+        self.buffer_names = [n for n, _ in ref.named_buffers()]
+        self.state_keys = list(ref.state_dict().keys())
+
+    # ---------------------------------------------------------------- engine args
+    def desc(self) -> List[int]:
+        out = []
+        for l, s in enumerate(self.specs):
+            out += [4 if l == 0 else s.cin, s.cout, s.hw, 1 if s.pool else 0]
+        return out
+
+    def offs(self) -> List[int]:
+        out = []
+        for s in self.specs:
+            out += [self.entries[f"layers.{s.conv_idx}.weight"][0], self.entries[f"layers.{s.conv_idx}.bias"][0],
+                    self.entries[f"layers.{s.bn_idx}.weight"][0], self.entries[f"layers.{s.bn_idx}.bias"][0]]
+        return out + [self.entries["fc1.weight"][0], self.entries["fc1.bias"][0]]
+
+    def buf_offs(self) -> List[int]:
+        out = []
+        for s in self.specs:
+            out += [self.buf_entries[f"layers.{s.bn_idx}.running_mean"][0],
+                    self.buf_entries[f"layers.{s.bn_idx}.running_var"][0]]
+        return out
+
+    def param_ranges(self) -> List[Tuple[int, int]]:
+        """(offset, numel) per parameter tensor in the reference's model.parameters() order."""
+        return [(self.entries[n][0], int(math.prod(self.entries[n][1]))) for n in self.param_names]
+
+    # ---------------------------------------------------------------- conversions
+    def view(self, flat: torch.Tensor, name: str) -> torch.Tensor:
+        """Torch-layout view (conv weights as a permuted OIHW view of the OHWI storage)."""
+        off, shape, kind = self.entries[name]
+        n = int(math.prod(shape))
+        v = flat[off:off + n]
+        if kind == "ohwi":
+            o, i, kh, kw = shape
+            return v.view(o, kh, kw, i).permute(0, 3, 1, 2)
+        return v.view(shape)
+
+    def pack(self, state: Dict[str, torch.Tensor], params: torch.Tensor, bufs: torch.Tensor,
+             nbt: torch.Tensor) -> None:
+        """Copy a reference-layout state_dict into the flat buffers (padding stays zero)."""
+        with torch.no_grad():
+            for name in self.order:
+                self.view(params, name).copy_(state[name])
+            for name, (off, n) in self.buf_entries.items():
+                bufs[off:off + n].copy_(state[name])
+            for l, s in enumerate(self.specs):
+                nbt[l].copy_(state[f"layers.{s.bn_idx}.num_batches_tracked"].reshape(()))
+
+    def unpack(self, params: torch.Tensor, bufs: torch.Tensor, nbt: torch.Tensor) -> Dict[str, torch.Tensor]:
+        """Flat buffers -> reference-layout state_dict (CPU, contiguous, reference key order)."""
+        out: Dict[str, torch.Tensor] = {}
+        for name in self.order:
+            out[name] = self.view(params, name).detach().cpu().contiguous()
+        for name, (off, n) in self.buf_entries.items():
+            out[name] = bufs[off:off + n].detach().cpu().clone()
+        for l, s in enumerate(self.specs):
+            out[f"layers.{s.bn_idx}.num_batches_tracked"] = nbt[l].detach().cpu().clone()
+        return {k: out[k] for k in self.state_keys}
+
+    def unpack_grads(self, grads: torch.Tensor) -> Dict[str, torch.Tensor]:
+        return {n: self.view(grads, n).detach().cpu().contiguous() for n in self.param_names}
+
+    # ---------------------------------------------------------------- buckets
+    def plan_buckets(self, cap_mb: float) -> Tuple[List[int], List[Tuple[int, int]]]:
+        """Block-aligned buckets from the top: (lowest block per bucket, (offset, numel) per bucket)."""
+        cap = cap_mb * 1024 * 1024
+        lows: List[int] = []
+        ranges: List[Tuple[int, int]] = []
+        start, acc = 0, self.block_start[self.L - 1] * 4  # fc1 rides in the first bucket
+        for l in range(self.L - 1, -1, -1):
+            acc += (self.block_end[l] - self.block_start[l]) * 4
+            if acc >= cap or l == 0:
+                lows.append(l)
+                ranges.append((start, self.block_end[l] - start))
+                start, acc = self.block_end[l], 0
+        return lows, ranges
+
+
+class NativeTrainer:
+    """VGG training on the native engine; one instance per rank (one GPU per process)."""
+
+    def __init__(self, model: str = "VGG11", batch_size: int = 64, device: Optional[torch.device] = None,
+                 rank: int = 0, world: int = 1, sync: str = "ddp", comm: str = "rccl", bucket_mb: float = 9.0,
+                 graph: str = "auto", lr: float = 0.1, momentum: float = 0.9, weight_decay: float = 1e-4,
+                 dampening: float = 0.0, seed: int = 5000, data_seed: int = 0, train_size: Optional[int] = None,
+                 test_size: Optional[int] = None, autotune: bool = True, broadcast_buffers: bool = True,
+                 drop_last: bool = True, init_state: Optional[Dict[str, torch.Tensor]] = None):
+        C = native.C()
+        self.device = device or torch.device("cuda", torch.cuda.current_device())
+        self.rank, self.world = rank, world
+        self.B = batch_size
+        self.lr, self.momentum, self.wd, self.damp = lr, momentum, weight_decay, dampening
+        self.sync_mode = sync if world > 1 else "none"
+        self.broadcast_buffers = broadcast_buffers
+        self.layout = lay = FlatLayout(model)
+        f32 = dict(device=self.device, dtype=torch.float32)
+        self.params = torch.zeros(lay.total, **f32)
+        self.grads = torch.zeros(lay.total, **f32)
+        self.mom = torch.zeros(lay.total, **f32)
+        self.bufs = torch.zeros(lay.buf_total, **f32)
+        self.nbt = torch.zeros(lay.L, dtype=torch.int64, device=self.device)
+        if init_state is None:
+            torch.manual_seed(seed)  # identical init on every rank (reference S1, master/part2b/part2b.py:82)
+            init_state = VGG(model).state_dict()
+        lay.pack(init_state, self.params, self.bufs, self.nbt)
+
+        # communicator + DDP construction-time sync (params + buffers from rank 0)
+        self.comm = None
+        if world > 1:
+            from ..parallel.comm import make_comm
+            self.comm = make_comm(comm)
+            self.comm.broadcast(self.params, 0)
+            self.comm.broadcast(self.bufs, 0)
+            self.comm.broadcast(self.nbt, 0)
+        self.native_comm = getattr(self.comm, "native", None)
+        self.bucket_lows, self.bucket_ranges = lay.plan_buckets(bucket_mb if sync == "ddp" else 1e9)
+        self.flat_sync = FlatGradSync(self.sync_mode if self.sync_mode != "ddp" else "none", self.comm,
+                                      lay.param_ranges(), lay.total) if self.comm is not None else None
+
+        # data: whole synthetic CIFAR-10 resident in HBM; sampler shard per rank
+        self.train_set = dm.SyntheticCIFAR10(train=True, size=train_size, seed=data_seed)
+        self.test_set = dm.SyntheticCIFAR10(train=False, size=test_size, seed=data_seed)
+        self.sampler = dm.DistributedSampler(len(self.train_set), world, rank, shuffle=True, seed=0)
+        self.data_seed = data_seed
+        self.drop_last = drop_last
+        self.train_data = self.train_set.data.to(self.device)
+        self.train_labels = self.train_set.targets.to(self.device)
+        self.test_data = self.test_set.data.to(self.device)
+        self.test_labels = self.test_set.targets.to(self.device)
+        self.aug_train = dm.augment_params(len(self.train_set), data_seed, 0, True).to(self.device)
+        self.aug_test = dm.augment_params(len(self.test_set), data_seed, 0, False).to(self.device)
+
+        self.engine = C.VggEngine(self.B, lay.desc(), lay.offs(), lay.buf_offs(), lay.feat, lay.ncls,
+                                  self.params, self.grads, self.mom, self.bufs, self.nbt)
+        self.engine.set_data(0, self.train_data, self.train_labels, self.aug_train)
+        self.engine.set_data(1, self.test_data, self.test_labels, self.aug_test)
+        self.idx_buf = self.engine.idx()
+        self.tune_us: Optional[List[float]] = None
+        if autotune:
+            self.tune_us = list(self.engine.autotune(self.B, 5))
+        if graph == "auto":
+            graph = "full" if world == 1 else "segments"
+        if graph == "full" and world > 1 and (self.native_comm is None or self.sync_mode not in ("ddp", "none")):
+            graph = "segments"  # only the native communicator can be captured together with the step
+        if graph not in ("full", "segments", "none"):
+            raise ValueError(f"graph mode {graph!r}: choose full | segments | none | auto")
+        self.graph_mode = graph
+        self._graphs: Optional[List[torch.cuda.CUDAGraph]] = None
+        self._pool = None
+        self.epoch = 0
+        self.iter_in_epoch = 0
+        self.global_step = 0
+        self._epoch_idx = None
+        self._start_epoch(0)
+
+    # ---------------------------------------------------------------- data
+    def steps_per_epoch(self) -> int:
+        n = len(self.sampler)
+        return n // self.B if self.drop_last else math.ceil(n / self.B)
+
+    def _start_epoch(self, epoch: int) -> None:
+        self.epoch = epoch
+        self.sampler.set_epoch(epoch)
+        self._epoch_idx = torch.tensor(self.sampler.indices(), dtype=torch.int64).to(self.device)
+        self.aug_train.copy_(dm.augment_params(len(self.train_set), self.data_seed, epoch, True).to(self.device))
+        self.iter_in_epoch = 0
+
+    def _load_next_batch(self) -> int:
+        if self.iter_in_epoch >= self.steps_per_epoch():
+            self._start_epoch(self.epoch + 1)
+        s = self.iter_in_epoch * self.B
+        idx = self._epoch_idx[s:s + self.B]
+        self.idx_buf[:idx.numel()].copy_(idx)
+        self.iter_in_epoch += 1
+        return idx.numel()
+
+    # ---------------------------------------------------------------- step pieces
+    def _segments(self) -> List[Tuple[int, int]]:
+        hi, out = self.layout.L - 1, []
+        for lo in self.bucket_lows:
+            out.append((hi, lo))
+            hi = lo - 1
+        return out
+
+    def _run_segment(self, k: int, B: int) -> None:
+        hi, lo = self._segments()[k]
+        if k == 0:
+            self.engine.forward_train(B)
+        self.engine.backward(hi, lo, B)
+
+    def _sgd(self) -> None:
+        self.engine.sgd(self.lr, self.momentum, self.wd, self.damp, 0, self.layout.total)
+
+    def _bucket_view(self, k: int) -> torch.Tensor:
+        off, n = self.bucket_ranges[k]
+        return self.grads[off:off + n]
+
+    def _step_full_native(self, B: int) -> None:
+        ranges = [v for r in self.bucket_ranges for v in r]
+        self.engine.step(B, self.native_comm, self.bucket_lows, ranges, self.broadcast_buffers and self.world > 1,
+                         self.lr, self.momentum, self.wd, self.damp)
+
+    def _pre_forward_sync(self) -> None:
+        if self.comm is not None and self.sync_mode == "ddp" and self.broadcast_buffers:
+            self.comm.broadcast(self.bufs, 0)
+            self.comm.broadcast(self.nbt, 0)
+
+    def _step_eager(self, B: int, graphs: Optional[List] = None) -> None:
+        """Eager (or segment-graph) orchestration with collectives between segments."""
+        nseg = len(self.bucket_lows)
+        if self.sync_mode == "ddp":
+            self._pre_forward_sync()
+            handles = []
+            for k in range(nseg):
+                if graphs is not None:
+                    graphs[k].replay()
+                else:
+                    self._run_segment(k, B)
+                handles.append(self.comm.all_reduce_avg(self._bucket_view(k), async_op=True))
+            for h in handles:
+                h.wait()
+        else:
+            for k in range(nseg):
+                if graphs is not None:
+                    graphs[k].replay()
+                else:
+                    self._run_segment(k, B)
+            if self.flat_sync is not None:
+                self.flat_sync(self.grads)
+        if graphs is not None:
+            graphs[nseg].replay()
+        else:
+            self._sgd()
+
+    def _capture(self) -> None:
+        B = self.B
+        self._pool = torch.cuda.graph_pool_handle()
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream())
+        graphs = []
+        with torch.cuda.stream(s):
+            if self.graph_mode == "full":
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=self._pool, stream=s):
+                    self._step_full_native(B)
+                graphs.append(g)
+            else:
+                for k in range(len(self.bucket_lows)):
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g, pool=self._pool, stream=s):
+                        self._run_segment(k, B)
+                    graphs.append(g)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=self._pool, stream=s):
+                    self._sgd()
+                graphs.append(g)
+        torch.cuda.current_stream().wait_stream(s)
+        self._graphs = graphs
+
+    def step(self) -> None:
+        """One training iteration: next batch -> forward -> backward (+grad sync) -> SGD."""
+        B = self._load_next_batch()
+        use_graph = self.graph_mode != "none" and B == self.B and self.global_step >= 2
+        if use_graph and self._graphs is None:
+            self._capture()
+        if use_graph and self.graph_mode == "full":
+            self._graphs[0].replay()
+        elif use_graph:
+            self._step_eager(B, self._graphs)
+        elif self.sync_mode in ("ddp", "none") and (self.comm is None or self.native_comm is not None):
+            self._step_full_native(B)
+        else:
+            self._step_eager(B)
+        self.global_step += 1
+
+    def last_loss(self) -> float:
+        return float(self.engine.loss().item())
+
+    def loss_tensor(self) -> torch.Tensor:
+        return self.engine.loss()
+
+    # ---------------------------------------------------------------- eval / state
+    @torch.no_grad()
+    def evaluate(self, max_batches: Optional[int] = None) -> Dict[str, float]:
+        """Full (non-sharded) test-set evaluation, as every reference rank does (`part2b.py:111-115`)."""
+        if self.comm is not None and self.sync_mode == "ddp" and self.broadcast_buffers:
+            self._pre_forward_sync()
+        n = len(self.test_set)
+        loss_sum = torch.zeros((), dtype=torch.float64, device=self.device)
+        correct = torch.zeros((), dtype=torch.int64, device=self.device)
+        nb = 0
+        all_idx = torch.arange(n, device=self.device)
+        for s in range(0, n, self.B):
+            if max_batches is not None and nb >= max_batches:
+                break
+            idx = all_idx[s:s + self.B]
+            self.idx_buf[:idx.numel()].copy_(idx)
+            self.engine.forward_eval(idx.numel())
+            loss_sum += self.engine.loss().double()
+            correct += self.engine.correct().long()
+            nb += 1
+        total = min(n, nb * self.B)
+        return {"avg_loss": float(loss_sum.item()) / max(nb, 1), "correct": int(correct.item()), "total": total}
+
+    def state_dict(self) -> Dict[str, torch.Tensor]:
+        return self.layout.unpack(self.params, self.bufs, self.nbt)
+
+    def load_state_dict(self, sd: Dict[str, torch.Tensor]) -> None:
+        self.layout.pack(sd, self.params, self.bufs, self.nbt)
+
+    def optimizer_state_dict(self) -> dict:
+        """torch.optim.SGD ``state_dict`` format (momentum_buffer per parameter index)."""
+        state = {i: {"momentum_buffer": self.layout.view(self.mom, n).detach().cpu().contiguous()}
+                 for i, n in enumerate(self.layout.param_names)} if self.global_step > 0 else {}
+        group = {"lr": self.lr, "momentum": self.momentum, "dampening": self.damp, "weight_decay": self.wd,
+                 "nesterov": False, "maximize": False, "foreach": None, "differentiable": False, "fused": None,
+                 "params": list(range(len(self.layout.param_names)))}
+        return {"state": state, "param_groups": [group]}
+
+    def load_optimizer_state_dict(self, sd: dict) -> None:
+        with torch.no_grad():
+            self.mom.zero_()
+            for i, n in enumerate(self.layout.param_names):
+                st = sd["state"].get(i) or sd["state"].get(str(i))
+                if st is not None and st.get("momentum_buffer") is not None:
+                    self.layout.view(self.mom, n).copy_(st["momentum_buffer"])
+            if sd["state"]:
+                self.global_step = max(self.global_step, 1)
+
+    def grads_state(self) -> Dict[str, torch.Tensor]:
+        return self.layout.unpack_grads(self.grads)
+
+    @classmethod
+    def from_bench_args(cls, args, device, rank, world) -> "NativeTrainer":
+        return cls(model=args.model, batch_size=args.batch_size, device=device, rank=rank, world=world,
+                   sync=args.sync, comm=args.comm, bucket_mb=args.bucket_mb,
+                   graph="none" if args.no_graph else getattr(args, "graph", "auto"))
+
+
+def run_native(cfg, device, logger) -> dict:
+    """Entry-point runner (part1/part2*/part3 with ``--engine native``)."""
+    import time
+    rank, world = D.get_rank(), D.get_world_size()
+    mode = cfg.resolved_sync() if world > 1 else "none"
+    tr = NativeTrainer(model=cfg.model, batch_size=cfg.resolved_batch_size(), device=device, rank=rank,
+                       world=world, sync=mode, comm=cfg.comm if cfg.comm != "torch" else "torch",
+                       bucket_mb=cfg.bucket_mb, lr=cfg.lr, momentum=cfg.momentum, weight_decay=cfg.weight_decay,
+                       seed=cfg.seed, data_seed=cfg.data_seed, train_size=cfg.train_size, test_size=cfg.test_size,
+                       drop_last=False)
+    if cfg.resume:
+        from ..utils.checkpoint import load_checkpoint
+        st = load_checkpoint(cfg.resume)
+        tr.load_state_dict(st["model"])
+        if st.get("optimizer"):
+            tr.load_optimizer_state_dict(st["optimizer"])
+    results = {"rank": rank, "world": world, "sync": mode, "engine": "native", "epochs": []}
+    for epoch in range(cfg.epochs):
+        tr._start_epoch(epoch)
+        steps = tr.steps_per_epoch()
+        if cfg.max_steps is not None:
+            steps = min(steps, cfg.max_steps)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        stamps = []
+        for i in range(steps):
+            tr.step()
+            if i <= 10:
+                torch.cuda.synchronize()
+                stamps.append(time.perf_counter())
+            if i % cfg.log_every == 0:
+                logger.loss_line(i, tr.last_loss())
+            if i == 10:
+                logger.average_time_line((stamps[10] - stamps[0]) / 9)
+                logger.print(f"(true mean over iters 1..10: {(stamps[10] - stamps[0]) / 10:.6f} s; "
+                             "the line above uses the reference /9 formula)")
+        torch.cuda.synchronize()
+        sec = time.perf_counter() - t0
+        ips = steps * tr.B * world / max(sec, 1e-9)
+        logger.metric(kind="train_epoch", epoch=epoch, sync=mode, world=world, images_per_s=ips, engine="native")
+        te = None
+        if cfg.eval:
+            te = tr.evaluate()
+            logger.test_line(te["avg_loss"], te["correct"], te["total"])
+        results["epochs"].append({"images_per_s": ips, "seconds": sec, "steps": steps, "test": te,
+                                  "last_loss": tr.last_loss()})
+    if cfg.checkpoint:
+        from ..utils.checkpoint import save_checkpoint
+        save_checkpoint(cfg.checkpoint, tr.state_dict(), tr.optimizer_state_dict(), cfg.epochs, 0, 0, world, rank)
+    results["final_state"] = tr.state_dict()
+    return results

@@ -1,4 +1,6 @@
-"""One tiny forward+backward of VGG-11 through the native HIP path (driver smoke test)."""
+"""One tiny training step of VGG-11 through the native engine (driver smoke test):
+on-device augmentation -> conv/BN/ReLU/pool forward -> fused linear+xent ->
+hand-scheduled backward -> fused SGD, every op a gfx950 kernel from ``_C.so``."""
 from __future__ import annotations
 
 import torch
@@ -6,29 +8,18 @@ import torch
 
 def run_smoke(device: torch.device, batch: int = 8) -> dict:
     from ..ops import native
-    from ..models import VGG11
-    from ..utils import data as dm
-    C = native.C()  # fails loudly if the extension is missing
-    torch.manual_seed(0)
-    ds = dm.SyntheticCIFAR10(train=True, size=64, seed=0)
-    data = ds.data.to(device)
-    idx = torch.arange(batch, device=device)
-    params = dm.augment_params(len(ds), 0, 0, True).to(device)
-    x = native.augment(data, idx, params, False, 3)
-    y = ds.targets[:batch].to(device)
-    model = VGG11().to(device)
-    try:
-        model.native = True
-        feat = model(x)
-    except NotImplementedError:
-        model.native = False
-        feat = model(x)
-    loss = torch.nn.functional.cross_entropy(feat, y)
-    loss.backward()
-    g = sum(float(p.grad.abs().sum()) for p in model.parameters())
+    from .engine import NativeTrainer
+    native.C()  # fails loudly if the extension is missing
+    torch.cuda.set_device(device)
+    tr = NativeTrainer(batch_size=batch, device=device, train_size=64, test_size=16, autotune=False, graph="none")
+    p0 = tr.params.clone()
+    tr.step()
     torch.cuda.synchronize()
-    out = {"loss": float(loss), "grad_l1": g, "native_module": bool(model.native)}
-    if not (out["loss"] == out["loss"] and g == g and g > 0):
+    loss = tr.last_loss()
+    g = float(tr.grads.abs().sum())
+    moved = float((tr.params - p0).abs().max())
+    out = {"loss": loss, "grad_l1": g, "max_param_update": moved, "engine": "native"}
+    if not (loss == loss and g == g and g > 0 and moved > 0):
         raise RuntimeError(f"smoke failed: {out}")
     print(f"[smoke] {out}")
     return out

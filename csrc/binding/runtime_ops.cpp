@@ -1,2 +1,155 @@
-#include <torch/extension.h>
-void register_runtime(pybind11::module& m) {}
+// pybind11 bindings of the native runtime: the RCCL communicator and the VGG engine.
+// Collectives take torch tensors and run stream-ordered w.r.t. torch's current stream.
+#include "binding/torch_util.h"
+#include "runtime/rccl_comm.h"
+#include "runtime/vgg_engine.h"
+
+namespace {
+
+using csb::cur_stream;
+
+ncclDataType_t nccl_dtype(const torch::Tensor& t) {
+  switch (t.scalar_type()) {
+    case at::kFloat: return ncclFloat32;
+    case at::kHalf: return ncclFloat16;
+    case at::kBFloat16: return ncclBfloat16;
+    case at::kDouble: return ncclFloat64;
+    case at::kLong: return ncclInt64;
+    case at::kInt: return ncclInt32;
+    case at::kByte: return ncclUint8;
+    case at::kChar: return ncclInt8;
+    default: TORCH_CHECK(false, "RcclComm: unsupported dtype ", t.scalar_type());
+  }
+  return ncclFloat32;
+}
+
+ncclRedOp_t nccl_op(const std::string& op) {
+  if (op == "sum") return ncclSum;
+  if (op == "avg") return ncclAvg;
+  if (op == "max") return ncclMax;
+  if (op == "min") return ncclMin;
+  if (op == "prod") return ncclProd;
+  TORCH_CHECK(false, "RcclComm: unknown reduce op ", op);
+  return ncclSum;
+}
+
+void check_gpu(const torch::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous(), name, " must be a contiguous GPU tensor");
+}
+
+}  // namespace
+
+void register_runtime(pybind11::module& m) {
+  namespace py = pybind11;
+  m.def("rccl_unique_id", []() { return py::bytes(cs::RcclComm::unique_id()); });
+  m.def("rccl_version", []() {
+    int v = 0;
+    ncclGetVersion(&v);
+    return v;
+  });
+  py::class_<cs::RcclComm>(m, "RcclComm")
+      .def(py::init([](py::bytes uid, int rank, int world, int device, bool high_priority) {
+             return new cs::RcclComm(std::string(uid), rank, world, device, high_priority);
+           }),
+           py::arg("uid"), py::arg("rank"), py::arg("world"), py::arg("device"), py::arg("high_priority") = true)
+      .def_property_readonly("rank", &cs::RcclComm::rank)
+      .def_property_readonly("world_size", &cs::RcclComm::world)
+      .def("stream_ptr", [](cs::RcclComm& c) { return reinterpret_cast<intptr_t>(c.stream()); })
+      .def("all_reduce",
+           [](cs::RcclComm& c, torch::Tensor t, const std::string& op) {
+             check_gpu(t, "tensor");
+             c.all_reduce(t.data_ptr(), t.numel(), nccl_dtype(t), nccl_op(op), cur_stream());
+           },
+           py::arg("tensor"), py::arg("op") = "sum")
+      .def("broadcast",
+           [](cs::RcclComm& c, torch::Tensor t, int root) {
+             check_gpu(t, "tensor");
+             c.broadcast(t.data_ptr(), t.numel(), nccl_dtype(t), root, cur_stream());
+           })
+      .def("all_gather",
+           [](cs::RcclComm& c, torch::Tensor in, torch::Tensor out) {
+             check_gpu(in, "in"); check_gpu(out, "out");
+             TORCH_CHECK(out.numel() == in.numel() * c.world() && out.scalar_type() == in.scalar_type(),
+                         "all_gather: out must hold world * in.numel() elements");
+             c.all_gather(in.data_ptr(), out.data_ptr(), in.numel(), nccl_dtype(in), cur_stream());
+           })
+      .def("reduce_scatter",
+           [](cs::RcclComm& c, torch::Tensor in, torch::Tensor out, const std::string& op) {
+             check_gpu(in, "in"); check_gpu(out, "out");
+             TORCH_CHECK(in.numel() == out.numel() * c.world() && out.scalar_type() == in.scalar_type(),
+                         "reduce_scatter: in must hold world * out.numel() elements");
+             c.reduce_scatter(in.data_ptr(), out.data_ptr(), out.numel(), nccl_dtype(in), nccl_op(op), cur_stream());
+           },
+           py::arg("input"), py::arg("output"), py::arg("op") = "sum")
+      .def("reduce",
+           [](cs::RcclComm& c, torch::Tensor t, int root, const std::string& op) {
+             check_gpu(t, "tensor");
+             c.reduce(t.data_ptr(), t.data_ptr(), t.numel(), nccl_dtype(t), nccl_op(op), root, cur_stream());
+           },
+           py::arg("tensor"), py::arg("root"), py::arg("op") = "sum")
+      .def("gather",
+           [](cs::RcclComm& c, torch::Tensor in, c10::optional<torch::Tensor> out, int root) {
+             check_gpu(in, "in");
+             void* o = nullptr;
+             if (c.rank() == root) {
+               TORCH_CHECK(out.has_value() && out->numel() == in.numel() * c.world(), "gather: root needs out");
+               check_gpu(*out, "out");
+               o = out->data_ptr();
+             }
+             c.gather(in.data_ptr(), o, in.numel(), nccl_dtype(in), root, cur_stream());
+           })
+      .def("scatter",
+           [](cs::RcclComm& c, c10::optional<torch::Tensor> in, torch::Tensor out, int root) {
+             check_gpu(out, "out");
+             const void* i = nullptr;
+             if (c.rank() == root) {
+               TORCH_CHECK(in.has_value() && in->numel() == out.numel() * c.world(), "scatter: root needs in");
+               check_gpu(*in, "in");
+               i = in->data_ptr();
+             }
+             c.scatter(i, out.data_ptr(), out.numel(), nccl_dtype(out), root, cur_stream());
+           })
+      .def("all_to_all",
+           [](cs::RcclComm& c, torch::Tensor in, torch::Tensor out) {
+             check_gpu(in, "in"); check_gpu(out, "out");
+             TORCH_CHECK(in.numel() == out.numel() && in.numel() % c.world() == 0, "all_to_all: sizes");
+             c.all_to_all(in.data_ptr(), out.data_ptr(), in.numel() / c.world(), nccl_dtype(in), cur_stream());
+           })
+      .def("send",
+           [](cs::RcclComm& c, torch::Tensor t, int peer) {
+             check_gpu(t, "tensor");
+             c.send(t.data_ptr(), t.numel(), nccl_dtype(t), peer, cur_stream());
+           })
+      .def("recv",
+           [](cs::RcclComm& c, torch::Tensor t, int peer) {
+             check_gpu(t, "tensor");
+             c.recv(t.data_ptr(), t.numel(), nccl_dtype(t), peer, cur_stream());
+           })
+      .def("group_start", [](cs::RcclComm& c) { c.group_start(cur_stream()); })
+      .def("group_end", &cs::RcclComm::group_end)
+      .def("join", [](cs::RcclComm& c) { c.join(cur_stream()); })
+      .def("async_error", &cs::RcclComm::async_error)
+      .def("abort", &cs::RcclComm::abort);
+
+  py::class_<cs::VggEngine>(m, "VggEngine")
+      .def(py::init<int64_t, std::vector<int64_t>, std::vector<int64_t>, std::vector<int64_t>, int64_t, int64_t,
+                    torch::Tensor, torch::Tensor, torch::Tensor, torch::Tensor, torch::Tensor>())
+      .def("set_data", &cs::VggEngine::set_data)
+      .def("idx", &cs::VggEngine::idx)
+      .def("loss", &cs::VggEngine::loss)
+      .def("correct", &cs::VggEngine::correct)
+      .def("logits", &cs::VggEngine::logits)
+      .def("num_blocks", &cs::VggEngine::num_blocks)
+      .def("tensor", &cs::VggEngine::tensor)
+      .def("forward_train", &cs::VggEngine::forward_train)
+      .def("backward", &cs::VggEngine::backward)
+      .def("sgd", &cs::VggEngine::sgd)
+      .def("forward_eval", &cs::VggEngine::forward_eval)
+      .def("step", &cs::VggEngine::step, py::arg("B"), py::arg("comm").none(true), py::arg("bucket_blocks"),
+           py::arg("bucket_ranges"), py::arg("broadcast_buffers"), py::arg("lr"), py::arg("momentum"),
+           py::arg("wd"), py::arg("dampening"))
+      .def("set_tile", &cs::VggEngine::set_tile)
+      .def("get_tile", &cs::VggEngine::get_tile)
+      .def("autotune", &cs::VggEngine::autotune)
+      .def("run_conv", &cs::VggEngine::run_conv);
+}

@@ -65,3 +65,17 @@ hipError_t cs_augment(const uint8_t* data, const int64_t* idx, const int32_t* pa
                      cstride, nm);
   return hipGetLastError();
 }
+
+namespace {
+__global__ void gather_labels_kernel(const int64_t* __restrict__ labels, const int64_t* __restrict__ idx,
+                                     int64_t* __restrict__ out, int B) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < B) out[b] = labels[idx[b]];
+}
+}  // namespace
+
+hipError_t cs_gather_labels(const int64_t* labels, const int64_t* idx, int64_t* out, int B, hipStream_t stream) {
+  if (B <= 0) return hipSuccess;
+  hipLaunchKernelGGL(gather_labels_kernel, dim3((B + 255) / 256), dim3(256), 0, stream, labels, idx, out, B);
+  return hipGetLastError();
+}

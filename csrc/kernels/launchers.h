@@ -14,6 +14,7 @@ struct CsTensorEntry {
 // data pipeline
 hipError_t cs_augment(const uint8_t* data, const int64_t* idx, const int32_t* params, float* out, int B, int nhwc,
                       int cstride, const float* mean, const float* std_, hipStream_t stream);
+hipError_t cs_gather_labels(const int64_t* labels, const int64_t* idx, int64_t* out, int B, hipStream_t stream);
 
 // optimizer
 hipError_t cs_sgd_flat(float* p, const float* g, float* m, int64_t n, float lr, float mom, float wd, float damp,

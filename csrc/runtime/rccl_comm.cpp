@@ -1,0 +1,141 @@
+#include "runtime/rccl_comm.h"
+
+#include <cstring>
+#include <stdexcept>
+
+namespace cs {
+
+namespace {
+void hip_ok(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string("HIP error in ") + what + ": " + hipGetErrorString(e));
+}
+void nccl_ok(ncclResult_t r, const char* what) {
+  if (r != ncclSuccess) throw std::runtime_error(std::string("RCCL error in ") + what + ": " + ncclGetErrorString(r));
+}
+constexpr size_t kForkEvents = 64;
+}  // namespace
+
+std::string RcclComm::unique_id() {
+  ncclUniqueId id;
+  nccl_ok(ncclGetUniqueId(&id), "ncclGetUniqueId");
+  return std::string(reinterpret_cast<const char*>(&id), sizeof(id));
+}
+
+RcclComm::RcclComm(const std::string& uid, int rank, int world, int device, bool high_priority)
+    : rank_(rank), world_(world), device_(device) {
+  if (uid.size() != sizeof(ncclUniqueId)) throw std::runtime_error("RcclComm: unique id must be 128 bytes");
+  if (rank < 0 || rank >= world) throw std::runtime_error("RcclComm: bad rank");
+  hip_ok(hipSetDevice(device), "hipSetDevice");
+  int lo = 0, hi = 0;
+  hip_ok(hipDeviceGetStreamPriorityRange(&lo, &hi), "hipDeviceGetStreamPriorityRange");
+  hip_ok(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, high_priority ? hi : lo), "stream");
+  fork_events_.resize(kForkEvents);
+  for (auto& e : fork_events_) hip_ok(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event");
+  hip_ok(hipEventCreateWithFlags(&join_event_, hipEventDisableTiming), "event");
+  ncclUniqueId id;
+  std::memcpy(&id, uid.data(), sizeof(id));
+  nccl_ok(ncclCommInitRank(&comm_, world, id, rank), "ncclCommInitRank");
+}
+
+RcclComm::~RcclComm() {
+  if (comm_ != nullptr) {
+    if (!aborted_) {
+      hipStreamSynchronize(stream_);
+      ncclCommDestroy(comm_);
+    }
+  }
+  for (auto& e : fork_events_) hipEventDestroy(e);
+  if (join_event_) hipEventDestroy(join_event_);
+  if (stream_) hipStreamDestroy(stream_);
+}
+
+void RcclComm::fork(hipStream_t compute) {
+  // inside ncclGroupStart/End the first op's fork covers the whole group
+  hipEvent_t e = fork_events_[next_fork_++ % kForkEvents];
+  hip_ok(hipEventRecord(e, compute), "hipEventRecord(fork)");
+  hip_ok(hipStreamWaitEvent(stream_, e, 0), "hipStreamWaitEvent(fork)");
+}
+
+void RcclComm::join(hipStream_t compute) {
+  hip_ok(hipEventRecord(join_event_, stream_), "hipEventRecord(join)");
+  hip_ok(hipStreamWaitEvent(compute, join_event_, 0), "hipStreamWaitEvent(join)");
+}
+
+void RcclComm::all_reduce(void* buf, size_t count, ncclDataType_t dt, ncclRedOp_t op, hipStream_t compute) {
+  fork(compute);
+  nccl_ok(ncclAllReduce(buf, buf, count, dt, op, comm_, stream_), "ncclAllReduce");
+}
+
+void RcclComm::broadcast(void* buf, size_t count, ncclDataType_t dt, int root, hipStream_t compute) {
+  fork(compute);
+  nccl_ok(ncclBroadcast(buf, buf, count, dt, root, comm_, stream_), "ncclBroadcast");
+}
+
+void RcclComm::all_gather(const void* send, void* recv, size_t count, ncclDataType_t dt, hipStream_t compute) {
+  fork(compute);
+  nccl_ok(ncclAllGather(send, recv, count, dt, comm_, stream_), "ncclAllGather");
+}
+
+void RcclComm::reduce_scatter(const void* send, void* recv, size_t count, ncclDataType_t dt, ncclRedOp_t op,
+                              hipStream_t compute) {
+  fork(compute);
+  nccl_ok(ncclReduceScatter(send, recv, count, dt, op, comm_, stream_), "ncclReduceScatter");
+}
+
+void RcclComm::reduce(const void* send, void* recv, size_t count, ncclDataType_t dt, ncclRedOp_t op, int root,
+                      hipStream_t compute) {
+  fork(compute);
+  nccl_ok(ncclReduce(send, recv, count, dt, op, root, comm_, stream_), "ncclReduce");
+}
+
+void RcclComm::gather(const void* send, void* recv, size_t count, ncclDataType_t dt, int root, hipStream_t compute) {
+  fork(compute);
+  nccl_ok(ncclGather(send, recv, count, dt, root, comm_, stream_), "ncclGather");
+}
+
+void RcclComm::scatter(const void* send, void* recv, size_t count, ncclDataType_t dt, int root,
+                       hipStream_t compute) {
+  fork(compute);
+  nccl_ok(ncclScatter(send, recv, count, dt, root, comm_, stream_), "ncclScatter");
+}
+
+void RcclComm::all_to_all(const void* send, void* recv, size_t count, ncclDataType_t dt, hipStream_t compute) {
+  fork(compute);
+  nccl_ok(ncclAllToAll(send, recv, count, dt, comm_, stream_), "ncclAllToAll");
+}
+
+void RcclComm::send(const void* buf, size_t count, ncclDataType_t dt, int peer, hipStream_t compute) {
+  if (group_depth_ == 0) fork(compute);
+  nccl_ok(ncclSend(buf, count, dt, peer, comm_, stream_), "ncclSend");
+}
+
+void RcclComm::recv(void* buf, size_t count, ncclDataType_t dt, int peer, hipStream_t compute) {
+  if (group_depth_ == 0) fork(compute);
+  nccl_ok(ncclRecv(buf, count, dt, peer, comm_, stream_), "ncclRecv");
+}
+
+void RcclComm::group_start(hipStream_t compute) {
+  if (group_depth_ == 0) fork(compute);
+  ++group_depth_;
+  nccl_ok(ncclGroupStart(), "ncclGroupStart");
+}
+
+void RcclComm::group_end() {
+  --group_depth_;
+  nccl_ok(ncclGroupEnd(), "ncclGroupEnd");
+}
+
+std::string RcclComm::async_error() {
+  ncclResult_t r = ncclSuccess;
+  if (ncclCommGetAsyncError(comm_, &r) != ncclSuccess) return "ncclCommGetAsyncError failed";
+  return r == ncclSuccess ? std::string() : std::string(ncclGetErrorString(r));
+}
+
+void RcclComm::abort() {
+  if (comm_ != nullptr && !aborted_) {
+    ncclCommAbort(comm_);
+    aborted_ = true;
+  }
+}
+
+}  // namespace cs

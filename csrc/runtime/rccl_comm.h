@@ -1,0 +1,67 @@
+// Native RCCL communicator (one process per MI355X, collectives over xGMI).
+//
+// Replaces the reference's gloo/TCP process group as the gradient data plane
+// (SURVEY.md §2.2 N17-N21, §5.8): one ncclComm_t built from a unique id that the
+// Python side shares through the c10d TCPStore, a dedicated high-priority comm
+// stream, and HIP-event fork/join between the caller's compute stream and the
+// comm stream — so every collective is stream-ordered, never blocks the host,
+// overlaps with whatever the compute stream does next, and can be captured into
+// a hipGraph. Averaging uses ncclAvg (the reference divides by 4 in a separate
+// pass, master/part2b/part2b.py:44).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <string>
+#include <vector>
+
+namespace cs {
+
+class RcclComm {
+ public:
+  static std::string unique_id();  // 128 raw bytes (NCCL_UNIQUE_ID_BYTES)
+
+  RcclComm(const std::string& uid, int rank, int world, int device, bool high_priority = true);
+  ~RcclComm();
+  RcclComm(const RcclComm&) = delete;
+  RcclComm& operator=(const RcclComm&) = delete;
+
+  int rank() const { return rank_; }
+  int world() const { return world_; }
+  hipStream_t stream() const { return stream_; }
+
+  // All calls: the comm stream first waits for everything already enqueued on
+  // `compute`; the collective then runs on the comm stream. join() makes `compute`
+  // wait for everything enqueued on the comm stream so far.
+  void all_reduce(void* buf, size_t count, ncclDataType_t dt, ncclRedOp_t op, hipStream_t compute);
+  void broadcast(void* buf, size_t count, ncclDataType_t dt, int root, hipStream_t compute);
+  void all_gather(const void* send, void* recv, size_t count, ncclDataType_t dt, hipStream_t compute);
+  void reduce_scatter(const void* send, void* recv, size_t count, ncclDataType_t dt, ncclRedOp_t op,
+                      hipStream_t compute);
+  void reduce(const void* send, void* recv, size_t count, ncclDataType_t dt, ncclRedOp_t op, int root,
+              hipStream_t compute);
+  void gather(const void* send, void* recv, size_t count, ncclDataType_t dt, int root, hipStream_t compute);
+  void scatter(const void* send, void* recv, size_t count, ncclDataType_t dt, int root, hipStream_t compute);
+  void all_to_all(const void* send, void* recv, size_t count, ncclDataType_t dt, hipStream_t compute);
+  void send(const void* buf, size_t count, ncclDataType_t dt, int peer, hipStream_t compute);
+  void recv(void* buf, size_t count, ncclDataType_t dt, int peer, hipStream_t compute);
+  void group_start(hipStream_t compute);  // forks once for the whole group
+  void group_end();
+  void join(hipStream_t compute);
+  // async error polling: returns "" when healthy
+  std::string async_error();
+  void abort();
+
+ private:
+  void fork(hipStream_t compute);
+  ncclComm_t comm_ = nullptr;
+  hipStream_t stream_ = nullptr;
+  std::vector<hipEvent_t> fork_events_;
+  hipEvent_t join_event_ = nullptr;
+  size_t next_fork_ = 0;
+  int rank_ = 0, world_ = 1, device_ = 0;
+  int group_depth_ = 0;
+  bool aborted_ = false;
+};
+
+}  // namespace cs

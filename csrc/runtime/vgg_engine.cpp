@@ -1,0 +1,399 @@
+#include "runtime/vgg_engine.h"
+
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+
+#include <algorithm>
+#include <stdexcept>
+#include <string>
+
+namespace cs {
+
+namespace {
+
+const float kMean[3] = {125.3f / 255.f, 123.0f / 255.f, 113.9f / 255.f};  // master/part1/part1.py:66-67
+const float kStd[3] = {63.0f / 255.f, 62.1f / 255.f, 66.7f / 255.f};
+constexpr float kBnMomentum = 0.1f, kBnEps = 1e-5f;
+constexpr int64_t kWsElems = 16ll << 20;  // 64 MiB split-K workspace
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
+
+void ok(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string("VggEngine: ") + what + ": " + hipGetErrorString(e));
+}
+
+int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+struct Dims {
+  int64_t M, N, K;
+};
+
+Dims dims(const VggBlock& b, int mode, int64_t B) {
+  const int64_t pix = B * b.H * b.H;
+  if (mode == CS_CONV_FWD) return {pix, b.cout, 9ll * b.cin};
+  if (mode == CS_CONV_DGRAD) return {pix, b.cin, 9ll * b.cout};
+  return {b.cout, 9ll * b.cin, pix};
+}
+
+// the split count cs_conv_gemm will actually use (it re-balances K-steps per split)
+int eff_splits(int64_t K, int splits) {
+  const int64_t ks = cdiv(K, 16);
+  int64_t s = std::max<int64_t>(1, std::min<int64_t>(splits, ks));
+  const int64_t per = cdiv(ks, s);
+  return (int)cdiv(ks, per);
+}
+
+// default tile before autotune: ~2 waves of 256 CUs, >= 8 K-steps per split
+ConvTile default_tile(const VggBlock& b, int mode, int64_t B) {
+  const Dims d = dims(b, mode, B);
+  ConvTile t;
+  t.bm = 64;
+  t.bn = 64;
+  const int64_t tiles = cdiv(d.M, 64) * cdiv(d.N, 64);
+  const int64_t ks = cdiv(d.K, 16);
+  int s = 1;
+  while (tiles * s < 512 && ks / (2 * s) >= 8 && (2 * s) * d.M * d.N <= kWsElems) s *= 2;
+  t.splits = s;
+  return t;
+}
+
+}  // namespace
+
+VggEngine::VggEngine(int64_t Bmax, std::vector<int64_t> desc, std::vector<int64_t> offs,
+                     std::vector<int64_t> buf_offs, int64_t feat, int64_t ncls, torch::Tensor params,
+                     torch::Tensor grads, torch::Tensor mom, torch::Tensor bufs, torch::Tensor nbt)
+    : Bmax_(Bmax), feat_(feat), ncls_(ncls), params_(params), grads_(grads), mom_(mom), bufs_(bufs), nbt_(nbt) {
+  TORCH_CHECK(desc.size() % 4 == 0 && !desc.empty(), "VggEngine: desc must be 4 ints per block");
+  const int64_t L = desc.size() / 4;
+  TORCH_CHECK((int64_t)offs.size() == 4 * L + 2 && (int64_t)buf_offs.size() == 2 * L, "VggEngine: offsets");
+  TORCH_CHECK(Bmax > 0 && Bmax <= 2048, "VggEngine: 0 < Bmax <= 2048");
+  TORCH_CHECK(ncls > 0 && ncls <= 16, "VggEngine: <= 16 classes (fused head)");
+  for (auto* t : {&params_, &grads_, &mom_, &bufs_}) {
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->is_contiguous() && t->dim() == 1,
+                "VggEngine: flat buffers must be contiguous 1-D float32 GPU tensors");
+  }
+  TORCH_CHECK(params_.numel() == grads_.numel() && params_.numel() == mom_.numel(), "VggEngine: flat sizes");
+  TORCH_CHECK(nbt_.is_cuda() && nbt_.scalar_type() == at::kLong && nbt_.numel() == L, "VggEngine: nbt int64 [L]");
+  const auto fo = params_.options();
+  const int64_t P = params_.numel();
+  int64_t gmax = 0, dzmax = 0, partmax = 0, cmax = 0;
+  blocks_.resize(L);
+  for (int64_t l = 0; l < L; ++l) {
+    VggBlock& b = blocks_[l];
+    b.cin = desc[4 * l];
+    b.cout = desc[4 * l + 1];
+    b.H = desc[4 * l + 2];
+    b.pool = desc[4 * l + 3] ? 1 : 0;
+    TORCH_CHECK(b.H >= 1 && (b.H & (b.H - 1)) == 0 && (b.cin & (b.cin - 1)) == 0 && (b.cout & (b.cout - 1)) == 0 &&
+                    b.cout >= 64 && b.cout <= 1024 && b.cin >= 4,
+                "VggEngine: block ", l, " needs power-of-two H/cin/cout, cin>=4, 64<=cout<=1024");
+    TORCH_CHECK(l == 0 || b.cin >= 64, "VggEngine: only block 0 may have a padded (4-channel) input");
+    if (l > 0) {
+      const VggBlock& p = blocks_[l - 1];
+      TORCH_CHECK(p.cout == b.cin && (p.pool ? p.H / 2 : p.H) == b.H, "VggEngine: blocks ", l - 1, "->", l,
+                  " do not chain");
+    }
+    b.w_off = offs[4 * l];
+    b.b_off = offs[4 * l + 1];
+    b.g_off = offs[4 * l + 2];
+    b.be_off = offs[4 * l + 3];
+    b.rm_off = buf_offs[2 * l];
+    b.rv_off = buf_offs[2 * l + 1];
+    const int64_t wn = (l == 0 && b.cin == 4) ? b.cout * 27 : b.cout * 9 * b.cin;
+    for (int64_t o : {b.w_off, b.b_off, b.g_off, b.be_off})
+      TORCH_CHECK(o % 4 == 0 && o >= 0, "VggEngine: tensor offsets must be 16-B aligned");
+    TORCH_CHECK(b.w_off + wn <= P && b.b_off + b.cout <= P && b.g_off + b.cout <= P && b.be_off + b.cout <= P,
+                "VggEngine: block ", l, " exceeds the flat buffer");
+    TORCH_CHECK(b.rm_off + b.cout <= bufs_.numel() && b.rv_off + b.cout <= bufs_.numel(), "VggEngine: bufs");
+    const int64_t pix = Bmax * b.H * b.H;
+    b.x = torch::zeros({Bmax, b.H, b.H, b.cin}, fo);
+    b.y = torch::zeros({pix, b.cout}, fo);
+    b.stats = torch::zeros({cdiv(pix, 64), b.cout, 2}, fo);
+    b.bn = torch::zeros({4, b.cout}, fo);
+    const int64_t ho = b.pool ? b.H / 2 : b.H;
+    gmax = std::max(gmax, Bmax * ho * ho * b.cout);
+    dzmax = std::max(dzmax, pix * b.cout);
+    partmax = std::max<int64_t>(partmax, (int64_t)cs_bn_bwd_blocks(Bmax, b.H, b.H, b.cout, b.pool) * b.cout * 3);
+    cmax = std::max<int64_t>(cmax, b.cout);
+    for (int m = 0; m < 3; ++m) b.tile[m] = default_tile(b, m, Bmax);
+  }
+  const VggBlock& last = blocks_.back();
+  TORCH_CHECK((last.pool ? last.H / 2 : last.H) == 1 && last.cout == feat, "VggEngine: last block must end at 1x1x",
+              feat);
+  fc_w_ = offs[4 * L];
+  fc_b_ = offs[4 * L + 1];
+  TORCH_CHECK(fc_w_ % 4 == 0 && fc_w_ + ncls * feat <= P && fc_b_ + ncls <= P, "VggEngine: fc offsets");
+  const auto lo = torch::TensorOptions().dtype(at::kLong).device(params_.device());
+  idx_ = torch::zeros({Bmax}, lo);
+  ylab_ = torch::zeros({Bmax}, lo);
+  pred_ = torch::zeros({Bmax}, lo);
+  loss_ = torch::zeros({}, fo);
+  correct_ = torch::zeros({}, fo.dtype(at::kInt));
+  logits_ = torch::zeros({Bmax, ncls}, fo);
+  gbuf_[0] = torch::zeros({gmax}, fo);
+  gbuf_[1] = torch::zeros({gmax}, fo);
+  dz_ = torch::zeros({dzmax}, fo);
+  ws_elems_ = kWsElems;
+  ws_ = torch::zeros({ws_elems_}, fo);
+  bn_part_ = torch::zeros({partmax}, fo);
+  bn_coef_ = torch::zeros({cmax * 3}, fo);
+  bn_eval_ = torch::zeros({2, cmax}, fo);
+}
+
+torch::Tensor VggEngine::tensor(int64_t block, const std::string& name) const {
+  if (name == "g0") return gbuf_[0];
+  if (name == "g1") return gbuf_[1];
+  if (name == "dz") return dz_;
+  TORCH_CHECK(block >= 0 && block < (int64_t)blocks_.size(), "tensor: block index");
+  const VggBlock& b = blocks_[block];
+  if (name == "x") return b.x;
+  if (name == "y") return b.y;
+  if (name == "bn") return b.bn;
+  if (name == "stats") return b.stats;
+  TORCH_CHECK(false, "tensor: unknown name ", name);
+  return b.x;
+}
+
+void VggEngine::set_data(int64_t slot, torch::Tensor data, torch::Tensor labels, torch::Tensor aug) {
+  TORCH_CHECK(slot == 0 || slot == 1, "set_data: slot 0 (train) or 1 (eval)");
+  TORCH_CHECK(data.is_cuda() && data.scalar_type() == at::kByte && data.dim() == 4 && data.size(1) == 32 &&
+                  data.size(2) == 32 && data.size(3) == 3 && data.is_contiguous(),
+              "set_data: data must be contiguous uint8 [N,32,32,3] on the GPU");
+  TORCH_CHECK(labels.is_cuda() && labels.scalar_type() == at::kLong && labels.numel() == data.size(0),
+              "set_data: labels int64 [N]");
+  TORCH_CHECK(aug.is_cuda() && aug.scalar_type() == at::kInt && aug.dim() == 2 && aug.size(0) == data.size(0) &&
+                  aug.size(1) == 3 && aug.is_contiguous(),
+              "set_data: aug int32 [N,3]");
+  data_[slot] = data;
+  labels_[slot] = labels.contiguous();
+  aug_[slot] = aug;
+}
+
+void VggEngine::conv(int l, int mode, int B, const ConvTile& t, hipStream_t s, bool with_stats) {
+  VggBlock& b = blocks_[l];
+  const int L = (int)blocks_.size();
+  CsConvArgs a{};
+  a.B = B;
+  a.H = b.H;
+  a.W = b.H;
+  a.Cin = b.cin;
+  a.Cout = b.cout;
+  a.w_oihw = (l == 0 && b.cin == 4) ? 1 : 0;
+  a.ws = ws_.data_ptr<float>();
+  const Dims d = dims(b, mode, B);
+  const int sp = eff_splits(d.K, t.splits);
+  TORCH_CHECK(sp == 1 || (int64_t)sp * d.M * d.N <= ws_elems_, "VggEngine: split-K workspace too small");
+  if (mode == CS_CONV_FWD) {
+    a.x = b.x.data_ptr<float>();
+    a.w = P(b.w_off);
+    a.bias = P(b.b_off);
+    a.out = b.y.data_ptr<float>();
+    a.stats = with_stats ? b.stats.data_ptr<float>() : nullptr;
+  } else if (mode == CS_CONV_DGRAD) {
+    TORCH_CHECK(l > 0, "VggEngine: no dgrad for block 0");
+    a.dz = dz_.data_ptr<float>();
+    a.w = P(b.w_off);
+    a.out = gbuf_[(L - l) % 2].data_ptr<float>();
+  } else {
+    a.x = b.x.data_ptr<float>();
+    a.dz = dz_.data_ptr<float>();
+    a.out = G(b.w_off);
+  }
+  ok(cs_conv_gemm(a, mode, t.bm, t.bn, t.splits, s), "conv_gemm");
+}
+
+void VggEngine::forward_train(int64_t B) {
+  TORCH_CHECK(B > 0 && B <= Bmax_, "forward_train: 0 < B <= Bmax");
+  TORCH_CHECK(data_[0].defined(), "forward_train: set_data(0, ...) first");
+  hipStream_t s = cur_stream();
+  const int L = (int)blocks_.size();
+  ok(cs_gather_labels(labels_[0].data_ptr<int64_t>(), idx_.data_ptr<int64_t>(), ylab_.data_ptr<int64_t>(), (int)B, s),
+     "gather_labels");
+  ok(cs_augment(data_[0].data_ptr<uint8_t>(), idx_.data_ptr<int64_t>(), aug_[0].data_ptr<int32_t>(),
+                blocks_[0].x.data_ptr<float>(), (int)B, 1, blocks_[0].cin, kMean, kStd, s),
+     "augment");
+  for (int l = 0; l < L; ++l) {
+    VggBlock& b = blocks_[l];
+    const ConvTile& t = b.tile[CS_CONV_FWD];
+    conv(l, CS_CONV_FWD, (int)B, t, s, true);
+    const int64_t M = B * b.H * b.H;
+    const int rows = eff_splits(9ll * b.cin, t.splits) > 1 ? 64 : t.bm;
+    float* bn = b.bn.data_ptr<float>();
+    float* bufs = bufs_.data_ptr<float>();
+    ok(cs_bn_finalize(b.stats.data_ptr<float>(), (int)cdiv(M, rows), rows, (int)M, b.cout, P(b.g_off), P(b.be_off),
+                      bufs + b.rm_off, bufs + b.rv_off, nbt_.data_ptr<int64_t>() + l, kBnMomentum, kBnEps, bn,
+                      bn + b.cout, bn + 2 * b.cout, bn + 3 * b.cout, s),
+       "bn_finalize");
+    float* out = (l + 1 < L) ? blocks_[l + 1].x.data_ptr<float>() : gbuf_[1].data_ptr<float>();
+    ok(cs_bn_apply(b.y.data_ptr<float>(), bn, bn + b.cout, out, (int)B, b.H, b.H, b.cout, b.pool, s), "bn_apply");
+  }
+  // features of the last block were staged in gbuf_[1] (free until the first dgrad); dfeat -> gbuf_[0]
+  ok(cs_linear_xent(gbuf_[1].data_ptr<float>(), P(fc_w_), P(fc_b_), ylab_.data_ptr<int64_t>(), (int)B, (int)feat_,
+                    (int)ncls_, 1.0f, loss_.data_ptr<float>(), correct_.data_ptr<int>(), logits_.data_ptr<float>(),
+                    G(fc_w_), G(fc_b_), gbuf_[0].data_ptr<float>(), pred_.data_ptr<int64_t>(), s),
+     "linear_xent");
+}
+
+void VggEngine::backward(int64_t hi, int64_t lo, int64_t B) {
+  const int L = (int)blocks_.size();
+  TORCH_CHECK(0 <= lo && lo <= hi && hi < L, "backward: need 0 <= lo <= hi < num_blocks");
+  TORCH_CHECK(B > 0 && B <= Bmax_, "backward: 0 < B <= Bmax");
+  hipStream_t s = cur_stream();
+  for (int l = (int)hi; l >= (int)lo; --l) {
+    VggBlock& b = blocks_[l];
+    float* bn = b.bn.data_ptr<float>();
+    ok(cs_bn_bwd(b.y.data_ptr<float>(), gbuf_[(L - 1 - l) % 2].data_ptr<float>(), (int)B, b.H, b.H, b.cout, b.pool,
+                 bn, bn + b.cout, bn + 2 * b.cout, bn + 3 * b.cout, P(b.g_off), bn_part_.data_ptr<float>(),
+                 bn_coef_.data_ptr<float>(), G(b.g_off), G(b.be_off), G(b.b_off), dz_.data_ptr<float>(), s),
+       "bn_bwd");
+    conv(l, CS_CONV_WGRAD, (int)B, b.tile[CS_CONV_WGRAD], s, false);
+    if (l > 0) conv(l, CS_CONV_DGRAD, (int)B, b.tile[CS_CONV_DGRAD], s, false);
+  }
+}
+
+void VggEngine::sgd(double lr, double momentum, double wd, double dampening, int64_t off, int64_t n) {
+  TORCH_CHECK(off >= 0 && n >= 0 && off + n <= params_.numel(), "sgd: range");
+  if (n == 0) return;
+  // momentum buffers start at zero, so buf = 0*mom + (1-damp)*d == torch's first-step clone for damp = 0
+  ok(cs_sgd_flat(P(off), G(off), mom_.data_ptr<float>() + off, n, (float)lr, (float)momentum, (float)wd,
+                 (float)dampening, 1.0f, 0, cur_stream()),
+     "sgd_flat");
+}
+
+void VggEngine::forward_eval(int64_t B) {
+  TORCH_CHECK(B > 0 && B <= Bmax_, "forward_eval: 0 < B <= Bmax");
+  TORCH_CHECK(data_[1].defined(), "forward_eval: set_data(1, ...) first");
+  hipStream_t s = cur_stream();
+  const int L = (int)blocks_.size();
+  ok(cs_gather_labels(labels_[1].data_ptr<int64_t>(), idx_.data_ptr<int64_t>(), ylab_.data_ptr<int64_t>(), (int)B, s),
+     "gather_labels");
+  ok(cs_augment(data_[1].data_ptr<uint8_t>(), idx_.data_ptr<int64_t>(), aug_[1].data_ptr<int32_t>(),
+                blocks_[0].x.data_ptr<float>(), (int)B, 1, blocks_[0].cin, kMean, kStd, s),
+     "augment");
+  float* sc = bn_eval_.data_ptr<float>();
+  float* sh = sc + bn_eval_.size(1);
+  float* bufs = bufs_.data_ptr<float>();
+  for (int l = 0; l < L; ++l) {
+    VggBlock& b = blocks_[l];
+    conv(l, CS_CONV_FWD, (int)B, b.tile[CS_CONV_FWD], s, false);
+    ok(cs_bn_eval_coeffs(P(b.g_off), P(b.be_off), bufs + b.rm_off, bufs + b.rv_off, b.cout, kBnEps, sc, sh, s),
+       "bn_eval_coeffs");
+    float* out = (l + 1 < L) ? blocks_[l + 1].x.data_ptr<float>() : gbuf_[1].data_ptr<float>();
+    ok(cs_bn_apply(b.y.data_ptr<float>(), sc, sh, out, (int)B, b.H, b.H, b.cout, b.pool, s), "bn_apply");
+  }
+  ok(cs_linear_xent(gbuf_[1].data_ptr<float>(), P(fc_w_), P(fc_b_), ylab_.data_ptr<int64_t>(), (int)B, (int)feat_,
+                    (int)ncls_, 1.0f, loss_.data_ptr<float>(), correct_.data_ptr<int>(), logits_.data_ptr<float>(),
+                    nullptr, nullptr, nullptr, pred_.data_ptr<int64_t>(), s),
+     "linear_xent");
+}
+
+void VggEngine::step(int64_t B, RcclComm* comm, const std::vector<int64_t>& bucket_blocks,
+                     const std::vector<int64_t>& bucket_ranges, bool broadcast_buffers, double lr, double momentum,
+                     double wd, double dampening) {
+  const int64_t L = (int64_t)blocks_.size();
+  const size_t nb = bucket_blocks.size();
+  TORCH_CHECK(nb >= 1 && bucket_ranges.size() == 2 * nb && bucket_blocks.back() == 0, "step: bucket plan");
+  hipStream_t s = cur_stream();
+  if (comm != nullptr && broadcast_buffers && comm->world() > 1) {
+    // DDP broadcast_buffers: rank 0's BN running stats before every training forward
+    comm->broadcast(bufs_.data_ptr<float>(), bufs_.numel(), ncclFloat32, 0, s);
+    comm->broadcast(nbt_.data_ptr<int64_t>(), nbt_.numel(), ncclInt64, 0, s);
+    comm->join(s);
+  }
+  forward_train(B);
+  int64_t hi = L - 1;
+  for (size_t k = 0; k < nb; ++k) {
+    const int64_t lo = bucket_blocks[k];
+    TORCH_CHECK(lo <= hi, "step: bucket blocks must decrease");
+    backward(hi, lo, B);
+    hi = lo - 1;
+    if (comm != nullptr && comm->world() > 1)
+      comm->all_reduce(G(bucket_ranges[2 * k]), bucket_ranges[2 * k + 1], ncclFloat32, ncclAvg, s);
+  }
+  if (comm != nullptr && comm->world() > 1) comm->join(s);
+  sgd(lr, momentum, wd, dampening, 0, params_.numel());
+}
+
+void VggEngine::set_tile(int64_t block, int64_t mode, int64_t bm, int64_t bn, int64_t splits) {
+  TORCH_CHECK(block >= 0 && block < (int64_t)blocks_.size() && mode >= 0 && mode <= 2, "set_tile: index");
+  TORCH_CHECK((bm == 64 || bm == 128) && (bn == 64 || bn == 128) && splits >= 1 && splits <= 64, "set_tile: tile");
+  const Dims d = dims(blocks_[block], (int)mode, Bmax_);
+  const int sp = eff_splits(d.K, (int)splits);
+  TORCH_CHECK(sp == 1 || (int64_t)sp * d.M * d.N <= ws_elems_, "set_tile: split-K workspace too small");
+  ConvTile& t = blocks_[block].tile[mode];
+  t.bm = (int)bm;
+  t.bn = (int)bn;
+  t.splits = (int)splits;
+  t.us = -1.f;
+}
+
+std::vector<int64_t> VggEngine::get_tile(int64_t block, int64_t mode) const {
+  TORCH_CHECK(block >= 0 && block < (int64_t)blocks_.size() && mode >= 0 && mode <= 2, "get_tile: index");
+  const ConvTile& t = blocks_[block].tile[mode];
+  return {t.bm, t.bn, t.splits};
+}
+
+void VggEngine::run_conv(int64_t block, int64_t mode, int64_t B) {
+  TORCH_CHECK(block >= 0 && block < (int64_t)blocks_.size() && mode >= 0 && mode <= 2, "run_conv: index");
+  TORCH_CHECK(!(block == 0 && mode == CS_CONV_DGRAD), "run_conv: no dgrad for block 0");
+  TORCH_CHECK(B > 0 && B <= Bmax_, "run_conv: B");
+  conv((int)block, (int)mode, (int)B, blocks_[block].tile[mode], cur_stream(), mode == CS_CONV_FWD);
+}
+
+std::vector<double> VggEngine::autotune(int64_t B, int64_t iters) {
+  TORCH_CHECK(B > 0 && B <= Bmax_ && iters >= 1, "autotune: args");
+  hipStream_t s = cur_stream();
+  hipEvent_t e0, e1;
+  ok(hipEventCreate(&e0), "event");
+  ok(hipEventCreate(&e1), "event");
+  std::vector<double> best_us;
+  const int split_opts[] = {1, 2, 3, 4, 6, 8, 12, 16, 24, 32};
+  for (int l = 0; l < (int)blocks_.size(); ++l) {
+    for (int mode = 0; mode < 3; ++mode) {
+      if (l == 0 && mode == CS_CONV_DGRAD) {
+        best_us.push_back(0.0);
+        continue;
+      }
+      const Dims d = dims(blocks_[l], mode, B);
+      const int64_t ks = cdiv(d.K, 16);
+      ConvTile best = blocks_[l].tile[mode];
+      float best_t = 1e30f;
+      std::vector<std::vector<int>> seen;
+      for (int bm : {64, 128}) {
+        for (int bn : {64, 128}) {
+          for (int sp : split_opts) {
+            if (sp > 1 && ks / sp < 3) continue;
+            const int e = eff_splits(d.K, sp);
+            if (e > 1 && (int64_t)e * d.M * d.N > ws_elems_) continue;
+            std::vector<int> key = {bm, bn, e};
+            if (std::find(seen.begin(), seen.end(), key) != seen.end()) continue;
+            seen.push_back(key);
+            ConvTile t;
+            t.bm = bm;
+            t.bn = bn;
+            t.splits = sp;
+            conv(l, mode, (int)B, t, s, mode == CS_CONV_FWD);  // warm
+            ok(hipEventRecord(e0, s), "record");
+            for (int64_t i = 0; i < iters; ++i) conv(l, mode, (int)B, t, s, mode == CS_CONV_FWD);
+            ok(hipEventRecord(e1, s), "record");
+            ok(hipEventSynchronize(e1), "sync");
+            float ms = 0.f;
+            ok(hipEventElapsedTime(&ms, e0, e1), "elapsed");
+            const float us = 1000.f * ms / (float)iters;
+            if (us < best_t) {
+              best_t = us;
+              best = t;
+            }
+          }
+        }
+      }
+      best.us = best_t;
+      blocks_[l].tile[mode] = best;
+      best_us.push_back(best_t);
+    }
+  }
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  return best_us;
+}
+
+}  // namespace cs

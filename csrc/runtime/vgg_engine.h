@@ -1,0 +1,103 @@
+// Native VGG training engine: a hand-scheduled forward/backward (no autograd) over
+// flat parameter / gradient / momentum buffers, every op a gfx950 HIP kernel.
+//
+// Replaces, for the reference's whole hot loop (master/part1/part1.py:31-38 and
+// its part2/part3 variants): the torchvision batch pipeline, nn.Sequential VGG
+// forward (master/part1/model.py:42-46), CrossEntropyLoss, autograd backward,
+// the gradient synchronisation of part2a/2b/3 and optimizer.step().
+//
+// Layout (set by the Python side, runtime/engine.py):
+//  * flat buffers hold tensors in BACKWARD-READY order — fc1.{weight,bias}, then
+//    the conv blocks from last to first, each {conv.weight (OHWI; conv0 OIHW),
+//    conv.bias, bn.weight, bn.bias} — every tensor 256-B aligned, so a gradient
+//    bucket is one contiguous range that is complete as soon as the backward of
+//    its last block has run;
+//  * activations NHWC; conv0's input padded to 4 channels (one float4 / pixel);
+//  * per block: conv input x, conv output y (pre-BN, kept for BN/ReLU/pool
+//    backward recompute), BN tile partials (from the conv epilogue), BN coeffs.
+// Every method enqueues on the caller's current HIP stream and never syncs the
+// host, so a whole step (or any bucket segment of it) can be captured as a graph.
+#pragma once
+#include <torch/extension.h>
+
+#include <memory>
+#include <vector>
+
+#include "kernels/launchers.h"
+#include "runtime/rccl_comm.h"
+
+namespace cs {
+
+struct ConvTile {
+  int bm = 64, bn = 64, splits = 1;
+  float us = -1.f;  // measured time of the chosen config (autotune), -1 = untuned
+};
+
+struct VggBlock {
+  int cin = 0, cout = 0, H = 0, pool = 0;  // cin = 4 for the padded conv0
+  int64_t w_off = 0, b_off = 0, g_off = 0, be_off = 0, rm_off = 0, rv_off = 0;
+  ConvTile tile[3];
+  torch::Tensor x;      // [Bmax, H, H, cin]
+  torch::Tensor y;      // [Bmax*H*H, cout]
+  torch::Tensor stats;  // [ceil(Bmax*H*H/64), cout, 2]
+  torch::Tensor bn;     // [4, cout]: scale, shift, mean, invstd
+};
+
+class VggEngine {
+ public:
+  // desc: 4 ints per block (cin, cout, H, pool); offs: 4 per block (w, b, gamma, beta) + (fc_w, fc_b);
+  // buf_offs: 2 per block (running_mean, running_var) into `bufs`.
+  VggEngine(int64_t Bmax, std::vector<int64_t> desc, std::vector<int64_t> offs, std::vector<int64_t> buf_offs,
+            int64_t feat, int64_t ncls, torch::Tensor params, torch::Tensor grads, torch::Tensor mom,
+            torch::Tensor bufs, torch::Tensor nbt);
+
+  // slot 0 = train, 1 = eval. data uint8 [N,32,32,3], labels int64 [N], aug int32 [N,3] (dy, dx, flip)
+  void set_data(int64_t slot, torch::Tensor data, torch::Tensor labels, torch::Tensor aug);
+  torch::Tensor idx() const { return idx_; }
+  torch::Tensor loss() const { return loss_; }
+  torch::Tensor correct() const { return correct_; }
+  torch::Tensor logits() const { return logits_; }
+  int64_t num_blocks() const { return (int64_t)blocks_.size(); }
+  // debug/test access: "x" (block input), "y" (conv output), "bn" ([4,C] scale/shift/mean/invstd), "stats",
+  // "g0"/"g1" (gradient ping-pong), "dz"
+  torch::Tensor tensor(int64_t block, const std::string& name) const;
+
+  // augment + conv/BN/ReLU/pool chain + fused linear/xent fwd+bwd (train) for B <= Bmax samples
+  void forward_train(int64_t B);
+  // backward of blocks hi..lo (inclusive, hi >= lo), writing their gradients into `grads`
+  void backward(int64_t hi, int64_t lo, int64_t B);
+  // SGD (momentum, weight decay, dampening) on [off, off+n) of the flat buffers
+  void sgd(double lr, double momentum, double wd, double dampening, int64_t off, int64_t n);
+  // eval forward (running stats): loss (mean over the batch) -> loss(), correct count -> correct()
+  void forward_eval(int64_t B);
+
+  // whole step in C++: forward, bucketed backward with (optional) RCCL all-reduce(avg)
+  // of each bucket as soon as it is complete, SGD. bucket_blocks[k] = lowest block of
+  // bucket k (buckets cover blocks from the top), bucket_ranges = (off, n) per bucket.
+  void step(int64_t B, RcclComm* comm, const std::vector<int64_t>& bucket_blocks,
+            const std::vector<int64_t>& bucket_ranges, bool broadcast_buffers, double lr, double momentum,
+            double wd, double dampening);
+
+  // conv tile control: mode 0 fwd / 1 dgrad / 2 wgrad
+  void set_tile(int64_t block, int64_t mode, int64_t bm, int64_t bn, int64_t splits);
+  std::vector<int64_t> get_tile(int64_t block, int64_t mode) const;
+  // time every candidate (bm, bn in {64,128}, split-K) per (block, mode) with HIP events and keep the fastest
+  std::vector<double> autotune(int64_t B, int64_t iters);
+  // run a single conv GEMM of the training step (for profiling / tests)
+  void run_conv(int64_t block, int64_t mode, int64_t B);
+
+ private:
+  void conv(int l, int mode, int B, const ConvTile& t, hipStream_t s, bool with_stats);
+  float* P(int64_t off) { return params_.data_ptr<float>() + off; }
+  float* G(int64_t off) { return grads_.data_ptr<float>() + off; }
+  int64_t Bmax_, feat_, ncls_;
+  std::vector<VggBlock> blocks_;
+  int64_t fc_w_ = 0, fc_b_ = 0;
+  torch::Tensor params_, grads_, mom_, bufs_, nbt_;
+  torch::Tensor data_[2], labels_[2], aug_[2];
+  torch::Tensor idx_, ylab_, loss_, correct_, logits_, pred_;
+  torch::Tensor gbuf_[2], dz_, ws_, bn_part_, bn_coef_, bn_eval_;
+  int64_t ws_elems_ = 0;
+};
+
+}  // namespace cs

@@ -95,7 +95,9 @@ def test_conv_wgrad(dev, shape, tile):
 
 
 @pytest.mark.parametrize("B,H,C,pool", [(2, 32, 64, True), (4, 8, 256, False), (3, 4, 512, True),
-                                        (64, 2, 512, True), (5, 16, 128, True)])
+                                        (64, 2, 512, True), (5, 16, 128, True), (8, 8, 256, False),
+                                        (16, 8, 256, False), (8, 4, 512, False), (64, 8, 256, False),
+                                        (64, 32, 64, True)])
 def test_bn_relu_pool_fwd_bwd(dev, B, H, C, pool):
     from cs744_pytorch_distributed_tutorial_amd.ops import functional as Fn
     torch.manual_seed(B * C)

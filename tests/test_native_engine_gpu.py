@@ -1,0 +1,170 @@
+"""The native engine (C++ VggEngine + gfx950 kernels) vs a float64 PyTorch
+reference of the reference model, plus graph/eager bit-equality and the native
+RCCL communicator at world_size 1 (MI355X only)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from cs744_pytorch_distributed_tutorial_amd.ops import native
+    native.C()
+    return torch.device("cuda", 0)
+
+
+def _trainer(dev, **kw):
+    from cs744_pytorch_distributed_tutorial_amd.runtime.engine import NativeTrainer
+    args = dict(batch_size=8, device=dev, train_size=256, test_size=40, autotune=False, graph="none")
+    args.update(kw)
+    return NativeTrainer(**args)
+
+
+def _rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return ((a - b).abs().max() / (b.abs().max() + 1e-12)).item()
+
+
+def test_engine_matches_fp64_reference_two_steps(dev):
+    from cs744_pytorch_distributed_tutorial_amd.models import VGG11
+    from cs744_pytorch_distributed_tutorial_amd.utils import data as dm
+    tr = _trainer(dev)
+    ref = VGG11().double()
+    ref.load_state_dict({k: v.double() if v.is_floating_point() else v for k, v in tr.state_dict().items()})
+    opt = torch.optim.SGD(ref.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+    order = tr.sampler.indices()
+    for step in range(2):
+        idx = torch.tensor(order[step * 8:(step + 1) * 8])
+        x = dm.augment_reference(tr.train_set.data, idx, tr.aug_train.cpu()).double()
+        y = tr.train_set.targets[idx]
+        opt.zero_grad()
+        loss = F.cross_entropy(ref(x), y)
+        loss.backward()
+        tr.step()
+        assert abs(tr.last_loss() - loss.item()) <= 1e-4 * max(1.0, abs(loss.item())), (step, tr.last_loss(), loss)
+        if step == 0:
+            # A pre-activation within fp32 rounding of 0 can flip a ReLU mask between fp32 and fp64
+            # (measured: sum(g) = 0.0037 vs sum|g| = 0.37 for one BN bias at B=8), which moves that
+            # bias grad by ~1e-2 relative and everything below it by ~1e-3. So: tight per-tensor
+            # checks for most tensors, a norm bound for the whole gradient.
+            g = tr.grads_state()
+            tight, num, den = 0, 0.0, 0.0
+            conv_bias = {f"layers.{s.conv_idx}.bias" for s in tr.layout.specs}
+            names = [n for n, _ in ref.named_parameters() if n not in conv_bias]
+            for n, p in ref.named_parameters():
+                if n not in names:
+                    assert g[n].abs().max() < 1e-4, n  # conv bias grad is ~0: BN removes it
+                    continue
+                tight += _rel(g[n], p.grad) < 1e-4
+                num += float(((g[n].double() - p.grad) ** 2).sum())
+                den += float((p.grad ** 2).sum())
+            assert tight >= len(names) // 2, tight
+            assert (num / den) ** 0.5 < 5e-3, (num / den) ** 0.5
+        opt.step()
+    sd = tr.state_dict()
+    num = den = 0.0
+    for k, v in ref.state_dict().items():
+        if v.is_floating_point():
+            # lr 0.1 at B=8 moves conv weights by about their own size per step, so a gradient
+            # perturbed by a ReLU-mask flip shows up 1:1 in that tensor: bound the global norm only
+            num += float(((sd[k].double() - v) ** 2).sum())
+            den += float((v ** 2).sum())
+        else:
+            assert torch.equal(sd[k], v), k
+    assert (num / den) ** 0.5 < 2e-3, (num / den) ** 0.5
+
+
+def test_graph_full_equals_eager_bitwise(dev):
+    a = _trainer(dev, graph="none")
+    b = _trainer(dev, graph="full")
+    for _ in range(5):
+        a.step()
+        b.step()
+    torch.cuda.synchronize()
+    assert b._graphs is not None and len(b._graphs) == 1
+    assert torch.equal(a.params, b.params)
+    assert torch.equal(a.mom, b.mom)
+    assert torch.equal(a.bufs, b.bufs)
+    assert torch.equal(a.nbt, b.nbt)
+
+
+def test_graph_segments_equals_eager_bitwise(dev):
+    a = _trainer(dev, graph="none", bucket_mb=1.0)
+    b = _trainer(dev, graph="segments", bucket_mb=1.0)
+    for _ in range(4):
+        a.step()
+        b.step()
+    torch.cuda.synchronize()
+    assert b._graphs is not None and len(b._graphs) == len(b.bucket_lows) + 1
+    assert torch.equal(a.params, b.params)
+
+
+def test_autotune_keeps_numerics(dev):
+    a = _trainer(dev)
+    b = _trainer(dev, autotune=True)
+    assert b.tune_us is not None and all(t >= 0 for t in b.tune_us)
+    for _ in range(2):
+        a.step()
+        b.step()
+    assert _rel(b.params, a.params) < 1e-5
+
+
+def test_loss_decreases_and_eval(dev):
+    tr = _trainer(dev, batch_size=64, train_size=2048, test_size=256, graph="full")
+    first = None
+    for i in range(60):
+        tr.step()
+        if i == 0:
+            first = tr.last_loss()
+    last = tr.last_loss()
+    assert last < first, (first, last)
+    ev = tr.evaluate()
+    assert ev["total"] == 256 and 0 <= ev["correct"] <= 256 and ev["avg_loss"] == ev["avg_loss"]
+
+
+def test_state_dict_loads_into_reference_model(dev):
+    from cs744_pytorch_distributed_tutorial_amd.models import VGG11
+    tr = _trainer(dev)
+    tr.step()
+    m = VGG11()
+    m.load_state_dict(tr.state_dict())  # the reference's 58-key layout
+    osd = tr.optimizer_state_dict()
+    opt = torch.optim.SGD(m.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+    opt.load_state_dict(osd)
+    tr2 = _trainer(dev, init_state=m.state_dict())
+    tr2.load_optimizer_state_dict(opt.state_dict())
+    assert torch.equal(tr2.params, tr.params) and torch.equal(tr2.mom, tr.mom)
+
+
+def test_rccl_comm_world1_and_graph_capture(dev):
+    from cs744_pytorch_distributed_tutorial_amd.parallel.rccl import RcclComm
+    c = RcclComm.create(0, 1, 0)
+    x = torch.arange(1000, dtype=torch.float32, device=dev)
+    c.all_reduce_avg(x).wait()
+    torch.testing.assert_close(x, torch.arange(1000, dtype=torch.float32, device=dev))
+    out = torch.empty(1000, device=dev)
+    c.gather_flat(x, out, 0)
+    torch.testing.assert_close(out, x)
+    g = c.all_gather_int64(torch.tensor([3, 4], device=dev))
+    assert g.tolist() == [[3, 4]]
+    # stream-ordered collective captured in a hipGraph
+    y = torch.ones(4096, device=dev)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(graph, stream=s):
+            y.mul_(2.0)
+            c.all_reduce_avg(y).wait()
+            y.add_(1.0)
+    torch.cuda.current_stream().wait_stream(s)
+    y.fill_(1.0)
+    graph.replay()
+    graph.replay()
+    torch.cuda.synchronize()
+    assert torch.all(y == 7.0)
+    assert c.native.async_error() == ""
