@@ -22,6 +22,7 @@ from . import native
 FWD, DGRAD, WGRAD = 0, 1, 2
 BN_EPS = 1e-5
 BN_MOMENTUM = 0.1
+SPLITK_STAT_ROWS = 16  # csrc/kernels/launchers.h CS_SPLITK_STAT_ROWS
 
 
 def oihw_to_ohwi(w: torch.Tensor) -> torch.Tensor:
@@ -54,7 +55,7 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], *, 
     B, H, W, cin = x.shape
     cout = w.shape[0]
     y = torch.empty(B * H * W, cout, device=x.device, dtype=torch.float32)
-    R = 64 if splits > 1 else bm
+    R = SPLITK_STAT_ROWS if splits > 1 else bm
     T = (B * H * W + R - 1) // R
     st = torch.empty(T, cout, 2, device=x.device, dtype=torch.float32) if stats else None
     rows = native.C().conv_gemm(FWD, x, w, None, bias, y, _ws(FWD, B, H, W, cin, cout, splits, x.device), st,

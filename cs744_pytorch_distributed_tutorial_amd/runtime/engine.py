@@ -223,7 +223,7 @@ class NativeTrainer:
         self.idx_buf = self.engine.idx()
         self.tune_us: Optional[List[float]] = None
         if autotune:
-            self.tune_us = list(self.engine.autotune(self.B, 5))
+            self._tune(model, os.environ.get("CS744_TUNE_CACHE"))
         if graph == "auto":
             graph = "full" if world == 1 else "segments"
         if graph == "full" and world > 1 and (self.native_comm is None or self.sync_mode not in ("ddp", "none")):
@@ -238,6 +238,40 @@ class NativeTrainer:
         self.global_step = 0
         self._epoch_idx = None
         self._start_epoch(0)
+
+    def _tune(self, model: str, cache: Optional[str]) -> None:
+        """Autotune conv tiles (HIP-event timed), or reuse a JSON tuning cache keyed by model/batch."""
+        import json
+        key = f"{model}/B{self.B}/gfx950"
+        db = {}
+        if cache and os.path.exists(cache):
+            with open(cache) as f:
+                db = json.load(f)
+        if key in db:
+            for l, m, bm, bn, sp in db[key]["tiles"]:
+                self.engine.set_tile(l, m, bm, bn, sp)
+            self.tune_us = db[key]["us"]
+            return
+        self.tune_us = list(self.engine.autotune(self.B, 5))
+        if cache and self.rank == 0:
+            tiles = [[l, m] + list(self.engine.get_tile(l, m)) for l in range(self.layout.L) for m in range(3)
+                     if not (l == 0 and m == 1)]
+            db[key] = {"tiles": tiles, "us": self.tune_us}
+            with open(cache, "w") as f:
+                json.dump(db, f, indent=1)
+
+    def tile_table(self) -> List[dict]:
+        """Chosen (bm, bn, split-K) and measured time per conv GEMM of the step."""
+        out = []
+        names = ("fwd", "dgrad", "wgrad")
+        for l in range(self.layout.L):
+            for m in range(3):
+                if l == 0 and m == 1:
+                    continue
+                bm, bn, sp = self.engine.get_tile(l, m)
+                us = self.tune_us[3 * l + m] if self.tune_us else None
+                out.append({"block": l, "op": names[m], "bm": bm, "bn": bn, "splits": sp, "us": us})
+        return out
 
     # ---------------------------------------------------------------- data
     def steps_per_epoch(self) -> int:

@@ -44,7 +44,7 @@ int64_t conv_gemm(int64_t mode, c10::optional<torch::Tensor> x, c10::optional<to
     TORCH_CHECK(x.has_value() && w.has_value(), "conv fwd needs x and w");
     check_t(x, pix * Cin, "x"); check_t(w, wnum, "w"); check_t(bias, Cout, "bias");
     check_t(out, pix * Cout, "out");
-    const int64_t R = std::min<int64_t>(splits, (9 * Cin + 15) / 16) > 1 ? 64 : bm;
+    const int64_t R = std::min<int64_t>(splits, (9 * Cin + 15) / 16) > 1 ? CS_SPLITK_STAT_ROWS : bm;
     check_t(stats, ((pix + R - 1) / R) * Cout * 2, "stats");
   } else if (mode == CS_CONV_DGRAD) {
     TORCH_CHECK(dz.has_value() && w.has_value(), "conv dgrad needs dz and w");
@@ -63,7 +63,7 @@ int64_t conv_gemm(int64_t mode, c10::optional<torch::Tensor> x, c10::optional<to
   a.x = cptr(x); a.w = cptr(w); a.dz = cptr(dz); a.bias = cptr(bias);
   a.out = out.data_ptr<float>(); a.ws = mptr(ws); a.stats = mptr(stats);
   CS_LAUNCH(cs_conv_gemm(a, (int)mode, (int)bm, (int)bn, (int)splits, cur_stream()));
-  return sp > 1 ? 64 : bm;
+  return sp > 1 ? CS_SPLITK_STAT_ROWS : bm;
 }
 
 void bn_finalize(torch::Tensor part, int64_t T, int64_t R, int64_t M, torch::Tensor gamma, torch::Tensor beta,

@@ -86,12 +86,13 @@ std::vector<torch::Tensor> linear_xent(torch::Tensor feat, torch::Tensor W, torc
   TORCH_CHECK(feat.dim() == 2 && W.dim() == 2 && bias.dim() == 1 && feat.size(1) == W.size(1) &&
               W.size(0) == bias.size(0) && labels.size(0) == feat.size(0), "linear_xent: shapes");
   const int B = feat.size(0), K = feat.size(1), C = W.size(0);
-  TORCH_CHECK(C <= 16 && 2 * B * C + 16 <= 40960, "linear_xent: C<=16 and B*C small enough for LDS");
+  TORCH_CHECK(C <= 16 && K % 4 == 0, "linear_xent: C <= 16 and K % 4 == 0");
   DevGuard gd(feat.device());
   auto loss = torch::empty({}, feat.options());
   auto correct = torch::empty({}, feat.options().dtype(at::kInt));
   auto logits = torch::empty({B, C}, feat.options());
   auto pred = torch::empty({B}, feat.options().dtype(at::kLong));
+  auto ws = torch::empty({cs_linear_xent_ws(B, C)}, feat.options());
   torch::Tensor dW, db, dfeat;
   if (backward) {
     dW = torch::empty_like(W);
@@ -102,7 +103,8 @@ std::vector<torch::Tensor> linear_xent(torch::Tensor feat, torch::Tensor W, torc
                            labels.data_ptr<int64_t>(), B, K, C, (float)gscale, loss.data_ptr<float>(),
                            correct.data_ptr<int>(), logits.data_ptr<float>(),
                            backward ? dW.data_ptr<float>() : nullptr, backward ? db.data_ptr<float>() : nullptr,
-                           backward ? dfeat.data_ptr<float>() : nullptr, pred.data_ptr<int64_t>(), cur_stream()));
+                           backward ? dfeat.data_ptr<float>() : nullptr, pred.data_ptr<int64_t>(),
+                           ws.data_ptr<float>(), cur_stream()));
   if (backward) return {loss, correct, logits, dW, db, dfeat, pred};
   return {loss, correct, logits, pred};
 }

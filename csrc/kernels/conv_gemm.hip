@@ -367,72 +367,104 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(CsConvArgs a) {
 }
 
 // Deterministic split-K combine: out = sum_z ws[z] (+bias, +BN tile stats for FWD;
-// OIHW scatter for the conv0 weight gradient). Tile = 64 rows x 64 columns.
-__global__ __launch_bounds__(256) void splitk_reduce_kernel(CsConvArgs a, int mode, int splits) {
-  __shared__ float red[16][64];
+// OIHW scatter for the conv0 weight gradient). Tile = 16 rows x 64 columns (one row
+// and one float4 per thread) so even an M = 256 GEMM gets enough blocks to stream
+// the slabs at HBM rate. Large split counts are first folded in groups of
+// kFold slabs (pre-pass, in place into the group's first slab), so no thread
+// walks more than ~kFold dependent loads. Summation order is fixed.
+constexpr int kRedRows = 16;
+constexpr int kFold = 16;
+
+__global__ __launch_bounds__(256) void splitk_fold_kernel(float* __restrict__ ws, size_t slab, int splits) {
+  // grid.y = group g: ws[g*kFold] = sum_{z in group} ws[z]
+  const size_t n4 = slab >> 2;
+  const int z0 = blockIdx.y * kFold;
+  const int z1 = min(splits, z0 + kFold);
+  float4* w4 = reinterpret_cast<float4*>(ws);
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
+    float4 acc = w4[(size_t)z0 * n4 + i];
+    for (int z = z0 + 1; z < z1; ++z) {
+      const float4 t = w4[(size_t)z * n4 + i];
+      acc.x += t.x; acc.y += t.y; acc.z += t.z; acc.w += t.w;
+    }
+    w4[(size_t)z0 * n4 + i] = acc;
+  }
+}
+
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(CsConvArgs a, int mode, int nslab, int zstep) {
+  __shared__ float red[kRedRows][64];
   __shared__ float meanv[64];
   const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
   const int ntn = (a.N + 63) / 64;
   const int mt = blockIdx.x / ntn, nt = blockIdx.x - mt * ntn;
-  const int m0 = mt * 64, n0 = nt * 64, n = n0 + 4 * tx;
+  const int m0 = mt * kRedRows, n0 = nt * 64, n = n0 + 4 * tx, m = m0 + ty;
   const size_t slab = (size_t)a.M * a.N;
-  float4 v[4];
-  float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (mode == CS_CONV_FWD && a.bias != nullptr && n < a.N) bv = *reinterpret_cast<const float4*>(a.bias + n);
-  float4 s1 = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-  for (int rr = 0; rr < 4; ++rr) {
-    const int m = m0 + ty + 16 * rr;
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (m < a.M && n < a.N) {
-      const float* p = a.ws + (size_t)m * a.N + n;
-      for (int z = 0; z < splits; ++z) {
-        const float4 t = *reinterpret_cast<const float4*>(p + z * slab);
-        acc.x += t.x; acc.y += t.y; acc.z += t.z; acc.w += t.w;
-      }
-      acc.x += bv.x; acc.y += bv.y; acc.z += bv.z; acc.w += bv.w;
-      if (mode == CS_CONV_WGRAD && a.w_oihw) {
-        const float vals[4] = {acc.x, acc.y, acc.z, acc.w};
-        for (int q = 0; q < 4; ++q) {
-          const int nn = n + q, tap = nn >> 2, ci = nn & 3;
-          if (ci < 3) a.out[(size_t)m * 27 + ci * 9 + tap] = vals[q];
-        }
-      } else {
-        *reinterpret_cast<float4*>(a.out + (size_t)m * a.N + n) = acc;
-      }
-      s1.x += acc.x; s1.y += acc.y; s1.z += acc.z; s1.w += acc.w;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  const bool in = m < a.M && n < a.N;
+  if (in) {
+    const float* p = a.ws + (size_t)m * a.N + n;
+    for (int z = 0; z < nslab; ++z) {
+      const float4 t = *reinterpret_cast<const float4*>(p + (size_t)z * zstep * slab);
+      acc.x += t.x; acc.y += t.y; acc.z += t.z; acc.w += t.w;
     }
-    v[rr] = acc;
+    if (mode == CS_CONV_FWD && a.bias != nullptr) {
+      const float4 bv = *reinterpret_cast<const float4*>(a.bias + n);
+      acc.x += bv.x; acc.y += bv.y; acc.z += bv.z; acc.w += bv.w;
+    }
+    if (mode == CS_CONV_WGRAD && a.w_oihw) {
+      const float vals[4] = {acc.x, acc.y, acc.z, acc.w};
+      for (int q = 0; q < 4; ++q) {
+        const int nn = n + q, tap = nn >> 2, ci = nn & 3;
+        if (ci < 3) a.out[(size_t)m * 27 + ci * 9 + tap] = vals[q];
+      }
+    } else {
+      *reinterpret_cast<float4*>(a.out + (size_t)m * a.N + n) = acc;
+    }
   }
   if (mode != CS_CONV_FWD || a.stats == nullptr) return;
-  const int cnt = (a.M - m0) < 64 ? (a.M - m0) : 64;
-  red[ty][4 * tx + 0] = s1.x; red[ty][4 * tx + 1] = s1.y; red[ty][4 * tx + 2] = s1.z; red[ty][4 * tx + 3] = s1.w;
+  // per-column (mean, M2) of this 16-row tile (two-pass inside the tile: robust)
+  const int cnt = (a.M - m0) < kRedRows ? (a.M - m0) : kRedRows;
+  red[ty][4 * tx + 0] = in ? acc.x : 0.f;
+  red[ty][4 * tx + 1] = in ? acc.y : 0.f;
+  red[ty][4 * tx + 2] = in ? acc.z : 0.f;
+  red[ty][4 * tx + 3] = in ? acc.w : 0.f;
   __syncthreads();
   if (threadIdx.x < 64) {
-    float s = 0.f;
-    for (int k = 0; k < 16; ++k) s += red[k][threadIdx.x];
-    meanv[threadIdx.x] = s / (float)cnt;
+    float sum = 0.f;
+    for (int k = 0; k < kRedRows; ++k) sum += red[k][threadIdx.x];
+    meanv[threadIdx.x] = sum / (float)cnt;
   }
   __syncthreads();
-  const float mx = meanv[4 * tx], my = meanv[4 * tx + 1], mz = meanv[4 * tx + 2], mw = meanv[4 * tx + 3];
-  float4 s2 = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-  for (int rr = 0; rr < 4; ++rr) {
-    const int m = m0 + ty + 16 * rr;
-    if (m < a.M && n < a.N) {
-      const float dx = v[rr].x - mx, dy = v[rr].y - my, dz = v[rr].z - mz, dw = v[rr].w - mw;
-      s2.x += dx * dx; s2.y += dy * dy; s2.z += dz * dz; s2.w += dw * dw;
-    }
-  }
+  const float dx = in ? acc.x - meanv[4 * tx] : 0.f, dy = in ? acc.y - meanv[4 * tx + 1] : 0.f;
+  const float dz = in ? acc.z - meanv[4 * tx + 2] : 0.f, dw = in ? acc.w - meanv[4 * tx + 3] : 0.f;
   __syncthreads();
-  red[ty][4 * tx + 0] = s2.x; red[ty][4 * tx + 1] = s2.y; red[ty][4 * tx + 2] = s2.z; red[ty][4 * tx + 3] = s2.w;
+  red[ty][4 * tx + 0] = dx * dx;
+  red[ty][4 * tx + 1] = dy * dy;
+  red[ty][4 * tx + 2] = dz * dz;
+  red[ty][4 * tx + 3] = dw * dw;
   __syncthreads();
   if (threadIdx.x < 64 && n0 + (int)threadIdx.x < a.N) {
-    float s = 0.f;
-    for (int k = 0; k < 16; ++k) s += red[k][threadIdx.x];
+    float sq = 0.f;
+    for (int k = 0; k < kRedRows; ++k) sq += red[k][threadIdx.x];
     a.stats[((size_t)mt * a.N + n0 + threadIdx.x) * 2 + 0] = meanv[threadIdx.x];
-    a.stats[((size_t)mt * a.N + n0 + threadIdx.x) * 2 + 1] = s;
+    a.stats[((size_t)mt * a.N + n0 + threadIdx.x) * 2 + 1] = sq;
   }
+}
+
+hipError_t launch_reduce(const CsConvArgs& a, int mode, int splits, hipStream_t stream) {
+  int nslab = splits, zstep = 1;
+  if (splits > 2 * kFold) {
+    const size_t slab = (size_t)a.M * a.N;
+    const int groups = (splits + kFold - 1) / kFold;
+    int bx = (int)((slab / 4 + 255) / 256);
+    if (bx > 1024) bx = 1024;
+    hipLaunchKernelGGL(splitk_fold_kernel, dim3(bx, groups), dim3(256), 0, stream, a.ws, slab, splits);
+    nslab = groups;
+    zstep = kFold;
+  }
+  const int nt = ((a.M + kRedRows - 1) / kRedRows) * ((a.N + 63) / 64);
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(nt), dim3(256), 0, stream, a, mode, nslab, zstep);
+  return hipGetLastError();
 }
 
 template <int BM, int BN, int MODE>
@@ -490,9 +522,7 @@ hipError_t cs_conv_gemm(CsConvArgs a, int mode, int bm, int bn, int splits, hipS
     else if (mode == CS_CONV_DGRAD) e = launch_gemm<BM_, BN_, CS_CONV_DGRAD>(a, splits, stream); \
     else e = launch_gemm<BM_, BN_, CS_CONV_WGRAD>(a, splits, stream);                            \
     if (e != hipSuccess || splits == 1) return e;                               \
-    const int nt = ((a.M + 63) / 64) * ((a.N + 63) / 64);                        \
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(nt), dim3(256), 0, stream, a, mode, splits); \
-    return hipGetLastError();                                                   \
+    return launch_reduce(a, mode, splits, stream);                              \
   }
   CS_DISPATCH(64, 64)
   CS_DISPATCH(128, 64)

@@ -25,7 +25,8 @@ hipError_t cs_sgd_multi(const CsTensorEntry* tab_dev, int ntens, const int64_t* 
 // classifier head
 hipError_t cs_linear_xent(const float* feat, const float* W, const float* bias, const int64_t* labels, int B, int K,
                           int C, float gscale, float* loss_out, int* correct_out, float* logits_out, float* dW,
-                          float* db, float* dfeat, int64_t* pred_out, hipStream_t stream);
+                          float* db, float* dfeat, int64_t* pred_out, float* ws, hipStream_t stream);
+inline int64_t cs_linear_xent_ws(int B, int C) { return (int64_t)B * (C + 2); }
 hipError_t cs_softmax_xent(const float* logits, const int64_t* labels, int B, int C, float gscale, float* loss_out,
                            float* dlogits, int* correct_out, hipStream_t stream);
 
@@ -48,7 +49,8 @@ struct CsConvArgs {
 
 void cs_conv_fill_dims(CsConvArgs* a, int mode);
 // bm, bn in {64, 128}; splits >= 1 (split-K over blockIdx.z + deterministic reduce).
-// FWD stats tiles have `bm` rows when splits == 1 and 64 rows otherwise.
+// FWD stats tiles have `bm` rows when splits == 1 and CS_SPLITK_STAT_ROWS rows otherwise.
+#define CS_SPLITK_STAT_ROWS 16
 hipError_t cs_conv_gemm(CsConvArgs a, int mode, int bm, int bn, int splits, hipStream_t stream);
 
 // ---------------------------------------------------------------- BatchNorm + ReLU (+ 2x2 max-pool), NHWC

@@ -2,10 +2,10 @@
 // CrossEntropyLoss(mean) (master/part1/part1.py:94) forward AND backward, plus the
 // eval argmax/accuracy count (master/part2b/part2b.py:64-65) — SURVEY.md §2.2 N8/N9/N13.
 //
-// The head is tiny (B x 10 x 512), so one 512-thread workgroup does everything with
-// the logits / dlogits in LDS: no intermediate tensor ever touches HBM and the five
-// ATen kernels of the reference (addmm, log_softmax, nll, their backwards, argmax)
-// become one launch. The loss is written as a device scalar so the training loop
+// Two launches replace the reference's five ATen kernels (addmm, log_softmax, nll,
+// their backwards, argmax): a row pass (one wave per sample: logits, softmax, loss,
+// argmax and dfeat from registers) and a column pass (dW / db / batch loss), both
+// with fixed summation order. `ws` holds dl [B][C] + per-sample loss/correct. The loss is written as a device scalar so the training loop
 // never syncs the host (the loss is read only every 20 iterations).
 #include "common.h"
 #include "launchers.h"
@@ -14,21 +14,6 @@ namespace {
 
 constexpr int kThreads = 512;
 constexpr int kMaxC = 16;
-
-// logits[b][j] = bias[j] + <feat[b], W[j]>   (one wave per (b, j) pair)
-__device__ void head_forward(const float* __restrict__ feat, const float* __restrict__ W,
-                             const float* __restrict__ bias, int B, int K, int C, float* lg) {
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  for (int pr = wid; pr < B * C; pr += nw) {
-    const int b = pr / C, j = pr - b * C;
-    const float* f = feat + (size_t)b * K;
-    const float* w = W + (size_t)j * K;
-    float acc = 0.f;
-    for (int k = lane; k < K; k += 64) acc += f[k] * w[k];
-    acc = cs::wave_sum(acc);
-    if (lane == 0) lg[pr] = acc + (bias ? bias[j] : 0.f);
-  }
-}
 
 // per-sample softmax-xent: loss partial, dlogits (mean reduction), argmax correctness
 __device__ void head_loss(const float* lg, const int64_t* __restrict__ labels, int B, int C, float gscale,
@@ -67,41 +52,124 @@ __device__ void head_loss(const float* lg, const int64_t* __restrict__ labels, i
   }
 }
 
-__global__ __launch_bounds__(kThreads) void linear_xent_kernel(
-    const float* __restrict__ feat, const float* __restrict__ W, const float* __restrict__ bias,
-    const int64_t* __restrict__ labels, int B, int K, int C, float gscale, float* __restrict__ loss_out,
-    int* __restrict__ correct_out, float* __restrict__ logits_out, float* __restrict__ dW,
-    float* __restrict__ db, float* __restrict__ dfeat, int64_t* __restrict__ pred_out) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* lg = smem;              // [B*C]
-  float* dlg = smem + B * C;     // [B*C]
-  float* red = dlg + B * C;      // [16]
-  head_forward(feat, W, bias, B, K, C, lg);
-  __syncthreads();
-  const bool bwd = dW != nullptr;
-  head_loss(lg, labels, B, C, gscale, bwd ? dlg : nullptr, red, loss_out, correct_out, logits_out, pred_out);
-  __syncthreads();
-  if (!bwd) return;
-  // dW[j][k] = sum_b dlg[b][j] * feat[b][k];  db[j] = sum_b dlg[b][j]
-  for (int e = threadIdx.x; e < C * K; e += blockDim.x) {
-    const int j = e / K, k = e - j * K;
-    float acc = 0.f;
-    for (int b = 0; b < B; ++b) acc += dlg[b * C + j] * feat[(size_t)b * K + k];
-    dW[e] = acc;
-  }
-  if (threadIdx.x < (unsigned)C) {
-    float acc = 0.f;
-    for (int b = 0; b < B; ++b) acc += dlg[b * C + threadIdx.x];
-    db[threadIdx.x] = acc;
-  }
-  // dfeat[b][k] = sum_j dlg[b][j] * W[j][k]
-  if (dfeat) {
-    for (int e = threadIdx.x; e < B * K; e += blockDim.x) {
-      const int b = e / K, k = e - b * K;
-      float acc = 0.f;
-      for (int j = 0; j < C; ++j) acc += dlg[b * C + j] * W[(size_t)j * K + k];
-      dfeat[e] = acc;
+// Row pass: one wave per sample. Each lane holds K/256 float4 slices of the
+// sample's features and of every W row, so the C logits, the softmax, the
+// per-sample loss/argmax AND dfeat[b] = sum_j dl[b][j] W[j] come out of
+// registers; dl is staged in `ws` for the column pass.
+__global__ __launch_bounds__(256) void head_rows_kernel(const float* __restrict__ feat, const float* __restrict__ W,
+                                                        const float* __restrict__ bias,
+                                                        const int64_t* __restrict__ labels, int B, int K, int C,
+                                                        float gscale, float* __restrict__ ws,
+                                                        float* __restrict__ logits_out, int64_t* __restrict__ pred_out,
+                                                        float* __restrict__ dfeat) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= B) return;
+  const int K4 = K >> 2;
+  const float4* f4 = reinterpret_cast<const float4*>(feat) + (size_t)row * K4;
+  const float4* w4 = reinterpret_cast<const float4*>(W);
+  float acc[kMaxC];
+#pragma unroll
+  for (int j = 0; j < kMaxC; ++j) acc[j] = 0.f;
+  for (int k = lane; k < K4; k += 64) {
+    const float4 f = f4[k];
+#pragma unroll
+    for (int j = 0; j < kMaxC; ++j) {
+      if (j < C) {
+        const float4 w = w4[(size_t)j * K4 + k];
+        acc[j] += f.x * w.x + f.y * w.y + f.z * w.z + f.w * w.w;
+      }
     }
+  }
+  float mx = -INFINITY;
+  int am = 0;
+#pragma unroll
+  for (int j = 0; j < kMaxC; ++j) {
+    if (j < C) {
+      acc[j] = cs::wave_sum(acc[j]) + (bias ? bias[j] : 0.f);
+      if (acc[j] > mx) { mx = acc[j]; am = j; }
+    }
+  }
+  float se = 0.f;
+#pragma unroll
+  for (int j = 0; j < kMaxC; ++j)
+    if (j < C) se += expf(acc[j] - mx);
+  const float lse = logf(se);
+  const int y = (int)labels[row];
+  float xy = 0.f;
+#pragma unroll
+  for (int j = 0; j < kMaxC; ++j)
+    if (j == y) xy = acc[j];
+  float* dl = ws;                      // [B][C]
+  float* rowloss = ws + (size_t)B * C;  // [B]
+  float* rowcorr = rowloss + B;         // [B]
+  if (lane == 0) {
+    rowloss[row] = (mx + lse) - xy;
+    rowcorr[row] = (am == y) ? 1.f : 0.f;
+    if (pred_out) pred_out[row] = am;
+  }
+  if (logits_out && lane < C) {
+#pragma unroll
+    for (int j = 0; j < kMaxC; ++j)
+      if (j == lane) logits_out[(size_t)row * C + j] = acc[j];
+  }
+  if (dfeat == nullptr) return;
+  const float inv = gscale / (float)B;
+#pragma unroll
+  for (int j = 0; j < kMaxC; ++j) {
+    if (j < C) {
+      acc[j] = (expf(acc[j] - mx - lse) - (j == y ? 1.f : 0.f)) * inv;
+      if (lane == j) dl[(size_t)row * C + j] = acc[j];
+    }
+  }
+  float4* d4 = reinterpret_cast<float4*>(dfeat) + (size_t)row * K4;
+  for (int k = lane; k < K4; k += 64) {
+    float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int j = 0; j < kMaxC; ++j) {
+      if (j < C) {
+        const float4 w = w4[(size_t)j * K4 + k];
+        o.x += acc[j] * w.x; o.y += acc[j] * w.y; o.z += acc[j] * w.z; o.w += acc[j] * w.w;
+      }
+    }
+    d4[k] = o;
+  }
+}
+
+// Column pass: block j < C computes dW[j][:] = sum_b dl[b][j] feat[b][:]; the last block
+// computes db and the batch loss / correct count (fixed summation order: deterministic).
+__global__ __launch_bounds__(256) void head_cols_kernel(const float* __restrict__ feat, int B, int K, int C,
+                                                        const float* __restrict__ ws, float* __restrict__ dW,
+                                                        float* __restrict__ db, float* __restrict__ loss_out,
+                                                        int* __restrict__ correct_out) {
+  __shared__ float red[16];
+  const float* dl = ws;
+  const float* rowloss = ws + (size_t)B * C;
+  const float* rowcorr = rowloss + B;
+  const int j = blockIdx.x;
+  if (dW != nullptr && j < C) {
+    for (int k = threadIdx.x; k < K; k += blockDim.x) {
+      float s = 0.f;
+      for (int b = 0; b < B; ++b) s += dl[(size_t)b * C + j] * feat[(size_t)b * K + k];
+      dW[(size_t)j * K + k] = s;
+    }
+    return;
+  }
+  float l = 0.f, c = 0.f;
+  for (int b = threadIdx.x; b < B; b += blockDim.x) {
+    l += rowloss[b];
+    c += rowcorr[b];
+  }
+  l = cs::block_sum(l, red);
+  c = cs::block_sum(c, red);
+  if (threadIdx.x == 0) {
+    if (loss_out) *loss_out = l / (float)B;
+    if (correct_out) *correct_out = (int)(c + 0.5f);
+  }
+  if (db != nullptr && threadIdx.x < (unsigned)C) {
+    float s = 0.f;
+    for (int b = 0; b < B; ++b) s += dl[(size_t)b * C + threadIdx.x];
+    db[threadIdx.x] = s;
   }
 }
 
@@ -118,12 +186,13 @@ __global__ __launch_bounds__(kThreads) void softmax_xent_kernel(const float* __r
 
 hipError_t cs_linear_xent(const float* feat, const float* W, const float* bias, const int64_t* labels, int B, int K,
                           int C, float gscale, float* loss_out, int* correct_out, float* logits_out, float* dW,
-                          float* db, float* dfeat, int64_t* pred_out, hipStream_t stream) {
-  if (C > kMaxC || B <= 0) return hipErrorInvalidValue;
-  const size_t lds = (size_t)(2 * B * C + 16) * sizeof(float);
-  if (lds > 160 * 1024) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(linear_xent_kernel, dim3(1), dim3(kThreads), lds, stream, feat, W, bias, labels, B, K, C, gscale,
-                     loss_out, correct_out, logits_out, dW, db, dfeat, pred_out);
+                          float* db, float* dfeat, int64_t* pred_out, float* ws, hipStream_t stream) {
+  if (C > kMaxC || C < 1 || B <= 0 || (K & 3) != 0 || ws == nullptr) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(head_rows_kernel, dim3((B + 3) / 4), dim3(256), 0, stream, feat, W, bias, labels, B, K, C,
+                     gscale, ws, logits_out, pred_out, dfeat);
+  const bool bwd = dW != nullptr && db != nullptr && dfeat != nullptr;
+  hipLaunchKernelGGL(head_cols_kernel, dim3(bwd ? C + 1 : 1), dim3(256), 0, stream, feat, B, K, C, ws,
+                     bwd ? dW : nullptr, bwd ? db : nullptr, loss_out, correct_out);
   return hipGetLastError();
 }
 

@@ -107,7 +107,7 @@ VggEngine::VggEngine(int64_t Bmax, std::vector<int64_t> desc, std::vector<int64_
     const int64_t pix = Bmax * b.H * b.H;
     b.x = torch::zeros({Bmax, b.H, b.H, b.cin}, fo);
     b.y = torch::zeros({pix, b.cout}, fo);
-    b.stats = torch::zeros({cdiv(pix, 64), b.cout, 2}, fo);
+    b.stats = torch::zeros({cdiv(pix, CS_SPLITK_STAT_ROWS), b.cout, 2}, fo);
     b.bn = torch::zeros({4, b.cout}, fo);
     const int64_t ho = b.pool ? b.H / 2 : b.H;
     gmax = std::max(gmax, Bmax * ho * ho * b.cout);
@@ -137,6 +137,8 @@ VggEngine::VggEngine(int64_t Bmax, std::vector<int64_t> desc, std::vector<int64_
   bn_part_ = torch::zeros({partmax}, fo);
   bn_coef_ = torch::zeros({cmax * 3}, fo);
   bn_eval_ = torch::zeros({2, cmax}, fo);
+  TORCH_CHECK(feat % 4 == 0, "VggEngine: feature size must be a multiple of 4");
+  head_ws_ = torch::zeros({cs_linear_xent_ws((int)Bmax, (int)ncls)}, fo);
 }
 
 torch::Tensor VggEngine::tensor(int64_t block, const std::string& name) const {
@@ -216,7 +218,7 @@ void VggEngine::forward_train(int64_t B) {
     const ConvTile& t = b.tile[CS_CONV_FWD];
     conv(l, CS_CONV_FWD, (int)B, t, s, true);
     const int64_t M = B * b.H * b.H;
-    const int rows = eff_splits(9ll * b.cin, t.splits) > 1 ? 64 : t.bm;
+    const int rows = eff_splits(9ll * b.cin, t.splits) > 1 ? CS_SPLITK_STAT_ROWS : t.bm;
     float* bn = b.bn.data_ptr<float>();
     float* bufs = bufs_.data_ptr<float>();
     ok(cs_bn_finalize(b.stats.data_ptr<float>(), (int)cdiv(M, rows), rows, (int)M, b.cout, P(b.g_off), P(b.be_off),
@@ -229,7 +231,7 @@ void VggEngine::forward_train(int64_t B) {
   // features of the last block were staged in gbuf_[1] (free until the first dgrad); dfeat -> gbuf_[0]
   ok(cs_linear_xent(gbuf_[1].data_ptr<float>(), P(fc_w_), P(fc_b_), ylab_.data_ptr<int64_t>(), (int)B, (int)feat_,
                     (int)ncls_, 1.0f, loss_.data_ptr<float>(), correct_.data_ptr<int>(), logits_.data_ptr<float>(),
-                    G(fc_w_), G(fc_b_), gbuf_[0].data_ptr<float>(), pred_.data_ptr<int64_t>(), s),
+                    G(fc_w_), G(fc_b_), gbuf_[0].data_ptr<float>(), pred_.data_ptr<int64_t>(), head_ws_.data_ptr<float>(), s),
      "linear_xent");
 }
 
@@ -282,7 +284,7 @@ void VggEngine::forward_eval(int64_t B) {
   }
   ok(cs_linear_xent(gbuf_[1].data_ptr<float>(), P(fc_w_), P(fc_b_), ylab_.data_ptr<int64_t>(), (int)B, (int)feat_,
                     (int)ncls_, 1.0f, loss_.data_ptr<float>(), correct_.data_ptr<int>(), logits_.data_ptr<float>(),
-                    nullptr, nullptr, nullptr, pred_.data_ptr<int64_t>(), s),
+                    nullptr, nullptr, nullptr, pred_.data_ptr<int64_t>(), head_ws_.data_ptr<float>(), s),
      "linear_xent");
 }
 
@@ -315,7 +317,7 @@ void VggEngine::step(int64_t B, RcclComm* comm, const std::vector<int64_t>& buck
 
 void VggEngine::set_tile(int64_t block, int64_t mode, int64_t bm, int64_t bn, int64_t splits) {
   TORCH_CHECK(block >= 0 && block < (int64_t)blocks_.size() && mode >= 0 && mode <= 2, "set_tile: index");
-  TORCH_CHECK((bm == 64 || bm == 128) && (bn == 64 || bn == 128) && splits >= 1 && splits <= 64, "set_tile: tile");
+  TORCH_CHECK((bm == 64 || bm == 128) && (bn == 64 || bn == 128) && splits >= 1 && splits <= 1024, "set_tile: tile");
   const Dims d = dims(blocks_[block], (int)mode, Bmax_);
   const int sp = eff_splits(d.K, (int)splits);
   TORCH_CHECK(sp == 1 || (int64_t)sp * d.M * d.N <= ws_elems_, "set_tile: split-K workspace too small");
@@ -346,7 +348,7 @@ std::vector<double> VggEngine::autotune(int64_t B, int64_t iters) {
   ok(hipEventCreate(&e0), "event");
   ok(hipEventCreate(&e1), "event");
   std::vector<double> best_us;
-  const int split_opts[] = {1, 2, 3, 4, 6, 8, 12, 16, 24, 32};
+  const int split_opts[] = {1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 64, 128, 256};
   for (int l = 0; l < (int)blocks_.size(); ++l) {
     for (int mode = 0; mode < 3; ++mode) {
       if (l == 0 && mode == CS_CONV_DGRAD) {

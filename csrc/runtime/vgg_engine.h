@@ -39,7 +39,7 @@ struct VggBlock {
   ConvTile tile[3];
   torch::Tensor x;      // [Bmax, H, H, cin]
   torch::Tensor y;      // [Bmax*H*H, cout]
-  torch::Tensor stats;  // [ceil(Bmax*H*H/64), cout, 2]
+  torch::Tensor stats;  // [ceil(Bmax*H*H/16), cout, 2] BN (mean, M2) partials per row tile
   torch::Tensor bn;     // [4, cout]: scale, shift, mean, invstd
 };
 
@@ -96,7 +96,7 @@ class VggEngine {
   torch::Tensor params_, grads_, mom_, bufs_, nbt_;
   torch::Tensor data_[2], labels_[2], aug_[2];
   torch::Tensor idx_, ylab_, loss_, correct_, logits_, pred_;
-  torch::Tensor gbuf_[2], dz_, ws_, bn_part_, bn_coef_, bn_eval_;
+  torch::Tensor gbuf_[2], dz_, ws_, bn_part_, bn_coef_, bn_eval_, head_ws_;
   int64_t ws_elems_ = 0;
 };
 

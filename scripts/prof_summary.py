@@ -34,6 +34,7 @@ def main():
     p.add_argument("--top", type=int, default=40)
     p.add_argument("--skip-first", type=float, default=0.0, help="drop dispatches in the first X fraction of time")
     p.add_argument("--steps", type=int, default=0, help="divide totals by this many steps")
+    p.add_argument("--timeline", type=int, default=0, help="also print the last N dispatches in order (one step)")
     a = p.parse_args()
     files = [a.path] if os.path.isfile(a.path) else (glob.glob(os.path.join(a.path, "**", "*.db"), recursive=True) or
                                                      glob.glob(os.path.join(a.path, "**", "*kernel_trace.csv"),
@@ -67,6 +68,15 @@ def main():
         m = meta[k]
         print(f"{k[:70]:70s} {e[0]:6d} {e[1]:10.1f} {e[1] / e[0]:9.2f} {e[2]:8.2f} {e[3]:8.2f} {100 * e[1] / total:6.2f}"
               f"  {m['grid']} / {m['wg']} / {m['vgpr']}+{m['agpr']} / {m['lds']}")
+    if a.timeline and rows:
+        tl = rows[-a.timeline:]
+        print(f"\n# timeline of the last {len(tl)} dispatches: start offset / duration / gap to previous end (us)")
+        prev = None
+        for r in tl:
+            gap = (r["start"] - prev) / 1e3 if prev is not None else 0.0
+            print(f"{(r['start'] - tl[0]['start']) / 1e3:9.1f} {(r['end'] - r['start']) / 1e3:8.2f} {gap:7.2f}  "
+                  f"{r['name'][:60]}  {r['grid']}")
+            prev = r["end"]
 
 
 if __name__ == "__main__":

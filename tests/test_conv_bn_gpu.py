@@ -80,7 +80,7 @@ def test_conv_dgrad(dev, shape, tile):
 
 
 @pytest.mark.parametrize("shape", SHAPES)
-@pytest.mark.parametrize("tile", [(64, 64, 1), (64, 64, 8), (128, 128, 4), (128, 64, 2)])
+@pytest.mark.parametrize("tile", [(64, 64, 1), (64, 64, 8), (128, 128, 4), (128, 64, 2), (64, 64, 64)])
 def test_conv_wgrad(dev, shape, tile):
     from cs744_pytorch_distributed_tutorial_amd.ops import functional as Fn
     B, H, cin, cout = shape
