@@ -248,8 +248,8 @@ class NativeTrainer:
             with open(cache) as f:
                 db = json.load(f)
         if key in db:
-            for l, m, bm, bn, sp in db[key]["tiles"]:
-                self.engine.set_tile(l, m, bm, bn, sp)
+            for l, m, bm, bn, sp, bk in db[key]["tiles"]:
+                self.engine.set_tile(l, m, bm, bn, sp, bk)
             self.tune_us = db[key]["us"]
             return
         self.tune_us = list(self.engine.autotune(self.B, 5))
@@ -268,9 +268,9 @@ class NativeTrainer:
             for m in range(3):
                 if l == 0 and m == 1:
                     continue
-                bm, bn, sp = self.engine.get_tile(l, m)
+                bm, bn, sp, bk = self.engine.get_tile(l, m)
                 us = self.tune_us[3 * l + m] if self.tune_us else None
-                out.append({"block": l, "op": names[m], "bm": bm, "bn": bn, "splits": sp, "us": us})
+                out.append({"block": l, "op": names[m], "bm": bm, "bn": bn, "bk": bk, "splits": sp, "us": us})
         return out
 
     # ---------------------------------------------------------------- data

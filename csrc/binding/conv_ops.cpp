@@ -28,11 +28,12 @@ bool pow2(int64_t v) { return v > 0 && (v & (v - 1)) == 0; }
 int64_t conv_gemm(int64_t mode, c10::optional<torch::Tensor> x, c10::optional<torch::Tensor> w,
                   c10::optional<torch::Tensor> dz, c10::optional<torch::Tensor> bias, torch::Tensor out,
                   c10::optional<torch::Tensor> ws, c10::optional<torch::Tensor> stats, int64_t B, int64_t H, int64_t W,
-                  int64_t Cin, int64_t Cout, bool w_oihw, int64_t bm, int64_t bn, int64_t splits) {
+                  int64_t Cin, int64_t Cout, bool w_oihw, int64_t bm, int64_t bn, int64_t splits, int64_t bk) {
   TORCH_CHECK(mode >= 0 && mode <= 2, "conv_gemm: bad mode");
   TORCH_CHECK(pow2(H) && pow2(W) && pow2(Cin) && pow2(Cout) && Cin >= 4 && Cout >= 64 && B > 0,
               "conv_gemm: H, W, Cin, Cout must be powers of two (Cin>=4, Cout>=64)");
-  TORCH_CHECK((bm == 64 || bm == 128) && (bn == 64 || bn == 128) && splits >= 1, "conv_gemm: bad tiling");
+  TORCH_CHECK((bm == 64 || bm == 128) && (bn == 64 || bn == 128) && (bk == 16 || bk == 32) && splits >= 1,
+              "conv_gemm: bad tiling");
   TORCH_CHECK(!w_oihw || Cin == 4, "conv_gemm: OIHW weights only for the padded conv0 (Cin=4)");
   if (mode == CS_CONV_DGRAD) TORCH_CHECK(Cin >= 64 && !w_oihw, "conv_gemm: dgrad needs Cin >= 64");
   const int64_t pix = B * H * W;
@@ -44,7 +45,7 @@ int64_t conv_gemm(int64_t mode, c10::optional<torch::Tensor> x, c10::optional<to
     TORCH_CHECK(x.has_value() && w.has_value(), "conv fwd needs x and w");
     check_t(x, pix * Cin, "x"); check_t(w, wnum, "w"); check_t(bias, Cout, "bias");
     check_t(out, pix * Cout, "out");
-    const int64_t R = std::min<int64_t>(splits, (9 * Cin + 15) / 16) > 1 ? CS_SPLITK_STAT_ROWS : bm;
+    const int64_t R = cs_conv_effective_splits(9 * Cin, bk, splits) > 1 ? CS_SPLITK_STAT_ROWS : bm;
     check_t(stats, ((pix + R - 1) / R) * Cout * 2, "stats");
   } else if (mode == CS_CONV_DGRAD) {
     TORCH_CHECK(dz.has_value() && w.has_value(), "conv dgrad needs dz and w");
@@ -53,8 +54,7 @@ int64_t conv_gemm(int64_t mode, c10::optional<torch::Tensor> x, c10::optional<to
     TORCH_CHECK(dz.has_value() && x.has_value(), "conv wgrad needs dz and x");
     check_t(dz, pix * Cout, "dz"); check_t(x, pix * Cin, "x"); check_t(out, wnum, "out");
   }
-  const int64_t ksteps = (a.K + 15) / 16;
-  const int64_t sp = std::min<int64_t>(splits, ksteps);
+  const int64_t sp = cs_conv_effective_splits(a.K, bk, splits);
   if (sp > 1) {
     TORCH_CHECK(ws.has_value() && ws->defined(), "conv_gemm: split-K needs a workspace");
     check_t(ws, sp * (int64_t)a.M * a.N, "ws");
@@ -62,7 +62,7 @@ int64_t conv_gemm(int64_t mode, c10::optional<torch::Tensor> x, c10::optional<to
   DevGuard g(out.device());
   a.x = cptr(x); a.w = cptr(w); a.dz = cptr(dz); a.bias = cptr(bias);
   a.out = out.data_ptr<float>(); a.ws = mptr(ws); a.stats = mptr(stats);
-  CS_LAUNCH(cs_conv_gemm(a, (int)mode, (int)bm, (int)bn, (int)splits, cur_stream()));
+  CS_LAUNCH(cs_conv_gemm(a, (int)mode, (int)bm, (int)bn, (int)bk, (int)splits, cur_stream()));
   return sp > 1 ? CS_SPLITK_STAT_ROWS : bm;
 }
 
@@ -133,7 +133,10 @@ void bn_bwd(torch::Tensor y, torch::Tensor G, int64_t B, int64_t H, int64_t W, i
 }  // namespace
 
 void register_conv_ops(pybind11::module& m) {
-  m.def("conv_gemm", &conv_gemm, "implicit-GEMM 3x3 conv (mode 0 fwd / 1 dgrad / 2 wgrad), fp32 MFMA");
+  m.def("conv_gemm", &conv_gemm, "implicit-GEMM 3x3 conv (mode 0 fwd / 1 dgrad / 2 wgrad), fp32 MFMA",
+        py::arg("mode"), py::arg("x"), py::arg("w"), py::arg("dz"), py::arg("bias"), py::arg("out"), py::arg("ws"),
+        py::arg("stats"), py::arg("B"), py::arg("H"), py::arg("W"), py::arg("Cin"), py::arg("Cout"),
+        py::arg("w_oihw"), py::arg("bm"), py::arg("bn"), py::arg("splits"), py::arg("bk") = 16);
   m.def("bn_finalize", &bn_finalize);
   m.def("bn_eval_coeffs", &bn_eval_coeffs);
   m.def("bn_apply", &bn_apply);

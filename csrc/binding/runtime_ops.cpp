@@ -142,13 +142,16 @@ void register_runtime(pybind11::module& m) {
       .def("num_blocks", &cs::VggEngine::num_blocks)
       .def("tensor", &cs::VggEngine::tensor)
       .def("forward_train", &cs::VggEngine::forward_train)
-      .def("backward", &cs::VggEngine::backward)
+      .def("backward", &cs::VggEngine::backward, py::arg("hi"), py::arg("lo"), py::arg("B"),
+           py::arg("join") = true)
       .def("sgd", &cs::VggEngine::sgd)
       .def("forward_eval", &cs::VggEngine::forward_eval)
       .def("step", &cs::VggEngine::step, py::arg("B"), py::arg("comm").none(true), py::arg("bucket_blocks"),
            py::arg("bucket_ranges"), py::arg("broadcast_buffers"), py::arg("lr"), py::arg("momentum"),
            py::arg("wd"), py::arg("dampening"))
-      .def("set_tile", &cs::VggEngine::set_tile)
+      .def("set_overlap_wgrad", &cs::VggEngine::set_overlap_wgrad)
+      .def("set_tile", &cs::VggEngine::set_tile, py::arg("block"), py::arg("mode"), py::arg("bm"), py::arg("bn"),
+           py::arg("splits"), py::arg("bk") = 16)
       .def("get_tile", &cs::VggEngine::get_tile)
       .def("autotune", &cs::VggEngine::autotune)
       .def("run_conv", &cs::VggEngine::run_conv);

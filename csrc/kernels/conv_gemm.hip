@@ -7,15 +7,14 @@
 //   DGRAD: dX[M=B*H*W][N=Cin]   = shift(dZ)[M][K=9*Cout] . W        (flipped taps)
 //   WGRAD: dW[M=Cout][N=9*Cin]  = dZ^T[Cout][K=B*H*W] . im2col(X)
 //
-// Tiling: 256 threads = 4 waves (2x2), block tile BMxBN, BK = 16, wave tile
-// (BM/2)x(BN/2) built from 32x32 MFMA tiles. Global -> registers -> LDS double
-// buffer with one barrier per K-step; the next K-step's global loads are issued
-// before the current step's MFMAs so HBM/L2 latency hides under matrix work.
-// K is permuted inside a K-step so each lane's 8 A (and B) values are contiguous
-// in LDS: lane-half h feeds k = 8h + s at MFMA sub-step s (s = 0..7), turning the
-// operand fetch into two ds_read_b128 per tile ([row][16+4] padded rows are
-// bank-conflict free for the ds_read_b128 lane groups), or 8 conflict-free
-// ds_read_b32 for operands that are staged K-major ([k][rows+4]).
+// Tiling: 256 threads = 4 waves (2x2), block tile BMxBN, K-step BK (16 or 32),
+// wave tile (BM/2)x(BN/2) built from 32x32 MFMA tiles. Global -> registers -> LDS
+// double buffer with one barrier per K-step; the next K-step's global loads are
+// issued before the current step's MFMAs so HBM/L2 latency hides under matrix work.
+// K is permuted inside a K-step so each lane's BK/2 A (and B) values are contiguous
+// in LDS: lane-half h feeds k = (BK/2)h + s at MFMA sub-step s, turning the operand
+// fetch into BK/8 ds_read_b128 per tile ([row][BK+4] padded rows), or BK/2
+// conflict-free ds_read_b32 for operands that are staged K-major ([k][rows+4]).
 // Split-K over blockIdx.z writes fp32 slabs that `splitk_reduce` sums in a fixed
 // order (deterministic, no float atomics). Tiles are dealt to XCDs in contiguous
 // ranges (common.h xcd_remap) so neighbouring tiles share an L2.
@@ -25,7 +24,6 @@
 namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
-constexpr int BK = 16;
 
 __device__ __forceinline__ void pix_decode(int p, const CsConvArgs& a, int& b, int& h, int& w) {
   w = p & (a.W - 1);
@@ -48,20 +46,22 @@ struct Traits<CS_CONV_WGRAD> {
   static constexpr bool A_KC = false, B_KC = false;
 };
 
-template <int BM, int BN, int MODE>
+template <int BM, int BN, int MODE, int BK>
 struct Tile {
   static constexpr bool A_KC = Traits<MODE>::A_KC, B_KC = Traits<MODE>::B_KC;
   static constexpr int A_ELEMS = A_KC ? BM * (BK + 4) : BK * (BM + 4);
   static constexpr int B_ELEMS = B_KC ? BN * (BK + 4) : BK * (BN + 4);
   static constexpr int STAGE = A_ELEMS + B_ELEMS;
-  static constexpr int AC = BM / 64;  // float4 chunks per thread per stage
-  static constexpr int BC = BN / 64;
+  static constexpr int AC = BM * BK / 1024;  // float4 chunks per thread per stage
+  static constexpr int BC = BN * BK / 1024;
+  static constexpr int KQ = BK / 4;          // float4 chunks per K-contiguous row
+  static constexpr int HK = BK / 2;          // MFMA sub-steps per K-step
   static constexpr int WM = BM / 2, WN = BN / 2, RM = WM / 32, RN = WN / 32;
 };
 
-template <int BM, int BN, int MODE>
+template <int BM, int BN, int MODE, int BK>
 struct Loader {
-  using T = Tile<BM, BN, MODE>;
+  using T = Tile<BM, BN, MODE, BK>;
   // per-thread precomputed row info for K-contiguous A rows (FWD/DGRAD: pixel rows)
   int a_b[T::AC], a_h[T::AC], a_w[T::AC];
   bool a_ok[T::AC];
@@ -71,7 +71,7 @@ struct Loader {
     if constexpr (T::A_KC) {
 #pragma unroll
       for (int i = 0; i < T::AC; ++i) {
-        const int q = threadIdx.x + 256 * i, row = q >> 2, m = m0 + row;
+        const int q = threadIdx.x + 256 * i, row = q / T::KQ, m = m0 + row;
         a_ok[i] = m < a.M;
         pix_decode(a_ok[i] ? m : 0, a, a_b[i], a_h[i], a_w[i]);
       }
@@ -86,7 +86,7 @@ struct Loader {
       const int q = threadIdx.x + 256 * i;
       float4 v = z4;
       if constexpr (MODE == CS_CONV_FWD || MODE == CS_CONV_DGRAD) {
-        const int c = q & 3, kk = k0 + 4 * c;
+        const int c = q % T::KQ, kk = k0 + 4 * c;
         const int lgC = (MODE == CS_CONV_FWD) ? a.lgCin : a.lgCout;
         const int tap = kk >> lgC, ch = kk & ((1 << lgC) - 1);
         if (a_ok[i] && tap < 9) {
@@ -112,7 +112,7 @@ struct Loader {
       const int q = threadIdx.x + 256 * i;
       float4 v = z4;
       if constexpr (MODE == CS_CONV_FWD) {
-        const int row = q >> 2, c = q & 3, n = n0 + row, kk = k0 + 4 * c;
+        const int row = q / T::KQ, c = q % T::KQ, n = n0 + row, kk = k0 + 4 * c;
         if (n < a.N && kk < a.K) {
           if (!a.w_oihw) {
             v = *reinterpret_cast<const float4*>(a.w + (size_t)n * a.K + kk);
@@ -149,7 +149,7 @@ struct Loader {
     for (int i = 0; i < T::AC; ++i) {
       const int q = threadIdx.x + 256 * i;
       if constexpr (T::A_KC) {
-        *reinterpret_cast<float4*>(As + (q >> 2) * (BK + 4) + 4 * (q & 3)) = ra[i];
+        *reinterpret_cast<float4*>(As + (q / T::KQ) * (BK + 4) + 4 * (q % T::KQ)) = ra[i];
       } else {
         constexpr int CPR = BM / 4;
         const int kr = q / CPR, c = q - kr * CPR;
@@ -160,7 +160,7 @@ struct Loader {
     for (int i = 0; i < T::BC; ++i) {
       const int q = threadIdx.x + 256 * i;
       if constexpr (T::B_KC) {
-        *reinterpret_cast<float4*>(Bs + (q >> 2) * (BK + 4) + 4 * (q & 3)) = rb[i];
+        *reinterpret_cast<float4*>(Bs + (q / T::KQ) * (BK + 4) + 4 * (q % T::KQ)) = rb[i];
       } else {
         constexpr int CPR = BN / 4;
         const int kr = q / CPR, c = q - kr * CPR;
@@ -170,9 +170,9 @@ struct Loader {
   }
 };
 
-template <int BM, int BN, int MODE>
+template <int BM, int BN, int MODE, int BK>
 __global__ __launch_bounds__(256) void conv_gemm_kernel(CsConvArgs a) {
-  using T = Tile<BM, BN, MODE>;
+  using T = Tile<BM, BN, MODE, BK>;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int ntn = (a.N + BN - 1) / BN;
   const int ntiles = ((a.M + BM - 1) / BM) * ntn;
@@ -195,7 +195,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(CsConvArgs a) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
-  Loader<BM, BN, MODE> ld;
+  Loader<BM, BN, MODE, BK> ld;
   ld.init(a, m0);
   float* stage0 = smem;
   float* stage1 = smem + T::STAGE;
@@ -210,35 +210,37 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(CsConvArgs a) {
     if (more) ld.load(a, m0, n0, (ks + 1) * BK);
     const float* As = cur ? stage1 : stage0;
     const float* Bs = As + T::A_ELEMS;
-    float af[T::RM][8], bf[T::RN][8];
+    float af[T::RM][T::HK], bf[T::RN][T::HK];
 #pragma unroll
     for (int i = 0; i < T::RM; ++i) {
       const int row = wm * T::WM + i * 32 + r;
       if constexpr (T::A_KC) {
-        const float4 lo = *reinterpret_cast<const float4*>(As + row * (BK + 4) + 8 * hh);
-        const float4 hi = *reinterpret_cast<const float4*>(As + row * (BK + 4) + 8 * hh + 4);
-        af[i][0] = lo.x; af[i][1] = lo.y; af[i][2] = lo.z; af[i][3] = lo.w;
-        af[i][4] = hi.x; af[i][5] = hi.y; af[i][6] = hi.z; af[i][7] = hi.w;
+#pragma unroll
+        for (int c4 = 0; c4 < T::HK / 4; ++c4) {
+          const float4 v = *reinterpret_cast<const float4*>(As + row * (BK + 4) + T::HK * hh + 4 * c4);
+          af[i][4 * c4 + 0] = v.x; af[i][4 * c4 + 1] = v.y; af[i][4 * c4 + 2] = v.z; af[i][4 * c4 + 3] = v.w;
+        }
       } else {
 #pragma unroll
-        for (int s = 0; s < 8; ++s) af[i][s] = As[(8 * hh + s) * (BM + 4) + row];
+        for (int s = 0; s < T::HK; ++s) af[i][s] = As[(T::HK * hh + s) * (BM + 4) + row];
       }
     }
 #pragma unroll
     for (int j = 0; j < T::RN; ++j) {
       const int col = wn * T::WN + j * 32 + r;
       if constexpr (T::B_KC) {
-        const float4 lo = *reinterpret_cast<const float4*>(Bs + col * (BK + 4) + 8 * hh);
-        const float4 hi = *reinterpret_cast<const float4*>(Bs + col * (BK + 4) + 8 * hh + 4);
-        bf[j][0] = lo.x; bf[j][1] = lo.y; bf[j][2] = lo.z; bf[j][3] = lo.w;
-        bf[j][4] = hi.x; bf[j][5] = hi.y; bf[j][6] = hi.z; bf[j][7] = hi.w;
+#pragma unroll
+        for (int c4 = 0; c4 < T::HK / 4; ++c4) {
+          const float4 v = *reinterpret_cast<const float4*>(Bs + col * (BK + 4) + T::HK * hh + 4 * c4);
+          bf[j][4 * c4 + 0] = v.x; bf[j][4 * c4 + 1] = v.y; bf[j][4 * c4 + 2] = v.z; bf[j][4 * c4 + 3] = v.w;
+        }
       } else {
 #pragma unroll
-        for (int s = 0; s < 8; ++s) bf[j][s] = Bs[(8 * hh + s) * (BN + 4) + col];
+        for (int s = 0; s < T::HK; ++s) bf[j][s] = Bs[(T::HK * hh + s) * (BN + 4) + col];
       }
     }
 #pragma unroll
-    for (int s = 0; s < 8; ++s)
+    for (int s = 0; s < T::HK; ++s)
 #pragma unroll
       for (int i = 0; i < T::RM; ++i)
 #pragma unroll
@@ -467,12 +469,12 @@ hipError_t launch_reduce(const CsConvArgs& a, int mode, int splits, hipStream_t 
   return hipGetLastError();
 }
 
-template <int BM, int BN, int MODE>
+template <int BM, int BN, int MODE, int BK>
 hipError_t launch_gemm(const CsConvArgs& a, int splits, hipStream_t stream) {
-  using T = Tile<BM, BN, MODE>;
+  using T = Tile<BM, BN, MODE, BK>;
   const int ntiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
   const size_t lds = 2 * T::STAGE * sizeof(float);
-  hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, MODE>), dim3(ntiles, 1, splits), dim3(256), lds, stream, a);
+  hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, MODE, BK>), dim3(ntiles, 1, splits), dim3(256), lds, stream, a);
   return hipGetLastError();
 }
 
@@ -507,27 +509,37 @@ void cs_conv_fill_dims(CsConvArgs* a, int mode) {
   }
 }
 
-hipError_t cs_conv_gemm(CsConvArgs a, int mode, int bm, int bn, int splits, hipStream_t stream) {
+int cs_conv_effective_splits(int K, int bk, int splits) {
+  const int ks = (K + bk - 1) / bk;
+  int s = splits < 1 ? 1 : (splits > ks ? ks : splits);
+  const int per = (ks + s - 1) / s;
+  return (ks + per - 1) / per;
+}
+
+hipError_t cs_conv_gemm(CsConvArgs a, int mode, int bm, int bn, int bk, int splits, hipStream_t stream) {
+  if (bk != 16 && bk != 32) return hipErrorInvalidValue;
   cs_conv_fill_dims(&a, mode);
-  a.total_ksteps = (a.K + BK - 1) / BK;
-  if (splits < 1) splits = 1;
-  if (splits > a.total_ksteps) splits = a.total_ksteps;
+  a.total_ksteps = (a.K + bk - 1) / bk;
+  splits = cs_conv_effective_splits(a.K, bk, splits);
   a.ksteps_per_split = (a.total_ksteps + splits - 1) / splits;
-  splits = (a.total_ksteps + a.ksteps_per_split - 1) / a.ksteps_per_split;
   if (splits > 1 && a.ws == nullptr) return hipErrorInvalidValue;
-#define CS_DISPATCH(BM_, BN_)                                                   \
-  if (bm == BM_ && bn == BN_) {                                                 \
-    hipError_t e;                                                               \
-    if (mode == CS_CONV_FWD) e = launch_gemm<BM_, BN_, CS_CONV_FWD>(a, splits, stream);          \
-    else if (mode == CS_CONV_DGRAD) e = launch_gemm<BM_, BN_, CS_CONV_DGRAD>(a, splits, stream); \
-    else e = launch_gemm<BM_, BN_, CS_CONV_WGRAD>(a, splits, stream);                            \
-    if (e != hipSuccess || splits == 1) return e;                               \
-    return launch_reduce(a, mode, splits, stream);                              \
+#define CS_DISPATCH(BM_, BN_, BK_)                                                                       \
+  if (bm == BM_ && bn == BN_ && bk == BK_) {                                                             \
+    hipError_t e;                                                                                        \
+    if (mode == CS_CONV_FWD) e = launch_gemm<BM_, BN_, CS_CONV_FWD, BK_>(a, splits, stream);            \
+    else if (mode == CS_CONV_DGRAD) e = launch_gemm<BM_, BN_, CS_CONV_DGRAD, BK_>(a, splits, stream);   \
+    else e = launch_gemm<BM_, BN_, CS_CONV_WGRAD, BK_>(a, splits, stream);                              \
+    if (e != hipSuccess || splits == 1) return e;                                                        \
+    return launch_reduce(a, mode, splits, stream);                                                       \
   }
-  CS_DISPATCH(64, 64)
-  CS_DISPATCH(128, 64)
-  CS_DISPATCH(64, 128)
-  CS_DISPATCH(128, 128)
+  CS_DISPATCH(64, 64, 16)
+  CS_DISPATCH(128, 64, 16)
+  CS_DISPATCH(64, 128, 16)
+  CS_DISPATCH(128, 128, 16)
+  CS_DISPATCH(64, 64, 32)
+  CS_DISPATCH(128, 64, 32)
+  CS_DISPATCH(64, 128, 32)
+  CS_DISPATCH(128, 128, 32)
 #undef CS_DISPATCH
   return hipErrorInvalidValue;
 }

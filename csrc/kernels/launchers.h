@@ -48,10 +48,12 @@ struct CsConvArgs {
 };
 
 void cs_conv_fill_dims(CsConvArgs* a, int mode);
-// bm, bn in {64, 128}; splits >= 1 (split-K over blockIdx.z + deterministic reduce).
+// bm, bn in {64, 128}; bk in {16, 32}; splits >= 1 (split-K over blockIdx.z + deterministic reduce).
 // FWD stats tiles have `bm` rows when splits == 1 and CS_SPLITK_STAT_ROWS rows otherwise.
 #define CS_SPLITK_STAT_ROWS 16
-hipError_t cs_conv_gemm(CsConvArgs a, int mode, int bm, int bn, int splits, hipStream_t stream);
+hipError_t cs_conv_gemm(CsConvArgs a, int mode, int bm, int bn, int bk, int splits, hipStream_t stream);
+// the split count cs_conv_gemm actually launches (K-steps re-balanced over splits)
+int cs_conv_effective_splits(int K, int bk, int splits);
 
 // ---------------------------------------------------------------- BatchNorm + ReLU (+ 2x2 max-pool), NHWC
 hipError_t cs_bn_finalize(const float* part, int T, int R, int M, int C, const float* gamma, const float* beta,

@@ -136,29 +136,38 @@ __global__ __launch_bounds__(256) void head_rows_kernel(const float* __restrict_
   }
 }
 
-// Column pass: block j < C computes dW[j][:] = sum_b dl[b][j] feat[b][:]; the last block
+// Column pass: blocks [0, C*ceil(K/64)) compute dW[j][k] = sum_b dl[b][j] feat[b][k] for one j and
+// 64 consecutive k (one wave, lane = k, b-loop unrolled so the loads pipeline); the last block
 // computes db and the batch loss / correct count (fixed summation order: deterministic).
-__global__ __launch_bounds__(256) void head_cols_kernel(const float* __restrict__ feat, int B, int K, int C,
-                                                        const float* __restrict__ ws, float* __restrict__ dW,
-                                                        float* __restrict__ db, float* __restrict__ loss_out,
-                                                        int* __restrict__ correct_out) {
+__global__ __launch_bounds__(64) void head_cols_kernel(const float* __restrict__ feat, int B, int K, int C,
+                                                       const float* __restrict__ ws, float* __restrict__ dW,
+                                                       float* __restrict__ db, float* __restrict__ loss_out,
+                                                       int* __restrict__ correct_out) {
   __shared__ float red[16];
   const float* dl = ws;
   const float* rowloss = ws + (size_t)B * C;
   const float* rowcorr = rowloss + B;
-  const int j = blockIdx.x;
-  if (dW != nullptr && j < C) {
-    for (int k = threadIdx.x; k < K; k += blockDim.x) {
-      float s = 0.f;
-      for (int b = 0; b < B; ++b) s += dl[(size_t)b * C + j] * feat[(size_t)b * K + k];
-      dW[(size_t)j * K + k] = s;
+  const int nkc = (K + 63) / 64;
+  const int bid = blockIdx.x;
+  if (dW != nullptr && bid < C * nkc) {
+    const int j = bid / nkc, k = (bid - j * nkc) * 64 + threadIdx.x;
+    if (k >= K) return;
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    int b = 0;
+    for (; b + 4 <= B; b += 4) {
+      s0 += dl[(size_t)b * C + j] * feat[(size_t)b * K + k];
+      s1 += dl[(size_t)(b + 1) * C + j] * feat[(size_t)(b + 1) * K + k];
+      s2 += dl[(size_t)(b + 2) * C + j] * feat[(size_t)(b + 2) * K + k];
+      s3 += dl[(size_t)(b + 3) * C + j] * feat[(size_t)(b + 3) * K + k];
     }
+    for (; b < B; ++b) s0 += dl[(size_t)b * C + j] * feat[(size_t)b * K + k];
+    dW[(size_t)j * K + k] = (s0 + s1) + (s2 + s3);
     return;
   }
   float l = 0.f, c = 0.f;
-  for (int b = threadIdx.x; b < B; b += blockDim.x) {
-    l += rowloss[b];
-    c += rowcorr[b];
+  for (int r = threadIdx.x; r < B; r += blockDim.x) {
+    l += rowloss[r];
+    c += rowcorr[r];
   }
   l = cs::block_sum(l, red);
   c = cs::block_sum(c, red);
@@ -167,9 +176,9 @@ __global__ __launch_bounds__(256) void head_cols_kernel(const float* __restrict_
     if (correct_out) *correct_out = (int)(c + 0.5f);
   }
   if (db != nullptr && threadIdx.x < (unsigned)C) {
-    float s = 0.f;
-    for (int b = 0; b < B; ++b) s += dl[(size_t)b * C + threadIdx.x];
-    db[threadIdx.x] = s;
+    float acc = 0.f;
+    for (int r = 0; r < B; ++r) acc += dl[(size_t)r * C + threadIdx.x];
+    db[threadIdx.x] = acc;
   }
 }
 
@@ -191,7 +200,7 @@ hipError_t cs_linear_xent(const float* feat, const float* W, const float* bias, 
   hipLaunchKernelGGL(head_rows_kernel, dim3((B + 3) / 4), dim3(256), 0, stream, feat, W, bias, labels, B, K, C,
                      gscale, ws, logits_out, pred_out, dfeat);
   const bool bwd = dW != nullptr && db != nullptr && dfeat != nullptr;
-  hipLaunchKernelGGL(head_cols_kernel, dim3(bwd ? C + 1 : 1), dim3(256), 0, stream, feat, B, K, C, ws,
+  hipLaunchKernelGGL(head_cols_kernel, dim3(bwd ? C * ((K + 63) / 64) + 1 : 1), dim3(64), 0, stream, feat, B, K, C, ws,
                      bwd ? dW : nullptr, bwd ? db : nullptr, loss_out, correct_out);
   return hipGetLastError();
 }

@@ -35,12 +35,7 @@ Dims dims(const VggBlock& b, int mode, int64_t B) {
 }
 
 // the split count cs_conv_gemm will actually use (it re-balances K-steps per split)
-int eff_splits(int64_t K, int splits) {
-  const int64_t ks = cdiv(K, 16);
-  int64_t s = std::max<int64_t>(1, std::min<int64_t>(splits, ks));
-  const int64_t per = cdiv(ks, s);
-  return (int)cdiv(ks, per);
-}
+int eff_splits(int64_t K, int splits, int bk) { return cs_conv_effective_splits((int)K, bk, splits); }
 
 // default tile before autotune: ~2 waves of 256 CUs, >= 8 K-steps per split
 ConvTile default_tile(const VggBlock& b, int mode, int64_t B) {
@@ -52,6 +47,7 @@ ConvTile default_tile(const VggBlock& b, int mode, int64_t B) {
   const int64_t ks = cdiv(d.K, 16);
   int s = 1;
   while (tiles * s < 512 && ks / (2 * s) >= 8 && (2 * s) * d.M * d.N <= kWsElems) s *= 2;
+  t.bk = 16;
   t.splits = s;
   return t;
 }
@@ -131,9 +127,18 @@ VggEngine::VggEngine(int64_t Bmax, std::vector<int64_t> desc, std::vector<int64_
   logits_ = torch::zeros({Bmax, ncls}, fo);
   gbuf_[0] = torch::zeros({gmax}, fo);
   gbuf_[1] = torch::zeros({gmax}, fo);
-  dz_ = torch::zeros({dzmax}, fo);
+  dz_[0] = torch::zeros({dzmax}, fo);
+  dz_[1] = torch::zeros({dzmax}, fo);
   ws_elems_ = kWsElems;
   ws_ = torch::zeros({ws_elems_}, fo);
+  ws_side_ = torch::zeros({ws_elems_}, fo);
+  ok(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking), "side stream");
+  ev_bn_.resize(L);
+  ev_wg_.resize(L);
+  for (int64_t l = 0; l < L; ++l) {
+    ok(hipEventCreateWithFlags(&ev_bn_[l], hipEventDisableTiming), "event");
+    ok(hipEventCreateWithFlags(&ev_wg_[l], hipEventDisableTiming), "event");
+  }
   bn_part_ = torch::zeros({partmax}, fo);
   bn_coef_ = torch::zeros({cmax * 3}, fo);
   bn_eval_ = torch::zeros({2, cmax}, fo);
@@ -144,7 +149,7 @@ VggEngine::VggEngine(int64_t Bmax, std::vector<int64_t> desc, std::vector<int64_
 torch::Tensor VggEngine::tensor(int64_t block, const std::string& name) const {
   if (name == "g0") return gbuf_[0];
   if (name == "g1") return gbuf_[1];
-  if (name == "dz") return dz_;
+  if (name == "dz") return dz_[block & 1];
   TORCH_CHECK(block >= 0 && block < (int64_t)blocks_.size(), "tensor: block index");
   const VggBlock& b = blocks_[block];
   if (name == "x") return b.x;
@@ -170,7 +175,8 @@ void VggEngine::set_data(int64_t slot, torch::Tensor data, torch::Tensor labels,
   aug_[slot] = aug;
 }
 
-void VggEngine::conv(int l, int mode, int B, const ConvTile& t, hipStream_t s, bool with_stats) {
+void VggEngine::conv(int l, int mode, int B, const ConvTile& t, hipStream_t s, bool with_stats, float* ws,
+                     float* dz) {
   VggBlock& b = blocks_[l];
   const int L = (int)blocks_.size();
   CsConvArgs a{};
@@ -180,9 +186,10 @@ void VggEngine::conv(int l, int mode, int B, const ConvTile& t, hipStream_t s, b
   a.Cin = b.cin;
   a.Cout = b.cout;
   a.w_oihw = (l == 0 && b.cin == 4) ? 1 : 0;
-  a.ws = ws_.data_ptr<float>();
+  a.ws = ws != nullptr ? ws : ws_.data_ptr<float>();
+  if (dz == nullptr) dz = dz_[0].data_ptr<float>();
   const Dims d = dims(b, mode, B);
-  const int sp = eff_splits(d.K, t.splits);
+  const int sp = eff_splits(d.K, t.splits, t.bk);
   TORCH_CHECK(sp == 1 || (int64_t)sp * d.M * d.N <= ws_elems_, "VggEngine: split-K workspace too small");
   if (mode == CS_CONV_FWD) {
     a.x = b.x.data_ptr<float>();
@@ -192,15 +199,15 @@ void VggEngine::conv(int l, int mode, int B, const ConvTile& t, hipStream_t s, b
     a.stats = with_stats ? b.stats.data_ptr<float>() : nullptr;
   } else if (mode == CS_CONV_DGRAD) {
     TORCH_CHECK(l > 0, "VggEngine: no dgrad for block 0");
-    a.dz = dz_.data_ptr<float>();
+    a.dz = dz;
     a.w = P(b.w_off);
     a.out = gbuf_[(L - l) % 2].data_ptr<float>();
   } else {
     a.x = b.x.data_ptr<float>();
-    a.dz = dz_.data_ptr<float>();
+    a.dz = dz;
     a.out = G(b.w_off);
   }
-  ok(cs_conv_gemm(a, mode, t.bm, t.bn, t.splits, s), "conv_gemm");
+  ok(cs_conv_gemm(a, mode, t.bm, t.bn, t.bk, t.splits, s), "conv_gemm");
 }
 
 void VggEngine::forward_train(int64_t B) {
@@ -218,7 +225,7 @@ void VggEngine::forward_train(int64_t B) {
     const ConvTile& t = b.tile[CS_CONV_FWD];
     conv(l, CS_CONV_FWD, (int)B, t, s, true);
     const int64_t M = B * b.H * b.H;
-    const int rows = eff_splits(9ll * b.cin, t.splits) > 1 ? CS_SPLITK_STAT_ROWS : t.bm;
+    const int rows = eff_splits(9ll * b.cin, t.splits, t.bk) > 1 ? CS_SPLITK_STAT_ROWS : t.bm;
     float* bn = b.bn.data_ptr<float>();
     float* bufs = bufs_.data_ptr<float>();
     ok(cs_bn_finalize(b.stats.data_ptr<float>(), (int)cdiv(M, rows), rows, (int)M, b.cout, P(b.g_off), P(b.be_off),
@@ -235,7 +242,7 @@ void VggEngine::forward_train(int64_t B) {
      "linear_xent");
 }
 
-void VggEngine::backward(int64_t hi, int64_t lo, int64_t B) {
+void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
   const int L = (int)blocks_.size();
   TORCH_CHECK(0 <= lo && lo <= hi && hi < L, "backward: need 0 <= lo <= hi < num_blocks");
   TORCH_CHECK(B > 0 && B <= Bmax_, "backward: 0 < B <= Bmax");
@@ -243,13 +250,34 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B) {
   for (int l = (int)hi; l >= (int)lo; --l) {
     VggBlock& b = blocks_[l];
     float* bn = b.bn.data_ptr<float>();
+    float* dz = dz_[l & 1].data_ptr<float>();
+    // WAR: block l+2's weight-gradient GEMM (side stream) reads the same dz buffer; it may
+    // belong to an earlier backward() call of this step that did not join (bucketed step)
+    if (overlap_wgrad_ && l + 2 < L) ok(hipStreamWaitEvent(s, ev_wg_[l + 2], 0), "wait wgrad");
     ok(cs_bn_bwd(b.y.data_ptr<float>(), gbuf_[(L - 1 - l) % 2].data_ptr<float>(), (int)B, b.H, b.H, b.cout, b.pool,
                  bn, bn + b.cout, bn + 2 * b.cout, bn + 3 * b.cout, P(b.g_off), bn_part_.data_ptr<float>(),
-                 bn_coef_.data_ptr<float>(), G(b.g_off), G(b.be_off), G(b.b_off), dz_.data_ptr<float>(), s),
+                 bn_coef_.data_ptr<float>(), G(b.g_off), G(b.be_off), G(b.b_off), dz, s),
        "bn_bwd");
-    conv(l, CS_CONV_WGRAD, (int)B, b.tile[CS_CONV_WGRAD], s, false);
-    if (l > 0) conv(l, CS_CONV_DGRAD, (int)B, b.tile[CS_CONV_DGRAD], s, false);
+    if (overlap_wgrad_) {
+      ok(hipEventRecord(ev_bn_[l], s), "record bn");
+      ok(hipStreamWaitEvent(side_, ev_bn_[l], 0), "side wait");
+      conv(l, CS_CONV_WGRAD, (int)B, b.tile[CS_CONV_WGRAD], side_, false, ws_side_.data_ptr<float>(), dz);
+      ok(hipEventRecord(ev_wg_[l], side_), "record wgrad");
+    } else {
+      conv(l, CS_CONV_WGRAD, (int)B, b.tile[CS_CONV_WGRAD], s, false, ws_side_.data_ptr<float>(), dz);
+    }
+    if (l > 0) conv(l, CS_CONV_DGRAD, (int)B, b.tile[CS_CONV_DGRAD], s, false, nullptr, dz);
   }
+  if (join && overlap_wgrad_) ok(hipStreamWaitEvent(s, ev_wg_[lo], 0), "join side");
+}
+
+VggEngine::~VggEngine() {
+  if (side_ != nullptr) {
+    hipStreamSynchronize(side_);
+    hipStreamDestroy(side_);
+  }
+  for (auto e : ev_bn_) hipEventDestroy(e);
+  for (auto e : ev_wg_) hipEventDestroy(e);
 }
 
 void VggEngine::sgd(double lr, double momentum, double wd, double dampening, int64_t off, int64_t n) {
@@ -306,32 +334,38 @@ void VggEngine::step(int64_t B, RcclComm* comm, const std::vector<int64_t>& buck
   for (size_t k = 0; k < nb; ++k) {
     const int64_t lo = bucket_blocks[k];
     TORCH_CHECK(lo <= hi, "step: bucket blocks must decrease");
-    backward(hi, lo, B);
+    backward(hi, lo, B, /*join=*/false);
     hi = lo - 1;
+    // a bucket is complete once its last weight-gradient GEMM (side stream) is: fork the
+    // all-reduce from there, so it overlaps the rest of the backward on the main stream
     if (comm != nullptr && comm->world() > 1)
-      comm->all_reduce(G(bucket_ranges[2 * k]), bucket_ranges[2 * k + 1], ncclFloat32, ncclAvg, s);
+      comm->all_reduce(G(bucket_ranges[2 * k]), bucket_ranges[2 * k + 1], ncclFloat32, ncclAvg,
+                       overlap_wgrad_ ? side_ : s);
   }
+  if (overlap_wgrad_) ok(hipStreamWaitEvent(s, ev_wg_[0], 0), "join side");
   if (comm != nullptr && comm->world() > 1) comm->join(s);
   sgd(lr, momentum, wd, dampening, 0, params_.numel());
 }
 
-void VggEngine::set_tile(int64_t block, int64_t mode, int64_t bm, int64_t bn, int64_t splits) {
+void VggEngine::set_tile(int64_t block, int64_t mode, int64_t bm, int64_t bn, int64_t splits, int64_t bk) {
   TORCH_CHECK(block >= 0 && block < (int64_t)blocks_.size() && mode >= 0 && mode <= 2, "set_tile: index");
   TORCH_CHECK((bm == 64 || bm == 128) && (bn == 64 || bn == 128) && splits >= 1 && splits <= 1024, "set_tile: tile");
   const Dims d = dims(blocks_[block], (int)mode, Bmax_);
-  const int sp = eff_splits(d.K, (int)splits);
+  TORCH_CHECK(bk == 16 || bk == 32, "set_tile: bk must be 16 or 32");
+  const int sp = eff_splits(d.K, (int)splits, (int)bk);
   TORCH_CHECK(sp == 1 || (int64_t)sp * d.M * d.N <= ws_elems_, "set_tile: split-K workspace too small");
   ConvTile& t = blocks_[block].tile[mode];
   t.bm = (int)bm;
   t.bn = (int)bn;
   t.splits = (int)splits;
+  t.bk = (int)bk;
   t.us = -1.f;
 }
 
 std::vector<int64_t> VggEngine::get_tile(int64_t block, int64_t mode) const {
   TORCH_CHECK(block >= 0 && block < (int64_t)blocks_.size() && mode >= 0 && mode <= 2, "get_tile: index");
   const ConvTile& t = blocks_[block].tile[mode];
-  return {t.bm, t.bn, t.splits};
+  return {t.bm, t.bn, t.splits, t.bk};
 }
 
 void VggEngine::run_conv(int64_t block, int64_t mode, int64_t B) {
@@ -356,34 +390,37 @@ std::vector<double> VggEngine::autotune(int64_t B, int64_t iters) {
         continue;
       }
       const Dims d = dims(blocks_[l], mode, B);
-      const int64_t ks = cdiv(d.K, 16);
       ConvTile best = blocks_[l].tile[mode];
       float best_t = 1e30f;
       std::vector<std::vector<int>> seen;
-      for (int bm : {64, 128}) {
-        for (int bn : {64, 128}) {
-          for (int sp : split_opts) {
-            if (sp > 1 && ks / sp < 3) continue;
-            const int e = eff_splits(d.K, sp);
-            if (e > 1 && (int64_t)e * d.M * d.N > ws_elems_) continue;
-            std::vector<int> key = {bm, bn, e};
-            if (std::find(seen.begin(), seen.end(), key) != seen.end()) continue;
-            seen.push_back(key);
-            ConvTile t;
-            t.bm = bm;
-            t.bn = bn;
-            t.splits = sp;
-            conv(l, mode, (int)B, t, s, mode == CS_CONV_FWD);  // warm
-            ok(hipEventRecord(e0, s), "record");
-            for (int64_t i = 0; i < iters; ++i) conv(l, mode, (int)B, t, s, mode == CS_CONV_FWD);
-            ok(hipEventRecord(e1, s), "record");
-            ok(hipEventSynchronize(e1), "sync");
-            float ms = 0.f;
-            ok(hipEventElapsedTime(&ms, e0, e1), "elapsed");
-            const float us = 1000.f * ms / (float)iters;
-            if (us < best_t) {
-              best_t = us;
-              best = t;
+      for (int bk : {16, 32}) {
+        const int64_t ks = cdiv(d.K, bk);
+        for (int bm : {64, 128}) {
+          for (int bn : {64, 128}) {
+            for (int sp : split_opts) {
+              if (sp > 1 && ks / sp < 2) continue;
+              const int e = eff_splits(d.K, sp, bk);
+              if (e > 1 && (int64_t)e * d.M * d.N > ws_elems_) continue;
+              std::vector<int> key = {bm, bn, bk, e};
+              if (std::find(seen.begin(), seen.end(), key) != seen.end()) continue;
+              seen.push_back(key);
+              ConvTile t;
+              t.bm = bm;
+              t.bn = bn;
+              t.bk = bk;
+              t.splits = sp;
+              conv(l, mode, (int)B, t, s, mode == CS_CONV_FWD);  // warm
+              ok(hipEventRecord(e0, s), "record");
+              for (int64_t i = 0; i < iters; ++i) conv(l, mode, (int)B, t, s, mode == CS_CONV_FWD);
+              ok(hipEventRecord(e1, s), "record");
+              ok(hipEventSynchronize(e1), "sync");
+              float ms = 0.f;
+              ok(hipEventElapsedTime(&ms, e0, e1), "elapsed");
+              const float us = 1000.f * ms / (float)iters;
+              if (us < best_t) {
+                best_t = us;
+                best = t;
+              }
             }
           }
         }

@@ -29,7 +29,7 @@
 namespace cs {
 
 struct ConvTile {
-  int bm = 64, bn = 64, splits = 1;
+  int bm = 64, bn = 64, splits = 1, bk = 16;
   float us = -1.f;  // measured time of the chosen config (autotune), -1 = untuned
 };
 
@@ -64,8 +64,15 @@ class VggEngine {
 
   // augment + conv/BN/ReLU/pool chain + fused linear/xent fwd+bwd (train) for B <= Bmax samples
   void forward_train(int64_t B);
-  // backward of blocks hi..lo (inclusive, hi >= lo), writing their gradients into `grads`
-  void backward(int64_t hi, int64_t lo, int64_t B);
+  // backward of blocks hi..lo (inclusive, hi >= lo), writing their gradients into `grads`.
+  // With overlap_wgrad the weight-gradient GEMM of a block runs on a side stream
+  // concurrently with its data-gradient GEMM (they only share read-only inputs); join =
+  // true makes the caller's stream wait for the side stream before returning. Off by
+  // default: measured on MI355X at B=64 both split-K GEMMs already fill the 256 CUs, so
+  // running them together only shares CUs, and each cross-stream event wait inside the
+  // graph cost a 10-20 us bubble (1.16 -> 1.26 ms/step).
+  void backward(int64_t hi, int64_t lo, int64_t B, bool join = true);
+  void set_overlap_wgrad(bool on) { overlap_wgrad_ = on; }
   // SGD (momentum, weight decay, dampening) on [off, off+n) of the flat buffers
   void sgd(double lr, double momentum, double wd, double dampening, int64_t off, int64_t n);
   // eval forward (running stats): loss (mean over the batch) -> loss(), correct count -> correct()
@@ -79,15 +86,18 @@ class VggEngine {
             double wd, double dampening);
 
   // conv tile control: mode 0 fwd / 1 dgrad / 2 wgrad
-  void set_tile(int64_t block, int64_t mode, int64_t bm, int64_t bn, int64_t splits);
+  void set_tile(int64_t block, int64_t mode, int64_t bm, int64_t bn, int64_t splits, int64_t bk = 16);
+  // -> {bm, bn, splits, bk}
   std::vector<int64_t> get_tile(int64_t block, int64_t mode) const;
-  // time every candidate (bm, bn in {64,128}, split-K) per (block, mode) with HIP events and keep the fastest
+  // time every candidate (bm, bn in {64,128}, bk in {16,32}, split-K) per (block, mode) with
+  // HIP events and keep the fastest
   std::vector<double> autotune(int64_t B, int64_t iters);
   // run a single conv GEMM of the training step (for profiling / tests)
   void run_conv(int64_t block, int64_t mode, int64_t B);
 
  private:
-  void conv(int l, int mode, int B, const ConvTile& t, hipStream_t s, bool with_stats);
+  void conv(int l, int mode, int B, const ConvTile& t, hipStream_t s, bool with_stats, float* ws = nullptr,
+            float* dz = nullptr);
   float* P(int64_t off) { return params_.data_ptr<float>() + off; }
   float* G(int64_t off) { return grads_.data_ptr<float>() + off; }
   int64_t Bmax_, feat_, ncls_;
@@ -96,8 +106,16 @@ class VggEngine {
   torch::Tensor params_, grads_, mom_, bufs_, nbt_;
   torch::Tensor data_[2], labels_[2], aug_[2];
   torch::Tensor idx_, ylab_, loss_, correct_, logits_, pred_;
-  torch::Tensor gbuf_[2], dz_, ws_, bn_part_, bn_coef_, bn_eval_, head_ws_;
+  torch::Tensor gbuf_[2], dz_[2], ws_, ws_side_, bn_part_, bn_coef_, bn_eval_, head_ws_;
   int64_t ws_elems_ = 0;
+  hipStream_t side_ = nullptr;
+  bool overlap_wgrad_ = false;
+  std::vector<hipEvent_t> ev_bn_, ev_wg_;  // per block: BN-backward done (main), wgrad done (side)
+
+ public:
+  ~VggEngine();
+  VggEngine(const VggEngine&) = delete;
+  VggEngine& operator=(const VggEngine&) = delete;
 };
 
 }  // namespace cs

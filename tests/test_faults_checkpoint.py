@@ -1,0 +1,126 @@
+"""Aux subsystems: fault injection through the facade's
+collectives, the step watchdog, the cross-rank replica checksum, NaN guard,
+and checkpoint save -> resume with the reference's 58-key state_dict layout."""
+import os
+import subprocess
+import sys
+import textwrap
+
+import pytest
+import torch
+
+from mp_util import run_world
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_fault_spec_raise_and_nth(monkeypatch):
+    from cs744_pytorch_distributed_tutorial_amd.utils import faults
+    faults._calls.clear()
+    monkeypatch.setenv("CS744_FAULT", "all_reduce@2:0:raise")
+    faults.maybe_inject("all_reduce", 0)  # 1st call: no fault
+    with pytest.raises(RuntimeError, match="injected failure"):
+        faults.maybe_inject("all_reduce", 0)
+    faults.maybe_inject("all_reduce", 1)  # other rank unaffected
+    faults.maybe_inject("broadcast", 0)   # other op unaffected
+    monkeypatch.setenv("CS744_FAULT", "bogus")
+    with pytest.raises(ValueError):
+        faults.maybe_inject("x", 0)
+
+
+def test_check_finite():
+    from cs744_pytorch_distributed_tutorial_amd.utils import faults
+    faults.check_finite([torch.ones(3)])
+    with pytest.raises(FloatingPointError):
+        faults.check_finite([torch.ones(2), torch.tensor([1.0, float("nan")])])
+
+
+def _kill_child(port, spec):
+    code = textwrap.dedent(f"""
+        import os, sys
+        sys.path.insert(0, {ROOT!r})
+        os.environ["CS744_FAULT"] = {spec!r}
+        import torch
+        from cs744_pytorch_distributed_tutorial_amd import distributed as D
+        D.init_process_group("gloo", rank=0, world_size=1, master_addr="127.0.0.1", master_port={port})
+        t = torch.ones(4)
+        D.all_reduce(t)
+        D.all_reduce(t)
+        print("survived", flush=True)
+    """)
+    return subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+
+
+def test_fault_kill_exits_rank_with_code_17(port):
+    r = _kill_child(port, "all_reduce@2:0:kill")
+    assert r.returncode == 17, (r.returncode, r.stderr[-500:])
+    assert "survived" not in r.stdout and "[fault]" in r.stderr
+
+
+def test_watchdog_aborts_stalled_step():
+    code = textwrap.dedent(f"""
+        import sys, time
+        sys.path.insert(0, {ROOT!r})
+        from cs744_pytorch_distributed_tutorial_amd.utils.faults import Watchdog
+        w = Watchdog(0.5, "step").start()
+        time.sleep(5)
+        print("not aborted")
+    """)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 18 and "[watchdog]" in r.stderr
+
+
+def _replicas(rank, world, diverge):
+    from cs744_pytorch_distributed_tutorial_amd.utils import faults
+    ts = [torch.arange(10.0), torch.ones(3)]
+    if diverge and rank == 1:
+        ts[1] = ts[1] * 2
+    try:
+        return {"spread": faults.assert_replicas_in_sync(ts), "err": ""}
+    except RuntimeError as e:
+        return {"spread": -1.0, "err": str(e)}
+
+
+@pytest.mark.slow
+def test_replica_checksum_detects_divergence():
+    ok = run_world(_replicas, 2, False)
+    assert all(o["spread"] == 0.0 for o in ok)
+    bad = run_world(_replicas, 2, True)
+    assert all("replicas diverged" in o["err"] for o in bad)
+
+
+def test_checkpoint_roundtrip_resume_matches_uninterrupted(tmp_path):
+    """train 2 steps -> save -> load into fresh model+optimizer -> 2 more steps ==
+    4 uninterrupted steps (bitwise, CPU)."""
+    from cs744_pytorch_distributed_tutorial_amd.models import VGG11
+    from cs744_pytorch_distributed_tutorial_amd.utils.checkpoint import (load_training_state,
+                                                                         save_training_state)
+    torch.set_num_threads(2)
+    g = torch.Generator().manual_seed(0)
+    batches = [(torch.randn(8, 3, 32, 32, generator=g), torch.randint(0, 10, (8,), generator=g)) for _ in range(4)]
+
+    def make():
+        torch.manual_seed(5000)
+        m = VGG11()
+        return m, torch.optim.SGD(m.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+
+    def run(m, opt, bs):
+        m.train()
+        for x, y in bs:
+            opt.zero_grad()
+            torch.nn.functional.cross_entropy(m(x), y).backward()
+            opt.step()
+
+    m_ref, o_ref = make()
+    run(m_ref, o_ref, batches)
+    m1, o1 = make()
+    run(m1, o1, batches[:2])
+    path = str(tmp_path / "ck.pt")
+    save_training_state(path, m1, o1, epoch=0, iteration=2)
+    st = torch.load(path, weights_only=True)
+    assert len(st["model"]) == 58 and st["iter"] == 2 and st["format"] == "cs744-amd/1"
+    m2, o2 = make()
+    load_training_state(path, m2, o2)
+    run(m2, o2, batches[2:])
+    for a, b in zip(m_ref.state_dict().values(), m2.state_dict().values()):
+        assert torch.equal(a, b)
