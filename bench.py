@@ -3,9 +3,16 @@
 
 Metric (BASELINE.json): images/sec for the WHOLE node, VGG-11, 3x32x32 -> 10
 classes, per-GPU batch 64 (the reference's part2/part3 per-rank batch,
-`master/part2b/part2b.py:20`), SGD(0.1, 0.9, 1e-4), one process per GPU,
-data-parallel gradient averaging (part3 = DDP semantics) over RCCL/xGMI.
-Weak scaling: per-GPU batch fixed, global batch = 64 * N.
+`master/part2b/part2b.py:20`), SGD(0.1, 0.9, 1e-4), fp32 (the reference's
+precision), one process per GPU, data-parallel gradient averaging with part3
+(DDP) semantics: bucketed all-reduce(AVG) over RCCL/xGMI overlapped with the
+backward pass. Weak scaling: per-GPU batch fixed, global batch = 64 * N.
+
+Default engine = ``native``: the C++ VggEngine (hand-written gfx950 kernels for
+every op, hipGraph-replayed step, native RcclComm). ``--engine torch`` runs the
+same model through stock PyTorch-ROCm modules + the framework's DDP (the
+comparison baseline). ``--model resnet50`` / ``--model llama-tiny`` etc. run the
+BASELINE.json extension configs through the autograd-path trainer.
 
 Contract: ``python bench.py --gpus N --steps K --warmup W``; for N > 1 launched by
 ``torch.distributed.run`` (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* from env). W untimed
@@ -40,7 +47,7 @@ def parse(argv=None):
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=10)
-    p.add_argument("--batch-size", type=int, default=64, help="per-GPU batch")
+    p.add_argument("--batch-size", type=int, default=None, help="per-GPU batch (default: 64 VGG, 128 ResNet)")
     p.add_argument("--model", type=str, default="VGG11")
     p.add_argument("--engine", type=str, default=os.environ.get("CS744_BENCH_ENGINE", "native"),
                    choices=["torch", "native"])
@@ -50,68 +57,45 @@ def parse(argv=None):
     p.add_argument("--bucket-mb", type=float, default=9.0)
     p.add_argument("--bucket-policy", type=str, default="layer", choices=["size", "layer", "single"])
     p.add_argument("--dtype", type=str, default="fp32", choices=["fp32", "bf16"])
+    p.add_argument("--seq-len", type=int, default=0, help="decoder LM sequence length")
     p.add_argument("--no-graph", action="store_true", help="native engine: disable hipGraph capture")
     p.add_argument("--graph", type=str, default="auto", choices=["auto", "full", "segments", "none"])
     p.add_argument("--json-out", type=str, default=None)
     return p.parse_args(argv)
 
 
-class TorchTrainer:
-    """Stock-PyTorch path (MIOpen/hipBLASLt kernels via autograd) — the comparison baseline."""
-
-    def __init__(self, args, device, rank, world):
-        from cs744_pytorch_distributed_tutorial_amd.models import VGG
-        from cs744_pytorch_distributed_tutorial_amd.parallel import DistributedDataParallel, make_comm, make_sync
-        from cs744_pytorch_distributed_tutorial_amd.utils import data as dm
-        torch.manual_seed(5000)
-        self.model = VGG(args.model).to(device)
-        self.world = world
-        if world > 1 and args.sync == "ddp":
-            self.net = DistributedDataParallel(self.model, comm=make_comm(args.comm), bucket_cap_mb=args.bucket_mb,
-                                               bucket_policy=args.bucket_policy)
-            self.sync = make_sync("none", [])
-        else:
-            self.net = self.model
-            self.sync = make_sync(args.sync if world > 1 else "none", self.model.parameters())
-        self.opt = torch.optim.SGD(self.net.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
-        self.crit = torch.nn.CrossEntropyLoss()
-        ds = dm.SyntheticCIFAR10(train=True, size=50_000, seed=0)
-        sampler = dm.DistributedSampler(len(ds), world, rank, shuffle=True, seed=0)
-        self.loader = dm.DeviceDataLoader(ds, args.batch_size, sampler=sampler, train=True, device=device,
-                                          drop_last=True)
-        self._it = iter(self.loader)
-        self.loss = None
-
-    def _batch(self):
-        try:
-            return next(self._it)
-        except StopIteration:
-            self.loader.set_epoch(self.loader.epoch + 1)
-            self._it = iter(self.loader)
-            return next(self._it)
-
-    def step(self):
-        x, y = self._batch()
-        self.opt.zero_grad()
-        loss = self.crit(self.net(x), y)
-        loss.backward()
-        self.sync()
-        self.opt.step()
-        self.loss = loss.detach()
-
-    def last_loss(self) -> float:
-        return float(self.loss.item())
+def is_vgg(name: str) -> bool:
+    return name.upper().startswith("VGG")
 
 
 def make_trainer(args, device, rank, world):
-    if args.engine == "torch":
-        return TorchTrainer(args, device, rank, world)
-    from cs744_pytorch_distributed_tutorial_amd.runtime.engine import NativeTrainer
-    return NativeTrainer.from_bench_args(args, device, rank, world)
+    if args.engine == "native" and is_vgg(args.model):
+        from cs744_pytorch_distributed_tutorial_amd.runtime.engine import NativeTrainer
+        return NativeTrainer.from_bench_args(args, device, rank, world)
+    from cs744_pytorch_distributed_tutorial_amd.runtime.torch_trainer import TorchTrainer
+    return TorchTrainer(args.model, args.batch_size, device, rank, world, sync=args.sync, comm=args.comm,
+                        bucket_mb=args.bucket_mb, bucket_policy=args.bucket_policy, dtype=args.dtype,
+                        seq_len=args.seq_len)
+
+
+def describe(args, trainer, world):
+    name = args.model
+    if is_vgg(name):
+        return (f"images/sec (whole node) {name[:3]}-{name[3:]} CIFAR-shape", "images/s",
+                args.batch_size * world, None, BASELINE_IMG_S,
+                "synthetic (CIFAR-10 shape 3x32x32 uint8, on-device augmentation), random-init weights")
+    if getattr(trainer, "is_lm", False):
+        seq = trainer.data.tokens.shape[1] - 1
+        return (f"tokens/sec (whole node) {name} decoder LM", "tokens/s", args.batch_size * world, seq, None,
+                "synthetic random token ids, random-init weights")
+    return (f"images/sec (whole node) {name} ImageNet-shape", "images/s", args.batch_size * world, None, None,
+            "synthetic (ImageNet shape 3x224x224 uint8 pool on device), random-init weights")
 
 
 def main(argv=None) -> int:
     args = parse(argv)
+    if args.batch_size is None:
+        args.batch_size = 64 if is_vgg(args.model) else (8 if "llama" in args.model.lower() else 128)
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
     if world_env > 1:
         D.init_process_group(backend="nccl")
@@ -136,26 +120,28 @@ def main(argv=None) -> int:
     elapsed = time.perf_counter() - t0
     elapsed = D.all_reduce_scalar(elapsed, op=D.ReduceOp.MAX) if world > 1 else elapsed
     loss = trainer.last_loss()
-    imgs = args.batch_size * world * args.steps
-    value = imgs / elapsed
+    metric, unit, gbatch, seq, baseline, data = describe(args, trainer, world)
+    per_step = gbatch * (seq or 1)
+    value = per_step * args.steps / elapsed
+    engine = args.engine if is_vgg(args.model) else "torch"
     out = {
-        "metric": "images/sec (whole node) VGG-11 CIFAR-shape",
+        "metric": metric,
         "value": round(value, 2),
-        "unit": "images/s",
+        "unit": unit,
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(1e3 * elapsed / args.steps, 4),
         "higher_is_better": True,
         "scaling": "weak",
-        "vs_baseline": round(value / BASELINE_IMG_S, 2),
-        "dtype": "fp32" if args.dtype == "fp32" else "bf16",
-        "data": "synthetic (CIFAR-10 shape 3x32x32 uint8, on-device augmentation), random-init weights",
-        "config": {"model": "VGG-11", "global_batch": args.batch_size * world, "per_gpu_batch": args.batch_size,
-                   "seq_len": None, "parallelism": f"dp{world}", "sync": args.sync if world > 1 else "none",
-                   "engine": args.engine, "comm": args.comm, "bucket_mb": args.bucket_mb,
-                   "bucket_policy": args.bucket_policy, "optimizer": "SGD(lr=0.1, momentum=0.9, wd=1e-4)",
-                   "final_loss": round(loss, 4), "baseline_img_s": BASELINE_IMG_S},
+        "vs_baseline": round(value / baseline, 2) if baseline else None,
+        "dtype": args.dtype,
+        "data": data,
+        "config": {"model": args.model, "global_batch": gbatch, "per_gpu_batch": args.batch_size, "seq_len": seq,
+                   "parallelism": f"dp{world}", "sync": args.sync if world > 1 else "none", "engine": engine,
+                   "comm": args.comm, "bucket_mb": args.bucket_mb,
+                   "optimizer": "SGD(lr=0.1, momentum=0.9, wd=1e-4)", "final_loss": round(loss, 4),
+                   "baseline_img_s": baseline},
     }
     if rank == 0:
         line = json.dumps(out)

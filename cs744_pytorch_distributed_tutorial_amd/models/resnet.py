@@ -1,0 +1,130 @@
+"""ResNet family (BASELINE.json config "ResNet-50 on synthetic ImageNet-shape, 8xMI355X
+bucketed all-reduce + backward overlap" — an extension: the reference only has VGG,
+SURVEY.md §0.1 item 3, §7.1 step 7).
+
+Bottleneck ResNet (He et al. 2016, v1.5 placement of the stride on the 3x3 conv),
+written from the architecture definition; parameter names follow the de-facto
+layout of the widely used ImageNet implementation (``conv1``, ``bn1``,
+``layer{1..4}.{i}.conv{1,2,3}``, ``.downsample.{0,1}``, ``fc``) so checkpoints are
+interchangeable with it. ResNet-50 has 25,557,032 parameters (97.5 MiB of fp32
+gradients per step — the all-reduce payload of the scaling benchmark).
+
+MI355X notes: the model is meant to run ``channels_last`` (NHWC, the layout the
+MFMA implicit-GEMM convolutions want) under optional bf16 autocast, trained by
+``parallel.ddp.DistributedDataParallel`` (flat bucketed gradients, RCCL all-reduce
+overlapped with backward) and ``ops.optim.FusedSGD`` (one HIP launch per step).
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Type, Union
+
+import torch
+import torch.nn as nn
+
+
+def conv3x3(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
+    return nn.Conv2d(cin, cout, 3, stride=stride, padding=1, bias=False)
+
+
+def conv1x1(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
+    return nn.Conv2d(cin, cout, 1, stride=stride, bias=False)
+
+
+class BasicBlock(nn.Module):
+    expansion = 1
+
+    def __init__(self, cin: int, width: int, stride: int = 1, downsample: Optional[nn.Module] = None):
+        super().__init__()
+        self.conv1 = conv3x3(cin, width, stride)
+        self.bn1 = nn.BatchNorm2d(width)
+        self.conv2 = conv3x3(width, width)
+        self.bn2 = nn.BatchNorm2d(width)
+        self.relu = nn.ReLU(inplace=True)
+        self.downsample = downsample
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        idt = x if self.downsample is None else self.downsample(x)
+        y = self.relu(self.bn1(self.conv1(x)))
+        y = self.bn2(self.conv2(y))
+        return self.relu(y + idt)
+
+
+class Bottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, cin: int, width: int, stride: int = 1, downsample: Optional[nn.Module] = None):
+        super().__init__()
+        self.conv1 = conv1x1(cin, width)
+        self.bn1 = nn.BatchNorm2d(width)
+        self.conv2 = conv3x3(width, width, stride)
+        self.bn2 = nn.BatchNorm2d(width)
+        self.conv3 = conv1x1(width, width * 4)
+        self.bn3 = nn.BatchNorm2d(width * 4)
+        self.relu = nn.ReLU(inplace=True)
+        self.downsample = downsample
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        idt = x if self.downsample is None else self.downsample(x)
+        y = self.relu(self.bn1(self.conv1(x)))
+        y = self.relu(self.bn2(self.conv2(y)))
+        y = self.bn3(self.conv3(y))
+        return self.relu(y + idt)
+
+
+class ResNet(nn.Module):
+    def __init__(self, block: Type[Union[BasicBlock, Bottleneck]], layers: List[int], num_classes: int = 1000,
+                 zero_init_residual: bool = False):
+        super().__init__()
+        self.inplanes = 64
+        self.conv1 = nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False)
+        self.bn1 = nn.BatchNorm2d(64)
+        self.relu = nn.ReLU(inplace=True)
+        self.maxpool = nn.MaxPool2d(3, stride=2, padding=1)
+        self.layer1 = self._make_layer(block, 64, layers[0])
+        self.layer2 = self._make_layer(block, 128, layers[1], stride=2)
+        self.layer3 = self._make_layer(block, 256, layers[2], stride=2)
+        self.layer4 = self._make_layer(block, 512, layers[3], stride=2)
+        self.avgpool = nn.AdaptiveAvgPool2d((1, 1))
+        self.fc = nn.Linear(512 * block.expansion, num_classes)
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+            elif isinstance(m, nn.BatchNorm2d):
+                nn.init.ones_(m.weight)
+                nn.init.zeros_(m.bias)
+        if zero_init_residual:
+            for m in self.modules():
+                last = getattr(m, "bn3", None) if isinstance(m, Bottleneck) else getattr(m, "bn2", None)
+                if isinstance(m, (Bottleneck, BasicBlock)) and last is not None:
+                    nn.init.zeros_(last.weight)
+
+    def _make_layer(self, block, width: int, blocks: int, stride: int = 1) -> nn.Sequential:
+        down = None
+        if stride != 1 or self.inplanes != width * block.expansion:
+            down = nn.Sequential(conv1x1(self.inplanes, width * block.expansion, stride),
+                                 nn.BatchNorm2d(width * block.expansion))
+        layers = [block(self.inplanes, width, stride, down)]
+        self.inplanes = width * block.expansion
+        layers += [block(self.inplanes, width) for _ in range(1, blocks)]
+        return nn.Sequential(*layers)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
+        x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+        return self.fc(torch.flatten(self.avgpool(x), 1))
+
+
+def resnet18(num_classes: int = 1000) -> ResNet:
+    return ResNet(BasicBlock, [2, 2, 2, 2], num_classes)
+
+
+def resnet34(num_classes: int = 1000) -> ResNet:
+    return ResNet(BasicBlock, [3, 4, 6, 3], num_classes)
+
+
+def resnet50(num_classes: int = 1000) -> ResNet:
+    return ResNet(Bottleneck, [3, 4, 6, 3], num_classes)
+
+
+def resnet101(num_classes: int = 1000) -> ResNet:
+    return ResNet(Bottleneck, [3, 4, 23, 3], num_classes)

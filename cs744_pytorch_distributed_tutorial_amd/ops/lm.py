@@ -1,0 +1,100 @@
+"""Autograd wrappers of the decoder-LM gfx950 kernels (``csrc/kernels/lm.hip``).
+
+On GPU tensors every op runs the hand-written HIP kernel (forward and backward);
+on CPU tensors the plain-PyTorch reference below runs instead (this is the
+numerics oracle of ``tests/test_lm_gpu.py`` and lets the LM train on CPU in the
+multi-process gloo tests).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import native
+
+
+# ------------------------------------------------------------------ references
+def rms_norm_ref(x: torch.Tensor, w: torch.Tensor, eps: float) -> torch.Tensor:
+    xf = x.float()
+    y = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps) * w.float()
+    return y.to(x.dtype)
+
+
+def swiglu_ref(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    return (torch.nn.functional.silu(a.float()) * b.float()).to(a.dtype)
+
+
+def rope_ref(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
+    """x: [B, S, H, hd], rotate interleaved pairs (2j, 2j+1) by angle table [S, hd/2]."""
+    xf = x.float().view(*x.shape[:-1], -1, 2)
+    c = cos[None, :, None, :]
+    s = sin[None, :, None, :]
+    x0, x1 = xf[..., 0], xf[..., 1]
+    out = torch.stack([x0 * c - x1 * s, x0 * s + x1 * c], -1)
+    return out.view(x.shape).to(x.dtype)
+
+
+# ------------------------------------------------------------------ autograd functions
+class _RMSNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, eps):
+        xc = x.contiguous()
+        y, rstd = native.C().rmsnorm_fwd(xc, w.contiguous(), eps)
+        ctx.save_for_backward(xc, w, rstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w, rstd = ctx.saved_tensors
+        dx, dw = native.C().rmsnorm_bwd(x, w.contiguous(), rstd, gy.contiguous().to(x.dtype))
+        return dx, dw, None
+
+
+class _SwiGLU(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, a, b):
+        a, b = a.contiguous(), b.contiguous()
+        ctx.save_for_backward(a, b)
+        return native.C().swiglu_fwd(a, b)
+
+    @staticmethod
+    def backward(ctx, gy):
+        a, b = ctx.saved_tensors
+        da, db = native.C().swiglu_bwd(a, b, gy.contiguous().to(a.dtype))
+        return da, db
+
+
+class _RoPE(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, cos, sin):
+        cos, sin = cos.float().contiguous(), sin.float().contiguous()
+        ctx.save_for_backward(cos, sin)
+        return native.C().rope(x.contiguous(), cos, sin, False)
+
+    @staticmethod
+    def backward(ctx, gy):
+        cos, sin = ctx.saved_tensors
+        return native.C().rope(gy.contiguous(), cos, sin, True), None, None
+
+
+def _native_ok(*ts) -> bool:
+    return all(t.is_cuda for t in ts) and all(t.dtype in (torch.float32, torch.bfloat16) for t in ts)
+
+
+def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float = 1e-5) -> torch.Tensor:
+    if _native_ok(x, w):
+        if torch.is_autocast_enabled() and x.dtype == torch.float32:
+            pass  # residual stream stays fp32; the following Linear casts under autocast
+        return _RMSNorm.apply(x, w, eps)
+    return rms_norm_ref(x, w, eps)
+
+
+def swiglu(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    if _native_ok(a, b) and a.dtype == b.dtype:
+        return _SwiGLU.apply(a, b)
+    return swiglu_ref(a, b)
+
+
+def rope(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
+    if _native_ok(x):
+        return _RoPE.apply(x, cos, sin)
+    return rope_ref(x, cos, sin)

@@ -1,0 +1,122 @@
+"""Autograd-path trainer for every model that is not VGG (ResNet family now; the
+decoder LM of ``models.llama``): PyTorch-ROCm modules for the layer math, the
+framework's own data-parallel runtime around them.
+
+* DDP = ``parallel.ddp.DistributedDataParallel`` (flat gradient buffer, grads as
+  bucket views, post-accumulate hooks launch bucketed all-reduce(AVG) while
+  autograd is still producing earlier layers' gradients) over the native
+  ``RcclComm`` (``comm="rccl"``) or ProcessGroupNCCL (``comm="torch"``);
+  or any explicit strategy of ``parallel.sync`` (part2a / part2a_extra / part2b);
+* optimizer = ``ops.optim.FusedSGD`` (one multi-tensor HIP launch per step);
+* CNNs run ``channels_last`` (NHWC, MIOpen/hipBLASLt's fast layout), optionally
+  under bf16 autocast (``dtype="bf16"``; master weights and the optimizer stay fp32);
+* data = device-resident synthetic batches of the named shape (no host traffic).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.nn as nn
+
+from ..parallel import DistributedDataParallel, make_comm, make_sync
+
+
+def build_model(name: str) -> nn.Module:
+    from ..models import resnet, vgg
+    n = name.lower().replace("-", "")
+    if n.startswith("vgg"):
+        return vgg.VGG(n.upper())
+    if n in ("resnet18", "resnet34", "resnet50", "resnet101"):
+        return getattr(resnet, n)()
+    if n.startswith("llama") or n.startswith("decoder"):
+        from ..models import llama
+        return llama.build(name.lower())
+    raise ValueError(f"unknown model {name!r}")
+
+
+class SyntheticBatches:
+    """A pool of random, fixed, device-resident samples; each step gathers a random batch.
+
+    Images: uint8 NHWC pool -> fp32/bf16 normalised NCHW(channels_last) batch.
+    Tokens: int64 [pool, seq+1] -> (input, target) shifted pair.
+    """
+
+    def __init__(self, kind: str, batch: int, device, shape=(3, 224, 224), classes: int = 1000, pool: int = 512,
+                 seq: int = 0, vocab: int = 0, seed: int = 0):
+        g = torch.Generator(device="cpu").manual_seed(seed)
+        self.kind, self.batch, self.device = kind, batch, device
+        self.pool = max(pool, batch)
+        if kind == "image":
+            c, h, w = shape
+            self.data = torch.randint(0, 256, (self.pool, h, w, c), generator=g, dtype=torch.uint8).to(device)
+            self.labels = torch.randint(0, classes, (self.pool,), generator=g).to(device)
+            self.mean = torch.tensor([0.485, 0.456, 0.406], device=device).view(1, 3, 1, 1) * 255
+            self.std = torch.tensor([0.229, 0.224, 0.225], device=device).view(1, 3, 1, 1) * 255
+        else:
+            self.tokens = torch.randint(0, vocab, (self.pool, seq + 1), generator=g).to(device)
+        self.gen = torch.Generator(device=device).manual_seed(seed + 1)
+
+    def next(self):
+        idx = torch.randint(0, self.pool, (self.batch,), device=self.device, generator=self.gen)
+        if self.kind == "image":
+            x = self.data.index_select(0, idx).permute(0, 3, 1, 2).float()
+            x = ((x - self.mean) / self.std).contiguous(memory_format=torch.channels_last)
+            return x, self.labels.index_select(0, idx)
+        t = self.tokens.index_select(0, idx)
+        return t[:, :-1].contiguous(), t[:, 1:].contiguous()
+
+
+class TorchTrainer:
+    def __init__(self, model: str, batch_size: int, device, rank: int = 0, world: int = 1, sync: str = "ddp",
+                 comm: str = "rccl", bucket_mb: float = 25.0, bucket_policy: str = "layer", dtype: str = "fp32",
+                 lr: float = 0.1, momentum: float = 0.9, weight_decay: float = 1e-4, seed: int = 5000,
+                 seq_len: int = 0, fused_sgd: bool = True):
+        from ..ops.optim import FusedSGD
+        torch.manual_seed(seed)
+        self.device, self.world, self.B = device, world, batch_size
+        self.model_name = model
+        self.module = build_model(model).to(device)
+        self.is_lm = hasattr(self.module, "vocab_size")
+        if not self.is_lm:
+            self.module = self.module.to(memory_format=torch.channels_last)
+        self.dtype = dtype
+        if world > 1 and sync == "ddp":
+            self.net = DistributedDataParallel(self.module, comm=make_comm(comm), bucket_cap_mb=bucket_mb,
+                                               bucket_policy=bucket_policy)
+            self.sync = make_sync("none", [])
+        else:
+            self.net = self.module
+            self.sync = make_sync(sync if world > 1 else "none", self.module.parameters())
+        params = self.net.parameters()
+        self.opt = FusedSGD(params, lr=lr, momentum=momentum, weight_decay=weight_decay) if fused_sgd and \
+            torch.cuda.is_available() else torch.optim.SGD(params, lr=lr, momentum=momentum, weight_decay=weight_decay)
+        self.crit = nn.CrossEntropyLoss()
+        if self.is_lm:
+            self.data = SyntheticBatches("tokens", batch_size, device, seq=seq_len or self.module.max_seq,
+                                         vocab=self.module.vocab_size, seed=seed)
+        else:
+            shape = (3, 32, 32) if model.lower().startswith("vgg") else (3, 224, 224)
+            classes = 10 if model.lower().startswith("vgg") else 1000
+            self.data = SyntheticBatches("image", batch_size, device, shape=shape, classes=classes, seed=seed)
+        self.loss: Optional[torch.Tensor] = None
+
+    def step(self) -> None:
+        x, y = self.data.next()
+        self.opt.zero_grad()  # DDP re-attaches its bucket views (and zeroes them) in forward
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=self.dtype == "bf16"):
+            out = self.net(x)
+            if self.is_lm:
+                loss = self.crit(out.float().view(-1, out.shape[-1]), y.view(-1))
+            else:
+                loss = self.crit(out.float(), y)
+        loss.backward()
+        self.sync()
+        self.opt.step()
+        self.loss = loss.detach()
+
+    def last_loss(self) -> float:
+        return float(self.loss.item()) if self.loss is not None else float("nan")
+
+    def tokens_per_step(self) -> int:
+        return self.B * (self.data.tokens.shape[1] - 1) if self.is_lm else self.B

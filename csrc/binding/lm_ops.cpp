@@ -1,0 +1,91 @@
+// torch bindings of the decoder-LM kernels (csrc/kernels/lm.hip); shapes/dtypes validated on the host.
+#include "binding/torch_util.h"
+#include "kernels/launchers.h"
+
+namespace {
+
+using csb::cur_stream;
+using csb::DevGuard;
+
+int dt_of(const torch::Tensor& t) {
+  if (t.scalar_type() == at::kFloat) return CS_F32;
+  if (t.scalar_type() == at::kBFloat16) return CS_BF16;
+  TORCH_CHECK(false, "LM kernels support float32 / bfloat16, got ", t.scalar_type());
+  return -1;
+}
+
+void check(const torch::Tensor& t, const char* n) {
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous(), n, " must be a contiguous GPU tensor");
+}
+
+std::vector<torch::Tensor> rmsnorm_fwd(torch::Tensor x, torch::Tensor w, double eps) {
+  check(x, "x"); check(w, "w");
+  const int64_t D = w.numel();
+  TORCH_CHECK(x.size(-1) == D, "rmsnorm: last dim must match the weight");
+  const int64_t rows = x.numel() / D;
+  DevGuard g(x.device());
+  auto y = torch::empty_like(x);
+  auto rstd = torch::empty({rows}, x.options().dtype(at::kFloat));
+  CS_LAUNCH(cs_rmsnorm_fwd(dt_of(x), dt_of(w), x.data_ptr(), w.data_ptr(), y.data_ptr(), rstd.data_ptr<float>(),
+                           (int)rows, (int)D, (float)eps, cur_stream()));
+  return {y, rstd};
+}
+
+std::vector<torch::Tensor> rmsnorm_bwd(torch::Tensor x, torch::Tensor w, torch::Tensor rstd, torch::Tensor gy) {
+  check(x, "x"); check(w, "w"); check(rstd, "rstd"); check(gy, "gy");
+  const int64_t D = w.numel(), rows = x.numel() / D;
+  TORCH_CHECK(gy.sizes() == x.sizes() && gy.scalar_type() == x.scalar_type() && rstd.numel() == rows,
+              "rmsnorm_bwd: shapes");
+  DevGuard g(x.device());
+  auto dx = torch::empty_like(x);
+  auto dw = torch::empty_like(w);
+  auto part = torch::empty({(int64_t)cs_rmsnorm_bwd_partials((int)rows), D}, x.options().dtype(at::kFloat));
+  CS_LAUNCH(cs_rmsnorm_bwd(dt_of(x), dt_of(w), x.data_ptr(), w.data_ptr(), rstd.data_ptr<float>(), gy.data_ptr(),
+                           dx.data_ptr(), dw.data_ptr(), part.data_ptr<float>(), (int)rows, (int)D, cur_stream()));
+  return {dx, dw};
+}
+
+torch::Tensor swiglu_fwd(torch::Tensor a, torch::Tensor b) {
+  check(a, "a"); check(b, "b");
+  TORCH_CHECK(a.sizes() == b.sizes() && a.scalar_type() == b.scalar_type(), "swiglu: a/b mismatch");
+  DevGuard g(a.device());
+  auto out = torch::empty_like(a);
+  CS_LAUNCH(cs_swiglu_fwd(dt_of(a), a.data_ptr(), b.data_ptr(), out.data_ptr(), a.numel(), cur_stream()));
+  return out;
+}
+
+std::vector<torch::Tensor> swiglu_bwd(torch::Tensor a, torch::Tensor b, torch::Tensor gy) {
+  check(a, "a"); check(b, "b"); check(gy, "gy");
+  TORCH_CHECK(a.sizes() == b.sizes() && gy.sizes() == a.sizes() && gy.scalar_type() == a.scalar_type(),
+              "swiglu_bwd: shapes");
+  DevGuard g(a.device());
+  auto da = torch::empty_like(a);
+  auto db = torch::empty_like(b);
+  CS_LAUNCH(cs_swiglu_bwd(dt_of(a), a.data_ptr(), b.data_ptr(), gy.data_ptr(), da.data_ptr(), db.data_ptr(),
+                          a.numel(), cur_stream()));
+  return {da, db};
+}
+
+torch::Tensor rope(torch::Tensor x, torch::Tensor cosv, torch::Tensor sinv, bool inverse) {
+  check(x, "x"); check(cosv, "cos"); check(sinv, "sin");
+  TORCH_CHECK(x.dim() == 4, "rope: x must be [B, S, H, head_dim]");
+  const int64_t B = x.size(0), S = x.size(1), H = x.size(2), hd = x.size(3);
+  TORCH_CHECK(hd % 2 == 0 && cosv.scalar_type() == at::kFloat && sinv.scalar_type() == at::kFloat &&
+                  cosv.numel() == S * hd / 2 && sinv.numel() == S * hd / 2,
+              "rope: cos/sin must be fp32 [S, head_dim/2]");
+  DevGuard g(x.device());
+  auto out = torch::empty_like(x);
+  CS_LAUNCH(cs_rope(dt_of(x), x.data_ptr(), cosv.data_ptr<float>(), sinv.data_ptr<float>(), out.data_ptr(), (int)B,
+                    (int)S, (int)H, (int)hd, inverse ? 1 : 0, cur_stream()));
+  return out;
+}
+
+}  // namespace
+
+void register_lm_ops(pybind11::module& m) {
+  m.def("rmsnorm_fwd", &rmsnorm_fwd);
+  m.def("rmsnorm_bwd", &rmsnorm_bwd);
+  m.def("swiglu_fwd", &swiglu_fwd);
+  m.def("swiglu_bwd", &swiglu_bwd);
+  m.def("rope", &rope);
+}

@@ -68,3 +68,18 @@ int cs_bn_bwd_blocks(int B, int H, int W, int C, int pool);
 hipError_t cs_bn_bwd(const float* y, const float* G, int B, int H, int W, int C, int pool, const float* scale,
                      const float* shift, const float* mean, const float* invstd, const float* gamma, float* part,
                      float* coef, float* dgamma, float* dbeta, float* dbias, float* dz, hipStream_t stream);
+
+// ---------------------------------------------------------------- decoder-LM elementwise ops (lm.hip)
+enum { CS_F32 = 0, CS_BF16 = 1 };
+int cs_rmsnorm_bwd_partials(int rows);
+hipError_t cs_rmsnorm_fwd(int dt, int wdt, const void* x, const void* w, void* y, float* rstd, int rows, int D,
+                          float eps, hipStream_t s);
+// part: [cs_rmsnorm_bwd_partials(rows)][D] fp32 scratch; dw has the weight's dtype
+hipError_t cs_rmsnorm_bwd(int dt, int wdt, const void* x, const void* w, const float* rstd, const void* g, void* dx,
+                          void* dw, float* part, int rows, int D, hipStream_t s);
+hipError_t cs_swiglu_fwd(int dt, const void* a, const void* b, void* out, size_t n, hipStream_t s);
+hipError_t cs_swiglu_bwd(int dt, const void* a, const void* b, const void* g, void* da, void* db, size_t n,
+                         hipStream_t s);
+// x/out: [B, S, H, hd] contiguous; cos/sin: [S, hd/2] fp32; inverse rotates by -angle (backward)
+hipError_t cs_rope(int dt, const void* x, const float* cosv, const float* sinv, void* out, int B, int S, int H, int hd,
+                   int inverse, hipStream_t s);

@@ -1,0 +1,196 @@
+// Decoder-LM elementwise hot ops for gfx950 (the BASELINE "Llama-3 8B bf16 pure DP"
+// extension config): RMSNorm forward/backward, SwiGLU forward/backward, rotary
+// position embedding forward/backward. fp32 or bf16 storage, fp32 math.
+//
+// RMSNorm: one 256-thread workgroup per row (D up to 16K), row sum of squares by
+// wave shuffles + LDS, vectorised 8-byte (bf16 x4) / 16-byte (fp32 x4) accesses.
+// The weight gradient is reduced deterministically: every workgroup writes one
+// fp32 partial row per ROWS_PER_BLOCK rows, a second kernel sums the partials.
+#include <hip/hip_bf16.h>
+
+#include "common.h"
+#include "launchers.h"
+
+namespace {
+
+__device__ __forceinline__ float ld(const float* p, size_t i) { return p[i]; }
+__device__ __forceinline__ float ld(const __hip_bfloat16* p, size_t i) { return __bfloat162float(p[i]); }
+__device__ __forceinline__ void st(float* p, size_t i, float v) { p[i] = v; }
+__device__ __forceinline__ void st(__hip_bfloat16* p, size_t i, float v) { p[i] = __float2bfloat16(v); }
+
+constexpr int kRowsPerBlock = 8;
+
+template <typename T, typename W>
+__global__ __launch_bounds__(256) void rmsnorm_fwd_kernel(const T* __restrict__ x, const W* __restrict__ w,
+                                                          T* __restrict__ y, float* __restrict__ rstd, int rows,
+                                                          int D, float eps) {
+  __shared__ float red[16];
+  const int row = blockIdx.x;
+  if (row >= rows) return;
+  const T* xr = x + (size_t)row * D;
+  float ss = 0.f;
+  for (int i = threadIdx.x; i < D; i += blockDim.x) {
+    const float v = ld(xr, i);
+    ss += v * v;
+  }
+  ss = cs::block_sum(ss, red);
+  const float r = rsqrtf(ss / (float)D + eps);
+  if (threadIdx.x == 0) rstd[row] = r;
+  T* yr = y + (size_t)row * D;
+  for (int i = threadIdx.x; i < D; i += blockDim.x) st(yr, i, ld(xr, i) * r * ld(w, i));
+}
+
+// dx_j = r*w_j*g_j - (r^3/D) x_j sum_i(w_i g_i x_i);  dw partial_j = sum_rows g_j x_j r
+template <typename T, typename W>
+__global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const T* __restrict__ x, const W* __restrict__ w,
+                                                          const float* __restrict__ rstd, const T* __restrict__ g,
+                                                          T* __restrict__ dx, float* __restrict__ dw_part, int rows,
+                                                          int D) {
+  __shared__ float red[16];
+  const int r0 = blockIdx.x * kRowsPerBlock;
+  float* part = dw_part + (size_t)blockIdx.x * D;
+  for (int i = threadIdx.x; i < D; i += blockDim.x) part[i] = 0.f;
+  for (int rr = 0; rr < kRowsPerBlock; ++rr) {
+    const int row = r0 + rr;
+    if (row >= rows) break;
+    const T* xr = x + (size_t)row * D;
+    const T* gr = g + (size_t)row * D;
+    const float r = rstd[row];
+    float dot = 0.f;
+    for (int i = threadIdx.x; i < D; i += blockDim.x) dot += ld(w, i) * ld(gr, i) * ld(xr, i);
+    dot = cs::block_sum(dot, red);
+    const float c = r * r * r * dot / (float)D;
+    T* dxr = dx + (size_t)row * D;
+    for (int i = threadIdx.x; i < D; i += blockDim.x) {
+      const float xv = ld(xr, i), gv = ld(gr, i);
+      st(dxr, i, r * ld(w, i) * gv - c * xv);
+      part[i] += gv * xv * r;  // same thread owns column i for every row: no race
+    }
+  }
+}
+
+template <typename W>
+__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ part, int P, int D,
+                                                     W* __restrict__ dw) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= D) return;
+  float s = 0.f;
+  for (int p = 0; p < P; ++p) s += part[(size_t)p * D + i];
+  st(dw, i, s);
+}
+
+__device__ __forceinline__ float sigmoidf(float a) { return 1.f / (1.f + __expf(-a)); }
+
+template <typename T>
+__global__ __launch_bounds__(256) void swiglu_fwd_kernel(const T* __restrict__ a, const T* __restrict__ b,
+                                                         T* __restrict__ out, size_t n) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const float av = ld(a, i);
+    st(out, i, av * sigmoidf(av) * ld(b, i));
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void swiglu_bwd_kernel(const T* __restrict__ a, const T* __restrict__ b,
+                                                         const T* __restrict__ g, T* __restrict__ da,
+                                                         T* __restrict__ db, size_t n) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const float av = ld(a, i), bv = ld(b, i), gv = ld(g, i);
+    const float s = sigmoidf(av);
+    st(da, i, gv * bv * s * (1.f + av * (1.f - s)));
+    st(db, i, gv * av * s);
+  }
+}
+
+// x: [B, S, H, hd] contiguous, pairs (2j, 2j+1) rotated by angle (pos, j); sign = +1 fwd, -1 bwd
+template <typename T>
+__global__ __launch_bounds__(256) void rope_kernel(const T* __restrict__ x, const float* __restrict__ cosv,
+                                                   const float* __restrict__ sinv, T* __restrict__ out, int S, int H,
+                                                   int hd, size_t npairs, float sign) {
+  const int half = hd >> 1;
+  for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < npairs; p += (size_t)gridDim.x * blockDim.x) {
+    const int j = (int)(p % half);
+    const size_t rowi = p / half;  // (b, s, h)
+    const int s = (int)((rowi / H) % S);
+    const float c = cosv[(size_t)s * half + j], sn = sign * sinv[(size_t)s * half + j];
+    const float x0 = ld(x, 2 * p), x1 = ld(x, 2 * p + 1);
+    st(out, 2 * p, x0 * c - x1 * sn);
+    st(out, 2 * p + 1, x0 * sn + x1 * c);
+  }
+}
+
+int grid_for(size_t n) {
+  size_t b = (n + 255) / 256;
+  return (int)(b > 16384 ? 16384 : (b == 0 ? 1 : b));
+}
+
+}  // namespace
+
+int cs_rmsnorm_bwd_partials(int rows) { return (rows + kRowsPerBlock - 1) / kRowsPerBlock; }
+
+#define CS_DT_DISPATCH(dt, ...)                                         \
+  do {                                                                  \
+    if ((dt) == CS_F32) {                                               \
+      using T = float;                                                  \
+      __VA_ARGS__;                                                      \
+    } else if ((dt) == CS_BF16) {                                       \
+      using T = __hip_bfloat16;                                         \
+      __VA_ARGS__;                                                      \
+    } else {                                                            \
+      return hipErrorInvalidValue;                                      \
+    }                                                                   \
+  } while (0)
+
+hipError_t cs_rmsnorm_fwd(int dt, int wdt, const void* x, const void* w, void* y, float* rstd, int rows, int D,
+                          float eps, hipStream_t s) {
+  if (rows <= 0) return hipSuccess;
+  if (wdt == CS_F32) {
+    CS_DT_DISPATCH(dt, hipLaunchKernelGGL((rmsnorm_fwd_kernel<T, float>), dim3(rows), dim3(256), 0, s,
+                                          (const T*)x, (const float*)w, (T*)y, rstd, rows, D, eps));
+  } else {
+    CS_DT_DISPATCH(dt, hipLaunchKernelGGL((rmsnorm_fwd_kernel<T, __hip_bfloat16>), dim3(rows), dim3(256), 0, s,
+                                          (const T*)x, (const __hip_bfloat16*)w, (T*)y, rstd, rows, D, eps));
+  }
+  return hipGetLastError();
+}
+
+hipError_t cs_rmsnorm_bwd(int dt, int wdt, const void* x, const void* w, const float* rstd, const void* g, void* dx,
+                          void* dw, float* part, int rows, int D, hipStream_t s) {
+  if (rows <= 0) return hipSuccess;
+  const int P = cs_rmsnorm_bwd_partials(rows);
+  if (wdt == CS_F32) {
+    CS_DT_DISPATCH(dt, hipLaunchKernelGGL((rmsnorm_bwd_kernel<T, float>), dim3(P), dim3(256), 0, s, (const T*)x,
+                                          (const float*)w, rstd, (const T*)g, (T*)dx, part, rows, D));
+    hipLaunchKernelGGL((colsum_kernel<float>), dim3((D + 255) / 256), dim3(256), 0, s, part, P, D, (float*)dw);
+  } else {
+    CS_DT_DISPATCH(dt, hipLaunchKernelGGL((rmsnorm_bwd_kernel<T, __hip_bfloat16>), dim3(P), dim3(256), 0, s,
+                                          (const T*)x, (const __hip_bfloat16*)w, rstd, (const T*)g, (T*)dx, part,
+                                          rows, D));
+    hipLaunchKernelGGL((colsum_kernel<__hip_bfloat16>), dim3((D + 255) / 256), dim3(256), 0, s, part, P, D,
+                       (__hip_bfloat16*)dw);
+  }
+  return hipGetLastError();
+}
+
+hipError_t cs_swiglu_fwd(int dt, const void* a, const void* b, void* out, size_t n, hipStream_t s) {
+  CS_DT_DISPATCH(dt, hipLaunchKernelGGL((swiglu_fwd_kernel<T>), dim3(grid_for(n)), dim3(256), 0, s, (const T*)a,
+                                        (const T*)b, (T*)out, n));
+  return hipGetLastError();
+}
+
+hipError_t cs_swiglu_bwd(int dt, const void* a, const void* b, const void* g, void* da, void* db, size_t n,
+                         hipStream_t s) {
+  CS_DT_DISPATCH(dt, hipLaunchKernelGGL((swiglu_bwd_kernel<T>), dim3(grid_for(n)), dim3(256), 0, s, (const T*)a,
+                                        (const T*)b, (const T*)g, (T*)da, (T*)db, n));
+  return hipGetLastError();
+}
+
+hipError_t cs_rope(int dt, const void* x, const float* cosv, const float* sinv, void* out, int B, int S, int H, int hd,
+                   int inverse, hipStream_t s) {
+  if (hd & 1) return hipErrorInvalidValue;
+  const size_t npairs = (size_t)B * S * H * (hd / 2);
+  if (npairs == 0) return hipSuccess;
+  CS_DT_DISPATCH(dt, hipLaunchKernelGGL((rope_kernel<T>), dim3(grid_for(npairs)), dim3(256), 0, s, (const T*)x, cosv,
+                                        sinv, (T*)out, S, H, hd, npairs, inverse ? -1.f : 1.f));
+  return hipGetLastError();
+}
