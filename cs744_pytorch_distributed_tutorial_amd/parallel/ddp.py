@@ -58,7 +58,11 @@ class DistributedDataParallel(nn.Module):
         for b in self.buckets:
             for i, off in zip(b.param_indices, b.param_offsets):
                 p = self._params[i]
-                self._views[i] = self.flat_grad[off:off + p.numel()].view_as(p)
+                seg = self.flat_grad[off:off + p.numel()]
+                # keep the parameter's own dense layout (channels_last conv weights), so the
+                # gradient, the parameter and the fused optimizer's state all share strides
+                self._views[i] = seg.as_strided(p.shape, p.stride()) if p.dim() == 4 and \
+                    p.is_contiguous(memory_format=torch.channels_last) else seg.view_as(p)
                 self._bucket_of[i] = b.index
         self._attach_grad_views(zero=True)
         self._pending = [0] * len(self.buckets)

@@ -55,7 +55,14 @@ torch::Tensor sgd_multi_table(std::vector<torch::Tensor> ps, std::vector<torch::
   int64_t* h = host.data_ptr<int64_t>();
   int64_t chunks = 0;
   for (int64_t i = 0; i < nt; ++i) {
-    for (auto* t : {&ps[i], &gs[i], &ms[i]}) { CS_CHECK_CUDA(*t); CS_CHECK_F32(*t); CS_CHECK_CONTIG(*t); }
+    // the update is elementwise: any dense layout works as long as p, g and m share it
+    // (channels_last conv weights of the CNN models are dense but not "contiguous")
+    for (auto* t : {&ps[i], &gs[i], &ms[i]}) {
+      CS_CHECK_CUDA(*t); CS_CHECK_F32(*t);
+      TORCH_CHECK(t->is_non_overlapping_and_dense(), "sgd_multi_table: tensors must be dense");
+    }
+    TORCH_CHECK(ps[i].strides() == gs[i].strides() && ps[i].strides() == ms[i].strides(),
+                "sgd_multi_table: param, grad and momentum must share one memory layout");
     TORCH_CHECK(ps[i].numel() == gs[i].numel() && ps[i].numel() == ms[i].numel(), "sgd_multi_table: numel");
     h[i * 4 + 0] = (int64_t)ps[i].data_ptr<float>();
     h[i * 4 + 1] = (int64_t)gs[i].data_ptr<float>();

@@ -65,7 +65,7 @@ struct Loader {
   // per-thread precomputed row info for K-contiguous A rows (FWD/DGRAD: pixel rows)
   int a_b[T::AC], a_h[T::AC], a_w[T::AC];
   bool a_ok[T::AC];
-  float4 ra[T::AC], rb[T::BC];
+  float4 ra[2][T::AC], rb[2][T::BC];  // two register stages (tile k+1 and k+2 in flight)
 
   __device__ void init(const CsConvArgs& a, int m0) {
     if constexpr (T::A_KC) {
@@ -78,97 +78,156 @@ struct Loader {
     }
   }
 
+  // Branch-free loads: an out-of-range / padding element loads from the (valid) base
+  // pointer and is zeroed at store time through its flag, so every load is issued
+  // unconditionally and the compiler can count outstanding loads exactly (partial
+  // vmcnt) instead of draining the queue around exec-masked branches.
+  bool oka[2][T::AC], okb[2][T::BC];
+
+  template <int S>
   __device__ void load(const CsConvArgs& a, int m0, int n0, int k0) {
-    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
     // ---------------- A operand
 #pragma unroll
     for (int i = 0; i < T::AC; ++i) {
       const int q = threadIdx.x + 256 * i;
-      float4 v = z4;
+      size_t off = 0;
+      bool ok;
+      const float* src;
       if constexpr (MODE == CS_CONV_FWD || MODE == CS_CONV_DGRAD) {
         const int c = q % T::KQ, kk = k0 + 4 * c;
         const int lgC = (MODE == CS_CONV_FWD) ? a.lgCin : a.lgCout;
         const int tap = kk >> lgC, ch = kk & ((1 << lgC) - 1);
-        if (a_ok[i] && tap < 9) {
-          const int t3 = tap / 3, dh = t3 - 1, dw = tap - 3 * t3 - 1;
-          const int hh = (MODE == CS_CONV_FWD) ? a_h[i] + dh : a_h[i] - dh;
-          const int ww = (MODE == CS_CONV_FWD) ? a_w[i] + dw : a_w[i] - dw;
-          if ((unsigned)hh < (unsigned)a.H && (unsigned)ww < (unsigned)a.W) {
-            const float* src = (MODE == CS_CONV_FWD) ? a.x : a.dz;
-            v = *reinterpret_cast<const float4*>(src + ((((size_t)a_b[i] * a.H + hh) * a.W + ww) << lgC) + ch);
-          }
-        }
+        const int t3 = tap / 3, dh = t3 - 1, dw = tap - 3 * t3 - 1;
+        const int hh = (MODE == CS_CONV_FWD) ? a_h[i] + dh : a_h[i] - dh;
+        const int ww = (MODE == CS_CONV_FWD) ? a_w[i] + dw : a_w[i] - dw;
+        ok = a_ok[i] && tap < 9 && (unsigned)hh < (unsigned)a.H && (unsigned)ww < (unsigned)a.W;
+        src = (MODE == CS_CONV_FWD) ? a.x : a.dz;
+        if (ok) off = ((((size_t)a_b[i] * a.H + hh) * a.W + ww) << lgC) + ch;
       } else {  // WGRAD: A[k = pixel][m' = cout]  (K-major staging)
         constexpr int CPR = BM / 4;
         const int kr = q / CPR, c = q - kr * CPR, p = k0 + kr;
-        if (p < a.K && m0 + 4 * c < a.M)
-          v = *reinterpret_cast<const float4*>(a.dz + ((size_t)p << a.lgCout) + m0 + 4 * c);
+        ok = p < a.K && m0 + 4 * c < a.M;
+        src = a.dz;
+        if (ok) off = ((size_t)p << a.lgCout) + m0 + 4 * c;
       }
-      ra[i] = v;
+      ra[S][i] = *reinterpret_cast<const float4*>(src + off);
+      oka[S][i] = ok;
     }
     // ---------------- B operand
 #pragma unroll
     for (int i = 0; i < T::BC; ++i) {
       const int q = threadIdx.x + 256 * i;
-      float4 v = z4;
+      size_t off = 0;
+      bool ok;
       if constexpr (MODE == CS_CONV_FWD) {
         const int row = q / T::KQ, c = q % T::KQ, n = n0 + row, kk = k0 + 4 * c;
-        if (n < a.N && kk < a.K) {
-          if (!a.w_oihw) {
-            v = *reinterpret_cast<const float4*>(a.w + (size_t)n * a.K + kk);
-          } else {  // conv0: OIHW [Cout][3][3x3], K = 9 taps x 4 (padded) channels
-            const int tap = kk >> 2;
-            const float* wr = a.w + (size_t)n * 27 + tap;
-            v = make_float4(wr[0], wr[9], wr[18], 0.f);
-          }
+        ok = n < a.N && kk < a.K;
+        if (!a.w_oihw) {
+          if (ok) off = (size_t)n * a.K + kk;
+          rb[S][i] = *reinterpret_cast<const float4*>(a.w + off);
+        } else {  // conv0: OIHW [Cout][3][3x3], K = 9 taps x 4 (padded) channels
+          if (ok) off = (size_t)n * 27 + (kk >> 2);
+          const float* wr = a.w + off;
+          rb[S][i] = make_float4(wr[0], wr[9], wr[18], 0.f);
         }
       } else if constexpr (MODE == CS_CONV_DGRAD) {  // B[k = (tap, cout)][n = cin]
         constexpr int CPR = BN / 4;
         const int kr = q / CPR, c = q - kr * CPR, kk = k0 + kr;
         const int tap = kk >> a.lgCout, co = kk & (a.Cout - 1);
-        if (kk < a.K && n0 + 4 * c < a.N)
-          v = *reinterpret_cast<const float4*>(a.w + ((size_t)co * 9 + tap) * a.Cin + n0 + 4 * c);
+        ok = kk < a.K && n0 + 4 * c < a.N;
+        if (ok) off = ((size_t)co * 9 + tap) * a.Cin + n0 + 4 * c;
+        rb[S][i] = *reinterpret_cast<const float4*>(a.w + off);
       } else {  // WGRAD: B[k = pixel][n' = (tap, cin)]
         constexpr int CPR = BN / 4;
         const int kr = q / CPR, c = q - kr * CPR, p = k0 + kr, nn = n0 + 4 * c;
         const int tap = nn >> a.lgCin, ci = nn & (a.Cin - 1);
-        if (p < a.K && nn < a.N && tap < 9) {
-          int b, h, w;
-          pix_decode(p, a, b, h, w);
-          const int t3 = tap / 3, hh = h + t3 - 1, ww = w + (tap - 3 * t3) - 1;
-          if ((unsigned)hh < (unsigned)a.H && (unsigned)ww < (unsigned)a.W)
-            v = *reinterpret_cast<const float4*>(a.x + ((((size_t)b * a.H + hh) * a.W + ww) << a.lgCin) + ci);
-        }
+        int b, h, w;
+        pix_decode(p, a, b, h, w);
+        const int t3 = tap / 3, hh = h + t3 - 1, ww = w + (tap - 3 * t3) - 1;
+        ok = p < a.K && nn < a.N && tap < 9 && (unsigned)hh < (unsigned)a.H && (unsigned)ww < (unsigned)a.W;
+        if (ok) off = ((((size_t)b * a.H + hh) * a.W + ww) << a.lgCin) + ci;
+        rb[S][i] = *reinterpret_cast<const float4*>(a.x + off);
       }
-      rb[i] = v;
+      okb[S][i] = ok;
     }
   }
 
+  __device__ static float4 keep(float4 v, bool ok) {
+    return ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+
+  template <int S>
   __device__ void store(float* As, float* Bs) const {
 #pragma unroll
     for (int i = 0; i < T::AC; ++i) {
       const int q = threadIdx.x + 256 * i;
       if constexpr (T::A_KC) {
-        *reinterpret_cast<float4*>(As + (q / T::KQ) * (BK + 4) + 4 * (q % T::KQ)) = ra[i];
+        *reinterpret_cast<float4*>(As + (q / T::KQ) * (BK + 4) + 4 * (q % T::KQ)) = keep(ra[S][i], oka[S][i]);
       } else {
         constexpr int CPR = BM / 4;
         const int kr = q / CPR, c = q - kr * CPR;
-        *reinterpret_cast<float4*>(As + kr * (BM + 4) + 4 * c) = ra[i];
+        *reinterpret_cast<float4*>(As + kr * (BM + 4) + 4 * c) = keep(ra[S][i], oka[S][i]);
       }
     }
 #pragma unroll
     for (int i = 0; i < T::BC; ++i) {
       const int q = threadIdx.x + 256 * i;
       if constexpr (T::B_KC) {
-        *reinterpret_cast<float4*>(Bs + (q / T::KQ) * (BK + 4) + 4 * (q % T::KQ)) = rb[i];
+        *reinterpret_cast<float4*>(Bs + (q / T::KQ) * (BK + 4) + 4 * (q % T::KQ)) = keep(rb[S][i], okb[S][i]);
       } else {
         constexpr int CPR = BN / 4;
         const int kr = q / CPR, c = q - kr * CPR;
-        *reinterpret_cast<float4*>(Bs + kr * (BN + 4) + 4 * c) = rb[i];
+        *reinterpret_cast<float4*>(Bs + kr * (BN + 4) + 4 * c) = keep(rb[S][i], okb[S][i]);
       }
     }
   }
 };
+
+// One K-step on a staged LDS tile: every fragment read is issued first (one
+// lgkmcnt wait), then the BK/2 x RM x RN MFMA chain runs back to back.
+template <int BM, int BN, int MODE, int BK>
+__device__ __forceinline__ void mma_stage(const float* __restrict__ As, const float* __restrict__ Bs,
+                                          f32x16 (&acc)[Tile<BM, BN, MODE, BK>::RM][Tile<BM, BN, MODE, BK>::RN],
+                                          int wm, int wn, int r, int hh) {
+  using T = Tile<BM, BN, MODE, BK>;
+  float af[T::RM][T::HK], bf[T::RN][T::HK];
+#pragma unroll
+  for (int i = 0; i < T::RM; ++i) {
+    const int row = wm * T::WM + i * 32 + r;
+    if constexpr (T::A_KC) {
+#pragma unroll
+      for (int c4 = 0; c4 < T::HK / 4; ++c4) {
+        const float4 v = *reinterpret_cast<const float4*>(As + row * (BK + 4) + T::HK * hh + 4 * c4);
+        af[i][4 * c4 + 0] = v.x; af[i][4 * c4 + 1] = v.y; af[i][4 * c4 + 2] = v.z; af[i][4 * c4 + 3] = v.w;
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < T::HK; ++s) af[i][s] = As[(T::HK * hh + s) * (BM + 4) + row];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < T::RN; ++j) {
+    const int col = wn * T::WN + j * 32 + r;
+    if constexpr (T::B_KC) {
+#pragma unroll
+      for (int c4 = 0; c4 < T::HK / 4; ++c4) {
+        const float4 v = *reinterpret_cast<const float4*>(Bs + col * (BK + 4) + T::HK * hh + 4 * c4);
+        bf[j][4 * c4 + 0] = v.x; bf[j][4 * c4 + 1] = v.y; bf[j][4 * c4 + 2] = v.z; bf[j][4 * c4 + 3] = v.w;
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < T::HK; ++s) bf[j][s] = Bs[(T::HK * hh + s) * (BN + 4) + col];
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int s = 0; s < T::HK; ++s)
+#pragma unroll
+    for (int i = 0; i < T::RM; ++i)
+#pragma unroll
+      for (int j = 0; j < T::RN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][s], bf[j][s], acc[i][j], 0, 0, 0);
+}
 
 template <int BM, int BN, int MODE, int BK>
 __global__ __launch_bounds__(256) void conv_gemm_kernel(CsConvArgs a) {
@@ -197,58 +256,31 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(CsConvArgs a) {
 
   Loader<BM, BN, MODE, BK> ld;
   ld.init(a, m0);
-  float* stage0 = smem;
-  float* stage1 = smem + T::STAGE;
-  if (ks_begin < ks_end) {
-    ld.load(a, m0, n0, ks_begin * BK);
-    ld.store(stage0, stage0 + T::A_ELEMS);
+  float* lds0 = smem;
+  float* lds1 = smem + T::STAGE;
+  // Pipeline: LDS double buffer + two register stages, so a tile's global loads are
+  // issued two K-steps before its LDS store (they survive the plain s_barrier; the
+  // store waits with a partial vmcnt that leaves the newer stage in flight).
+  // Unrolled by two so every register-stage index is a compile-time constant.
+  const int nks = ks_end - ks_begin;
+  if (nks > 0) {
+    ld.template load<0>(a, m0, n0, ks_begin * BK);
+    ld.template store<0>(lds0, lds0 + T::A_ELEMS);
+    if (nks > 1) ld.template load<1>(a, m0, n0, (ks_begin + 1) * BK);
   }
   __syncthreads();
-  int cur = 0;
-  for (int ks = ks_begin; ks < ks_end; ++ks) {
-    const bool more = ks + 1 < ks_end;
-    if (more) ld.load(a, m0, n0, (ks + 1) * BK);
-    const float* As = cur ? stage1 : stage0;
-    const float* Bs = As + T::A_ELEMS;
-    float af[T::RM][T::HK], bf[T::RN][T::HK];
-#pragma unroll
-    for (int i = 0; i < T::RM; ++i) {
-      const int row = wm * T::WM + i * 32 + r;
-      if constexpr (T::A_KC) {
-#pragma unroll
-        for (int c4 = 0; c4 < T::HK / 4; ++c4) {
-          const float4 v = *reinterpret_cast<const float4*>(As + row * (BK + 4) + T::HK * hh + 4 * c4);
-          af[i][4 * c4 + 0] = v.x; af[i][4 * c4 + 1] = v.y; af[i][4 * c4 + 2] = v.z; af[i][4 * c4 + 3] = v.w;
-        }
-      } else {
-#pragma unroll
-        for (int s = 0; s < T::HK; ++s) af[i][s] = As[(T::HK * hh + s) * (BM + 4) + row];
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < T::RN; ++j) {
-      const int col = wn * T::WN + j * 32 + r;
-      if constexpr (T::B_KC) {
-#pragma unroll
-        for (int c4 = 0; c4 < T::HK / 4; ++c4) {
-          const float4 v = *reinterpret_cast<const float4*>(Bs + col * (BK + 4) + T::HK * hh + 4 * c4);
-          bf[j][4 * c4 + 0] = v.x; bf[j][4 * c4 + 1] = v.y; bf[j][4 * c4 + 2] = v.z; bf[j][4 * c4 + 3] = v.w;
-        }
-      } else {
-#pragma unroll
-        for (int s = 0; s < T::HK; ++s) bf[j][s] = Bs[(T::HK * hh + s) * (BN + 4) + col];
-      }
-    }
-#pragma unroll
-    for (int s = 0; s < T::HK; ++s)
-#pragma unroll
-      for (int i = 0; i < T::RM; ++i)
-#pragma unroll
-        for (int j = 0; j < T::RN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][s], bf[j][s], acc[i][j], 0, 0, 0);
-    if (more) ld.store(cur ? stage0 : stage1, (cur ? stage0 : stage1) + T::A_ELEMS);
+  for (int t = 0; t < nks; t += 2) {
+    // even step: tile t in lds0, tile t+1 in registers[1]
+    if (t + 2 < nks) ld.template load<0>(a, m0, n0, (ks_begin + t + 2) * BK);
+    mma_stage<BM, BN, MODE, BK>(lds0, lds0 + T::A_ELEMS, acc, wm, wn, r, hh);
+    if (t + 1 < nks) ld.template store<1>(lds1, lds1 + T::A_ELEMS);
     __syncthreads();
-    cur ^= 1;
+    if (t + 1 >= nks) break;
+    // odd step: tile t+1 in lds1, tile t+2 in registers[0]
+    if (t + 3 < nks) ld.template load<1>(a, m0, n0, (ks_begin + t + 3) * BK);
+    mma_stage<BM, BN, MODE, BK>(lds1, lds1 + T::A_ELEMS, acc, wm, wn, r, hh);
+    if (t + 2 < nks) ld.template store<0>(lds0, lds0 + T::A_ELEMS);
+    __syncthreads();
   }
 
   // ------------------------------------------------------------------ epilogue
