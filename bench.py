@@ -54,7 +54,8 @@ def parse(argv=None):
     p.add_argument("--sync", type=str, default="ddp",
                    choices=["ddp", "allreduce", "gather_scatter", "p2p", "flat"])
     p.add_argument("--comm", type=str, default="rccl", choices=["torch", "rccl"])
-    p.add_argument("--bucket-mb", type=float, default=9.0)
+    p.add_argument("--bucket-mb", type=float, default=4.0,
+                   help="DDP bucket cap; buckets close at layer boundaries (VGG-11: 9|9|9|4.5|3.7 MiB)")
     p.add_argument("--bucket-policy", type=str, default="layer", choices=["size", "layer", "single"])
     p.add_argument("--dtype", type=str, default="fp32", choices=["fp32", "bf16"])
     p.add_argument("--seq-len", type=int, default=0, help="decoder LM sequence length")
@@ -149,6 +150,8 @@ def main(argv=None) -> int:
         if args.json_out:
             with open(args.json_out, "a") as f:
                 f.write(line + "\n")
+    if hasattr(trainer, "close"):
+        trainer.close()
     if world > 1:
         D.barrier()
         D.destroy_process_group()

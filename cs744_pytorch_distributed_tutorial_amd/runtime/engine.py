@@ -166,7 +166,7 @@ class NativeTrainer:
     """VGG training on the native engine; one instance per rank (one GPU per process)."""
 
     def __init__(self, model: str = "VGG11", batch_size: int = 64, device: Optional[torch.device] = None,
-                 rank: int = 0, world: int = 1, sync: str = "ddp", comm: str = "rccl", bucket_mb: float = 9.0,
+                 rank: int = 0, world: int = 1, sync: str = "ddp", comm: str = "rccl", bucket_mb: float = 4.0,
                  graph: str = "auto", lr: float = 0.1, momentum: float = 0.9, weight_decay: float = 1e-4,
                  dampening: float = 0.0, seed: int = 5000, data_seed: int = 0, train_size: Optional[int] = None,
                  test_size: Optional[int] = None, autotune: bool = True, broadcast_buffers: bool = True,
@@ -446,6 +446,20 @@ class NativeTrainer:
                     self.layout.view(self.mom, n).copy_(st["momentum_buffer"])
             if sd["state"]:
                 self.global_step = max(self.global_step, 1)
+
+    def close(self) -> None:
+        """Release graphs, the engine and the native communicator deterministically (before the
+        process group is torn down), instead of leaving ncclCommDestroy to interpreter exit."""
+        torch.cuda.synchronize()
+        self._graphs = None
+        self.engine = None
+        if self.native_comm is not None:
+            self.comm.join()
+            torch.cuda.synchronize()
+            self.comm.native = None
+            self.native_comm = None
+        import gc
+        gc.collect()
 
     def grads_state(self) -> Dict[str, torch.Tensor]:
         return self.layout.unpack_grads(self.grads)

@@ -18,6 +18,8 @@
 // Split-K over blockIdx.z writes fp32 slabs that `splitk_reduce` sums in a fixed
 // order (deterministic, no float atomics). Tiles are dealt to XCDs in contiguous
 // ranges (common.h xcd_remap) so neighbouring tiles share an L2.
+#include <stdlib.h>
+
 #include "common.h"
 #include "launchers.h"
 
@@ -185,7 +187,7 @@ struct Loader {
 
 // One K-step on a staged LDS tile: every fragment read is issued first (one
 // lgkmcnt wait), then the BK/2 x RM x RN MFMA chain runs back to back.
-template <int BM, int BN, int MODE, int BK>
+template <int BM, int BN, int MODE, int BK, int SCHED>
 __device__ __forceinline__ void mma_stage(const float* __restrict__ As, const float* __restrict__ Bs,
                                           f32x16 (&acc)[Tile<BM, BN, MODE, BK>::RM][Tile<BM, BN, MODE, BK>::RN],
                                           int wm, int wn, int r, int hh) {
@@ -219,7 +221,7 @@ __device__ __forceinline__ void mma_stage(const float* __restrict__ As, const fl
       for (int s = 0; s < T::HK; ++s) bf[j][s] = Bs[(T::HK * hh + s) * (BN + 4) + col];
     }
   }
-  __builtin_amdgcn_sched_barrier(0);
+  if constexpr (SCHED != 1) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int s = 0; s < T::HK; ++s)
 #pragma unroll
@@ -229,7 +231,12 @@ __device__ __forceinline__ void mma_stage(const float* __restrict__ As, const fl
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][s], bf[j][s], acc[i][j], 0, 0, 0);
 }
 
-template <int BM, int BN, int MODE, int BK>
+// SCHED: instruction-schedule variant of the main loop (A/B-tested on MI355X):
+//   0 = next tile's loads, then fragment reads, sched barrier, MFMA chain
+//   1 = same without the sched barrier (compiler interleaves freely)
+//   2 = fragment reads, MFMA chain, then the next tile's loads (their address VALU
+//       overlaps the tail of the matrix pipe)
+template <int BM, int BN, int MODE, int BK, int SCHED>
 __global__ __launch_bounds__(256) void conv_gemm_kernel(CsConvArgs a) {
   using T = Tile<BM, BN, MODE, BK>;
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -271,14 +278,16 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(CsConvArgs a) {
   __syncthreads();
   for (int t = 0; t < nks; t += 2) {
     // even step: tile t in lds0, tile t+1 in registers[1]
-    if (t + 2 < nks) ld.template load<0>(a, m0, n0, (ks_begin + t + 2) * BK);
-    mma_stage<BM, BN, MODE, BK>(lds0, lds0 + T::A_ELEMS, acc, wm, wn, r, hh);
+    if (SCHED != 2 && t + 2 < nks) ld.template load<0>(a, m0, n0, (ks_begin + t + 2) * BK);
+    mma_stage<BM, BN, MODE, BK, SCHED>(lds0, lds0 + T::A_ELEMS, acc, wm, wn, r, hh);
+    if (SCHED == 2 && t + 2 < nks) ld.template load<0>(a, m0, n0, (ks_begin + t + 2) * BK);
     if (t + 1 < nks) ld.template store<1>(lds1, lds1 + T::A_ELEMS);
     __syncthreads();
     if (t + 1 >= nks) break;
     // odd step: tile t+1 in lds1, tile t+2 in registers[0]
-    if (t + 3 < nks) ld.template load<1>(a, m0, n0, (ks_begin + t + 3) * BK);
-    mma_stage<BM, BN, MODE, BK>(lds1, lds1 + T::A_ELEMS, acc, wm, wn, r, hh);
+    if (SCHED != 2 && t + 3 < nks) ld.template load<1>(a, m0, n0, (ks_begin + t + 3) * BK);
+    mma_stage<BM, BN, MODE, BK, SCHED>(lds1, lds1 + T::A_ELEMS, acc, wm, wn, r, hh);
+    if (SCHED == 2 && t + 3 < nks) ld.template load<1>(a, m0, n0, (ks_begin + t + 3) * BK);
     if (t + 2 < nks) ld.template store<0>(lds0, lds0 + T::A_ELEMS);
     __syncthreads();
   }
@@ -501,12 +510,26 @@ hipError_t launch_reduce(const CsConvArgs& a, int mode, int splits, hipStream_t 
   return hipGetLastError();
 }
 
+int conv_sched() {
+  static int v = [] {
+    const char* e = getenv("CS_CONV_SCHED");
+    return e ? atoi(e) : 1;  // default: measured 3-5% faster than 0 and 2 on MI355X
+  }();
+  return v;
+}
+
 template <int BM, int BN, int MODE, int BK>
 hipError_t launch_gemm(const CsConvArgs& a, int splits, hipStream_t stream) {
   using T = Tile<BM, BN, MODE, BK>;
   const int ntiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
   const size_t lds = 2 * T::STAGE * sizeof(float);
-  hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, MODE, BK>), dim3(ntiles, 1, splits), dim3(256), lds, stream, a);
+  const dim3 grid(ntiles, 1, splits);
+  switch (conv_sched()) {
+    case 1: hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, MODE, BK, 1>), grid, dim3(256), lds, stream, a); break;
+    case 2: hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, MODE, BK, 2>), grid, dim3(256), lds, stream, a); break;
+    case 0: hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, MODE, BK, 0>), grid, dim3(256), lds, stream, a); break;
+    default: hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, MODE, BK, 1>), grid, dim3(256), lds, stream, a); break;
+  }
   return hipGetLastError();
 }
 
