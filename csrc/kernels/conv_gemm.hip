@@ -9,16 +9,30 @@
 //
 // Tiling: 256 threads = 4 waves (2x2), block tile BMxBN, K-step BK (16 or 32),
 // wave tile (BM/2)x(BN/2) built from 32x32 MFMA tiles. Global -> registers -> LDS
-// double buffer with one barrier per K-step; the next K-step's global loads are
-// issued before the current step's MFMAs so HBM/L2 latency hides under matrix work.
+// double buffer with one barrier per K-step and two register stages (a tile's
+// global loads are issued two K-steps before its LDS store).
+//
+// Addressing is built for the CDNA4 buffer unit, not for flat pointers:
+//  * every operand is read through a buffer resource (32-bit byte offsets, one
+//    SGPR descriptor per tensor); a padding / out-of-range element gets an offset
+//    past the descriptor's size, and the range check returns 0 — no selects, no
+//    branches, no 64-bit address math in the K loop;
+//  * the per-K-step part of every offset is wave-uniform (the 3x3 tap and the
+//    channel base of a K-step: BK divides the channel count), so it lives in an
+//    SGPR (added to the fixed per-thread part with one VALU add, so the range check
+//    sees the whole offset); per-thread parts (pixel row, channel lane) are fixed for the whole
+//    loop, and the padding test is one bit of a 9-bit per-row tap mask built once.
 // K is permuted inside a K-step so each lane's BK/2 A (and B) values are contiguous
-// in LDS: lane-half h feeds k = (BK/2)h + s at MFMA sub-step s, turning the operand
-// fetch into BK/8 ds_read_b128 per tile ([row][BK+4] padded rows), or BK/2
-// conflict-free ds_read_b32 for operands that are staged K-major ([k][rows+4]).
+// in LDS: lane-half h feeds k = (BK/2)h + s at MFMA sub-step s, so K-contiguous
+// operands ([row][BK+4] padded rows) are fetched with ds_read_b128 and K-major
+// operands ([k][rows+4]) with conflict-free ds_read_b32. The MFMA chain is
+// software-pipelined one 4-deep chunk ahead of its fragment reads.
 // Split-K over blockIdx.z writes fp32 slabs that `splitk_reduce` sums in a fixed
 // order (deterministic, no float atomics). Tiles are dealt to XCDs in contiguous
 // ranges (common.h xcd_remap) so neighbouring tiles share an L2.
 #include <stdlib.h>
+
+#include <algorithm>
 
 #include "common.h"
 #include "launchers.h"
@@ -26,11 +40,32 @@
 namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
 
-__device__ __forceinline__ void pix_decode(int p, const CsConvArgs& a, int& b, int& h, int& w) {
-  w = p & (a.W - 1);
-  h = (p >> a.lgW) & (a.H - 1);
-  b = p >> (a.lgW + a.lgH);
+// byte offset past every descriptor's range: loads return 0, stores are dropped
+constexpr int kOOB = 0x7ffffff0;
+
+__device__ __forceinline__ rsrc_t make_rsrc(const void* p, int64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+// the whole offset goes in voffset: the range check is only guaranteed to cover it
+__device__ __forceinline__ float4 bload4(rsrc_t r, int voff) {
+  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, 0));
+}
+__device__ __forceinline__ void bstore1(rsrc_t r, float v, int voff) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, voff, 0, 0);
+}
+
+// 9-bit mask of the 3x3 taps whose source pixel (h + s*dh, w + s*dw) is inside the image
+// (s = +1 for FWD / WGRAD, -1 for DGRAD's flipped kernel); bit t = tap t = 3*(dh+1)+(dw+1)
+__device__ __forceinline__ unsigned tap_mask(int h, int w, int H, int W, int s) {
+  unsigned m = 0;
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const int hh = h + s * (t / 3 - 1), ww = w + s * (t % 3 - 1);
+    if ((unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W) m |= 1u << t;
+  }
+  return m;
 }
 
 template <int MODE>
@@ -58,185 +93,221 @@ struct Tile {
   static constexpr int BC = BN * BK / 1024;
   static constexpr int KQ = BK / 4;          // float4 chunks per K-contiguous row
   static constexpr int HK = BK / 2;          // MFMA sub-steps per K-step
+  static constexpr int NG = HK / 4;          // 4-deep sub-step chunks per K-step
   static constexpr int WM = BM / 2, WN = BN / 2, RM = WM / 32, RN = WN / 32;
 };
 
-template <int BM, int BN, int MODE, int BK>
+// C4: FWD of the padded conv0 (Cin = 4 < BK, OIHW weights) — a compile-time variant so
+// the common kernels carry no branch for it.
+template <int BM, int BN, int MODE, int BK, bool C4 = false>
 struct Loader {
   using T = Tile<BM, BN, MODE, BK>;
-  // per-thread precomputed row info for K-contiguous A rows (FWD/DGRAD: pixel rows)
-  int a_b[T::AC], a_h[T::AC], a_w[T::AC];
-  bool a_ok[T::AC];
-  float4 ra[2][T::AC], rb[2][T::BC];  // two register stages (tile k+1 and k+2 in flight)
+  rsrc_t ra_, rb_;
+  int av[T::AC], bv[T::BC];        // per-thread fixed byte offsets
+  unsigned am[T::AC], bm_[T::BC];  // per-thread tap masks / flags
+  int lds_a[T::AC], lds_b[T::BC];  // LDS float offsets of this thread's chunks
+  float4 ra[2][T::AC], rb[2][T::BC];
 
-  __device__ void init(const CsConvArgs& a, int m0) {
-    if constexpr (T::A_KC) {
-#pragma unroll
-      for (int i = 0; i < T::AC; ++i) {
-        const int q = threadIdx.x + 256 * i, row = q / T::KQ, m = m0 + row;
-        a_ok[i] = m < a.M;
-        pix_decode(a_ok[i] ? m : 0, a, a_b[i], a_h[i], a_w[i]);
-      }
-    }
-  }
-
-  // Branch-free loads: an out-of-range / padding element loads from the (valid) base
-  // pointer and is zeroed at store time through its flag, so every load is issued
-  // unconditionally and the compiler can count outstanding loads exactly (partial
-  // vmcnt) instead of draining the queue around exec-masked branches.
-  bool oka[2][T::AC], okb[2][T::BC];
-
-  template <int S>
-  __device__ void load(const CsConvArgs& a, int m0, int n0, int k0) {
-    // ---------------- A operand
+  __device__ void init(const CsConvArgs& a, int m0, int n0) {
+    const int pix = a.B * a.H * a.W;
+    const int64_t xbytes = (int64_t)pix * a.Cin * 4, zbytes = (int64_t)pix * a.Cout * 4;
+    const int64_t wbytes = (a.w_oihw ? (int64_t)a.Cout * 27 : (int64_t)a.Cout * 9 * a.Cin) * 4;
 #pragma unroll
     for (int i = 0; i < T::AC; ++i) {
       const int q = threadIdx.x + 256 * i;
-      size_t off = 0;
-      bool ok;
-      const float* src;
-      if constexpr (MODE == CS_CONV_FWD || MODE == CS_CONV_DGRAD) {
-        const int c = q % T::KQ, kk = k0 + 4 * c;
+      if constexpr (T::A_KC) {  // FWD / DGRAD: A[m = pixel][k = (tap, ch)], one pixel row per chunk
+        const int row = q / T::KQ, c = q % T::KQ, m = m0 + row;
+        const int w = m & (a.W - 1), h = (m >> a.lgW) & (a.H - 1);
         const int lgC = (MODE == CS_CONV_FWD) ? a.lgCin : a.lgCout;
-        const int tap = kk >> lgC, ch = kk & ((1 << lgC) - 1);
-        const int t3 = tap / 3, dh = t3 - 1, dw = tap - 3 * t3 - 1;
-        const int hh = (MODE == CS_CONV_FWD) ? a_h[i] + dh : a_h[i] - dh;
-        const int ww = (MODE == CS_CONV_FWD) ? a_w[i] + dw : a_w[i] - dw;
-        ok = a_ok[i] && tap < 9 && (unsigned)hh < (unsigned)a.H && (unsigned)ww < (unsigned)a.W;
-        src = (MODE == CS_CONV_FWD) ? a.x : a.dz;
-        if (ok) off = ((((size_t)a_b[i] * a.H + hh) * a.W + ww) << lgC) + ch;
-      } else {  // WGRAD: A[k = pixel][m' = cout]  (K-major staging)
+        am[i] = m < a.M ? tap_mask(h, w, a.H, a.W, MODE == CS_CONV_FWD ? 1 : -1) : 0u;
+        av[i] = ((m << lgC) + 4 * c) * 4;
+        lds_a[i] = row * (BK + 4) + 4 * c;
+      } else {  // WGRAD: A[m = cout][k = pixel] from dZ [pixel][cout], K-major staging
         constexpr int CPR = BM / 4;
-        const int kr = q / CPR, c = q - kr * CPR, p = k0 + kr;
-        ok = p < a.K && m0 + 4 * c < a.M;
-        src = a.dz;
-        if (ok) off = ((size_t)p << a.lgCout) + m0 + 4 * c;
+        const int kr = q / CPR, c = q - kr * CPR;
+        am[i] = (m0 + 4 * c < a.M) ? 1u : 0u;
+        av[i] = ((kr << a.lgCout) + m0 + 4 * c) * 4;
+        lds_a[i] = kr * (BM + 4) + 4 * c;
       }
-      ra[S][i] = *reinterpret_cast<const float4*>(src + off);
-      oka[S][i] = ok;
+    }
+#pragma unroll
+    for (int i = 0; i < T::BC; ++i) {
+      const int q = threadIdx.x + 256 * i;
+      if constexpr (MODE == CS_CONV_FWD) {  // B[n = cout][k]: weights [Cout][K] (K-contiguous)
+        const int row = q / T::KQ, c = q % T::KQ, n = n0 + row;
+        bm_[i] = n < a.N ? 1u : 0u;
+        bv[i] = C4 ? (n * 27 + c) : (n * a.K + 4 * c) * 4;  // conv0: element index (gather path)
+        lds_b[i] = row * (BK + 4) + 4 * c;
+      } else if constexpr (MODE == CS_CONV_DGRAD) {  // B[k = (tap, cout)][n = cin]: OHWI weights, K-major
+        constexpr int CPR = BN / 4;
+        const int kr = q / CPR, c = q - kr * CPR;
+        bm_[i] = (n0 + 4 * c < a.N) ? 1u : 0u;
+        bv[i] = (kr * 9 * a.Cin + n0 + 4 * c) * 4;
+        lds_b[i] = kr * (BN + 4) + 4 * c;
+      } else {  // WGRAD: B[k = pixel][n = (tap, cin)] = X[pixel + tap shift][cin], K-major
+        constexpr int CPR = BN / 4;
+        const int kr = q / CPR, c = q - kr * CPR, nn = n0 + 4 * c;
+        const int tap = nn >> a.lgCin, ci = nn & (a.Cin - 1);
+        const int t3 = tap / 3, dh = t3 - 1, dw = tap - 3 * t3 - 1;
+        // flag bits: [0] column valid, [4..] signed tap delta (dh, dw) packed as (dh+1)*3+(dw+1)
+        bm_[i] = (nn < a.N && tap < 9) ? (1u | ((unsigned)tap << 4)) : 0u;
+        bv[i] = (((dh * a.W + dw) << a.lgCin) + ci) * 4;  // + (pixel << lgCin)*4 per K-step
+        lds_b[i] = kr * (BN + 4) + 4 * c;
+      }
+    }
+    if constexpr (MODE == CS_CONV_FWD) {
+      ra_ = make_rsrc(a.x, xbytes);
+      rb_ = make_rsrc(a.w, wbytes);
+    } else if constexpr (MODE == CS_CONV_DGRAD) {
+      ra_ = make_rsrc(a.dz, zbytes);
+      rb_ = make_rsrc(a.w, wbytes);
+    } else {
+      ra_ = make_rsrc(a.dz, (int64_t)a.K * a.Cout * 4);  // pixels >= K fall off the end: zero
+      rb_ = make_rsrc(a.x, xbytes);
+    }
+  }
+
+  template <int S>
+  __device__ __forceinline__ void load(const CsConvArgs& a, int k0) {
+    // ---------------- A operand
+    if constexpr (T::A_KC) {
+      const int lgC = (MODE == CS_CONV_FWD) ? a.lgCin : a.lgCout;
+      const int C = 1 << lgC;
+      if constexpr (!C4) {  // the whole K-step sits inside one tap (BK divides C): uniform
+        const int tap = k0 >> lgC, ch0 = k0 & (C - 1);
+        const int t3 = tap / 3, dh = t3 - 1, dw = tap - 3 * t3 - 1;
+        const int sh = (MODE == CS_CONV_FWD) ? (dh * a.W + dw) : -(dh * a.W + dw);
+        const int soff = ((sh << lgC) + ch0) * 4;
+#pragma unroll
+        for (int i = 0; i < T::AC; ++i) {
+          const int off = ((am[i] >> tap) & 1u) ? av[i] + soff : kOOB;
+          ra[S][i] = bload4(ra_, off);
+        }
+      } else {  // conv0 (C = 4 < BK): each float4 is its own tap
+#pragma unroll
+        for (int i = 0; i < T::AC; ++i) {
+          const int c = (threadIdx.x + 256 * i) % T::KQ;
+          const int tap = (k0 >> lgC) + c;
+          const int t3 = tap / 3, dh = t3 - 1, dw = tap - 3 * t3 - 1;
+          const int sh = (MODE == CS_CONV_FWD) ? (dh * a.W + dw) : -(dh * a.W + dw);
+          const int off = (tap < 9 && ((am[i] >> tap) & 1u)) ? av[i] - 16 * c + (sh << lgC) * 4 : kOOB;
+          ra[S][i] = bload4(ra_, off);
+        }
+      }
+    } else {  // WGRAD A: rows k0.. of dZ, uniform part k0*Cout
+      const int soff = (k0 << a.lgCout) * 4;
+#pragma unroll
+      for (int i = 0; i < T::AC; ++i) ra[S][i] = bload4(ra_, am[i] ? av[i] + soff : kOOB);
     }
     // ---------------- B operand
 #pragma unroll
     for (int i = 0; i < T::BC; ++i) {
-      const int q = threadIdx.x + 256 * i;
-      size_t off = 0;
-      bool ok;
       if constexpr (MODE == CS_CONV_FWD) {
-        const int row = q / T::KQ, c = q % T::KQ, n = n0 + row, kk = k0 + 4 * c;
-        ok = n < a.N && kk < a.K;
-        if (!a.w_oihw) {
-          if (ok) off = (size_t)n * a.K + kk;
-          rb[S][i] = *reinterpret_cast<const float4*>(a.w + off);
+        if constexpr (!C4) {  // K = 9*Cin is a multiple of BK
+          rb[S][i] = bload4(rb_, bm_[i] ? bv[i] + k0 * 4 : kOOB);
         } else {  // conv0: OIHW [Cout][3][3x3], K = 9 taps x 4 (padded) channels
-          if (ok) off = (size_t)n * 27 + (kk >> 2);
-          const float* wr = a.w + off;
-          rb[S][i] = make_float4(wr[0], wr[9], wr[18], 0.f);
+          const int tap = (k0 >> 2) + (threadIdx.x + 256 * i) % T::KQ;
+          const bool ok = bm_[i] && tap < 9;
+          const int e = bv[i] - ((threadIdx.x + 256 * i) % T::KQ) + tap;  // n*27 + tap
+          const float* wr = a.w + (ok ? e : 0);
+          rb[S][i] = ok ? make_float4(wr[0], wr[9], wr[18], 0.f) : make_float4(0.f, 0.f, 0.f, 0.f);
         }
-      } else if constexpr (MODE == CS_CONV_DGRAD) {  // B[k = (tap, cout)][n = cin]
-        constexpr int CPR = BN / 4;
-        const int kr = q / CPR, c = q - kr * CPR, kk = k0 + kr;
-        const int tap = kk >> a.lgCout, co = kk & (a.Cout - 1);
-        ok = kk < a.K && n0 + 4 * c < a.N;
-        if (ok) off = ((size_t)co * 9 + tap) * a.Cin + n0 + 4 * c;
-        rb[S][i] = *reinterpret_cast<const float4*>(a.w + off);
-      } else {  // WGRAD: B[k = pixel][n' = (tap, cin)]
-        constexpr int CPR = BN / 4;
-        const int kr = q / CPR, c = q - kr * CPR, p = k0 + kr, nn = n0 + 4 * c;
-        const int tap = nn >> a.lgCin, ci = nn & (a.Cin - 1);
-        int b, h, w;
-        pix_decode(p, a, b, h, w);
-        const int t3 = tap / 3, hh = h + t3 - 1, ww = w + (tap - 3 * t3) - 1;
-        ok = p < a.K && nn < a.N && tap < 9 && (unsigned)hh < (unsigned)a.H && (unsigned)ww < (unsigned)a.W;
-        if (ok) off = ((((size_t)b * a.H + hh) * a.W + ww) << a.lgCin) + ci;
-        rb[S][i] = *reinterpret_cast<const float4*>(a.x + off);
+      } else if constexpr (MODE == CS_CONV_DGRAD) {
+        const int tap = k0 >> a.lgCout, co0 = k0 & (a.Cout - 1);
+        const int soff = ((co0 * 9 + tap) << a.lgCin) * 4;
+        rb[S][i] = bload4(rb_, bm_[i] ? bv[i] + soff : kOOB);
+      } else {
+        const int q = threadIdx.x + 256 * i, kr = q / (BN / 4), p = k0 + kr;
+        const int w = p & (a.W - 1), h = (p >> a.lgW) & (a.H - 1);
+        const int tap = (int)(bm_[i] >> 4), t3 = tap / 3;
+        const int hh = h + t3 - 1, ww = w + (tap - 3 * t3) - 1;
+        const bool ok = (bm_[i] & 1u) && p < a.K && (unsigned)hh < (unsigned)a.H && (unsigned)ww < (unsigned)a.W;
+        rb[S][i] = bload4(rb_, ok ? bv[i] + ((p << a.lgCin) * 4) : kOOB);
       }
-      okb[S][i] = ok;
     }
-  }
-
-  __device__ static float4 keep(float4 v, bool ok) {
-    return ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
   }
 
   template <int S>
-  __device__ void store(float* As, float* Bs) const {
+  __device__ __forceinline__ void store(float* As, float* Bs) const {
 #pragma unroll
-    for (int i = 0; i < T::AC; ++i) {
-      const int q = threadIdx.x + 256 * i;
-      if constexpr (T::A_KC) {
-        *reinterpret_cast<float4*>(As + (q / T::KQ) * (BK + 4) + 4 * (q % T::KQ)) = keep(ra[S][i], oka[S][i]);
-      } else {
-        constexpr int CPR = BM / 4;
-        const int kr = q / CPR, c = q - kr * CPR;
-        *reinterpret_cast<float4*>(As + kr * (BM + 4) + 4 * c) = keep(ra[S][i], oka[S][i]);
-      }
-    }
+    for (int i = 0; i < T::AC; ++i) *reinterpret_cast<float4*>(As + lds_a[i]) = ra[S][i];
 #pragma unroll
-    for (int i = 0; i < T::BC; ++i) {
-      const int q = threadIdx.x + 256 * i;
-      if constexpr (T::B_KC) {
-        *reinterpret_cast<float4*>(Bs + (q / T::KQ) * (BK + 4) + 4 * (q % T::KQ)) = keep(rb[S][i], okb[S][i]);
-      } else {
-        constexpr int CPR = BN / 4;
-        const int kr = q / CPR, c = q - kr * CPR;
-        *reinterpret_cast<float4*>(Bs + kr * (BN + 4) + 4 * c) = keep(rb[S][i], okb[S][i]);
-      }
-    }
+    for (int i = 0; i < T::BC; ++i) *reinterpret_cast<float4*>(Bs + lds_b[i]) = rb[S][i];
   }
 };
 
-// One K-step on a staged LDS tile: every fragment read is issued first (one
-// lgkmcnt wait), then the BK/2 x RM x RN MFMA chain runs back to back.
-template <int BM, int BN, int MODE, int BK, int SCHED>
-__device__ __forceinline__ void mma_stage(const float* __restrict__ As, const float* __restrict__ Bs,
-                                          f32x16 (&acc)[Tile<BM, BN, MODE, BK>::RM][Tile<BM, BN, MODE, BK>::RN],
-                                          int wm, int wn, int r, int hh) {
+// Fragment reads of 4-deep sub-step chunk g (sub-steps 4g..4g+3) of one staged tile.
+template <int BM, int BN, int MODE, int BK>
+__device__ __forceinline__ void read_chunk(const float* __restrict__ As, const float* __restrict__ Bs, int g,
+                                           float (&af)[Tile<BM, BN, MODE, BK>::RM][4],
+                                           float (&bf)[Tile<BM, BN, MODE, BK>::RN][4], int wm, int wn, int r,
+                                           int hh) {
   using T = Tile<BM, BN, MODE, BK>;
-  float af[T::RM][T::HK], bf[T::RN][T::HK];
 #pragma unroll
   for (int i = 0; i < T::RM; ++i) {
     const int row = wm * T::WM + i * 32 + r;
     if constexpr (T::A_KC) {
-#pragma unroll
-      for (int c4 = 0; c4 < T::HK / 4; ++c4) {
-        const float4 v = *reinterpret_cast<const float4*>(As + row * (BK + 4) + T::HK * hh + 4 * c4);
-        af[i][4 * c4 + 0] = v.x; af[i][4 * c4 + 1] = v.y; af[i][4 * c4 + 2] = v.z; af[i][4 * c4 + 3] = v.w;
-      }
+      const float4 v = *reinterpret_cast<const float4*>(As + row * (BK + 4) + T::HK * hh + 4 * g);
+      af[i][0] = v.x; af[i][1] = v.y; af[i][2] = v.z; af[i][3] = v.w;
     } else {
 #pragma unroll
-      for (int s = 0; s < T::HK; ++s) af[i][s] = As[(T::HK * hh + s) * (BM + 4) + row];
+      for (int s = 0; s < 4; ++s) af[i][s] = As[(T::HK * hh + 4 * g + s) * (BM + 4) + row];
     }
   }
 #pragma unroll
   for (int j = 0; j < T::RN; ++j) {
     const int col = wn * T::WN + j * 32 + r;
     if constexpr (T::B_KC) {
-#pragma unroll
-      for (int c4 = 0; c4 < T::HK / 4; ++c4) {
-        const float4 v = *reinterpret_cast<const float4*>(Bs + col * (BK + 4) + T::HK * hh + 4 * c4);
-        bf[j][4 * c4 + 0] = v.x; bf[j][4 * c4 + 1] = v.y; bf[j][4 * c4 + 2] = v.z; bf[j][4 * c4 + 3] = v.w;
-      }
+      const float4 v = *reinterpret_cast<const float4*>(Bs + col * (BK + 4) + T::HK * hh + 4 * g);
+      bf[j][0] = v.x; bf[j][1] = v.y; bf[j][2] = v.z; bf[j][3] = v.w;
     } else {
 #pragma unroll
-      for (int s = 0; s < T::HK; ++s) bf[j][s] = Bs[(T::HK * hh + s) * (BN + 4) + col];
+      for (int s = 0; s < 4; ++s) bf[j][s] = Bs[(T::HK * hh + 4 * g + s) * (BN + 4) + col];
     }
   }
-  if constexpr (SCHED != 1) __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int RM, int RN>
+__device__ __forceinline__ void mma_chunk(const float (&af)[RM][4], const float (&bf)[RN][4],
+                                          f32x16 (&acc)[RM][RN]) {
 #pragma unroll
-  for (int s = 0; s < T::HK; ++s)
+  for (int s = 0; s < 4; ++s)
 #pragma unroll
-    for (int i = 0; i < T::RM; ++i)
+    for (int i = 0; i < RM; ++i)
 #pragma unroll
-      for (int j = 0; j < T::RN; ++j)
+      for (int j = 0; j < RN; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][s], bf[j][s], acc[i][j], 0, 0, 0);
 }
 
-// SCHED: instruction-schedule variant of the main loop (A/B-tested on MI355X):
-//   0 = next tile's loads, then fragment reads, sched barrier, MFMA chain
-//   1 = same without the sched barrier (compiler interleaves freely)
-//   2 = fragment reads, MFMA chain, then the next tile's loads (their address VALU
-//       overlaps the tail of the matrix pipe)
-template <int BM, int BN, int MODE, int BK, int SCHED>
+// One K-step on a staged LDS tile, with the next tiles' global loads (tile t+2 -> register
+// stage LS) and LDS store (tile t+1, register stage SS -> the other LDS buffer) folded in.
+// Both are unconditional (no branch around a load: hipcc would drain vmcnt there): past the
+// split's last K-step they fetch a neighbouring range or zeros (range check) into a
+// register stage / LDS buffer that is never read again.
+// SCHED 0: the MFMA chain runs one chunk behind its fragment reads; the global loads
+//          go out after the first chunk, the LDS store after the second (sched barriers
+//          pin the phases so hipcc cannot hoist every read ahead of the chain).
+// SCHED 1: same code order, compiler schedules freely.
+template <int BM, int BN, int MODE, int BK, int SCHED, int LS, int SS, bool C4>
+__device__ __forceinline__ void kstep(Loader<BM, BN, MODE, BK, C4>& ld, const CsConvArgs& a, const float* cur,
+                                      float* nxt, f32x16 (&acc)[Tile<BM, BN, MODE, BK>::RM][Tile<BM, BN, MODE, BK>::RN],
+                                      int wm, int wn, int r, int hh, int k_load) {
+  using T = Tile<BM, BN, MODE, BK>;
+  float af[2][T::RM][4], bf[2][T::RN][4];
+  read_chunk<BM, BN, MODE, BK>(cur, cur + T::A_ELEMS, 0, af[0], bf[0], wm, wn, r, hh);
+#pragma unroll
+  for (int g = 0; g < T::NG; ++g) {
+    if (g + 1 < T::NG) read_chunk<BM, BN, MODE, BK>(cur, cur + T::A_ELEMS, g + 1, af[(g + 1) & 1], bf[(g + 1) & 1],
+                                                    wm, wn, r, hh);
+    if constexpr (SCHED == 0) __builtin_amdgcn_sched_barrier(0);
+    mma_chunk<T::RM, T::RN>(af[g & 1], bf[g & 1], acc);
+    if (g == 0) ld.template load<LS>(a, k_load);
+    if (g == (T::NG > 1 ? 1 : 0)) ld.template store<SS>(nxt, nxt + T::A_ELEMS);
+    if constexpr (SCHED == 0) __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+template <int BM, int BN, int MODE, int BK, int SCHED, bool C4>
 __global__ __launch_bounds__(256) void conv_gemm_kernel(CsConvArgs a) {
   using T = Tile<BM, BN, MODE, BK>;
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -261,42 +332,33 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(CsConvArgs a) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
-  Loader<BM, BN, MODE, BK> ld;
-  ld.init(a, m0);
+  Loader<BM, BN, MODE, BK, C4> ld;
+  ld.init(a, m0, n0);
   float* lds0 = smem;
   float* lds1 = smem + T::STAGE;
-  // Pipeline: LDS double buffer + two register stages, so a tile's global loads are
-  // issued two K-steps before its LDS store (they survive the plain s_barrier; the
-  // store waits with a partial vmcnt that leaves the newer stage in flight).
-  // Unrolled by two so every register-stage index is a compile-time constant.
   const int nks = ks_end - ks_begin;
   if (nks > 0) {
-    ld.template load<0>(a, m0, n0, ks_begin * BK);
+    ld.template load<0>(a, ks_begin * BK);
+    if (nks > 1) ld.template load<1>(a, (ks_begin + 1) * BK);
     ld.template store<0>(lds0, lds0 + T::A_ELEMS);
-    if (nks > 1) ld.template load<1>(a, m0, n0, (ks_begin + 1) * BK);
   }
   __syncthreads();
+  // even step t: tile t in lds0, tile t+1 in registers[1] -> lds1, tile t+2 -> registers[0]
   for (int t = 0; t < nks; t += 2) {
-    // even step: tile t in lds0, tile t+1 in registers[1]
-    if (SCHED != 2 && t + 2 < nks) ld.template load<0>(a, m0, n0, (ks_begin + t + 2) * BK);
-    mma_stage<BM, BN, MODE, BK, SCHED>(lds0, lds0 + T::A_ELEMS, acc, wm, wn, r, hh);
-    if (SCHED == 2 && t + 2 < nks) ld.template load<0>(a, m0, n0, (ks_begin + t + 2) * BK);
-    if (t + 1 < nks) ld.template store<1>(lds1, lds1 + T::A_ELEMS);
+    kstep<BM, BN, MODE, BK, SCHED, 0, 1, C4>(ld, a, lds0, lds1, acc, wm, wn, r, hh, (ks_begin + t + 2) * BK);
     __syncthreads();
     if (t + 1 >= nks) break;
-    // odd step: tile t+1 in lds1, tile t+2 in registers[0]
-    if (SCHED != 2 && t + 3 < nks) ld.template load<1>(a, m0, n0, (ks_begin + t + 3) * BK);
-    mma_stage<BM, BN, MODE, BK, SCHED>(lds1, lds1 + T::A_ELEMS, acc, wm, wn, r, hh);
-    if (SCHED == 2 && t + 3 < nks) ld.template load<1>(a, m0, n0, (ks_begin + t + 3) * BK);
-    if (t + 2 < nks) ld.template store<0>(lds0, lds0 + T::A_ELEMS);
+    kstep<BM, BN, MODE, BK, SCHED, 1, 0, C4>(ld, a, lds1, lds0, acc, wm, wn, r, hh, (ks_begin + t + 3) * BK);
     __syncthreads();
   }
 
   // ------------------------------------------------------------------ epilogue
-  // C/D map (32x32 f32 MFMA): col = lane & 31, row = (reg&3) + 8*(reg>>2) + 4*(lane>>5)
+  // C/D map (32x32 f32 MFMA): col = lane & 31, row = (reg&3) + 8*(reg>>2) + 4*(lane>>5).
+  // Stores go through a buffer descriptor: rows/cols outside the GEMM get kOOB (dropped).
   const bool slab = gridDim.z > 1;
-  if (slab) {
-    float* dst = a.ws + (size_t)split * a.M * a.N;
+  if (slab || MODE == CS_CONV_DGRAD || (MODE == CS_CONV_WGRAD && !a.w_oihw)) {
+    float* dst = slab ? a.ws + (size_t)split * a.M * a.N : a.out;
+    const rsrc_t ro = make_rsrc(dst, (int64_t)a.M * a.N * 4);
 #pragma unroll
     for (int i = 0; i < T::RM; ++i)
 #pragma unroll
@@ -305,42 +367,22 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(CsConvArgs a) {
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
           const int m = m0 + wm * T::WM + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * hh;
-          if (m < a.M && n < a.N) dst[(size_t)m * a.N + n] = acc[i][j][e];
+          bstore1(ro, acc[i][j][e], (m < a.M && n < a.N) ? (m * a.N + n) * 4 : kOOB);
         }
       }
-    return;
+    if (slab || MODE != CS_CONV_FWD) return;
   }
-  if constexpr (MODE == CS_CONV_WGRAD) {
+  if constexpr (MODE == CS_CONV_WGRAD) {  // conv0: scatter the padded (tap, ci) columns to OIHW
 #pragma unroll
     for (int i = 0; i < T::RM; ++i)
 #pragma unroll
       for (int j = 0; j < T::RN; ++j) {
         const int n = n0 + wn * T::WN + j * 32 + r;
+        const int tap = n >> 2, ci = n & 3;
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
           const int m = m0 + wm * T::WM + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * hh;
-          if (m < a.M && n < a.N) {
-            if (!a.w_oihw) {
-              a.out[(size_t)m * a.N + n] = acc[i][j][e];
-            } else {
-              const int tap = n >> 2, ci = n & 3;
-              if (ci < 3) a.out[(size_t)m * 27 + ci * 9 + tap] = acc[i][j][e];
-            }
-          }
-        }
-      }
-    return;
-  }
-  if constexpr (MODE == CS_CONV_DGRAD) {
-#pragma unroll
-    for (int i = 0; i < T::RM; ++i)
-#pragma unroll
-      for (int j = 0; j < T::RN; ++j) {
-        const int n = n0 + wn * T::WN + j * 32 + r;
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int m = m0 + wm * T::WM + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * hh;
-          if (m < a.M && n < a.N) a.out[(size_t)m * a.N + n] = acc[i][j][e];
+          if (m < a.M && n < a.N && ci < 3) a.out[(size_t)m * 27 + ci * 9 + tap] = acc[i][j][e];
         }
       }
     return;
@@ -349,6 +391,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(CsConvArgs a) {
     // bias, store, and this tile's per-channel (mean, M2) for the BN statistics
     float* red = smem;  // [2][BN] after the main loop's final barrier
     const int cnt = (a.M - m0) < BM ? (a.M - m0) : BM;
+    const rsrc_t ro = make_rsrc(a.out, (int64_t)a.M * a.N * 4);
     float colsum[T::RN];
 #pragma unroll
     for (int j = 0; j < T::RN; ++j) {
@@ -362,10 +405,8 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(CsConvArgs a) {
           const int m = m0 + wm * T::WM + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * hh;
           const float v = acc[i][j][e] + bv;
           acc[i][j][e] = v;
-          if (m < a.M) {
-            s += v;
-            if (n < a.N) a.out[(size_t)m * a.N + n] = v;
-          }
+          s += m < a.M ? v : 0.f;
+          bstore1(ro, v, (m < a.M && n < a.N) ? (m * a.N + n) * 4 : kOOB);
         }
       colsum[j] = s + __shfl_xor(s, 32, 64);
     }
@@ -390,7 +431,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(CsConvArgs a) {
         for (int e = 0; e < 16; ++e) {
           const int m = m0 + wm * T::WM + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * hh;
           const float d = acc[i][j][e] - mean[j];
-          if (m < a.M) s += d * d;
+          s += m < a.M ? d * d : 0.f;
         }
       s += __shfl_xor(s, 32, 64);
       if (hh == 0) red[wm * BN + wn * T::WN + j * 32 + r] = s;
@@ -513,7 +554,7 @@ hipError_t launch_reduce(const CsConvArgs& a, int mode, int splits, hipStream_t 
 int conv_sched() {
   static int v = [] {
     const char* e = getenv("CS_CONV_SCHED");
-    return e ? atoi(e) : 1;  // default: measured 3-5% faster than 0 and 2 on MI355X
+    return e ? atoi(e) : 0;
   }();
   return v;
 }
@@ -524,12 +565,16 @@ hipError_t launch_gemm(const CsConvArgs& a, int splits, hipStream_t stream) {
   const int ntiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
   const size_t lds = 2 * T::STAGE * sizeof(float);
   const dim3 grid(ntiles, 1, splits);
-  switch (conv_sched()) {
-    case 1: hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, MODE, BK, 1>), grid, dim3(256), lds, stream, a); break;
-    case 2: hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, MODE, BK, 2>), grid, dim3(256), lds, stream, a); break;
-    case 0: hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, MODE, BK, 0>), grid, dim3(256), lds, stream, a); break;
-    default: hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, MODE, BK, 1>), grid, dim3(256), lds, stream, a); break;
+  if constexpr (MODE == CS_CONV_FWD) {
+    if (a.w_oihw) {  // padded conv0: Cin = 4 < BK
+      hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, MODE, BK, 0, true>), grid, dim3(256), lds, stream, a);
+      return hipGetLastError();
+    }
   }
+  if (conv_sched() == 1)
+    hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, MODE, BK, 1, false>), grid, dim3(256), lds, stream, a);
+  else
+    hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, MODE, BK, 0, false>), grid, dim3(256), lds, stream, a);
   return hipGetLastError();
 }
 
@@ -574,10 +619,15 @@ int cs_conv_effective_splits(int K, int bk, int splits) {
 hipError_t cs_conv_gemm(CsConvArgs a, int mode, int bm, int bn, int bk, int splits, hipStream_t stream) {
   if (bk != 16 && bk != 32) return hipErrorInvalidValue;
   cs_conv_fill_dims(&a, mode);
+  // 32-bit buffer offsets: every operand / output / workspace must stay below 2 GiB
+  const int64_t pix = (int64_t)a.B * a.H * a.W;
+  const int64_t big = std::max<int64_t>(pix * std::max(a.Cin, a.Cout), (int64_t)a.M * a.N) * 4;
+  if (big >= 0x7ffffff0ll) return hipErrorInvalidValue;
   a.total_ksteps = (a.K + bk - 1) / bk;
   splits = cs_conv_effective_splits(a.K, bk, splits);
   a.ksteps_per_split = (a.total_ksteps + splits - 1) / splits;
   if (splits > 1 && a.ws == nullptr) return hipErrorInvalidValue;
+  if (splits > 1 && (int64_t)splits * a.M * a.N * 4 >= 0x7ffffff0ll) return hipErrorInvalidValue;
 #define CS_DISPATCH(BM_, BN_, BK_)                                                                       \
   if (bm == BM_ && bn == BN_ && bk == BK_) {                                                             \
     hipError_t e;                                                                                        \
