@@ -32,7 +32,9 @@ __device__ __forceinline__ void chan_combine(float& n, float& m, float& M2, floa
   n = nn;
 }
 
-// 256 threads = 16 channels x 16 tile-lanes
+// 256 threads = 4 waves = 4 channels; the 64 lanes of a channel's wave each combine every
+// 64th tile partial, then a 6-step butterfly (fixed order: deterministic). One wave per
+// channel keeps even conv0's 1024-4096 partials per channel to <= 64 serial combines.
 __global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restrict__ part, int T, int R, int M, int C,
                                                           const float* __restrict__ gamma,
                                                           const float* __restrict__ beta, float* running_mean,
@@ -40,21 +42,22 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restric
                                                           float* __restrict__ scale, float* __restrict__ shift,
                                                           float* __restrict__ save_mean,
                                                           float* __restrict__ save_invstd) {
-  const int cl = threadIdx.x >> 4, tl = threadIdx.x & 15;
-  const int c = blockIdx.x * 16 + cl;
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
   float n = 0.f, m = 0.f, M2 = 0.f;
   if (c < C) {
-    for (int t = tl; t < T; t += 16) {
+    for (int t = lane; t < T; t += 64) {
       const int cnt = (M - t * R) < R ? (M - t * R) : R;
-      chan_combine(n, m, M2, (float)cnt, part[((size_t)t * C + c) * 2], part[((size_t)t * C + c) * 2 + 1]);
+      const float2 pm = *reinterpret_cast<const float2*>(part + ((size_t)t * C + c) * 2);
+      chan_combine(n, m, M2, (float)cnt, pm.x, pm.y);
     }
   }
 #pragma unroll
-  for (int off = 8; off > 0; off >>= 1) {
+  for (int off = 32; off > 0; off >>= 1) {
     const float nb = __shfl_xor(n, off, 64), mb = __shfl_xor(m, off, 64), M2b = __shfl_xor(M2, off, 64);
     chan_combine(n, m, M2, nb, mb, M2b);
   }
-  if (tl == 0 && c < C) {
+  if (lane == 0 && c < C) {
     const float var = M2 / n;
     const float inv = 1.0f / sqrtf(var + eps);
     const float g = gamma[c], b = beta[c];
@@ -213,32 +216,28 @@ __global__ __launch_bounds__(256) void bn_bwd_kernel(const float* __restrict__ y
   }
 }
 
-// 256 threads = 16 channels x 16 partial-lanes: each lane sums every 16th block's
-// partials, then a 16-lane butterfly (fixed order: deterministic). The serial
-// per-channel loop this replaces was latency-bound (33-65 us at P = 128-256).
+// 256 threads = 4 waves = 4 channels: each lane sums every 64th block's partials, then
+// a wave butterfly (fixed order: deterministic).
 __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __restrict__ part, int P, int C, int M,
                                                               const float* __restrict__ gamma,
                                                               const float* __restrict__ invstd,
                                                               float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                               float* __restrict__ dbias, float* __restrict__ coef) {
-  const int cl = threadIdx.x >> 4, pl = threadIdx.x & 15;
-  const int c = blockIdx.x * 16 + cl;
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
   float sg = 0.f, sgx = 0.f, sx = 0.f;
   if (c < C) {
-    for (int p = pl; p < P; p += 16) {
+    for (int p = lane; p < P; p += 64) {
       const float* q = part + ((size_t)p * C + c) * 3;
       sg += q[0];
       sgx += q[1];
       sx += q[2];
     }
   }
-#pragma unroll
-  for (int off = 8; off > 0; off >>= 1) {
-    sg += __shfl_xor(sg, off, 64);
-    sgx += __shfl_xor(sgx, off, 64);
-    sx += __shfl_xor(sx, off, 64);
-  }
-  if (pl != 0 || c >= C) return;
+  sg = cs::wave_sum(sg);
+  sgx = cs::wave_sum(sgx);
+  sx = cs::wave_sum(sx);
+  if (lane != 0 || c >= C) return;
   const float k1 = gamma[c] * invstd[c], k2 = sg / (float)M, k3 = sgx / (float)M;
   if (dgamma) dgamma[c] = sgx;
   if (dbeta) dbeta[c] = sg;
@@ -260,7 +259,7 @@ int cs_bn_bwd_blocks(int B, int H, int W, int C, int pool) {
 hipError_t cs_bn_finalize(const float* part, int T, int R, int M, int C, const float* gamma, const float* beta,
                           float* running_mean, float* running_var, int64_t* nbt, float momentum, float eps,
                           float* scale, float* shift, float* save_mean, float* save_invstd, hipStream_t stream) {
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, stream, part, T, R, M, C, gamma, beta,
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 3) / 4), dim3(256), 0, stream, part, T, R, M, C, gamma, beta,
                      running_mean, running_var, nbt, momentum, eps, scale, shift, save_mean, save_invstd);
   return hipGetLastError();
 }
@@ -297,7 +296,7 @@ hipError_t cs_bn_bwd(const float* y, const float* G, int B, int H, int W, int C,
     hipLaunchKernelGGL((bn_bwd_kernel<false, false>), dim3(P), dim3(256), lds, stream, y, G, B, H, W, C, scale, shift,
                        mean, invstd, nullptr, nullptr, part);
   }
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, stream, part, P, C, M, gamma, invstd,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 3) / 4), dim3(256), 0, stream, part, P, C, M, gamma, invstd,
                      dgamma, dbeta, dbias, coef);
   // the apply pass is sized for bandwidth, independent of the reduce's P
   const int units = pool ? B * (H / 2) * (W / 2) : B * H * W;

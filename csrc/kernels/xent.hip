@@ -55,26 +55,31 @@ __device__ void head_loss(const float* lg, const int64_t* __restrict__ labels, i
 // Row pass: one wave per sample. Each lane holds K/256 float4 slices of the
 // sample's features and of every W row, so the C logits, the softmax, the
 // per-sample loss/argmax AND dfeat[b] = sum_j dl[b][j] W[j] come out of
-// registers; dl is staged in `ws` for the column pass.
+// registers; dl is staged in `ws` for the column pass. CT = compile-time class count
+// (10 for CIFAR-10: every class loop and cross-lane sum is unrolled and interleaved),
+// 0 = runtime C <= kMaxC.
+template <int CT>
 __global__ __launch_bounds__(256) void head_rows_kernel(const float* __restrict__ feat, const float* __restrict__ W,
                                                         const float* __restrict__ bias,
                                                         const int64_t* __restrict__ labels, int B, int K, int C,
                                                         float gscale, float* __restrict__ ws,
                                                         float* __restrict__ logits_out, int64_t* __restrict__ pred_out,
                                                         float* __restrict__ dfeat) {
+  constexpr int NC = CT ? CT : kMaxC;
+  if (CT) C = CT;
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= B) return;
   const int K4 = K >> 2;
   const float4* f4 = reinterpret_cast<const float4*>(feat) + (size_t)row * K4;
   const float4* w4 = reinterpret_cast<const float4*>(W);
-  float acc[kMaxC];
+  float acc[NC];
 #pragma unroll
-  for (int j = 0; j < kMaxC; ++j) acc[j] = 0.f;
+  for (int j = 0; j < NC; ++j) acc[j] = 0.f;
   for (int k = lane; k < K4; k += 64) {
     const float4 f = f4[k];
 #pragma unroll
-    for (int j = 0; j < kMaxC; ++j) {
+    for (int j = 0; j < NC; ++j) {
       if (j < C) {
         const float4 w = w4[(size_t)j * K4 + k];
         acc[j] += f.x * w.x + f.y * w.y + f.z * w.z + f.w * w.w;
@@ -84,7 +89,7 @@ __global__ __launch_bounds__(256) void head_rows_kernel(const float* __restrict_
   float mx = -INFINITY;
   int am = 0;
 #pragma unroll
-  for (int j = 0; j < kMaxC; ++j) {
+  for (int j = 0; j < NC; ++j) {
     if (j < C) {
       acc[j] = cs::wave_sum(acc[j]) + (bias ? bias[j] : 0.f);
       if (acc[j] > mx) { mx = acc[j]; am = j; }
@@ -92,13 +97,13 @@ __global__ __launch_bounds__(256) void head_rows_kernel(const float* __restrict_
   }
   float se = 0.f;
 #pragma unroll
-  for (int j = 0; j < kMaxC; ++j)
+  for (int j = 0; j < NC; ++j)
     if (j < C) se += expf(acc[j] - mx);
   const float lse = logf(se);
   const int y = (int)labels[row];
   float xy = 0.f;
 #pragma unroll
-  for (int j = 0; j < kMaxC; ++j)
+  for (int j = 0; j < NC; ++j)
     if (j == y) xy = acc[j];
   float* dl = ws;                      // [B][C]
   float* rowloss = ws + (size_t)B * C;  // [B]
@@ -110,13 +115,13 @@ __global__ __launch_bounds__(256) void head_rows_kernel(const float* __restrict_
   }
   if (logits_out && lane < C) {
 #pragma unroll
-    for (int j = 0; j < kMaxC; ++j)
+    for (int j = 0; j < NC; ++j)
       if (j == lane) logits_out[(size_t)row * C + j] = acc[j];
   }
   if (dfeat == nullptr) return;
   const float inv = gscale / (float)B;
 #pragma unroll
-  for (int j = 0; j < kMaxC; ++j) {
+  for (int j = 0; j < NC; ++j) {
     if (j < C) {
       acc[j] = (expf(acc[j] - mx - lse) - (j == y ? 1.f : 0.f)) * inv;
       if (lane == j) dl[(size_t)row * C + j] = acc[j];
@@ -126,7 +131,7 @@ __global__ __launch_bounds__(256) void head_rows_kernel(const float* __restrict_
   for (int k = lane; k < K4; k += 64) {
     float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-    for (int j = 0; j < kMaxC; ++j) {
+    for (int j = 0; j < NC; ++j) {
       if (j < C) {
         const float4 w = w4[(size_t)j * K4 + k];
         o.x += acc[j] * w.x; o.y += acc[j] * w.y; o.z += acc[j] * w.z; o.w += acc[j] * w.w;
@@ -197,8 +202,12 @@ hipError_t cs_linear_xent(const float* feat, const float* W, const float* bias, 
                           int C, float gscale, float* loss_out, int* correct_out, float* logits_out, float* dW,
                           float* db, float* dfeat, int64_t* pred_out, float* ws, hipStream_t stream) {
   if (C > kMaxC || C < 1 || B <= 0 || (K & 3) != 0 || ws == nullptr) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(head_rows_kernel, dim3((B + 3) / 4), dim3(256), 0, stream, feat, W, bias, labels, B, K, C,
-                     gscale, ws, logits_out, pred_out, dfeat);
+  if (C == 10)
+    hipLaunchKernelGGL(head_rows_kernel<10>, dim3((B + 3) / 4), dim3(256), 0, stream, feat, W, bias, labels, B, K, C,
+                       gscale, ws, logits_out, pred_out, dfeat);
+  else
+    hipLaunchKernelGGL(head_rows_kernel<0>, dim3((B + 3) / 4), dim3(256), 0, stream, feat, W, bias, labels, B, K, C,
+                       gscale, ws, logits_out, pred_out, dfeat);
   const bool bwd = dW != nullptr && db != nullptr && dfeat != nullptr;
   hipLaunchKernelGGL(head_cols_kernel, dim3(bwd ? C * ((K + 63) / 64) + 1 : 1), dim3(64), 0, stream, feat, B, K, C, ws,
                      bwd ? dW : nullptr, bwd ? db : nullptr, loss_out, correct_out);
