@@ -59,6 +59,10 @@ class GatherScatterSync(GradSync):
         self.root, self.coalesce = root, coalesce
 
     def _one(self, g: torch.Tensor) -> None:
+        with _dense(g) as g:
+            self._one_dense(g)
+
+    def _one_dense(self, g: torch.Tensor) -> None:
         if self.rank == self.root:
             grad_list = [torch.zeros_like(g) for _ in range(self.world)]
             D.gather(g, grad_list, dst=self.root, group=self.group)
@@ -90,6 +94,10 @@ class StarP2PSync(GradSync):
         self.root, self.coalesce, self.serialize = root, coalesce, serialize
 
     def _one(self, g: torch.Tensor) -> None:
+        with _dense(g) as g:
+            self._one_dense(g)
+
+    def _one_dense(self, g: torch.Tensor) -> None:
         others = [r for r in range(self.world) if r != self.root]
         if self.rank == self.root:
             bufs = [torch.zeros_like(g) for _ in others]
@@ -135,8 +143,13 @@ class PerParamAllReduceSync(GradSync):
         if self.world == 1:
             return
         for p in self.params:
-            p.grad = p.grad / self.world
-            D.all_reduce(p.grad, op=D.reduce_op.SUM, group=self.group, async_op=False)
+            if p.grad.is_contiguous():
+                p.grad = p.grad / self.world
+                D.all_reduce(p.grad, op=D.reduce_op.SUM, group=self.group, async_op=False)
+            else:  # channels_last conv grads: collectives need a dense standard-layout tensor
+                g = p.grad.contiguous().div_(self.world)
+                D.all_reduce(g, op=D.reduce_op.SUM, group=self.group, async_op=False)
+                p.grad.copy_(g)
 
 
 class FlatAllReduceSync(GradSync):
@@ -151,6 +164,22 @@ class FlatAllReduceSync(GradSync):
         flat = torch.cat([g.reshape(-1) for g in grads])
         D.all_reduce(flat, op=D.ReduceOp.AVG, group=self.group)
         _unflatten_into(flat, grads)
+
+
+class _dense:
+    """Context: a contiguous alias of ``g`` (channels_last grads get a dense copy that is
+    written back on exit), since gloo / RCCL collectives need standard-layout tensors."""
+
+    def __init__(self, g: torch.Tensor):
+        self.g = g
+        self.c = g if g.is_contiguous() else g.contiguous()
+
+    def __enter__(self) -> torch.Tensor:
+        return self.c
+
+    def __exit__(self, *exc) -> None:
+        if self.c is not self.g:
+            self.g.copy_(self.c)
 
 
 def _unflatten_into(flat: torch.Tensor, tensors: List[torch.Tensor]) -> None:
