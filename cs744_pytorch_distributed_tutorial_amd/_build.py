@@ -112,7 +112,21 @@ def build(jobs: int = 0, force: bool = False, verbose: bool = False) -> str:
             raise RuntimeError(f"link failed\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
         print(f"[build] linked {os.path.relpath(OUT, ROOT)} ({len(objs)} objects, {time.time() - t0:.1f}s)",
               flush=True)
+        _check_stubs(OUT)
     return OUT
+
+
+def _check_stubs(so: str) -> None:
+    """Fail the build if a kernel's host stub is left undefined (hipcc can drop implicitly
+    instantiated template-kernel stubs; the .so would then fail at import on the GPU box)."""
+    nm = os.path.join(ROCM, "lib", "llvm", "bin", "llvm-nm")
+    if not os.path.exists(nm):
+        return
+    r = subprocess.run([nm, "--undefined-only", "-C", so], capture_output=True, text=True)
+    bad = [l.strip() for l in r.stdout.splitlines() if "__device_stub__" in l]
+    if bad:
+        os.remove(so)
+        raise RuntimeError("undefined kernel stubs (add explicit instantiations):\n" + "\n".join(bad[:10]))
 
 
 def main(argv=None) -> int:

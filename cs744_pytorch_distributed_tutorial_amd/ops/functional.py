@@ -49,37 +49,50 @@ def _ws(mode, B, H, W, cin, cout, splits, device) -> Optional[torch.Tensor]:
     return torch.empty(splits * M * N, device=device, dtype=torch.float32)
 
 
+def _counters(fixup: bool, mode, B, H, W, cin, cout, bm, bn, device) -> Optional[torch.Tensor]:
+    """Zeroed split-K tile tickets for the in-launch combine (``fixup``), one per output tile."""
+    if not fixup:
+        return None
+    M, N, _ = gemm_dims(mode, B, H, W, cin, cout)
+    return torch.zeros(((M + bm - 1) // bm) * ((N + bn - 1) // bn), device=device, dtype=torch.int32)
+
+
 def conv_fwd(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], *, w_oihw: bool = False,
-             bm: int = 64, bn: int = 64, splits: int = 1, stats: bool = False, bk: int = 16):
-    """y[B*H*W, Cout] = conv3x3(x NHWC) (+bias); optionally per-tile (mean, M2) BN partials."""
+             bm: int = 64, bn: int = 64, splits: int = 1, stats: bool = False, bk: int = 16, fixup: bool = False,
+             stage: int = 0):
+    """y[B*H*W, Cout] = conv3x3(x NHWC) (+bias); optionally per-tile (mean, M2) BN partials.
+    ``fixup``: split-K slabs combined in-launch by each tile's last block (no reduce kernel)."""
     B, H, W, cin = x.shape
     cout = w.shape[0]
     y = torch.empty(B * H * W, cout, device=x.device, dtype=torch.float32)
-    R = SPLITK_STAT_ROWS if splits > 1 else bm
+    R = native.C().conv_stat_rows(9 * cin, bm, bn, bk, splits, fixup)
     T = (B * H * W + R - 1) // R
     st = torch.empty(T, cout, 2, device=x.device, dtype=torch.float32) if stats else None
     rows = native.C().conv_gemm(FWD, x, w, None, bias, y, _ws(FWD, B, H, W, cin, cout, splits, x.device), st,
-                                B, H, W, cin, cout, w_oihw, bm, bn, splits, bk)
+                                B, H, W, cin, cout, w_oihw, bm, bn, splits, bk,
+                                _counters(fixup, FWD, B, H, W, cin, cout, bm, bn, x.device), stage)
     return (y, st, rows) if stats else y
 
 
 def conv_dgrad(dz: torch.Tensor, w_ohwi: torch.Tensor, B: int, H: int, W: int, *, bm: int = 64, bn: int = 64,
-               splits: int = 1, bk: int = 16) -> torch.Tensor:
+               splits: int = 1, bk: int = 16, fixup: bool = False, stage: int = 0) -> torch.Tensor:
     """dx[B*H*W, Cin] from dz[B*H*W, Cout] and OHWI weights."""
     cout, _, _, cin = w_ohwi.shape
     dx = torch.empty(B * H * W, cin, device=dz.device, dtype=torch.float32)
     native.C().conv_gemm(DGRAD, None, w_ohwi, dz, None, dx, _ws(DGRAD, B, H, W, cin, cout, splits, dz.device), None,
-                         B, H, W, cin, cout, False, bm, bn, splits, bk)
+                         B, H, W, cin, cout, False, bm, bn, splits, bk,
+                         _counters(fixup, DGRAD, B, H, W, cin, cout, bm, bn, dz.device), stage)
     return dx
 
 
 def conv_wgrad(dz: torch.Tensor, x: torch.Tensor, cout: int, *, w_oihw: bool = False, bm: int = 64, bn: int = 64,
-               splits: int = 1, bk: int = 16) -> torch.Tensor:
+               splits: int = 1, bk: int = 16, fixup: bool = False, stage: int = 0) -> torch.Tensor:
     """dW (OHWI, or OIHW [Cout,3,3,3] for the padded conv0) from dz and the NHWC input."""
     B, H, W, cin = x.shape
     dw = torch.empty(cout * 27 if w_oihw else cout * 9 * cin, device=x.device, dtype=torch.float32)
     native.C().conv_gemm(WGRAD, x, None, dz, None, dw, _ws(WGRAD, B, H, W, cin, cout, splits, x.device), None,
-                         B, H, W, cin, cout, w_oihw, bm, bn, splits, bk)
+                         B, H, W, cin, cout, w_oihw, bm, bn, splits, bk,
+                         _counters(fixup, WGRAD, B, H, W, cin, cout, bm, bn, x.device), stage)
     return dw.view(cout, 3, 3, 3) if w_oihw else dw.view(cout, 3, 3, cin)
 
 

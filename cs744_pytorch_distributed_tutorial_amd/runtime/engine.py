@@ -248,15 +248,18 @@ class NativeTrainer:
             with open(cache) as f:
                 db = json.load(f)
         if key in db:
-            for l, m, bm, bn, sp, bk in db[key]["tiles"]:
-                self.engine.set_tile(l, m, bm, bn, sp, bk)
+            for ent in db[key]["tiles"]:  # [block, mode, bm, bn, splits, bk(, stage)]
+                self.engine.set_tile(*ent[:6], ent[6] if len(ent) > 6 else 0)
+            for l, on in enumerate(db[key].get("dual", [])):
+                self.engine.set_block_dual(l, bool(on))
             self.tune_us = db[key]["us"]
             return
         self.tune_us = list(self.engine.autotune(self.B, 5))
         if cache and self.rank == 0:
             tiles = [[l, m] + list(self.engine.get_tile(l, m)) for l in range(self.layout.L) for m in range(3)
                      if not (l == 0 and m == 1)]
-            db[key] = {"tiles": tiles, "us": self.tune_us}
+            db[key] = {"tiles": tiles, "us": self.tune_us,
+                       "dual": [int(self.engine.block_dual(l)) for l in range(self.layout.L)]}
             with open(cache, "w") as f:
                 json.dump(db, f, indent=1)
 
@@ -268,9 +271,10 @@ class NativeTrainer:
             for m in range(3):
                 if l == 0 and m == 1:
                     continue
-                bm, bn, sp, bk = self.engine.get_tile(l, m)
+                bm, bn, sp, bk, st = self.engine.get_tile(l, m)
                 us = self.tune_us[3 * l + m] if self.tune_us else None
-                out.append({"block": l, "op": names[m], "bm": bm, "bn": bn, "bk": bk, "splits": sp, "us": us})
+                out.append({"block": l, "op": names[m], "bm": bm, "bn": bn, "bk": bk, "splits": sp,
+                            "stage": "lds_dma" if st else "regs", "us": us})
         return out
 
     # ---------------------------------------------------------------- data

@@ -28,7 +28,8 @@ bool pow2(int64_t v) { return v > 0 && (v & (v - 1)) == 0; }
 int64_t conv_gemm(int64_t mode, c10::optional<torch::Tensor> x, c10::optional<torch::Tensor> w,
                   c10::optional<torch::Tensor> dz, c10::optional<torch::Tensor> bias, torch::Tensor out,
                   c10::optional<torch::Tensor> ws, c10::optional<torch::Tensor> stats, int64_t B, int64_t H, int64_t W,
-                  int64_t Cin, int64_t Cout, bool w_oihw, int64_t bm, int64_t bn, int64_t splits, int64_t bk) {
+                  int64_t Cin, int64_t Cout, bool w_oihw, int64_t bm, int64_t bn, int64_t splits, int64_t bk,
+                  c10::optional<torch::Tensor> counters, int64_t stage) {
   TORCH_CHECK(mode >= 0 && mode <= 2, "conv_gemm: bad mode");
   TORCH_CHECK(pow2(H) && pow2(W) && pow2(Cin) && pow2(Cout) && Cin >= 4 && Cout >= 64 && B > 0,
               "conv_gemm: H, W, Cin, Cout must be powers of two (Cin>=4, Cout>=64)");
@@ -45,7 +46,7 @@ int64_t conv_gemm(int64_t mode, c10::optional<torch::Tensor> x, c10::optional<to
     TORCH_CHECK(x.has_value() && w.has_value(), "conv fwd needs x and w");
     check_t(x, pix * Cin, "x"); check_t(w, wnum, "w"); check_t(bias, Cout, "bias");
     check_t(out, pix * Cout, "out");
-    const int64_t R = cs_conv_effective_splits(9 * Cin, bk, splits) > 1 ? CS_SPLITK_STAT_ROWS : bm;
+    const int64_t R = cs_conv_stat_rows(9 * Cin, bm, bn, bk, splits, counters.has_value());
     check_t(stats, ((pix + R - 1) / R) * Cout * 2, "stats");
   } else if (mode == CS_CONV_DGRAD) {
     TORCH_CHECK(dz.has_value() && w.has_value(), "conv dgrad needs dz and w");
@@ -59,11 +60,21 @@ int64_t conv_gemm(int64_t mode, c10::optional<torch::Tensor> x, c10::optional<to
     TORCH_CHECK(ws.has_value() && ws->defined(), "conv_gemm: split-K needs a workspace");
     check_t(ws, sp * (int64_t)a.M * a.N, "ws");
   }
+  const int64_t ntiles = ((a.M + bm - 1) / bm) * ((a.N + bn - 1) / bn);
+  if (counters.has_value()) {
+    TORCH_CHECK(counters->is_cuda() && counters->scalar_type() == at::kInt && counters->is_contiguous() &&
+                    counters->numel() >= ntiles,
+                "conv_gemm: counters must be a zeroed contiguous int32 GPU tensor with >= ", ntiles, " elements");
+    a.counters = counters->data_ptr<int>();
+  }
   DevGuard g(out.device());
   a.x = cptr(x); a.w = cptr(w); a.dz = cptr(dz); a.bias = cptr(bias);
   a.out = out.data_ptr<float>(); a.ws = mptr(ws); a.stats = mptr(stats);
-  CS_LAUNCH(cs_conv_gemm(a, (int)mode, (int)bm, (int)bn, (int)bk, (int)splits, cur_stream()));
-  return sp > 1 ? CS_SPLITK_STAT_ROWS : bm;
+  TORCH_CHECK(stage == CS_STAGE_REGS || ((stage == CS_STAGE_LDS_DMA || stage == CS_STAGE_LDS_DMA_DEEP) && bk == 32 &&
+                                         !(w_oihw && mode == CS_CONV_FWD)),
+              "conv_gemm: LDS-DMA staging needs bk 32 and not conv0's forward");
+  CS_LAUNCH(cs_conv_gemm(a, (int)mode, (int)bm, (int)bn, (int)bk, (int)splits, cur_stream(), (int)stage));
+  return cs_conv_stat_rows(a.K, bm, bn, bk, splits, counters.has_value());
 }
 
 void bn_finalize(torch::Tensor part, int64_t T, int64_t R, int64_t M, torch::Tensor gamma, torch::Tensor beta,
@@ -136,7 +147,11 @@ void register_conv_ops(pybind11::module& m) {
   m.def("conv_gemm", &conv_gemm, "implicit-GEMM 3x3 conv (mode 0 fwd / 1 dgrad / 2 wgrad), fp32 MFMA",
         py::arg("mode"), py::arg("x"), py::arg("w"), py::arg("dz"), py::arg("bias"), py::arg("out"), py::arg("ws"),
         py::arg("stats"), py::arg("B"), py::arg("H"), py::arg("W"), py::arg("Cin"), py::arg("Cout"),
-        py::arg("w_oihw"), py::arg("bm"), py::arg("bn"), py::arg("splits"), py::arg("bk") = 16);
+        py::arg("w_oihw"), py::arg("bm"), py::arg("bn"), py::arg("splits"), py::arg("bk") = 16,
+        py::arg("counters") = py::none(), py::arg("stage") = 0);
+  m.def("conv_stat_rows", [](int64_t K, int64_t bm, int64_t bn, int64_t bk, int64_t splits, bool counters) {
+    return cs_conv_stat_rows((int)K, (int)bm, (int)bn, (int)bk, (int)splits, counters);
+  }, "FWD BN-statistics tile height of a conv_gemm launch");
   m.def("bn_finalize", &bn_finalize);
   m.def("bn_eval_coeffs", &bn_eval_coeffs);
   m.def("bn_apply", &bn_apply);

@@ -150,8 +150,12 @@ void register_runtime(pybind11::module& m) {
            py::arg("bucket_ranges"), py::arg("broadcast_buffers"), py::arg("lr"), py::arg("momentum"),
            py::arg("wd"), py::arg("dampening"))
       .def("set_overlap_wgrad", &cs::VggEngine::set_overlap_wgrad)
+      .def("set_fixup", &cs::VggEngine::set_fixup)
+      .def("set_dual", &cs::VggEngine::set_dual)
+      .def("block_dual", &cs::VggEngine::block_dual)
+      .def("set_block_dual", &cs::VggEngine::set_block_dual)
       .def("set_tile", &cs::VggEngine::set_tile, py::arg("block"), py::arg("mode"), py::arg("bm"), py::arg("bn"),
-           py::arg("splits"), py::arg("bk") = 16)
+           py::arg("splits"), py::arg("bk") = 16, py::arg("stage") = 0)
       .def("get_tile", &cs::VggEngine::get_tile)
       .def("autotune", &cs::VggEngine::autotune)
       .def("run_conv", &cs::VggEngine::run_conv);

@@ -83,11 +83,14 @@ struct Traits<CS_CONV_WGRAD> {
   static constexpr bool A_KC = false, B_KC = false;
 };
 
-template <int BM, int BN, int MODE, int BK>
+// GL = LDS-DMA staging (buffer_load ... lds): images are lane-linear, so unpadded; a
+// K-contiguous row (BK = 32 -> 8 float4 chunks) stores logical chunk c at physical chunk
+// c ^ ((row >> 1) & 7), which makes the ds_read_b128 fragment reads conflict-free.
+template <int BM, int BN, int MODE, int BK, bool GL = false>
 struct Tile {
   static constexpr bool A_KC = Traits<MODE>::A_KC, B_KC = Traits<MODE>::B_KC;
-  static constexpr int A_ELEMS = A_KC ? BM * (BK + 4) : BK * (BM + 4);
-  static constexpr int B_ELEMS = B_KC ? BN * (BK + 4) : BK * (BN + 4);
+  static constexpr int A_ELEMS = GL ? BM * BK : (A_KC ? BM * (BK + 4) : BK * (BM + 4));
+  static constexpr int B_ELEMS = GL ? BN * BK : (B_KC ? BN * (BK + 4) : BK * (BN + 4));
   static constexpr int STAGE = A_ELEMS + B_ELEMS;
   static constexpr int AC = BM * BK / 1024;  // float4 chunks per thread per stage
   static constexpr int BC = BN * BK / 1024;
@@ -99,14 +102,41 @@ struct Tile {
 
 // C4: FWD of the padded conv0 (Cin = 4 < BK, OIHW weights) — a compile-time variant so
 // the common kernels carry no branch for it.
-template <int BM, int BN, int MODE, int BK, bool C4 = false>
+//
+// GL: the same per-chunk offsets feed LDS-DMA instead of registers. Chunk i of a thread is
+// then slot s = (wave * AC + i) * 64 + lane of the operand's lane-linear LDS image (one
+// 1 KiB wave-instruction per chunk index), instead of q = tid + 256 * i.
+template <int BM, int BN, int MODE, int BK, bool C4 = false, bool GL = false>
 struct Loader {
-  using T = Tile<BM, BN, MODE, BK>;
+  using T = Tile<BM, BN, MODE, BK, GL>;
   rsrc_t ra_, rb_;
   int av[T::AC], bv[T::BC];        // per-thread fixed byte offsets
   unsigned am[T::AC], bm_[T::BC];  // per-thread tap masks / flags
-  int lds_a[T::AC], lds_b[T::BC];  // LDS float offsets of this thread's chunks
-  float4 ra[2][T::AC], rb[2][T::BC];
+  int lds_a[T::AC], lds_b[T::BC];  // LDS float offsets of this thread's chunks (register staging)
+  int kb[T::BC];                   // WGRAD B: the chunk's pixel row within the K-step
+  float4 ra[GL ? 1 : 2][T::AC], rb[GL ? 1 : 2][T::BC];
+
+  // chunk -> (row or k-row, logical float4 chunk) of the operand image
+  template <int CHUNKS>
+  __device__ static void slot_kc(int i, int& row, int& c) {
+    if constexpr (GL) {
+      const int s = (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * CHUNKS + i) * 64 + (threadIdx.x & 63);
+      row = s / T::KQ;
+      c = (s % T::KQ) ^ ((row >> 1) & 7);
+    } else {
+      const int q = threadIdx.x + 256 * i;
+      row = q / T::KQ;
+      c = q % T::KQ;
+    }
+  }
+  template <int ROWS, int CHUNKS>
+  __device__ static void slot_km(int i, int& kr, int& c) {
+    constexpr int CPR = ROWS / 4;
+    const int s = GL ? (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * CHUNKS + i) * 64 + (threadIdx.x & 63)
+                     : threadIdx.x + 256 * i;
+    kr = s / CPR;
+    c = s - kr * CPR;
+  }
 
   __device__ void init(const CsConvArgs& a, int m0, int n0) {
     const int pix = a.B * a.H * a.W;
@@ -114,17 +144,18 @@ struct Loader {
     const int64_t wbytes = (a.w_oihw ? (int64_t)a.Cout * 27 : (int64_t)a.Cout * 9 * a.Cin) * 4;
 #pragma unroll
     for (int i = 0; i < T::AC; ++i) {
-      const int q = threadIdx.x + 256 * i;
       if constexpr (T::A_KC) {  // FWD / DGRAD: A[m = pixel][k = (tap, ch)], one pixel row per chunk
-        const int row = q / T::KQ, c = q % T::KQ, m = m0 + row;
+        int row, c;
+        slot_kc<T::AC>(i, row, c);
+        const int m = m0 + row;
         const int w = m & (a.W - 1), h = (m >> a.lgW) & (a.H - 1);
         const int lgC = (MODE == CS_CONV_FWD) ? a.lgCin : a.lgCout;
         am[i] = m < a.M ? tap_mask(h, w, a.H, a.W, MODE == CS_CONV_FWD ? 1 : -1) : 0u;
         av[i] = ((m << lgC) + 4 * c) * 4;
         lds_a[i] = row * (BK + 4) + 4 * c;
       } else {  // WGRAD: A[m = cout][k = pixel] from dZ [pixel][cout], K-major staging
-        constexpr int CPR = BM / 4;
-        const int kr = q / CPR, c = q - kr * CPR;
+        int kr, c;
+        slot_km<BM, T::AC>(i, kr, c);
         am[i] = (m0 + 4 * c < a.M) ? 1u : 0u;
         av[i] = ((kr << a.lgCout) + m0 + 4 * c) * 4;
         lds_a[i] = kr * (BM + 4) + 4 * c;
@@ -132,21 +163,24 @@ struct Loader {
     }
 #pragma unroll
     for (int i = 0; i < T::BC; ++i) {
-      const int q = threadIdx.x + 256 * i;
       if constexpr (MODE == CS_CONV_FWD) {  // B[n = cout][k]: weights [Cout][K] (K-contiguous)
-        const int row = q / T::KQ, c = q % T::KQ, n = n0 + row;
+        int row, c;
+        slot_kc<T::BC>(i, row, c);
+        const int n = n0 + row;
         bm_[i] = n < a.N ? 1u : 0u;
         bv[i] = C4 ? (n * 27 + c) : (n * a.K + 4 * c) * 4;  // conv0: element index (gather path)
         lds_b[i] = row * (BK + 4) + 4 * c;
       } else if constexpr (MODE == CS_CONV_DGRAD) {  // B[k = (tap, cout)][n = cin]: OHWI weights, K-major
-        constexpr int CPR = BN / 4;
-        const int kr = q / CPR, c = q - kr * CPR;
+        int kr, c;
+        slot_km<BN, T::BC>(i, kr, c);
         bm_[i] = (n0 + 4 * c < a.N) ? 1u : 0u;
         bv[i] = (kr * 9 * a.Cin + n0 + 4 * c) * 4;
         lds_b[i] = kr * (BN + 4) + 4 * c;
       } else {  // WGRAD: B[k = pixel][n = (tap, cin)] = X[pixel + tap shift][cin], K-major
-        constexpr int CPR = BN / 4;
-        const int kr = q / CPR, c = q - kr * CPR, nn = n0 + 4 * c;
+        int kr, c;
+        slot_km<BN, T::BC>(i, kr, c);
+        const int nn = n0 + 4 * c;
+        kb[i] = kr;
         const int tap = nn >> a.lgCin, ci = nn & (a.Cin - 1);
         const int t3 = tap / 3, dh = t3 - 1, dw = tap - 3 * t3 - 1;
         // flag bits: [0] column valid, [4..] signed tap delta (dh, dw) packed as (dh+1)*3+(dw+1)
@@ -167,62 +201,77 @@ struct Loader {
     }
   }
 
+  // byte offset (or kOOB) of A chunk i / B chunk i for the K-step starting at k0 (non-C4)
+  __device__ __forceinline__ int a_off(const CsConvArgs& a, int k0, int i) const {
+    if constexpr (T::A_KC) {
+      const int lgC = (MODE == CS_CONV_FWD) ? a.lgCin : a.lgCout;
+      const int tap = k0 >> lgC, ch0 = k0 & ((1 << lgC) - 1);
+      const int t3 = tap / 3, dh = t3 - 1, dw = tap - 3 * t3 - 1;
+      const int sh = (MODE == CS_CONV_FWD) ? (dh * a.W + dw) : -(dh * a.W + dw);
+      return ((am[i] >> tap) & 1u) ? av[i] + ((sh << lgC) + ch0) * 4 : kOOB;
+    } else {
+      return am[i] ? av[i] + ((k0 << a.lgCout) * 4) : kOOB;
+    }
+  }
+  __device__ __forceinline__ int b_off(const CsConvArgs& a, int k0, int i) const {
+    if constexpr (MODE == CS_CONV_FWD) {
+      return bm_[i] ? bv[i] + k0 * 4 : kOOB;
+    } else if constexpr (MODE == CS_CONV_DGRAD) {
+      const int tap = k0 >> a.lgCout, co0 = k0 & (a.Cout - 1);
+      return bm_[i] ? bv[i] + (((co0 * 9 + tap) << a.lgCin) * 4) : kOOB;
+    } else {
+      const int p = k0 + kb[i];
+      const int w = p & (a.W - 1), h = (p >> a.lgW) & (a.H - 1);
+      const int tap = (int)(bm_[i] >> 4), t3 = tap / 3;
+      const int hh = h + t3 - 1, ww = w + (tap - 3 * t3) - 1;
+      const bool ok = (bm_[i] & 1u) && p < a.K && (unsigned)hh < (unsigned)a.H && (unsigned)ww < (unsigned)a.W;
+      return ok ? bv[i] + ((p << a.lgCin) * 4) : kOOB;
+    }
+  }
+
+  // LDS-DMA staging of the K-step at k0 into an operand image pair (GL only): one
+  // buffer_load_dwordx4 ... lds per chunk; out-of-range offsets land as zeros.
+  __device__ __forceinline__ void gload(const CsConvArgs& a, int k0, float* As, float* Bs) const {
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#pragma unroll
+    for (int i = 0; i < T::AC; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra_, (__attribute__((address_space(3))) void*)(As + (wv * T::AC + i) * 256),
+                                               16, a_off(a, k0, i), 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < T::BC; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb_, (__attribute__((address_space(3))) void*)(Bs + (wv * T::BC + i) * 256),
+                                               16, b_off(a, k0, i), 0, 0, 0);
+  }
+
   template <int S>
   __device__ __forceinline__ void load(const CsConvArgs& a, int k0) {
     // ---------------- A operand
-    if constexpr (T::A_KC) {
-      const int lgC = (MODE == CS_CONV_FWD) ? a.lgCin : a.lgCout;
-      const int C = 1 << lgC;
-      if constexpr (!C4) {  // the whole K-step sits inside one tap (BK divides C): uniform
-        const int tap = k0 >> lgC, ch0 = k0 & (C - 1);
+    if constexpr (!C4) {
+#pragma unroll
+      for (int i = 0; i < T::AC; ++i) ra[S][i] = bload4(ra_, a_off(a, k0, i));
+    } else {  // conv0 (C = 4 < BK): each float4 is its own tap
+      const int lgC = a.lgCin;
+#pragma unroll
+      for (int i = 0; i < T::AC; ++i) {
+        const int c = (threadIdx.x + 256 * i) % T::KQ;
+        const int tap = (k0 >> lgC) + c;
         const int t3 = tap / 3, dh = t3 - 1, dw = tap - 3 * t3 - 1;
-        const int sh = (MODE == CS_CONV_FWD) ? (dh * a.W + dw) : -(dh * a.W + dw);
-        const int soff = ((sh << lgC) + ch0) * 4;
-#pragma unroll
-        for (int i = 0; i < T::AC; ++i) {
-          const int off = ((am[i] >> tap) & 1u) ? av[i] + soff : kOOB;
-          ra[S][i] = bload4(ra_, off);
-        }
-      } else {  // conv0 (C = 4 < BK): each float4 is its own tap
-#pragma unroll
-        for (int i = 0; i < T::AC; ++i) {
-          const int c = (threadIdx.x + 256 * i) % T::KQ;
-          const int tap = (k0 >> lgC) + c;
-          const int t3 = tap / 3, dh = t3 - 1, dw = tap - 3 * t3 - 1;
-          const int sh = (MODE == CS_CONV_FWD) ? (dh * a.W + dw) : -(dh * a.W + dw);
-          const int off = (tap < 9 && ((am[i] >> tap) & 1u)) ? av[i] - 16 * c + (sh << lgC) * 4 : kOOB;
-          ra[S][i] = bload4(ra_, off);
-        }
+        const int sh = dh * a.W + dw;
+        const int off = (tap < 9 && ((am[i] >> tap) & 1u)) ? av[i] - 16 * c + (sh << lgC) * 4 : kOOB;
+        ra[S][i] = bload4(ra_, off);
       }
-    } else {  // WGRAD A: rows k0.. of dZ, uniform part k0*Cout
-      const int soff = (k0 << a.lgCout) * 4;
-#pragma unroll
-      for (int i = 0; i < T::AC; ++i) ra[S][i] = bload4(ra_, am[i] ? av[i] + soff : kOOB);
     }
     // ---------------- B operand
 #pragma unroll
     for (int i = 0; i < T::BC; ++i) {
-      if constexpr (MODE == CS_CONV_FWD) {
-        if constexpr (!C4) {  // K = 9*Cin is a multiple of BK
-          rb[S][i] = bload4(rb_, bm_[i] ? bv[i] + k0 * 4 : kOOB);
-        } else {  // conv0: OIHW [Cout][3][3x3], K = 9 taps x 4 (padded) channels
-          const int tap = (k0 >> 2) + (threadIdx.x + 256 * i) % T::KQ;
-          const bool ok = bm_[i] && tap < 9;
-          const int e = bv[i] - ((threadIdx.x + 256 * i) % T::KQ) + tap;  // n*27 + tap
-          const float* wr = a.w + (ok ? e : 0);
-          rb[S][i] = ok ? make_float4(wr[0], wr[9], wr[18], 0.f) : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-      } else if constexpr (MODE == CS_CONV_DGRAD) {
-        const int tap = k0 >> a.lgCout, co0 = k0 & (a.Cout - 1);
-        const int soff = ((co0 * 9 + tap) << a.lgCin) * 4;
-        rb[S][i] = bload4(rb_, bm_[i] ? bv[i] + soff : kOOB);
+      if constexpr (MODE == CS_CONV_FWD && C4) {  // conv0: OIHW [Cout][3][3x3], K = 9 taps x 4 (padded) channels
+        const int tap = (k0 >> 2) + (threadIdx.x + 256 * i) % T::KQ;
+        const bool ok = bm_[i] && tap < 9;
+        const int e = bv[i] - ((threadIdx.x + 256 * i) % T::KQ) + tap;  // n*27 + tap
+        const float* wr = a.w + (ok ? e : 0);
+        rb[S][i] = ok ? make_float4(wr[0], wr[9], wr[18], 0.f) : make_float4(0.f, 0.f, 0.f, 0.f);
       } else {
-        const int q = threadIdx.x + 256 * i, kr = q / (BN / 4), p = k0 + kr;
-        const int w = p & (a.W - 1), h = (p >> a.lgW) & (a.H - 1);
-        const int tap = (int)(bm_[i] >> 4), t3 = tap / 3;
-        const int hh = h + t3 - 1, ww = w + (tap - 3 * t3) - 1;
-        const bool ok = (bm_[i] & 1u) && p < a.K && (unsigned)hh < (unsigned)a.H && (unsigned)ww < (unsigned)a.W;
-        rb[S][i] = bload4(rb_, ok ? bv[i] + ((p << a.lgCin) * 4) : kOOB);
+        rb[S][i] = bload4(rb_, b_off(a, k0, i));
       }
     }
   }
@@ -237,32 +286,39 @@ struct Loader {
 };
 
 // Fragment reads of 4-deep sub-step chunk g (sub-steps 4g..4g+3) of one staged tile.
-template <int BM, int BN, int MODE, int BK>
+// Register-staged images are padded ([row][BK+4] / [k][rows+4]); LDS-DMA images (GL) are
+// unpadded, K-contiguous rows chunk-swizzled (Tile).
+template <int BM, int BN, int MODE, int BK, bool GL = false>
 __device__ __forceinline__ void read_chunk(const float* __restrict__ As, const float* __restrict__ Bs, int g,
-                                           float (&af)[Tile<BM, BN, MODE, BK>::RM][4],
-                                           float (&bf)[Tile<BM, BN, MODE, BK>::RN][4], int wm, int wn, int r,
+                                           float (&af)[Tile<BM, BN, MODE, BK, GL>::RM][4],
+                                           float (&bf)[Tile<BM, BN, MODE, BK, GL>::RN][4], int wm, int wn, int r,
                                            int hh) {
-  using T = Tile<BM, BN, MODE, BK>;
+  using T = Tile<BM, BN, MODE, BK, GL>;
+  constexpr int KP = GL ? BK : BK + 4;  // K-contiguous row pitch
 #pragma unroll
   for (int i = 0; i < T::RM; ++i) {
     const int row = wm * T::WM + i * 32 + r;
     if constexpr (T::A_KC) {
-      const float4 v = *reinterpret_cast<const float4*>(As + row * (BK + 4) + T::HK * hh + 4 * g);
+      const int ch = GL ? ((T::HK / 4 * hh + g) ^ ((row >> 1) & 7)) : (T::HK / 4 * hh + g);
+      const float4 v = *reinterpret_cast<const float4*>(As + row * KP + 4 * ch);
       af[i][0] = v.x; af[i][1] = v.y; af[i][2] = v.z; af[i][3] = v.w;
     } else {
+      constexpr int RP = GL ? BM : BM + 4;
 #pragma unroll
-      for (int s = 0; s < 4; ++s) af[i][s] = As[(T::HK * hh + 4 * g + s) * (BM + 4) + row];
+      for (int s = 0; s < 4; ++s) af[i][s] = As[(T::HK * hh + 4 * g + s) * RP + row];
     }
   }
 #pragma unroll
   for (int j = 0; j < T::RN; ++j) {
     const int col = wn * T::WN + j * 32 + r;
     if constexpr (T::B_KC) {
-      const float4 v = *reinterpret_cast<const float4*>(Bs + col * (BK + 4) + T::HK * hh + 4 * g);
+      const int ch = GL ? ((T::HK / 4 * hh + g) ^ ((col >> 1) & 7)) : (T::HK / 4 * hh + g);
+      const float4 v = *reinterpret_cast<const float4*>(Bs + col * KP + 4 * ch);
       bf[j][0] = v.x; bf[j][1] = v.y; bf[j][2] = v.z; bf[j][3] = v.w;
     } else {
+      constexpr int RP = GL ? BN : BN + 4;
 #pragma unroll
-      for (int s = 0; s < 4; ++s) bf[j][s] = Bs[(T::HK * hh + 4 * g + s) * (BN + 4) + col];
+      for (int s = 0; s < 4; ++s) bf[j][s] = Bs[(T::HK * hh + 4 * g + s) * RP + col];
     }
   }
 }
@@ -307,16 +363,172 @@ __device__ __forceinline__ void kstep(Loader<BM, BN, MODE, BK, C4>& ld, const Cs
   }
 }
 
-template <int BM, int BN, int MODE, int BK, int SCHED, bool C4>
-__global__ __launch_bounds__(256) void conv_gemm_kernel(CsConvArgs a) {
+// In-launch split-K combine (cdna_hip_programming.md §5 "In-launch split-K reduction"):
+// every split block has stored its fp32 slab; it publishes it (vmcnt drain, barrier, one
+// agent-scope release) and takes a ticket on the tile's counter. The block that draws the
+// last ticket resets the counter, acquires, and sums the tile's slabs in split order
+// z = 0..S-1 (the same fixed order as the separate reduce kernel: deterministic and
+// independent of which block arrives last), then runs the epilogue: bias + output (+ this
+// tile's BN (mean, M2) over its BM rows for FWD; the OIHW scatter for conv0's wgrad).
+// Saves the reduce launch and the slab round trip for GEMMs whose S * BM * BN slabs are
+// small enough for one block to read (cs_conv_fixup_ok).
+template <int BM, int BN, int MODE>
+__device__ void splitk_fixup(const CsConvArgs& a, int tile, int mt, int nt, int nsplit, float* smem) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int* flag = reinterpret_cast<int*>(smem);
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int t = __hip_atomic_fetch_add(a.counters + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = t == nsplit - 1;
+    if (last) {
+      __hip_atomic_store(a.counters + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    flag[0] = last;
+  }
+  __syncthreads();
+  const int last = flag[0];
+  __syncthreads();  // flag is read by every wave before smem is reused below
+  if (!last) return;
+  constexpr int CG = BN / 4, RL = 256 / CG, RPT = BM / RL;
+  const int cg = threadIdx.x % CG, rl = threadIdx.x / CG;
+  const int m0 = mt * BM, n0 = nt * BN, n = n0 + 4 * cg;
+  const int S = nsplit;
+  const size_t slab = (size_t)a.M * a.N;
+  const bool nok = n < a.N;
+  float4 v[RPT];
+#pragma unroll
+  for (int k = 0; k < RPT; ++k) v[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+  const float* base = a.ws + n;
+  int z = 0;
+  for (; z + 4 <= S; z += 4) {  // 4 slabs per trip: RPT * 4 loads in flight, added in z order
+    float4 t[4][RPT];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int k = 0; k < RPT; ++k) {
+        const int m = m0 + rl + k * RL;
+        t[u][k] = (m < a.M && nok) ? *reinterpret_cast<const float4*>(base + (size_t)(z + u) * slab + (size_t)m * a.N)
+                                   : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int k = 0; k < RPT; ++k) {
+        v[k].x += t[u][k].x; v[k].y += t[u][k].y; v[k].z += t[u][k].z; v[k].w += t[u][k].w;
+      }
+  }
+  for (; z < S; ++z)
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+      const int m = m0 + rl + k * RL;
+      if (m < a.M && nok) {
+        const float4 t = *reinterpret_cast<const float4*>(base + (size_t)z * slab + (size_t)m * a.N);
+        v[k].x += t.x; v[k].y += t.y; v[k].z += t.z; v[k].w += t.w;
+      }
+    }
+  if constexpr (MODE == CS_CONV_FWD) {
+    if (a.bias != nullptr && nok) {
+      const float4 bv = *reinterpret_cast<const float4*>(a.bias + n);
+#pragma unroll
+      for (int k = 0; k < RPT; ++k) { v[k].x += bv.x; v[k].y += bv.y; v[k].z += bv.z; v[k].w += bv.w; }
+    }
+  }
+  if (MODE == CS_CONV_WGRAD && a.w_oihw) {
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+      const int m = m0 + rl + k * RL;
+      const float vals[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+      if (m < a.M)
+        for (int q = 0; q < 4; ++q) {
+          const int nn = n + q, tap = nn >> 2, ci = nn & 3;
+          if (nn < a.N && ci < 3) a.out[(size_t)m * 27 + ci * 9 + tap] = vals[q];
+        }
+    }
+    return;
+  }
+#pragma unroll
+  for (int k = 0; k < RPT; ++k) {
+    const int m = m0 + rl + k * RL;
+    if (m < a.M && nok) *reinterpret_cast<float4*>(a.out + (size_t)m * a.N + n) = v[k];
+  }
+  if constexpr (MODE == CS_CONV_FWD) {
+    if (a.stats == nullptr) return;
+    // per-column (mean, M2) over the tile's valid rows, two passes through LDS
+    float* red = smem;             // [RL][BN]
+    float* meanv = smem + RL * BN;  // [BN]
+    const int cnt = (a.M - m0) < BM ? (a.M - m0) : BM;
+    float4 cs = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int k = 0; k < RPT; ++k)
+      if (m0 + rl + k * RL < a.M) { cs.x += v[k].x; cs.y += v[k].y; cs.z += v[k].z; cs.w += v[k].w; }
+    *reinterpret_cast<float4*>(red + rl * BN + 4 * cg) = cs;
+    __syncthreads();
+    if (threadIdx.x < BN) {
+      float sum = 0.f;
+      for (int q = 0; q < RL; ++q) sum += red[q * BN + threadIdx.x];
+      meanv[threadIdx.x] = sum / (float)cnt;
+    }
+    __syncthreads();
+    const float4 mu = *reinterpret_cast<const float4*>(meanv + 4 * cg);
+    float4 sq = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int k = 0; k < RPT; ++k)
+      if (m0 + rl + k * RL < a.M) {
+        const float dx = v[k].x - mu.x, dy = v[k].y - mu.y, dz = v[k].z - mu.z, dw = v[k].w - mu.w;
+        sq.x += dx * dx; sq.y += dy * dy; sq.z += dz * dz; sq.w += dw * dw;
+      }
+    *reinterpret_cast<float4*>(red + rl * BN + 4 * cg) = sq;
+    __syncthreads();
+    if (threadIdx.x < BN && n0 + (int)threadIdx.x < a.N) {
+      float m2 = 0.f;
+      for (int q = 0; q < RL; ++q) m2 += red[q * BN + threadIdx.x];
+      a.stats[((size_t)mt * a.N + n0 + threadIdx.x) * 2 + 0] = meanv[threadIdx.x];
+      a.stats[((size_t)mt * a.N + n0 + threadIdx.x) * 2 + 1] = m2;
+    }
+  }
+}
+
+// One K-step's MFMA chain on a staged LDS-DMA tile (GL): fragment reads one chunk ahead.
+template <int BM, int BN, int MODE, int BK>
+__device__ __forceinline__ void kcompute_gl(const float* cur,
+                                            f32x16 (&acc)[Tile<BM, BN, MODE, BK, true>::RM][Tile<BM, BN, MODE, BK, true>::RN],
+                                            int wm, int wn, int r, int hh) {
+  using T = Tile<BM, BN, MODE, BK, true>;
+  float af[2][T::RM][4], bf[2][T::RN][4];
+  read_chunk<BM, BN, MODE, BK, true>(cur, cur + T::A_ELEMS, 0, af[0], bf[0], wm, wn, r, hh);
+#pragma unroll
+  for (int g = 0; g < T::NG; ++g) {
+    if (g + 1 < T::NG)
+      read_chunk<BM, BN, MODE, BK, true>(cur, cur + T::A_ELEMS, g + 1, af[(g + 1) & 1], bf[(g + 1) & 1], wm, wn, r, hh);
+    __builtin_amdgcn_sched_barrier(0);
+    mma_chunk<T::RM, T::RN>(af[g & 1], bf[g & 1], acc);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// s_waitcnt vmcnt(N) alone (expcnt / lgkmcnt left at their maxima), gfx9 encoding
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+
+// GL > 0: LDS-DMA staging through a GL-deep ring of LDS images — tile t+GL-1 is fetched
+// while tile t is multiplied, one raw s_barrier per K-step after a counted vmcnt (tile t
+// landed, newer tiles may still be in flight); no register stage, no ds_write.
+// One output tile (`tile`, already XCD-remapped) x one K split of a conv GEMM; the body of
+// both the single-GEMM kernel and the dual (wgrad + dgrad) kernel.
+template <int BM, int BN, int MODE, int BK, int SCHED, bool C4, int GL>
+__device__ __forceinline__ void gemm_body(const CsConvArgs& a, const int tile, const int split, const int nsplit,
+                                          float* smem) {
   using T = Tile<BM, BN, MODE, BK>;
-  extern __shared__ __attribute__((aligned(16))) float smem[];
   const int ntn = (a.N + BN - 1) / BN;
-  const int ntiles = ((a.M + BM - 1) / BM) * ntn;
-  const int tile = cs::xcd_remap(blockIdx.x, ntiles);
   const int mt = tile / ntn, nt = tile - mt * ntn;
   const int m0 = mt * BM, n0 = nt * BN;
-  const int split = blockIdx.z;
   const int ks_begin = split * a.ksteps_per_split;
   int ks_end = ks_begin + a.ksteps_per_split;
   if (ks_end > a.total_ksteps) ks_end = a.total_ksteps;
@@ -332,11 +544,40 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(CsConvArgs a) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
+  const int nks = ks_end - ks_begin;
+  if constexpr (GL > 0) {
+    using TG = Tile<BM, BN, MODE, BK, true>;
+    constexpr int NI = TG::AC + TG::BC;  // LDS-DMA instructions per wave per tile
+    constexpr int NB = GL;               // ring depth: tiles t+1 .. t+NB-1 in flight during tile t
+    Loader<BM, BN, MODE, BK, false, true> ld;
+    ld.init(a, m0, n0);
+#pragma unroll
+    for (int p = 0; p < NB - 1; ++p)
+      if (p < nks) ld.gload(a, (ks_begin + p) * BK, smem + p * TG::STAGE, smem + p * TG::STAGE + TG::A_ELEMS);
+    int cur = 0;
+    for (int t = 0; t < nks; ++t) {
+      // tile t has landed once at most `ahead` newer tiles are outstanding (loads retire in order)
+      const int ahead = min(NB - 2, nks - 1 - t);
+      if (ahead >= 4) wait_vmcnt<4 * NI>();
+      else if (ahead == 3) wait_vmcnt<3 * NI>();
+      else if (ahead == 2) wait_vmcnt<2 * NI>();
+      else if (ahead == 1) wait_vmcnt<NI>();
+      else wait_vmcnt<0>();
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      if (t + NB - 1 < nks) {
+        const int nx = cur == 0 ? NB - 1 : cur - 1;  // (t + NB - 1) % NB: the buffer read at step t-1
+        ld.gload(a, (ks_begin + t + NB - 1) * BK, smem + nx * TG::STAGE, smem + nx * TG::STAGE + TG::A_ELEMS);
+      }
+      kcompute_gl<BM, BN, MODE, BK>(smem + cur * TG::STAGE, acc, wm, wn, r, hh);
+      cur = cur == NB - 1 ? 0 : cur + 1;
+    }
+    __syncthreads();  // every wave's fragment reads are done before the epilogue reuses LDS
+  } else {
   Loader<BM, BN, MODE, BK, C4> ld;
   ld.init(a, m0, n0);
   float* lds0 = smem;
   float* lds1 = smem + T::STAGE;
-  const int nks = ks_end - ks_begin;
   if (nks > 0) {
     ld.template load<0>(a, ks_begin * BK);
     if (nks > 1) ld.template load<1>(a, (ks_begin + 1) * BK);
@@ -351,11 +592,12 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(CsConvArgs a) {
     kstep<BM, BN, MODE, BK, SCHED, 1, 0, C4>(ld, a, lds1, lds0, acc, wm, wn, r, hh, (ks_begin + t + 3) * BK);
     __syncthreads();
   }
+  }
 
   // ------------------------------------------------------------------ epilogue
   // C/D map (32x32 f32 MFMA): col = lane & 31, row = (reg&3) + 8*(reg>>2) + 4*(lane>>5).
   // Stores go through a buffer descriptor: rows/cols outside the GEMM get kOOB (dropped).
-  const bool slab = gridDim.z > 1;
+  const bool slab = nsplit > 1;
   if (slab || MODE == CS_CONV_DGRAD || (MODE == CS_CONV_WGRAD && !a.w_oihw)) {
     float* dst = slab ? a.ws + (size_t)split * a.M * a.N : a.out;
     const rsrc_t ro = make_rsrc(dst, (int64_t)a.M * a.N * 4);
@@ -370,6 +612,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(CsConvArgs a) {
           bstore1(ro, acc[i][j][e], (m < a.M && n < a.N) ? (m * a.N + n) * 4 : kOOB);
         }
       }
+    if (slab && a.counters != nullptr) splitk_fixup<BM, BN, MODE>(a, tile, mt, nt, nsplit, smem);
     if (slab || MODE != CS_CONV_FWD) return;
   }
   if constexpr (MODE == CS_CONV_WGRAD) {  // conv0: scatter the padded (tap, ci) columns to OIHW
@@ -450,6 +693,29 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(CsConvArgs a) {
   }
 }
 
+template <int BM, int BN, int MODE, int BK, int SCHED, bool C4, int GL>
+__global__ __launch_bounds__(256) void conv_gemm_kernel(CsConvArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int ntiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
+  gemm_body<BM, BN, MODE, BK, SCHED, C4, GL>(a, cs::xcd_remap(blockIdx.x, ntiles), blockIdx.z, gridDim.z, smem);
+}
+
+// Horizontal fusion of one block's two independent backward GEMMs: blocks [0, nb1) run the
+// weight gradient (64x64 tiles, K-step BK1, s1 splits), the rest the data gradient (64x64,
+// BK2, s2 splits) — one launch, one ramp and one tail instead of two.
+template <int BK1, int BK2>
+__global__ __launch_bounds__(256) void conv_dual_kernel(CsConvArgs wg, CsConvArgs dg, int nb1, int s1, int s2) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int b = blockIdx.x;
+  if (b < nb1) {
+    const int nt = ((wg.M + 63) / 64) * ((wg.N + 63) / 64);
+    gemm_body<64, 64, CS_CONV_WGRAD, BK1, 0, false, 0>(wg, cs::xcd_remap(b % nt, nt), b / nt, s1, smem);
+  } else {
+    const int nt = ((dg.M + 63) / 64) * ((dg.N + 63) / 64), c = b - nb1;
+    gemm_body<64, 64, CS_CONV_DGRAD, BK2, 0, false, 0>(dg, cs::xcd_remap(c % nt, nt), c / nt, s2, smem);
+  }
+}
+
 // Deterministic split-K combine: out = sum_z ws[z] (+bias, +BN tile stats for FWD;
 // OIHW scatter for the conv0 weight gradient). Tile = 16 rows x 64 columns (one row
 // and one float4 per thread) so even an M = 256 GEMM gets enough blocks to stream
@@ -475,12 +741,11 @@ __global__ __launch_bounds__(256) void splitk_fold_kernel(float* __restrict__ ws
   }
 }
 
-__global__ __launch_bounds__(256) void splitk_reduce_kernel(CsConvArgs a, int mode, int nslab, int zstep) {
-  __shared__ float red[kRedRows][64];
-  __shared__ float meanv[64];
+__device__ __forceinline__ void splitk_reduce_body(const CsConvArgs& a, int mode, int nslab, int zstep, int blk,
+                                                   float (&red)[kRedRows][64], float (&meanv)[64]) {
   const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
   const int ntn = (a.N + 63) / 64;
-  const int mt = blockIdx.x / ntn, nt = blockIdx.x - mt * ntn;
+  const int mt = blk / ntn, nt = blk - mt * ntn;
   const int m0 = mt * kRedRows, n0 = nt * 64, n = n0 + 4 * tx, m = m0 + ty;
   const size_t slab = (size_t)a.M * a.N;
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -535,8 +800,28 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(CsConvArgs a, int mo
   }
 }
 
-hipError_t launch_reduce(const CsConvArgs& a, int mode, int splits, hipStream_t stream) {
-  int nslab = splits, zstep = 1;
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(CsConvArgs a, int mode, int nslab, int zstep) {
+  __shared__ float red[kRedRows][64];
+  __shared__ float meanv[64];
+  splitk_reduce_body(a, mode, nslab, zstep, blockIdx.x, red, meanv);
+}
+
+// both split-K combines of a dual launch in one grid
+__global__ __launch_bounds__(256) void splitk_reduce_dual_kernel(CsConvArgs a1, int mode1, int nslab1, int zstep1,
+                                                                 int nb1, CsConvArgs a2, int mode2, int nslab2,
+                                                                 int zstep2) {
+  __shared__ float red[kRedRows][64];
+  __shared__ float meanv[64];
+  if ((int)blockIdx.x < nb1) splitk_reduce_body(a1, mode1, nslab1, zstep1, blockIdx.x, red, meanv);
+  else splitk_reduce_body(a2, mode2, nslab2, zstep2, blockIdx.x - nb1, red, meanv);
+}
+
+int reduce_blocks(const CsConvArgs& a) { return ((a.M + kRedRows - 1) / kRedRows) * ((a.N + 63) / 64); }
+
+// fold pre-pass for large split counts; returns (nslab, zstep) for the combine
+void fold_if_needed(const CsConvArgs& a, int splits, hipStream_t stream, int& nslab, int& zstep) {
+  nslab = splits;
+  zstep = 1;
   if (splits > 2 * kFold) {
     const size_t slab = (size_t)a.M * a.N;
     const int groups = (splits + kFold - 1) / kFold;
@@ -546,8 +831,12 @@ hipError_t launch_reduce(const CsConvArgs& a, int mode, int splits, hipStream_t 
     nslab = groups;
     zstep = kFold;
   }
-  const int nt = ((a.M + kRedRows - 1) / kRedRows) * ((a.N + 63) / 64);
-  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(nt), dim3(256), 0, stream, a, mode, nslab, zstep);
+}
+
+hipError_t launch_reduce(const CsConvArgs& a, int mode, int splits, hipStream_t stream) {
+  int nslab, zstep;
+  fold_if_needed(a, splits, stream, nslab, zstep);
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(reduce_blocks(a)), dim3(256), 0, stream, a, mode, nslab, zstep);
   return hipGetLastError();
 }
 
@@ -559,24 +848,65 @@ int conv_sched() {
   return v;
 }
 
+template <int BM, int BN, int MODE, int BK, int SCHED, bool C4, int GL>
+hipError_t launch_k(dim3 grid, size_t lds, hipStream_t stream, const CsConvArgs& a) {
+  hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, MODE, BK, SCHED, C4, GL>), grid, dim3(256), lds, stream, a);
+  return hipGetLastError();
+}
+
 template <int BM, int BN, int MODE, int BK>
-hipError_t launch_gemm(const CsConvArgs& a, int splits, hipStream_t stream) {
+hipError_t launch_gemm(const CsConvArgs& a, int splits, int stage, hipStream_t stream) {
   using T = Tile<BM, BN, MODE, BK>;
+  using TG = Tile<BM, BN, MODE, BK, true>;
   const int ntiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
   const size_t lds = 2 * T::STAGE * sizeof(float);
   const dim3 grid(ntiles, 1, splits);
-  if constexpr (MODE == CS_CONV_FWD) {
-    if (a.w_oihw) {  // padded conv0: Cin = 4 < BK
-      hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, MODE, BK, 0, true>), grid, dim3(256), lds, stream, a);
-      return hipGetLastError();
+  constexpr bool deep_fits = (BM + BN) * BK * 4 * 5 < 160 * 1024;
+  if (MODE == CS_CONV_FWD && a.w_oihw)  // padded conv0: Cin = 4 < BK
+    return launch_k<BM, BN, MODE, BK, 0, true, 0>(grid, lds, stream, a);
+  if constexpr (BK == 32) {
+    if (stage == CS_STAGE_LDS_DMA)
+      return launch_k<BM, BN, MODE, BK, 0, false, 3>(grid, 3 * TG::STAGE * sizeof(float), stream, a);
+    if constexpr (deep_fits) {
+      if (stage == CS_STAGE_LDS_DMA_DEEP)
+        return launch_k<BM, BN, MODE, BK, 0, false, 5>(grid, 5 * TG::STAGE * sizeof(float), stream, a);
     }
   }
-  if (conv_sched() == 1)
-    hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, MODE, BK, 1, false>), grid, dim3(256), lds, stream, a);
-  else
-    hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, MODE, BK, 0, false>), grid, dim3(256), lds, stream, a);
-  return hipGetLastError();
+  if (stage != CS_STAGE_REGS) return hipErrorInvalidValue;
+  if (conv_sched() == 1) return launch_k<BM, BN, MODE, BK, 1, false, 0>(grid, lds, stream, a);
+  return launch_k<BM, BN, MODE, BK, 0, false, 0>(grid, lds, stream, a);
 }
+
+// hipcc (ROCm 7.2) leaves some host-side kernel stubs undefined when they are only
+// implicitly instantiated through launch_k (an undefined-symbol error at import, seen for
+// the LDS-DMA variants); explicit instantiation of every launched variant emits them all.
+#define CS_K(BM_, BN_, MODE_, BK_, SCHED_, C4_, GL_) \
+  template __global__ void conv_gemm_kernel<BM_, BN_, MODE_, BK_, SCHED_, C4_, GL_>(CsConvArgs);
+#define CS_MODE(BM_, BN_, MODE_)                                            \
+  CS_K(BM_, BN_, MODE_, 16, 0, false, 0) CS_K(BM_, BN_, MODE_, 16, 1, false, 0) \
+  CS_K(BM_, BN_, MODE_, 32, 0, false, 0) CS_K(BM_, BN_, MODE_, 32, 1, false, 0) \
+  CS_K(BM_, BN_, MODE_, 32, 0, false, 3)
+#define CS_TILE(BM_, BN_)                                                                       \
+  CS_MODE(BM_, BN_, CS_CONV_FWD) CS_MODE(BM_, BN_, CS_CONV_DGRAD) CS_MODE(BM_, BN_, CS_CONV_WGRAD) \
+  CS_K(BM_, BN_, CS_CONV_FWD, 16, 0, true, 0) CS_K(BM_, BN_, CS_CONV_FWD, 32, 0, true, 0)
+CS_TILE(64, 64)
+CS_TILE(64, 128)
+CS_TILE(128, 64)
+CS_TILE(128, 128)
+#define CS_DEEP(BM_, BN_)                                                                  \
+  CS_K(BM_, BN_, CS_CONV_FWD, 32, 0, false, 5) CS_K(BM_, BN_, CS_CONV_DGRAD, 32, 0, false, 5) \
+  CS_K(BM_, BN_, CS_CONV_WGRAD, 32, 0, false, 5)
+CS_DEEP(64, 64)
+CS_DEEP(64, 128)
+CS_DEEP(128, 64)
+#undef CS_DEEP
+template __global__ void conv_dual_kernel<16, 16>(CsConvArgs, CsConvArgs, int, int, int);
+template __global__ void conv_dual_kernel<16, 32>(CsConvArgs, CsConvArgs, int, int, int);
+template __global__ void conv_dual_kernel<32, 16>(CsConvArgs, CsConvArgs, int, int, int);
+template __global__ void conv_dual_kernel<32, 32>(CsConvArgs, CsConvArgs, int, int, int);
+#undef CS_TILE
+#undef CS_MODE
+#undef CS_K
 
 int ilog2(int v) {
   int l = 0;
@@ -609,6 +939,15 @@ void cs_conv_fill_dims(CsConvArgs* a, int mode) {
   }
 }
 
+bool cs_conv_fixup_ok(int splits, int bm, int bn) {
+  return splits > 1 && (int64_t)splits * bm * bn * 4 <= CS_FIXUP_MAX_BYTES;
+}
+
+int cs_conv_stat_rows(int K, int bm, int bn, int bk, int splits, bool counters) {
+  const int s = cs_conv_effective_splits(K, bk, splits);
+  return (s == 1 || (counters && cs_conv_fixup_ok(s, bm, bn))) ? bm : CS_SPLITK_STAT_ROWS;
+}
+
 int cs_conv_effective_splits(int K, int bk, int splits) {
   const int ks = (K + bk - 1) / bk;
   int s = splits < 1 ? 1 : (splits > ks ? ks : splits);
@@ -616,25 +955,69 @@ int cs_conv_effective_splits(int K, int bk, int splits) {
   return (ks + per - 1) / per;
 }
 
-hipError_t cs_conv_gemm(CsConvArgs a, int mode, int bm, int bn, int bk, int splits, hipStream_t stream) {
-  if (bk != 16 && bk != 32) return hipErrorInvalidValue;
+namespace {
+// dims, K-step split and size checks shared by the single and dual launchers; -> effective splits or -1
+int prep_gemm(CsConvArgs& a, int mode, int bk, int splits) {
+  if (bk != 16 && bk != 32) return -1;
   cs_conv_fill_dims(&a, mode);
   // 32-bit buffer offsets: every operand / output / workspace must stay below 2 GiB
   const int64_t pix = (int64_t)a.B * a.H * a.W;
   const int64_t big = std::max<int64_t>(pix * std::max(a.Cin, a.Cout), (int64_t)a.M * a.N) * 4;
-  if (big >= 0x7ffffff0ll) return hipErrorInvalidValue;
+  if (big >= 0x7ffffff0ll) return -1;
   a.total_ksteps = (a.K + bk - 1) / bk;
   splits = cs_conv_effective_splits(a.K, bk, splits);
   a.ksteps_per_split = (a.total_ksteps + splits - 1) / splits;
-  if (splits > 1 && a.ws == nullptr) return hipErrorInvalidValue;
-  if (splits > 1 && (int64_t)splits * a.M * a.N * 4 >= 0x7ffffff0ll) return hipErrorInvalidValue;
+  if (splits > 1 && a.ws == nullptr) return -1;
+  if (splits > 1 && (int64_t)splits * a.M * a.N * 4 >= 0x7ffffff0ll) return -1;
+  return splits;
+}
+}  // namespace
+
+hipError_t cs_conv_gemm_dual(CsConvArgs wg, int wbk, int wsplits, CsConvArgs dg, int dbk, int dsplits,
+                             hipStream_t stream) {
+  if (wg.w_oihw) return hipErrorInvalidValue;  // conv0 has no data gradient
+  wg.counters = dg.counters = nullptr;
+  const int s1 = prep_gemm(wg, CS_CONV_WGRAD, wbk, wsplits), s2 = prep_gemm(dg, CS_CONV_DGRAD, dbk, dsplits);
+  if (s1 < 0 || s2 < 0) return hipErrorInvalidValue;
+  if (s1 > 1 && s2 > 1 && wg.ws == dg.ws) return hipErrorInvalidValue;  // slabs must not alias
+  const int nt1 = ((wg.M + 63) / 64) * ((wg.N + 63) / 64), nt2 = ((dg.M + 63) / 64) * ((dg.N + 63) / 64);
+  const int nb1 = nt1 * s1, nb = nb1 + nt2 * s2;
+  const size_t lds = 2 * (size_t)std::max(Tile<64, 64, CS_CONV_WGRAD, 32>::STAGE, Tile<64, 64, CS_CONV_DGRAD, 32>::STAGE) *
+                     sizeof(float);
+#define CS_DUAL(B1, B2)                                                                                      \
+  if (wbk == B1 && dbk == B2)                                                                                \
+    hipLaunchKernelGGL((conv_dual_kernel<B1, B2>), dim3(nb), dim3(256), lds, stream, wg, dg, nb1, s1, s2);
+  CS_DUAL(16, 16)
+  CS_DUAL(16, 32)
+  CS_DUAL(32, 16)
+  CS_DUAL(32, 32)
+#undef CS_DUAL
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || (s1 == 1 && s2 == 1)) return e;
+  if (s1 > 1 && s2 > 1) {
+    int ns1, z1, ns2, z2;
+    fold_if_needed(wg, s1, stream, ns1, z1);
+    fold_if_needed(dg, s2, stream, ns2, z2);
+    const int r1 = reduce_blocks(wg);
+    hipLaunchKernelGGL(splitk_reduce_dual_kernel, dim3(r1 + reduce_blocks(dg)), dim3(256), 0, stream, wg,
+                       (int)CS_CONV_WGRAD, ns1, z1, r1, dg, (int)CS_CONV_DGRAD, ns2, z2);
+    return hipGetLastError();
+  }
+  return s1 > 1 ? launch_reduce(wg, CS_CONV_WGRAD, s1, stream) : launch_reduce(dg, CS_CONV_DGRAD, s2, stream);
+}
+
+hipError_t cs_conv_gemm(CsConvArgs a, int mode, int bm, int bn, int bk, int splits, hipStream_t stream, int stage) {
+  if (stage != CS_STAGE_REGS && (bk != 32 || (a.w_oihw && mode == CS_CONV_FWD))) return hipErrorInvalidValue;
+  splits = prep_gemm(a, mode, bk, splits);
+  if (splits < 0) return hipErrorInvalidValue;
+  if (!cs_conv_fixup_ok(splits, bm, bn)) a.counters = nullptr;
 #define CS_DISPATCH(BM_, BN_, BK_)                                                                       \
   if (bm == BM_ && bn == BN_ && bk == BK_) {                                                             \
     hipError_t e;                                                                                        \
-    if (mode == CS_CONV_FWD) e = launch_gemm<BM_, BN_, CS_CONV_FWD, BK_>(a, splits, stream);            \
-    else if (mode == CS_CONV_DGRAD) e = launch_gemm<BM_, BN_, CS_CONV_DGRAD, BK_>(a, splits, stream);   \
-    else e = launch_gemm<BM_, BN_, CS_CONV_WGRAD, BK_>(a, splits, stream);                              \
-    if (e != hipSuccess || splits == 1) return e;                                                        \
+    if (mode == CS_CONV_FWD) e = launch_gemm<BM_, BN_, CS_CONV_FWD, BK_>(a, splits, stage, stream);     \
+    else if (mode == CS_CONV_DGRAD) e = launch_gemm<BM_, BN_, CS_CONV_DGRAD, BK_>(a, splits, stage, stream); \
+    else e = launch_gemm<BM_, BN_, CS_CONV_WGRAD, BK_>(a, splits, stage, stream);                       \
+    if (e != hipSuccess || splits == 1 || a.counters != nullptr) return e;                               \
     return launch_reduce(a, mode, splits, stream);                                                       \
   }
   CS_DISPATCH(64, 64, 16)

@@ -41,6 +41,7 @@ struct CsConvArgs {
   float* out;         // FWD: y [M][Cout]; DGRAD: dx [M][Cin]; WGRAD: dW (OHWI, or OIHW for conv0)
   float* ws;          // split-K slabs [splits][M][N] (required when splits > 1)
   float* stats;       // FWD: per-row-tile BN partials [tiles][Cout][2] = (mean, M2); may be null
+  int* counters;      // split-K tile tickets (zeroed, >= #tiles ints) for the in-launch combine; null = reduce kernel
   int B, H, W, Cin, Cout;
   int w_oihw;
   // filled by the launcher:
@@ -51,9 +52,24 @@ void cs_conv_fill_dims(CsConvArgs* a, int mode);
 // bm, bn in {64, 128}; bk in {16, 32}; splits >= 1 (split-K over blockIdx.z + deterministic reduce).
 // FWD stats tiles have `bm` rows when splits == 1 and CS_SPLITK_STAT_ROWS rows otherwise.
 #define CS_SPLITK_STAT_ROWS 16
-hipError_t cs_conv_gemm(CsConvArgs a, int mode, int bm, int bn, int bk, int splits, hipStream_t stream);
+// stage: CS_STAGE_REGS (global -> registers -> ds_write, padded LDS) or CS_STAGE_LDS_DMA(_DEEP)
+// (buffer_load ... lds into a 3- (5-) deep ring of swizzled images; bk = 32, not conv0's fwd;
+// the deep ring only where 5 images fit the 160 KiB LDS)
+enum { CS_STAGE_REGS = 0, CS_STAGE_LDS_DMA = 1, CS_STAGE_LDS_DMA_DEEP = 2 };
+hipError_t cs_conv_gemm(CsConvArgs a, int mode, int bm, int bn, int bk, int splits, hipStream_t stream,
+                        int stage = CS_STAGE_REGS);
+// one launch for a block's weight gradient (wg) and data gradient (dg), both 64x64 tiles with
+// register staging (K-steps wbk / dbk in {16, 32}); split-K slabs combined by one launch
+// (their workspaces must differ)
+hipError_t cs_conv_gemm_dual(CsConvArgs wg, int wbk, int wsplits, CsConvArgs dg, int dbk, int dsplits,
+                             hipStream_t stream);
 // the split count cs_conv_gemm actually launches (K-steps re-balanced over splits)
 int cs_conv_effective_splits(int K, int bk, int splits);
+// split-K slabs of one tile a single block combines in-launch (S * BM * BN * 4 bytes)
+#define CS_FIXUP_MAX_BYTES (256 << 10)
+bool cs_conv_fixup_ok(int splits, int bm, int bn);
+// FWD statistics tile height for a launch (bm, or CS_SPLITK_STAT_ROWS behind the reduce kernel)
+int cs_conv_stat_rows(int K, int bm, int bn, int bk, int splits, bool counters);
 
 // ---------------------------------------------------------------- BatchNorm + ReLU (+ 2x2 max-pool), NHWC
 hipError_t cs_bn_finalize(const float* part, int T, int R, int M, int C, const float* gamma, const float* beta,

@@ -2,6 +2,9 @@
 
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 
+#include <stdio.h>
+#include <stdlib.h>
+
 #include <algorithm>
 #include <stdexcept>
 #include <string>
@@ -139,6 +142,16 @@ VggEngine::VggEngine(int64_t Bmax, std::vector<int64_t> desc, std::vector<int64_
     ok(hipEventCreateWithFlags(&ev_bn_[l], hipEventDisableTiming), "event");
     ok(hipEventCreateWithFlags(&ev_wg_[l], hipEventDisableTiming), "event");
   }
+  // split-K tile tickets for the in-launch combine: one zeroed region per (block, mode) call site
+  tiles_max_ = 1;
+  for (int64_t l = 0; l < L; ++l)
+    for (int m = 0; m < 3; ++m) {
+      const Dims d = dims(blocks_[l], m, Bmax);
+      tiles_max_ = std::max(tiles_max_, cdiv(d.M, 64) * cdiv(d.N, 64));
+    }
+  counters_ = torch::zeros({3 * L * tiles_max_}, fo.dtype(at::kInt));
+  if (const char* e = getenv("CS_CONV_FIXUP")) fixup_ = atoi(e) != 0;
+  if (const char* e = getenv("CS_CONV_DUAL")) dual_ = atoi(e) != 0;
   bn_part_ = torch::zeros({partmax}, fo);
   bn_coef_ = torch::zeros({cmax * 3}, fo);
   bn_eval_ = torch::zeros({2, cmax}, fo);
@@ -175,8 +188,7 @@ void VggEngine::set_data(int64_t slot, torch::Tensor data, torch::Tensor labels,
   aug_[slot] = aug;
 }
 
-void VggEngine::conv(int l, int mode, int B, const ConvTile& t, hipStream_t s, bool with_stats, float* ws,
-                     float* dz) {
+CsConvArgs VggEngine::conv_args(int l, int mode, int B, bool with_stats, float* ws, float* dz) {
   VggBlock& b = blocks_[l];
   const int L = (int)blocks_.size();
   CsConvArgs a{};
@@ -187,10 +199,8 @@ void VggEngine::conv(int l, int mode, int B, const ConvTile& t, hipStream_t s, b
   a.Cout = b.cout;
   a.w_oihw = (l == 0 && b.cin == 4) ? 1 : 0;
   a.ws = ws != nullptr ? ws : ws_.data_ptr<float>();
+  a.counters = fixup_ ? counters_.data_ptr<int>() + (3 * l + mode) * tiles_max_ : nullptr;
   if (dz == nullptr) dz = dz_[0].data_ptr<float>();
-  const Dims d = dims(b, mode, B);
-  const int sp = eff_splits(d.K, t.splits, t.bk);
-  TORCH_CHECK(sp == 1 || (int64_t)sp * d.M * d.N <= ws_elems_, "VggEngine: split-K workspace too small");
   if (mode == CS_CONV_FWD) {
     a.x = b.x.data_ptr<float>();
     a.w = P(b.w_off);
@@ -207,7 +217,33 @@ void VggEngine::conv(int l, int mode, int B, const ConvTile& t, hipStream_t s, b
     a.dz = dz;
     a.out = G(b.w_off);
   }
-  ok(cs_conv_gemm(a, mode, t.bm, t.bn, t.bk, t.splits, s), "conv_gemm");
+  return a;
+}
+
+void VggEngine::conv(int l, int mode, int B, const ConvTile& t, hipStream_t s, bool with_stats, float* ws,
+                     float* dz) {
+  VggBlock& b = blocks_[l];
+  CsConvArgs a = conv_args(l, mode, B, with_stats, ws, dz);
+  const Dims d = dims(b, mode, B);
+  const int sp = eff_splits(d.K, t.splits, t.bk);
+  TORCH_CHECK(sp == 1 || (int64_t)sp * d.M * d.N <= ws_elems_, "VggEngine: split-K workspace too small");
+  ok(cs_conv_gemm(a, mode, t.bm, t.bn, t.bk, t.splits, s, t.stage), "conv_gemm");
+}
+
+bool VggEngine::dual_ok(int l) const {
+  if (!dual_ || l == 0 || !blocks_[l].use_dual) return false;
+  const ConvTile& w = blocks_[l].tile[CS_CONV_WGRAD];
+  const ConvTile& d = blocks_[l].tile[CS_CONV_DGRAD];
+  return w.bm == 64 && w.bn == 64 && w.stage == CS_STAGE_REGS && d.bm == 64 && d.bn == 64 &&
+         d.stage == CS_STAGE_REGS;
+}
+
+void VggEngine::conv_dual(int l, int B, hipStream_t s, float* dz) {
+  const ConvTile& w = blocks_[l].tile[CS_CONV_WGRAD];
+  const ConvTile& d = blocks_[l].tile[CS_CONV_DGRAD];
+  CsConvArgs wa = conv_args(l, CS_CONV_WGRAD, B, false, ws_side_.data_ptr<float>(), dz);
+  CsConvArgs da = conv_args(l, CS_CONV_DGRAD, B, false, nullptr, dz);
+  ok(cs_conv_gemm_dual(wa, w.bk, w.splits, da, d.bk, d.splits, s), "conv_gemm_dual");
 }
 
 void VggEngine::forward_train(int64_t B) {
@@ -225,7 +261,7 @@ void VggEngine::forward_train(int64_t B) {
     const ConvTile& t = b.tile[CS_CONV_FWD];
     conv(l, CS_CONV_FWD, (int)B, t, s, true);
     const int64_t M = B * b.H * b.H;
-    const int rows = eff_splits(9ll * b.cin, t.splits, t.bk) > 1 ? CS_SPLITK_STAT_ROWS : t.bm;
+    const int rows = cs_conv_stat_rows(9 * b.cin, t.bm, t.bn, t.bk, t.splits, fixup_);
     float* bn = b.bn.data_ptr<float>();
     float* bufs = bufs_.data_ptr<float>();
     ok(cs_bn_finalize(b.stats.data_ptr<float>(), (int)cdiv(M, rows), rows, (int)M, b.cout, P(b.g_off), P(b.be_off),
@@ -258,6 +294,10 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
                  bn, bn + b.cout, bn + 2 * b.cout, bn + 3 * b.cout, P(b.g_off), bn_part_.data_ptr<float>(),
                  bn_coef_.data_ptr<float>(), G(b.g_off), G(b.be_off), G(b.b_off), dz, s),
        "bn_bwd");
+    if (!overlap_wgrad_ && dual_ok(l)) {  // wgrad + dgrad in one launch
+      conv_dual(l, (int)B, s, dz);
+      continue;
+    }
     if (overlap_wgrad_) {
       ok(hipEventRecord(ev_bn_[l], s), "record bn");
       ok(hipStreamWaitEvent(side_, ev_bn_[l], 0), "side wait");
@@ -347,11 +387,15 @@ void VggEngine::step(int64_t B, RcclComm* comm, const std::vector<int64_t>& buck
   sgd(lr, momentum, wd, dampening, 0, params_.numel());
 }
 
-void VggEngine::set_tile(int64_t block, int64_t mode, int64_t bm, int64_t bn, int64_t splits, int64_t bk) {
+void VggEngine::set_tile(int64_t block, int64_t mode, int64_t bm, int64_t bn, int64_t splits, int64_t bk,
+                         int64_t stage) {
   TORCH_CHECK(block >= 0 && block < (int64_t)blocks_.size() && mode >= 0 && mode <= 2, "set_tile: index");
   TORCH_CHECK((bm == 64 || bm == 128) && (bn == 64 || bn == 128) && splits >= 1 && splits <= 1024, "set_tile: tile");
   const Dims d = dims(blocks_[block], (int)mode, Bmax_);
   TORCH_CHECK(bk == 16 || bk == 32, "set_tile: bk must be 16 or 32");
+  TORCH_CHECK(stage == CS_STAGE_REGS || ((stage == CS_STAGE_LDS_DMA || stage == CS_STAGE_LDS_DMA_DEEP) && bk == 32 &&
+                                         !(block == 0 && mode == CS_CONV_FWD && blocks_[0].cin == 4)),
+              "set_tile: LDS-DMA staging needs bk 32 (and not conv0's padded forward)");
   const int sp = eff_splits(d.K, (int)splits, (int)bk);
   TORCH_CHECK(sp == 1 || (int64_t)sp * d.M * d.N <= ws_elems_, "set_tile: split-K workspace too small");
   ConvTile& t = blocks_[block].tile[mode];
@@ -359,13 +403,14 @@ void VggEngine::set_tile(int64_t block, int64_t mode, int64_t bm, int64_t bn, in
   t.bn = (int)bn;
   t.splits = (int)splits;
   t.bk = (int)bk;
+  t.stage = (int)stage;
   t.us = -1.f;
 }
 
 std::vector<int64_t> VggEngine::get_tile(int64_t block, int64_t mode) const {
   TORCH_CHECK(block >= 0 && block < (int64_t)blocks_.size() && mode >= 0 && mode <= 2, "get_tile: index");
   const ConvTile& t = blocks_[block].tile[mode];
-  return {t.bm, t.bn, t.splits, t.bk};
+  return {t.bm, t.bn, t.splits, t.bk, t.stage};
 }
 
 void VggEngine::run_conv(int64_t block, int64_t mode, int64_t B) {
@@ -383,6 +428,8 @@ std::vector<double> VggEngine::autotune(int64_t B, int64_t iters) {
   ok(hipEventCreate(&e1), "event");
   std::vector<double> best_us;
   const int split_opts[] = {1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 64, 128, 256};
+  ConvTile best64[3];
+  float best64_t[3] = {1e30f, 1e30f, 1e30f};
   for (int l = 0; l < (int)blocks_.size(); ++l) {
     for (int mode = 0; mode < 3; ++mode) {
       if (l == 0 && mode == CS_CONV_DGRAD) {
@@ -392,16 +439,22 @@ std::vector<double> VggEngine::autotune(int64_t B, int64_t iters) {
       const Dims d = dims(blocks_[l], mode, B);
       ConvTile best = blocks_[l].tile[mode];
       float best_t = 1e30f;
+      best64[mode] = best;
+      best64_t[mode] = 1e30f;
       std::vector<std::vector<int>> seen;
+      const bool conv0_fwd = l == 0 && mode == CS_CONV_FWD && blocks_[0].cin == 4;
+      for (int stage : {(int)CS_STAGE_REGS, (int)CS_STAGE_LDS_DMA, (int)CS_STAGE_LDS_DMA_DEEP})
       for (int bk : {16, 32}) {
+        if (stage != CS_STAGE_REGS && (bk != 32 || conv0_fwd)) continue;
         const int64_t ks = cdiv(d.K, bk);
         for (int bm : {64, 128}) {
           for (int bn : {64, 128}) {
+            if (stage == CS_STAGE_LDS_DMA_DEEP && (bm + bn) * bk * 4 * 5 >= 160 * 1024) continue;
             for (int sp : split_opts) {
               if (sp > 1 && ks / sp < 2) continue;
               const int e = eff_splits(d.K, sp, bk);
               if (e > 1 && (int64_t)e * d.M * d.N > ws_elems_) continue;
-              std::vector<int> key = {bm, bn, bk, e};
+              std::vector<int> key = {bm, bn, bk, e, stage};
               if (std::find(seen.begin(), seen.end(), key) != seen.end()) continue;
               seen.push_back(key);
               ConvTile t;
@@ -409,6 +462,7 @@ std::vector<double> VggEngine::autotune(int64_t B, int64_t iters) {
               t.bn = bn;
               t.bk = bk;
               t.splits = sp;
+              t.stage = stage;
               conv(l, mode, (int)B, t, s, mode == CS_CONV_FWD);  // warm
               ok(hipEventRecord(e0, s), "record");
               for (int64_t i = 0; i < iters; ++i) conv(l, mode, (int)B, t, s, mode == CS_CONV_FWD);
@@ -421,6 +475,10 @@ std::vector<double> VggEngine::autotune(int64_t B, int64_t iters) {
                 best_t = us;
                 best = t;
               }
+              if (bm == 64 && bn == 64 && stage == CS_STAGE_REGS && us < best64_t[mode]) {
+                best64_t[mode] = us;
+                best64[mode] = t;
+              }
             }
           }
         }
@@ -428,6 +486,38 @@ std::vector<double> VggEngine::autotune(int64_t B, int64_t iters) {
       best.us = best_t;
       blocks_[l].tile[mode] = best;
       best_us.push_back(best_t);
+    }
+    // joint choice for the backward pair: the dual launch with the best 64x64 register-staged
+    // wgrad / dgrad tiles, or the two separately tuned launches, whichever is faster
+    VggBlock& b = blocks_[l];
+    b.use_dual = false;
+    if (dual_ && l > 0 && best64_t[CS_CONV_WGRAD] < 1e29f && best64_t[CS_CONV_DGRAD] < 1e29f) {
+      const ConvTile keep_w = b.tile[CS_CONV_WGRAD], keep_d = b.tile[CS_CONV_DGRAD];
+      b.tile[CS_CONV_WGRAD] = best64[CS_CONV_WGRAD];
+      b.tile[CS_CONV_DGRAD] = best64[CS_CONV_DGRAD];
+      float* dz = dz_[l & 1].data_ptr<float>();
+      conv_dual(l, (int)B, s, dz);  // warm
+      ok(hipEventRecord(e0, s), "record");
+      for (int64_t i = 0; i < iters; ++i) conv_dual(l, (int)B, s, dz);
+      ok(hipEventRecord(e1, s), "record");
+      ok(hipEventSynchronize(e1), "sync");
+      float ms = 0.f;
+      ok(hipEventElapsedTime(&ms, e0, e1), "elapsed");
+      const float dual_us = 1000.f * ms / (float)iters;
+      const float sep_us = keep_w.us + keep_d.us;
+      if (getenv("CS_TUNE_VERBOSE"))
+        fprintf(stderr, "[tune] block %d: dual %.1f us vs separate %.1f us\n", l, dual_us, sep_us);
+      if (dual_us < sep_us) {
+        b.use_dual = true;
+        const float wsh = best64_t[CS_CONV_WGRAD] / (best64_t[CS_CONV_WGRAD] + best64_t[CS_CONV_DGRAD]);
+        b.tile[CS_CONV_WGRAD].us = dual_us * wsh;
+        b.tile[CS_CONV_DGRAD].us = dual_us * (1.f - wsh);
+        best_us[3 * l + CS_CONV_WGRAD] = b.tile[CS_CONV_WGRAD].us;
+        best_us[3 * l + CS_CONV_DGRAD] = b.tile[CS_CONV_DGRAD].us;
+      } else {
+        b.tile[CS_CONV_WGRAD] = keep_w;
+        b.tile[CS_CONV_DGRAD] = keep_d;
+      }
     }
   }
   hipEventDestroy(e0);

