@@ -33,7 +33,7 @@ int64_t conv_gemm(int64_t mode, c10::optional<torch::Tensor> x, c10::optional<to
   TORCH_CHECK(mode >= 0 && mode <= 2, "conv_gemm: bad mode");
   TORCH_CHECK(pow2(H) && pow2(W) && pow2(Cin) && pow2(Cout) && Cin >= 4 && Cout >= 64 && B > 0,
               "conv_gemm: H, W, Cin, Cout must be powers of two (Cin>=4, Cout>=64)");
-  TORCH_CHECK((bm == 64 || bm == 128) && (bn == 64 || bn == 128) && (bk == 16 || bk == 32) && splits >= 1,
+  TORCH_CHECK((bm == 64 || bm == 128) && (bn == 64 || bn == 128) && (bk == 16 || bk == 32 || bk == 64) && splits >= 1,
               "conv_gemm: bad tiling");
   TORCH_CHECK(!w_oihw || Cin == 4, "conv_gemm: OIHW weights only for the padded conv0 (Cin=4)");
   if (mode == CS_CONV_DGRAD) TORCH_CHECK(Cin >= 64 && !w_oihw, "conv_gemm: dgrad needs Cin >= 64");
@@ -70,9 +70,9 @@ int64_t conv_gemm(int64_t mode, c10::optional<torch::Tensor> x, c10::optional<to
   DevGuard g(out.device());
   a.x = cptr(x); a.w = cptr(w); a.dz = cptr(dz); a.bias = cptr(bias);
   a.out = out.data_ptr<float>(); a.ws = mptr(ws); a.stats = mptr(stats);
-  TORCH_CHECK(stage == CS_STAGE_REGS || ((stage == CS_STAGE_LDS_DMA || stage == CS_STAGE_LDS_DMA_DEEP) && bk == 32 &&
-                                         !(w_oihw && mode == CS_CONV_FWD)),
-              "conv_gemm: LDS-DMA staging needs bk 32 and not conv0's forward");
+  TORCH_CHECK(cs_conv_stage_ok((int)stage, (int)bm, (int)bn, (int)bk, w_oihw && mode == CS_CONV_FWD) &&
+                  !(bk == 64 && w_oihw && mode == CS_CONV_FWD),
+              "conv_gemm: no kernel for stage ", stage, " / ", bm, "x", bn, " / bk ", bk);
   CS_LAUNCH(cs_conv_gemm(a, (int)mode, (int)bm, (int)bn, (int)bk, (int)splits, cur_stream(), (int)stage));
   return cs_conv_stat_rows(a.K, bm, bn, bk, splits, counters.has_value());
 }
@@ -149,6 +149,9 @@ void register_conv_ops(pybind11::module& m) {
         py::arg("stats"), py::arg("B"), py::arg("H"), py::arg("W"), py::arg("Cin"), py::arg("Cout"),
         py::arg("w_oihw"), py::arg("bm"), py::arg("bn"), py::arg("splits"), py::arg("bk") = 16,
         py::arg("counters") = py::none(), py::arg("stage") = 0);
+  m.def("conv_stage_ok", [](int64_t stage, int64_t bm, int64_t bn, int64_t bk, bool conv0_fwd) {
+    return cs_conv_stage_ok((int)stage, (int)bm, (int)bn, (int)bk, conv0_fwd) && !(bk == 64 && conv0_fwd);
+  }, "whether a conv GEMM (staging, tile, K-step) variant exists");
   m.def("conv_stat_rows", [](int64_t K, int64_t bm, int64_t bn, int64_t bk, int64_t splits, bool counters) {
     return cs_conv_stat_rows((int)K, (int)bm, (int)bn, (int)bk, (int)splits, counters);
   }, "FWD BN-statistics tile height of a conv_gemm launch");

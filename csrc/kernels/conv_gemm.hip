@@ -86,14 +86,20 @@ struct Traits<CS_CONV_WGRAD> {
 // GL = LDS-DMA staging (buffer_load ... lds): images are lane-linear, so unpadded; a
 // K-contiguous row (BK = 32 -> 8 float4 chunks) stores logical chunk c at physical chunk
 // c ^ ((row >> 1) & 7), which makes the ds_read_b128 fragment reads conflict-free.
-template <int BM, int BN, int MODE, int BK, bool GL = false>
+// KG = K-groups: the block has 4*KG waves; wave group g multiplies sub-step chunks
+// [g*NG/KG, (g+1)*NG/KG) of every K-step on the shared LDS tile, and the KG partial
+// accumulators are summed through LDS (fixed order) before the epilogue — more waves per
+// SIMD for latency hiding without more split-K slabs.
+template <int BM, int BN, int MODE, int BK, bool GL = false, int KG = 1>
 struct Tile {
+  static constexpr int NT = 256 * KG;  // threads per block
   static constexpr bool A_KC = Traits<MODE>::A_KC, B_KC = Traits<MODE>::B_KC;
   static constexpr int A_ELEMS = GL ? BM * BK : (A_KC ? BM * (BK + 4) : BK * (BM + 4));
   static constexpr int B_ELEMS = GL ? BN * BK : (B_KC ? BN * (BK + 4) : BK * (BN + 4));
   static constexpr int STAGE = A_ELEMS + B_ELEMS;
-  static constexpr int AC = BM * BK / 1024;  // float4 chunks per thread per stage
-  static constexpr int BC = BN * BK / 1024;
+  static constexpr int AC = BM * BK / (4 * NT);  // float4 chunks per thread per stage
+  static constexpr int BC = BN * BK / (4 * NT);
+  static_assert(AC >= 1 && BC >= 1, "tile too small for this many threads");
   static constexpr int KQ = BK / 4;          // float4 chunks per K-contiguous row
   static constexpr int HK = BK / 2;          // MFMA sub-steps per K-step
   static constexpr int NG = HK / 4;          // 4-deep sub-step chunks per K-step
@@ -106,9 +112,9 @@ struct Tile {
 // GL: the same per-chunk offsets feed LDS-DMA instead of registers. Chunk i of a thread is
 // then slot s = (wave * AC + i) * 64 + lane of the operand's lane-linear LDS image (one
 // 1 KiB wave-instruction per chunk index), instead of q = tid + 256 * i.
-template <int BM, int BN, int MODE, int BK, bool C4 = false, bool GL = false>
+template <int BM, int BN, int MODE, int BK, bool C4 = false, bool GL = false, int KG = 1>
 struct Loader {
-  using T = Tile<BM, BN, MODE, BK, GL>;
+  using T = Tile<BM, BN, MODE, BK, GL, KG>;
   rsrc_t ra_, rb_;
   int av[T::AC], bv[T::BC];        // per-thread fixed byte offsets
   unsigned am[T::AC], bm_[T::BC];  // per-thread tap masks / flags
@@ -124,7 +130,7 @@ struct Loader {
       row = s / T::KQ;
       c = (s % T::KQ) ^ ((row >> 1) & 7);
     } else {
-      const int q = threadIdx.x + 256 * i;
+      const int q = threadIdx.x + T::NT * i;
       row = q / T::KQ;
       c = q % T::KQ;
     }
@@ -133,7 +139,7 @@ struct Loader {
   __device__ static void slot_km(int i, int& kr, int& c) {
     constexpr int CPR = ROWS / 4;
     const int s = GL ? (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * CHUNKS + i) * 64 + (threadIdx.x & 63)
-                     : threadIdx.x + 256 * i;
+                     : threadIdx.x + T::NT * i;
     kr = s / CPR;
     c = s - kr * CPR;
   }
@@ -253,7 +259,7 @@ struct Loader {
       const int lgC = a.lgCin;
 #pragma unroll
       for (int i = 0; i < T::AC; ++i) {
-        const int c = (threadIdx.x + 256 * i) % T::KQ;
+        const int c = (threadIdx.x + T::NT * i) % T::KQ;
         const int tap = (k0 >> lgC) + c;
         const int t3 = tap / 3, dh = t3 - 1, dw = tap - 3 * t3 - 1;
         const int sh = dh * a.W + dw;
@@ -265,9 +271,9 @@ struct Loader {
 #pragma unroll
     for (int i = 0; i < T::BC; ++i) {
       if constexpr (MODE == CS_CONV_FWD && C4) {  // conv0: OIHW [Cout][3][3x3], K = 9 taps x 4 (padded) channels
-        const int tap = (k0 >> 2) + (threadIdx.x + 256 * i) % T::KQ;
+        const int tap = (k0 >> 2) + (threadIdx.x + T::NT * i) % T::KQ;
         const bool ok = bm_[i] && tap < 9;
-        const int e = bv[i] - ((threadIdx.x + 256 * i) % T::KQ) + tap;  // n*27 + tap
+        const int e = bv[i] - ((threadIdx.x + T::NT * i) % T::KQ) + tap;  // n*27 + tap
         const float* wr = a.w + (ok ? e : 0);
         rb[S][i] = ok ? make_float4(wr[0], wr[9], wr[18], 0.f) : make_float4(0.f, 0.f, 0.f, 0.f);
       } else {
@@ -344,21 +350,25 @@ __device__ __forceinline__ void mma_chunk(const float (&af)[RM][4], const float 
 //          go out after the first chunk, the LDS store after the second (sched barriers
 //          pin the phases so hipcc cannot hoist every read ahead of the chain).
 // SCHED 1: same code order, compiler schedules freely.
-template <int BM, int BN, int MODE, int BK, int SCHED, int LS, int SS, bool C4>
-__device__ __forceinline__ void kstep(Loader<BM, BN, MODE, BK, C4>& ld, const CsConvArgs& a, const float* cur,
-                                      float* nxt, f32x16 (&acc)[Tile<BM, BN, MODE, BK>::RM][Tile<BM, BN, MODE, BK>::RN],
-                                      int wm, int wn, int r, int hh, int k_load) {
+template <int BM, int BN, int MODE, int BK, int SCHED, int LS, int SS, bool C4, int KG>
+__device__ __forceinline__ void kstep(Loader<BM, BN, MODE, BK, C4, false, KG>& ld, const CsConvArgs& a,
+                                      const float* cur, float* nxt,
+                                      f32x16 (&acc)[Tile<BM, BN, MODE, BK>::RM][Tile<BM, BN, MODE, BK>::RN],
+                                      int wm, int wn, int r, int hh, int kg, int k_load) {
   using T = Tile<BM, BN, MODE, BK>;
+  constexpr int NGK = T::NG / KG;  // chunks of this K-group
+  static_assert(NGK >= 1, "K-step too short for the K-groups");
+  const int g0 = kg * NGK;
   float af[2][T::RM][4], bf[2][T::RN][4];
-  read_chunk<BM, BN, MODE, BK>(cur, cur + T::A_ELEMS, 0, af[0], bf[0], wm, wn, r, hh);
+  read_chunk<BM, BN, MODE, BK>(cur, cur + T::A_ELEMS, g0, af[0], bf[0], wm, wn, r, hh);
 #pragma unroll
-  for (int g = 0; g < T::NG; ++g) {
-    if (g + 1 < T::NG) read_chunk<BM, BN, MODE, BK>(cur, cur + T::A_ELEMS, g + 1, af[(g + 1) & 1], bf[(g + 1) & 1],
-                                                    wm, wn, r, hh);
+  for (int g = 0; g < NGK; ++g) {
+    if (g + 1 < NGK) read_chunk<BM, BN, MODE, BK>(cur, cur + T::A_ELEMS, g0 + g + 1, af[(g + 1) & 1],
+                                                  bf[(g + 1) & 1], wm, wn, r, hh);
     if constexpr (SCHED == 0) __builtin_amdgcn_sched_barrier(0);
     mma_chunk<T::RM, T::RN>(af[g & 1], bf[g & 1], acc);
     if (g == 0) ld.template load<LS>(a, k_load);
-    if (g == (T::NG > 1 ? 1 : 0)) ld.template store<SS>(nxt, nxt + T::A_ELEMS);
+    if (g == (NGK > 1 ? 1 : 0)) ld.template store<SS>(nxt, nxt + T::A_ELEMS);
     if constexpr (SCHED == 0) __builtin_amdgcn_sched_barrier(0);
   }
 }
@@ -522,9 +532,10 @@ __device__ __forceinline__ void wait_vmcnt() {
 // landed, newer tiles may still be in flight); no register stage, no ds_write.
 // One output tile (`tile`, already XCD-remapped) x one K split of a conv GEMM; the body of
 // both the single-GEMM kernel and the dual (wgrad + dgrad) kernel.
-template <int BM, int BN, int MODE, int BK, int SCHED, bool C4, int GL>
+template <int BM, int BN, int MODE, int BK, int SCHED, bool C4, int GL, int KG = 1>
 __device__ __forceinline__ void gemm_body(const CsConvArgs& a, const int tile, const int split, const int nsplit,
                                           float* smem) {
+  static_assert(KG == 1 || GL == 0, "K-groups use register staging");
   using T = Tile<BM, BN, MODE, BK>;
   const int ntn = (a.N + BN - 1) / BN;
   const int mt = tile / ntn, nt = tile - mt * ntn;
@@ -534,7 +545,8 @@ __device__ __forceinline__ void gemm_body(const CsConvArgs& a, const int tile, c
   if (ks_end > a.total_ksteps) ks_end = a.total_ksteps;
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1, r = lane & 31, hh = lane >> 5;
+  const int kg = wid >> 2, wsp = wid & 3;  // K-group, spatial wave (2x2)
+  const int wm = wsp >> 1, wn = wsp & 1, r = lane & 31, hh = lane >> 5;
 
   f32x16 acc[T::RM][T::RN];
 #pragma unroll
@@ -574,7 +586,7 @@ __device__ __forceinline__ void gemm_body(const CsConvArgs& a, const int tile, c
     }
     __syncthreads();  // every wave's fragment reads are done before the epilogue reuses LDS
   } else {
-  Loader<BM, BN, MODE, BK, C4> ld;
+  Loader<BM, BN, MODE, BK, C4, false, KG> ld;
   ld.init(a, m0, n0);
   float* lds0 = smem;
   float* lds1 = smem + T::STAGE;
@@ -586,13 +598,41 @@ __device__ __forceinline__ void gemm_body(const CsConvArgs& a, const int tile, c
   __syncthreads();
   // even step t: tile t in lds0, tile t+1 in registers[1] -> lds1, tile t+2 -> registers[0]
   for (int t = 0; t < nks; t += 2) {
-    kstep<BM, BN, MODE, BK, SCHED, 0, 1, C4>(ld, a, lds0, lds1, acc, wm, wn, r, hh, (ks_begin + t + 2) * BK);
+    kstep<BM, BN, MODE, BK, SCHED, 0, 1, C4, KG>(ld, a, lds0, lds1, acc, wm, wn, r, hh, kg, (ks_begin + t + 2) * BK);
     __syncthreads();
     if (t + 1 >= nks) break;
-    kstep<BM, BN, MODE, BK, SCHED, 1, 0, C4>(ld, a, lds1, lds0, acc, wm, wn, r, hh, (ks_begin + t + 3) * BK);
+    kstep<BM, BN, MODE, BK, SCHED, 1, 0, C4, KG>(ld, a, lds1, lds0, acc, wm, wn, r, hh, kg, (ks_begin + t + 3) * BK);
     __syncthreads();
   }
   }
+
+  if constexpr (KG > 1) {
+    // K-group partials -> group 0, summed in group order through LDS (the main loop ended on
+    // a barrier; every group's last LDS reads are done)
+    float* red = smem;  // [KG-1][4 spatial waves][RM*RN*16][64 lanes]
+    constexpr int PER = T::RM * T::RN * 16 * 64;
+    if (kg > 0) {
+#pragma unroll
+      for (int i = 0; i < T::RM; ++i)
+#pragma unroll
+        for (int j = 0; j < T::RN; ++j)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) red[((kg - 1) * 4 + wsp) * PER + ((i * T::RN + j) * 16 + e) * 64 + lane] = acc[i][j][e];
+    }
+    __syncthreads();
+    if (kg == 0) {
+#pragma unroll
+      for (int q = 0; q < KG - 1; ++q)
+#pragma unroll
+        for (int i = 0; i < T::RM; ++i)
+#pragma unroll
+          for (int j = 0; j < T::RN; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] += red[(q * 4 + wsp) * PER + ((i * T::RN + j) * 16 + e) * 64 + lane];
+    }
+    __syncthreads();
+  }
+  const bool owner = kg == 0;  // only K-group 0 holds the full sums; the others' stores are dropped
 
   // ------------------------------------------------------------------ epilogue
   // C/D map (32x32 f32 MFMA): col = lane & 31, row = (reg&3) + 8*(reg>>2) + 4*(lane>>5).
@@ -609,10 +649,12 @@ __device__ __forceinline__ void gemm_body(const CsConvArgs& a, const int tile, c
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
           const int m = m0 + wm * T::WM + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * hh;
-          bstore1(ro, acc[i][j][e], (m < a.M && n < a.N) ? (m * a.N + n) * 4 : kOOB);
+          bstore1(ro, acc[i][j][e], (owner && m < a.M && n < a.N) ? (m * a.N + n) * 4 : kOOB);
         }
       }
-    if (slab && a.counters != nullptr) splitk_fixup<BM, BN, MODE>(a, tile, mt, nt, nsplit, smem);
+    if constexpr (KG == 1) {
+      if (slab && a.counters != nullptr) splitk_fixup<BM, BN, MODE>(a, tile, mt, nt, nsplit, smem);
+    }
     if (slab || MODE != CS_CONV_FWD) return;
   }
   if constexpr (MODE == CS_CONV_WGRAD) {  // conv0: scatter the padded (tap, ci) columns to OIHW
@@ -625,7 +667,7 @@ __device__ __forceinline__ void gemm_body(const CsConvArgs& a, const int tile, c
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
           const int m = m0 + wm * T::WM + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * hh;
-          if (m < a.M && n < a.N && ci < 3) a.out[(size_t)m * 27 + ci * 9 + tap] = acc[i][j][e];
+          if (owner && m < a.M && n < a.N && ci < 3) a.out[(size_t)m * 27 + ci * 9 + tap] = acc[i][j][e];
         }
       }
     return;
@@ -649,14 +691,14 @@ __device__ __forceinline__ void gemm_body(const CsConvArgs& a, const int tile, c
           const float v = acc[i][j][e] + bv;
           acc[i][j][e] = v;
           s += m < a.M ? v : 0.f;
-          bstore1(ro, v, (m < a.M && n < a.N) ? (m * a.N + n) * 4 : kOOB);
+          bstore1(ro, v, (owner && m < a.M && n < a.N) ? (m * a.N + n) * 4 : kOOB);
         }
       colsum[j] = s + __shfl_xor(s, 32, 64);
     }
     if (a.stats == nullptr) return;
 #pragma unroll
     for (int j = 0; j < T::RN; ++j)
-      if (hh == 0) red[wm * BN + wn * T::WN + j * 32 + r] = colsum[j];
+      if (owner && hh == 0) red[wm * BN + wn * T::WN + j * 32 + r] = colsum[j];
     __syncthreads();
     float mean[T::RN];
 #pragma unroll
@@ -677,10 +719,10 @@ __device__ __forceinline__ void gemm_body(const CsConvArgs& a, const int tile, c
           s += m < a.M ? d * d : 0.f;
         }
       s += __shfl_xor(s, 32, 64);
-      if (hh == 0) red[wm * BN + wn * T::WN + j * 32 + r] = s;
+      if (owner && hh == 0) red[wm * BN + wn * T::WN + j * 32 + r] = s;
     }
     __syncthreads();
-    if (wm == 0 && hh == 0) {
+    if (owner && wm == 0 && hh == 0) {
 #pragma unroll
       for (int j = 0; j < T::RN; ++j) {
         const int c = wn * T::WN + j * 32 + r, n = n0 + c;
@@ -693,11 +735,11 @@ __device__ __forceinline__ void gemm_body(const CsConvArgs& a, const int tile, c
   }
 }
 
-template <int BM, int BN, int MODE, int BK, int SCHED, bool C4, int GL>
-__global__ __launch_bounds__(256) void conv_gemm_kernel(CsConvArgs a) {
+template <int BM, int BN, int MODE, int BK, int SCHED, bool C4, int GL, int KG = 1>
+__global__ __launch_bounds__(256 * KG) void conv_gemm_kernel(CsConvArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int ntiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
-  gemm_body<BM, BN, MODE, BK, SCHED, C4, GL>(a, cs::xcd_remap(blockIdx.x, ntiles), blockIdx.z, gridDim.z, smem);
+  gemm_body<BM, BN, MODE, BK, SCHED, C4, GL, KG>(a, cs::xcd_remap(blockIdx.x, ntiles), blockIdx.z, gridDim.z, smem);
 }
 
 // Horizontal fusion of one block's two independent backward GEMMs: blocks [0, nb1) run the
@@ -848,9 +890,9 @@ int conv_sched() {
   return v;
 }
 
-template <int BM, int BN, int MODE, int BK, int SCHED, bool C4, int GL>
+template <int BM, int BN, int MODE, int BK, int SCHED, bool C4, int GL, int KG = 1>
 hipError_t launch_k(dim3 grid, size_t lds, hipStream_t stream, const CsConvArgs& a) {
-  hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, MODE, BK, SCHED, C4, GL>), grid, dim3(256), lds, stream, a);
+  hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, MODE, BK, SCHED, C4, GL, KG>), grid, dim3(256 * KG), lds, stream, a);
   return hipGetLastError();
 }
 
@@ -862,14 +904,29 @@ hipError_t launch_gemm(const CsConvArgs& a, int splits, int stage, hipStream_t s
   const size_t lds = 2 * T::STAGE * sizeof(float);
   const dim3 grid(ntiles, 1, splits);
   constexpr bool deep_fits = (BM + BN) * BK * 4 * 5 < 160 * 1024;
-  if (MODE == CS_CONV_FWD && a.w_oihw)  // padded conv0: Cin = 4 < BK
-    return launch_k<BM, BN, MODE, BK, 0, true, 0>(grid, lds, stream, a);
+  if constexpr (BK != 64) {
+    if (MODE == CS_CONV_FWD && a.w_oihw)  // padded conv0: Cin = 4 < BK
+      return launch_k<BM, BN, MODE, BK, 0, true, 0>(grid, lds, stream, a);
+  }
   if constexpr (BK == 32) {
     if (stage == CS_STAGE_LDS_DMA)
       return launch_k<BM, BN, MODE, BK, 0, false, 3>(grid, 3 * TG::STAGE * sizeof(float), stream, a);
     if constexpr (deep_fits) {
       if (stage == CS_STAGE_LDS_DMA_DEEP)
         return launch_k<BM, BN, MODE, BK, 0, false, 5>(grid, 5 * TG::STAGE * sizeof(float), stream, a);
+    }
+  }
+  // K-groups: the LDS tile ring must also hold the (KG-1) partial-accumulator images
+  if constexpr (BK >= 32 && BM * BK >= 2048 && BN * BK >= 2048) {
+    if (stage == CS_STAGE_KG2) {
+      const size_t red = (size_t)1 * 4 * (BM / 64) * (BN / 64) * 16 * 64 * sizeof(float);
+      return launch_k<BM, BN, MODE, BK, 0, false, 0, 2>(grid, std::max(lds, red), stream, a);
+    }
+  }
+  if constexpr (BK == 64 && BM * BK >= 4096 && BN * BK >= 4096) {
+    if (stage == CS_STAGE_KG4) {
+      const size_t red = (size_t)3 * 4 * (BM / 64) * (BN / 64) * 16 * 64 * sizeof(float);
+      return launch_k<BM, BN, MODE, BK, 0, false, 0, 4>(grid, std::max(lds, red), stream, a);
     }
   }
   if (stage != CS_STAGE_REGS) return hipErrorInvalidValue;
@@ -893,6 +950,28 @@ CS_TILE(64, 64)
 CS_TILE(64, 128)
 CS_TILE(128, 64)
 CS_TILE(128, 128)
+#define CS_BK64(BM_, BN_, MODE_) CS_K(BM_, BN_, MODE_, 64, 0, false, 0) CS_K(BM_, BN_, MODE_, 64, 1, false, 0)
+#define CS_TILE64(BM_, BN_) CS_BK64(BM_, BN_, CS_CONV_FWD) CS_BK64(BM_, BN_, CS_CONV_DGRAD) CS_BK64(BM_, BN_, CS_CONV_WGRAD)
+CS_TILE64(64, 64)
+CS_TILE64(128, 64)
+CS_TILE64(64, 128)
+#undef CS_TILE64
+#undef CS_BK64
+#define CS_KG(BM_, BN_, BK_, KG_)                                                                \
+  template __global__ void conv_gemm_kernel<BM_, BN_, CS_CONV_FWD, BK_, 0, false, 0, KG_>(CsConvArgs);   \
+  template __global__ void conv_gemm_kernel<BM_, BN_, CS_CONV_DGRAD, BK_, 0, false, 0, KG_>(CsConvArgs); \
+  template __global__ void conv_gemm_kernel<BM_, BN_, CS_CONV_WGRAD, BK_, 0, false, 0, KG_>(CsConvArgs);
+CS_KG(64, 64, 32, 2)
+CS_KG(128, 64, 32, 2)
+CS_KG(64, 128, 32, 2)
+CS_KG(128, 128, 32, 2)
+CS_KG(64, 64, 64, 2)
+CS_KG(128, 64, 64, 2)
+CS_KG(64, 128, 64, 2)
+CS_KG(64, 64, 64, 4)
+CS_KG(128, 64, 64, 4)
+CS_KG(64, 128, 64, 4)
+#undef CS_KG
 #define CS_DEEP(BM_, BN_)                                                                  \
   CS_K(BM_, BN_, CS_CONV_FWD, 32, 0, false, 5) CS_K(BM_, BN_, CS_CONV_DGRAD, 32, 0, false, 5) \
   CS_K(BM_, BN_, CS_CONV_WGRAD, 32, 0, false, 5)
@@ -939,6 +1018,18 @@ void cs_conv_fill_dims(CsConvArgs* a, int mode) {
   }
 }
 
+bool cs_conv_stage_ok(int stage, int bm, int bn, int bk, bool conv0_fwd) {
+  if (conv0_fwd && stage != CS_STAGE_REGS) return false;
+  switch (stage) {
+    case CS_STAGE_REGS: return bk != 64 || !(bm == 128 && bn == 128);
+    case CS_STAGE_LDS_DMA: return bk == 32;
+    case CS_STAGE_LDS_DMA_DEEP: return bk == 32 && (bm + bn) * bk * 4 * 5 < 160 * 1024;
+    case CS_STAGE_KG2: return bk >= 32 && !(bk == 64 && bm == 128 && bn == 128);
+    case CS_STAGE_KG4: return bk == 64 && !(bm == 128 && bn == 128);
+    default: return false;
+  }
+}
+
 bool cs_conv_fixup_ok(int splits, int bm, int bn) {
   return splits > 1 && (int64_t)splits * bm * bn * 4 <= CS_FIXUP_MAX_BYTES;
 }
@@ -958,7 +1049,8 @@ int cs_conv_effective_splits(int K, int bk, int splits) {
 namespace {
 // dims, K-step split and size checks shared by the single and dual launchers; -> effective splits or -1
 int prep_gemm(CsConvArgs& a, int mode, int bk, int splits) {
-  if (bk != 16 && bk != 32) return -1;
+  if (bk != 16 && bk != 32 && bk != 64) return -1;
+  if (bk == 64 && mode == CS_CONV_FWD && a.w_oihw) return -1;  // conv0's K = 36
   cs_conv_fill_dims(&a, mode);
   // 32-bit buffer offsets: every operand / output / workspace must stay below 2 GiB
   const int64_t pix = (int64_t)a.B * a.H * a.W;
@@ -1007,7 +1099,10 @@ hipError_t cs_conv_gemm_dual(CsConvArgs wg, int wbk, int wsplits, CsConvArgs dg,
 }
 
 hipError_t cs_conv_gemm(CsConvArgs a, int mode, int bm, int bn, int bk, int splits, hipStream_t stream, int stage) {
-  if (stage != CS_STAGE_REGS && (bk != 32 || (a.w_oihw && mode == CS_CONV_FWD))) return hipErrorInvalidValue;
+  if ((stage == CS_STAGE_LDS_DMA || stage == CS_STAGE_LDS_DMA_DEEP) && (bk != 32 || (a.w_oihw && mode == CS_CONV_FWD)))
+    return hipErrorInvalidValue;
+  if ((stage == CS_STAGE_KG2 || stage == CS_STAGE_KG4) && !cs_conv_stage_ok(stage, bm, bn, bk, a.w_oihw && mode == CS_CONV_FWD))
+    return hipErrorInvalidValue;
   splits = prep_gemm(a, mode, bk, splits);
   if (splits < 0) return hipErrorInvalidValue;
   if (!cs_conv_fixup_ok(splits, bm, bn)) a.counters = nullptr;
@@ -1028,6 +1123,9 @@ hipError_t cs_conv_gemm(CsConvArgs a, int mode, int bm, int bn, int bk, int spli
   CS_DISPATCH(128, 64, 32)
   CS_DISPATCH(64, 128, 32)
   CS_DISPATCH(128, 128, 32)
+  CS_DISPATCH(64, 64, 64)
+  CS_DISPATCH(128, 64, 64)
+  CS_DISPATCH(64, 128, 64)
 #undef CS_DISPATCH
   return hipErrorInvalidValue;
 }

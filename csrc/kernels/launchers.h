@@ -55,7 +55,10 @@ void cs_conv_fill_dims(CsConvArgs* a, int mode);
 // stage: CS_STAGE_REGS (global -> registers -> ds_write, padded LDS) or CS_STAGE_LDS_DMA(_DEEP)
 // (buffer_load ... lds into a 3- (5-) deep ring of swizzled images; bk = 32, not conv0's fwd;
 // the deep ring only where 5 images fit the 160 KiB LDS)
-enum { CS_STAGE_REGS = 0, CS_STAGE_LDS_DMA = 1, CS_STAGE_LDS_DMA_DEEP = 2 };
+// CS_STAGE_KG2 / KG4: register staging with 2 / 4 K-groups of 4 waves per block (bk >= 32 / 64)
+enum { CS_STAGE_REGS = 0, CS_STAGE_LDS_DMA = 1, CS_STAGE_LDS_DMA_DEEP = 2, CS_STAGE_KG2 = 3, CS_STAGE_KG4 = 4 };
+// whether a (stage, tile, bk) combination has a kernel
+bool cs_conv_stage_ok(int stage, int bm, int bn, int bk, bool conv0_fwd);
 hipError_t cs_conv_gemm(CsConvArgs a, int mode, int bm, int bn, int bk, int splits, hipStream_t stream,
                         int stage = CS_STAGE_REGS);
 // one launch for a block's weight gradient (wg) and data gradient (dg), both 64x64 tiles with

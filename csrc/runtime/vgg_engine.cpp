@@ -392,10 +392,10 @@ void VggEngine::set_tile(int64_t block, int64_t mode, int64_t bm, int64_t bn, in
   TORCH_CHECK(block >= 0 && block < (int64_t)blocks_.size() && mode >= 0 && mode <= 2, "set_tile: index");
   TORCH_CHECK((bm == 64 || bm == 128) && (bn == 64 || bn == 128) && splits >= 1 && splits <= 1024, "set_tile: tile");
   const Dims d = dims(blocks_[block], (int)mode, Bmax_);
-  TORCH_CHECK(bk == 16 || bk == 32, "set_tile: bk must be 16 or 32");
-  TORCH_CHECK(stage == CS_STAGE_REGS || ((stage == CS_STAGE_LDS_DMA || stage == CS_STAGE_LDS_DMA_DEEP) && bk == 32 &&
-                                         !(block == 0 && mode == CS_CONV_FWD && blocks_[0].cin == 4)),
-              "set_tile: LDS-DMA staging needs bk 32 (and not conv0's padded forward)");
+  const bool conv0_fwd = block == 0 && mode == CS_CONV_FWD && blocks_[0].cin == 4;
+  TORCH_CHECK((bk == 16 || bk == 32 || bk == 64) && cs_conv_stage_ok((int)stage, (int)bm, (int)bn, (int)bk, conv0_fwd) &&
+                  !(conv0_fwd && bk == 64),
+              "set_tile: no kernel for stage ", stage, " with a ", bm, "x", bn, " tile and bk ", bk);
   const int sp = eff_splits(d.K, (int)splits, (int)bk);
   TORCH_CHECK(sp == 1 || (int64_t)sp * d.M * d.N <= ws_elems_, "set_tile: split-K workspace too small");
   ConvTile& t = blocks_[block].tile[mode];
@@ -443,13 +443,14 @@ std::vector<double> VggEngine::autotune(int64_t B, int64_t iters) {
       best64_t[mode] = 1e30f;
       std::vector<std::vector<int>> seen;
       const bool conv0_fwd = l == 0 && mode == CS_CONV_FWD && blocks_[0].cin == 4;
-      for (int stage : {(int)CS_STAGE_REGS, (int)CS_STAGE_LDS_DMA, (int)CS_STAGE_LDS_DMA_DEEP})
-      for (int bk : {16, 32}) {
-        if (stage != CS_STAGE_REGS && (bk != 32 || conv0_fwd)) continue;
+      for (int stage : {(int)CS_STAGE_REGS, (int)CS_STAGE_LDS_DMA, (int)CS_STAGE_LDS_DMA_DEEP, (int)CS_STAGE_KG2,
+                        (int)CS_STAGE_KG4})
+      for (int bk : {16, 32, 64}) {
+        if (bk == 64 && conv0_fwd) continue;
         const int64_t ks = cdiv(d.K, bk);
         for (int bm : {64, 128}) {
           for (int bn : {64, 128}) {
-            if (stage == CS_STAGE_LDS_DMA_DEEP && (bm + bn) * bk * 4 * 5 >= 160 * 1024) continue;
+            if (!cs_conv_stage_ok(stage, bm, bn, bk, conv0_fwd)) continue;
             for (int sp : split_opts) {
               if (sp > 1 && ks / sp < 2) continue;
               const int e = eff_splits(d.K, sp, bk);

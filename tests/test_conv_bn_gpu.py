@@ -27,17 +27,17 @@ def _close(a, b, rel=2e-5):
 # (B, H, cin, cout) — VGG-11 layer shapes at a small batch, plus conv0 (padded cin 4)
 SHAPES = [(2, 32, 3, 64), (2, 16, 64, 128), (2, 8, 128, 256), (3, 4, 256, 512), (4, 2, 512, 512)]
 TILES = [(64, 64, 1, 16), (128, 64, 1, 16), (64, 128, 3, 16), (128, 128, 2, 16), (64, 64, 1, 32), (128, 128, 3, 32),
-         (64, 128, 4, 32), (128, 64, 2, 32)]
+         (64, 128, 4, 32), (128, 64, 2, 32), (64, 64, 2, 64), (128, 64, 1, 64)]
 # (in-launch split-K combine, operand staging): 0 = registers + ds_write, 1/2 = LDS-DMA ring of
 # depth 3/5 (bk 32 only)
-VARIANTS = [(False, 0), (True, 0), (False, 1), (True, 1), (False, 2)]
+# 3/4 = register staging with 2/4 K-groups of waves per block
+VARIANTS = [(False, 0), (True, 0), (False, 1), (True, 1), (False, 2), (False, 3), (False, 4)]
 
 
 def _skip_stage(stage, bk, bm, bn, conv0_fwd=False):
-    if stage > 0 and (bk != 32 or conv0_fwd):
-        pytest.skip("LDS-DMA staging is for bk 32 (not conv0's forward)")
-    if stage == 2 and (bm + bn) * bk * 4 * 5 >= 160 * 1024:
-        pytest.skip("a 5-deep ring of this tile does not fit the 160 KiB LDS")
+    from cs744_pytorch_distributed_tutorial_amd.ops import native
+    if not native.C().conv_stage_ok(stage, bm, bn, bk, conv0_fwd):
+        pytest.skip(f"no kernel for stage {stage} / {bm}x{bn} / bk {bk}")
 
 
 def _inputs(dev, B, H, cin, cout, seed=0):
@@ -97,7 +97,7 @@ def test_conv_dgrad(dev, shape, tile, fixup, stage):
 
 @pytest.mark.parametrize("shape", SHAPES)
 @pytest.mark.parametrize("tile", [(64, 64, 1, 16), (64, 64, 8, 16), (128, 128, 4, 16), (128, 64, 2, 16),
-                                  (64, 64, 64, 16), (64, 128, 4, 32), (128, 128, 1, 32)])
+                                  (64, 64, 64, 16), (64, 128, 4, 32), (128, 128, 1, 32), (64, 64, 4, 64)])
 @pytest.mark.parametrize("fixup,stage", VARIANTS)
 def test_conv_wgrad(dev, shape, tile, fixup, stage):
     from cs744_pytorch_distributed_tutorial_amd.ops import functional as Fn
