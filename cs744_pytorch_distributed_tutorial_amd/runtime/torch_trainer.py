@@ -8,8 +8,10 @@ framework's own data-parallel runtime around them.
   ``RcclComm`` (``comm="rccl"``) or ProcessGroupNCCL (``comm="torch"``);
   or any explicit strategy of ``parallel.sync`` (part2a / part2a_extra / part2b);
 * optimizer = ``ops.optim.FusedSGD`` (one multi-tensor HIP launch per step);
-* CNNs run ``channels_last`` (NHWC, MIOpen/hipBLASLt's fast layout), optionally
-  under bf16 autocast (``dtype="bf16"``; master weights and the optimizer stay fp32);
+* CNNs run NCHW by default: measured on MI355X (torch 2.10+rocm7.0, MIOpen FAST find) the
+  channels_last (NHWC) ResNet-50 step is 10-18x SLOWER (its composable_kernel weight-gradient
+  kernels take up to 225 ms each; 210 vs 1923 img/s bf16, 115 vs 2131 img/s fp32), so NHWC
+  is opt-in (``CS744_CHANNELS_LAST=1``); optionally under bf16 autocast (``dtype="bf16"``; master weights and the optimizer stay fp32);
 * data = device-resident synthetic batches of the named shape (no host traffic).
 """
 from __future__ import annotations
@@ -43,7 +45,8 @@ class SyntheticBatches:
     """
 
     def __init__(self, kind: str, batch: int, device, shape=(3, 224, 224), classes: int = 1000, pool: int = 512,
-                 seq: int = 0, vocab: int = 0, seed: int = 0):
+                 seq: int = 0, vocab: int = 0, seed: int = 0, channels_last: bool = True):
+        self.fmt = torch.channels_last if channels_last else torch.contiguous_format
         g = torch.Generator(device="cpu").manual_seed(seed)
         self.kind, self.batch, self.device = kind, batch, device
         self.pool = max(pool, batch)
@@ -61,7 +64,7 @@ class SyntheticBatches:
         idx = torch.randint(0, self.pool, (self.batch,), device=self.device, generator=self.gen)
         if self.kind == "image":
             x = self.data.index_select(0, idx).permute(0, 3, 1, 2).float()
-            x = ((x - self.mean) / self.std).contiguous(memory_format=torch.channels_last)
+            x = ((x - self.mean) / self.std).contiguous(memory_format=self.fmt)
             return x, self.labels.index_select(0, idx)
         t = self.tokens.index_select(0, idx)
         return t[:, :-1].contiguous(), t[:, 1:].contiguous()
@@ -78,7 +81,9 @@ class TorchTrainer:
         self.model_name = model
         self.module = build_model(model).to(device)
         self.is_lm = hasattr(self.module, "vocab_size")
-        if not self.is_lm:
+        import os
+        self.channels_last = not self.is_lm and os.environ.get("CS744_CHANNELS_LAST", "0") == "1"
+        if self.channels_last:
             self.module = self.module.to(memory_format=torch.channels_last)
         self.dtype = dtype
         if world > 1 and sync == "ddp":
@@ -98,7 +103,8 @@ class TorchTrainer:
         else:
             shape = (3, 32, 32) if model.lower().startswith("vgg") else (3, 224, 224)
             classes = 10 if model.lower().startswith("vgg") else 1000
-            self.data = SyntheticBatches("image", batch_size, device, shape=shape, classes=classes, seed=seed)
+            self.data = SyntheticBatches("image", batch_size, device, shape=shape, classes=classes, seed=seed,
+                                         channels_last=self.channels_last)
         self.loss: Optional[torch.Tensor] = None
 
     def step(self) -> None:
