@@ -147,15 +147,25 @@ class FlatLayout:
         return {n: self.view(grads, n).detach().cpu().contiguous() for n in self.param_names}
 
     # ---------------------------------------------------------------- buckets
-    def plan_buckets(self, cap_mb: float) -> Tuple[List[int], List[Tuple[int, int]]]:
-        """Block-aligned buckets from the top: (lowest block per bucket, (offset, numel) per bucket)."""
+    def plan_buckets(self, cap_mb: float, tail_mb: float = 0.5) -> Tuple[List[int], List[Tuple[int, int]]]:
+        """Block-aligned buckets from the top: (lowest block per bucket, (offset, numel) per bucket).
+
+        A bucket closes at a block boundary once it holds >= ``cap_mb``, and also as soon as
+        everything below it is <= ``tail_mb``: the last bucket's all-reduce cannot overlap any
+        backward work, so it is kept to the few cheap bottom blocks (VGG-11 at 4 MiB:
+        fc1+b7 | b6 | b5 | b4 | b3+b2 | b1+b0 (0.3 MiB) instead of a 3.9 MiB b3..b0 tail)."""
         cap = cap_mb * 1024 * 1024
+        tail = tail_mb * 1024 * 1024
         lows: List[int] = []
         ranges: List[Tuple[int, int]] = []
         start, acc = 0, self.block_start[self.L - 1] * 4  # fc1 rides in the first bucket
+        in_tail = False
         for l in range(self.L - 1, -1, -1):
             acc += (self.block_end[l] - self.block_start[l]) * 4
-            if acc >= cap or l == 0:
+            below = sum(self.block_end[j] - self.block_start[j] for j in range(l)) * 4
+            to_tail = not in_tail and cap_mb < 1e8 and 0 < below <= tail
+            in_tail = in_tail or to_tail
+            if l == 0 or to_tail or (acc >= cap and not in_tail):
                 lows.append(l)
                 ranges.append((start, self.block_end[l] - start))
                 start, acc = self.block_end[l], 0
@@ -333,7 +343,15 @@ class NativeTrainer:
         """Eager (or segment-graph) orchestration with collectives between segments."""
         nseg = len(self.bucket_lows)
         if self.sync_mode == "ddp":
-            self._pre_forward_sync()
+            # DDP broadcast_buffers: rank 0's BN running stats reach every rank before each
+            # training forward. With the native comm the broadcast for the NEXT step is issued
+            # here, right after this step's forward (segment 0) has produced the buffers and
+            # behind the first bucket's all-reduce, so it rides the comm stream while the
+            # backward runs instead of stalling the next forward; nothing touches the buffers
+            # between this forward and the next (step 0 is covered by construction's broadcast).
+            early = self.native_comm is not None and self.broadcast_buffers
+            if not early:
+                self._pre_forward_sync()
             handles = []
             for k in range(nseg):
                 if graphs is not None:
@@ -341,6 +359,9 @@ class NativeTrainer:
                 else:
                     self._run_segment(k, B)
                 handles.append(self.comm.all_reduce_avg(self._bucket_view(k), async_op=True))
+                if early and k == 0:
+                    self.native_comm.broadcast(self.bufs, 0)
+                    self.native_comm.broadcast(self.nbt, 0)
             for h in handles:
                 h.wait()
         else:

@@ -20,8 +20,29 @@ constexpr int64_t kWsElems = 16ll << 20;  // 64 MiB split-K workspace
 
 hipStream_t cur_stream() { return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
 
+// CS_DEBUG_SYNC=1: race/fault isolation mode — every launch is followed by a
+// stream sync + error check (skipped while a hipGraph is being captured), so an async fault
+// is reported at the kernel that caused it instead of at a later sync.
+bool debug_sync() {
+  static const bool on = [] {
+    const char* e = getenv("CS_DEBUG_SYNC");
+    return e != nullptr && atoi(e) != 0;
+  }();
+  return on;
+}
+
 void ok(hipError_t e, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string("VggEngine: ") + what + ": " + hipGetErrorString(e));
+  if (debug_sync()) {
+    hipStream_t s = cur_stream();
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &st) == hipSuccess && st == hipStreamCaptureStatusNone) {
+      hipError_t e2 = hipStreamSynchronize(s);
+      if (e2 == hipSuccess) e2 = hipGetLastError();
+      if (e2 != hipSuccess)
+        throw std::runtime_error(std::string("VggEngine [debug sync] after ") + what + ": " + hipGetErrorString(e2));
+    }
+  }
 }
 
 int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }

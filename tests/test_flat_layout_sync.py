@@ -59,8 +59,10 @@ def test_bucket_plan_is_contiguous_and_block_aligned(cap):
     assert pos == lay.total
     if cap >= 1e8:
         assert len(ranges) == 1
-    if cap == 9.0:  # xGMI-sized: fc1+block7 | block6 | block5 | blocks 4..0
-        assert lows == [7, 6, 5, 0]
+    if cap == 9.0:  # xGMI-sized: fc1+block7 | block6 | block5 | blocks 4..2 | small tail blocks 1..0
+        assert lows == [7, 6, 5, 2, 0]
+    if cap == 4.0:
+        assert lows == [7, 6, 5, 4, 2, 0]  # b3+b2 | b1+b0 tail
 
 
 def test_desc_chains():

@@ -192,3 +192,20 @@ def test_dual_backward_launch_is_bitwise_equal(dev):
         b.step()
     torch.cuda.synchronize()
     assert torch.equal(a.params, b.params) and torch.equal(a.mom, b.mom)
+
+
+def test_debug_sync_mode_runs(dev):
+    # CS_DEBUG_SYNC=1 (read once per process): every engine launch is followed by a stream sync +
+    # error check outside graph capture; run it in a child process
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import torch; from cs744_pytorch_distributed_tutorial_amd.runtime.engine import NativeTrainer;"
+            "tr = NativeTrainer(batch_size=8, device=torch.device('cuda', 0), train_size=64, test_size=8,"
+            " autotune=False, graph='full');"
+            "[tr.step() for _ in range(4)]; torch.cuda.synchronize(); print('loss', tr.last_loss())")
+    env = dict(os.environ, CS_DEBUG_SYNC="1", PYTHONPATH=root)
+    p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=110)
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert "loss" in p.stdout
