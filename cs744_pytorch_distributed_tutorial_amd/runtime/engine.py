@@ -293,9 +293,12 @@ class NativeTrainer:
         return n // self.B if self.drop_last else math.ceil(n / self.B)
 
     def _start_epoch(self, epoch: int) -> None:
+        """New sampler order on the device; the engine's batch kernel walks it with a device-side
+        cursor that each step's SGD launch advances, so a step needs no host-side index copy."""
         self.epoch = epoch
         self.sampler.set_epoch(epoch)
-        self._epoch_idx = torch.tensor(self.sampler.indices(), dtype=torch.int64).to(self.device)
+        self._epoch_idx = torch.tensor(self.sampler.indices(), dtype=torch.int64)
+        self.engine.set_perm(self._epoch_idx)
         self.aug_train.copy_(dm.augment_params(len(self.train_set), self.data_seed, epoch, True).to(self.device))
         self.iter_in_epoch = 0
 
@@ -303,10 +306,9 @@ class NativeTrainer:
         if self.iter_in_epoch >= self.steps_per_epoch():
             self._start_epoch(self.epoch + 1)
         s = self.iter_in_epoch * self.B
-        idx = self._epoch_idx[s:s + self.B]
-        self.idx_buf[:idx.numel()].copy_(idx)
+        n = min(self.B, len(self._epoch_idx) - s)
         self.iter_in_epoch += 1
-        return idx.numel()
+        return n
 
     # ---------------------------------------------------------------- step pieces
     def _segments(self) -> List[Tuple[int, int]]:

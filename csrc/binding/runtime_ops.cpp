@@ -136,6 +136,8 @@ void register_runtime(pybind11::module& m) {
                     torch::Tensor, torch::Tensor, torch::Tensor, torch::Tensor, torch::Tensor>())
       .def("set_data", &cs::VggEngine::set_data)
       .def("idx", &cs::VggEngine::idx)
+      .def("set_perm", &cs::VggEngine::set_perm)
+      .def("cursor", &cs::VggEngine::cursor)
       .def("loss", &cs::VggEngine::loss)
       .def("correct", &cs::VggEngine::correct)
       .def("logits", &cs::VggEngine::logits)

@@ -15,10 +15,15 @@ struct CsTensorEntry {
 hipError_t cs_augment(const uint8_t* data, const int64_t* idx, const int32_t* params, float* out, int B, int nhwc,
                       int cstride, const float* mean, const float* std_, hipStream_t stream);
 hipError_t cs_gather_labels(const int64_t* labels, const int64_t* idx, int64_t* out, int B, hipStream_t stream);
+// engine batch: sample = perm[*cursor * stride + b] (or idx_in[b] when perm is null) -> NHWC x4 input, idx_out, labels
+hipError_t cs_make_batch(const uint8_t* data, const int64_t* labels, const int64_t* perm, const int64_t* cursor,
+                         int stride, const int64_t* idx_in, const int32_t* params, float* out, int64_t* idx_out,
+                         int64_t* ylab, int B, const float* mean, const float* std_, hipStream_t stream);
 
 // optimizer
+// counter (optional): incremented once by the launch (the engine's device-side step cursor)
 hipError_t cs_sgd_flat(float* p, const float* g, float* m, int64_t n, float lr, float mom, float wd, float damp,
-                       float scale, int first, hipStream_t stream);
+                       float scale, int first, hipStream_t stream, int64_t* counter = nullptr);
 hipError_t cs_sgd_multi(const CsTensorEntry* tab_dev, int ntens, const int64_t* chunk_start_dev, int nchunks,
                         float lr, float mom, float wd, float damp, float scale, int first, hipStream_t stream);
 

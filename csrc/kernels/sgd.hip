@@ -27,7 +27,9 @@ __device__ __forceinline__ void sgd1(float& p, float g, float& m, const SgdArgs&
 }
 
 __global__ __launch_bounds__(256) void sgd_flat_kernel(float* __restrict__ p, const float* __restrict__ g,
-                                                       float* __restrict__ m, int64_t n, SgdArgs a) {
+                                                       float* __restrict__ m, int64_t n, SgdArgs a,
+                                                       int64_t* __restrict__ counter) {
+  if (counter != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *counter += 1;
   const int64_t n4 = n >> 2;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   float4* p4 = reinterpret_cast<float4*>(p);
@@ -77,13 +79,13 @@ __global__ __launch_bounds__(256) void sgd_multi_kernel(const CsTensorEntry* __r
 }  // namespace
 
 hipError_t cs_sgd_flat(float* p, const float* g, float* m, int64_t n, float lr, float mom, float wd, float damp,
-                       float scale, int first, hipStream_t stream) {
+                       float scale, int first, hipStream_t stream, int64_t* counter) {
   if (n <= 0) return hipSuccess;
   SgdArgs a{lr, mom, wd, damp, scale, first};
   const int64_t work = (n + 3) / 4;
   int blocks = (int)((work + 255) / 256);
   if (blocks > 2048) blocks = 2048;
-  hipLaunchKernelGGL(sgd_flat_kernel, dim3(blocks), dim3(256), 0, stream, p, g, m, n, a);
+  hipLaunchKernelGGL(sgd_flat_kernel, dim3(blocks), dim3(256), 0, stream, p, g, m, n, a, counter);
   return hipGetLastError();
 }
 

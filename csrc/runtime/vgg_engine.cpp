@@ -241,6 +241,21 @@ CsConvArgs VggEngine::conv_args(int l, int mode, int B, bool with_stats, float* 
   return a;
 }
 
+void VggEngine::set_perm(torch::Tensor perm) {
+  TORCH_CHECK(data_[0].defined(), "set_perm: set_data(0, ...) first");
+  TORCH_CHECK(perm.scalar_type() == at::kLong && perm.dim() == 1 && perm.numel() > 0, "set_perm: int64 [n] indices");
+  const int64_t n = perm.numel();
+  TORCH_CHECK(n <= data_[0].size(0) + Bmax_, "set_perm: permutation longer than the dataset");
+  if (!perm_.defined()) {
+    // fixed capacity (graph-captured kernels keep the pointer): dataset size + one batch of slack
+    perm_ = torch::zeros({data_[0].size(0) + Bmax_}, params_.options().dtype(at::kLong));
+    cursor_ = torch::zeros({1}, params_.options().dtype(at::kLong));
+  }
+  perm_.narrow(0, 0, n).copy_(perm.to(perm_.device()), /*non_blocking=*/false);
+  cursor_.zero_();
+  perm_len_ = n;
+}
+
 void VggEngine::conv(int l, int mode, int B, const ConvTile& t, hipStream_t s, bool with_stats, float* ws,
                      float* dz) {
   VggBlock& b = blocks_[l];
@@ -272,11 +287,25 @@ void VggEngine::forward_train(int64_t B) {
   TORCH_CHECK(data_[0].defined(), "forward_train: set_data(0, ...) first");
   hipStream_t s = cur_stream();
   const int L = (int)blocks_.size();
-  ok(cs_gather_labels(labels_[0].data_ptr<int64_t>(), idx_.data_ptr<int64_t>(), ylab_.data_ptr<int64_t>(), (int)B, s),
-     "gather_labels");
-  ok(cs_augment(data_[0].data_ptr<uint8_t>(), idx_.data_ptr<int64_t>(), aug_[0].data_ptr<int32_t>(),
-                blocks_[0].x.data_ptr<float>(), (int)B, 1, blocks_[0].cin, kMean, kStd, s),
-     "augment");
+  // one launch: sampler index (device cursor into the epoch permutation, or idx_ when no
+  // permutation is set), label gather, crop/flip/normalize into block 0's NHWC input
+  const bool use_perm = perm_len_ > 0;
+  ok(cs_make_batch(data_[0].data_ptr<uint8_t>(), labels_[0].data_ptr<int64_t>(),
+                   use_perm ? perm_.data_ptr<int64_t>() : nullptr, use_perm ? cursor_.data_ptr<int64_t>() : nullptr,
+                   (int)Bmax_, use_perm ? nullptr : idx_.data_ptr<int64_t>(), aug_[0].data_ptr<int32_t>(),
+                   blocks_[0].x.data_ptr<float>(), idx_.data_ptr<int64_t>(), ylab_.data_ptr<int64_t>(), (int)B, kMean,
+                   kStd, s),
+     "make_batch");
+  // CS_PROBE_EXTRA_LAUNCHES=k (measurement only): k redundant tiny launches per step, to price
+  // one kernel boundary inside the replayed graph (measured: ~1.5 us each on MI355X)
+  static const int extra = [] {
+    const char* e = getenv("CS_PROBE_EXTRA_LAUNCHES");
+    return e ? atoi(e) : 0;
+  }();
+  for (int i = 0; i < extra; ++i)
+    ok(cs_gather_labels(labels_[0].data_ptr<int64_t>(), idx_.data_ptr<int64_t>(), ylab_.data_ptr<int64_t>(), (int)B,
+                        s),
+       "probe");
   for (int l = 0; l < L; ++l) {
     VggBlock& b = blocks_[l];
     const ConvTile& t = b.tile[CS_CONV_FWD];
@@ -345,8 +374,9 @@ void VggEngine::sgd(double lr, double momentum, double wd, double dampening, int
   TORCH_CHECK(off >= 0 && n >= 0 && off + n <= params_.numel(), "sgd: range");
   if (n == 0) return;
   // momentum buffers start at zero, so buf = 0*mom + (1-damp)*d == torch's first-step clone for damp = 0
+  // the step's one optimizer launch also advances the device-side batch cursor
   ok(cs_sgd_flat(P(off), G(off), mom_.data_ptr<float>() + off, n, (float)lr, (float)momentum, (float)wd,
-                 (float)dampening, 1.0f, 0, cur_stream()),
+                 (float)dampening, 1.0f, 0, cur_stream(), perm_len_ > 0 ? cursor_.data_ptr<int64_t>() : nullptr),
      "sgd_flat");
 }
 

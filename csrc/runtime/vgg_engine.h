@@ -56,6 +56,10 @@ class VggEngine {
   // slot 0 = train, 1 = eval. data uint8 [N,32,32,3], labels int64 [N], aug int32 [N,3] (dy, dx, flip)
   void set_data(int64_t slot, torch::Tensor data, torch::Tensor labels, torch::Tensor aug);
   torch::Tensor idx() const { return idx_; }
+  // epoch sampling order for the training forward: batch k = perm[k*Bmax ...]; resets the device
+  // cursor, which the step's SGD launch advances (no per-step host copy)
+  void set_perm(torch::Tensor perm);
+  torch::Tensor cursor() const { return cursor_; }
   torch::Tensor loss() const { return loss_; }
   torch::Tensor correct() const { return correct_; }
   torch::Tensor logits() const { return logits_; }
@@ -117,6 +121,8 @@ class VggEngine {
   torch::Tensor params_, grads_, mom_, bufs_, nbt_;
   torch::Tensor data_[2], labels_[2], aug_[2];
   torch::Tensor idx_, ylab_, loss_, correct_, logits_, pred_;
+  torch::Tensor perm_, cursor_;
+  int64_t perm_len_ = 0;
   torch::Tensor gbuf_[2], dz_[2], ws_, ws_side_, bn_part_, bn_coef_, bn_eval_, head_ws_;
   int64_t ws_elems_ = 0;
   torch::Tensor counters_;  // split-K tile tickets, [3 * L][tiles_max_] int32

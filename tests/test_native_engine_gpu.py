@@ -209,3 +209,23 @@ def test_debug_sync_mode_runs(dev):
     p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=110)
     assert p.returncode == 0, p.stderr[-2000:]
     assert "loss" in p.stdout
+
+
+def test_device_cursor_walks_sampler_order_across_epochs(dev):
+    # the batch kernel reads perm[cursor * B + i]; SGD advances the cursor; a new epoch uploads
+    # the next sampler order and resets it — no per-step host copy, same order as the sampler
+    tr = _trainer(dev, batch_size=16, train_size=64, graph="full")
+    seen = []
+    for step in range(7):  # 4 steps per epoch: crosses into epoch 1 and replays the graph
+        tr.step()
+        torch.cuda.synchronize()
+        seen.append(tr.engine.idx()[:16].cpu().tolist())
+    from cs744_pytorch_distributed_tutorial_amd.utils import data as dm
+    s = dm.DistributedSampler(64, 1, 0, shuffle=True, seed=0)
+    want = []
+    for ep in range(2):
+        s.set_epoch(ep)
+        order = s.indices()
+        want += [order[k * 16:(k + 1) * 16] for k in range(4)]
+    assert seen == want[:7]
+    assert int(tr.engine.cursor().item()) == 3  # 3 steps into epoch 1
