@@ -109,12 +109,22 @@ class BNState:
 
 def bn_relu_pool_fwd(y: torch.Tensor, stats: torch.Tensor, rows: int, B: int, H: int, W: int, gamma, beta,
                      running_mean=None, running_var=None, nbt=None, pool: bool = False,
-                     momentum: float = BN_MOMENTUM, eps: float = BN_EPS):
-    """Training-mode BN (batch stats from the conv epilogue partials) + ReLU (+2x2 max-pool)."""
+                     momentum: float = BN_MOMENTUM, eps: float = BN_EPS, fused: bool = False):
+    """Training-mode BN (batch stats from the conv epilogue partials) + ReLU (+2x2 max-pool).
+    ``fused``: the single-launch kernel (one block per 16 channels; the engine's small layers)."""
     C = gamma.numel()
     M = B * H * W
-    st = BNState(C, y.device)
     T = stats.shape[0]
+    if fused:
+        bnv = torch.empty(4, C, device=y.device, dtype=torch.float32)
+        Ho, Wo = (H // 2, W // 2) if pool else (H, W)
+        out = torch.empty(B, Ho, Wo, C, device=y.device, dtype=torch.float32)
+        native.C().bn_fused_fwd(stats, T, rows, M, gamma, beta, running_mean, running_var, nbt, momentum, eps, bnv,
+                                y, out, B, H, W, pool)
+        st = BNState(C, y.device)
+        st.scale, st.shift, st.mean, st.invstd = bnv[0], bnv[1], bnv[2], bnv[3]
+        return out, st
+    st = BNState(C, y.device)
     native.C().bn_finalize(stats, T, rows, M, gamma, beta, running_mean, running_var, nbt, momentum, eps,
                            st.scale, st.shift, st.mean, st.invstd)
     Ho, Wo = (H // 2, W // 2) if pool else (H, W)
@@ -136,9 +146,16 @@ def bn_relu_pool_eval(y: torch.Tensor, B: int, H: int, W: int, gamma, beta, runn
 
 
 def bn_relu_pool_bwd(y: torch.Tensor, G: torch.Tensor, st: BNState, gamma: torch.Tensor, B: int, H: int, W: int,
-                     pool: bool = False):
+                     pool: bool = False, fused: bool = False):
     """-> (dz [B*H*W, C], dgamma, dbeta, dbias) for z = maxpool?(relu(bn(y)))."""
     C = gamma.numel()
+    if fused:
+        bnv = torch.stack([st.scale, st.shift, st.mean, st.invstd]).contiguous()
+        coef = torch.empty(C * 3, device=y.device)
+        dgamma, dbeta, dbias = (torch.empty(C, device=y.device) for _ in range(3))
+        dz = torch.empty(B * H * W, C, device=y.device)
+        native.C().bn_fused_bwd(y, G, B, H, W, C, pool, bnv, gamma, coef, dgamma, dbeta, dbias, dz)
+        return dz, dgamma, dbeta, dbias
     P = native.C().bn_bwd_blocks(B, H, W, C, pool)
     part = torch.empty(P * C * 3, device=y.device)
     coef = torch.empty(C * 3, device=y.device)

@@ -141,9 +141,45 @@ void bn_bwd(torch::Tensor y, torch::Tensor G, int64_t B, int64_t H, int64_t W, i
                       mptr(dbeta), mptr(dbias), dz.data_ptr<float>(), cur_stream()));
 }
 
+void bn_fused_fwd(torch::Tensor part, int64_t T, int64_t R, int64_t M, torch::Tensor gamma, torch::Tensor beta,
+                  c10::optional<torch::Tensor> running_mean, c10::optional<torch::Tensor> running_var,
+                  c10::optional<torch::Tensor> nbt, double momentum, double eps, torch::Tensor bnv, torch::Tensor y,
+                  torch::Tensor out, int64_t B, int64_t H, int64_t W, bool pool) {
+  const int64_t C = gamma.numel();
+  TORCH_CHECK(C % 16 == 0 && (!pool || (H % 2 == 0 && W % 2 == 0)) && M == B * H * W && T == (M + R - 1) / R,
+              "bn_fused_fwd: shape");
+  check_t(part, T * C * 2, "part"); check_t(beta, C, "beta"); check_t(bnv, 4 * C, "bnv");
+  check_t(running_mean, C, "running_mean"); check_t(running_var, C, "running_var");
+  check_t(y, M * C, "y"); check_t(out, B * (pool ? H / 2 : H) * (pool ? W / 2 : W) * C, "out");
+  if (nbt.has_value()) TORCH_CHECK(nbt->scalar_type() == at::kLong && nbt->is_cuda(), "nbt: int64 GPU scalar");
+  DevGuard g(y.device());
+  CS_LAUNCH(cs_bn_fused_fwd(part.data_ptr<float>(), T, R, M, C, gamma.data_ptr<float>(), beta.data_ptr<float>(),
+                            mptr(running_mean), mptr(running_var),
+                            nbt.has_value() ? nbt->data_ptr<int64_t>() : nullptr, (float)momentum, (float)eps,
+                            bnv.data_ptr<float>(), y.data_ptr<float>(), out.data_ptr<float>(), B, H, W, pool ? 1 : 0,
+                            cur_stream()));
+}
+
+void bn_fused_bwd(torch::Tensor y, torch::Tensor G, int64_t B, int64_t H, int64_t W, int64_t C, bool pool,
+                  torch::Tensor bnv, torch::Tensor gamma, torch::Tensor coef, c10::optional<torch::Tensor> dgamma,
+                  c10::optional<torch::Tensor> dbeta, c10::optional<torch::Tensor> dbias, torch::Tensor dz) {
+  TORCH_CHECK(C % 16 == 0 && (!pool || (H % 2 == 0 && W % 2 == 0)), "bn_fused_bwd: shape");
+  check_t(y, B * H * W * C, "y");
+  check_t(G, B * (pool ? H / 2 : H) * (pool ? W / 2 : W) * C, "G");
+  check_t(bnv, 4 * C, "bnv"); check_t(gamma, C, "gamma"); check_t(coef, 3 * C, "coef");
+  check_t(dgamma, C, "dgamma"); check_t(dbeta, C, "dbeta"); check_t(dbias, C, "dbias");
+  check_t(dz, B * H * W * C, "dz");
+  DevGuard g(y.device());
+  CS_LAUNCH(cs_bn_fused_bwd(y.data_ptr<float>(), G.data_ptr<float>(), B, H, W, C, pool ? 1 : 0, bnv.data_ptr<float>(),
+                            gamma.data_ptr<float>(), coef.data_ptr<float>(), mptr(dgamma), mptr(dbeta), mptr(dbias),
+                            dz.data_ptr<float>(), cur_stream()));
+}
+
 }  // namespace
 
 void register_conv_ops(pybind11::module& m) {
+  m.def("bn_fused_fwd", &bn_fused_fwd, "single-launch BN finalize + normalize/ReLU(/pool) (small layers)");
+  m.def("bn_fused_bwd", &bn_fused_bwd, "single-launch BN backward: reduce + finalize + apply (small layers)");
   m.def("conv_gemm", &conv_gemm, "implicit-GEMM 3x3 conv (mode 0 fwd / 1 dgrad / 2 wgrad), fp32 MFMA",
         py::arg("mode"), py::arg("x"), py::arg("w"), py::arg("dz"), py::arg("bias"), py::arg("out"), py::arg("ws"),
         py::arg("stats"), py::arg("B"), py::arg("H"), py::arg("W"), py::arg("Cin"), py::arg("Cout"),

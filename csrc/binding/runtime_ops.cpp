@@ -154,6 +154,7 @@ void register_runtime(pybind11::module& m) {
       .def("set_overlap_wgrad", &cs::VggEngine::set_overlap_wgrad)
       .def("set_fixup", &cs::VggEngine::set_fixup)
       .def("set_dual", &cs::VggEngine::set_dual)
+      .def("set_bn_fused_rows", &cs::VggEngine::set_bn_fused_rows)
       .def("block_dual", &cs::VggEngine::block_dual)
       .def("set_block_dual", &cs::VggEngine::set_block_dual)
       .def("set_tile", &cs::VggEngine::set_tile, py::arg("block"), py::arg("mode"), py::arg("bm"), py::arg("bn"),

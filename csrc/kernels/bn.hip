@@ -247,6 +247,173 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
   coef[3 * c + 2] = k3;
 }
 
+// ------------------------------------------------------------------ single-kernel BN for small layers
+// One block owns 16 channels (4 float4 lanes x 64 row lanes) and ALL rows of them, so the
+// statistics -> coefficients -> apply dependency stays inside the block: forward = finalize
+// + normalize/ReLU/pool, backward = reduce + finalize + apply, each ONE launch instead of
+// two / three (each launch boundary plus its dependent global round trip costs ~3-5 us on
+// MI355X, more than these layers' data movement). Reductions run in a fixed order
+// (row-lane butterfly, then the 4 waves in order): deterministic. Used where the rows per
+// block are few (the engine's small-spatial layers).
+constexpr int kFusedCh = 16;
+
+// fixed-order Chan combine of 64 row lanes (tid = rl*4 + cq) -> lanes with rl == 0
+__device__ __forceinline__ void chan_reduce_block(float (&n)[4], float (&m)[4], float (&M2)[4], float* lds) {
+#pragma unroll
+  for (int off = 4; off < 64; off <<= 1)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float nb = __shfl_xor(n[q], off, 64), mb = __shfl_xor(m[q], off, 64), M2b = __shfl_xor(M2[q], off, 64);
+      chan_combine(n[q], m[q], M2[q], nb, mb, M2b);
+    }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, cq = threadIdx.x & 3;
+  if (lane < 4)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      lds[((wv * 4 + cq) * 4 + q) * 3 + 0] = n[q];
+      lds[((wv * 4 + cq) * 4 + q) * 3 + 1] = m[q];
+      lds[((wv * 4 + cq) * 4 + q) * 3 + 2] = M2[q];
+    }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      n[q] = m[q] = M2[q] = 0.f;
+      for (int w = 0; w < 4; ++w)
+        chan_combine(n[q], m[q], M2[q], lds[((w * 4 + cq) * 4 + q) * 3], lds[((w * 4 + cq) * 4 + q) * 3 + 1],
+                     lds[((w * 4 + cq) * 4 + q) * 3 + 2]);
+    }
+  }
+}
+
+// fixed-order sum of 3x4 per-thread accumulators over the 64 row lanes -> threads < 4
+__device__ __forceinline__ void sum_reduce_block(float (&acc)[3][4], float* lds) {
+#pragma unroll
+  for (int off = 4; off < 64; off <<= 1)
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[k][q] += __shfl_xor(acc[k][q], off, 64);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, cq = threadIdx.x & 3;
+  if (lane < 4)
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) lds[((wv * 4 + cq) * 3 + k) * 4 + q] = acc[k][q];
+  __syncthreads();
+  if (threadIdx.x < 4)
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float s = 0.f;
+        for (int w = 0; w < 4; ++w) s += lds[((w * 4 + cq) * 3 + k) * 4 + q];
+        acc[k][q] = s;
+      }
+}
+
+__global__ __launch_bounds__(256) void bn_fused_fwd_kernel(const float* __restrict__ part, int T, int R, int M,
+                                                           int C, const float* __restrict__ gamma,
+                                                           const float* __restrict__ beta, float* running_mean,
+                                                           float* running_var, int64_t* nbt, float momentum,
+                                                           float eps, float* __restrict__ bnv, const float* __restrict__ y,
+                                                           float* __restrict__ out, int B, int H, int W, int pool) {
+  __shared__ float lds[4 * 4 * 4 * 3];
+  __shared__ float4 sc_sh[2][4];
+  const int cq = threadIdx.x & 3, rl = threadIdx.x >> 2;
+  const int cqg = blockIdx.x * 4 + cq;  // global channel quad
+  float n[4] = {0.f, 0.f, 0.f, 0.f}, m[4] = {0.f, 0.f, 0.f, 0.f}, M2[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int t = rl; t < T; t += 64) {
+    const int cnt = (M - t * R) < R ? (M - t * R) : R;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float2 pm = *reinterpret_cast<const float2*>(part + ((size_t)t * C + 4 * cqg + q) * 2);
+      chan_combine(n[q], m[q], M2[q], (float)cnt, pm.x, pm.y);
+    }
+  }
+  chan_reduce_block(n, m, M2, lds);
+  if (threadIdx.x < 4) {
+    float sc[4], sh[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int c = 4 * cqg + q;
+      const float var = M2[q] / n[q], inv = 1.0f / sqrtf(var + eps);
+      sc[q] = gamma[c] * inv;
+      sh[q] = beta[c] - m[q] * gamma[c] * inv;
+      bnv[c] = sc[q];
+      bnv[C + c] = sh[q];
+      bnv[2 * C + c] = m[q];
+      bnv[3 * C + c] = inv;
+      if (running_mean != nullptr) {
+        const float unb = n[q] > 1.f ? M2[q] / (n[q] - 1.f) : var;
+        running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * m[q];
+        running_var[c] = (1.f - momentum) * running_var[c] + momentum * unb;
+      }
+    }
+    sc_sh[0][cq] = make_float4(sc[0], sc[1], sc[2], sc[3]);
+    sc_sh[1][cq] = make_float4(sh[0], sh[1], sh[2], sh[3]);
+  }
+  if (nbt != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *nbt += 1;
+  __syncthreads();
+  const float4 s = sc_sh[0][cq], t = sc_sh[1][cq];
+  const int C4 = C >> 2;
+  const int Ho = pool ? H >> 1 : H, Wo = pool ? W >> 1 : W;
+  const int units = B * Ho * Wo;
+  const float4* y4 = reinterpret_cast<const float4*>(y);
+  for (int u = rl; u < units; u += 64) {
+    float4 r;
+    if (!pool) {
+      r = bnrelu4(y4[(size_t)u * C4 + cqg], s, t);
+    } else {
+      const int wo = u % Wo, ho = (u / Wo) % Ho, b = u / (Wo * Ho);
+      const size_t base = (((size_t)b * H + 2 * ho) * W + 2 * wo) * C4 + cqg;
+      const float4 a0 = bnrelu4(y4[base], s, t), a1 = bnrelu4(y4[base + C4], s, t);
+      const float4 a2 = bnrelu4(y4[base + (size_t)W * C4], s, t), a3 = bnrelu4(y4[base + (size_t)W * C4 + C4], s, t);
+      r = make_float4(fmaxf(fmaxf(a0.x, a1.x), fmaxf(a2.x, a3.x)), fmaxf(fmaxf(a0.y, a1.y), fmaxf(a2.y, a3.y)),
+                      fmaxf(fmaxf(a0.z, a1.z), fmaxf(a2.z, a3.z)), fmaxf(fmaxf(a0.w, a1.w), fmaxf(a2.w, a3.w)));
+    }
+    reinterpret_cast<float4*>(out)[(size_t)u * C4 + cqg] = r;
+  }
+}
+
+template <bool POOL>
+__global__ __launch_bounds__(256) void bn_fused_bwd_kernel(const float* __restrict__ y, const float* __restrict__ G,
+                                                           int B, int H, int W, int C, const float* __restrict__ bnv,
+                                                           const float* __restrict__ gamma, float* __restrict__ coef,
+                                                           float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                           float* __restrict__ dbias, float* __restrict__ dz) {
+  __shared__ float lds[4 * 4 * 3 * 4];
+  const int cq = threadIdx.x & 3, rl = threadIdx.x >> 2;
+  const int cqg = blockIdx.x * 4 + cq;
+  const float* scale = bnv;
+  const float* shift = bnv + C;
+  const float* mean = bnv + 2 * C;
+  const float* invstd = bnv + 3 * C;
+  const int units = POOL ? B * (H >> 1) * (W >> 1) : B * H * W;
+  float acc[3][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  for (int u = rl; u < units; u += 64)
+    bwd_visit<false, POOL>(y, G, B, H, W, C, cqg, u, scale, shift, mean, invstd, coef, dz, acc);
+  sum_reduce_block(acc, lds);
+  if (threadIdx.x < 4) {
+    const float Mf = (float)(B * H * W);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int c = 4 * cqg + q;
+      const float k1 = gamma[c] * invstd[c], k2 = acc[0][q] / Mf, k3 = acc[1][q] / Mf;
+      if (dgamma) dgamma[c] = acc[1][q];
+      if (dbeta) dbeta[c] = acc[0][q];
+      if (dbias) dbias[c] = -k1 * k3 * acc[2][q];
+      coef[3 * c] = k1;
+      coef[3 * c + 1] = k2;
+      coef[3 * c + 2] = k3;
+    }
+  }
+  __syncthreads();  // coef (global, written by this block) is visible to the whole workgroup
+  float dummy[3][4];
+  for (int u = rl; u < units; u += 64)
+    bwd_visit<true, POOL>(y, G, B, H, W, C, cqg, u, scale, shift, mean, invstd, coef, dz, dummy);
+}
+
 }  // namespace
 
 int cs_bn_bwd_blocks(int B, int H, int W, int C, int pool) {
@@ -309,5 +476,27 @@ hipError_t cs_bn_bwd(const float* y, const float* G, int B, int H, int W, int C,
     hipLaunchKernelGGL((bn_bwd_kernel<true, false>), dim3(blocks), dim3(256), 0, stream, y, G, B, H, W, C, scale,
                        shift, mean, invstd, coef, dz, nullptr);
   }
+  return hipGetLastError();
+}
+
+hipError_t cs_bn_fused_fwd(const float* part, int T, int R, int M, int C, const float* gamma, const float* beta,
+                           float* running_mean, float* running_var, int64_t* nbt, float momentum, float eps,
+                           float* bnv, const float* y, float* out, int B, int H, int W, int pool, hipStream_t stream) {
+  if (C % kFusedCh != 0 || (pool && ((H | W) & 1))) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(bn_fused_fwd_kernel, dim3(C / kFusedCh), dim3(256), 0, stream, part, T, R, M, C, gamma, beta,
+                     running_mean, running_var, nbt, momentum, eps, bnv, y, out, B, H, W, pool);
+  return hipGetLastError();
+}
+
+hipError_t cs_bn_fused_bwd(const float* y, const float* G, int B, int H, int W, int C, int pool, const float* bnv,
+                           const float* gamma, float* coef, float* dgamma, float* dbeta, float* dbias, float* dz,
+                           hipStream_t stream) {
+  if (C % kFusedCh != 0 || (pool && ((H | W) & 1))) return hipErrorInvalidValue;
+  if (pool)
+    hipLaunchKernelGGL((bn_fused_bwd_kernel<true>), dim3(C / kFusedCh), dim3(256), 0, stream, y, G, B, H, W, C, bnv,
+                       gamma, coef, dgamma, dbeta, dbias, dz);
+  else
+    hipLaunchKernelGGL((bn_fused_bwd_kernel<false>), dim3(C / kFusedCh), dim3(256), 0, stream, y, G, B, H, W, C, bnv,
+                       gamma, coef, dgamma, dbeta, dbias, dz);
   return hipGetLastError();
 }

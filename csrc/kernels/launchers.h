@@ -93,6 +93,16 @@ hipError_t cs_bn_bwd(const float* y, const float* G, int B, int H, int W, int C,
                      const float* shift, const float* mean, const float* invstd, const float* gamma, float* part,
                      float* coef, float* dgamma, float* dbeta, float* dbias, float* dz, hipStream_t stream);
 
+// single-launch BN for small layers (one block per 16 channels owns all their rows):
+// forward = finalize (tile partials -> bnv [4][C] = scale, shift, mean, invstd + running stats)
+// + normalize/ReLU(/pool); backward = reduce + finalize + apply (coef [C][3] scratch)
+hipError_t cs_bn_fused_fwd(const float* part, int T, int R, int M, int C, const float* gamma, const float* beta,
+                           float* running_mean, float* running_var, int64_t* nbt, float momentum, float eps,
+                           float* bnv, const float* y, float* out, int B, int H, int W, int pool, hipStream_t stream);
+hipError_t cs_bn_fused_bwd(const float* y, const float* G, int B, int H, int W, int C, int pool, const float* bnv,
+                           const float* gamma, float* coef, float* dgamma, float* dbeta, float* dbias, float* dz,
+                           hipStream_t stream);
+
 // ---------------------------------------------------------------- decoder-LM elementwise ops (lm.hip)
 enum { CS_F32 = 0, CS_BF16 = 1 };
 int cs_rmsnorm_bwd_partials(int rows);

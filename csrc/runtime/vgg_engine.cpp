@@ -173,6 +173,7 @@ VggEngine::VggEngine(int64_t Bmax, std::vector<int64_t> desc, std::vector<int64_
   counters_ = torch::zeros({3 * L * tiles_max_}, fo.dtype(at::kInt));
   if (const char* e = getenv("CS_CONV_FIXUP")) fixup_ = atoi(e) != 0;
   if (const char* e = getenv("CS_CONV_DUAL")) dual_ = atoi(e) != 0;
+  if (const char* e = getenv("CS_BN_FUSED_ROWS")) bn_fused_rows_ = atoll(e);
   bn_part_ = torch::zeros({partmax}, fo);
   bn_coef_ = torch::zeros({cmax * 3}, fo);
   bn_eval_ = torch::zeros({2, cmax}, fo);
@@ -266,6 +267,11 @@ void VggEngine::conv(int l, int mode, int B, const ConvTile& t, hipStream_t s, b
   ok(cs_conv_gemm(a, mode, t.bm, t.bn, t.bk, t.splits, s, t.stage), "conv_gemm");
 }
 
+bool VggEngine::bn_fused(int l, int64_t B) const {
+  const VggBlock& b = blocks_[l];
+  return B * b.H * b.H <= bn_fused_rows_ && b.cout % 16 == 0;
+}
+
 bool VggEngine::dual_ok(int l) const {
   if (!dual_ || l == 0 || !blocks_[l].use_dual) return false;
   const ConvTile& w = blocks_[l].tile[CS_CONV_WGRAD];
@@ -314,11 +320,18 @@ void VggEngine::forward_train(int64_t B) {
     const int rows = cs_conv_stat_rows(9 * b.cin, t.bm, t.bn, t.bk, t.splits, fixup_);
     float* bn = b.bn.data_ptr<float>();
     float* bufs = bufs_.data_ptr<float>();
+    float* out = (l + 1 < L) ? blocks_[l + 1].x.data_ptr<float>() : gbuf_[1].data_ptr<float>();
+    if (bn_fused(l, B)) {  // finalize + normalize/ReLU/pool in one launch
+      ok(cs_bn_fused_fwd(b.stats.data_ptr<float>(), (int)cdiv(M, rows), rows, (int)M, b.cout, P(b.g_off),
+                         P(b.be_off), bufs + b.rm_off, bufs + b.rv_off, nbt_.data_ptr<int64_t>() + l, kBnMomentum,
+                         kBnEps, bn, b.y.data_ptr<float>(), out, (int)B, b.H, b.H, b.pool, s),
+         "bn_fused_fwd");
+      continue;
+    }
     ok(cs_bn_finalize(b.stats.data_ptr<float>(), (int)cdiv(M, rows), rows, (int)M, b.cout, P(b.g_off), P(b.be_off),
                       bufs + b.rm_off, bufs + b.rv_off, nbt_.data_ptr<int64_t>() + l, kBnMomentum, kBnEps, bn,
                       bn + b.cout, bn + 2 * b.cout, bn + 3 * b.cout, s),
        "bn_finalize");
-    float* out = (l + 1 < L) ? blocks_[l + 1].x.data_ptr<float>() : gbuf_[1].data_ptr<float>();
     ok(cs_bn_apply(b.y.data_ptr<float>(), bn, bn + b.cout, out, (int)B, b.H, b.H, b.cout, b.pool, s), "bn_apply");
   }
   // features of the last block were staged in gbuf_[1] (free until the first dgrad); dfeat -> gbuf_[0]
@@ -340,10 +353,17 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
     // WAR: block l+2's weight-gradient GEMM (side stream) reads the same dz buffer; it may
     // belong to an earlier backward() call of this step that did not join (bucketed step)
     if (overlap_wgrad_ && l + 2 < L) ok(hipStreamWaitEvent(s, ev_wg_[l + 2], 0), "wait wgrad");
-    ok(cs_bn_bwd(b.y.data_ptr<float>(), gbuf_[(L - 1 - l) % 2].data_ptr<float>(), (int)B, b.H, b.H, b.cout, b.pool,
-                 bn, bn + b.cout, bn + 2 * b.cout, bn + 3 * b.cout, P(b.g_off), bn_part_.data_ptr<float>(),
-                 bn_coef_.data_ptr<float>(), G(b.g_off), G(b.be_off), G(b.b_off), dz, s),
-       "bn_bwd");
+    if (bn_fused(l, B)) {  // reduce + finalize + apply in one launch
+      ok(cs_bn_fused_bwd(b.y.data_ptr<float>(), gbuf_[(L - 1 - l) % 2].data_ptr<float>(), (int)B, b.H, b.H, b.cout,
+                         b.pool, bn, P(b.g_off), bn_coef_.data_ptr<float>(), G(b.g_off), G(b.be_off), G(b.b_off), dz,
+                         s),
+         "bn_fused_bwd");
+    } else {
+      ok(cs_bn_bwd(b.y.data_ptr<float>(), gbuf_[(L - 1 - l) % 2].data_ptr<float>(), (int)B, b.H, b.H, b.cout, b.pool,
+                   bn, bn + b.cout, bn + 2 * b.cout, bn + 3 * b.cout, P(b.g_off), bn_part_.data_ptr<float>(),
+                   bn_coef_.data_ptr<float>(), G(b.g_off), G(b.be_off), G(b.b_off), dz, s),
+         "bn_bwd");
+    }
     if (!overlap_wgrad_ && dual_ok(l)) {  // wgrad + dgrad in one launch
       conv_dual(l, (int)B, s, dz);
       continue;

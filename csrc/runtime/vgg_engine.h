@@ -81,6 +81,7 @@ class VggEngine {
   void set_overlap_wgrad(bool on) { overlap_wgrad_ = on; }
   void set_fixup(bool on) { fixup_ = on; }
   void set_dual(bool on) { dual_ = on; }
+  void set_bn_fused_rows(int64_t r) { bn_fused_rows_ = r; }
   bool block_dual(int64_t l) const { return blocks_.at(l).use_dual; }
   void set_block_dual(int64_t l, bool on) { blocks_.at(l).use_dual = on; }
   // SGD (momentum, weight decay, dampening) on [off, off+n) of the flat buffers
@@ -112,6 +113,8 @@ class VggEngine {
   CsConvArgs conv_args(int l, int mode, int B, bool with_stats, float* ws, float* dz);
   // block l's wgrad + dgrad as one launch (both 64x64 register-staged tiles)
   bool dual_ok(int l) const;
+  // single-launch BN forward / backward for layers with at most bn_fused_rows_ rows (B*H*W)
+  bool bn_fused(int l, int64_t B) const;
   void conv_dual(int l, int B, hipStream_t s, float* dz);
   float* P(int64_t off) { return params_.data_ptr<float>() + off; }
   float* G(int64_t off) { return grads_.data_ptr<float>() + off; }
@@ -131,7 +134,10 @@ class VggEngine {
   // at B=64 every tuned GEMM was slower with it (the last block's serial slab read costs more
   // than the separate reduce launch it saves): 64.8k vs 69.1k img/s.
   bool fixup_ = false;
-  bool dual_ = true;  // horizontal wgrad+dgrad fusion in backward (CS_CONV_DUAL=0 disables)
+  bool dual_ = true;
+  // CS_BN_FUSED_ROWS; 0 disables. Measured on MI355X at B=64 (img/s): 0 -> 71.46k, 256 (blocks 6-7)
+  // -> 71.64k, 1024 -> 69.85k, 4096 -> 63.07k: one block per 16 channels serialises too many rows
+  int64_t bn_fused_rows_ = 256;  // horizontal wgrad+dgrad fusion in backward (CS_CONV_DUAL=0 disables)
   hipStream_t side_ = nullptr;
   bool overlap_wgrad_ = false;
   std::vector<hipEvent_t> ev_bn_, ev_wg_;  // per block: BN-backward done (main), wgrad done (side)

@@ -117,7 +117,8 @@ def test_conv_wgrad(dev, shape, tile, fixup, stage):
                                         (64, 2, 512, True), (5, 16, 128, True), (8, 8, 256, False),
                                         (16, 8, 256, False), (8, 4, 512, False), (64, 8, 256, False),
                                         (64, 32, 64, True)])
-def test_bn_relu_pool_fwd_bwd(dev, B, H, C, pool):
+@pytest.mark.parametrize("fused", [False, True])
+def test_bn_relu_pool_fwd_bwd(dev, B, H, C, pool, fused):
     from cs744_pytorch_distributed_tutorial_amd.ops import functional as Fn
     torch.manual_seed(B * C)
     y = (torch.randn(B, C, H, H, dtype=torch.float64) * 2 + 0.5).requires_grad_()
@@ -136,12 +137,20 @@ def test_bn_relu_pool_fwd_bwd(dev, B, H, C, pool):
     rmd, rvd = torch.zeros(C, device=dev), torch.ones(C, device=dev)
     nbt = torch.zeros((), dtype=torch.int64, device=dev)
     gd, bd = gamma.detach().float().to(dev), beta.detach().float().to(dev)
-    out, bst = Fn.bn_relu_pool_fwd(yd, st, yd.shape[0], B, H, H, gd, bd, rmd, rvd, nbt, pool=pool)
+    if fused:  # several partial tiles, to exercise the in-block Chan combine
+        R = 16 if yd.shape[0] % 16 == 0 else yd.shape[0]
+        seg = yd.double().view(-1, R, C)
+        mu_t = seg.mean(1)
+        st = torch.stack([mu_t, ((seg - mu_t[:, None]) ** 2).sum(1)], 2).float().contiguous()
+        out, bst = Fn.bn_relu_pool_fwd(yd, st, R, B, H, H, gd, bd, rmd, rvd, nbt, pool=pool, fused=True)
+    else:
+        out, bst = Fn.bn_relu_pool_fwd(yd, st, yd.shape[0], B, H, H, gd, bd, rmd, rvd, nbt, pool=pool)
     _close(out, z.detach().permute(0, 2, 3, 1), 1e-5)
     _close(rmd, rm, 1e-5)
     _close(rvd, rv, 1e-5)
     assert int(nbt) == 1
-    dz, dgamma, dbeta, dbias = Fn.bn_relu_pool_bwd(yd, _nhwc(G).float().to(dev), bst, gd, B, H, H, pool=pool)
+    dz, dgamma, dbeta, dbias = Fn.bn_relu_pool_bwd(yd, _nhwc(G).float().to(dev), bst, gd, B, H, H, pool=pool,
+                                                   fused=fused)
     _close(dz, y.grad.permute(0, 2, 3, 1).reshape(-1, C), 1e-4)
     _close(dgamma, gamma.grad, 1e-4)
     _close(dbeta, beta.grad, 1e-4)

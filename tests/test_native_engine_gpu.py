@@ -229,3 +229,19 @@ def test_device_cursor_walks_sampler_order_across_epochs(dev):
         want += [order[k * 16:(k + 1) * 16] for k in range(4)]
     assert seen == want[:7]
     assert int(tr.engine.cursor().item()) == 3  # 3 steps into epoch 1
+
+
+def test_single_launch_bn_matches_multi_kernel_bn(dev):
+    # small layers use one BN launch per direction; the reduction order differs from the
+    # 2/3-kernel path, so compare with a norm bound (see the autotune test) after two steps
+    a = _trainer(dev, batch_size=32, train_size=256)
+    b = _trainer(dev, batch_size=32, train_size=256)
+    a.engine.set_bn_fused_rows(0)
+    b.engine.set_bn_fused_rows(1 << 30)
+    for _ in range(2):
+        a.step()
+        b.step()
+        assert abs(a.last_loss() - b.last_loss()) < 1e-3 * max(1.0, abs(a.last_loss()))
+    d = (b.params.double() - a.params.double()).norm() / a.params.double().norm()
+    assert d.item() < 2e-3, d.item()
+    torch.testing.assert_close(b.nbt, a.nbt)
