@@ -144,6 +144,11 @@ def main(argv=None) -> int:
                    "optimizer": "SGD(lr=0.1, momentum=0.9, wd=1e-4)", "final_loss": round(loss, 4),
                    "baseline_img_s": baseline},
     }
+    if hasattr(trainer, "tile_table"):
+        # which MFMA math the autotuner picked per conv GEMM: f32-input MFMA, or the fp32-accurate
+        # split-bf16 x6 kernels (3 bf16 pieces per operand, 6 MFMAs; f64-checked like the f32 path)
+        maths = [t["math"] for t in trainer.tile_table()]
+        out["config"]["conv_gemm_math"] = {m: maths.count(m) for m in sorted(set(maths))}
     if rank == 0:
         line = json.dumps(out)
         print(line, flush=True)

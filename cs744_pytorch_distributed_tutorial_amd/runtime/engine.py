@@ -172,6 +172,9 @@ class FlatLayout:
         return lows, ranges
 
 
+_STAGE_NAMES = {0: "regs", 1: "lds_dma", 2: "lds_dma_deep", 3: "kgroups2", 4: "kgroups4"}
+
+
 class NativeTrainer:
     """VGG training on the native engine; one instance per rank (one GPU per process)."""
 
@@ -284,7 +287,8 @@ class NativeTrainer:
                 bm, bn, sp, bk, st = self.engine.get_tile(l, m)
                 us = self.tune_us[3 * l + m] if self.tune_us else None
                 out.append({"block": l, "op": names[m], "bm": bm, "bn": bn, "bk": bk, "splits": sp,
-                            "stage": "lds_dma" if st else "regs", "us": us})
+                            "stage": _STAGE_NAMES.get(st & 7, str(st & 7)),
+                            "math": "x6" if st & 8 else "f32", "us": us})
         return out
 
     # ---------------------------------------------------------------- data

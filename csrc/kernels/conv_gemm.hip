@@ -341,6 +341,79 @@ __device__ __forceinline__ void mma_chunk(const float (&af)[RM][4], const float 
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][s], bf[j][s], acc[i][j], 0, 0, 0);
 }
 
+// ---------------------------------------------------------------- fp32-accurate split-bf16 math (X6)
+// gfx950 has no xf32, and its bf16 MFMA (v_mfma_f32_32x32x16_bf16: 32 cyc / 32K FLOP) runs 16x
+// the rate of the f32-input one (32x32x2f32: 64 cyc / 4K FLOP). Each f32 operand is split
+// exactly into three bf16 pieces by round-to-nearest: x = h + m + l, |m| <= 2^-9 |x|,
+// |l| <= 2^-18 |x| (the residuals x - h and r - m are exact in f32). The product is the six
+// terms down to 2^-18 relative — hh + hm + mh + mm + hl + lh — accumulated in f32 by the MFMA;
+// the dropped ml + lm + ll are <= 2^-26 |a||b|, below f32's own product rounding (2^-24). So
+// a K=16 step costs 6 x 32 = 192 MFMA cycles instead of 8 x 64 = 512, with f32-level error
+// (tests/test_conv_bn_gpu.py checks it against the f64 reference next to the f32 path).
+// Fragment mapping: two 4-deep f32 sub-step chunks (k = base + 0..3 and base + 4..7 of the
+// lane half) are the 8 bf16 elements j of one 32x32x16 fragment; A and B use the same k
+// order, so the K permutation cancels in the dot product.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ void split3(const float (&x0)[4], const float (&x1)[4], bf16x8& h, bf16x8& m,
+                                       bf16x8& l) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float x = j < 4 ? x0[j] : x1[j - 4];
+    const __bf16 hj = (__bf16)x;
+    const float r = x - (float)hj;
+    const __bf16 mj = (__bf16)r;
+    h[j] = hj;
+    m[j] = mj;
+    l[j] = (__bf16)(r - (float)mj);
+  }
+}
+
+template <int RM, int RN>
+__device__ __forceinline__ void mma_x6(const float (&a0)[RM][4], const float (&a1)[RM][4], const float (&b0)[RN][4],
+                                       const float (&b1)[RN][4], f32x16 (&acc)[RM][RN]) {
+  bf16x8 ah[RM], am[RM], al[RM], bh[RN], bm[RN], bl[RN];
+#pragma unroll
+  for (int i = 0; i < RM; ++i) split3(a0[i], a1[i], ah[i], am[i], al[i]);
+#pragma unroll
+  for (int j = 0; j < RN; ++j) split3(b0[j], b1[j], bh[j], bm[j], bl[j]);
+  // small terms first (they are exact products; the f32 chain rounds once per MFMA)
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j) {
+      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[i], bm[j], acc[i][j], 0, 0, 0);
+      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bm[j], acc[i][j], 0, 0, 0);
+      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[i], bh[j], acc[i][j], 0, 0, 0);
+      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+    }
+}
+
+// SCHED 2 (X6 math): one K-step as pairs of sub-step chunks, each pair one split-bf16 MFMA
+// group; the next tiles' global loads go out after the first pair, the LDS store after the
+// second (or the first when the K-group owns a single pair).
+template <int BM, int BN, int MODE, int BK, int LS, int SS, bool C4, int KG>
+__device__ __forceinline__ void kstep_x6(Loader<BM, BN, MODE, BK, C4, false, KG>& ld, const CsConvArgs& a,
+                                         const float* cur, float* nxt,
+                                         f32x16 (&acc)[Tile<BM, BN, MODE, BK>::RM][Tile<BM, BN, MODE, BK>::RN],
+                                         int wm, int wn, int r, int hh, int kg, int k_load) {
+  using T = Tile<BM, BN, MODE, BK>;
+  constexpr int NGK = T::NG / KG;
+  static_assert(NGK >= 2 && NGK % 2 == 0, "X6 math needs pairs of sub-step chunks per K-group");
+  const int g0 = kg * NGK;
+#pragma unroll
+  for (int gp = 0; gp < NGK; gp += 2) {
+    float af[2][T::RM][4], bf[2][T::RN][4];
+    read_chunk<BM, BN, MODE, BK>(cur, cur + T::A_ELEMS, g0 + gp, af[0], bf[0], wm, wn, r, hh);
+    read_chunk<BM, BN, MODE, BK>(cur, cur + T::A_ELEMS, g0 + gp + 1, af[1], bf[1], wm, wn, r, hh);
+    mma_x6<T::RM, T::RN>(af[0], af[1], bf[0], bf[1], acc);
+    if (gp == 0) ld.template load<LS>(a, k_load);
+    if (gp == (NGK > 2 ? 2 : 0)) ld.template store<SS>(nxt, nxt + T::A_ELEMS);
+  }
+}
+
 // One K-step on a staged LDS tile, with the next tiles' global loads (tile t+2 -> register
 // stage LS) and LDS store (tile t+1, register stage SS -> the other LDS buffer) folded in.
 // Both are unconditional (no branch around a load: hipcc would drain vmcnt there): past the
@@ -503,11 +576,22 @@ __device__ void splitk_fixup(const CsConvArgs& a, int tile, int mt, int nt, int 
 }
 
 // One K-step's MFMA chain on a staged LDS-DMA tile (GL): fragment reads one chunk ahead.
-template <int BM, int BN, int MODE, int BK>
+template <int BM, int BN, int MODE, int BK, bool X6 = false>
 __device__ __forceinline__ void kcompute_gl(const float* cur,
                                             f32x16 (&acc)[Tile<BM, BN, MODE, BK, true>::RM][Tile<BM, BN, MODE, BK, true>::RN],
                                             int wm, int wn, int r, int hh) {
   using T = Tile<BM, BN, MODE, BK, true>;
+  if constexpr (X6) {
+    static_assert(T::NG % 2 == 0, "X6 math needs pairs of sub-step chunks");
+#pragma unroll
+    for (int gp = 0; gp < T::NG; gp += 2) {
+      float a2[2][T::RM][4], b2[2][T::RN][4];
+      read_chunk<BM, BN, MODE, BK, true>(cur, cur + T::A_ELEMS, gp, a2[0], b2[0], wm, wn, r, hh);
+      read_chunk<BM, BN, MODE, BK, true>(cur, cur + T::A_ELEMS, gp + 1, a2[1], b2[1], wm, wn, r, hh);
+      mma_x6<T::RM, T::RN>(a2[0], a2[1], b2[0], b2[1], acc);
+    }
+    return;
+  }
   float af[2][T::RM][4], bf[2][T::RN][4];
   read_chunk<BM, BN, MODE, BK, true>(cur, cur + T::A_ELEMS, 0, af[0], bf[0], wm, wn, r, hh);
 #pragma unroll
@@ -581,7 +665,7 @@ __device__ __forceinline__ void gemm_body(const CsConvArgs& a, const int tile, c
         const int nx = cur == 0 ? NB - 1 : cur - 1;  // (t + NB - 1) % NB: the buffer read at step t-1
         ld.gload(a, (ks_begin + t + NB - 1) * BK, smem + nx * TG::STAGE, smem + nx * TG::STAGE + TG::A_ELEMS);
       }
-      kcompute_gl<BM, BN, MODE, BK>(smem + cur * TG::STAGE, acc, wm, wn, r, hh);
+      kcompute_gl<BM, BN, MODE, BK, SCHED == 2>(smem + cur * TG::STAGE, acc, wm, wn, r, hh);
       cur = cur == NB - 1 ? 0 : cur + 1;
     }
     __syncthreads();  // every wave's fragment reads are done before the epilogue reuses LDS
@@ -598,10 +682,16 @@ __device__ __forceinline__ void gemm_body(const CsConvArgs& a, const int tile, c
   __syncthreads();
   // even step t: tile t in lds0, tile t+1 in registers[1] -> lds1, tile t+2 -> registers[0]
   for (int t = 0; t < nks; t += 2) {
-    kstep<BM, BN, MODE, BK, SCHED, 0, 1, C4, KG>(ld, a, lds0, lds1, acc, wm, wn, r, hh, kg, (ks_begin + t + 2) * BK);
+    if constexpr (SCHED == 2)
+      kstep_x6<BM, BN, MODE, BK, 0, 1, C4, KG>(ld, a, lds0, lds1, acc, wm, wn, r, hh, kg, (ks_begin + t + 2) * BK);
+    else
+      kstep<BM, BN, MODE, BK, SCHED, 0, 1, C4, KG>(ld, a, lds0, lds1, acc, wm, wn, r, hh, kg, (ks_begin + t + 2) * BK);
     __syncthreads();
     if (t + 1 >= nks) break;
-    kstep<BM, BN, MODE, BK, SCHED, 1, 0, C4, KG>(ld, a, lds1, lds0, acc, wm, wn, r, hh, kg, (ks_begin + t + 3) * BK);
+    if constexpr (SCHED == 2)
+      kstep_x6<BM, BN, MODE, BK, 1, 0, C4, KG>(ld, a, lds1, lds0, acc, wm, wn, r, hh, kg, (ks_begin + t + 3) * BK);
+    else
+      kstep<BM, BN, MODE, BK, SCHED, 1, 0, C4, KG>(ld, a, lds1, lds0, acc, wm, wn, r, hh, kg, (ks_begin + t + 3) * BK);
     __syncthreads();
   }
   }
@@ -896,42 +986,53 @@ hipError_t launch_k(dim3 grid, size_t lds, hipStream_t stream, const CsConvArgs&
   return hipGetLastError();
 }
 
-template <int BM, int BN, int MODE, int BK>
-hipError_t launch_gemm(const CsConvArgs& a, int splits, int stage, hipStream_t stream) {
+// MATH 0: f32 MFMA (register staging honours CS_CONV_SCHED); MATH 2: X6 split-bf16 kernels
+template <int BM, int BN, int MODE, int BK, int MATH>
+hipError_t launch_gemm_m(const CsConvArgs& a, int splits, int stage, hipStream_t stream) {
   using T = Tile<BM, BN, MODE, BK>;
   using TG = Tile<BM, BN, MODE, BK, true>;
   const int ntiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
   const size_t lds = 2 * T::STAGE * sizeof(float);
   const dim3 grid(ntiles, 1, splits);
   constexpr bool deep_fits = (BM + BN) * BK * 4 * 5 < 160 * 1024;
-  if constexpr (BK != 64) {
+  if constexpr (BK != 64 && MATH == 0) {
     if (MODE == CS_CONV_FWD && a.w_oihw)  // padded conv0: Cin = 4 < BK
       return launch_k<BM, BN, MODE, BK, 0, true, 0>(grid, lds, stream, a);
   }
   if constexpr (BK == 32) {
     if (stage == CS_STAGE_LDS_DMA)
-      return launch_k<BM, BN, MODE, BK, 0, false, 3>(grid, 3 * TG::STAGE * sizeof(float), stream, a);
+      return launch_k<BM, BN, MODE, BK, MATH, false, 3>(grid, 3 * TG::STAGE * sizeof(float), stream, a);
     if constexpr (deep_fits) {
       if (stage == CS_STAGE_LDS_DMA_DEEP)
-        return launch_k<BM, BN, MODE, BK, 0, false, 5>(grid, 5 * TG::STAGE * sizeof(float), stream, a);
+        return launch_k<BM, BN, MODE, BK, MATH, false, 5>(grid, 5 * TG::STAGE * sizeof(float), stream, a);
     }
   }
   // K-groups: the LDS tile ring must also hold the (KG-1) partial-accumulator images
   if constexpr (BK >= 32 && BM * BK >= 2048 && BN * BK >= 2048) {
     if (stage == CS_STAGE_KG2) {
       const size_t red = (size_t)1 * 4 * (BM / 64) * (BN / 64) * 16 * 64 * sizeof(float);
-      return launch_k<BM, BN, MODE, BK, 0, false, 0, 2>(grid, std::max(lds, red), stream, a);
+      return launch_k<BM, BN, MODE, BK, MATH, false, 0, 2>(grid, std::max(lds, red), stream, a);
     }
   }
   if constexpr (BK == 64 && BM * BK >= 4096 && BN * BK >= 4096) {
     if (stage == CS_STAGE_KG4) {
       const size_t red = (size_t)3 * 4 * (BM / 64) * (BN / 64) * 16 * 64 * sizeof(float);
-      return launch_k<BM, BN, MODE, BK, 0, false, 0, 4>(grid, std::max(lds, red), stream, a);
+      return launch_k<BM, BN, MODE, BK, MATH, false, 0, 4>(grid, std::max(lds, red), stream, a);
     }
   }
   if (stage != CS_STAGE_REGS) return hipErrorInvalidValue;
-  if (conv_sched() == 1) return launch_k<BM, BN, MODE, BK, 1, false, 0>(grid, lds, stream, a);
-  return launch_k<BM, BN, MODE, BK, 0, false, 0>(grid, lds, stream, a);
+  if constexpr (MATH == 2) {
+    return launch_k<BM, BN, MODE, BK, 2, false, 0>(grid, lds, stream, a);
+  } else {
+    if (conv_sched() == 1) return launch_k<BM, BN, MODE, BK, 1, false, 0>(grid, lds, stream, a);
+    return launch_k<BM, BN, MODE, BK, 0, false, 0>(grid, lds, stream, a);
+  }
+}
+
+template <int BM, int BN, int MODE, int BK>
+hipError_t launch_gemm(const CsConvArgs& a, int splits, int stage, hipStream_t stream) {
+  if (stage & CS_STAGE_X6) return launch_gemm_m<BM, BN, MODE, BK, 2>(a, splits, stage & ~CS_STAGE_X6, stream);
+  return launch_gemm_m<BM, BN, MODE, BK, 0>(a, splits, stage, stream);
 }
 
 // hipcc (ROCm 7.2) leaves some host-side kernel stubs undefined when they are only
@@ -942,7 +1043,9 @@ hipError_t launch_gemm(const CsConvArgs& a, int splits, int stage, hipStream_t s
 #define CS_MODE(BM_, BN_, MODE_)                                            \
   CS_K(BM_, BN_, MODE_, 16, 0, false, 0) CS_K(BM_, BN_, MODE_, 16, 1, false, 0) \
   CS_K(BM_, BN_, MODE_, 32, 0, false, 0) CS_K(BM_, BN_, MODE_, 32, 1, false, 0) \
-  CS_K(BM_, BN_, MODE_, 32, 0, false, 3)
+  CS_K(BM_, BN_, MODE_, 32, 0, false, 3)                                      \
+  CS_K(BM_, BN_, MODE_, 16, 2, false, 0) CS_K(BM_, BN_, MODE_, 32, 2, false, 0) \
+  CS_K(BM_, BN_, MODE_, 32, 2, false, 3)
 #define CS_TILE(BM_, BN_)                                                                       \
   CS_MODE(BM_, BN_, CS_CONV_FWD) CS_MODE(BM_, BN_, CS_CONV_DGRAD) CS_MODE(BM_, BN_, CS_CONV_WGRAD) \
   CS_K(BM_, BN_, CS_CONV_FWD, 16, 0, true, 0) CS_K(BM_, BN_, CS_CONV_FWD, 32, 0, true, 0)
@@ -950,17 +1053,19 @@ CS_TILE(64, 64)
 CS_TILE(64, 128)
 CS_TILE(128, 64)
 CS_TILE(128, 128)
-#define CS_BK64(BM_, BN_, MODE_) CS_K(BM_, BN_, MODE_, 64, 0, false, 0) CS_K(BM_, BN_, MODE_, 64, 1, false, 0)
+#define CS_BK64(BM_, BN_, MODE_) \
+  CS_K(BM_, BN_, MODE_, 64, 0, false, 0) CS_K(BM_, BN_, MODE_, 64, 1, false, 0) CS_K(BM_, BN_, MODE_, 64, 2, false, 0)
 #define CS_TILE64(BM_, BN_) CS_BK64(BM_, BN_, CS_CONV_FWD) CS_BK64(BM_, BN_, CS_CONV_DGRAD) CS_BK64(BM_, BN_, CS_CONV_WGRAD)
 CS_TILE64(64, 64)
 CS_TILE64(128, 64)
 CS_TILE64(64, 128)
 #undef CS_TILE64
 #undef CS_BK64
-#define CS_KG(BM_, BN_, BK_, KG_)                                                                \
-  template __global__ void conv_gemm_kernel<BM_, BN_, CS_CONV_FWD, BK_, 0, false, 0, KG_>(CsConvArgs);   \
-  template __global__ void conv_gemm_kernel<BM_, BN_, CS_CONV_DGRAD, BK_, 0, false, 0, KG_>(CsConvArgs); \
-  template __global__ void conv_gemm_kernel<BM_, BN_, CS_CONV_WGRAD, BK_, 0, false, 0, KG_>(CsConvArgs);
+#define CS_KG1(BM_, BN_, BK_, KG_, M_)                                                            \
+  template __global__ void conv_gemm_kernel<BM_, BN_, CS_CONV_FWD, BK_, M_, false, 0, KG_>(CsConvArgs);   \
+  template __global__ void conv_gemm_kernel<BM_, BN_, CS_CONV_DGRAD, BK_, M_, false, 0, KG_>(CsConvArgs); \
+  template __global__ void conv_gemm_kernel<BM_, BN_, CS_CONV_WGRAD, BK_, M_, false, 0, KG_>(CsConvArgs);
+#define CS_KG(BM_, BN_, BK_, KG_) CS_KG1(BM_, BN_, BK_, KG_, 0) CS_KG1(BM_, BN_, BK_, KG_, 2)
 CS_KG(64, 64, 32, 2)
 CS_KG(128, 64, 32, 2)
 CS_KG(64, 128, 32, 2)
@@ -972,13 +1077,16 @@ CS_KG(64, 64, 64, 4)
 CS_KG(128, 64, 64, 4)
 CS_KG(64, 128, 64, 4)
 #undef CS_KG
-#define CS_DEEP(BM_, BN_)                                                                  \
-  CS_K(BM_, BN_, CS_CONV_FWD, 32, 0, false, 5) CS_K(BM_, BN_, CS_CONV_DGRAD, 32, 0, false, 5) \
-  CS_K(BM_, BN_, CS_CONV_WGRAD, 32, 0, false, 5)
+#undef CS_KG1
+#define CS_DEEP1(BM_, BN_, M_)                                                                \
+  CS_K(BM_, BN_, CS_CONV_FWD, 32, M_, false, 5) CS_K(BM_, BN_, CS_CONV_DGRAD, 32, M_, false, 5) \
+  CS_K(BM_, BN_, CS_CONV_WGRAD, 32, M_, false, 5)
+#define CS_DEEP(BM_, BN_) CS_DEEP1(BM_, BN_, 0) CS_DEEP1(BM_, BN_, 2)
 CS_DEEP(64, 64)
 CS_DEEP(64, 128)
 CS_DEEP(128, 64)
 #undef CS_DEEP
+#undef CS_DEEP1
 template __global__ void conv_dual_kernel<16, 16>(CsConvArgs, CsConvArgs, int, int, int);
 template __global__ void conv_dual_kernel<16, 32>(CsConvArgs, CsConvArgs, int, int, int);
 template __global__ void conv_dual_kernel<32, 16>(CsConvArgs, CsConvArgs, int, int, int);
@@ -1019,6 +1127,10 @@ void cs_conv_fill_dims(CsConvArgs* a, int mode) {
 }
 
 bool cs_conv_stage_ok(int stage, int bm, int bn, int bk, bool conv0_fwd) {
+  if (stage & CS_STAGE_X6) {  // split-bf16 math: every staging, except the padded conv0 forward
+    if (conv0_fwd) return false;
+    stage &= ~CS_STAGE_X6;
+  }
   if (conv0_fwd && stage != CS_STAGE_REGS) return false;
   switch (stage) {
     case CS_STAGE_REGS: return bk != 64 || !(bm == 128 && bn == 128);
@@ -1099,10 +1211,7 @@ hipError_t cs_conv_gemm_dual(CsConvArgs wg, int wbk, int wsplits, CsConvArgs dg,
 }
 
 hipError_t cs_conv_gemm(CsConvArgs a, int mode, int bm, int bn, int bk, int splits, hipStream_t stream, int stage) {
-  if ((stage == CS_STAGE_LDS_DMA || stage == CS_STAGE_LDS_DMA_DEEP) && (bk != 32 || (a.w_oihw && mode == CS_CONV_FWD)))
-    return hipErrorInvalidValue;
-  if ((stage == CS_STAGE_KG2 || stage == CS_STAGE_KG4) && !cs_conv_stage_ok(stage, bm, bn, bk, a.w_oihw && mode == CS_CONV_FWD))
-    return hipErrorInvalidValue;
+  if (!cs_conv_stage_ok(stage, bm, bn, bk, a.w_oihw && mode == CS_CONV_FWD)) return hipErrorInvalidValue;
   splits = prep_gemm(a, mode, bk, splits);
   if (splits < 0) return hipErrorInvalidValue;
   if (!cs_conv_fixup_ok(splits, bm, bn)) a.counters = nullptr;

@@ -61,7 +61,10 @@ void cs_conv_fill_dims(CsConvArgs* a, int mode);
 // (buffer_load ... lds into a 3- (5-) deep ring of swizzled images; bk = 32, not conv0's fwd;
 // the deep ring only where 5 images fit the 160 KiB LDS)
 // CS_STAGE_KG2 / KG4: register staging with 2 / 4 K-groups of 4 waves per block (bk >= 32 / 64)
-enum { CS_STAGE_REGS = 0, CS_STAGE_LDS_DMA = 1, CS_STAGE_LDS_DMA_DEEP = 2, CS_STAGE_KG2 = 3, CS_STAGE_KG4 = 4 };
+// | CS_STAGE_X6: the same staging with fp32-accurate split-bf16 math (3 bf16 pieces per
+// operand, 6 v_mfma_f32_32x32x16_bf16 per 32x32x16 product; conv_gemm.hip "X6")
+enum { CS_STAGE_REGS = 0, CS_STAGE_LDS_DMA = 1, CS_STAGE_LDS_DMA_DEEP = 2, CS_STAGE_KG2 = 3, CS_STAGE_KG4 = 4,
+       CS_STAGE_X6 = 8 };
 // whether a (stage, tile, bk) combination has a kernel
 bool cs_conv_stage_ok(int stage, int bm, int bn, int bk, bool conv0_fwd);
 hipError_t cs_conv_gemm(CsConvArgs a, int mode, int bm, int bn, int bk, int splits, hipStream_t stream,

@@ -174,6 +174,7 @@ VggEngine::VggEngine(int64_t Bmax, std::vector<int64_t> desc, std::vector<int64_
   if (const char* e = getenv("CS_CONV_FIXUP")) fixup_ = atoi(e) != 0;
   if (const char* e = getenv("CS_CONV_DUAL")) dual_ = atoi(e) != 0;
   if (const char* e = getenv("CS_BN_FUSED_ROWS")) bn_fused_rows_ = atoll(e);
+  if (const char* e = getenv("CS_CONV_MATH")) math_ = atoi(e);
   bn_part_ = torch::zeros({partmax}, fo);
   bn_coef_ = torch::zeros({cmax * 3}, fo);
   bn_eval_ = torch::zeros({2, cmax}, fo);
@@ -515,8 +516,11 @@ std::vector<double> VggEngine::autotune(int64_t B, int64_t iters) {
       std::vector<std::vector<int>> seen;
       const bool conv0_fwd = l == 0 && mode == CS_CONV_FWD && blocks_[0].cin == 4;
       for (int stage : {(int)CS_STAGE_REGS, (int)CS_STAGE_LDS_DMA, (int)CS_STAGE_LDS_DMA_DEEP, (int)CS_STAGE_KG2,
-                        (int)CS_STAGE_KG4})
+                        (int)CS_STAGE_KG4, CS_STAGE_X6 | CS_STAGE_REGS, CS_STAGE_X6 | CS_STAGE_LDS_DMA,
+                        CS_STAGE_X6 | CS_STAGE_LDS_DMA_DEEP, CS_STAGE_X6 | CS_STAGE_KG2, CS_STAGE_X6 | CS_STAGE_KG4})
       for (int bk : {16, 32, 64}) {
+        // CS_CONV_MATH: 0 = f32 MFMA kernels only, 1 = split-bf16 (X6) only, 2 = both (default)
+        if (((stage & CS_STAGE_X6) && math_ == 0) || (!(stage & CS_STAGE_X6) && math_ == 1)) continue;
         if (bk == 64 && conv0_fwd) continue;
         const int64_t ks = cdiv(d.K, bk);
         for (int bm : {64, 128}) {
