@@ -288,7 +288,7 @@ class NativeTrainer:
                 us = self.tune_us[3 * l + m] if self.tune_us else None
                 out.append({"block": l, "op": names[m], "bm": bm, "bn": bn, "bk": bk, "splits": sp,
                             "stage": _STAGE_NAMES.get(st & 7, str(st & 7)),
-                            "math": "x6" if st & 8 else "f32", "us": us})
+                            "math": "x6s" if st & 16 else ("x6" if st & 8 else "f32"), "us": us})
         return out
 
     # ---------------------------------------------------------------- data

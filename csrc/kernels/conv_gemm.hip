@@ -357,6 +357,14 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 __device__ __forceinline__ void split3(const float (&x0)[4], const float (&x1)[4], bf16x8& h, bf16x8& m,
                                        bf16x8& l) {
+#ifdef CS_X6_PROBE  // measurement only: no split arithmetic (wrong numbers), prices the split VALU
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const __bf16 hj = (__bf16)(j < 4 ? x0[j] : x1[j - 4]);
+    h[j] = hj; m[j] = hj; l[j] = hj;
+  }
+  return;
+#endif
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const float x = j < 4 ? x0[j] : x1[j - 4];
@@ -370,13 +378,9 @@ __device__ __forceinline__ void split3(const float (&x0)[4], const float (&x1)[4
 }
 
 template <int RM, int RN>
-__device__ __forceinline__ void mma_x6(const float (&a0)[RM][4], const float (&a1)[RM][4], const float (&b0)[RN][4],
-                                       const float (&b1)[RN][4], f32x16 (&acc)[RM][RN]) {
-  bf16x8 ah[RM], am[RM], al[RM], bh[RN], bm[RN], bl[RN];
-#pragma unroll
-  for (int i = 0; i < RM; ++i) split3(a0[i], a1[i], ah[i], am[i], al[i]);
-#pragma unroll
-  for (int j = 0; j < RN; ++j) split3(b0[j], b1[j], bh[j], bm[j], bl[j]);
+__device__ __forceinline__ void mma_x6f(const bf16x8 (&ah)[RM], const bf16x8 (&am)[RM], const bf16x8 (&al)[RM],
+                                        const bf16x8 (&bh)[RN], const bf16x8 (&bm)[RN], const bf16x8 (&bl)[RN],
+                                        f32x16 (&acc)[RM][RN]) {
   // small terms first (they are exact products; the f32 chain rounds once per MFMA)
 #pragma unroll
   for (int i = 0; i < RM; ++i)
@@ -389,6 +393,17 @@ __device__ __forceinline__ void mma_x6(const float (&a0)[RM][4], const float (&a
       acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[i], bh[j], acc[i][j], 0, 0, 0);
       acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
     }
+}
+
+template <int RM, int RN>
+__device__ __forceinline__ void mma_x6(const float (&a0)[RM][4], const float (&a1)[RM][4], const float (&b0)[RN][4],
+                                       const float (&b1)[RN][4], f32x16 (&acc)[RM][RN]) {
+  bf16x8 ah[RM], am[RM], al[RM], bh[RN], bm[RN], bl[RN];
+#pragma unroll
+  for (int i = 0; i < RM; ++i) split3(a0[i], a1[i], ah[i], am[i], al[i]);
+#pragma unroll
+  for (int j = 0; j < RN; ++j) split3(b0[j], b1[j], bh[j], bm[j], bl[j]);
+  mma_x6f<RM, RN>(ah, am, al, bh, bm, bl, acc);
 }
 
 // SCHED 2 (X6 math): one K-step as pairs of sub-step chunks, each pair one split-bf16 MFMA
@@ -411,6 +426,128 @@ __device__ __forceinline__ void kstep_x6(Loader<BM, BN, MODE, BK, C4, false, KG>
     mma_x6<T::RM, T::RN>(af[0], af[1], bf[0], bf[1], acc);
     if (gp == 0) ld.template load<LS>(a, k_load);
     if (gp == (NGK > 2 ? 2 : 0)) ld.template store<SS>(nxt, nxt + T::A_ELEMS);
+  }
+}
+
+// ---------------------------------------------------------------- X6S: split once, at the LDS store
+// SCHED 3: the register-staged tile is split into three bf16 planes as it is written to LDS
+// (once per element per block, instead of once per element per consuming wave), and the
+// fragment reads take bf16 directly: ds_read_b128 from K-contiguous planes [row][BK+8], and
+// for K-major operands two ds_read_b64_tr_b16 per plane from [k][rows+32] images (the
+// hardware transpose delivers 4 k-values of one row per lane; +32 pads make the 4 rows of a
+// 16-lane block and the two blocks of a 32-lane half hit 8 distinct 8-bank ranges).
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef short i16x4 __attribute__((ext_vector_type(4)));
+
+template <int BM, int BN, int MODE, int BK>
+struct TileXS {
+  using T = Tile<BM, BN, MODE, BK>;
+  static constexpr int PA = T::A_KC ? BK + 8 : BM + 32;  // plane pitch (bf16 elements)
+  static constexpr int PB = T::B_KC ? BK + 8 : BN + 32;
+  static constexpr int PLA = (T::A_KC ? BM : BK) * PA;  // one plane
+  static constexpr int PLB = (T::B_KC ? BN : BK) * PB;
+  static constexpr int A16 = 3 * PLA, STAGE16 = 3 * PLA + 3 * PLB;
+  static constexpr size_t BYTES = 2 * (size_t)STAGE16 * 2;  // double buffer
+};
+
+__device__ __forceinline__ void split4(const float4 v, bf16x4& h, bf16x4& m, bf16x4& l) {
+  const float x[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const __bf16 hj = (__bf16)x[j];
+    const float r = x[j] - (float)hj;
+    const __bf16 mj = (__bf16)r;
+    h[j] = hj;
+    m[j] = mj;
+    l[j] = (__bf16)(r - (float)mj);
+  }
+}
+
+// bf16 plane offset of this thread's register-staged chunk i (Loader's slot map q = tid + NT*i)
+template <int ROWS, bool KC, int P, int BK, int NT>
+__device__ __forceinline__ int xs_off(int i) {
+  const int q = threadIdx.x + NT * i;
+  if constexpr (KC) {
+    constexpr int KQ = BK / 4;
+    return (q / KQ) * P + 4 * (q % KQ);
+  } else {
+    constexpr int CPR = ROWS / 4;
+    const int kr = q / CPR;
+    return kr * P + 4 * (q - kr * CPR);
+  }
+}
+
+template <int BM, int BN, int MODE, int BK, bool C4, int KG, int S>
+__device__ __forceinline__ void store_xs(const Loader<BM, BN, MODE, BK, C4, false, KG>& ld, __bf16* As, __bf16* Bs,
+                                         const int (&oa)[Tile<BM, BN, MODE, BK, false, KG>::AC],
+                                         const int (&ob)[Tile<BM, BN, MODE, BK, false, KG>::BC]) {
+  using T = Tile<BM, BN, MODE, BK, false, KG>;  // chunk counts depend on the block's thread count
+  using X = TileXS<BM, BN, MODE, BK>;
+#pragma unroll
+  for (int i = 0; i < T::AC; ++i) {
+    bf16x4 h, m, l;
+    split4(ld.ra[S][i], h, m, l);
+    *reinterpret_cast<bf16x4*>(As + oa[i]) = h;
+    *reinterpret_cast<bf16x4*>(As + X::PLA + oa[i]) = m;
+    *reinterpret_cast<bf16x4*>(As + 2 * X::PLA + oa[i]) = l;
+  }
+#pragma unroll
+  for (int i = 0; i < T::BC; ++i) {
+    bf16x4 h, m, l;
+    split4(ld.rb[S][i], h, m, l);
+    *reinterpret_cast<bf16x4*>(Bs + ob[i]) = h;
+    *reinterpret_cast<bf16x4*>(Bs + X::PLB + ob[i]) = m;
+    *reinterpret_cast<bf16x4*>(Bs + 2 * X::PLB + ob[i]) = l;
+  }
+}
+
+// 32x32x16 fragments (element j <-> k = (BK/2)*hh + 4*g0 + j) of R 32-row groups from one plane
+template <int R, bool KC, int P, int BK>
+__device__ __forceinline__ void read_xs(const __bf16* pl, int base, int g0, int lane, bf16x8 (&f)[R]) {
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    if constexpr (KC) {
+      const int row = base + i * 32 + (lane & 31);
+      f[i] = *reinterpret_cast<const bf16x8*>(pl + row * P + (BK / 2) * (lane >> 5) + 4 * g0);
+    } else {
+      const int grp = lane >> 4, l16 = lane & 15;
+      const int col = base + i * 32 + 16 * (grp & 1) + 4 * (l16 & 3);
+      const int kr = (BK / 2) * (grp >> 1) + 4 * g0 + (l16 >> 2);
+      const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (__attribute__((address_space(3))) i16x4*)(pl + kr * P + col));
+      const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (__attribute__((address_space(3))) i16x4*)(pl + (kr + 4) * P + col));
+      const bf16x4 blo = __builtin_bit_cast(bf16x4, lo), bhi = __builtin_bit_cast(bf16x4, hi);
+      f[i] = __builtin_shufflevector(blo, bhi, 0, 1, 2, 3, 4, 5, 6, 7);
+    }
+  }
+}
+
+template <int BM, int BN, int MODE, int BK, int LS, int SS, bool C4, int KG>
+__device__ __forceinline__ void kstep_xs(Loader<BM, BN, MODE, BK, C4, false, KG>& ld, const CsConvArgs& a,
+                                         const __bf16* cur, __bf16* nxt,
+                                         f32x16 (&acc)[Tile<BM, BN, MODE, BK>::RM][Tile<BM, BN, MODE, BK>::RN],
+                                         int wm, int wn, int kg, int k_load,
+                                         const int (&oa)[Tile<BM, BN, MODE, BK, false, KG>::AC],
+                                         const int (&ob)[Tile<BM, BN, MODE, BK, false, KG>::BC]) {
+  using T = Tile<BM, BN, MODE, BK>;
+  using X = TileXS<BM, BN, MODE, BK>;
+  constexpr int NGK = T::NG / KG;
+  static_assert(NGK >= 2 && NGK % 2 == 0, "X6 math needs pairs of sub-step chunks per K-group");
+  const int g0 = kg * NGK, lane = threadIdx.x & 63;
+  const __bf16* Bc = cur + X::A16;
+#pragma unroll
+  for (int gp = 0; gp < NGK; gp += 2) {
+    bf16x8 ah[T::RM], am[T::RM], al[T::RM], bh[T::RN], bm[T::RN], bl[T::RN];
+    read_xs<T::RM, T::A_KC, X::PA, BK>(cur, wm * T::WM, g0 + gp, lane, ah);
+    read_xs<T::RM, T::A_KC, X::PA, BK>(cur + X::PLA, wm * T::WM, g0 + gp, lane, am);
+    read_xs<T::RM, T::A_KC, X::PA, BK>(cur + 2 * X::PLA, wm * T::WM, g0 + gp, lane, al);
+    read_xs<T::RN, T::B_KC, X::PB, BK>(Bc, wn * T::WN, g0 + gp, lane, bh);
+    read_xs<T::RN, T::B_KC, X::PB, BK>(Bc + X::PLB, wn * T::WN, g0 + gp, lane, bm);
+    read_xs<T::RN, T::B_KC, X::PB, BK>(Bc + 2 * X::PLB, wn * T::WN, g0 + gp, lane, bl);
+    mma_x6f<T::RM, T::RN>(ah, am, al, bh, bm, bl, acc);
+    if (gp == 0) ld.template load<LS>(a, k_load);
+    if (gp == (NGK > 2 ? 2 : 0)) store_xs<BM, BN, MODE, BK, C4, KG, SS>(ld, nxt, nxt + X::A16, oa, ob);
   }
 }
 
@@ -669,6 +806,31 @@ __device__ __forceinline__ void gemm_body(const CsConvArgs& a, const int tile, c
       cur = cur == NB - 1 ? 0 : cur + 1;
     }
     __syncthreads();  // every wave's fragment reads are done before the epilogue reuses LDS
+  } else if constexpr (SCHED == 3) {
+    using X = TileXS<BM, BN, MODE, BK>;
+    Loader<BM, BN, MODE, BK, C4, false, KG> ld;
+    ld.init(a, m0, n0);
+    using TK = Tile<BM, BN, MODE, BK, false, KG>;
+    int oa[TK::AC], ob[TK::BC];
+#pragma unroll
+    for (int i = 0; i < TK::AC; ++i) oa[i] = xs_off<BM, T::A_KC, X::PA, BK, TK::NT>(i);
+#pragma unroll
+    for (int i = 0; i < TK::BC; ++i) ob[i] = xs_off<BN, T::B_KC, X::PB, BK, TK::NT>(i);
+    __bf16* l0 = reinterpret_cast<__bf16*>(smem);
+    __bf16* l1 = l0 + X::STAGE16;
+    if (nks > 0) {
+      ld.template load<0>(a, ks_begin * BK);
+      if (nks > 1) ld.template load<1>(a, (ks_begin + 1) * BK);
+      store_xs<BM, BN, MODE, BK, C4, KG, 0>(ld, l0, l0 + X::A16, oa, ob);
+    }
+    __syncthreads();
+    for (int t = 0; t < nks; t += 2) {
+      kstep_xs<BM, BN, MODE, BK, 0, 1, C4, KG>(ld, a, l0, l1, acc, wm, wn, kg, (ks_begin + t + 2) * BK, oa, ob);
+      __syncthreads();
+      if (t + 1 >= nks) break;
+      kstep_xs<BM, BN, MODE, BK, 1, 0, C4, KG>(ld, a, l1, l0, acc, wm, wn, kg, (ks_begin + t + 3) * BK, oa, ob);
+      __syncthreads();
+    }
   } else {
   Loader<BM, BN, MODE, BK, C4, false, KG> ld;
   ld.init(a, m0, n0);
@@ -986,20 +1148,21 @@ hipError_t launch_k(dim3 grid, size_t lds, hipStream_t stream, const CsConvArgs&
   return hipGetLastError();
 }
 
-// MATH 0: f32 MFMA (register staging honours CS_CONV_SCHED); MATH 2: X6 split-bf16 kernels
+// MATH 0: f32 MFMA (register staging honours CS_CONV_SCHED); MATH 2: X6 split-bf16 kernels;
+// MATH 3: X6 split at the LDS store (register staging only)
 template <int BM, int BN, int MODE, int BK, int MATH>
 hipError_t launch_gemm_m(const CsConvArgs& a, int splits, int stage, hipStream_t stream) {
   using T = Tile<BM, BN, MODE, BK>;
   using TG = Tile<BM, BN, MODE, BK, true>;
   const int ntiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
-  const size_t lds = 2 * T::STAGE * sizeof(float);
+  const size_t lds = MATH == 3 ? TileXS<BM, BN, MODE, BK>::BYTES : 2 * T::STAGE * sizeof(float);
   const dim3 grid(ntiles, 1, splits);
   constexpr bool deep_fits = (BM + BN) * BK * 4 * 5 < 160 * 1024;
   if constexpr (BK != 64 && MATH == 0) {
     if (MODE == CS_CONV_FWD && a.w_oihw)  // padded conv0: Cin = 4 < BK
       return launch_k<BM, BN, MODE, BK, 0, true, 0>(grid, lds, stream, a);
   }
-  if constexpr (BK == 32) {
+  if constexpr (BK == 32 && MATH != 3) {
     if (stage == CS_STAGE_LDS_DMA)
       return launch_k<BM, BN, MODE, BK, MATH, false, 3>(grid, 3 * TG::STAGE * sizeof(float), stream, a);
     if constexpr (deep_fits) {
@@ -1008,21 +1171,23 @@ hipError_t launch_gemm_m(const CsConvArgs& a, int splits, int stage, hipStream_t
     }
   }
   // K-groups: the LDS tile ring must also hold the (KG-1) partial-accumulator images
-  if constexpr (BK >= 32 && BM * BK >= 2048 && BN * BK >= 2048) {
+  if constexpr (BK >= 32 && BM * BK >= 2048 && BN * BK >= 2048 && (MATH != 3 || BK == 32 || (BM == 64 && BN == 64))) {
     if (stage == CS_STAGE_KG2) {
       const size_t red = (size_t)1 * 4 * (BM / 64) * (BN / 64) * 16 * 64 * sizeof(float);
       return launch_k<BM, BN, MODE, BK, MATH, false, 0, 2>(grid, std::max(lds, red), stream, a);
     }
   }
-  if constexpr (BK == 64 && BM * BK >= 4096 && BN * BK >= 4096) {
+  if constexpr (BK == 64 && BM * BK >= 4096 && BN * BK >= 4096 && (MATH != 3 || (BM == 64 && BN == 64))) {
     if (stage == CS_STAGE_KG4) {
       const size_t red = (size_t)3 * 4 * (BM / 64) * (BN / 64) * 16 * 64 * sizeof(float);
       return launch_k<BM, BN, MODE, BK, MATH, false, 0, 4>(grid, std::max(lds, red), stream, a);
     }
   }
   if (stage != CS_STAGE_REGS) return hipErrorInvalidValue;
-  if constexpr (MATH == 2) {
-    return launch_k<BM, BN, MODE, BK, 2, false, 0>(grid, lds, stream, a);
+  if constexpr (MATH == 3 && BK == 64 && !(BM == 64 && BN == 64)) {
+    return hipErrorInvalidValue;  // bf16 planes of a wider bk-64 tile exceed the 160 KiB LDS
+  } else if constexpr (MATH >= 2) {
+    return launch_k<BM, BN, MODE, BK, MATH, false, 0>(grid, lds, stream, a);
   } else {
     if (conv_sched() == 1) return launch_k<BM, BN, MODE, BK, 1, false, 0>(grid, lds, stream, a);
     return launch_k<BM, BN, MODE, BK, 0, false, 0>(grid, lds, stream, a);
@@ -1031,6 +1196,7 @@ hipError_t launch_gemm_m(const CsConvArgs& a, int splits, int stage, hipStream_t
 
 template <int BM, int BN, int MODE, int BK>
 hipError_t launch_gemm(const CsConvArgs& a, int splits, int stage, hipStream_t stream) {
+  if (stage & CS_STAGE_X6S) return launch_gemm_m<BM, BN, MODE, BK, 3>(a, splits, stage & ~CS_STAGE_X6S, stream);
   if (stage & CS_STAGE_X6) return launch_gemm_m<BM, BN, MODE, BK, 2>(a, splits, stage & ~CS_STAGE_X6, stream);
   return launch_gemm_m<BM, BN, MODE, BK, 0>(a, splits, stage, stream);
 }
@@ -1045,7 +1211,8 @@ hipError_t launch_gemm(const CsConvArgs& a, int splits, int stage, hipStream_t s
   CS_K(BM_, BN_, MODE_, 32, 0, false, 0) CS_K(BM_, BN_, MODE_, 32, 1, false, 0) \
   CS_K(BM_, BN_, MODE_, 32, 0, false, 3)                                      \
   CS_K(BM_, BN_, MODE_, 16, 2, false, 0) CS_K(BM_, BN_, MODE_, 32, 2, false, 0) \
-  CS_K(BM_, BN_, MODE_, 32, 2, false, 3)
+  CS_K(BM_, BN_, MODE_, 32, 2, false, 3)                                      \
+  CS_K(BM_, BN_, MODE_, 16, 3, false, 0) CS_K(BM_, BN_, MODE_, 32, 3, false, 0)
 #define CS_TILE(BM_, BN_)                                                                       \
   CS_MODE(BM_, BN_, CS_CONV_FWD) CS_MODE(BM_, BN_, CS_CONV_DGRAD) CS_MODE(BM_, BN_, CS_CONV_WGRAD) \
   CS_K(BM_, BN_, CS_CONV_FWD, 16, 0, true, 0) CS_K(BM_, BN_, CS_CONV_FWD, 32, 0, true, 0)
@@ -1059,6 +1226,9 @@ CS_TILE(128, 128)
 CS_TILE64(64, 64)
 CS_TILE64(128, 64)
 CS_TILE64(64, 128)
+CS_K(64, 64, CS_CONV_FWD, 64, 3, false, 0)
+CS_K(64, 64, CS_CONV_DGRAD, 64, 3, false, 0)
+CS_K(64, 64, CS_CONV_WGRAD, 64, 3, false, 0)
 #undef CS_TILE64
 #undef CS_BK64
 #define CS_KG1(BM_, BN_, BK_, KG_, M_)                                                            \
@@ -1070,6 +1240,12 @@ CS_KG(64, 64, 32, 2)
 CS_KG(128, 64, 32, 2)
 CS_KG(64, 128, 32, 2)
 CS_KG(128, 128, 32, 2)
+CS_KG1(64, 64, 32, 2, 3)
+CS_KG1(128, 64, 32, 2, 3)
+CS_KG1(64, 128, 32, 2, 3)
+CS_KG1(128, 128, 32, 2, 3)
+CS_KG1(64, 64, 64, 2, 3)
+CS_KG1(64, 64, 64, 4, 3)
 CS_KG(64, 64, 64, 2)
 CS_KG(128, 64, 64, 2)
 CS_KG(64, 128, 64, 2)
@@ -1127,9 +1303,15 @@ void cs_conv_fill_dims(CsConvArgs* a, int mode) {
 }
 
 bool cs_conv_stage_ok(int stage, int bm, int bn, int bk, bool conv0_fwd) {
+  if ((stage & CS_STAGE_X6) && (stage & CS_STAGE_X6S)) return false;
   if (stage & CS_STAGE_X6) {  // split-bf16 math: every staging, except the padded conv0 forward
     if (conv0_fwd) return false;
     stage &= ~CS_STAGE_X6;
+  }
+  if (stage & CS_STAGE_X6S) {  // split at the LDS store: register staging, bf16 planes within 160 KiB
+    stage &= ~CS_STAGE_X6S;
+    if (conv0_fwd || (stage != CS_STAGE_REGS && stage != CS_STAGE_KG2 && stage != CS_STAGE_KG4)) return false;
+    if (bk == 64 && !(bm == 64 && bn == 64)) return false;
   }
   if (conv0_fwd && stage != CS_STAGE_REGS) return false;
   switch (stage) {

@@ -63,8 +63,10 @@ void cs_conv_fill_dims(CsConvArgs* a, int mode);
 // CS_STAGE_KG2 / KG4: register staging with 2 / 4 K-groups of 4 waves per block (bk >= 32 / 64)
 // | CS_STAGE_X6: the same staging with fp32-accurate split-bf16 math (3 bf16 pieces per
 // operand, 6 v_mfma_f32_32x32x16_bf16 per 32x32x16 product; conv_gemm.hip "X6")
+// | CS_STAGE_X6S: X6 math with the split done once at the LDS store into bf16 planes (register
+// staging / K-groups only; bk 64 only with 64x64 tiles)
 enum { CS_STAGE_REGS = 0, CS_STAGE_LDS_DMA = 1, CS_STAGE_LDS_DMA_DEEP = 2, CS_STAGE_KG2 = 3, CS_STAGE_KG4 = 4,
-       CS_STAGE_X6 = 8 };
+       CS_STAGE_X6 = 8, CS_STAGE_X6S = 16 };
 // whether a (stage, tile, bk) combination has a kernel
 bool cs_conv_stage_ok(int stage, int bm, int bn, int bk, bool conv0_fwd);
 hipError_t cs_conv_gemm(CsConvArgs a, int mode, int bm, int bn, int bk, int splits, hipStream_t stream,

@@ -517,10 +517,12 @@ std::vector<double> VggEngine::autotune(int64_t B, int64_t iters) {
       const bool conv0_fwd = l == 0 && mode == CS_CONV_FWD && blocks_[0].cin == 4;
       for (int stage : {(int)CS_STAGE_REGS, (int)CS_STAGE_LDS_DMA, (int)CS_STAGE_LDS_DMA_DEEP, (int)CS_STAGE_KG2,
                         (int)CS_STAGE_KG4, CS_STAGE_X6 | CS_STAGE_REGS, CS_STAGE_X6 | CS_STAGE_LDS_DMA,
-                        CS_STAGE_X6 | CS_STAGE_LDS_DMA_DEEP, CS_STAGE_X6 | CS_STAGE_KG2, CS_STAGE_X6 | CS_STAGE_KG4})
+                        CS_STAGE_X6 | CS_STAGE_LDS_DMA_DEEP, CS_STAGE_X6 | CS_STAGE_KG2, CS_STAGE_X6 | CS_STAGE_KG4,
+                        CS_STAGE_X6S | CS_STAGE_REGS, CS_STAGE_X6S | CS_STAGE_KG2, CS_STAGE_X6S | CS_STAGE_KG4})
       for (int bk : {16, 32, 64}) {
         // CS_CONV_MATH: 0 = f32 MFMA kernels only, 1 = split-bf16 (X6) only, 2 = both (default)
-        if (((stage & CS_STAGE_X6) && math_ == 0) || (!(stage & CS_STAGE_X6) && math_ == 1)) continue;
+        const bool x6 = (stage & (CS_STAGE_X6 | CS_STAGE_X6S)) != 0;
+        if ((x6 && math_ == 0) || (!x6 && math_ == 1)) continue;
         if (bk == 64 && conv0_fwd) continue;
         const int64_t ks = cdiv(d.K, bk);
         for (int bm : {64, 128}) {

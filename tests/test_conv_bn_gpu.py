@@ -31,9 +31,11 @@ TILES = [(64, 64, 1, 16), (128, 64, 1, 16), (64, 128, 3, 16), (128, 128, 2, 16),
 # (in-launch split-K combine, operand staging): 0 = registers + ds_write, 1/2 = LDS-DMA ring of
 # depth 3/5 (bk 32 only)
 # 3/4 = register staging with 2/4 K-groups of waves per block
-# +8 = the same staging with the fp32-accurate split-bf16 (X6) math: held to the same f64 tolerance
+# +8 = the same staging with the fp32-accurate split-bf16 (X6) math, +16 = X6 split once at the LDS
+# store (bf16 planes, transposed LDS reads for K-major operands): held to the same f64 tolerance
 VARIANTS = [(False, 0), (True, 0), (False, 1), (True, 1), (False, 2), (False, 3), (False, 4),
-            (False, 8), (True, 8), (False, 9), (False, 10), (False, 11), (False, 12)]
+            (False, 8), (True, 8), (False, 9), (False, 10), (False, 11), (False, 12),
+            (False, 16), (True, 16), (False, 19), (False, 20)]
 
 
 def _skip_stage(stage, bk, bm, bn, conv0_fwd=False):
