@@ -213,6 +213,13 @@ class NativeTrainer:
             self.comm.broadcast(self.nbt, 0)
         self.native_comm = getattr(self.comm, "native", None)
         self.bucket_lows, self.bucket_ranges = lay.plan_buckets(bucket_mb if sync == "ddp" else 1e9)
+        at = 0
+        for off, n in self.bucket_ranges:  # buckets tile the flat buffer (per-bucket SGD relies on it)
+            assert off == at, "bucket plan must tile the flat parameter buffer"
+            at += n
+        assert at == lay.total, "bucket plan must cover the flat parameter buffer"
+        # opt-in (CS_SGD_OVERLAP=1): per-bucket SGD on the engine's optimizer stream (see vgg_engine.h)
+        self.sgd_overlap = os.environ.get("CS_SGD_OVERLAP", "0") != "0"
         self.flat_sync = FlatGradSync(self.sync_mode if self.sync_mode != "ddp" else "none", self.comm,
                                       lay.param_ranges(), lay.total) if self.comm is not None else None
 
@@ -358,6 +365,10 @@ class NativeTrainer:
             early = self.native_comm is not None and self.broadcast_buffers
             if not early:
                 self._pre_forward_sync()
+            # native comm: each bucket's SGD runs on the engine's optimizer stream once its
+            # all-reduce is in (and its weights' last reader, the bucket's lowest dgrad, is
+            # done), overlapping the backward of the blocks below
+            sgd_overlap = self.native_comm is not None and self.sgd_overlap
             handles = []
             for k in range(nseg):
                 if graphs is not None:
@@ -368,8 +379,15 @@ class NativeTrainer:
                 if early and k == 0:
                     self.native_comm.broadcast(self.bufs, 0)
                     self.native_comm.broadcast(self.nbt, 0)
+                if sgd_overlap:
+                    off, n = self.bucket_ranges[k]
+                    self.engine.sgd_bucket(self.native_comm, self.bucket_lows[k], off, n, self.lr, self.momentum,
+                                           self.wd, self.damp, k == nseg - 1)
             for h in handles:
                 h.wait()
+            if sgd_overlap:
+                self.engine.join_opt()
+                return
         else:
             for k in range(nseg):
                 if graphs is not None:

@@ -152,6 +152,11 @@ void register_runtime(pybind11::module& m) {
            py::arg("bucket_ranges"), py::arg("broadcast_buffers"), py::arg("lr"), py::arg("momentum"),
            py::arg("wd"), py::arg("dampening"))
       .def("set_overlap_wgrad", &cs::VggEngine::set_overlap_wgrad)
+      .def("set_sgd_overlap", &cs::VggEngine::set_sgd_overlap)
+      .def("join_opt", &cs::VggEngine::join_opt)
+      .def("sgd_bucket", &cs::VggEngine::sgd_bucket, py::arg("comm").none(true), py::arg("lo_block"), py::arg("off"),
+           py::arg("n"), py::arg("lr"), py::arg("momentum"), py::arg("wd"), py::arg("dampening"),
+           py::arg("advance_cursor"))
       .def("set_fixup", &cs::VggEngine::set_fixup)
       .def("set_dual", &cs::VggEngine::set_dual)
       .def("set_bn_fused_rows", &cs::VggEngine::set_bn_fused_rows)

@@ -997,16 +997,16 @@ __global__ __launch_bounds__(256 * KG) void conv_gemm_kernel(CsConvArgs a) {
 // Horizontal fusion of one block's two independent backward GEMMs: blocks [0, nb1) run the
 // weight gradient (64x64 tiles, K-step BK1, s1 splits), the rest the data gradient (64x64,
 // BK2, s2 splits) — one launch, one ramp and one tail instead of two.
-template <int BK1, int BK2>
-__global__ __launch_bounds__(256) void conv_dual_kernel(CsConvArgs wg, CsConvArgs dg, int nb1, int s1, int s2) {
+template <int BK1, int BK2, int SCHED = 0, int KG = 1>
+__global__ __launch_bounds__(256 * KG) void conv_dual_kernel(CsConvArgs wg, CsConvArgs dg, int nb1, int s1, int s2) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int b = blockIdx.x;
   if (b < nb1) {
     const int nt = ((wg.M + 63) / 64) * ((wg.N + 63) / 64);
-    gemm_body<64, 64, CS_CONV_WGRAD, BK1, 0, false, 0>(wg, cs::xcd_remap(b % nt, nt), b / nt, s1, smem);
+    gemm_body<64, 64, CS_CONV_WGRAD, BK1, SCHED, false, 0, KG>(wg, cs::xcd_remap(b % nt, nt), b / nt, s1, smem);
   } else {
     const int nt = ((dg.M + 63) / 64) * ((dg.N + 63) / 64), c = b - nb1;
-    gemm_body<64, 64, CS_CONV_DGRAD, BK2, 0, false, 0>(dg, cs::xcd_remap(c % nt, nt), c / nt, s2, smem);
+    gemm_body<64, 64, CS_CONV_DGRAD, BK2, SCHED, false, 0, KG>(dg, cs::xcd_remap(c % nt, nt), c / nt, s2, smem);
   }
 }
 
@@ -1267,6 +1267,9 @@ template __global__ void conv_dual_kernel<16, 16>(CsConvArgs, CsConvArgs, int, i
 template __global__ void conv_dual_kernel<16, 32>(CsConvArgs, CsConvArgs, int, int, int);
 template __global__ void conv_dual_kernel<32, 16>(CsConvArgs, CsConvArgs, int, int, int);
 template __global__ void conv_dual_kernel<32, 32>(CsConvArgs, CsConvArgs, int, int, int);
+template __global__ void conv_dual_kernel<64, 64, 3, 4>(CsConvArgs, CsConvArgs, int, int, int);
+template __global__ void conv_dual_kernel<64, 64, 3, 2>(CsConvArgs, CsConvArgs, int, int, int);
+template __global__ void conv_dual_kernel<16, 16, 3, 1>(CsConvArgs, CsConvArgs, int, int, int);
 #undef CS_TILE
 #undef CS_MODE
 #undef CS_K
@@ -1360,7 +1363,7 @@ int prep_gemm(CsConvArgs& a, int mode, int bk, int splits) {
 }  // namespace
 
 hipError_t cs_conv_gemm_dual(CsConvArgs wg, int wbk, int wsplits, CsConvArgs dg, int dbk, int dsplits,
-                             hipStream_t stream) {
+                             hipStream_t stream, int stage) {
   if (wg.w_oihw) return hipErrorInvalidValue;  // conv0 has no data gradient
   wg.counters = dg.counters = nullptr;
   const int s1 = prep_gemm(wg, CS_CONV_WGRAD, wbk, wsplits), s2 = prep_gemm(dg, CS_CONV_DGRAD, dbk, dsplits);
@@ -1370,14 +1373,32 @@ hipError_t cs_conv_gemm_dual(CsConvArgs wg, int wbk, int wsplits, CsConvArgs dg,
   const int nb1 = nt1 * s1, nb = nb1 + nt2 * s2;
   const size_t lds = 2 * (size_t)std::max(Tile<64, 64, CS_CONV_WGRAD, 32>::STAGE, Tile<64, 64, CS_CONV_DGRAD, 32>::STAGE) *
                      sizeof(float);
+  if (stage == CS_STAGE_REGS) {
 #define CS_DUAL(B1, B2)                                                                                      \
   if (wbk == B1 && dbk == B2)                                                                                \
     hipLaunchKernelGGL((conv_dual_kernel<B1, B2>), dim3(nb), dim3(256), lds, stream, wg, dg, nb1, s1, s2);
-  CS_DUAL(16, 16)
-  CS_DUAL(16, 32)
-  CS_DUAL(32, 16)
-  CS_DUAL(32, 32)
+    CS_DUAL(16, 16)
+    CS_DUAL(16, 32)
+    CS_DUAL(32, 16)
+    CS_DUAL(32, 32)
 #undef CS_DUAL
+  } else {
+    // split-bf16 planes (X6S), both halves with the same K-step and K-group count
+    const size_t xs = std::max(TileXS<64, 64, CS_CONV_WGRAD, 64>::BYTES, TileXS<64, 64, CS_CONV_DGRAD, 64>::BYTES);
+    const size_t red = (size_t)3 * 4 * 16 * 64 * sizeof(float);
+    if (wbk != dbk) return hipErrorInvalidValue;
+    if (stage == (CS_STAGE_X6S | CS_STAGE_KG4) && wbk == 64)
+      hipLaunchKernelGGL((conv_dual_kernel<64, 64, 3, 4>), dim3(nb), dim3(1024), std::max(xs, red), stream, wg, dg,
+                         nb1, s1, s2);
+    else if (stage == (CS_STAGE_X6S | CS_STAGE_KG2) && wbk == 64)
+      hipLaunchKernelGGL((conv_dual_kernel<64, 64, 3, 2>), dim3(nb), dim3(512), xs, stream, wg, dg, nb1, s1, s2);
+    else if (stage == (CS_STAGE_X6S | CS_STAGE_REGS) && wbk == 16)
+      hipLaunchKernelGGL((conv_dual_kernel<16, 16, 3, 1>), dim3(nb), dim3(256),
+                         std::max(TileXS<64, 64, CS_CONV_WGRAD, 16>::BYTES, TileXS<64, 64, CS_CONV_DGRAD, 16>::BYTES),
+                         stream, wg, dg, nb1, s1, s2);
+    else
+      return hipErrorInvalidValue;
+  }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || (s1 == 1 && s2 == 1)) return e;
   if (s1 > 1 && s2 > 1) {

@@ -74,8 +74,17 @@ hipError_t cs_conv_gemm(CsConvArgs a, int mode, int bm, int bn, int bk, int spli
 // one launch for a block's weight gradient (wg) and data gradient (dg), both 64x64 tiles with
 // register staging (K-steps wbk / dbk in {16, 32}); split-K slabs combined by one launch
 // (their workspaces must differ)
+// stage CS_STAGE_REGS (f32, bk 16/32 each), or an X6S stage shared by both halves:
+// X6S|KG4 and X6S|KG2 with bk 64, X6S|REGS with bk 16
 hipError_t cs_conv_gemm_dual(CsConvArgs wg, int wbk, int wsplits, CsConvArgs dg, int dbk, int dsplits,
-                             hipStream_t stream);
+                             hipStream_t stream, int stage = CS_STAGE_REGS);
+inline bool cs_conv_dual_ok(int wstage, int wbk, int dstage, int dbk) {
+  if (wstage != dstage) return false;
+  if (wstage == CS_STAGE_REGS) return (wbk == 16 || wbk == 32) && (dbk == 16 || dbk == 32);
+  if (wbk != dbk) return false;
+  return ((wstage == (CS_STAGE_X6S | CS_STAGE_KG4) || wstage == (CS_STAGE_X6S | CS_STAGE_KG2)) && wbk == 64) ||
+         (wstage == (CS_STAGE_X6S | CS_STAGE_REGS) && wbk == 16);
+}
 // the split count cs_conv_gemm actually launches (K-steps re-balanced over splits)
 int cs_conv_effective_splits(int K, int bk, int splits);
 // split-K slabs of one tile a single block combines in-launch (S * BM * BN * 4 bytes)

@@ -157,6 +157,10 @@ VggEngine::VggEngine(int64_t Bmax, std::vector<int64_t> desc, std::vector<int64_
   ws_ = torch::zeros({ws_elems_}, fo);
   ws_side_ = torch::zeros({ws_elems_}, fo);
   ok(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking), "side stream");
+  ok(hipStreamCreateWithFlags(&opt_, hipStreamNonBlocking), "optimizer stream");
+  ev_opt_.resize(64);
+  for (auto& e : ev_opt_) ok(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event");
+  if (const char* e = getenv("CS_SGD_OVERLAP")) sgd_overlap_ = atoi(e) != 0;
   ev_bn_.resize(L);
   ev_wg_.resize(L);
   for (int64_t l = 0; l < L; ++l) {
@@ -277,8 +281,7 @@ bool VggEngine::dual_ok(int l) const {
   if (!dual_ || l == 0 || !blocks_[l].use_dual) return false;
   const ConvTile& w = blocks_[l].tile[CS_CONV_WGRAD];
   const ConvTile& d = blocks_[l].tile[CS_CONV_DGRAD];
-  return w.bm == 64 && w.bn == 64 && w.stage == CS_STAGE_REGS && d.bm == 64 && d.bn == 64 &&
-         d.stage == CS_STAGE_REGS;
+  return w.bm == 64 && w.bn == 64 && d.bm == 64 && d.bn == 64 && cs_conv_dual_ok(w.stage, w.bk, d.stage, d.bk);
 }
 
 void VggEngine::conv_dual(int l, int B, hipStream_t s, float* dz) {
@@ -286,7 +289,7 @@ void VggEngine::conv_dual(int l, int B, hipStream_t s, float* dz) {
   const ConvTile& d = blocks_[l].tile[CS_CONV_DGRAD];
   CsConvArgs wa = conv_args(l, CS_CONV_WGRAD, B, false, ws_side_.data_ptr<float>(), dz);
   CsConvArgs da = conv_args(l, CS_CONV_DGRAD, B, false, nullptr, dz);
-  ok(cs_conv_gemm_dual(wa, w.bk, w.splits, da, d.bk, d.splits, s), "conv_gemm_dual");
+  ok(cs_conv_gemm_dual(wa, w.bk, w.splits, da, d.bk, d.splits, s, w.stage), "conv_gemm_dual");
 }
 
 void VggEngine::forward_train(int64_t B) {
@@ -387,6 +390,11 @@ VggEngine::~VggEngine() {
     hipStreamSynchronize(side_);
     hipStreamDestroy(side_);
   }
+  if (opt_ != nullptr) {
+    hipStreamSynchronize(opt_);
+    hipStreamDestroy(opt_);
+  }
+  for (auto e : ev_opt_) hipEventDestroy(e);
   for (auto e : ev_bn_) hipEventDestroy(e);
   for (auto e : ev_wg_) hipEventDestroy(e);
 }
@@ -399,6 +407,35 @@ void VggEngine::sgd(double lr, double momentum, double wd, double dampening, int
   ok(cs_sgd_flat(P(off), G(off), mom_.data_ptr<float>() + off, n, (float)lr, (float)momentum, (float)wd,
                  (float)dampening, 1.0f, 0, cur_stream(), perm_len_ > 0 ? cursor_.data_ptr<int64_t>() : nullptr),
      "sgd_flat");
+}
+
+hipEvent_t VggEngine::opt_event() { return ev_opt_[next_opt_ev_++ % ev_opt_.size()]; }
+
+void VggEngine::sgd_bucket(RcclComm* comm, int64_t lo_block, int64_t off, int64_t n, double lr, double momentum,
+                           double wd, double dampening, bool advance_cursor) {
+  TORCH_CHECK(off >= 0 && n >= 0 && off + n <= params_.numel(), "sgd_bucket: range");
+  TORCH_CHECK(lo_block >= 0 && lo_block < (int64_t)blocks_.size(), "sgd_bucket: block");
+  hipStream_t s = cur_stream();
+  hipEvent_t e = opt_event();
+  ok(hipEventRecord(e, s), "record main");
+  ok(hipStreamWaitEvent(opt_, e, 0), "opt wait main");
+  if (overlap_wgrad_) ok(hipStreamWaitEvent(opt_, ev_wg_[lo_block], 0), "opt wait wgrad");
+  if (comm != nullptr && comm->world() > 1) {
+    hipEvent_t c = opt_event();
+    ok(hipEventRecord(c, comm->stream()), "record comm");
+    ok(hipStreamWaitEvent(opt_, c, 0), "opt wait comm");
+  }
+  if (n == 0) return;
+  ok(cs_sgd_flat(P(off), G(off), mom_.data_ptr<float>() + off, n, (float)lr, (float)momentum, (float)wd,
+                 (float)dampening, 1.0f, 0, opt_,
+                 advance_cursor && perm_len_ > 0 ? cursor_.data_ptr<int64_t>() : nullptr),
+     "sgd_flat(bucket)");
+}
+
+void VggEngine::join_opt() {
+  hipEvent_t e = opt_event();
+  ok(hipEventRecord(e, opt_), "record opt");
+  ok(hipStreamWaitEvent(cur_stream(), e, 0), "join opt");
 }
 
 void VggEngine::forward_eval(int64_t B) {
@@ -442,6 +479,13 @@ void VggEngine::step(int64_t B, RcclComm* comm, const std::vector<int64_t>& buck
     comm->join(s);
   }
   forward_train(B);
+  // per-bucket SGD needs the buckets to tile the flat buffer exactly
+  bool tiled = sgd_overlap_;
+  for (size_t k = 0, at = 0; k < nb && tiled; ++k) {
+    tiled = bucket_ranges[2 * k] == (int64_t)at;
+    at += bucket_ranges[2 * k + 1];
+    if (k + 1 == nb) tiled = tiled && (int64_t)at == params_.numel();
+  }
   int64_t hi = L - 1;
   for (size_t k = 0; k < nb; ++k) {
     const int64_t lo = bucket_blocks[k];
@@ -453,10 +497,15 @@ void VggEngine::step(int64_t B, RcclComm* comm, const std::vector<int64_t>& buck
     if (comm != nullptr && comm->world() > 1)
       comm->all_reduce(G(bucket_ranges[2 * k]), bucket_ranges[2 * k + 1], ncclFloat32, ncclAvg,
                        overlap_wgrad_ ? side_ : s);
+    // ... and its SGD can run as soon as the averaged gradient is in and block lo's data
+    // gradient (the last reader of these weights) is done, beside the backward below
+    if (tiled)
+      sgd_bucket(comm, lo, bucket_ranges[2 * k], bucket_ranges[2 * k + 1], lr, momentum, wd, dampening, k + 1 == nb);
   }
   if (overlap_wgrad_) ok(hipStreamWaitEvent(s, ev_wg_[0], 0), "join side");
   if (comm != nullptr && comm->world() > 1) comm->join(s);
-  sgd(lr, momentum, wd, dampening, 0, params_.numel());
+  if (tiled) join_opt();
+  else sgd(lr, momentum, wd, dampening, 0, params_.numel());
 }
 
 void VggEngine::set_tile(int64_t block, int64_t mode, int64_t bm, int64_t bn, int64_t splits, int64_t bk,
@@ -556,6 +605,7 @@ std::vector<double> VggEngine::autotune(int64_t B, int64_t iters) {
               if (bm == 64 && bn == 64 && stage == CS_STAGE_REGS && us < best64_t[mode]) {
                 best64_t[mode] = us;
                 best64[mode] = t;
+                best64[mode].us = us;
               }
             }
           }
@@ -565,37 +615,50 @@ std::vector<double> VggEngine::autotune(int64_t B, int64_t iters) {
       blocks_[l].tile[mode] = best;
       best_us.push_back(best_t);
     }
-    // joint choice for the backward pair: the dual launch with the best 64x64 register-staged
-    // wgrad / dgrad tiles, or the two separately tuned launches, whichever is faster
+    // joint choice for the backward pair: one dual launch (wgrad + dgrad blocks in one grid)
+    // with the separately tuned tiles when they are dual-compatible (64x64, same staging), or
+    // with the best 64x64 f32 register-staged tiles, or the two separate launches — fastest wins
     VggBlock& b = blocks_[l];
     b.use_dual = false;
-    if (dual_ && l > 0 && best64_t[CS_CONV_WGRAD] < 1e29f && best64_t[CS_CONV_DGRAD] < 1e29f) {
+    if (dual_ && l > 0) {
       const ConvTile keep_w = b.tile[CS_CONV_WGRAD], keep_d = b.tile[CS_CONV_DGRAD];
-      b.tile[CS_CONV_WGRAD] = best64[CS_CONV_WGRAD];
-      b.tile[CS_CONV_DGRAD] = best64[CS_CONV_DGRAD];
+      float best_t = keep_w.us + keep_d.us;
+      ConvTile win_w = keep_w, win_d = keep_d;
+      std::vector<std::pair<ConvTile, ConvTile>> cands;
+      cands.emplace_back(keep_w, keep_d);
+      if (best64_t[CS_CONV_WGRAD] < 1e29f && best64_t[CS_CONV_DGRAD] < 1e29f)
+        cands.emplace_back(best64[CS_CONV_WGRAD], best64[CS_CONV_DGRAD]);
       float* dz = dz_[l & 1].data_ptr<float>();
-      conv_dual(l, (int)B, s, dz);  // warm
-      ok(hipEventRecord(e0, s), "record");
-      for (int64_t i = 0; i < iters; ++i) conv_dual(l, (int)B, s, dz);
-      ok(hipEventRecord(e1, s), "record");
-      ok(hipEventSynchronize(e1), "sync");
-      float ms = 0.f;
-      ok(hipEventElapsedTime(&ms, e0, e1), "elapsed");
-      const float dual_us = 1000.f * ms / (float)iters;
-      const float sep_us = keep_w.us + keep_d.us;
-      if (getenv("CS_TUNE_VERBOSE"))
-        fprintf(stderr, "[tune] block %d: dual %.1f us vs separate %.1f us\n", l, dual_us, sep_us);
-      if (dual_us < sep_us) {
+      for (const auto& c : cands) {
+        b.tile[CS_CONV_WGRAD] = c.first;
+        b.tile[CS_CONV_DGRAD] = c.second;
         b.use_dual = true;
-        const float wsh = best64_t[CS_CONV_WGRAD] / (best64_t[CS_CONV_WGRAD] + best64_t[CS_CONV_DGRAD]);
-        b.tile[CS_CONV_WGRAD].us = dual_us * wsh;
-        b.tile[CS_CONV_DGRAD].us = dual_us * (1.f - wsh);
-        best_us[3 * l + CS_CONV_WGRAD] = b.tile[CS_CONV_WGRAD].us;
-        best_us[3 * l + CS_CONV_DGRAD] = b.tile[CS_CONV_DGRAD].us;
-      } else {
-        b.tile[CS_CONV_WGRAD] = keep_w;
-        b.tile[CS_CONV_DGRAD] = keep_d;
+        if (!dual_ok(l)) continue;
+        conv_dual(l, (int)B, s, dz);  // warm
+        ok(hipEventRecord(e0, s), "record");
+        for (int64_t i = 0; i < iters; ++i) conv_dual(l, (int)B, s, dz);
+        ok(hipEventRecord(e1, s), "record");
+        ok(hipEventSynchronize(e1), "sync");
+        float ms = 0.f;
+        ok(hipEventElapsedTime(&ms, e0, e1), "elapsed");
+        const float dual_us = 1000.f * ms / (float)iters;
+        if (getenv("CS_TUNE_VERBOSE"))
+          fprintf(stderr, "[tune] block %d: dual (stage %d) %.1f us vs separate %.1f us\n", l, c.first.stage,
+                  dual_us, keep_w.us + keep_d.us);
+        if (dual_us < best_t) {
+          best_t = dual_us;
+          win_w = c.first;
+          win_d = c.second;
+          const float tw = std::max(c.first.us, 1e-3f), td = std::max(c.second.us, 1e-3f);
+          win_w.us = dual_us * tw / (tw + td);
+          win_d.us = dual_us * td / (tw + td);
+        }
       }
+      b.tile[CS_CONV_WGRAD] = win_w;
+      b.tile[CS_CONV_DGRAD] = win_d;
+      b.use_dual = best_t < keep_w.us + keep_d.us;
+      best_us[3 * l + CS_CONV_WGRAD] = win_w.us;
+      best_us[3 * l + CS_CONV_DGRAD] = win_d.us;
     }
   }
   hipEventDestroy(e0);

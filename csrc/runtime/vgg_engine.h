@@ -86,6 +86,15 @@ class VggEngine {
   void set_block_dual(int64_t l, bool on) { blocks_.at(l).use_dual = on; }
   // SGD (momentum, weight decay, dampening) on [off, off+n) of the flat buffers
   void sgd(double lr, double momentum, double wd, double dampening, int64_t off, int64_t n);
+  // SGD of one gradient bucket [off, off+n) (blocks >= lo_block) on the optimizer stream, overlapped
+  // with the rest of the backward: it waits for everything enqueued on the current stream (block
+  // lo_block's data gradient is the last reader of its weights) and, with a communicator, for the
+  // bucket's all-reduce already enqueued on the comm stream. advance_cursor: the step's last
+  // bucket moves the device-side batch cursor. join_opt() makes the current stream wait for it.
+  void sgd_bucket(RcclComm* comm, int64_t lo_block, int64_t off, int64_t n, double lr, double momentum, double wd,
+                  double dampening, bool advance_cursor);
+  void join_opt();
+  void set_sgd_overlap(bool on) { sgd_overlap_ = on; }
   // eval forward (running stats): loss (mean over the batch) -> loss(), correct count -> correct()
   void forward_eval(int64_t B);
 
@@ -141,6 +150,14 @@ class VggEngine {
   int64_t bn_fused_rows_ = 256;  // horizontal wgrad+dgrad fusion in backward (CS_CONV_DUAL=0 disables)
   hipStream_t side_ = nullptr;
   bool overlap_wgrad_ = false;
+  // per-bucket SGD on opt_ overlapping the backward of the blocks below (CS_SGD_OVERLAP=1 enables).
+  // Off: measured on MI355X (B=64, full-step hipGraph) 66.0-66.6k img/s with it vs 81.2k without —
+  // the graph's cross-stream fork/join edges cost far more than the 28 us SGD they hide
+  hipStream_t opt_ = nullptr;
+  bool sgd_overlap_ = false;
+  std::vector<hipEvent_t> ev_opt_;  // pool: main-stream / comm-stream marks per bucket, opt done
+  size_t next_opt_ev_ = 0;
+  hipEvent_t opt_event();
   std::vector<hipEvent_t> ev_bn_, ev_wg_;  // per block: BN-backward done (main), wgrad done (side)
 
  public:

@@ -174,9 +174,11 @@ def test_rccl_comm_world1_and_graph_capture(dev):
     assert c.native.async_error() == ""
 
 
-def test_dual_backward_launch_is_bitwise_equal(dev):
+@pytest.mark.parametrize("stage,bkw,bkd", [(0, 32, 16), (16 | 4, 64, 64), (16 | 3, 64, 64), (16, 16, 16)])
+def test_dual_backward_launch_is_bitwise_equal(dev, stage, bkw, bkd):
     # wgrad + dgrad horizontally fused into one launch (and one split-K combine) computes every
     # tile with the same K-split and summation order as two launches: bit-equal training
+    # (f32 register staging, and the X6S split-bf16 K-group / register variants)
     a = _trainer(dev, batch_size=32, train_size=256)
     b = _trainer(dev, batch_size=32, train_size=256)
     a.engine.set_dual(False)
@@ -186,7 +188,9 @@ def test_dual_backward_launch_is_bitwise_equal(dev):
             if l == 0 and m == 1:
                 continue
             for t in (a, b):
-                t.engine.set_tile(l, m, 64, 64, 4, 32 if m == 2 else 16)
+                t.engine.set_tile(l, m, 64, 64, 4, bkw if m == 2 else bkd, stage)
+        if l > 0:
+            b.engine.set_block_dual(l, True)
     for _ in range(3):
         a.step()
         b.step()
