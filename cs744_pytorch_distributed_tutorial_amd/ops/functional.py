@@ -147,8 +147,16 @@ def bn_relu_pool_eval(y: torch.Tensor, B: int, H: int, W: int, gamma, beta, runn
 
 def bn_relu_pool_bwd(y: torch.Tensor, G: torch.Tensor, st: BNState, gamma: torch.Tensor, B: int, H: int, W: int,
                      pool: bool = False, fused: bool = False):
-    """-> (dz [B*H*W, C], dgamma, dbeta, dbias) for z = maxpool?(relu(bn(y)))."""
+    """-> (dz [B*H*W, C], dgamma, dbeta, dbias) for z = maxpool?(relu(bn(y))).
+    ``fused``: True = one launch (small layers), "two" = chunk partials + finalize-in-apply."""
     C = gamma.numel()
+    if fused == "two":
+        bnv = torch.stack([st.scale, st.shift, st.mean, st.invstd]).contiguous()
+        part = torch.empty(native.C().bn_bwd_chunks(B, H, W, C, pool) * C * 3, device=y.device)
+        dgamma, dbeta, dbias = (torch.empty(C, device=y.device) for _ in range(3))
+        dz = torch.empty(B * H * W, C, device=y.device)
+        native.C().bn_bwd2(y, G, B, H, W, C, pool, bnv, gamma, part, dgamma, dbeta, dbias, dz)
+        return dz, dgamma, dbeta, dbias
     if fused:
         bnv = torch.stack([st.scale, st.shift, st.mean, st.invstd]).contiguous()
         coef = torch.empty(C * 3, device=y.device)

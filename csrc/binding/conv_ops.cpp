@@ -175,9 +175,29 @@ void bn_fused_bwd(torch::Tensor y, torch::Tensor G, int64_t B, int64_t H, int64_
                             dz.data_ptr<float>(), cur_stream()));
 }
 
+void bn_bwd2(torch::Tensor y, torch::Tensor G, int64_t B, int64_t H, int64_t W, int64_t C, bool pool,
+             torch::Tensor bnv, torch::Tensor gamma, torch::Tensor part, c10::optional<torch::Tensor> dgamma,
+             c10::optional<torch::Tensor> dbeta, c10::optional<torch::Tensor> dbias, torch::Tensor dz) {
+  TORCH_CHECK(C % 16 == 0 && C <= 1024 && (!pool || (H % 2 == 0 && W % 2 == 0)), "bn_bwd2: shape");
+  check_t(y, B * H * W * C, "y");
+  check_t(G, B * (pool ? H / 2 : H) * (pool ? W / 2 : W) * C, "G");
+  check_t(bnv, 4 * C, "bnv"); check_t(gamma, C, "gamma");
+  check_t(part, (int64_t)cs_bn_bwd_chunks(B, H, W, C, pool) * C * 3, "part");
+  check_t(dgamma, C, "dgamma"); check_t(dbeta, C, "dbeta"); check_t(dbias, C, "dbias");
+  check_t(dz, B * H * W * C, "dz");
+  DevGuard g(y.device());
+  CS_LAUNCH(cs_bn_bwd2(y.data_ptr<float>(), G.data_ptr<float>(), B, H, W, C, pool ? 1 : 0, bnv.data_ptr<float>(),
+                       gamma.data_ptr<float>(), part.data_ptr<float>(), mptr(dgamma), mptr(dbeta), mptr(dbias),
+                       dz.data_ptr<float>(), cur_stream()));
+}
+
 }  // namespace
 
 void register_conv_ops(pybind11::module& m) {
+  m.def("bn_bwd2", &bn_bwd2, "two-launch BN backward: chunk partials, then finalize folded into the apply");
+  m.def("bn_bwd_chunks", [](int64_t B, int64_t H, int64_t W, int64_t C, bool pool) {
+    return cs_bn_bwd_chunks(B, H, W, C, pool ? 1 : 0);
+  });
   m.def("bn_fused_fwd", &bn_fused_fwd, "single-launch BN finalize + normalize/ReLU(/pool) (small layers)");
   m.def("bn_fused_bwd", &bn_fused_bwd, "single-launch BN backward: reduce + finalize + apply (small layers)");
   m.def("conv_gemm", &conv_gemm, "implicit-GEMM 3x3 conv (mode 0 fwd / 1 dgrad / 2 wgrad), fp32 MFMA",

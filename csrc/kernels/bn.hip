@@ -15,6 +15,8 @@
 //   emits dgamma, dbeta, the conv-bias gradient (exact chain rule:
 //   sum_m dZ = -gamma*invstd*mean(g*xhat)*sum(xhat)) and the dZ coefficients;
 //   bn_bwd_apply writes dZ = gamma*invstd*(g - mean(g) - xhat*mean(g*xhat)).
+#include <algorithm>
+
 #include "common.h"
 #include "launchers.h"
 
@@ -312,12 +314,16 @@ __device__ __forceinline__ void sum_reduce_block(float (&acc)[3][4], float* lds)
       }
 }
 
+// grid (C/16, row chunks): every block finalizes its 16 channels from the T tile partials
+// (identical fixed-order combine in every block), block row 0 publishes bnv / running stats,
+// and each block normalizes its chunk of `upb` output units.
 __global__ __launch_bounds__(256) void bn_fused_fwd_kernel(const float* __restrict__ part, int T, int R, int M,
                                                            int C, const float* __restrict__ gamma,
                                                            const float* __restrict__ beta, float* running_mean,
                                                            float* running_var, int64_t* nbt, float momentum,
                                                            float eps, float* __restrict__ bnv, const float* __restrict__ y,
-                                                           float* __restrict__ out, int B, int H, int W, int pool) {
+                                                           float* __restrict__ out, int B, int H, int W, int pool,
+                                                           int upb) {
   __shared__ float lds[4 * 4 * 4 * 3];
   __shared__ float4 sc_sh[2][4];
   const int cq = threadIdx.x & 3, rl = threadIdx.x >> 2;
@@ -332,6 +338,7 @@ __global__ __launch_bounds__(256) void bn_fused_fwd_kernel(const float* __restri
     }
   }
   chan_reduce_block(n, m, M2, lds);
+  const bool lead = blockIdx.y == 0;
   if (threadIdx.x < 4) {
     float sc[4], sh[4];
 #pragma unroll
@@ -340,6 +347,7 @@ __global__ __launch_bounds__(256) void bn_fused_fwd_kernel(const float* __restri
       const float var = M2[q] / n[q], inv = 1.0f / sqrtf(var + eps);
       sc[q] = gamma[c] * inv;
       sh[q] = beta[c] - m[q] * gamma[c] * inv;
+      if (!lead) continue;
       bnv[c] = sc[q];
       bnv[C + c] = sh[q];
       bnv[2 * C + c] = m[q];
@@ -353,14 +361,14 @@ __global__ __launch_bounds__(256) void bn_fused_fwd_kernel(const float* __restri
     sc_sh[0][cq] = make_float4(sc[0], sc[1], sc[2], sc[3]);
     sc_sh[1][cq] = make_float4(sh[0], sh[1], sh[2], sh[3]);
   }
-  if (nbt != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *nbt += 1;
+  if (nbt != nullptr && lead && blockIdx.x == 0 && threadIdx.x == 0) *nbt += 1;
   __syncthreads();
   const float4 s = sc_sh[0][cq], t = sc_sh[1][cq];
   const int C4 = C >> 2;
   const int Ho = pool ? H >> 1 : H, Wo = pool ? W >> 1 : W;
-  const int units = B * Ho * Wo;
+  const int u_end = min(B * Ho * Wo, (int)(blockIdx.y + 1) * upb);
   const float4* y4 = reinterpret_cast<const float4*>(y);
-  for (int u = rl; u < units; u += 64) {
+  for (int u = blockIdx.y * upb + rl; u < u_end; u += 64) {
     float4 r;
     if (!pool) {
       r = bnrelu4(y4[(size_t)u * C4 + cqg], s, t);
@@ -414,7 +422,108 @@ __global__ __launch_bounds__(256) void bn_fused_bwd_kernel(const float* __restri
     bwd_visit<true, POOL>(y, G, B, H, W, C, cqg, u, scale, shift, mean, invstd, coef, dz, dummy);
 }
 
+// Two-launch backward for the larger layers (both channel-sliced like the fused kernel: 16
+// channels x a chunk of units per block): (1) per-chunk partial sums of (dy, dy*xhat, xhat)
+// -> part [chunks][C][3]; (2) every block re-sums the few chunk partials of its 16 channels
+// (fixed order, identical in every block), block row 0 publishes dgamma / dbeta / dbias, and
+// the block writes dZ for its own chunk of units — the finalize launch of the three-launch
+// path folded into the apply.
+template <bool POOL>
+__global__ __launch_bounds__(256) void bn_bwd_red_kernel(const float* __restrict__ y, const float* __restrict__ G,
+                                                         int B, int H, int W, int C, const float* __restrict__ bnv,
+                                                         float* __restrict__ part, int upb) {
+  __shared__ float lds[4 * 4 * 3 * 4];
+  const int cq = threadIdx.x & 3, rl = threadIdx.x >> 2;
+  const int cqg = blockIdx.x * 4 + cq;
+  const int units = POOL ? B * (H >> 1) * (W >> 1) : B * H * W;
+  const int u_end = min(units, (int)(blockIdx.y + 1) * upb);
+  float acc[3][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  for (int u = blockIdx.y * upb + rl; u < u_end; u += 64)
+    bwd_visit<false, POOL>(y, G, B, H, W, C, cqg, u, bnv, bnv + C, bnv + 2 * C, bnv + 3 * C, nullptr, nullptr, acc);
+  sum_reduce_block(acc, lds);
+  if (threadIdx.x < 4)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int k = 0; k < 3; ++k) part[((size_t)blockIdx.y * C + 4 * cqg + q) * 3 + k] = acc[k][q];
+}
+
+template <bool POOL>
+__global__ __launch_bounds__(256) void bn_bwd_fapply_kernel(const float* __restrict__ y, const float* __restrict__ G,
+                                                            int B, int H, int W, int C, const float* __restrict__ bnv,
+                                                            const float* __restrict__ gamma,
+                                                            const float* __restrict__ part, int nchunks,
+                                                            float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                            float* __restrict__ dbias, float* __restrict__ dz, int upb) {
+  __shared__ float lds[4 * 4 * 3 * 4];
+  __shared__ float coef[1024 * 3];  // indexed by global channel; this block fills its 16
+  const int cq = threadIdx.x & 3, rl = threadIdx.x >> 2;
+  const int cqg = blockIdx.x * 4 + cq;
+  float acc[3][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  for (int p = rl; p < nchunks; p += 64)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int k = 0; k < 3; ++k) acc[k][q] += part[((size_t)p * C + 4 * cqg + q) * 3 + k];
+  sum_reduce_block(acc, lds);
+  if (threadIdx.x < 4) {
+    const float Mf = (float)(B * H * W);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int c = 4 * cqg + q;
+      const float k1 = gamma[c] * bnv[3 * C + c], k2 = acc[0][q] / Mf, k3 = acc[1][q] / Mf;
+      if (blockIdx.y == 0) {
+        if (dgamma) dgamma[c] = acc[1][q];
+        if (dbeta) dbeta[c] = acc[0][q];
+        if (dbias) dbias[c] = -k1 * k3 * acc[2][q];
+      }
+      coef[3 * c] = k1;
+      coef[3 * c + 1] = k2;
+      coef[3 * c + 2] = k3;
+    }
+  }
+  __syncthreads();
+  const int units = POOL ? B * (H >> 1) * (W >> 1) : B * H * W;
+  const int u_end = min(units, (int)(blockIdx.y + 1) * upb);
+  float dummy[3][4];
+  for (int u = blockIdx.y * upb + rl; u < u_end; u += 64)
+    bwd_visit<true, POOL>(y, G, B, H, W, C, cqg, u, bnv, bnv + C, bnv + 2 * C, bnv + 3 * C, coef, dz, dummy);
+}
+
 }  // namespace
+
+int cs_bn_bwd_chunks(int B, int H, int W, int C, int pool) {
+  const int units = pool ? B * (H / 2) * (W / 2) : B * H * W;
+  const int want = std::max(1, std::min(64, 4096 / std::max(C, 1)));  // ~256 reduce blocks
+  const int upb = std::max(64, (units + want - 1) / want);
+  return (units + upb - 1) / upb;
+}
+
+hipError_t cs_bn_bwd2(const float* y, const float* G, int B, int H, int W, int C, int pool, const float* bnv,
+                      const float* gamma, float* part, float* dgamma, float* dbeta, float* dbias, float* dz,
+                      hipStream_t stream) {
+  if (C % kFusedCh != 0 || C > 1024 || (pool && ((H | W) & 1))) return hipErrorInvalidValue;
+  const int units = pool ? B * (H / 2) * (W / 2) : B * H * W;
+  const int cg = C / kFusedCh;
+  const int rc = cs_bn_bwd_chunks(B, H, W, C, pool);
+  const int upb_r = (units + rc - 1) / rc;
+  // apply chunks sized for bandwidth: >= 256 units per block, ~512 blocks at most
+  int ra = std::max(1, std::min((units + 255) / 256, std::max(1, 512 / cg)));
+  const int upb_a = (units + ra - 1) / ra;
+  ra = (units + upb_a - 1) / upb_a;
+  if (pool) {
+    hipLaunchKernelGGL((bn_bwd_red_kernel<true>), dim3(cg, rc), dim3(256), 0, stream, y, G, B, H, W, C, bnv, part,
+                       upb_r);
+    hipLaunchKernelGGL((bn_bwd_fapply_kernel<true>), dim3(cg, ra), dim3(256), 0, stream, y, G, B, H, W, C, bnv, gamma,
+                       part, rc, dgamma, dbeta, dbias, dz, upb_a);
+  } else {
+    hipLaunchKernelGGL((bn_bwd_red_kernel<false>), dim3(cg, rc), dim3(256), 0, stream, y, G, B, H, W, C, bnv, part,
+                       upb_r);
+    hipLaunchKernelGGL((bn_bwd_fapply_kernel<false>), dim3(cg, ra), dim3(256), 0, stream, y, G, B, H, W, C, bnv,
+                       gamma, part, rc, dgamma, dbeta, dbias, dz, upb_a);
+  }
+  return hipGetLastError();
+}
 
 int cs_bn_bwd_blocks(int B, int H, int W, int C, int pool) {
   const int units = pool ? B * (H / 2) * (W / 2) : B * H * W;
@@ -483,8 +592,14 @@ hipError_t cs_bn_fused_fwd(const float* part, int T, int R, int M, int C, const 
                            float* running_mean, float* running_var, int64_t* nbt, float momentum, float eps,
                            float* bnv, const float* y, float* out, int B, int H, int W, int pool, hipStream_t stream) {
   if (C % kFusedCh != 0 || (pool && ((H | W) & 1))) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(bn_fused_fwd_kernel, dim3(C / kFusedCh), dim3(256), 0, stream, part, T, R, M, C, gamma, beta,
-                     running_mean, running_var, nbt, momentum, eps, bnv, y, out, B, H, W, pool);
+  // row chunks of >= 256 output units (4 per row lane), ~512 blocks at most
+  const int units = B * (pool ? H / 2 : H) * (pool ? W / 2 : W);
+  const int cg = C / kFusedCh;
+  int chunks = std::max(1, std::min((units + 255) / 256, std::max(1, 512 / cg)));
+  const int upb = (units + chunks - 1) / chunks;
+  chunks = (units + upb - 1) / upb;
+  hipLaunchKernelGGL(bn_fused_fwd_kernel, dim3(cg, chunks), dim3(256), 0, stream, part, T, R, M, C, gamma, beta,
+                     running_mean, running_var, nbt, momentum, eps, bnv, y, out, B, H, W, pool, upb);
   return hipGetLastError();
 }
 

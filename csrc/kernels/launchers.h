@@ -116,6 +116,12 @@ hipError_t cs_bn_fused_fwd(const float* part, int T, int R, int M, int C, const 
 hipError_t cs_bn_fused_bwd(const float* y, const float* G, int B, int H, int W, int C, int pool, const float* bnv,
                            const float* gamma, float* coef, float* dgamma, float* dbeta, float* dbias, float* dz,
                            hipStream_t stream);
+// two-launch backward for larger layers (C % 16 == 0): channel-sliced chunk partials, then
+// finalize folded into the apply; part: [cs_bn_bwd_chunks][C][3] scratch
+int cs_bn_bwd_chunks(int B, int H, int W, int C, int pool);
+hipError_t cs_bn_bwd2(const float* y, const float* G, int B, int H, int W, int C, int pool, const float* bnv,
+                      const float* gamma, float* part, float* dgamma, float* dbeta, float* dbias, float* dz,
+                      hipStream_t stream);
 
 // ---------------------------------------------------------------- decoder-LM elementwise ops (lm.hip)
 enum { CS_F32 = 0, CS_BF16 = 1 };

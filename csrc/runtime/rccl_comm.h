@@ -58,6 +58,12 @@ class RcclComm {
   hipStream_t stream_ = nullptr;
   std::vector<hipEvent_t> fork_events_;
   hipEvent_t join_event_ = nullptr;
+  // CS_COMM_FORK=1: fork/join by stream memory operations on two signal-memory counters
+  // (hipStreamWriteValue64 / hipStreamWaitValue64) instead of event record + wait
+  bool value_sync_ = false;
+  uint64_t* fork_ctr_ = nullptr;
+  uint64_t* join_ctr_ = nullptr;
+  uint64_t fork_seq_ = 0, join_seq_ = 0;
   size_t next_fork_ = 0;
   int rank_ = 0, world_ = 1, device_ = 0;
   int group_depth_ = 0;

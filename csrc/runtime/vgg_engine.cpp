@@ -133,6 +133,7 @@ VggEngine::VggEngine(int64_t Bmax, std::vector<int64_t> desc, std::vector<int64_
     gmax = std::max(gmax, Bmax * ho * ho * b.cout);
     dzmax = std::max(dzmax, pix * b.cout);
     partmax = std::max<int64_t>(partmax, (int64_t)cs_bn_bwd_blocks(Bmax, b.H, b.H, b.cout, b.pool) * b.cout * 3);
+    partmax = std::max<int64_t>(partmax, (int64_t)cs_bn_bwd_chunks(Bmax, b.H, b.H, b.cout, b.pool) * b.cout * 3);
     cmax = std::max<int64_t>(cmax, b.cout);
     for (int m = 0; m < 3; ++m) b.tile[m] = default_tile(b, m, Bmax);
   }
@@ -179,6 +180,7 @@ VggEngine::VggEngine(int64_t Bmax, std::vector<int64_t> desc, std::vector<int64_
   if (const char* e = getenv("CS_CONV_DUAL")) dual_ = atoi(e) != 0;
   if (const char* e = getenv("CS_BN_FUSED_ROWS")) bn_fused_rows_ = atoll(e);
   if (const char* e = getenv("CS_CONV_MATH")) math_ = atoi(e);
+  if (const char* e = getenv("CS_BN_PATH")) bn_path_ = atoi(e);
   bn_part_ = torch::zeros({partmax}, fo);
   bn_coef_ = torch::zeros({cmax * 3}, fo);
   bn_eval_ = torch::zeros({2, cmax}, fo);
@@ -325,7 +327,7 @@ void VggEngine::forward_train(int64_t B) {
     float* bn = b.bn.data_ptr<float>();
     float* bufs = bufs_.data_ptr<float>();
     float* out = (l + 1 < L) ? blocks_[l + 1].x.data_ptr<float>() : gbuf_[1].data_ptr<float>();
-    if (bn_fused(l, B)) {  // finalize + normalize/ReLU/pool in one launch
+    if (bn_fused(l, B) || bn_path_ == 1) {  // finalize + normalize/ReLU/pool in one launch
       ok(cs_bn_fused_fwd(b.stats.data_ptr<float>(), (int)cdiv(M, rows), rows, (int)M, b.cout, P(b.g_off),
                          P(b.be_off), bufs + b.rm_off, bufs + b.rv_off, nbt_.data_ptr<int64_t>() + l, kBnMomentum,
                          kBnEps, bn, b.y.data_ptr<float>(), out, (int)B, b.H, b.H, b.pool, s),
@@ -362,6 +364,10 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
                          b.pool, bn, P(b.g_off), bn_coef_.data_ptr<float>(), G(b.g_off), G(b.be_off), G(b.b_off), dz,
                          s),
          "bn_fused_bwd");
+    } else if (bn_path_ == 1) {  // chunk partials, then finalize folded into the apply: two launches
+      ok(cs_bn_bwd2(b.y.data_ptr<float>(), gbuf_[(L - 1 - l) % 2].data_ptr<float>(), (int)B, b.H, b.H, b.cout, b.pool,
+                    bn, P(b.g_off), bn_part_.data_ptr<float>(), G(b.g_off), G(b.be_off), G(b.b_off), dz, s),
+         "bn_bwd2");
     } else {
       ok(cs_bn_bwd(b.y.data_ptr<float>(), gbuf_[(L - 1 - l) % 2].data_ptr<float>(), (int)B, b.H, b.H, b.cout, b.pool,
                    bn, bn + b.cout, bn + 2 * b.cout, bn + 3 * b.cout, P(b.g_off), bn_part_.data_ptr<float>(),
@@ -472,12 +478,13 @@ void VggEngine::step(int64_t B, RcclComm* comm, const std::vector<int64_t>& buck
   const size_t nb = bucket_blocks.size();
   TORCH_CHECK(nb >= 1 && bucket_ranges.size() == 2 * nb && bucket_blocks.back() == 0, "step: bucket plan");
   hipStream_t s = cur_stream();
-  if (comm != nullptr && broadcast_buffers && comm->world() > 1) {
-    // DDP broadcast_buffers: rank 0's BN running stats before every training forward
-    comm->broadcast(bufs_.data_ptr<float>(), bufs_.numel(), ncclFloat32, 0, s);
-    comm->broadcast(nbt_.data_ptr<int64_t>(), nbt_.numel(), ncclInt64, 0, s);
-    comm->join(s);
-  }
+  // CS_COMM_PROBE=1 (measurement only): run the collectives and their stream fork/join even on a
+  // one-rank communicator, to price the data-parallel plumbing on a single GPU
+  static const bool probe = [] {
+    const char* e = getenv("CS_COMM_PROBE");
+    return e != nullptr && atoi(e) != 0;
+  }();
+  const bool dp = comm != nullptr && (comm->world() > 1 || probe);
   forward_train(B);
   // per-bucket SGD needs the buckets to tile the flat buffer exactly
   bool tiled = sgd_overlap_;
@@ -494,16 +501,26 @@ void VggEngine::step(int64_t B, RcclComm* comm, const std::vector<int64_t>& buck
     hi = lo - 1;
     // a bucket is complete once its last weight-gradient GEMM (side stream) is: fork the
     // all-reduce from there, so it overlaps the rest of the backward on the main stream
-    if (comm != nullptr && comm->world() > 1)
+    if (dp)
       comm->all_reduce(G(bucket_ranges[2 * k]), bucket_ranges[2 * k + 1], ncclFloat32, ncclAvg,
                        overlap_wgrad_ ? side_ : s);
+    if (dp && broadcast_buffers && k == 0) {
+      // DDP broadcast_buffers (rank 0's BN running stats before every training forward), issued
+      // for the NEXT forward right behind the first bucket: this forward has produced the
+      // buffers, nothing touches them until the next forward, and the step's closing join
+      // orders them before it — no fork/join of its own at the head of the step (step 0 is
+      // covered by the construction-time broadcast)
+      // (no fork: the all-reduce just enqueued already waited for the forward)
+      comm->broadcast(bufs_.data_ptr<float>(), bufs_.numel(), ncclFloat32, 0, nullptr);
+      comm->broadcast(nbt_.data_ptr<int64_t>(), nbt_.numel(), ncclInt64, 0, nullptr);
+    }
     // ... and its SGD can run as soon as the averaged gradient is in and block lo's data
     // gradient (the last reader of these weights) is done, beside the backward below
     if (tiled)
       sgd_bucket(comm, lo, bucket_ranges[2 * k], bucket_ranges[2 * k + 1], lr, momentum, wd, dampening, k + 1 == nb);
   }
   if (overlap_wgrad_) ok(hipStreamWaitEvent(s, ev_wg_[0], 0), "join side");
-  if (comm != nullptr && comm->world() > 1) comm->join(s);
+  if (dp) comm->join(s);
   if (tiled) join_opt();
   else sgd(lr, momentum, wd, dampening, 0, params_.numel());
 }

@@ -146,6 +146,12 @@ class VggEngine {
   bool dual_ = true;
   // CS_BN_FUSED_ROWS; 0 disables. Measured on MI355X at B=64 (img/s): 0 -> 71.46k, 256 (blocks 6-7)
   // -> 71.64k, 1024 -> 69.85k, 4096 -> 63.07k: one block per 16 channels serialises too many rows
+  // BN launches (CS_BN_PATH): 1 = forward finalize+apply in one row-chunked launch, backward
+  // chunk partials + finalize-in-apply (two launches); 0 = the separate finalize launches.
+  // 0 by measurement (MI355X, B=64): 80.7k img/s vs 77.1k — the channel-sliced blocks of the
+  // folded launches stream NHWC rows as 64-B pieces and repeat the finalize in every block,
+  // which costs more than the launch they save (e.g. block 0 forward 27.8 us vs 4.9 + 5.2 us)
+  int bn_path_ = 0;
   int math_ = 2;  // conv autotune candidates: 0 f32 MFMA, 1 split-bf16 X6, 2 both (CS_CONV_MATH)
   int64_t bn_fused_rows_ = 256;  // horizontal wgrad+dgrad fusion in backward (CS_CONV_DUAL=0 disables)
   hipStream_t side_ = nullptr;
