@@ -9,7 +9,7 @@ precision), one process per GPU, data-parallel gradient averaging with part3
 backward pass. Weak scaling: per-GPU batch fixed, global batch = 64 * N.
 
 Default engine = ``native``: the C++ VggEngine (hand-written gfx950 kernels for
-every op, hipGraph-replayed step, native RcclComm). ``--engine torch`` runs the
+every op, eager C++ step (hipGraph optional), native RcclComm). ``--engine torch`` runs the
 same model through stock PyTorch-ROCm modules + the framework's DDP (the
 comparison baseline). ``--model resnet50`` / ``--model llama-tiny`` etc. run the
 BASELINE.json extension configs through the autograd-path trainer.
