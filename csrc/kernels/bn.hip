@@ -125,7 +125,7 @@ template <bool APPLY, bool POOL>
 __device__ __forceinline__ void bwd_visit(const float* __restrict__ y, const float* __restrict__ G, int B, int H,
                                           int W, int C, int cq, int unit, const float* scale, const float* shift,
                                           const float* mean, const float* invstd, const float* coef, float* dz,
-                                          float (&acc)[3][4]) {
+                                          float (&acc)[3][4], int gslabs = 1, int64_t gstride = 0) {
   const int C4 = C >> 2;
   float sc[4], sh[4], mu[4], is[4], k1[4], k2[4], k3[4];
 #pragma unroll
@@ -134,7 +134,11 @@ __device__ __forceinline__ void bwd_visit(const float* __restrict__ y, const flo
     sc[q] = scale[c]; sh[q] = shift[c]; mu[q] = mean[c]; is[q] = invstd[c];
     if (APPLY) { k1[q] = coef[3 * c]; k2[q] = coef[3 * c + 1]; k3[q] = coef[3 * c + 2]; }
   }
-  const float4 g4 = reinterpret_cast<const float4*>(G)[(size_t)unit * C4 + cq];
+  float4 g4 = reinterpret_cast<const float4*>(G)[(size_t)unit * C4 + cq];
+  for (int z = 1; z < gslabs; ++z) {  // split-K slabs of the producing GEMM, summed in z order
+    const float4 t = reinterpret_cast<const float4*>(G + (size_t)z * gstride)[(size_t)unit * C4 + cq];
+    g4.x += t.x; g4.y += t.y; g4.z += t.z; g4.w += t.w;
+  }
   const float gin[4] = {g4.x, g4.y, g4.z, g4.w};
   constexpr int NP = POOL ? 4 : 1;
   size_t off[NP];
@@ -192,7 +196,8 @@ __global__ __launch_bounds__(256) void bn_bwd_kernel(const float* __restrict__ y
                                                      int H, int W, int C, const float* __restrict__ scale,
                                                      const float* __restrict__ shift, const float* __restrict__ mean,
                                                      const float* __restrict__ invstd, const float* __restrict__ coef,
-                                                     float* __restrict__ dz, float* __restrict__ part) {
+                                                     float* __restrict__ dz, float* __restrict__ part, int gslabs,
+                                                     int64_t gstride) {
   extern __shared__ __attribute__((aligned(16))) float red[];  // [rows][C][3] (reduce only)
   const int C4 = C >> 2;
   const int rows = 256 / C4;  // C <= 1024
@@ -201,7 +206,7 @@ __global__ __launch_bounds__(256) void bn_bwd_kernel(const float* __restrict__ y
   float acc[3][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
   if (rl < rows) {
     for (int u = blockIdx.x * rows + rl; u < units; u += gridDim.x * rows)
-      bwd_visit<APPLY, POOL>(y, G, B, H, W, C, cq, u, scale, shift, mean, invstd, coef, dz, acc);
+      bwd_visit<APPLY, POOL>(y, G, B, H, W, C, cq, u, scale, shift, mean, invstd, coef, dz, acc, gslabs, gstride);
   }
   if (APPLY) return;
   if (rl < rows) {
@@ -389,7 +394,8 @@ __global__ __launch_bounds__(256) void bn_fused_bwd_kernel(const float* __restri
                                                            int B, int H, int W, int C, const float* __restrict__ bnv,
                                                            const float* __restrict__ gamma, float* __restrict__ coef,
                                                            float* __restrict__ dgamma, float* __restrict__ dbeta,
-                                                           float* __restrict__ dbias, float* __restrict__ dz) {
+                                                           float* __restrict__ dbias, float* __restrict__ dz,
+                                                           int gslabs, int64_t gstride) {
   __shared__ float lds[4 * 4 * 3 * 4];
   const int cq = threadIdx.x & 3, rl = threadIdx.x >> 2;
   const int cqg = blockIdx.x * 4 + cq;
@@ -400,7 +406,7 @@ __global__ __launch_bounds__(256) void bn_fused_bwd_kernel(const float* __restri
   const int units = POOL ? B * (H >> 1) * (W >> 1) : B * H * W;
   float acc[3][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
   for (int u = rl; u < units; u += 64)
-    bwd_visit<false, POOL>(y, G, B, H, W, C, cqg, u, scale, shift, mean, invstd, coef, dz, acc);
+    bwd_visit<false, POOL>(y, G, B, H, W, C, cqg, u, scale, shift, mean, invstd, coef, dz, acc, gslabs, gstride);
   sum_reduce_block(acc, lds);
   if (threadIdx.x < 4) {
     const float Mf = (float)(B * H * W);
@@ -419,7 +425,7 @@ __global__ __launch_bounds__(256) void bn_fused_bwd_kernel(const float* __restri
   __syncthreads();  // coef (global, written by this block) is visible to the whole workgroup
   float dummy[3][4];
   for (int u = rl; u < units; u += 64)
-    bwd_visit<true, POOL>(y, G, B, H, W, C, cqg, u, scale, shift, mean, invstd, coef, dz, dummy);
+    bwd_visit<true, POOL>(y, G, B, H, W, C, cqg, u, scale, shift, mean, invstd, coef, dz, dummy, gslabs, gstride);
 }
 
 // Two-launch backward for the larger layers (both channel-sliced like the fused kernel: 16
@@ -559,18 +565,19 @@ hipError_t cs_bn_apply(const float* y, const float* scale, const float* shift, f
 
 hipError_t cs_bn_bwd(const float* y, const float* G, int B, int H, int W, int C, int pool, const float* scale,
                      const float* shift, const float* mean, const float* invstd, const float* gamma, float* part,
-                     float* coef, float* dgamma, float* dbeta, float* dbias, float* dz, hipStream_t stream) {
-  if (C % 4 != 0 || C > 1024 || (pool && ((H | W) & 1))) return hipErrorInvalidValue;
+                     float* coef, float* dgamma, float* dbeta, float* dbias, float* dz, hipStream_t stream,
+                     int gslabs, int64_t gstride) {
+  if (C % 4 != 0 || C > 1024 || (pool && ((H | W) & 1)) || gslabs < 1) return hipErrorInvalidValue;
   const int P = cs_bn_bwd_blocks(B, H, W, C, pool);
   const int rows = 256 / (C / 4);
   const size_t lds = (size_t)rows * C * 3 * sizeof(float);
   const int M = B * H * W;
   if (pool) {
     hipLaunchKernelGGL((bn_bwd_kernel<false, true>), dim3(P), dim3(256), lds, stream, y, G, B, H, W, C, scale, shift,
-                       mean, invstd, nullptr, nullptr, part);
+                       mean, invstd, nullptr, nullptr, part, gslabs, gstride);
   } else {
     hipLaunchKernelGGL((bn_bwd_kernel<false, false>), dim3(P), dim3(256), lds, stream, y, G, B, H, W, C, scale, shift,
-                       mean, invstd, nullptr, nullptr, part);
+                       mean, invstd, nullptr, nullptr, part, gslabs, gstride);
   }
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 3) / 4), dim3(256), 0, stream, part, P, C, M, gamma, invstd,
                      dgamma, dbeta, dbias, coef);
@@ -580,10 +587,10 @@ hipError_t cs_bn_bwd(const float* y, const float* G, int B, int H, int W, int C,
   if (blocks > 2048) blocks = 2048;
   if (pool) {
     hipLaunchKernelGGL((bn_bwd_kernel<true, true>), dim3(blocks), dim3(256), 0, stream, y, G, B, H, W, C, scale, shift,
-                       mean, invstd, coef, dz, nullptr);
+                       mean, invstd, coef, dz, nullptr, gslabs, gstride);
   } else {
     hipLaunchKernelGGL((bn_bwd_kernel<true, false>), dim3(blocks), dim3(256), 0, stream, y, G, B, H, W, C, scale,
-                       shift, mean, invstd, coef, dz, nullptr);
+                       shift, mean, invstd, coef, dz, nullptr, gslabs, gstride);
   }
   return hipGetLastError();
 }
@@ -605,13 +612,13 @@ hipError_t cs_bn_fused_fwd(const float* part, int T, int R, int M, int C, const 
 
 hipError_t cs_bn_fused_bwd(const float* y, const float* G, int B, int H, int W, int C, int pool, const float* bnv,
                            const float* gamma, float* coef, float* dgamma, float* dbeta, float* dbias, float* dz,
-                           hipStream_t stream) {
-  if (C % kFusedCh != 0 || (pool && ((H | W) & 1))) return hipErrorInvalidValue;
+                           hipStream_t stream, int gslabs, int64_t gstride) {
+  if (C % kFusedCh != 0 || (pool && ((H | W) & 1)) || gslabs < 1) return hipErrorInvalidValue;
   if (pool)
     hipLaunchKernelGGL((bn_fused_bwd_kernel<true>), dim3(C / kFusedCh), dim3(256), 0, stream, y, G, B, H, W, C, bnv,
-                       gamma, coef, dgamma, dbeta, dbias, dz);
+                       gamma, coef, dgamma, dbeta, dbias, dz, gslabs, gstride);
   else
     hipLaunchKernelGGL((bn_fused_bwd_kernel<false>), dim3(C / kFusedCh), dim3(256), 0, stream, y, G, B, H, W, C, bnv,
-                       gamma, coef, dgamma, dbeta, dbias, dz);
+                       gamma, coef, dgamma, dbeta, dbias, dz, gslabs, gstride);
   return hipGetLastError();
 }

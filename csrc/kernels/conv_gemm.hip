@@ -1425,6 +1425,7 @@ hipError_t cs_conv_gemm(CsConvArgs a, int mode, int bm, int bn, int bk, int spli
     else if (mode == CS_CONV_DGRAD) e = launch_gemm<BM_, BN_, CS_CONV_DGRAD, BK_>(a, splits, stage, stream); \
     else e = launch_gemm<BM_, BN_, CS_CONV_WGRAD, BK_>(a, splits, stage, stream);                       \
     if (e != hipSuccess || splits == 1 || a.counters != nullptr) return e;                               \
+    if (a.keep_slabs && splits <= 2 * kFold) return e; /* the consumer sums the slabs */                  \
     return launch_reduce(a, mode, splits, stream);                                                       \
   }
   CS_DISPATCH(64, 64, 16)

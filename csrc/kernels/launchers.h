@@ -49,6 +49,7 @@ struct CsConvArgs {
   int* counters;      // split-K tile tickets (zeroed, >= #tiles ints) for the in-launch combine; null = reduce kernel
   int B, H, W, Cin, Cout;
   int w_oihw;
+  int keep_slabs;  // split-K: leave the <= 32 fp32 slabs in ws for the consumer to sum (no reduce launch)
   // filled by the launcher:
   int lgH, lgW, lgCin, lgCout, M, N, K, ksteps_per_split, total_ksteps;
 };
@@ -103,9 +104,12 @@ hipError_t cs_bn_apply(const float* y, const float* scale, const float* shift, f
                        int pool, hipStream_t stream);
 int cs_bn_bwd_blocks(int B, int H, int W, int C, int pool);
 // part: [cs_bn_bwd_blocks][C][3] scratch; coef: [C][3] scratch; dgamma/dbeta/dbias may be null.
+// G may be split-K slabs of the data-gradient GEMM: G = sum_{z < gslabs} G[z * gstride + i]
+// (summed in z order, bit-equal to the split-K combine launch it replaces)
 hipError_t cs_bn_bwd(const float* y, const float* G, int B, int H, int W, int C, int pool, const float* scale,
                      const float* shift, const float* mean, const float* invstd, const float* gamma, float* part,
-                     float* coef, float* dgamma, float* dbeta, float* dbias, float* dz, hipStream_t stream);
+                     float* coef, float* dgamma, float* dbeta, float* dbias, float* dz, hipStream_t stream,
+                     int gslabs = 1, int64_t gstride = 0);
 
 // single-launch BN for small layers (one block per 16 channels owns all their rows):
 // forward = finalize (tile partials -> bnv [4][C] = scale, shift, mean, invstd + running stats)
@@ -115,7 +119,7 @@ hipError_t cs_bn_fused_fwd(const float* part, int T, int R, int M, int C, const 
                            float* bnv, const float* y, float* out, int B, int H, int W, int pool, hipStream_t stream);
 hipError_t cs_bn_fused_bwd(const float* y, const float* G, int B, int H, int W, int C, int pool, const float* bnv,
                            const float* gamma, float* coef, float* dgamma, float* dbeta, float* dbias, float* dz,
-                           hipStream_t stream);
+                           hipStream_t stream, int gslabs = 1, int64_t gstride = 0);
 // two-launch backward for larger layers (C % 16 == 0): channel-sliced chunk partials, then
 // finalize folded into the apply; part: [cs_bn_bwd_chunks][C][3] scratch
 int cs_bn_bwd_chunks(int B, int H, int W, int C, int pool);

@@ -181,6 +181,7 @@ VggEngine::VggEngine(int64_t Bmax, std::vector<int64_t> desc, std::vector<int64_
   if (const char* e = getenv("CS_BN_FUSED_ROWS")) bn_fused_rows_ = atoll(e);
   if (const char* e = getenv("CS_CONV_MATH")) math_ = atoi(e);
   if (const char* e = getenv("CS_BN_PATH")) bn_path_ = atoi(e);
+  if (const char* e = getenv("CS_KEEP_SLABS")) keep_slabs_ = atoi(e) != 0;
   bn_part_ = torch::zeros({partmax}, fo);
   bn_coef_ = torch::zeros({cmax * 3}, fo);
   bn_eval_ = torch::zeros({2, cmax}, fo);
@@ -265,9 +266,10 @@ void VggEngine::set_perm(torch::Tensor perm) {
 }
 
 void VggEngine::conv(int l, int mode, int B, const ConvTile& t, hipStream_t s, bool with_stats, float* ws,
-                     float* dz) {
+                     float* dz, bool keep_slabs) {
   VggBlock& b = blocks_[l];
   CsConvArgs a = conv_args(l, mode, B, with_stats, ws, dz);
+  a.keep_slabs = keep_slabs ? 1 : 0;
   const Dims d = dims(b, mode, B);
   const int sp = eff_splits(d.K, t.splits, t.bk);
   TORCH_CHECK(sp == 1 || (int64_t)sp * d.M * d.N <= ws_elems_, "VggEngine: split-K workspace too small");
@@ -299,6 +301,7 @@ void VggEngine::forward_train(int64_t B) {
   TORCH_CHECK(data_[0].defined(), "forward_train: set_data(0, ...) first");
   hipStream_t s = cur_stream();
   const int L = (int)blocks_.size();
+  g_slabs_ = 1;  // the head writes the top block's gradient to gbuf_
   // one launch: sampler index (device cursor into the epoch permutation, or idx_ when no
   // permutation is set), label gather, crop/flip/normalize into block 0's NHWC input
   const bool use_perm = perm_len_ > 0;
@@ -359,21 +362,25 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
     // WAR: block l+2's weight-gradient GEMM (side stream) reads the same dz buffer; it may
     // belong to an earlier backward() call of this step that did not join (bucketed step)
     if (overlap_wgrad_ && l + 2 < L) ok(hipStreamWaitEvent(s, ev_wg_[l + 2], 0), "wait wgrad");
+    // this block's output gradient: gbuf_, or the split-K slabs the dgrad above left in ws_
+    const int gs = g_slabs_;
+    const float* Gin = gs > 1 ? ws_.data_ptr<float>() : gbuf_[(L - 1 - l) % 2].data_ptr<float>();
+    TORCH_CHECK(gs == 1 || bn_path_ == 0, "VggEngine: kept split-K slabs need the default BN path");
     if (bn_fused(l, B)) {  // reduce + finalize + apply in one launch
-      ok(cs_bn_fused_bwd(b.y.data_ptr<float>(), gbuf_[(L - 1 - l) % 2].data_ptr<float>(), (int)B, b.H, b.H, b.cout,
-                         b.pool, bn, P(b.g_off), bn_coef_.data_ptr<float>(), G(b.g_off), G(b.be_off), G(b.b_off), dz,
-                         s),
+      ok(cs_bn_fused_bwd(b.y.data_ptr<float>(), Gin, (int)B, b.H, b.H, b.cout, b.pool, bn, P(b.g_off),
+                         bn_coef_.data_ptr<float>(), G(b.g_off), G(b.be_off), G(b.b_off), dz, s, gs, g_stride_),
          "bn_fused_bwd");
     } else if (bn_path_ == 1) {  // chunk partials, then finalize folded into the apply: two launches
       ok(cs_bn_bwd2(b.y.data_ptr<float>(), gbuf_[(L - 1 - l) % 2].data_ptr<float>(), (int)B, b.H, b.H, b.cout, b.pool,
                     bn, P(b.g_off), bn_part_.data_ptr<float>(), G(b.g_off), G(b.be_off), G(b.b_off), dz, s),
          "bn_bwd2");
     } else {
-      ok(cs_bn_bwd(b.y.data_ptr<float>(), gbuf_[(L - 1 - l) % 2].data_ptr<float>(), (int)B, b.H, b.H, b.cout, b.pool,
-                   bn, bn + b.cout, bn + 2 * b.cout, bn + 3 * b.cout, P(b.g_off), bn_part_.data_ptr<float>(),
-                   bn_coef_.data_ptr<float>(), G(b.g_off), G(b.be_off), G(b.b_off), dz, s),
+      ok(cs_bn_bwd(b.y.data_ptr<float>(), Gin, (int)B, b.H, b.H, b.cout, b.pool, bn, bn + b.cout,
+                   bn + 2 * b.cout, bn + 3 * b.cout, P(b.g_off), bn_part_.data_ptr<float>(),
+                   bn_coef_.data_ptr<float>(), G(b.g_off), G(b.be_off), G(b.b_off), dz, s, gs, g_stride_),
          "bn_bwd");
     }
+    g_slabs_ = 1;
     if (!overlap_wgrad_ && dual_ok(l)) {  // wgrad + dgrad in one launch
       conv_dual(l, (int)B, s, dz);
       continue;
@@ -386,7 +393,17 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
     } else {
       conv(l, CS_CONV_WGRAD, (int)B, b.tile[CS_CONV_WGRAD], s, false, ws_side_.data_ptr<float>(), dz);
     }
-    if (l > 0) conv(l, CS_CONV_DGRAD, (int)B, b.tile[CS_CONV_DGRAD], s, false, nullptr, dz);
+    if (l > 0) {
+      const ConvTile& t = b.tile[CS_CONV_DGRAD];
+      const Dims d = dims(b, CS_CONV_DGRAD, B);
+      const int sp = eff_splits(d.K, t.splits, t.bk);
+      const bool keep = keep_slabs_ && bn_path_ == 0 && sp > 1 && sp <= 32;
+      conv(l, CS_CONV_DGRAD, (int)B, t, s, false, nullptr, dz, keep);
+      if (keep) {
+        g_slabs_ = sp;
+        g_stride_ = d.M * d.N;
+      }
+    }
   }
   if (join && overlap_wgrad_) ok(hipStreamWaitEvent(s, ev_wg_[lo], 0), "join side");
 }

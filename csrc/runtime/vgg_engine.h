@@ -118,7 +118,7 @@ class VggEngine {
 
  private:
   void conv(int l, int mode, int B, const ConvTile& t, hipStream_t s, bool with_stats, float* ws = nullptr,
-            float* dz = nullptr);
+            float* dz = nullptr, bool keep_slabs = false);
   CsConvArgs conv_args(int l, int mode, int B, bool with_stats, float* ws, float* dz);
   // block l's wgrad + dgrad as one launch (both 64x64 register-staged tiles)
   bool dual_ok(int l) const;
@@ -152,6 +152,14 @@ class VggEngine {
   // folded launches stream NHWC rows as 64-B pieces and repeat the finalize in every block,
   // which costs more than the launch they save (e.g. block 0 forward 27.8 us vs 4.9 + 5.2 us)
   int bn_path_ = 0;
+  // CS_KEEP_SLABS=1: split-K data gradients leave their slabs in ws_ and the next BN backward
+  // sums them (z order, bit-equal) while it reads G, instead of a separate combine launch.
+  // Off: measured equal on MI355X (81.8-82.0k vs 82.0-82.1k img/s) — both BN passes then read
+  // every slab, which costs what the saved launch did. g_slabs_ / g_stride_ describe where the
+  // gradient of the block below currently lives (1 = gbuf_)
+  bool keep_slabs_ = false;
+  int g_slabs_ = 1;
+  int64_t g_stride_ = 0;
   int math_ = 2;  // conv autotune candidates: 0 f32 MFMA, 1 split-bf16 X6, 2 both (CS_CONV_MATH)
   int64_t bn_fused_rows_ = 256;  // horizontal wgrad+dgrad fusion in backward (CS_CONV_DUAL=0 disables)
   hipStream_t side_ = nullptr;

@@ -249,3 +249,20 @@ def test_single_launch_bn_matches_multi_kernel_bn(dev):
     d = (b.params.double() - a.params.double()).norm() / a.params.double().norm()
     assert d.item() < 2e-3, d.item()
     torch.testing.assert_close(b.nbt, a.nbt)
+
+
+@pytest.mark.parametrize("stage", [0, 16 | 4])
+def test_kept_dgrad_slabs_bitwise_equal(dev, stage, monkeypatch):
+    # CS_KEEP_SLABS=1 (opt-in): split-K data gradients left as slabs and summed (z order) by the
+    # next BN backward while it reads G == the separate split-K combine launch, bit for bit
+    out = []
+    for keep in ("0", "1"):
+        monkeypatch.setenv("CS_KEEP_SLABS", keep)
+        t = _trainer(dev, batch_size=32, train_size=256)
+        for l in range(1, t.layout.L):
+            t.engine.set_tile(l, 1, 64, 64, 4 if l % 2 else 3, 64 if stage else 16, stage)
+        for _ in range(3):
+            t.step()
+        torch.cuda.synchronize()
+        out.append((t.params.clone(), t.mom.clone()))
+    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
