@@ -62,6 +62,9 @@ def parse(argv=None):
     p.add_argument("--no-graph", action="store_true", help="native engine: disable hipGraph capture")
     p.add_argument("--graph", type=str, default="auto", choices=["auto", "full", "segments", "none"])
     p.add_argument("--json-out", type=str, default=None)
+    p.add_argument("--phases", type=int, default=0,
+                   help="native engine: after the timed steps, N more steps with per-phase device timing "
+                        "(forward / bucket backward / all-reduce wait / SGD), printed to stderr as JSON")
     return p.parse_args(argv)
 
 
@@ -149,6 +152,11 @@ def main(argv=None) -> int:
         # split-bf16 x6 kernels (3 bf16 pieces per operand, 6 MFMAs; f64-checked like the f32 path)
         maths = [t["math"] for t in trainer.tile_table()]
         out["config"]["conv_gemm_math"] = {m: maths.count(m) for m in sorted(set(maths))}
+    if args.phases > 0 and hasattr(trainer, "phase_breakdown"):
+        ph = trainer.phase_breakdown(args.phases)
+        if rank == 0:
+            print(json.dumps({"phases_ms": {k: round(v, 4) for k, v in ph.items()}, "rank": rank}),
+                  file=sys.stderr, flush=True)
     if rank == 0:
         line = json.dumps(out)
         print(line, flush=True)

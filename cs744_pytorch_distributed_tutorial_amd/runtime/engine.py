@@ -455,6 +455,25 @@ class NativeTrainer:
             self._step_eager(B)
         self.global_step += 1
 
+    def phase_breakdown(self, steps: int = 5) -> Dict[str, float]:
+        """Per-phase device time (ms) of the C++ step, averaged over ``steps`` timed steps
+        (forward, each bucket's backward, all-reduce wait, SGD). Timing events cost a few us
+        per phase, so this runs its own steps rather than instrumenting a benchmark."""
+        self.engine.set_timing(True)
+        acc: Dict[str, float] = {}
+        n = 0
+        try:
+            for _ in range(steps):
+                B = self._load_next_batch()
+                self._step_full_native(B)
+                self.global_step += 1
+                for k, v in self.engine.phase_times():
+                    acc[k] = acc.get(k, 0.0) + v
+                n += 1
+        finally:
+            self.engine.set_timing(False)
+        return {k: v / max(n, 1) for k, v in acc.items()}
+
     def last_loss(self) -> float:
         return float(self.engine.loss().item())
 

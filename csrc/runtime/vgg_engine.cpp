@@ -418,6 +418,7 @@ VggEngine::~VggEngine() {
     hipStreamDestroy(opt_);
   }
   for (auto e : ev_opt_) hipEventDestroy(e);
+  for (auto e : tev_) hipEventDestroy(e);
   for (auto e : ev_bn_) hipEventDestroy(e);
   for (auto e : ev_wg_) hipEventDestroy(e);
 }
@@ -433,6 +434,39 @@ void VggEngine::sgd(double lr, double momentum, double wd, double dampening, int
 }
 
 hipEvent_t VggEngine::opt_event() { return ev_opt_[next_opt_ev_++ % ev_opt_.size()]; }
+
+void VggEngine::set_timing(bool on) {
+  timing_ = on;
+  if (on && tev_.empty()) {
+    tev_.resize(32);
+    for (auto& e : tev_) ok(hipEventCreate(&e), "timing event");
+  }
+}
+
+void VggEngine::mark(const char* phase) {
+  if (!timing_ || tn_ >= tev_.size()) return;
+  ok(hipEventRecord(tev_[tn_], cur_stream()), "timing record");
+  if (tn_ > 0) {
+    if (tnames_.size() < tn_) tnames_.resize(tn_);
+    tnames_[tn_ - 1] = phase;
+  }
+  ++tn_;
+}
+
+std::vector<std::pair<std::string, double>> VggEngine::phase_times() {
+  std::vector<std::pair<std::string, double>> out;
+  if (tn_ < 2) return out;
+  ok(hipEventSynchronize(tev_[tn_ - 1]), "timing sync");
+  double total = 0.0;
+  for (size_t i = 1; i < tn_; ++i) {
+    float ms = 0.f;
+    ok(hipEventElapsedTime(&ms, tev_[i - 1], tev_[i]), "elapsed");
+    out.emplace_back(tnames_[i - 1], (double)ms);
+    total += ms;
+  }
+  out.emplace_back("step", total);
+  return out;
+}
 
 void VggEngine::sgd_bucket(RcclComm* comm, int64_t lo_block, int64_t off, int64_t n, double lr, double momentum,
                            double wd, double dampening, bool advance_cursor) {
@@ -502,7 +536,10 @@ void VggEngine::step(int64_t B, RcclComm* comm, const std::vector<int64_t>& buck
     return e != nullptr && atoi(e) != 0;
   }();
   const bool dp = comm != nullptr && (comm->world() > 1 || probe);
+  tn_ = 0;
+  mark("start");
   forward_train(B);
+  mark("forward");
   // per-bucket SGD needs the buckets to tile the flat buffer exactly
   bool tiled = sgd_overlap_;
   for (size_t k = 0, at = 0; k < nb && tiled; ++k) {
@@ -515,6 +552,9 @@ void VggEngine::step(int64_t B, RcclComm* comm, const std::vector<int64_t>& buck
     const int64_t lo = bucket_blocks[k];
     TORCH_CHECK(lo <= hi, "step: bucket blocks must decrease");
     backward(hi, lo, B, /*join=*/false);
+    static const char* kBwd[] = {"backward_bucket0", "backward_bucket1", "backward_bucket2", "backward_bucket3",
+                                 "backward_bucket4", "backward_bucket5", "backward_bucket6", "backward_bucket7"};
+    mark(k < 8 ? kBwd[k] : "backward_bucket8+");
     hi = lo - 1;
     // a bucket is complete once its last weight-gradient GEMM (side stream) is: fork the
     // all-reduce from there, so it overlaps the rest of the backward on the main stream
@@ -538,8 +578,10 @@ void VggEngine::step(int64_t B, RcclComm* comm, const std::vector<int64_t>& buck
   }
   if (overlap_wgrad_) ok(hipStreamWaitEvent(s, ev_wg_[0], 0), "join side");
   if (dp) comm->join(s);
+  mark("allreduce_wait");
   if (tiled) join_opt();
   else sgd(lr, momentum, wd, dampening, 0, params_.numel());
+  mark("sgd");
 }
 
 void VggEngine::set_tile(int64_t block, int64_t mode, int64_t bm, int64_t bn, int64_t splits, int64_t bk,

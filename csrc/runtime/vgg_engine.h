@@ -105,6 +105,13 @@ class VggEngine {
             const std::vector<int64_t>& bucket_ranges, bool broadcast_buffers, double lr, double momentum,
             double wd, double dampening);
 
+  // Phase timing (opt-in): timing events on the compute stream at the step's phase
+  // boundaries (forward, each gradient bucket's backward, waiting for the all-reduces, SGD);
+  // phase_times() synchronizes and returns the last step's phases in ms. Off by default: an event
+  // record on the compute stream costs a few us of launch gap on this stack.
+  void set_timing(bool on);
+  std::vector<std::pair<std::string, double>> phase_times();
+
   // conv tile control: mode 0 fwd / 1 dgrad / 2 wgrad
   void set_tile(int64_t block, int64_t mode, int64_t bm, int64_t bn, int64_t splits, int64_t bk = 16,
                 int64_t stage = 0);
@@ -172,6 +179,11 @@ class VggEngine {
   std::vector<hipEvent_t> ev_opt_;  // pool: main-stream / comm-stream marks per bucket, opt done
   size_t next_opt_ev_ = 0;
   hipEvent_t opt_event();
+  bool timing_ = false;
+  std::vector<hipEvent_t> tev_;          // timing events (created on demand)
+  std::vector<std::string> tnames_;      // phase ending at tev_[i + 1]
+  size_t tn_ = 0;                        // events recorded in the last step
+  void mark(const char* phase);           // record the next timing event (timing_ only)
   std::vector<hipEvent_t> ev_bn_, ev_wg_;  // per block: BN-backward done (main), wgrad done (side)
 
  public:

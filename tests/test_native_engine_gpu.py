@@ -266,3 +266,14 @@ def test_kept_dgrad_slabs_bitwise_equal(dev, stage, monkeypatch):
         torch.cuda.synchronize()
         out.append((t.params.clone(), t.mom.clone()))
     assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
+
+
+def test_phase_breakdown(dev):
+    # opt-in device-side phase timing of the C++ step
+    t = _trainer(dev, batch_size=16, train_size=128)
+    t.step()
+    ph = t.phase_breakdown(3)
+    assert {"forward", "sgd", "allreduce_wait", "step"} <= set(ph)
+    assert any(k.startswith("backward_bucket") for k in ph)
+    parts = sum(v for k, v in ph.items() if k != "step")
+    assert ph["step"] > 0 and abs(parts - ph["step"]) <= 1e-3 * ph["step"] + 1e-3
