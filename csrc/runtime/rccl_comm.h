@@ -59,7 +59,8 @@ class RcclComm {
   std::vector<hipEvent_t> fork_events_;
   hipEvent_t join_event_ = nullptr;
   // CS_COMM_FORK=1: fork/join by stream memory operations on two signal-memory counters
-  // (hipStreamWriteValue64 / hipStreamWaitValue64) instead of event record + wait
+  // (hipStreamWriteValue64 / hipStreamWaitValue64) instead of event record + wait. Off: on the
+  // one-rank probe it measured 59.7k img/s vs 70.3-73.3k with events (profiles/r1_dp_plumbing_probe.md)
   bool value_sync_ = false;
   uint64_t* fork_ctr_ = nullptr;
   uint64_t* join_ctr_ = nullptr;
