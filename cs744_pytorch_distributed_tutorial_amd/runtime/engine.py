@@ -183,7 +183,8 @@ class NativeTrainer:
                  graph: str = "auto", lr: float = 0.1, momentum: float = 0.9, weight_decay: float = 1e-4,
                  dampening: float = 0.0, seed: int = 5000, data_seed: int = 0, train_size: Optional[int] = None,
                  test_size: Optional[int] = None, autotune: bool = True, broadcast_buffers: bool = True,
-                 drop_last: bool = True, init_state: Optional[Dict[str, torch.Tensor]] = None):
+                 drop_last: bool = True, init_state: Optional[Dict[str, torch.Tensor]] = None,
+                 dtype: str = "fp32"):
         C = native.C()
         self.device = device or torch.device("cuda", torch.cuda.current_device())
         self.rank, self.world = rank, world
@@ -246,9 +247,16 @@ class NativeTrainer:
         self.engine.set_data(0, self.train_data, self.train_labels, self.aug_train)
         self.engine.set_data(1, self.test_data, self.test_labels, self.aug_test)
         self.idx_buf = self.engine.idx()
+        # fp32: conv GEMMs on f32 MFMA or the fp32-accurate split-bf16 kernels (autotuned);
+        # bf16: conv operands rounded to bf16, f32 accumulation (BN, loss, SGD, storage stay f32)
+        if dtype not in ("fp32", "bf16"):
+            raise ValueError(f"dtype {dtype!r}: fp32 | bf16")
+        self.dtype = dtype
+        if dtype == "bf16":
+            self.engine.set_math(3)
         self.tune_us: Optional[List[float]] = None
         if autotune:
-            self._tune(model, os.environ.get("CS744_TUNE_CACHE"))
+            self._tune(model + ("" if dtype == "fp32" else "/bf16"), os.environ.get("CS744_TUNE_CACHE"))
         if graph == "auto":
             # Measured on MI355X (VGG-11, B=64, 1 GPU): eager C++ step 82.1-82.3k img/s, one
             # full-step hipGraph 81.7-81.8k, per-bucket segment graphs 78.2k, and RCCL captured
@@ -306,7 +314,8 @@ class NativeTrainer:
                 us = self.tune_us[3 * l + m] if self.tune_us else None
                 out.append({"block": l, "op": names[m], "bm": bm, "bn": bn, "bk": bk, "splits": sp,
                             "stage": _STAGE_NAMES.get(st & 7, str(st & 7)),
-                            "math": "x6s" if st & 16 else ("x6" if st & 8 else "f32"), "us": us})
+                            "math": "bf16" if st & 32 else ("x6s" if st & 16 else ("x6" if st & 8 else "f32")),
+                            "us": us})
         return out
 
     # ---------------------------------------------------------------- data
@@ -549,7 +558,7 @@ class NativeTrainer:
     @classmethod
     def from_bench_args(cls, args, device, rank, world) -> "NativeTrainer":
         return cls(model=args.model, batch_size=args.batch_size, device=device, rank=rank, world=world,
-                   sync=args.sync, comm=args.comm, bucket_mb=args.bucket_mb,
+                   sync=args.sync, comm=args.comm, bucket_mb=args.bucket_mb, dtype=args.dtype,
                    graph="none" if args.no_graph else getattr(args, "graph", "auto"))
 
 

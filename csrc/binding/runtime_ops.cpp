@@ -154,6 +154,7 @@ void register_runtime(pybind11::module& m) {
       .def("set_overlap_wgrad", &cs::VggEngine::set_overlap_wgrad)
       .def("set_sgd_overlap", &cs::VggEngine::set_sgd_overlap)
       .def("set_timing", &cs::VggEngine::set_timing)
+      .def("set_math", &cs::VggEngine::set_math)
       .def("phase_times", &cs::VggEngine::phase_times)
       .def("join_opt", &cs::VggEngine::join_opt)
       .def("sgd_bucket", &cs::VggEngine::sgd_bucket, py::arg("comm").none(true), py::arg("lo_block"), py::arg("off"),

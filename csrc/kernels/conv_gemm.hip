@@ -439,14 +439,16 @@ __device__ __forceinline__ void kstep_x6(Loader<BM, BN, MODE, BK, C4, false, KG>
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef short i16x4 __attribute__((ext_vector_type(4)));
 
-template <int BM, int BN, int MODE, int BK>
+// NP = bf16 planes per operand: 3 (h, m, l: the fp32-accurate X6S math) or 1 (h only: plain
+// bf16 operands with f32 accumulation, the native engine's opt-in bf16 mode)
+template <int BM, int BN, int MODE, int BK, int NP = 3>
 struct TileXS {
   using T = Tile<BM, BN, MODE, BK>;
   static constexpr int PA = T::A_KC ? BK + 8 : BM + 32;  // plane pitch (bf16 elements)
   static constexpr int PB = T::B_KC ? BK + 8 : BN + 32;
   static constexpr int PLA = (T::A_KC ? BM : BK) * PA;  // one plane
   static constexpr int PLB = (T::B_KC ? BN : BK) * PB;
-  static constexpr int A16 = 3 * PLA, STAGE16 = 3 * PLA + 3 * PLB;
+  static constexpr int A16 = NP * PLA, STAGE16 = NP * PLA + NP * PLB;
   static constexpr size_t BYTES = 2 * (size_t)STAGE16 * 2;  // double buffer
 };
 
@@ -477,27 +479,41 @@ __device__ __forceinline__ int xs_off(int i) {
   }
 }
 
-template <int BM, int BN, int MODE, int BK, bool C4, int KG, int S>
+__device__ __forceinline__ bf16x4 round4(const float4 v) {
+  bf16x4 h;
+  h[0] = (__bf16)v.x; h[1] = (__bf16)v.y; h[2] = (__bf16)v.z; h[3] = (__bf16)v.w;
+  return h;
+}
+
+template <int BM, int BN, int MODE, int BK, bool C4, int KG, int S, int NP = 3>
 __device__ __forceinline__ void store_xs(const Loader<BM, BN, MODE, BK, C4, false, KG>& ld, __bf16* As, __bf16* Bs,
                                          const int (&oa)[Tile<BM, BN, MODE, BK, false, KG>::AC],
                                          const int (&ob)[Tile<BM, BN, MODE, BK, false, KG>::BC]) {
   using T = Tile<BM, BN, MODE, BK, false, KG>;  // chunk counts depend on the block's thread count
-  using X = TileXS<BM, BN, MODE, BK>;
+  using X = TileXS<BM, BN, MODE, BK, NP>;
 #pragma unroll
   for (int i = 0; i < T::AC; ++i) {
-    bf16x4 h, m, l;
-    split4(ld.ra[S][i], h, m, l);
-    *reinterpret_cast<bf16x4*>(As + oa[i]) = h;
-    *reinterpret_cast<bf16x4*>(As + X::PLA + oa[i]) = m;
-    *reinterpret_cast<bf16x4*>(As + 2 * X::PLA + oa[i]) = l;
+    if constexpr (NP == 1) {
+      *reinterpret_cast<bf16x4*>(As + oa[i]) = round4(ld.ra[S][i]);
+    } else {
+      bf16x4 h, m, l;
+      split4(ld.ra[S][i], h, m, l);
+      *reinterpret_cast<bf16x4*>(As + oa[i]) = h;
+      *reinterpret_cast<bf16x4*>(As + X::PLA + oa[i]) = m;
+      *reinterpret_cast<bf16x4*>(As + 2 * X::PLA + oa[i]) = l;
+    }
   }
 #pragma unroll
   for (int i = 0; i < T::BC; ++i) {
-    bf16x4 h, m, l;
-    split4(ld.rb[S][i], h, m, l);
-    *reinterpret_cast<bf16x4*>(Bs + ob[i]) = h;
-    *reinterpret_cast<bf16x4*>(Bs + X::PLB + ob[i]) = m;
-    *reinterpret_cast<bf16x4*>(Bs + 2 * X::PLB + ob[i]) = l;
+    if constexpr (NP == 1) {
+      *reinterpret_cast<bf16x4*>(Bs + ob[i]) = round4(ld.rb[S][i]);
+    } else {
+      bf16x4 h, m, l;
+      split4(ld.rb[S][i], h, m, l);
+      *reinterpret_cast<bf16x4*>(Bs + ob[i]) = h;
+      *reinterpret_cast<bf16x4*>(Bs + X::PLB + ob[i]) = m;
+      *reinterpret_cast<bf16x4*>(Bs + 2 * X::PLB + ob[i]) = l;
+    }
   }
 }
 
@@ -523,7 +539,7 @@ __device__ __forceinline__ void read_xs(const __bf16* pl, int base, int g0, int 
   }
 }
 
-template <int BM, int BN, int MODE, int BK, int LS, int SS, bool C4, int KG>
+template <int BM, int BN, int MODE, int BK, int LS, int SS, bool C4, int KG, int NP = 3>
 __device__ __forceinline__ void kstep_xs(Loader<BM, BN, MODE, BK, C4, false, KG>& ld, const CsConvArgs& a,
                                          const __bf16* cur, __bf16* nxt,
                                          f32x16 (&acc)[Tile<BM, BN, MODE, BK>::RM][Tile<BM, BN, MODE, BK>::RN],
@@ -531,23 +547,32 @@ __device__ __forceinline__ void kstep_xs(Loader<BM, BN, MODE, BK, C4, false, KG>
                                          const int (&oa)[Tile<BM, BN, MODE, BK, false, KG>::AC],
                                          const int (&ob)[Tile<BM, BN, MODE, BK, false, KG>::BC]) {
   using T = Tile<BM, BN, MODE, BK>;
-  using X = TileXS<BM, BN, MODE, BK>;
+  using X = TileXS<BM, BN, MODE, BK, NP>;
   constexpr int NGK = T::NG / KG;
   static_assert(NGK >= 2 && NGK % 2 == 0, "X6 math needs pairs of sub-step chunks per K-group");
   const int g0 = kg * NGK, lane = threadIdx.x & 63;
   const __bf16* Bc = cur + X::A16;
 #pragma unroll
   for (int gp = 0; gp < NGK; gp += 2) {
-    bf16x8 ah[T::RM], am[T::RM], al[T::RM], bh[T::RN], bm[T::RN], bl[T::RN];
+    bf16x8 ah[T::RM], bh[T::RN];
     read_xs<T::RM, T::A_KC, X::PA, BK>(cur, wm * T::WM, g0 + gp, lane, ah);
-    read_xs<T::RM, T::A_KC, X::PA, BK>(cur + X::PLA, wm * T::WM, g0 + gp, lane, am);
-    read_xs<T::RM, T::A_KC, X::PA, BK>(cur + 2 * X::PLA, wm * T::WM, g0 + gp, lane, al);
     read_xs<T::RN, T::B_KC, X::PB, BK>(Bc, wn * T::WN, g0 + gp, lane, bh);
-    read_xs<T::RN, T::B_KC, X::PB, BK>(Bc + X::PLB, wn * T::WN, g0 + gp, lane, bm);
-    read_xs<T::RN, T::B_KC, X::PB, BK>(Bc + 2 * X::PLB, wn * T::WN, g0 + gp, lane, bl);
-    mma_x6f<T::RM, T::RN>(ah, am, al, bh, bm, bl, acc);
+    if constexpr (NP == 1) {
+#pragma unroll
+      for (int i = 0; i < T::RM; ++i)
+#pragma unroll
+        for (int j = 0; j < T::RN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+    } else {
+      bf16x8 am[T::RM], al[T::RM], bm[T::RN], bl[T::RN];
+      read_xs<T::RM, T::A_KC, X::PA, BK>(cur + X::PLA, wm * T::WM, g0 + gp, lane, am);
+      read_xs<T::RM, T::A_KC, X::PA, BK>(cur + 2 * X::PLA, wm * T::WM, g0 + gp, lane, al);
+      read_xs<T::RN, T::B_KC, X::PB, BK>(Bc + X::PLB, wn * T::WN, g0 + gp, lane, bm);
+      read_xs<T::RN, T::B_KC, X::PB, BK>(Bc + 2 * X::PLB, wn * T::WN, g0 + gp, lane, bl);
+      mma_x6f<T::RM, T::RN>(ah, am, al, bh, bm, bl, acc);
+    }
     if (gp == 0) ld.template load<LS>(a, k_load);
-    if (gp == (NGK > 2 ? 2 : 0)) store_xs<BM, BN, MODE, BK, C4, KG, SS>(ld, nxt, nxt + X::A16, oa, ob);
+    if (gp == (NGK > 2 ? 2 : 0)) store_xs<BM, BN, MODE, BK, C4, KG, SS, NP>(ld, nxt, nxt + X::A16, oa, ob);
   }
 }
 
@@ -806,8 +831,9 @@ __device__ __forceinline__ void gemm_body(const CsConvArgs& a, const int tile, c
       cur = cur == NB - 1 ? 0 : cur + 1;
     }
     __syncthreads();  // every wave's fragment reads are done before the epilogue reuses LDS
-  } else if constexpr (SCHED == 3) {
-    using X = TileXS<BM, BN, MODE, BK>;
+  } else if constexpr (SCHED == 3 || SCHED == 5) {
+    constexpr int NP = SCHED == 5 ? 1 : 3;  // SCHED 5: bf16 operands (h plane only)
+    using X = TileXS<BM, BN, MODE, BK, NP>;
     Loader<BM, BN, MODE, BK, C4, false, KG> ld;
     ld.init(a, m0, n0);
     using TK = Tile<BM, BN, MODE, BK, false, KG>;
@@ -821,14 +847,14 @@ __device__ __forceinline__ void gemm_body(const CsConvArgs& a, const int tile, c
     if (nks > 0) {
       ld.template load<0>(a, ks_begin * BK);
       if (nks > 1) ld.template load<1>(a, (ks_begin + 1) * BK);
-      store_xs<BM, BN, MODE, BK, C4, KG, 0>(ld, l0, l0 + X::A16, oa, ob);
+      store_xs<BM, BN, MODE, BK, C4, KG, 0, NP>(ld, l0, l0 + X::A16, oa, ob);
     }
     __syncthreads();
     for (int t = 0; t < nks; t += 2) {
-      kstep_xs<BM, BN, MODE, BK, 0, 1, C4, KG>(ld, a, l0, l1, acc, wm, wn, kg, (ks_begin + t + 2) * BK, oa, ob);
+      kstep_xs<BM, BN, MODE, BK, 0, 1, C4, KG, NP>(ld, a, l0, l1, acc, wm, wn, kg, (ks_begin + t + 2) * BK, oa, ob);
       __syncthreads();
       if (t + 1 >= nks) break;
-      kstep_xs<BM, BN, MODE, BK, 1, 0, C4, KG>(ld, a, l1, l0, acc, wm, wn, kg, (ks_begin + t + 3) * BK, oa, ob);
+      kstep_xs<BM, BN, MODE, BK, 1, 0, C4, KG, NP>(ld, a, l1, l0, acc, wm, wn, kg, (ks_begin + t + 3) * BK, oa, ob);
       __syncthreads();
     }
   } else {
@@ -1155,14 +1181,16 @@ hipError_t launch_gemm_m(const CsConvArgs& a, int splits, int stage, hipStream_t
   using T = Tile<BM, BN, MODE, BK>;
   using TG = Tile<BM, BN, MODE, BK, true>;
   const int ntiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
-  const size_t lds = MATH == 3 ? TileXS<BM, BN, MODE, BK>::BYTES : 2 * T::STAGE * sizeof(float);
+  const size_t lds = MATH == 3   ? TileXS<BM, BN, MODE, BK>::BYTES
+                     : MATH == 5 ? TileXS<BM, BN, MODE, BK, 1>::BYTES
+                                 : 2 * T::STAGE * sizeof(float);
   const dim3 grid(ntiles, 1, splits);
   constexpr bool deep_fits = (BM + BN) * BK * 4 * 5 < 160 * 1024;
   if constexpr (BK != 64 && MATH == 0) {
     if (MODE == CS_CONV_FWD && a.w_oihw)  // padded conv0: Cin = 4 < BK
       return launch_k<BM, BN, MODE, BK, 0, true, 0>(grid, lds, stream, a);
   }
-  if constexpr (BK == 32 && MATH != 3) {
+  if constexpr (BK == 32 && MATH != 3 && MATH != 5) {
     if (stage == CS_STAGE_LDS_DMA)
       return launch_k<BM, BN, MODE, BK, MATH, false, 3>(grid, 3 * TG::STAGE * sizeof(float), stream, a);
     if constexpr (deep_fits) {
@@ -1184,7 +1212,7 @@ hipError_t launch_gemm_m(const CsConvArgs& a, int splits, int stage, hipStream_t
     }
   }
   if (stage != CS_STAGE_REGS) return hipErrorInvalidValue;
-  if constexpr (MATH == 3 && BK == 64 && !(BM == 64 && BN == 64)) {
+  if constexpr ((MATH == 3 && BK == 64 && !(BM == 64 && BN == 64)) || (MATH == 5 && BK == 64 && BM == 128 && BN == 128)) {
     return hipErrorInvalidValue;  // bf16 planes of a wider bk-64 tile exceed the 160 KiB LDS
   } else if constexpr (MATH >= 2) {
     return launch_k<BM, BN, MODE, BK, MATH, false, 0>(grid, lds, stream, a);
@@ -1196,6 +1224,7 @@ hipError_t launch_gemm_m(const CsConvArgs& a, int splits, int stage, hipStream_t
 
 template <int BM, int BN, int MODE, int BK>
 hipError_t launch_gemm(const CsConvArgs& a, int splits, int stage, hipStream_t stream) {
+  if (stage & CS_STAGE_BF16) return launch_gemm_m<BM, BN, MODE, BK, 5>(a, splits, stage & ~CS_STAGE_BF16, stream);
   if (stage & CS_STAGE_X6S) return launch_gemm_m<BM, BN, MODE, BK, 3>(a, splits, stage & ~CS_STAGE_X6S, stream);
   if (stage & CS_STAGE_X6) return launch_gemm_m<BM, BN, MODE, BK, 2>(a, splits, stage & ~CS_STAGE_X6, stream);
   return launch_gemm_m<BM, BN, MODE, BK, 0>(a, splits, stage, stream);
@@ -1212,7 +1241,8 @@ hipError_t launch_gemm(const CsConvArgs& a, int splits, int stage, hipStream_t s
   CS_K(BM_, BN_, MODE_, 32, 0, false, 3)                                      \
   CS_K(BM_, BN_, MODE_, 16, 2, false, 0) CS_K(BM_, BN_, MODE_, 32, 2, false, 0) \
   CS_K(BM_, BN_, MODE_, 32, 2, false, 3)                                      \
-  CS_K(BM_, BN_, MODE_, 16, 3, false, 0) CS_K(BM_, BN_, MODE_, 32, 3, false, 0)
+  CS_K(BM_, BN_, MODE_, 16, 3, false, 0) CS_K(BM_, BN_, MODE_, 32, 3, false, 0)     \
+  CS_K(BM_, BN_, MODE_, 16, 5, false, 0) CS_K(BM_, BN_, MODE_, 32, 5, false, 0)
 #define CS_TILE(BM_, BN_)                                                                       \
   CS_MODE(BM_, BN_, CS_CONV_FWD) CS_MODE(BM_, BN_, CS_CONV_DGRAD) CS_MODE(BM_, BN_, CS_CONV_WGRAD) \
   CS_K(BM_, BN_, CS_CONV_FWD, 16, 0, true, 0) CS_K(BM_, BN_, CS_CONV_FWD, 32, 0, true, 0)
@@ -1226,6 +1256,15 @@ CS_TILE(128, 128)
 CS_TILE64(64, 64)
 CS_TILE64(128, 64)
 CS_TILE64(64, 128)
+CS_K(64, 64, CS_CONV_FWD, 64, 5, false, 0)
+CS_K(64, 64, CS_CONV_DGRAD, 64, 5, false, 0)
+CS_K(64, 64, CS_CONV_WGRAD, 64, 5, false, 0)
+CS_K(128, 64, CS_CONV_FWD, 64, 5, false, 0)
+CS_K(128, 64, CS_CONV_DGRAD, 64, 5, false, 0)
+CS_K(128, 64, CS_CONV_WGRAD, 64, 5, false, 0)
+CS_K(64, 128, CS_CONV_FWD, 64, 5, false, 0)
+CS_K(64, 128, CS_CONV_DGRAD, 64, 5, false, 0)
+CS_K(64, 128, CS_CONV_WGRAD, 64, 5, false, 0)
 CS_K(64, 64, CS_CONV_FWD, 64, 3, false, 0)
 CS_K(64, 64, CS_CONV_DGRAD, 64, 3, false, 0)
 CS_K(64, 64, CS_CONV_WGRAD, 64, 3, false, 0)
@@ -1246,6 +1285,16 @@ CS_KG1(64, 128, 32, 2, 3)
 CS_KG1(128, 128, 32, 2, 3)
 CS_KG1(64, 64, 64, 2, 3)
 CS_KG1(64, 64, 64, 4, 3)
+CS_KG1(64, 64, 32, 2, 5)
+CS_KG1(128, 64, 32, 2, 5)
+CS_KG1(64, 128, 32, 2, 5)
+CS_KG1(128, 128, 32, 2, 5)
+CS_KG1(64, 64, 64, 2, 5)
+CS_KG1(128, 64, 64, 2, 5)
+CS_KG1(64, 128, 64, 2, 5)
+CS_KG1(64, 64, 64, 4, 5)
+CS_KG1(128, 64, 64, 4, 5)
+CS_KG1(64, 128, 64, 4, 5)
 CS_KG(64, 64, 64, 2)
 CS_KG(128, 64, 64, 2)
 CS_KG(64, 128, 64, 2)
@@ -1306,7 +1355,12 @@ void cs_conv_fill_dims(CsConvArgs* a, int mode) {
 }
 
 bool cs_conv_stage_ok(int stage, int bm, int bn, int bk, bool conv0_fwd) {
-  if ((stage & CS_STAGE_X6) && (stage & CS_STAGE_X6S)) return false;
+  const int maths = ((stage & CS_STAGE_X6) != 0) + ((stage & CS_STAGE_X6S) != 0) + ((stage & CS_STAGE_BF16) != 0);
+  if (maths > 1) return false;
+  if (stage & CS_STAGE_BF16) {  // bf16 operands (one plane): register staging / K-groups
+    stage &= ~CS_STAGE_BF16;
+    if (conv0_fwd || (stage != CS_STAGE_REGS && stage != CS_STAGE_KG2 && stage != CS_STAGE_KG4)) return false;
+  }
   if (stage & CS_STAGE_X6) {  // split-bf16 math: every staging, except the padded conv0 forward
     if (conv0_fwd) return false;
     stage &= ~CS_STAGE_X6;

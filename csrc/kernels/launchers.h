@@ -66,8 +66,10 @@ void cs_conv_fill_dims(CsConvArgs* a, int mode);
 // operand, 6 v_mfma_f32_32x32x16_bf16 per 32x32x16 product; conv_gemm.hip "X6")
 // | CS_STAGE_X6S: X6 math with the split done once at the LDS store into bf16 planes (register
 // staging / K-groups only; bk 64 only with 64x64 tiles)
+// | CS_STAGE_BF16: operands rounded to bf16 at the LDS store, one bf16 MFMA, f32 accumulate
+// (reduced precision: only for the engine's opt-in bf16 mode, never picked by the f32 autotune)
 enum { CS_STAGE_REGS = 0, CS_STAGE_LDS_DMA = 1, CS_STAGE_LDS_DMA_DEEP = 2, CS_STAGE_KG2 = 3, CS_STAGE_KG4 = 4,
-       CS_STAGE_X6 = 8, CS_STAGE_X6S = 16 };
+       CS_STAGE_X6 = 8, CS_STAGE_X6S = 16, CS_STAGE_BF16 = 32 };
 // whether a (stage, tile, bk) combination has a kernel
 bool cs_conv_stage_ok(int stage, int bm, int bn, int bk, bool conv0_fwd);
 hipError_t cs_conv_gemm(CsConvArgs a, int mode, int bm, int bn, int bk, int splits, hipStream_t stream,

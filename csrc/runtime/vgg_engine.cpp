@@ -643,11 +643,18 @@ std::vector<double> VggEngine::autotune(int64_t B, int64_t iters) {
       for (int stage : {(int)CS_STAGE_REGS, (int)CS_STAGE_LDS_DMA, (int)CS_STAGE_LDS_DMA_DEEP, (int)CS_STAGE_KG2,
                         (int)CS_STAGE_KG4, CS_STAGE_X6 | CS_STAGE_REGS, CS_STAGE_X6 | CS_STAGE_LDS_DMA,
                         CS_STAGE_X6 | CS_STAGE_LDS_DMA_DEEP, CS_STAGE_X6 | CS_STAGE_KG2, CS_STAGE_X6 | CS_STAGE_KG4,
-                        CS_STAGE_X6S | CS_STAGE_REGS, CS_STAGE_X6S | CS_STAGE_KG2, CS_STAGE_X6S | CS_STAGE_KG4})
+                        CS_STAGE_X6S | CS_STAGE_REGS, CS_STAGE_X6S | CS_STAGE_KG2, CS_STAGE_X6S | CS_STAGE_KG4,
+                        CS_STAGE_BF16 | CS_STAGE_REGS, CS_STAGE_BF16 | CS_STAGE_KG2, CS_STAGE_BF16 | CS_STAGE_KG4})
       for (int bk : {16, 32, 64}) {
-        // CS_CONV_MATH: 0 = f32 MFMA kernels only, 1 = split-bf16 (X6) only, 2 = both (default)
+        // CS_CONV_MATH: 0 = f32 MFMA kernels only, 1 = split-bf16 (X6) only, 2 = both (default),
+        // 3 = bf16 operands (reduced precision, opt-in; the padded conv0 forward stays f32)
         const bool x6 = (stage & (CS_STAGE_X6 | CS_STAGE_X6S)) != 0;
-        if ((x6 && math_ == 0) || (!x6 && math_ == 1)) continue;
+        const bool bf = (stage & CS_STAGE_BF16) != 0;
+        if (math_ == 3) {
+          if (!bf && !(conv0_fwd && stage == CS_STAGE_REGS)) continue;
+        } else if (bf || (x6 && math_ == 0) || (!x6 && math_ == 1)) {
+          continue;
+        }
         if (bk == 64 && conv0_fwd) continue;
         const int64_t ks = cdiv(d.K, bk);
         for (int bm : {64, 128}) {

@@ -95,6 +95,11 @@ class VggEngine {
                   double dampening, bool advance_cursor);
   void join_opt();
   void set_sgd_overlap(bool on) { sgd_overlap_ = on; }
+  // conv autotune candidates (CS_CONV_MATH): 0 f32, 1 x6, 2 f32 + x6 (default), 3 bf16 operands
+  void set_math(int64_t m) {
+    TORCH_CHECK(m >= 0 && m <= 3, "set_math: 0..3");
+    math_ = (int)m;
+  }
   // eval forward (running stats): loss (mean over the batch) -> loss(), correct count -> correct()
   void forward_eval(int64_t B);
 

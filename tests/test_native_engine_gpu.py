@@ -277,3 +277,21 @@ def test_phase_breakdown(dev):
     assert any(k.startswith("backward_bucket") for k in ph)
     parts = sum(v for k, v in ph.items() if k != "step")
     assert ph["step"] > 0 and abs(parts - ph["step"]) <= 1e-3 * ph["step"] + 1e-3
+
+
+def test_bf16_mode_tracks_fp32(dev):
+    # opt-in bf16 conv operands (f32 accumulate, f32 BN / loss / SGD): every tuned conv GEMM is a
+    # bf16 kernel except the padded conv0 forward, and a step stays close to the f32 engine
+    a = _trainer(dev, batch_size=16, train_size=128)
+    b = _trainer(dev, batch_size=16, train_size=128, dtype="bf16", autotune=True)
+    assert all(t["math"] == "bf16" for t in b.tile_table() if not (t["block"] == 0 and t["op"] == "fwd"))
+    a.step()
+    b.step()
+    torch.cuda.synchronize()
+    # one step from identical weights: same loss to bf16 precision and the same gradient
+    # direction. Element-wise, BN backward amplifies bf16 rounding in near-cancelling sums: the
+    # PyTorch CPU model with bf16-rounded conv operands gives cosine 0.968 vs f32 at this shape
+    # (the engine measured 0.984)
+    assert abs(a.last_loss() - b.last_loss()) <= 1e-2 * abs(a.last_loss())
+    ga, gb = a.grads.double(), b.grads.double()
+    assert (ga @ gb / (ga.norm() * gb.norm())).item() > 0.95
