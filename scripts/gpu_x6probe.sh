@@ -1,4 +1,5 @@
-# X6 split cost probe: x6-only autotune with the real split vs a split-free build (wrong numbers)
+# X6 split cost probe: x6-only autotune with the real split vs a split-free build (wrong numbers).
+# Needs _probe_C.so in the repo root: the package linked with conv_gemm.hip built with -DCS_X6_PROBE=1
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
