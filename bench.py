@@ -99,7 +99,10 @@ def describe(args, trainer, world):
 def main(argv=None) -> int:
     args = parse(argv)
     if args.batch_size is None:
-        args.batch_size = 64 if is_vgg(args.model) else (8 if "llama" in args.model.lower() else 128)
+        # Llama-3-8B: 4 x 2048 tokens per GPU (measured on MI355X: 11.6k / 14.3k / 15.8k tokens/s at
+        # B = 1 / 2 / 4 — the fp32 master-weight SGD step amortises over more tokens)
+        m = args.model.lower()
+        args.batch_size = 64 if is_vgg(args.model) else (4 if "8b" in m else (8 if "llama" in m else 128))
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
     if world_env > 1:
         D.init_process_group(backend="nccl")
