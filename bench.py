@@ -59,7 +59,7 @@ def parse(argv=None):
     p.add_argument("--bucket-policy", type=str, default="layer", choices=["size", "layer", "single"])
     p.add_argument("--dtype", type=str, default="fp32", choices=["fp32", "bf16"])
     p.add_argument("--seq-len", type=int, default=0, help="decoder LM sequence length")
-    p.add_argument("--no-graph", action="store_true", help="native engine: disable hipGraph capture")
+    p.add_argument("--no-graph", action="store_true", help="native engine: same as --graph none")
     p.add_argument("--graph", type=str, default="auto", choices=["auto", "full", "segments", "none"])
     p.add_argument("--json-out", type=str, default=None)
     p.add_argument("--phases", type=int, default=0,

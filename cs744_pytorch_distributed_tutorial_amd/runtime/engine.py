@@ -1,9 +1,9 @@
-"""Native training engine: VGG on MI355X through the C++ ``VggEngine`` + hipGraphs.
+"""Native training engine: VGG on MI355X through the C++ ``VggEngine``.
 
 This is the MI355X-first replacement for the reference's whole training loop
 (`master/part1/part1.py:31-38`, `master/part2b/part2b.py:35-46`,
-`master/part3/part3.py:24-48`): no autograd, no nn.Module dispatch, no per-step
-host work beyond one index copy and graph replays.
+`master/part3/part3.py:24-48`): no autograd, no nn.Module dispatch; one C++ call
+enqueues the whole step (the batch cursor lives on the device).
 
 * ``FlatLayout`` — parameters / gradients / momentum live in three flat fp32
   buffers in *backward-ready* order (fc1, then conv blocks last -> first), each
@@ -15,9 +15,11 @@ host work beyond one index copy and graph replays.
   ``ddp`` (bucketed all-reduce(AVG) launched as soon as a bucket's backward
   completes, overlapped with the rest of backward), or the faithful modes
   ``allreduce`` / ``gather_scatter`` / ``p2p`` / ``flat`` run after backward.
-  Graph modes: ``full`` (the whole step, RCCL included, is ONE hipGraph),
-  ``segments`` (one graph per bucket segment, collectives issued eagerly
-  between them — the default with >1 rank), ``none`` (eager).
+  Graph modes: ``none`` (eager C++ step — the default at every world size with
+  the native communicator, measured as fast as any graph mode), ``full`` (the
+  whole step as ONE hipGraph), ``segments`` (one graph per bucket segment,
+  collectives issued from Python between them — the default for the torch
+  communicator / faithful sync modes).
 """
 from __future__ import annotations
 
