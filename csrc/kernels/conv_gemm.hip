@@ -436,6 +436,7 @@ __device__ __forceinline__ void kstep_x6(Loader<BM, BN, MODE, BK, C4, false, KG>
 // for K-major operands two ds_read_b64_tr_b16 per plane from [k][rows+32] images (the
 // hardware transpose delivers 4 k-values of one row per lane; +32 pads make the 4 rows of a
 // 16-lane block and the two blocks of a 32-lane half hit 8 distinct 8-bank ranges).
+// (s_setprio(1) around the MFMA chain measured -1%: 81.2-81.6k vs 82.3-82.6k img/s.)
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef short i16x4 __attribute__((ext_vector_type(4)));
 
