@@ -19,8 +19,11 @@
 
 #include "common.h"
 #include "launchers.h"
+#include "bn_device.h"
 
 namespace {
+
+using cs_bn::bwd_visit;
 
 __device__ __forceinline__ void chan_combine(float& n, float& m, float& M2, float nb, float mb, float M2b) {
   if (nb == 0.f) return;
@@ -118,79 +121,6 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__
   reinterpret_cast<float4*>(out)[t] = r;
 }
 
-// ------------------------------------------------------------------ backward
-// Visit every full-resolution element once: unit = a 2x2 window (pool) or a pixel.
-// APPLY = false: accumulate per-channel partials; APPLY = true: write dZ.
-template <bool APPLY, bool POOL>
-__device__ __forceinline__ void bwd_visit(const float* __restrict__ y, const float* __restrict__ G, int B, int H,
-                                          int W, int C, int cq, int unit, const float* scale, const float* shift,
-                                          const float* mean, const float* invstd, const float* coef, float* dz,
-                                          float (&acc)[3][4], int gslabs = 1, int64_t gstride = 0) {
-  const int C4 = C >> 2;
-  float sc[4], sh[4], mu[4], is[4], k1[4], k2[4], k3[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int c = 4 * cq + q;
-    sc[q] = scale[c]; sh[q] = shift[c]; mu[q] = mean[c]; is[q] = invstd[c];
-    if (APPLY) { k1[q] = coef[3 * c]; k2[q] = coef[3 * c + 1]; k3[q] = coef[3 * c + 2]; }
-  }
-  float4 g4 = reinterpret_cast<const float4*>(G)[(size_t)unit * C4 + cq];
-  for (int z = 1; z < gslabs; ++z) {  // split-K slabs of the producing GEMM, summed in z order
-    const float4 t = reinterpret_cast<const float4*>(G + (size_t)z * gstride)[(size_t)unit * C4 + cq];
-    g4.x += t.x; g4.y += t.y; g4.z += t.z; g4.w += t.w;
-  }
-  const float gin[4] = {g4.x, g4.y, g4.z, g4.w};
-  constexpr int NP = POOL ? 4 : 1;
-  size_t off[NP];
-  if (POOL) {
-    const int Wo = W >> 1, Ho = H >> 1;
-    const int wo = unit % Wo, ho = (unit / Wo) % Ho, b = unit / (Wo * Ho);
-    const size_t base = (((size_t)b * H + 2 * ho) * W + 2 * wo) * C4 + cq;
-    off[0] = base;
-    if (POOL) {
-      off[1 % NP] = base + C4;
-      off[2 % NP] = base + (size_t)W * C4;
-      off[3 % NP] = base + (size_t)W * C4 + C4;
-    }
-  } else {
-    off[0] = (size_t)unit * C4 + cq;
-  }
-  float yv[NP][4];
-#pragma unroll
-  for (int p = 0; p < NP; ++p) {
-    const float4 v = reinterpret_cast<const float4*>(y)[off[p]];
-    yv[p][0] = v.x; yv[p][1] = v.y; yv[p][2] = v.z; yv[p][3] = v.w;
-  }
-  float out[NP][4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    float z[NP];
-    int am = 0;
-#pragma unroll
-    for (int p = 0; p < NP; ++p) {
-      z[p] = fmaxf(yv[p][q] * sc[q] + sh[q], 0.f);
-      if (p > 0 && z[p] > z[am]) am = p;
-    }
-#pragma unroll
-    for (int p = 0; p < NP; ++p) {
-      const float g = (p == am && z[p] > 0.f) ? gin[q] : 0.f;
-      const float xh = (yv[p][q] - mu[q]) * is[q];
-      if (APPLY) {
-        out[p][q] = k1[q] * (g - k2[q] - xh * k3[q]);
-      } else {
-        acc[0][q] += g;
-        acc[1][q] += g * xh;
-        acc[2][q] += xh;
-      }
-    }
-  }
-  if (APPLY) {
-#pragma unroll
-    for (int p = 0; p < NP; ++p)
-      reinterpret_cast<float4*>(dz)[off[p]] = make_float4(out[p][0], out[p][1], out[p][2], out[p][3]);
-  }
-}
-
 template <bool APPLY, bool POOL>
 __global__ __launch_bounds__(256) void bn_bwd_kernel(const float* __restrict__ y, const float* __restrict__ G, int B,
                                                      int H, int W, int C, const float* __restrict__ scale,
@@ -199,6 +129,11 @@ __global__ __launch_bounds__(256) void bn_bwd_kernel(const float* __restrict__ y
                                                      float* __restrict__ dz, float* __restrict__ part, int gslabs,
                                                      int64_t gstride) {
   extern __shared__ __attribute__((aligned(16))) float red[];  // [rows][C][3] (reduce only)
+  if constexpr (!APPLY) {  // the shared body (also run inside weight-gradient GEMM launches)
+    const CsBnRed r{y, G, scale, shift, mean, invstd, part, gstride, B, H, W, C, POOL ? 1 : 0, (int)gridDim.x, gslabs};
+    cs_bn::bn_red_body<POOL>(r, blockIdx.x, gridDim.x, red);
+    return;
+  }
   const int C4 = C >> 2;
   const int rows = 256 / C4;  // C <= 1024
   const int cq = threadIdx.x % C4, rl = threadIdx.x / C4;
@@ -571,7 +506,6 @@ hipError_t cs_bn_bwd(const float* y, const float* G, int B, int H, int W, int C,
   const int P = cs_bn_bwd_blocks(B, H, W, C, pool);
   const int rows = 256 / (C / 4);
   const size_t lds = (size_t)rows * C * 3 * sizeof(float);
-  const int M = B * H * W;
   if (pool) {
     hipLaunchKernelGGL((bn_bwd_kernel<false, true>), dim3(P), dim3(256), lds, stream, y, G, B, H, W, C, scale, shift,
                        mean, invstd, nullptr, nullptr, part, gslabs, gstride);
@@ -579,6 +513,18 @@ hipError_t cs_bn_bwd(const float* y, const float* G, int B, int H, int W, int C,
     hipLaunchKernelGGL((bn_bwd_kernel<false, false>), dim3(P), dim3(256), lds, stream, y, G, B, H, W, C, scale, shift,
                        mean, invstd, nullptr, nullptr, part, gslabs, gstride);
   }
+  if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+  return cs_bn_bwd_tail(y, G, B, H, W, C, pool, scale, shift, mean, invstd, gamma, part, P, coef, dgamma, dbeta,
+                        dbias, dz, stream, gslabs, gstride);
+}
+
+hipError_t cs_bn_bwd_tail(const float* y, const float* G, int B, int H, int W, int C, int pool, const float* scale,
+                          const float* shift, const float* mean, const float* invstd, const float* gamma,
+                          const float* part, int P, float* coef, float* dgamma, float* dbeta, float* dbias, float* dz,
+                          hipStream_t stream, int gslabs, int64_t gstride) {
+  if (C % 4 != 0 || C > 1024 || (pool && ((H | W) & 1)) || gslabs < 1 || P < 1) return hipErrorInvalidValue;
+  const int M = B * H * W;
+  const int rows = 256 / (C / 4);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 3) / 4), dim3(256), 0, stream, part, P, C, M, gamma, invstd,
                      dgamma, dbeta, dbias, coef);
   // the apply pass is sized for bandwidth, independent of the reduce's P

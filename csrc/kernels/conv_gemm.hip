@@ -34,6 +34,7 @@
 
 #include <algorithm>
 
+#include "bn_device.h"
 #include "common.h"
 #include "launchers.h"
 
@@ -1018,7 +1019,17 @@ template <int BM, int BN, int MODE, int BK, int SCHED, bool C4, int GL, int KG =
 __global__ __launch_bounds__(256 * KG) void conv_gemm_kernel(CsConvArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int ntiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
-  gemm_body<BM, BN, MODE, BK, SCHED, C4, GL, KG>(a, cs::xcd_remap(blockIdx.x, ntiles), blockIdx.z, gridDim.z, smem);
+  // linear grid: ntiles x nsplit GEMM blocks (x fastest, as the old (ntiles, 1, nsplit) grid
+  // dispatched them), then red.P blocks of an independent BN-backward reduce that run in the
+  // GEMM's tail
+  const int nsplit = (a.total_ksteps + a.ksteps_per_split - 1) / a.ksteps_per_split;
+  const int ng = ntiles * nsplit, lin = blockIdx.x;
+  if (lin >= ng) {
+    if (a.red.pool) cs_bn::bn_red_body<true>(a.red, lin - ng, a.red.P, smem);
+    else cs_bn::bn_red_body<false>(a.red, lin - ng, a.red.P, smem);
+    return;
+  }
+  gemm_body<BM, BN, MODE, BK, SCHED, C4, GL, KG>(a, cs::xcd_remap(lin % ntiles, ntiles), lin / ntiles, nsplit, smem);
 }
 
 // Horizontal fusion of one block's two independent backward GEMMs: blocks [0, nb1) run the
@@ -1171,7 +1182,8 @@ int conv_sched() {
 
 template <int BM, int BN, int MODE, int BK, int SCHED, bool C4, int GL, int KG = 1>
 hipError_t launch_k(dim3 grid, size_t lds, hipStream_t stream, const CsConvArgs& a) {
-  hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, MODE, BK, SCHED, C4, GL, KG>), grid, dim3(256 * KG), lds, stream, a);
+  const size_t l = a.red.P > 0 ? std::max(lds, cs_bn_red_lds(a.red.C)) : lds;
+  hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, MODE, BK, SCHED, C4, GL, KG>), grid, dim3(256 * KG), l, stream, a);
   return hipGetLastError();
 }
 
@@ -1185,7 +1197,7 @@ hipError_t launch_gemm_m(const CsConvArgs& a, int splits, int stage, hipStream_t
   const size_t lds = MATH == 3   ? TileXS<BM, BN, MODE, BK>::BYTES
                      : MATH == 5 ? TileXS<BM, BN, MODE, BK, 1>::BYTES
                                  : 2 * T::STAGE * sizeof(float);
-  const dim3 grid(ntiles, 1, splits);
+  const dim3 grid(ntiles * splits + a.red.P);
   constexpr bool deep_fits = (BM + BN) * BK * 4 * 5 < 160 * 1024;
   if constexpr (BK != 64 && MATH == 0) {
     if (MODE == CS_CONV_FWD && a.w_oihw)  // padded conv0: Cin = 4 < BK
@@ -1419,6 +1431,7 @@ int prep_gemm(CsConvArgs& a, int mode, int bk, int splits) {
 
 hipError_t cs_conv_gemm_dual(CsConvArgs wg, int wbk, int wsplits, CsConvArgs dg, int dbk, int dsplits,
                              hipStream_t stream, int stage) {
+  if (wg.red.P != 0 || dg.red.P != 0) return hipErrorInvalidValue;  // no appended reduce in dual launches
   if (wg.w_oihw) return hipErrorInvalidValue;  // conv0 has no data gradient
   wg.counters = dg.counters = nullptr;
   const int s1 = prep_gemm(wg, CS_CONV_WGRAD, wbk, wsplits), s2 = prep_gemm(dg, CS_CONV_DGRAD, dbk, dsplits);

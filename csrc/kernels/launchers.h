@@ -38,6 +38,16 @@ hipError_t cs_softmax_xent(const float* logits, const int64_t* labels, int B, in
 // ---------------------------------------------------------------- conv (implicit GEMM, fp32 MFMA)
 enum { CS_CONV_FWD = 0, CS_CONV_DGRAD = 1, CS_CONV_WGRAD = 2 };
 
+// One BN-backward partial-sum pass (bn.hip "reduce"): y, incoming gradient G (optionally as
+// gslabs split-K slabs gstride apart), the forward's scale/shift/mean/invstd, partials out
+// part [P][C][3]. P == 0: none.
+struct CsBnRed {
+  const float *y, *G, *scale, *shift, *mean, *invstd;
+  float* part;
+  int64_t gstride;
+  int B, H, W, C, pool, P, gslabs;
+};
+
 struct CsConvArgs {
   const float* x;     // FWD / WGRAD: conv input, NHWC [B,H,W,Cin] (Cin = 4 for the padded conv0 input)
   const float* w;     // FWD / DGRAD: weights, OHWI [Cout][9][Cin]; conv0 (w_oihw=1): OIHW [Cout][3][9]
@@ -50,6 +60,9 @@ struct CsConvArgs {
   int B, H, W, Cin, Cout;
   int w_oihw;
   int keep_slabs;  // split-K: leave the <= 32 fp32 slabs in ws for the consumer to sum (no reduce launch)
+  // extra blocks after the GEMM tiles (dispatched last, they fill the GEMM's tail): an
+  // independent BN-backward reduce (the block below's), red.P blocks; red.P == 0: none
+  CsBnRed red;
   // filled by the launcher:
   int lgH, lgW, lgCin, lgCout, M, N, K, ksteps_per_split, total_ksteps;
 };
@@ -106,6 +119,14 @@ hipError_t cs_bn_apply(const float* y, const float* scale, const float* shift, f
                        int pool, hipStream_t stream);
 int cs_bn_bwd_blocks(int B, int H, int W, int C, int pool);
 // part: [cs_bn_bwd_blocks][C][3] scratch; coef: [C][3] scratch; dgamma/dbeta/dbias may be null.
+// LDS bytes the BN-backward reduce body needs (C channels)
+inline size_t cs_bn_red_lds(int C) { return (size_t)(256 / (C / 4)) * C * 3 * sizeof(float); }
+// finalize + apply of the BN backward when the reduce already ran (part from P blocks, e.g.
+// appended to the weight-gradient GEMM launch of the block above)
+hipError_t cs_bn_bwd_tail(const float* y, const float* G, int B, int H, int W, int C, int pool, const float* scale,
+                          const float* shift, const float* mean, const float* invstd, const float* gamma,
+                          const float* part, int P, float* coef, float* dgamma, float* dbeta, float* dbias, float* dz,
+                          hipStream_t stream, int gslabs = 1, int64_t gstride = 0);
 // G may be split-K slabs of the data-gradient GEMM: G = sum_{z < gslabs} G[z * gstride + i]
 // (summed in z order, bit-equal to the split-K combine launch it replaces)
 hipError_t cs_bn_bwd(const float* y, const float* G, int B, int H, int W, int C, int pool, const float* scale,

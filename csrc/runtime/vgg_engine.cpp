@@ -182,6 +182,7 @@ VggEngine::VggEngine(int64_t Bmax, std::vector<int64_t> desc, std::vector<int64_
   if (const char* e = getenv("CS_CONV_MATH")) math_ = atoi(e);
   if (const char* e = getenv("CS_BN_PATH")) bn_path_ = atoi(e);
   if (const char* e = getenv("CS_KEEP_SLABS")) keep_slabs_ = atoi(e) != 0;
+  if (const char* e = getenv("CS_FUSE_BN_RED")) fuse_red_ = atoi(e) != 0;
   bn_part_ = torch::zeros({partmax}, fo);
   bn_coef_ = torch::zeros({cmax * 3}, fo);
   bn_eval_ = torch::zeros({2, cmax}, fo);
@@ -266,10 +267,11 @@ void VggEngine::set_perm(torch::Tensor perm) {
 }
 
 void VggEngine::conv(int l, int mode, int B, const ConvTile& t, hipStream_t s, bool with_stats, float* ws,
-                     float* dz, bool keep_slabs) {
+                     float* dz, bool keep_slabs, const CsBnRed* red) {
   VggBlock& b = blocks_[l];
   CsConvArgs a = conv_args(l, mode, B, with_stats, ws, dz);
   a.keep_slabs = keep_slabs ? 1 : 0;
+  if (red != nullptr) a.red = *red;
   const Dims d = dims(b, mode, B);
   const int sp = eff_splits(d.K, t.splits, t.bk);
   TORCH_CHECK(sp == 1 || (int64_t)sp * d.M * d.N <= ws_elems_, "VggEngine: split-K workspace too small");
@@ -302,6 +304,7 @@ void VggEngine::forward_train(int64_t B) {
   hipStream_t s = cur_stream();
   const int L = (int)blocks_.size();
   g_slabs_ = 1;  // the head writes the top block's gradient to gbuf_
+  red_pending_ = -1;
   // one launch: sampler index (device cursor into the epoch permutation, or idx_ when no
   // permutation is set), label gather, crop/flip/normalize into block 0's NHWC input
   const bool use_perm = perm_len_ > 0;
@@ -366,7 +369,12 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
     const int gs = g_slabs_;
     const float* Gin = gs > 1 ? ws_.data_ptr<float>() : gbuf_[(L - 1 - l) % 2].data_ptr<float>();
     TORCH_CHECK(gs == 1 || bn_path_ == 0, "VggEngine: kept split-K slabs need the default BN path");
-    if (bn_fused(l, B)) {  // reduce + finalize + apply in one launch
+    if (red_pending_ == l) {  // the partial sums already ran inside the weight-gradient launch above
+      ok(cs_bn_bwd_tail(b.y.data_ptr<float>(), Gin, (int)B, b.H, b.H, b.cout, b.pool, bn, bn + b.cout,
+                        bn + 2 * b.cout, bn + 3 * b.cout, P(b.g_off), bn_part_.data_ptr<float>(), red_P_,
+                        bn_coef_.data_ptr<float>(), G(b.g_off), G(b.be_off), G(b.b_off), dz, s, gs, g_stride_),
+         "bn_bwd_tail");
+    } else if (bn_fused(l, B)) {  // reduce + finalize + apply in one launch
       ok(cs_bn_fused_bwd(b.y.data_ptr<float>(), Gin, (int)B, b.H, b.H, b.cout, b.pool, bn, P(b.g_off),
                          bn_coef_.data_ptr<float>(), G(b.g_off), G(b.be_off), G(b.b_off), dz, s, gs, g_stride_),
          "bn_fused_bwd");
@@ -381,8 +389,42 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
          "bn_bwd");
     }
     g_slabs_ = 1;
+    red_pending_ = -1;
     if (!overlap_wgrad_ && dual_ok(l)) {  // wgrad + dgrad in one launch
       conv_dual(l, (int)B, s, dz);
+      continue;
+    }
+    if (fuse_red_ && !overlap_wgrad_ && bn_path_ == 0 && l > 0 && !bn_fused(l - 1, B)) {
+      // dgrad(l) first, then wgrad(l) carrying block l-1's BN partial-sum pass
+      const ConvTile& t = b.tile[CS_CONV_DGRAD];
+      const Dims d = dims(b, CS_CONV_DGRAD, B);
+      const int sp = eff_splits(d.K, t.splits, t.bk);
+      const bool keep = keep_slabs_ && sp > 1 && sp <= 32;
+      conv(l, CS_CONV_DGRAD, (int)B, t, s, false, nullptr, dz, keep);
+      if (keep) {
+        g_slabs_ = sp;
+        g_stride_ = d.M * d.N;
+      }
+      VggBlock& c = blocks_[l - 1];
+      float* cb = c.bn.data_ptr<float>();
+      CsBnRed r{};
+      r.y = c.y.data_ptr<float>();
+      r.G = g_slabs_ > 1 ? ws_.data_ptr<float>() : gbuf_[(L - l) % 2].data_ptr<float>();
+      r.scale = cb;
+      r.shift = cb + c.cout;
+      r.mean = cb + 2 * c.cout;
+      r.invstd = cb + 3 * c.cout;
+      r.part = bn_part_.data_ptr<float>();
+      r.gstride = g_stride_;
+      r.B = (int)B;
+      r.H = r.W = (int)c.H;
+      r.C = (int)c.cout;
+      r.pool = c.pool;
+      r.P = cs_bn_bwd_blocks((int)B, (int)c.H, (int)c.H, (int)c.cout, c.pool);
+      r.gslabs = g_slabs_;
+      conv(l, CS_CONV_WGRAD, (int)B, b.tile[CS_CONV_WGRAD], s, false, ws_side_.data_ptr<float>(), dz, false, &r);
+      red_pending_ = l - 1;
+      red_P_ = r.P;
       continue;
     }
     if (overlap_wgrad_) {

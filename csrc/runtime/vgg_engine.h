@@ -130,7 +130,13 @@ class VggEngine {
 
  private:
   void conv(int l, int mode, int B, const ConvTile& t, hipStream_t s, bool with_stats, float* ws = nullptr,
-            float* dz = nullptr, bool keep_slabs = false);
+            float* dz = nullptr, bool keep_slabs = false, const CsBnRed* red = nullptr);
+  // Backward order dgrad(l) -> wgrad(l) with block l-1's BN partial-sum pass appended to the
+  // wgrad launch (extra blocks dispatched after the GEMM tiles, filling its tail): one launch
+  // per block fewer on the critical chain, bit-identical partials (CS_FUSE_BN_RED=0 disables)
+  bool fuse_red_ = true;
+  int red_pending_ = -1;  // block whose BN partials already sit in bn_part_ (from red_P_ blocks)
+  int red_P_ = 0;
   CsConvArgs conv_args(int l, int mode, int B, bool with_stats, float* ws, float* dz);
   // block l's wgrad + dgrad as one launch (both 64x64 register-staged tiles)
   bool dual_ok(int l) const;

@@ -295,3 +295,24 @@ def test_bf16_mode_tracks_fp32(dev):
     assert abs(a.last_loss() - b.last_loss()) <= 1e-2 * abs(a.last_loss())
     ga, gb = a.grads.double(), b.grads.double()
     assert (ga @ gb / (ga.norm() * gb.norm())).item() > 0.95
+
+
+@pytest.mark.parametrize("keep", ["0", "1"])
+def test_bn_reduce_in_wgrad_launch_bitwise_equal(dev, keep, monkeypatch):
+    # block l-1's BN partial-sum pass appended to block l's weight-gradient launch (extra blocks
+    # after the GEMM tiles) == the standalone reduce launch, bit for bit (also with kept slabs)
+    monkeypatch.setenv("CS_KEEP_SLABS", keep)
+    out = []
+    for fuse in ("0", "1"):
+        monkeypatch.setenv("CS_FUSE_BN_RED", fuse)
+        t = _trainer(dev, batch_size=32, train_size=256)
+        for l in range(1, t.layout.L):  # wgrad launches of both block sizes: 1024-thread X6S, 256-thread f32
+            if l % 2:
+                t.engine.set_tile(l, 2, 64, 64, 2, 64, 16 | 4)
+            t.engine.set_tile(l, 1, 64, 64, 2, 16, 0)
+        for _ in range(3):
+            t.step()
+        torch.cuda.synchronize()
+        out.append((t.params.clone(), t.mom.clone(), t.bufs.clone()))
+    for a, b in zip(out[0], out[1]):
+        assert torch.equal(a, b)
