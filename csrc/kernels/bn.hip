@@ -16,6 +16,7 @@
 //   sum_m dZ = -gamma*invstd*mean(g*xhat)*sum(xhat)) and the dZ coefficients;
 //   bn_bwd_apply writes dZ = gamma*invstd*(g - mean(g) - xhat*mean(g*xhat)).
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.h"
 #include "launchers.h"
@@ -37,6 +38,65 @@ __device__ __forceinline__ void chan_combine(float& n, float& m, float& M2, floa
   n = nn;
 }
 
+// scale/shift, saved batch statistics and the running-stat update of channel c from its
+// combined (count, mean, M2)
+// gamma / beta / running stats of channel c, loaded at kernel entry so their memory latency
+// overlaps the partial-sum gather instead of following it
+struct FinChan {
+  float g = 0.f, b = 0.f, rm = 0.f, rv = 0.f;
+};
+__device__ __forceinline__ FinChan finalize_load(int c, int C, const float* __restrict__ gamma,
+                                                 const float* __restrict__ beta, const float* running_mean,
+                                                 const float* running_var) {
+  FinChan f;
+  if (c < C) {
+    f.g = gamma[c];
+    f.b = beta[c];
+    if (running_mean != nullptr) {
+      f.rm = running_mean[c];
+      f.rv = running_var[c];
+    }
+  }
+  return f;
+}
+
+__device__ __forceinline__ void finalize_store(int c, float n, float m, float M2, const FinChan& f,
+                                               float* running_mean, float* running_var, float momentum, float eps,
+                                               float* __restrict__ scale, float* __restrict__ shift,
+                                               float* __restrict__ save_mean, float* __restrict__ save_invstd) {
+  const float var = M2 / n;
+  const float inv = 1.0f / sqrtf(var + eps);
+  scale[c] = f.g * inv;
+  shift[c] = f.b - m * f.g * inv;
+  save_mean[c] = m;
+  save_invstd[c] = inv;
+  if (running_mean != nullptr) {
+    const float unb = n > 1.f ? M2 / (n - 1.f) : var;
+    running_mean[c] = (1.f - momentum) * f.rm + momentum * m;
+    running_var[c] = (1.f - momentum) * f.rv + momentum * unb;
+  }
+}
+
+// Chan-combine channel c's partials t = first, first + stride, ... (tile t covers rows
+// [t*R, min(t*R+R, M))). The loads of 8 tiles are issued before any combine: a plain loop
+// waits one full memory latency per tile (measured ~0.6 us each on conv0's 16 tiles per lane).
+__device__ __forceinline__ void finalize_gather(const float* __restrict__ part, int T, int R, int M, int C, int c,
+                                                int first, int stride, float& n, float& m, float& M2) {
+  for (int t0 = first; t0 < T; t0 += 8 * stride) {
+    float2 v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int t = t0 + j * stride;
+      v[j] = t < T ? *reinterpret_cast<const float2*>(part + ((size_t)t * C + c) * 2) : make_float2(0.f, 0.f);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int t = t0 + j * stride;
+      if (t < T) chan_combine(n, m, M2, (float)((M - t * R) < R ? (M - t * R) : R), v[j].x, v[j].y);
+    }
+  }
+}
+
 // 256 threads = 4 waves = 4 channels; the 64 lanes of a channel's wave each combine every
 // 64th tile partial, then a 6-step butterfly (fixed order: deterministic). One wave per
 // channel keeps even conv0's 1024-4096 partials per channel to <= 64 serial combines.
@@ -50,32 +110,51 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restric
   const int lane = threadIdx.x & 63;
   const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
   float n = 0.f, m = 0.f, M2 = 0.f;
-  if (c < C) {
-    for (int t = lane; t < T; t += 64) {
-      const int cnt = (M - t * R) < R ? (M - t * R) : R;
-      const float2 pm = *reinterpret_cast<const float2*>(part + ((size_t)t * C + c) * 2);
-      chan_combine(n, m, M2, (float)cnt, pm.x, pm.y);
-    }
-  }
+  const FinChan fc = finalize_load(c, C, gamma, beta, running_mean, running_var);
+  if (c < C) finalize_gather(part, T, R, M, C, c, lane, 64, n, m, M2);
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
     const float nb = __shfl_xor(n, off, 64), mb = __shfl_xor(m, off, 64), M2b = __shfl_xor(M2, off, 64);
     chan_combine(n, m, M2, nb, mb, M2b);
   }
-  if (lane == 0 && c < C) {
-    const float var = M2 / n;
-    const float inv = 1.0f / sqrtf(var + eps);
-    const float g = gamma[c], b = beta[c];
-    scale[c] = g * inv;
-    shift[c] = b - m * g * inv;
-    save_mean[c] = m;
-    save_invstd[c] = inv;
-    if (running_mean != nullptr) {
-      const float unb = n > 1.f ? M2 / (n - 1.f) : var;
-      running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * m;
-      running_var[c] = (1.f - momentum) * running_var[c] + momentum * unb;
+  if (lane == 0 && c < C)
+    finalize_store(c, n, m, M2, fc, running_mean, running_var, momentum, eps, scale, shift, save_mean, save_invstd);
+  if (nbt != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *nbt += 1;
+}
+
+// Many-partials variant (conv0: 4096 row tiles x 64 channels at B=64). The one-wave-per-channel
+// kernel reads each channel's partials at a C*8-byte stride (one cache line per lane per load)
+// from only C waves; here a 1024-thread block owns 8 consecutive channels and 128 tile slices,
+// so every wave load covers 8 tiles x 64 contiguous bytes, and the 128 slice states are combined
+// through LDS in a fixed tree (deterministic).
+constexpr int kFinWideC = 8, kFinWideS = 128;
+__global__ __launch_bounds__(1024) void bn_finalize_wide_kernel(
+    const float* __restrict__ part, int T, int R, int M, int C, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float* running_mean, float* running_var, int64_t* nbt, float momentum, float eps,
+    float* __restrict__ scale, float* __restrict__ shift, float* __restrict__ save_mean,
+    float* __restrict__ save_invstd) {
+  __shared__ float sn[kFinWideS][kFinWideC], sm[kFinWideS][kFinWideC], sM2[kFinWideS][kFinWideC];
+  const int cl = threadIdx.x % kFinWideC, sl = threadIdx.x / kFinWideC;
+  const int c = blockIdx.x * kFinWideC + cl;
+  float n = 0.f, m = 0.f, M2 = 0.f;
+  const FinChan fc = finalize_load(c, C, gamma, beta, running_mean, running_var);
+  if (c < C) finalize_gather(part, T, R, M, C, c, sl, kFinWideS, n, m, M2);
+  sn[sl][cl] = n;
+  sm[sl][cl] = m;
+  sM2[sl][cl] = M2;
+  __syncthreads();
+#pragma unroll
+  for (int h = kFinWideS / 2; h > 0; h >>= 1) {
+    if (sl < h) {
+      chan_combine(n, m, M2, sn[sl + h][cl], sm[sl + h][cl], sM2[sl + h][cl]);
+      sn[sl][cl] = n;
+      sm[sl][cl] = m;
+      sM2[sl][cl] = M2;
     }
+    __syncthreads();
   }
+  if (sl == 0 && c < C)
+    finalize_store(c, n, m, M2, fc, running_mean, running_var, momentum, eps, scale, shift, save_mean, save_invstd);
   if (nbt != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *nbt += 1;
 }
 
@@ -168,19 +247,32 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
   const int lane = threadIdx.x & 63;
   const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
   float sg = 0.f, sgx = 0.f, sx = 0.f;
+  // per-channel operands first, then 8 partial loads in flight per lane (same summation order)
+  const float gam = c < C ? gamma[c] : 0.f, ist = c < C ? invstd[c] : 0.f;
   if (c < C) {
-    for (int p = lane; p < P; p += 64) {
-      const float* q = part + ((size_t)p * C + c) * 3;
-      sg += q[0];
-      sgx += q[1];
-      sx += q[2];
+    for (int p0 = lane; p0 < P; p0 += 8 * 64) {
+      float v[8][3];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int p = p0 + j * 64;
+        const float* q = part + ((size_t)p * C + c) * 3;
+        v[j][0] = p < P ? q[0] : 0.f;
+        v[j][1] = p < P ? q[1] : 0.f;
+        v[j][2] = p < P ? q[2] : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        sg += v[j][0];
+        sgx += v[j][1];
+        sx += v[j][2];
+      }
     }
   }
   sg = cs::wave_sum(sg);
   sgx = cs::wave_sum(sgx);
   sx = cs::wave_sum(sx);
   if (lane != 0 || c >= C) return;
-  const float k1 = gamma[c] * invstd[c], k2 = sg / (float)M, k3 = sgx / (float)M;
+  const float k1 = gam * ist, k2 = sg / (float)M, k3 = sgx / (float)M;
   if (dgamma) dgamma[c] = sgx;
   if (dbeta) dbeta[c] = sg;
   if (dbias) dbias[c] = -k1 * k3 * sx;
@@ -473,11 +565,25 @@ int cs_bn_bwd_blocks(int B, int H, int W, int C, int pool) {
   return blocks < 256 ? blocks : 256;
 }
 
+// CS_BN_FIN_WIDE: partial count from which the 8-channel / 1024-thread finalize runs (0 = never)
+static int bn_finalize_wide_min() {
+  static const int v = [] {
+    const char* e = getenv("CS_BN_FIN_WIDE");
+    const int x = e ? atoi(e) : 512;
+    return x > 0 ? x : (1 << 30);
+  }();
+  return v;
+}
+
 hipError_t cs_bn_finalize(const float* part, int T, int R, int M, int C, const float* gamma, const float* beta,
                           float* running_mean, float* running_var, int64_t* nbt, float momentum, float eps,
                           float* scale, float* shift, float* save_mean, float* save_invstd, hipStream_t stream) {
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 3) / 4), dim3(256), 0, stream, part, T, R, M, C, gamma, beta,
-                     running_mean, running_var, nbt, momentum, eps, scale, shift, save_mean, save_invstd);
+  if (T >= bn_finalize_wide_min() && C % kFinWideC == 0)
+    hipLaunchKernelGGL(bn_finalize_wide_kernel, dim3(C / kFinWideC), dim3(1024), 0, stream, part, T, R, M, C, gamma,
+                       beta, running_mean, running_var, nbt, momentum, eps, scale, shift, save_mean, save_invstd);
+  else
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 3) / 4), dim3(256), 0, stream, part, T, R, M, C, gamma, beta,
+                       running_mean, running_var, nbt, momentum, eps, scale, shift, save_mean, save_invstd);
   return hipGetLastError();
 }
 

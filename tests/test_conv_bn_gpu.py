@@ -182,3 +182,36 @@ def test_bn_eval(dev):
     out = Fn.bn_relu_pool_eval(_nhwc(y).float().to(dev).view(-1, C), B, H, H, f(gamma), f(beta), f(rm), f(rv),
                                pool=True)
     _close(out, ref.permute(0, 2, 3, 1), 1e-5)
+
+
+@pytest.mark.parametrize("B,H,C,R", [(64, 32, 64, 16), (64, 32, 64, 7), (3, 32, 64, 1), (8, 16, 128, 2),
+                                     (16, 16, 68, 2), (64, 16, 128, 16)])
+def test_bn_finalize_many_partials(dev, B, H, C, R):
+    # thousands of row-tile partials (conv0's 4096 at B=64): the 8-channel / 1024-thread finalize
+    # (T >= 2048, C % 8 == 0), ragged last tiles, and the one-wave-per-channel fallback (C = 68)
+    from cs744_pytorch_distributed_tutorial_amd.ops import functional as Fn
+    torch.manual_seed(B * C + R)
+    y = torch.randn(B, C, H, H, dtype=torch.float64) * 3 + 1.5
+    gamma, beta = torch.rand(C, dtype=torch.float64) + 0.5, torch.randn(C, dtype=torch.float64)
+    rm, rv = torch.zeros(C, dtype=torch.float64), torch.ones(C, dtype=torch.float64)
+    z = F.relu(F.batch_norm(y, rm, rv, gamma, beta, training=True, momentum=0.1, eps=1e-5))
+    yd = _nhwc(y).float().to(dev).view(-1, C)
+    M = yd.shape[0]
+    T = (M + R - 1) // R
+    yp = torch.cat([yd.double(), torch.zeros(T * R - M, C, dtype=torch.float64, device=dev)])
+    cnt = torch.full((T,), float(R), dtype=torch.float64, device=dev)
+    cnt[-1] = M - (T - 1) * R
+    seg = yp.view(T, R, C)
+    mu_t = seg.sum(1) / cnt[:, None]
+    valid = (torch.arange(T * R, device=dev) < M).view(T, R, 1)
+    m2_t = (((seg - mu_t[:, None]) ** 2) * valid).sum(1)
+    st = torch.stack([mu_t, m2_t], 2).float().contiguous()
+    rmd, rvd = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+    nbt = torch.zeros((), dtype=torch.int64, device=dev)
+    out, bst = Fn.bn_relu_pool_fwd(yd, st, R, B, H, H, gamma.float().to(dev), beta.float().to(dev), rmd, rvd, nbt,
+                                   pool=False)
+    _close(out, z.permute(0, 2, 3, 1), 1e-5)
+    _close(bst.mean, y.mean((0, 2, 3)), 1e-5)
+    _close(rmd, rm, 1e-5)
+    _close(rvd, rv, 1e-5)
+    assert int(nbt) == 1
