@@ -1064,11 +1064,17 @@ __global__ __launch_bounds__(256) void splitk_fold_kernel(float* __restrict__ ws
   const int z1 = min(splits, z0 + kFold);
   float4* w4 = reinterpret_cast<float4*>(ws);
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
-    float4 acc = w4[(size_t)z0 * n4 + i];
-    for (int z = z0 + 1; z < z1; ++z) {
-      const float4 t = w4[(size_t)z * n4 + i];
-      acc.x += t.x; acc.y += t.y; acc.z += t.z; acc.w += t.w;
-    }
+    // every load of the group in flight before the adds (same ascending-z order)
+    float4 t[kFold];
+#pragma unroll
+    for (int j = 0; j < kFold; ++j)
+      t[j] = z0 + j < z1 ? w4[(size_t)(z0 + j) * n4 + i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 acc = t[0];
+#pragma unroll
+    for (int j = 1; j < kFold; ++j)
+      if (z0 + j < z1) {
+        acc.x += t[j].x; acc.y += t[j].y; acc.z += t[j].z; acc.w += t[j].w;
+      }
     w4[(size_t)z0 * n4 + i] = acc;
   }
 }
@@ -1083,13 +1089,24 @@ __device__ __forceinline__ void splitk_reduce_body(const CsConvArgs& a, int mode
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   const bool in = m < a.M && n < a.N;
   if (in) {
+    const bool add_bias = mode == CS_CONV_FWD && a.bias != nullptr;
+    const float4 bv = add_bias ? *reinterpret_cast<const float4*>(a.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
     const float* p = a.ws + (size_t)m * a.N + n;
-    for (int z = 0; z < nslab; ++z) {
-      const float4 t = *reinterpret_cast<const float4*>(p + (size_t)z * zstep * slab);
-      acc.x += t.x; acc.y += t.y; acc.z += t.z; acc.w += t.w;
+    // 8 slab loads in flight before the adds (a plain loop waits one memory latency per
+    // slab); the summation order is unchanged: z ascending, then the bias
+    for (int z0 = 0; z0 < nslab; z0 += 8) {
+      float4 t[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        t[j] = z0 + j < nslab ? *reinterpret_cast<const float4*>(p + (size_t)(z0 + j) * zstep * slab)
+                              : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (z0 + j < nslab) {
+          acc.x += t[j].x; acc.y += t[j].y; acc.z += t[j].z; acc.w += t[j].w;
+        }
     }
-    if (mode == CS_CONV_FWD && a.bias != nullptr) {
-      const float4 bv = *reinterpret_cast<const float4*>(a.bias + n);
+    if (add_bias) {
       acc.x += bv.x; acc.y += bv.y; acc.z += bv.z; acc.w += bv.w;
     }
     if (mode == CS_CONV_WGRAD && a.w_oihw) {
