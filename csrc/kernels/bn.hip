@@ -38,8 +38,6 @@ __device__ __forceinline__ void chan_combine(float& n, float& m, float& M2, floa
   n = nn;
 }
 
-// scale/shift, saved batch statistics and the running-stat update of channel c from its
-// combined (count, mean, M2)
 // gamma / beta / running stats of channel c, loaded at kernel entry so their memory latency
 // overlaps the partial-sum gather instead of following it
 struct FinChan {
@@ -60,6 +58,8 @@ __device__ __forceinline__ FinChan finalize_load(int c, int C, const float* __re
   return f;
 }
 
+// scale/shift, saved batch statistics and the running-stat update of channel c from its
+// combined (count, mean, M2)
 __device__ __forceinline__ void finalize_store(int c, float n, float m, float M2, const FinChan& f,
                                                float* running_mean, float* running_var, float momentum, float eps,
                                                float* __restrict__ scale, float* __restrict__ shift,
@@ -360,6 +360,44 @@ __global__ __launch_bounds__(256) void bn_fused_fwd_kernel(const float* __restri
   __shared__ float4 sc_sh[2][4];
   const int cq = threadIdx.x & 3, rl = threadIdx.x >> 2;
   const int cqg = blockIdx.x * 4 + cq;  // global channel quad
+  const bool lead = blockIdx.y == 0;
+  const int C4 = C >> 2;
+  const int Ho = pool ? H >> 1 : H, Wo = pool ? W >> 1 : W;
+  const int u0 = blockIdx.y * upb + rl;
+  const int u_end = min(B * Ho * Wo, (int)(blockIdx.y + 1) * upb);
+  const float4* y4 = reinterpret_cast<const float4*>(y);
+  // Everything that does not depend on the statistics is loaded first, so its memory latency
+  // overlaps the partial gather: this block's first y rows (4 units without pooling, the first
+  // unit's 2x2 window with it) and the lead threads' per-channel operands
+  float4 pre[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) pre[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (!pool) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (u0 + 64 * j < u_end) pre[j] = y4[(size_t)(u0 + 64 * j) * C4 + cqg];
+  } else if (u0 < u_end) {
+    const int wo = u0 % Wo, ho = (u0 / Wo) % Ho, b = u0 / (Wo * Ho);
+    const size_t base = (((size_t)b * H + 2 * ho) * W + 2 * wo) * C4 + cqg;
+    pre[0] = y4[base];
+    pre[1] = y4[base + C4];
+    pre[2] = y4[base + (size_t)W * C4];
+    pre[3] = y4[base + (size_t)W * C4 + C4];
+  }
+  float gq[4] = {0.f, 0.f, 0.f, 0.f}, bq[4] = {0.f, 0.f, 0.f, 0.f}, rmq[4] = {0.f, 0.f, 0.f, 0.f},
+        rvq[4] = {0.f, 0.f, 0.f, 0.f};
+  if (threadIdx.x < 4) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int c = 4 * cqg + q;
+      gq[q] = gamma[c];
+      bq[q] = beta[c];
+      if (lead && running_mean != nullptr) {
+        rmq[q] = running_mean[c];
+        rvq[q] = running_var[c];
+      }
+    }
+  }
   float n[4] = {0.f, 0.f, 0.f, 0.f}, m[4] = {0.f, 0.f, 0.f, 0.f}, M2[4] = {0.f, 0.f, 0.f, 0.f};
   for (int t = rl; t < T; t += 64) {
     const int cnt = (M - t * R) < R ? (M - t * R) : R;
@@ -370,15 +408,14 @@ __global__ __launch_bounds__(256) void bn_fused_fwd_kernel(const float* __restri
     }
   }
   chan_reduce_block(n, m, M2, lds);
-  const bool lead = blockIdx.y == 0;
   if (threadIdx.x < 4) {
     float sc[4], sh[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int c = 4 * cqg + q;
       const float var = M2[q] / n[q], inv = 1.0f / sqrtf(var + eps);
-      sc[q] = gamma[c] * inv;
-      sh[q] = beta[c] - m[q] * gamma[c] * inv;
+      sc[q] = gq[q] * inv;
+      sh[q] = bq[q] - m[q] * gq[q] * inv;
       if (!lead) continue;
       bnv[c] = sc[q];
       bnv[C + c] = sh[q];
@@ -386,8 +423,8 @@ __global__ __launch_bounds__(256) void bn_fused_fwd_kernel(const float* __restri
       bnv[3 * C + c] = inv;
       if (running_mean != nullptr) {
         const float unb = n[q] > 1.f ? M2[q] / (n[q] - 1.f) : var;
-        running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * m[q];
-        running_var[c] = (1.f - momentum) * running_var[c] + momentum * unb;
+        running_mean[c] = (1.f - momentum) * rmq[q] + momentum * m[q];
+        running_var[c] = (1.f - momentum) * rvq[q] + momentum * unb;
       }
     }
     sc_sh[0][cq] = make_float4(sc[0], sc[1], sc[2], sc[3]);
@@ -396,11 +433,19 @@ __global__ __launch_bounds__(256) void bn_fused_fwd_kernel(const float* __restri
   if (nbt != nullptr && lead && blockIdx.x == 0 && threadIdx.x == 0) *nbt += 1;
   __syncthreads();
   const float4 s = sc_sh[0][cq], t = sc_sh[1][cq];
-  const int C4 = C >> 2;
-  const int Ho = pool ? H >> 1 : H, Wo = pool ? W >> 1 : W;
-  const int u_end = min(B * Ho * Wo, (int)(blockIdx.y + 1) * upb);
-  const float4* y4 = reinterpret_cast<const float4*>(y);
-  for (int u = blockIdx.y * upb + rl; u < u_end; u += 64) {
+  float4* out4 = reinterpret_cast<float4*>(out);
+  if (!pool) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (u0 + 64 * j < u_end) out4[(size_t)(u0 + 64 * j) * C4 + cqg] = bnrelu4(pre[j], s, t);
+  } else if (u0 < u_end) {
+    const float4 a0 = bnrelu4(pre[0], s, t), a1 = bnrelu4(pre[1], s, t);
+    const float4 a2 = bnrelu4(pre[2], s, t), a3 = bnrelu4(pre[3], s, t);
+    out4[(size_t)u0 * C4 + cqg] =
+        make_float4(fmaxf(fmaxf(a0.x, a1.x), fmaxf(a2.x, a3.x)), fmaxf(fmaxf(a0.y, a1.y), fmaxf(a2.y, a3.y)),
+                    fmaxf(fmaxf(a0.z, a1.z), fmaxf(a2.z, a3.z)), fmaxf(fmaxf(a0.w, a1.w), fmaxf(a2.w, a3.w)));
+  }
+  for (int u = u0 + (pool ? 64 : 256); u < u_end; u += 64) {
     float4 r;
     if (!pool) {
       r = bnrelu4(y4[(size_t)u * C4 + cqg], s, t);
