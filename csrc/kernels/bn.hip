@@ -469,6 +469,7 @@ __global__ __launch_bounds__(256) void bn_fused_bwd_kernel(const float* __restri
                                                            float* __restrict__ dbias, float* __restrict__ dz,
                                                            int gslabs, int64_t gstride) {
   __shared__ float lds[4 * 4 * 3 * 4];
+  __shared__ float coef_sh[3 * kFusedCh];  // this block's 16 channels' dZ coefficients
   const int cq = threadIdx.x & 3, rl = threadIdx.x >> 2;
   const int cqg = blockIdx.x * 4 + cq;
   const float* scale = bnv;
@@ -476,28 +477,38 @@ __global__ __launch_bounds__(256) void bn_fused_bwd_kernel(const float* __restri
   const float* mean = bnv + 2 * C;
   const float* invstd = bnv + 3 * C;
   const int units = POOL ? B * (H >> 1) * (W >> 1) : B * H * W;
+  // gamma * invstd loaded up front (its latency overlaps the reduce pass)
+  float k1q[4] = {0.f, 0.f, 0.f, 0.f};
+  if (threadIdx.x < 4)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) k1q[q] = gamma[4 * cqg + q] * invstd[4 * cqg + q];
   float acc[3][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
   for (int u = rl; u < units; u += 64)
     bwd_visit<false, POOL>(y, G, B, H, W, C, cqg, u, scale, shift, mean, invstd, coef, dz, acc, gslabs, gstride);
   sum_reduce_block(acc, lds);
+  const int c0 = blockIdx.x * kFusedCh;
   if (threadIdx.x < 4) {
     const float Mf = (float)(B * H * W);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int c = 4 * cqg + q;
-      const float k1 = gamma[c] * invstd[c], k2 = acc[0][q] / Mf, k3 = acc[1][q] / Mf;
+      const float k1 = k1q[q], k2 = acc[0][q] / Mf, k3 = acc[1][q] / Mf;
       if (dgamma) dgamma[c] = acc[1][q];
       if (dbeta) dbeta[c] = acc[0][q];
       if (dbias) dbias[c] = -k1 * k3 * acc[2][q];
       coef[3 * c] = k1;
       coef[3 * c + 1] = k2;
       coef[3 * c + 2] = k3;
+      coef_sh[3 * (c - c0)] = k1;
+      coef_sh[3 * (c - c0) + 1] = k2;
+      coef_sh[3 * (c - c0) + 2] = k3;
     }
   }
-  __syncthreads();  // coef (global, written by this block) is visible to the whole workgroup
+  __syncthreads();  // the apply pass reads the coefficients from LDS (no global round trip)
   float dummy[3][4];
   for (int u = rl; u < units; u += 64)
-    bwd_visit<true, POOL>(y, G, B, H, W, C, cqg, u, scale, shift, mean, invstd, coef, dz, dummy, gslabs, gstride);
+    bwd_visit<true, POOL>(y, G, B, H, W, C, cqg, u, scale, shift, mean, invstd, coef_sh, dz, dummy, gslabs, gstride,
+                          c0);
 }
 
 // Two-launch backward for the larger layers (both channel-sliced like the fused kernel: 16

@@ -19,14 +19,17 @@ template <bool APPLY, bool POOL>
 __device__ __forceinline__ void bwd_visit(const float* __restrict__ y, const float* __restrict__ G, int B, int H,
                                           int W, int C, int cq, int unit, const float* scale, const float* shift,
                                           const float* mean, const float* invstd, const float* coef, float* dz,
-                                          float (&acc)[3][4], int gslabs = 1, int64_t gstride = 0) {
+                                          float (&acc)[3][4], int gslabs = 1, int64_t gstride = 0,
+                                          int coef_c0 = 0) {
   const int C4 = C >> 2;
   float sc[4], sh[4], mu[4], is[4], k1[4], k2[4], k3[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int c = 4 * cq + q;
     sc[q] = scale[c]; sh[q] = shift[c]; mu[q] = mean[c]; is[q] = invstd[c];
-    if (APPLY) { k1[q] = coef[3 * c]; k2[q] = coef[3 * c + 1]; k3[q] = coef[3 * c + 2]; }
+    if (APPLY) {  // coef holds channels from coef_c0 on (an LDS copy in the single-launch kernel)
+      k1[q] = coef[3 * (c - coef_c0)]; k2[q] = coef[3 * (c - coef_c0) + 1]; k3[q] = coef[3 * (c - coef_c0) + 2];
+    }
   }
   float4 g4 = reinterpret_cast<const float4*>(G)[(size_t)unit * C4 + cq];
   for (int z = 1; z < gslabs; ++z) {  // split-K slabs of the producing GEMM, summed in z order
