@@ -73,16 +73,44 @@ __global__ __launch_bounds__(256) void head_rows_kernel(const float* __restrict_
   const int K4 = K >> 2;
   const float4* f4 = reinterpret_cast<const float4*>(feat) + (size_t)row * K4;
   const float4* w4 = reinterpret_cast<const float4*>(W);
+  // label and bias loaded up front: their latency overlaps the dot products
+  const int y = (int)labels[row];
+  float bj[NC];
+#pragma unroll
+  for (int j = 0; j < NC; ++j) bj[j] = (bias && j < C) ? bias[j] : 0.f;
   float acc[NC];
 #pragma unroll
   for (int j = 0; j < NC; ++j) acc[j] = 0.f;
-  for (int k = lane; k < K4; k += 64) {
-    const float4 f = f4[k];
+  // compile-time class count and K <= 512 (VGG's 512 features): the lane's W slices stay in
+  // registers for the dfeat pass (no second, dependent W read); same summation order
+  constexpr int KIT = 2;
+  const bool cached = CT != 0 && K4 <= 64 * KIT;
+  float4 wc[CT ? KIT : 1][CT ? NC : 1];
+  if constexpr (CT != 0) {
+    if (cached) {
 #pragma unroll
-    for (int j = 0; j < NC; ++j) {
-      if (j < C) {
-        const float4 w = w4[(size_t)j * K4 + k];
-        acc[j] += f.x * w.x + f.y * w.y + f.z * w.z + f.w * w.w;
+      for (int it = 0; it < KIT; ++it) {
+        const int k = lane + 64 * it;
+        if (k < K4) {
+          const float4 f = f4[k];
+#pragma unroll
+          for (int j = 0; j < NC; ++j) {
+            wc[it][j] = w4[(size_t)j * K4 + k];
+            acc[j] += f.x * wc[it][j].x + f.y * wc[it][j].y + f.z * wc[it][j].z + f.w * wc[it][j].w;
+          }
+        }
+      }
+    }
+  }
+  if (!cached) {
+    for (int k = lane; k < K4; k += 64) {
+      const float4 f = f4[k];
+#pragma unroll
+      for (int j = 0; j < NC; ++j) {
+        if (j < C) {
+          const float4 w = w4[(size_t)j * K4 + k];
+          acc[j] += f.x * w.x + f.y * w.y + f.z * w.z + f.w * w.w;
+        }
       }
     }
   }
@@ -91,7 +119,7 @@ __global__ __launch_bounds__(256) void head_rows_kernel(const float* __restrict_
 #pragma unroll
   for (int j = 0; j < NC; ++j) {
     if (j < C) {
-      acc[j] = cs::wave_sum(acc[j]) + (bias ? bias[j] : 0.f);
+      acc[j] = cs::wave_sum(acc[j]) + bj[j];
       if (acc[j] > mx) { mx = acc[j]; am = j; }
     }
   }
@@ -100,7 +128,6 @@ __global__ __launch_bounds__(256) void head_rows_kernel(const float* __restrict_
   for (int j = 0; j < NC; ++j)
     if (j < C) se += expf(acc[j] - mx);
   const float lse = logf(se);
-  const int y = (int)labels[row];
   float xy = 0.f;
 #pragma unroll
   for (int j = 0; j < NC; ++j)
@@ -128,6 +155,24 @@ __global__ __launch_bounds__(256) void head_rows_kernel(const float* __restrict_
     }
   }
   float4* d4 = reinterpret_cast<float4*>(dfeat) + (size_t)row * K4;
+  if constexpr (CT != 0) {
+    if (cached) {
+#pragma unroll
+      for (int it = 0; it < KIT; ++it) {
+        const int k = lane + 64 * it;
+        if (k < K4) {
+          float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+          for (int j = 0; j < NC; ++j) {
+            o.x += acc[j] * wc[it][j].x; o.y += acc[j] * wc[it][j].y;
+            o.z += acc[j] * wc[it][j].z; o.w += acc[j] * wc[it][j].w;
+          }
+          d4[k] = o;
+        }
+      }
+      return;
+    }
+  }
   for (int k = lane; k < K4; k += 64) {
     float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
@@ -159,6 +204,22 @@ __global__ __launch_bounds__(64) void head_cols_kernel(const float* __restrict__
     if (k >= K) return;
     float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
     int b = 0;
+    // 16 rows of loads in flight, then the adds in the 4-accumulator order of the loop below
+    for (; b + 16 <= B; b += 16) {
+      float d[16], f[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        d[i] = dl[(size_t)(b + i) * C + j];
+        f[i] = feat[(size_t)(b + i) * K + k];
+      }
+#pragma unroll
+      for (int i = 0; i < 16; i += 4) {
+        s0 += d[i] * f[i];
+        s1 += d[i + 1] * f[i + 1];
+        s2 += d[i + 2] * f[i + 2];
+        s3 += d[i + 3] * f[i + 3];
+      }
+    }
     for (; b + 4 <= B; b += 4) {
       s0 += dl[(size_t)b * C + j] * feat[(size_t)b * K + k];
       s1 += dl[(size_t)(b + 1) * C + j] * feat[(size_t)(b + 1) * K + k];
