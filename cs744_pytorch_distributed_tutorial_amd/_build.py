@@ -45,11 +45,22 @@ def _sources():
     return hip, cpp
 
 
-def _headers_mtime() -> float:
-    hs = glob.glob(os.path.join(CSRC, "**", "*.h"), recursive=True) + \
-        glob.glob(os.path.join(CSRC, "**", "*.hpp"), recursive=True) + \
-        glob.glob(os.path.join(CSRC, "**", "*.cuh"), recursive=True)
-    return max([os.path.getmtime(h) for h in hs] + [0.0])
+def _deps_mtime(obj: str) -> float:
+    """Newest in-tree header the object was compiled against (from the -MD depfile), or
+    +inf when the depfile is missing (forces a rebuild). Out-of-tree headers (torch, ROCm)
+    are skipped: they only change with the image."""
+    dep = obj + ".d"
+    if not os.path.exists(dep):
+        return float("inf")
+    with open(dep) as f:
+        text = f.read().replace("\\\n", " ")
+    newest = 0.0
+    for tok in text.split(":", 1)[-1].split():
+        if tok.startswith(CSRC):
+            if not os.path.exists(tok):
+                return float("inf")
+            newest = max(newest, os.path.getmtime(tok))
+    return newest
 
 
 def _obj_path(src: str) -> str:
@@ -64,12 +75,14 @@ def _common_flags():
 
 def _compile_cmd(src: str, obj: str):
     if src.endswith(".hip"):
-        return [HIPCC, f"--offload-arch={ARCH}", "-munsafe-fp-atomics", *_common_flags(), "-c", src, "-o", obj]
+        return [HIPCC, f"--offload-arch={ARCH}", "-munsafe-fp-atomics", *_common_flags(), "-MD", "-MF", obj + ".d",
+                "-c", src, "-o", obj]
     _, tinc, _ = _torch_paths()
     py_inc = sysconfig.get_paths()["include"]
     incs = [f"-I{p}" for p in tinc] + [f"-I{py_inc}", f"-I{ROCM}/include"]
     return [HIPCC, *_common_flags(), *incs, "-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H",
-            "-D_GLIBCXX_USE_CXX11_ABI=1", "-DUSE_ROCM=1", "-x", "c++", "-c", src, "-o", obj]
+            "-D_GLIBCXX_USE_CXX11_ABI=1", "-DUSE_ROCM=1", "-MD", "-MF", obj + ".d", "-x", "c++", "-c", src,
+            "-o", obj]
 
 
 def _link_cmd(objs):
@@ -82,13 +95,12 @@ def _link_cmd(objs):
 def build(jobs: int = 0, force: bool = False, verbose: bool = False) -> str:
     os.makedirs(BUILD, exist_ok=True)
     hip, cpp = _sources()
-    hdr = _headers_mtime()
     todo = []
     objs = []
     for s in hip + cpp:
         o = _obj_path(s)
         objs.append(o)
-        if force or not os.path.exists(o) or os.path.getmtime(o) < max(os.path.getmtime(s), hdr):
+        if force or not os.path.exists(o) or os.path.getmtime(o) < max(os.path.getmtime(s), _deps_mtime(o)):
             todo.append((s, o))
     jobs = jobs or min(8, os.cpu_count() or 4)
     t0 = time.time()

@@ -29,11 +29,16 @@ class TrainConfig:
     port: Optional[int] = None
     backend: Optional[str] = None       # gloo | nccl (RCCL) | None=auto
     device: str = "auto"                # auto | cpu | cuda
-    engine: str = "torch"               # torch (nn.Module + autograd) | native (fused HIP engine)
-    comm: str = "torch"                 # torch | rccl (native communicator)
-    bucket_mb: float = 25.0
+    # auto: the native HIP engine whenever the run is on a GPU, autograd + gloo on CPU
+    engine: str = "auto"                # auto | torch (nn.Module + autograd) | native (fused HIP engine)
+    # auto: native engine -> rccl (one GPU per rank), or staged when ranks outnumber the GPUs
+    # (RCCL refuses two ranks on one device); torch engine -> torch.distributed
+    comm: str = "auto"                  # auto | torch | rccl | staged
+    # xGMI-sized buckets closed at layer boundaries; the reference's DDP
+    # bucketing is --bucket-policy size --bucket-mb 25
+    bucket_mb: float = 4.0
     first_bucket_mb: float = 1.0
-    bucket_policy: str = "size"         # size (DDP semantics) | layer (xGMI-sized)
+    bucket_policy: str = "layer"        # layer (xGMI-sized) | size (torch DDP semantics) | single
     coalesce: bool = False              # coalesced variants of the faithful sync modes
     max_steps: Optional[int] = None     # cap iterations per epoch (None = full epoch)
     train_size: Optional[int] = None    # synthetic dataset size override
@@ -46,7 +51,8 @@ class TrainConfig:
     resume: Optional[str] = None        # path to load before training
     check_sync_every: int = 0           # cross-rank parameter checksum every K steps (0 = off)
     metrics_jsonl: Optional[str] = None
-    timeout_s: float = 1800.0
+    timeout_s: float = 1800.0           # collective timeout / native step watchdog (reference: gloo's 30 min)
+    check_comm_every: int = 20          # native engine: poll the communicator's async error every K steps
     extra: dict = field(default_factory=dict)
 
     def resolved_batch_size(self) -> int:
@@ -59,6 +65,23 @@ class TrainConfig:
             return self.sync
         return {"part1": "none", "part2a": "gather_scatter", "part2a_extra": "p2p",
                 "part2b": "allreduce", "part3": "ddp"}.get(self.part, "ddp")
+
+    def on_gpu(self) -> bool:
+        import torch
+        return self.device == "cuda" or (self.device == "auto" and torch.cuda.is_available())
+
+    def resolved_engine(self) -> str:
+        if self.engine != "auto":
+            return self.engine
+        return "native" if self.on_gpu() and self.model.upper().startswith("VGG") else "torch"
+
+    def resolved_comm(self, world: int = 1) -> str:
+        if self.comm != "auto":
+            return self.comm
+        if self.resolved_engine() != "native":
+            return "torch"
+        import torch
+        return "staged" if world > max(torch.cuda.device_count(), 1) else "rccl"
 
     def resolved_port(self) -> int:
         if self.port is not None:
@@ -90,11 +113,11 @@ def add_engine_flags(p: argparse.ArgumentParser) -> None:
     p.add_argument("--port", type=int, default=None)
     p.add_argument("--backend", type=str, default=None, choices=["gloo", "nccl"])
     p.add_argument("--device", type=str, default="auto", choices=["auto", "cpu", "cuda"])
-    p.add_argument("--engine", type=str, default="torch", choices=["torch", "native"])
-    p.add_argument("--comm", type=str, default="torch", choices=["torch", "rccl"])
-    p.add_argument("--bucket-mb", type=float, default=25.0)
+    p.add_argument("--engine", type=str, default="auto", choices=["auto", "torch", "native"])
+    p.add_argument("--comm", type=str, default="auto", choices=["auto", "torch", "rccl", "staged"])
+    p.add_argument("--bucket-mb", type=float, default=4.0)
     p.add_argument("--first-bucket-mb", type=float, default=1.0)
-    p.add_argument("--bucket-policy", type=str, default="size", choices=["size", "layer", "single"])
+    p.add_argument("--bucket-policy", type=str, default="layer", choices=["layer", "size", "single"])
     p.add_argument("--coalesce", action="store_true")
     p.add_argument("--steps", dest="max_steps", type=int, default=None)
     p.add_argument("--train-size", type=int, default=None)
@@ -108,6 +131,7 @@ def add_engine_flags(p: argparse.ArgumentParser) -> None:
     p.add_argument("--check-sync-every", type=int, default=0)
     p.add_argument("--metrics-jsonl", type=str, default=None)
     p.add_argument("--timeout-s", type=float, default=1800.0)
+    p.add_argument("--check-comm-every", type=int, default=20)
 
 
 def config_from_args(part: str, argv=None) -> TrainConfig:

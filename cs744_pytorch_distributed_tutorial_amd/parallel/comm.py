@@ -122,11 +122,16 @@ class TorchComm(Comm):
 
 
 def make_comm(kind: Optional[str] = None, group=None) -> Comm:
-    """``kind``: ``"torch"`` (default) or ``"rccl"`` (native C++ communicator)."""
+    """``kind``: ``"torch"`` (default), ``"rccl"`` (native C++ RCCL communicator, one GPU per
+    rank) or ``"staged"`` (native C++ communicator over a gloo group with host staging: the
+    engine's C++ step with several ranks on one GPU, ``parallel.staged``)."""
     kind = kind or "torch"
     if kind == "torch":
         return TorchComm(group)
     if kind == "rccl":
         from .rccl import RcclComm
         return RcclComm.from_process_group(group)
+    if kind == "staged":
+        from .staged import StagedComm
+        return StagedComm(group)
     raise ValueError(f"unknown comm kind {kind!r}")

@@ -186,7 +186,8 @@ class NativeTrainer:
                  dampening: float = 0.0, seed: int = 5000, data_seed: int = 0, train_size: Optional[int] = None,
                  test_size: Optional[int] = None, autotune: bool = True, broadcast_buffers: bool = True,
                  drop_last: bool = True, init_state: Optional[Dict[str, torch.Tensor]] = None,
-                 dtype: str = "fp32"):
+                 dtype: str = "fp32", probe: Optional[str] = None, probe_spin_us: float = 20.0,
+                 check_every: int = 0):
         C = native.C()
         self.device = device or torch.device("cuda", torch.cuda.current_device())
         self.rank, self.world = rank, world
@@ -208,18 +209,28 @@ class NativeTrainer:
 
         # communicator + DDP construction-time sync (params + buffers from rank 0)
         self.comm = None
+        self.comm_kind = comm if world > 1 else "none"
         if world > 1:
             from ..parallel.comm import make_comm
             self.comm = make_comm(comm)
-            self.comm.broadcast(self.params, 0)
-            self.comm.broadcast(self.bufs, 0)
-            self.comm.broadcast(self.nbt, 0)
+            self.sync_from_root()
         self.native_comm = getattr(self.comm, "native", None)
-        if world == 1 and os.environ.get("CS_COMM_PROBE", "0") != "0":
-            # measurement only: a one-rank RCCL communicator so the engine's bucketed all-reduce,
-            # buffer broadcast and stream fork/join run (and cost what they cost) on one GPU
-            from ..parallel.rccl import RcclComm
-            self.native_comm = RcclComm.create(0, 1, self.device.index or 0).native
+        probe = probe if probe is not None else os.environ.get("CS_COMM_PROBE", "0")
+        if world == 1 and probe not in (None, "", "0"):
+            if probe == "order":
+                # ordering test: every collective = spin + exact scramble/unscramble on the comm
+                # stream (parallel/staged.py ProbeComm); a missing fork/join is a bitwise mismatch
+                from ..parallel.staged import ProbeComm
+                self._probe = ProbeComm(self.device.index or 0, probe_spin_us)
+            else:
+                # measurement only: a one-rank RCCL communicator so the engine's bucketed all-reduce,
+                # buffer broadcast and stream fork/join run (and cost what they cost) on one GPU
+                from ..parallel.rccl import RcclComm
+                self._probe = RcclComm.create(0, 1, self.device.index or 0)
+            self.native_comm = self._probe.native
+            self.comm_kind = f"probe:{probe}"
+        # poll the native communicator's async error every K steps (0 = off)
+        self.check_every = check_every
         self.bucket_lows, self.bucket_ranges = lay.plan_buckets(bucket_mb if sync == "ddp" else 1e9)
         at = 0
         for off, n in self.bucket_ranges:  # buckets tile the flat buffer (per-bucket SGD relies on it)
@@ -244,6 +255,7 @@ class NativeTrainer:
         self.aug_train = dm.augment_params(len(self.train_set), data_seed, 0, True).to(self.device)
         self.aug_test = dm.augment_params(len(self.test_set), data_seed, 0, False).to(self.device)
 
+        self._probe = getattr(self, "_probe", None)
         self.engine = C.VggEngine(self.B, lay.desc(), lay.offs(), lay.buf_offs(), lay.feat, lay.ncls,
                                   self.params, self.grads, self.mom, self.bufs, self.nbt)
         self.engine.set_data(0, self.train_data, self.train_labels, self.aug_train)
@@ -269,6 +281,9 @@ class NativeTrainer:
             graph = "none" if native_ok else "segments"
         if graph == "full" and world > 1 and (self.native_comm is None or self.sync_mode not in ("ddp", "none")):
             graph = "segments"  # only the native communicator can be captured together with the step
+        if graph == "full" and self.native_comm is not None and self.native_comm.kind == "staged":
+            raise ValueError("graph='full': the staged communicator blocks the host inside each collective "
+                             "and cannot be captured; use graph='none'")
         if graph not in ("full", "segments", "none"):
             raise ValueError(f"graph mode {graph!r}: choose full | segments | none | auto")
         self.graph_mode = graph
@@ -277,8 +292,17 @@ class NativeTrainer:
         self.epoch = 0
         self.iter_in_epoch = 0
         self.global_step = 0
+        self._mom_valid = False  # momentum buffers hold state (after a step or a loaded optimizer state)
         self._epoch_idx = None
         self._start_epoch(0)
+
+    def sync_from_root(self) -> None:
+        """DDP construction-time sync (`torch:nn/parallel/distributed.py:855-870`): rank 0's
+        parameters, momentum, BN buffers and counters on every rank (also after a resume)."""
+        if self.comm is None:
+            return
+        for t in (self.params, self.mom, self.bufs, self.nbt):
+            self.comm.broadcast(t, 0)
 
     def _tune(self, model: str, cache: Optional[str]) -> None:
         """Autotune conv tiles (HIP-event timed), or reuse a JSON tuning cache keyed by model/batch."""
@@ -325,15 +349,21 @@ class NativeTrainer:
         n = len(self.sampler)
         return n // self.B if self.drop_last else math.ceil(n / self.B)
 
-    def _start_epoch(self, epoch: int) -> None:
+    def _start_epoch(self, epoch: int, start_iter: int = 0) -> None:
         """New sampler order on the device; the engine's batch kernel walks it with a device-side
-        cursor that each step's SGD launch advances, so a step needs no host-side index copy."""
+        cursor that each step's SGD launch advances, so a step needs no host-side index copy.
+        ``start_iter`` > 0 resumes inside the epoch (same order and augmentation as an
+        uninterrupted run: both depend only on (seed, epoch))."""
         self.epoch = epoch
         self.sampler.set_epoch(epoch)
         self._epoch_idx = torch.tensor(self.sampler.indices(), dtype=torch.int64)
         self.engine.set_perm(self._epoch_idx)
         self.aug_train.copy_(dm.augment_params(len(self.train_set), self.data_seed, epoch, True).to(self.device))
-        self.iter_in_epoch = 0
+        if not 0 <= start_iter <= self.steps_per_epoch():
+            raise ValueError(f"start_iter {start_iter} outside epoch of {self.steps_per_epoch()} steps")
+        if start_iter:
+            self.engine.cursor().fill_(start_iter)
+        self.iter_in_epoch = start_iter
 
     def _load_next_batch(self) -> int:
         if self.iter_in_epoch >= self.steps_per_epoch():
@@ -450,9 +480,30 @@ class NativeTrainer:
         torch.cuda.current_stream().wait_stream(s)
         self._graphs = graphs
 
+    def check_comm(self) -> None:
+        """Async-error poll of the native communicator (ncclCommGetAsyncError for RCCL): on an
+        error the communicator is aborted (ncclCommAbort) and the step raises, so a dead peer
+        becomes a prompt failure instead of a hang."""
+        if self.native_comm is None:
+            return
+        err = self.native_comm.async_error()
+        if err:
+            self.native_comm.abort()
+            raise RuntimeError(f"rank {self.rank}: {self.native_comm.kind} communicator failed: {err}")
+
+    def abort(self) -> None:
+        """Abort the native communicator (from a watchdog thread: unblocks RCCL kernels)."""
+        if self.native_comm is not None:
+            self.native_comm.abort()
+
     def step(self) -> None:
         """One training iteration: next batch -> forward -> backward (+grad sync) -> SGD."""
+        if self.check_every and self.global_step % self.check_every == 0:
+            self.check_comm()
         B = self._load_next_batch()
+        # torch.optim.SGD's first step clones d into the momentum buffer (matters with dampening)
+        self.engine.set_sgd_first(not self._mom_valid)
+        self._mom_valid = True
         use_graph = self.graph_mode != "none" and B == self.B and self.global_step >= 2
         if use_graph and self._graphs is None:
             self._capture()
@@ -476,6 +527,8 @@ class NativeTrainer:
         try:
             for _ in range(steps):
                 B = self._load_next_batch()
+                self.engine.set_sgd_first(not self._mom_valid)
+                self._mom_valid = True
                 self._step_full_native(B)
                 self.global_step += 1
                 for k, v in self.engine.phase_times():
@@ -512,7 +565,13 @@ class NativeTrainer:
             correct += self.engine.correct().long()
             nb += 1
         total = min(n, nb * self.B)
-        return {"avg_loss": float(loss_sum.item()) / max(nb, 1), "correct": int(correct.item()), "total": total}
+        out = {"avg_loss": float(loss_sum.item()) / max(nb, 1), "correct": int(correct.item()), "total": total}
+        if self.comm is not None:
+            # the reference's intended cross-rank accuracy (its unmatched isend, C-4,
+            # `slave/part2b/part2b.py:67-69`): (loss sum, correct, total, batches) summed over ranks
+            from ..utils.metrics import reduce_eval
+            out.update(reduce_eval(self.comm, float(loss_sum.item()), out["correct"], total, nb, self.device))
+        return out
 
     def state_dict(self) -> Dict[str, torch.Tensor]:
         return self.layout.unpack(self.params, self.bufs, self.nbt)
@@ -523,7 +582,7 @@ class NativeTrainer:
     def optimizer_state_dict(self) -> dict:
         """torch.optim.SGD ``state_dict`` format (momentum_buffer per parameter index)."""
         state = {i: {"momentum_buffer": self.layout.view(self.mom, n).detach().cpu().contiguous()}
-                 for i, n in enumerate(self.layout.param_names)} if self.global_step > 0 else {}
+                 for i, n in enumerate(self.layout.param_names)} if self._mom_valid else {}
         group = {"lr": self.lr, "momentum": self.momentum, "dampening": self.damp, "weight_decay": self.wd,
                  "nesterov": False, "maximize": False, "foreach": None, "differentiable": False, "fused": None,
                  "params": list(range(len(self.layout.param_names)))}
@@ -538,6 +597,7 @@ class NativeTrainer:
                     self.layout.view(self.mom, n).copy_(st["momentum_buffer"])
             if sd["state"]:
                 self.global_step = max(self.global_step, 1)
+                self._mom_valid = True
 
     def close(self) -> None:
         """Release graphs, the engine and the native communicator deterministically (before the
@@ -550,6 +610,9 @@ class NativeTrainer:
             torch.cuda.synchronize()
             if self.comm is not None:
                 self.comm.native = None
+            if getattr(self, "_probe", None) is not None:
+                self._probe.native = None
+                self._probe = None
             self.native_comm = None
         import gc
         gc.collect()
@@ -565,53 +628,92 @@ class NativeTrainer:
 
 
 def run_native(cfg, device, logger) -> dict:
-    """Entry-point runner (part1/part2*/part3 with ``--engine native``)."""
+    """Entry-point runner (part1/part2*/part3 on the native engine — the default on a GPU).
+
+    Resume: the checkpoint's (epoch, iter) continue where it stopped — the
+    sampler order and augmentation of an epoch depend only on (seed, epoch), and the device
+    batch cursor is set to ``iter`` — and rank 0's state is broadcast after the load, so a
+    resumed run is bitwise the uninterrupted one. A ``--steps``-truncated epoch saves
+    (epoch, steps); a completed one (epoch + 1, 0).
+    Failure handling (§5.3): a watchdog aborts the native communicator and exits non-zero
+    when a step stalls past ``cfg.timeout_s``; the communicator's async error is polled
+    every ``cfg.check_comm_every`` steps."""
     import time
+    from ..utils import faults
     rank, world = D.get_rank(), D.get_world_size()
     mode = cfg.resolved_sync() if world > 1 else "none"
     tr = NativeTrainer(model=cfg.model, batch_size=cfg.resolved_batch_size(), device=device, rank=rank,
-                       world=world, sync=mode, comm=cfg.comm if cfg.comm != "torch" else "torch",
-                       bucket_mb=cfg.bucket_mb, lr=cfg.lr, momentum=cfg.momentum, weight_decay=cfg.weight_decay,
-                       seed=cfg.seed, data_seed=cfg.data_seed, train_size=cfg.train_size, test_size=cfg.test_size,
-                       drop_last=False)
+                       world=world, sync=mode, comm=cfg.resolved_comm(world), bucket_mb=cfg.bucket_mb, lr=cfg.lr,
+                       momentum=cfg.momentum, weight_decay=cfg.weight_decay, seed=cfg.seed, data_seed=cfg.data_seed,
+                       train_size=cfg.train_size, test_size=cfg.test_size, drop_last=False,
+                       check_every=cfg.check_comm_every)
+    start_epoch, start_iter = 0, 0
     if cfg.resume:
         from ..utils.checkpoint import load_checkpoint
         st = load_checkpoint(cfg.resume)
         tr.load_state_dict(st["model"])
         if st.get("optimizer"):
             tr.load_optimizer_state_dict(st["optimizer"])
-    results = {"rank": rank, "world": world, "sync": mode, "engine": "native", "epochs": []}
-    for epoch in range(cfg.epochs):
-        tr._start_epoch(epoch)
-        steps = tr.steps_per_epoch()
-        if cfg.max_steps is not None:
-            steps = min(steps, cfg.max_steps)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        stamps = []
-        for i in range(steps):
-            tr.step()
-            if i <= 10:
-                torch.cuda.synchronize()
-                stamps.append(time.perf_counter())
-            if i % cfg.log_every == 0:
-                logger.loss_line(i, tr.last_loss())
-            if i == 10:
-                logger.average_time_line((stamps[10] - stamps[0]) / 9)
-                logger.print(f"(true mean over iters 1..10: {(stamps[10] - stamps[0]) / 10:.6f} s; "
-                             "the line above uses the reference /9 formula)")
-        torch.cuda.synchronize()
-        sec = time.perf_counter() - t0
-        ips = steps * tr.B * world / max(sec, 1e-9)
-        logger.metric(kind="train_epoch", epoch=epoch, sync=mode, world=world, images_per_s=ips, engine="native")
-        te = None
-        if cfg.eval:
-            te = tr.evaluate()
-            logger.test_line(te["avg_loss"], te["correct"], te["total"])
-        results["epochs"].append({"images_per_s": ips, "seconds": sec, "steps": steps, "test": te,
-                                  "last_loss": tr.last_loss()})
+        start_epoch, start_iter = int(st.get("epoch", 0)), int(st.get("iter", 0))
+        tr.global_step = max(tr.global_step, int(st.get("extra", {}).get("global_step", 0)))
+        tr.sync_from_root()
+    wd = faults.Watchdog(cfg.timeout_s, "native training step", on_timeout=tr.abort).start() \
+        if cfg.timeout_s and cfg.timeout_s > 0 else None
+    results = {"rank": rank, "world": world, "sync": mode, "engine": "native", "comm": tr.comm_kind,
+               "epochs": [], "losses": []}
+    logger.print(f"[engine] native (gfx950 HIP kernels), world {world}, sync {mode}, comm {tr.comm_kind}, "
+                 f"batch {tr.B}/rank")
+    end_epoch, end_iter = start_epoch, start_iter
+    try:
+        for epoch in range(start_epoch, start_epoch + cfg.epochs):
+            first = start_iter if epoch == start_epoch else 0
+            tr._start_epoch(epoch, first)
+            steps = tr.steps_per_epoch()
+            if cfg.max_steps is not None:
+                steps = min(steps, cfg.max_steps)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            stamps = []
+            for i in range(first, steps):
+                tr.step()
+                if wd is not None:
+                    wd.kick()
+                if i <= 10:
+                    torch.cuda.synchronize()
+                    stamps.append(time.perf_counter())
+                if i % cfg.log_every == 0:
+                    lv = tr.last_loss()
+                    results["losses"].append((epoch, i, lv))
+                    logger.loss_line(i, lv)
+                if i == 10 and len(stamps) == 11:
+                    logger.average_time_line((stamps[10] - stamps[0]) / 9)
+                    logger.print(f"(true mean over iters 1..10: {(stamps[10] - stamps[0]) / 10:.6f} s; "
+                                 "the line above uses the reference /9 formula)")
+            torch.cuda.synchronize()
+            sec = time.perf_counter() - t0
+            ips = (steps - first) * tr.B * world / max(sec, 1e-9)
+            logger.metric(kind="train_epoch", epoch=epoch, sync=mode, world=world, images_per_s=ips, engine="native")
+            te = None
+            if cfg.eval:
+                te = tr.evaluate()
+                logger.test_line(te["avg_loss"], te["correct"], te["total"])
+                if "global_correct" in te:
+                    gc, gt = te["global_correct"], te["global_total"]
+                    logger.print(f"All ranks: Average loss: {te['global_avg_loss']:.4f}, "
+                                 f"Accuracy: {gc}/{gt} ({100.0 * gc / max(gt, 1):.0f}%)")
+            results["epochs"].append({"images_per_s": ips, "seconds": sec, "steps": steps - first, "test": te,
+                                      "last_loss": tr.last_loss()})
+            end_epoch, end_iter = (epoch + 1, 0) if steps == tr.steps_per_epoch() else (epoch, steps)
+            if wd is not None:
+                wd.kick()
+    finally:
+        if wd is not None:
+            wd.stop()
     if cfg.checkpoint:
         from ..utils.checkpoint import save_checkpoint
-        save_checkpoint(cfg.checkpoint, tr.state_dict(), tr.optimizer_state_dict(), cfg.epochs, 0, 0, world, rank)
+        save_checkpoint(cfg.checkpoint, tr.state_dict(), tr.optimizer_state_dict(), end_epoch, end_iter, 0, world,
+                        rank, extra={"global_step": tr.global_step})
     results["final_state"] = tr.state_dict()
+    results["resume_point"] = (end_epoch, end_iter)
+    tr.close()
     return results

@@ -143,7 +143,7 @@ def run(cfg: TrainConfig) -> dict:
     rank, world = D.get_rank(), D.get_world_size()
     device = resolve_device(cfg)
     logger = RankLogger(rank, all_ranks=cfg.all_ranks_print, jsonl_path=cfg.metrics_jsonl)
-    if cfg.engine == "native":
+    if cfg.resolved_engine() == "native" and device.type == "cuda":
         from .runtime.engine import run_native
         return run_native(cfg, device, logger)
 
@@ -170,7 +170,7 @@ def run(cfg: TrainConfig) -> dict:
     model = VGG(cfg.model).to(device)
     mode = cfg.resolved_sync() if world > 1 else "none"
     if mode == "ddp":
-        comm = make_comm(cfg.comm)
+        comm = make_comm(cfg.resolved_comm(world))
         net: nn.Module = DistributedDataParallel(model, comm=comm, bucket_cap_mb=cfg.bucket_mb,
                                                  first_bucket_cap_mb=cfg.first_bucket_mb,
                                                  bucket_policy=cfg.bucket_policy)
@@ -186,7 +186,7 @@ def run(cfg: TrainConfig) -> dict:
     if cfg.resume:
         st = load_training_state(cfg.resume, net, optimizer)
         start_epoch = int(st.get("epoch", 0))
-    results = {"rank": rank, "world": world, "sync": mode, "epochs": []}
+    results = {"rank": rank, "world": world, "sync": mode, "engine": "torch", "epochs": []}
     for epoch in range(start_epoch, start_epoch + cfg.epochs):
         if hasattr(train_loader, "set_epoch"):
             train_loader.set_epoch(epoch)

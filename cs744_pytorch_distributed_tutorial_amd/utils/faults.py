@@ -102,10 +102,16 @@ def assert_replicas_in_sync(tensors: Iterable[torch.Tensor], rtol: float = 0.0, 
 
 
 class Watchdog:
-    """Abort the process if ``kick()`` is not called within ``timeout_s``."""
+    """Abort the process if ``kick()`` is not called within ``timeout_s``.
 
-    def __init__(self, timeout_s: float, what: str = "step"):
+    ``on_timeout`` runs first (the native trainers pass their communicator's abort —
+    ``ncclCommAbort`` unblocks RCCL kernels spinning on a dead peer), then the process
+    exits with code 18: a hung collective becomes a prompt, loud failure instead of the
+    reference's silent 30-minute gloo stall (`master/part2a/part2a.py:84`)."""
+
+    def __init__(self, timeout_s: float, what: str = "step", on_timeout=None):
         self.timeout_s, self.what = timeout_s, what
+        self.on_timeout = on_timeout
         self._last = time.monotonic()
         self._stop = threading.Event()
         self._thread: Optional[threading.Thread] = None
@@ -126,4 +132,9 @@ class Watchdog:
             if time.monotonic() - self._last > self.timeout_s:
                 sys.stderr.write(f"[watchdog] {self.what} exceeded {self.timeout_s:.1f}s — aborting\n")
                 sys.stderr.flush()
+                if self.on_timeout is not None:
+                    try:
+                        self.on_timeout()
+                    except Exception as e:  # noqa: BLE001 - exiting anyway
+                        sys.stderr.write(f"[watchdog] abort hook failed: {e}\n")
                 os._exit(18)

@@ -132,6 +132,21 @@ class PhaseTimer:
         return out
 
 
+def reduce_eval(comm, loss_sum: float, correct: int, total: int, batches: int,
+                device: Optional[torch.device] = None) -> Dict[str, Any]:
+    """Cross-rank evaluation totals — what the reference meant its ranks' unmatched
+    ``isend(correct, dst=0)`` to deliver (C-4, `slave/part2b/part2b.py:67-69`,
+    `slave/part2a/part2a_extra.py:69-70`): one SUM all-reduce of (loss sum, correct, total,
+    batches) over ``comm`` (any ``parallel.comm.Comm``), float64 (exact for counts < 2^53).
+    Every rank gets the global numbers; rank 0 prints them."""
+    t = torch.tensor([loss_sum, float(correct), float(total), float(batches)], dtype=torch.float64,
+                     device=device or "cpu")
+    if comm is not None and getattr(comm, "world_size", 1) > 1:
+        comm.all_reduce(t, "sum")
+    ls, c, n, nb = t.tolist()
+    return {"global_avg_loss": ls / max(nb, 1.0), "global_correct": int(c), "global_total": int(n)}
+
+
 def roctx_range(name: str):
     """Context manager emitting a roctx range (visible in rocprofv3 marker traces)."""
     try:

@@ -134,7 +134,6 @@ std::vector<torch::Tensor> softmax_xent(torch::Tensor logits, torch::Tensor labe
 }  // namespace
 
 void register_conv_ops(pybind11::module& m);
-void register_bn_ops(pybind11::module& m);
 void register_runtime(pybind11::module& m);
 void register_lm_ops(pybind11::module& m);
 
@@ -147,7 +146,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("linear_xent", &linear_xent, "fused Linear + softmax cross-entropy fwd(+bwd)");
   m.def("softmax_xent", &softmax_xent, "softmax cross-entropy fwd+bwd");
   register_conv_ops(m);
-  register_bn_ops(m);
   register_runtime(m);
   register_lm_ops(m);
 }

@@ -2,6 +2,7 @@
 // Collectives take torch tensors and run stream-ordered w.r.t. torch's current stream.
 #include "binding/torch_util.h"
 #include "runtime/rccl_comm.h"
+#include "runtime/staged_comm.h"
 #include "runtime/vgg_engine.h"
 
 namespace {
@@ -47,25 +48,36 @@ void register_runtime(pybind11::module& m) {
     ncclGetVersion(&v);
     return v;
   });
-  py::class_<cs::RcclComm>(m, "RcclComm")
+  // the engine's communicator interface (device_comm.h): RcclComm, StagedComm, ProbeComm
+  py::class_<cs::DeviceComm>(m, "DeviceComm")
+      .def_property_readonly("rank", &cs::DeviceComm::rank)
+      .def_property_readonly("world_size", &cs::DeviceComm::world)
+      .def_property_readonly("kind", [](cs::DeviceComm& c) { return std::string(c.kind()); })
+      .def("calls", &cs::DeviceComm::calls)
+      .def("stream_ptr", [](cs::DeviceComm& c) { return reinterpret_cast<intptr_t>(c.stream()); })
+      .def("all_reduce",
+           [](cs::DeviceComm& c, torch::Tensor t, const std::string& op) {
+             check_gpu(t, "tensor");
+             c.all_reduce(t.data_ptr(), t.numel(), nccl_dtype(t), nccl_op(op), cur_stream(), true);
+           },
+           py::arg("tensor"), py::arg("op") = "sum")
+      .def("broadcast",
+           [](cs::DeviceComm& c, torch::Tensor t, int root) {
+             check_gpu(t, "tensor");
+             c.broadcast(t.data_ptr(), t.numel(), nccl_dtype(t), root, cur_stream(), true);
+           })
+      .def("join", [](cs::DeviceComm& c) { c.join(cur_stream()); })
+      .def("async_error", &cs::DeviceComm::async_error)
+      .def("abort", &cs::DeviceComm::abort);
+  py::class_<cs::StagedComm, cs::DeviceComm>(m, "StagedComm")
+      .def(py::init<const std::string&, int>(), py::arg("group_name"), py::arg("device"));
+  py::class_<cs::ProbeComm, cs::DeviceComm>(m, "ProbeComm")
+      .def(py::init<int, double>(), py::arg("device"), py::arg("spin_us") = 20.0);
+  py::class_<cs::RcclComm, cs::DeviceComm>(m, "RcclComm")
       .def(py::init([](py::bytes uid, int rank, int world, int device, bool high_priority) {
              return new cs::RcclComm(std::string(uid), rank, world, device, high_priority);
            }),
            py::arg("uid"), py::arg("rank"), py::arg("world"), py::arg("device"), py::arg("high_priority") = true)
-      .def_property_readonly("rank", &cs::RcclComm::rank)
-      .def_property_readonly("world_size", &cs::RcclComm::world)
-      .def("stream_ptr", [](cs::RcclComm& c) { return reinterpret_cast<intptr_t>(c.stream()); })
-      .def("all_reduce",
-           [](cs::RcclComm& c, torch::Tensor t, const std::string& op) {
-             check_gpu(t, "tensor");
-             c.all_reduce(t.data_ptr(), t.numel(), nccl_dtype(t), nccl_op(op), cur_stream());
-           },
-           py::arg("tensor"), py::arg("op") = "sum")
-      .def("broadcast",
-           [](cs::RcclComm& c, torch::Tensor t, int root) {
-             check_gpu(t, "tensor");
-             c.broadcast(t.data_ptr(), t.numel(), nccl_dtype(t), root, cur_stream());
-           })
       .def("all_gather",
            [](cs::RcclComm& c, torch::Tensor in, torch::Tensor out) {
              check_gpu(in, "in"); check_gpu(out, "out");
@@ -126,10 +138,7 @@ void register_runtime(pybind11::module& m) {
              c.recv(t.data_ptr(), t.numel(), nccl_dtype(t), peer, cur_stream());
            })
       .def("group_start", [](cs::RcclComm& c) { c.group_start(cur_stream()); })
-      .def("group_end", &cs::RcclComm::group_end)
-      .def("join", [](cs::RcclComm& c) { c.join(cur_stream()); })
-      .def("async_error", &cs::RcclComm::async_error)
-      .def("abort", &cs::RcclComm::abort);
+      .def("group_end", &cs::RcclComm::group_end);
 
   py::class_<cs::VggEngine>(m, "VggEngine")
       .def(py::init<int64_t, std::vector<int64_t>, std::vector<int64_t>, std::vector<int64_t>, int64_t, int64_t,
@@ -153,6 +162,8 @@ void register_runtime(pybind11::module& m) {
            py::arg("wd"), py::arg("dampening"))
       .def("set_overlap_wgrad", &cs::VggEngine::set_overlap_wgrad)
       .def("set_sgd_overlap", &cs::VggEngine::set_sgd_overlap)
+      .def("set_sgd_first", &cs::VggEngine::set_sgd_first)
+      .def("set_debug_skip", &cs::VggEngine::set_debug_skip)
       .def("set_timing", &cs::VggEngine::set_timing)
       .def("set_math", &cs::VggEngine::set_math)
       .def("phase_times", &cs::VggEngine::phase_times)

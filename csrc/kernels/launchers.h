@@ -150,6 +150,13 @@ hipError_t cs_bn_bwd2(const float* y, const float* G, int B, int H, int W, int C
                       const float* gamma, float* part, float* dgamma, float* dbeta, float* dbias, float* dz,
                       hipStream_t stream);
 
+// ---------------------------------------------------------------- ordering-probe communicator (comm_probe.hip)
+enum { CS_SCRAMBLE_F32 = 0, CS_SCRAMBLE_I64 = 1, CS_SCRAMBLE_I32 = 2 };
+// a bounded (<= 0.1 s) busy wait of `us` microseconds on `stream`
+hipError_t cs_comm_spin(double us, hipStream_t stream);
+// exact invertible scramble: floats x2 (inverse x0.5), integers +1 (inverse -1)
+hipError_t cs_comm_scramble(void* buf, int64_t n, int kind, int inverse, hipStream_t stream);
+
 // ---------------------------------------------------------------- decoder-LM elementwise ops (lm.hip)
 enum { CS_F32 = 0, CS_BF16 = 1 };
 int cs_rmsnorm_bwd_partials(int rows);

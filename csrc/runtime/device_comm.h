@@ -1,0 +1,56 @@
+// Stream-ordered communicator interface the C++ engines drive.
+//
+// The engine's data-parallel step (VggEngine::step) only needs four things from a
+// transport: an all-reduce and a broadcast that run behind a fork from a compute
+// stream, a join back into a compute stream, and the rank/world. Three
+// implementations share that contract:
+//  * RcclComm   — the production data plane: RCCL over xGMI on a dedicated comm stream
+//                 (one GPU per rank, rccl_comm.h);
+//  * StagedComm — the same collectives through a c10d ProcessGroup (gloo) with host
+//                 staging, so the exact C++ step runs with N ranks that share ONE GPU
+//                 (RCCL refuses two ranks on one device) and on the 1-GPU test box;
+//  * ProbeComm  — world 1, every collective replaced by a delay kernel plus an exact
+//                 scramble / unscramble of the buffer on the comm stream: a missing fork
+//                 or join in the engine shows up as a bitwise mismatch (ordering test).
+// Contract of every collective: with fork = true the comm stream first waits for everything
+// already enqueued on `compute` (fork = false: no fork, ordered only behind what the comm
+// stream already holds — `compute` may be the null stream, so "no fork" is a flag, never a
+// null stream); the collective runs on the comm stream; join(compute) makes `compute` wait
+// for everything enqueued on the comm stream so far. Nothing blocks the
+// host except where an implementation says so (StagedComm).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <string>
+
+namespace cs {
+
+class DeviceComm {
+ public:
+  virtual ~DeviceComm() = default;
+  virtual int rank() const = 0;
+  virtual int world() const = 0;
+  virtual hipStream_t stream() const = 0;
+  virtual const char* kind() const = 0;
+  virtual void all_reduce(void* buf, size_t count, ncclDataType_t dt, ncclRedOp_t op, hipStream_t compute,
+                          bool fork) = 0;
+  virtual void broadcast(void* buf, size_t count, ncclDataType_t dt, int root, hipStream_t compute, bool fork) = 0;
+  virtual void join(hipStream_t compute) = 0;
+  // async error polling: "" when healthy
+  virtual std::string async_error() { return std::string(); }
+  virtual void abort() {}
+  // collectives issued so far (tests / fault injection)
+  virtual int64_t calls() const { return 0; }
+};
+
+inline size_t comm_dtype_bytes(ncclDataType_t dt) {
+  switch (dt) {
+    case ncclInt8: case ncclUint8: return 1;
+    case ncclFloat16: case ncclBfloat16: return 2;
+    case ncclInt32: case ncclUint32: case ncclFloat32: return 4;
+    default: return 8;
+  }
+}
+
+}  // namespace cs

@@ -4,6 +4,8 @@
 #include <cstring>
 #include <stdexcept>
 
+#include "runtime/fault.h"
+
 namespace cs {
 
 namespace {
@@ -72,6 +74,7 @@ RcclComm::~RcclComm() {
 }
 
 void RcclComm::fork(hipStream_t compute) {
+  if (aborted_) throw std::runtime_error("RcclComm: communicator aborted");
   // inside ncclGroupStart/End the first op's fork covers the whole group
   if (value_sync_) {
     ++fork_seq_;
@@ -97,55 +100,71 @@ void RcclComm::join(hipStream_t compute) {
   hip_ok(hipStreamWaitEvent(compute, join_event_, 0), "hipStreamWaitEvent(join)");
 }
 
-void RcclComm::all_reduce(void* buf, size_t count, ncclDataType_t dt, ncclRedOp_t op, hipStream_t compute) {
-  fork(compute);
+void RcclComm::all_reduce(void* buf, size_t count, ncclDataType_t dt, ncclRedOp_t op, hipStream_t compute,
+                          bool do_fork) {
+  ++calls_;
+  fault_point("all_reduce", rank_);
+  if (aborted_) throw std::runtime_error("RcclComm: communicator aborted");
+  if (do_fork) fork(compute);
   nccl_ok(ncclAllReduce(buf, buf, count, dt, op, comm_, stream_), "ncclAllReduce");
 }
 
-void RcclComm::broadcast(void* buf, size_t count, ncclDataType_t dt, int root, hipStream_t compute) {
-  if (compute != nullptr) fork(compute);  // null: ordered only behind what the comm stream already has
+void RcclComm::broadcast(void* buf, size_t count, ncclDataType_t dt, int root, hipStream_t compute,
+                         bool do_fork) {
+  ++calls_;
+  fault_point("broadcast", rank_);
+  if (aborted_) throw std::runtime_error("RcclComm: communicator aborted");
+  if (do_fork) fork(compute);  // no fork: ordered only behind what the comm stream already has
   nccl_ok(ncclBroadcast(buf, buf, count, dt, root, comm_, stream_), "ncclBroadcast");
 }
 
 void RcclComm::all_gather(const void* send, void* recv, size_t count, ncclDataType_t dt, hipStream_t compute) {
+  ++calls_;
   fork(compute);
   nccl_ok(ncclAllGather(send, recv, count, dt, comm_, stream_), "ncclAllGather");
 }
 
 void RcclComm::reduce_scatter(const void* send, void* recv, size_t count, ncclDataType_t dt, ncclRedOp_t op,
                               hipStream_t compute) {
+  ++calls_;
   fork(compute);
   nccl_ok(ncclReduceScatter(send, recv, count, dt, op, comm_, stream_), "ncclReduceScatter");
 }
 
 void RcclComm::reduce(const void* send, void* recv, size_t count, ncclDataType_t dt, ncclRedOp_t op, int root,
                       hipStream_t compute) {
+  ++calls_;
   fork(compute);
   nccl_ok(ncclReduce(send, recv, count, dt, op, root, comm_, stream_), "ncclReduce");
 }
 
 void RcclComm::gather(const void* send, void* recv, size_t count, ncclDataType_t dt, int root, hipStream_t compute) {
+  ++calls_;
   fork(compute);
   nccl_ok(ncclGather(send, recv, count, dt, root, comm_, stream_), "ncclGather");
 }
 
 void RcclComm::scatter(const void* send, void* recv, size_t count, ncclDataType_t dt, int root,
                        hipStream_t compute) {
+  ++calls_;
   fork(compute);
   nccl_ok(ncclScatter(send, recv, count, dt, root, comm_, stream_), "ncclScatter");
 }
 
 void RcclComm::all_to_all(const void* send, void* recv, size_t count, ncclDataType_t dt, hipStream_t compute) {
+  ++calls_;
   fork(compute);
   nccl_ok(ncclAllToAll(send, recv, count, dt, comm_, stream_), "ncclAllToAll");
 }
 
 void RcclComm::send(const void* buf, size_t count, ncclDataType_t dt, int peer, hipStream_t compute) {
+  ++calls_;
   if (group_depth_ == 0) fork(compute);
   nccl_ok(ncclSend(buf, count, dt, peer, comm_, stream_), "ncclSend");
 }
 
 void RcclComm::recv(void* buf, size_t count, ncclDataType_t dt, int peer, hipStream_t compute) {
+  ++calls_;
   if (group_depth_ == 0) fork(compute);
   nccl_ok(ncclRecv(buf, count, dt, peer, comm_, stream_), "ncclRecv");
 }
@@ -162,6 +181,7 @@ void RcclComm::group_end() {
 }
 
 std::string RcclComm::async_error() {
+  if (aborted_) return "aborted";
   ncclResult_t r = ncclSuccess;
   if (ncclCommGetAsyncError(comm_, &r) != ncclSuccess) return "ncclCommGetAsyncError failed";
   return r == ncclSuccess ? std::string() : std::string(ncclGetErrorString(r));

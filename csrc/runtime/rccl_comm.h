@@ -15,9 +15,11 @@
 #include <string>
 #include <vector>
 
+#include "runtime/device_comm.h"
+
 namespace cs {
 
-class RcclComm {
+class RcclComm final : public DeviceComm {
  public:
   static std::string unique_id();  // 128 raw bytes (NCCL_UNIQUE_ID_BYTES)
 
@@ -26,15 +28,18 @@ class RcclComm {
   RcclComm(const RcclComm&) = delete;
   RcclComm& operator=(const RcclComm&) = delete;
 
-  int rank() const { return rank_; }
-  int world() const { return world_; }
-  hipStream_t stream() const { return stream_; }
+  int rank() const override { return rank_; }
+  int world() const override { return world_; }
+  hipStream_t stream() const override { return stream_; }
+  const char* kind() const override { return "rccl"; }
+  int64_t calls() const override { return calls_; }
 
   // All calls: the comm stream first waits for everything already enqueued on
   // `compute`; the collective then runs on the comm stream. join() makes `compute`
   // wait for everything enqueued on the comm stream so far.
-  void all_reduce(void* buf, size_t count, ncclDataType_t dt, ncclRedOp_t op, hipStream_t compute);
-  void broadcast(void* buf, size_t count, ncclDataType_t dt, int root, hipStream_t compute);
+  void all_reduce(void* buf, size_t count, ncclDataType_t dt, ncclRedOp_t op, hipStream_t compute,
+                  bool fork = true) override;
+  void broadcast(void* buf, size_t count, ncclDataType_t dt, int root, hipStream_t compute, bool fork = true) override;
   void all_gather(const void* send, void* recv, size_t count, ncclDataType_t dt, hipStream_t compute);
   void reduce_scatter(const void* send, void* recv, size_t count, ncclDataType_t dt, ncclRedOp_t op,
                       hipStream_t compute);
@@ -47,10 +52,10 @@ class RcclComm {
   void recv(void* buf, size_t count, ncclDataType_t dt, int peer, hipStream_t compute);
   void group_start(hipStream_t compute);  // forks once for the whole group
   void group_end();
-  void join(hipStream_t compute);
+  void join(hipStream_t compute) override;
   // async error polling: returns "" when healthy
-  std::string async_error();
-  void abort();
+  std::string async_error() override;
+  void abort() override;
 
  private:
   void fork(hipStream_t compute);
@@ -69,6 +74,7 @@ class RcclComm {
   int rank_ = 0, world_ = 1, device_ = 0;
   int group_depth_ = 0;
   bool aborted_ = false;
+  int64_t calls_ = 0;
 };
 
 }  // namespace cs

@@ -468,11 +468,14 @@ VggEngine::~VggEngine() {
 void VggEngine::sgd(double lr, double momentum, double wd, double dampening, int64_t off, int64_t n) {
   TORCH_CHECK(off >= 0 && n >= 0 && off + n <= params_.numel(), "sgd: range");
   if (n == 0) return;
-  // momentum buffers start at zero, so buf = 0*mom + (1-damp)*d == torch's first-step clone for damp = 0
-  // the step's one optimizer launch also advances the device-side batch cursor
+  // first step (set_sgd_first): buf = d, torch's clone — with dampening 0 bit-equal to the
+  // 0*mom + (1-damp)*d of later steps. The step's one optimizer launch also advances the
+  // device-side batch cursor
   ok(cs_sgd_flat(P(off), G(off), mom_.data_ptr<float>() + off, n, (float)lr, (float)momentum, (float)wd,
-                 (float)dampening, 1.0f, 0, cur_stream(), perm_len_ > 0 ? cursor_.data_ptr<int64_t>() : nullptr),
+                 (float)dampening, 1.0f, sgd_first_ ? 1 : 0, cur_stream(),
+                 perm_len_ > 0 ? cursor_.data_ptr<int64_t>() : nullptr),
      "sgd_flat");
+  sgd_first_ = false;
 }
 
 hipEvent_t VggEngine::opt_event() { return ev_opt_[next_opt_ev_++ % ev_opt_.size()]; }
@@ -510,7 +513,7 @@ std::vector<std::pair<std::string, double>> VggEngine::phase_times() {
   return out;
 }
 
-void VggEngine::sgd_bucket(RcclComm* comm, int64_t lo_block, int64_t off, int64_t n, double lr, double momentum,
+void VggEngine::sgd_bucket(DeviceComm* comm, int64_t lo_block, int64_t off, int64_t n, double lr, double momentum,
                            double wd, double dampening, bool advance_cursor) {
   TORCH_CHECK(off >= 0 && n >= 0 && off + n <= params_.numel(), "sgd_bucket: range");
   TORCH_CHECK(lo_block >= 0 && lo_block < (int64_t)blocks_.size(), "sgd_bucket: block");
@@ -519,16 +522,17 @@ void VggEngine::sgd_bucket(RcclComm* comm, int64_t lo_block, int64_t off, int64_
   ok(hipEventRecord(e, s), "record main");
   ok(hipStreamWaitEvent(opt_, e, 0), "opt wait main");
   if (overlap_wgrad_) ok(hipStreamWaitEvent(opt_, ev_wg_[lo_block], 0), "opt wait wgrad");
-  if (comm != nullptr && comm->world() > 1) {
+  if (comm != nullptr) {
     hipEvent_t c = opt_event();
     ok(hipEventRecord(c, comm->stream()), "record comm");
     ok(hipStreamWaitEvent(opt_, c, 0), "opt wait comm");
   }
   if (n == 0) return;
   ok(cs_sgd_flat(P(off), G(off), mom_.data_ptr<float>() + off, n, (float)lr, (float)momentum, (float)wd,
-                 (float)dampening, 1.0f, 0, opt_,
+                 (float)dampening, 1.0f, sgd_first_ ? 1 : 0, opt_,
                  advance_cursor && perm_len_ > 0 ? cursor_.data_ptr<int64_t>() : nullptr),
      "sgd_flat(bucket)");
+  if (advance_cursor) sgd_first_ = false;  // the step's last bucket
 }
 
 void VggEngine::join_opt() {
@@ -564,20 +568,16 @@ void VggEngine::forward_eval(int64_t B) {
      "linear_xent");
 }
 
-void VggEngine::step(int64_t B, RcclComm* comm, const std::vector<int64_t>& bucket_blocks,
+void VggEngine::step(int64_t B, DeviceComm* comm, const std::vector<int64_t>& bucket_blocks,
                      const std::vector<int64_t>& bucket_ranges, bool broadcast_buffers, double lr, double momentum,
                      double wd, double dampening) {
   const int64_t L = (int64_t)blocks_.size();
   const size_t nb = bucket_blocks.size();
   TORCH_CHECK(nb >= 1 && bucket_ranges.size() == 2 * nb && bucket_blocks.back() == 0, "step: bucket plan");
   hipStream_t s = cur_stream();
-  // CS_COMM_PROBE=1 (measurement only): run the collectives and their stream fork/join even on a
-  // one-rank communicator, to price the data-parallel plumbing on a single GPU
-  static const bool probe = [] {
-    const char* e = getenv("CS_COMM_PROBE");
-    return e != nullptr && atoi(e) != 0;
-  }();
-  const bool dp = comm != nullptr && (comm->world() > 1 || probe);
+  // the caller passes a communicator only when the step is data-parallel (a one-rank
+  // communicator too: the CS_COMM_PROBE measurement and the ProbeComm ordering test)
+  const bool dp = comm != nullptr;
   tn_ = 0;
   mark("start");
   forward_train(B);
@@ -602,7 +602,7 @@ void VggEngine::step(int64_t B, RcclComm* comm, const std::vector<int64_t>& buck
     // all-reduce from there, so it overlaps the rest of the backward on the main stream
     if (dp)
       comm->all_reduce(G(bucket_ranges[2 * k]), bucket_ranges[2 * k + 1], ncclFloat32, ncclAvg,
-                       overlap_wgrad_ ? side_ : s);
+                       overlap_wgrad_ ? side_ : s, /*fork=*/!(debug_skip_ & 2));
     if (dp && broadcast_buffers && k == 0) {
       // DDP broadcast_buffers (rank 0's BN running stats before every training forward), issued
       // for the NEXT forward right behind the first bucket: this forward has produced the
@@ -610,8 +610,8 @@ void VggEngine::step(int64_t B, RcclComm* comm, const std::vector<int64_t>& buck
       // orders them before it — no fork/join of its own at the head of the step (step 0 is
       // covered by the construction-time broadcast)
       // (no fork: the all-reduce just enqueued already waited for the forward)
-      comm->broadcast(bufs_.data_ptr<float>(), bufs_.numel(), ncclFloat32, 0, nullptr);
-      comm->broadcast(nbt_.data_ptr<int64_t>(), nbt_.numel(), ncclInt64, 0, nullptr);
+      comm->broadcast(bufs_.data_ptr<float>(), bufs_.numel(), ncclFloat32, 0, s, /*fork=*/false);
+      comm->broadcast(nbt_.data_ptr<int64_t>(), nbt_.numel(), ncclInt64, 0, s, /*fork=*/false);
     }
     // ... and its SGD can run as soon as the averaged gradient is in and block lo's data
     // gradient (the last reader of these weights) is done, beside the backward below
@@ -619,7 +619,7 @@ void VggEngine::step(int64_t B, RcclComm* comm, const std::vector<int64_t>& buck
       sgd_bucket(comm, lo, bucket_ranges[2 * k], bucket_ranges[2 * k + 1], lr, momentum, wd, dampening, k + 1 == nb);
   }
   if (overlap_wgrad_) ok(hipStreamWaitEvent(s, ev_wg_[0], 0), "join side");
-  if (dp) comm->join(s);
+  if (dp && !(debug_skip_ & 1)) comm->join(s);
   mark("allreduce_wait");
   if (tiled) join_opt();
   else sgd(lr, momentum, wd, dampening, 0, params_.numel());

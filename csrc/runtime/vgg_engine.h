@@ -24,7 +24,7 @@
 #include <vector>
 
 #include "kernels/launchers.h"
-#include "runtime/rccl_comm.h"
+#include "runtime/device_comm.h"
 
 namespace cs {
 
@@ -91,10 +91,16 @@ class VggEngine {
   // lo_block's data gradient is the last reader of its weights) and, with a communicator, for the
   // bucket's all-reduce already enqueued on the comm stream. advance_cursor: the step's last
   // bucket moves the device-side batch cursor. join_opt() makes the current stream wait for it.
-  void sgd_bucket(RcclComm* comm, int64_t lo_block, int64_t off, int64_t n, double lr, double momentum, double wd,
+  void sgd_bucket(DeviceComm* comm, int64_t lo_block, int64_t off, int64_t n, double lr, double momentum, double wd,
                   double dampening, bool advance_cursor);
   void join_opt();
   void set_sgd_overlap(bool on) { sgd_overlap_ = on; }
+  // torch.optim.SGD's first step sets buf = d (no dampening): the next step's SGD launches
+  // use first = 1 (only matters with dampening != 0); cleared once that step's SGD is enqueued
+  void set_sgd_first(bool on) { sgd_first_ = on; }
+  // test-only ordering faults for the ProbeComm test's negative control (tests must see a
+  // mismatch): bit 0 = step() skips the join before SGD, bit 1 = its all-reduces skip the fork
+  void set_debug_skip(int64_t mask) { debug_skip_ = (int)mask; }
   // conv autotune candidates (CS_CONV_MATH): 0 f32, 1 x6, 2 f32 + x6 (default), 3 bf16 operands
   void set_math(int64_t m) {
     TORCH_CHECK(m >= 0 && m <= 3, "set_math: 0..3");
@@ -103,10 +109,11 @@ class VggEngine {
   // eval forward (running stats): loss (mean over the batch) -> loss(), correct count -> correct()
   void forward_eval(int64_t B);
 
-  // whole step in C++: forward, bucketed backward with (optional) RCCL all-reduce(avg)
-  // of each bucket as soon as it is complete, SGD. bucket_blocks[k] = lowest block of
+  // whole step in C++: forward, bucketed backward with (optional) all-reduce(avg) of each
+  // bucket on `comm` (RcclComm on a multi-GPU job; StagedComm / ProbeComm in tests: any
+  // DeviceComm, device_comm.h) as soon as it is complete, SGD. comm == nullptr: no DP. bucket_blocks[k] = lowest block of
   // bucket k (buckets cover blocks from the top), bucket_ranges = (off, n) per bucket.
-  void step(int64_t B, RcclComm* comm, const std::vector<int64_t>& bucket_blocks,
+  void step(int64_t B, DeviceComm* comm, const std::vector<int64_t>& bucket_blocks,
             const std::vector<int64_t>& bucket_ranges, bool broadcast_buffers, double lr, double momentum,
             double wd, double dampening);
 
@@ -187,6 +194,8 @@ class VggEngine {
   // the graph's cross-stream fork/join edges cost far more than the 28 us SGD they hide
   hipStream_t opt_ = nullptr;
   bool sgd_overlap_ = false;
+  bool sgd_first_ = false;
+  int debug_skip_ = 0;
   std::vector<hipEvent_t> ev_opt_;  // pool: main-stream / comm-stream marks per bucket, opt done
   size_t next_opt_ev_ = 0;
   hipEvent_t opt_event();

@@ -1,26 +1,51 @@
-"""Multi-rank native engine on ONE MI355X: two processes share cuda:0 and talk over
-gloo (RCCL refuses two ranks on one device), which exercises everything but the
-transport: construction-time broadcast, per-step BN-buffer broadcast, bucketed
-all-reduce between segment graphs, the faithful sync modes, replica equality."""
+"""Multi-rank native engine on ONE MI355X.
+
+RCCL refuses two ranks on one device ("Duplicate GPU detected", measured on the 1-GPU
+box), so N processes share cuda:0 and talk over gloo:
+
+* ``comm="staged"``: the native C++ ``StagedComm`` (csrc/runtime/staged_comm.h) drives the
+  EXACT C++ data-parallel step the N-GPU benchmark runs (``VggEngine::step``: per-bucket
+  all-reduce forked from the backward, BN-buffer broadcast behind bucket 0, join before
+  SGD) — only the wire differs from RcclComm. Replicas must be bitwise identical and
+  equal to the Python-orchestrated segment-graph path.
+* ``comm="torch"``: the segment-graph path with collectives from Python (the reference's
+  part3 loop shape, `master/part3/part3.py:116-123`).
+* ``probe="order"`` (world 1): every collective is a scramble + spin + unscramble on the
+  comm stream; the step must stay bitwise equal to a no-comm run, and skipping the join
+  (negative control) must not.
+"""
+import os
+import socket
+import subprocess
+import sys
+import textwrap
+
 import pytest
 import torch
 
 from mp_util import run_world
 
-pytestmark = [pytest.mark.gpu, pytest.mark.slow]
+pytestmark = [pytest.mark.gpu]
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _train(rank, world, sync, graph, steps):
+def _train(rank, world, sync, graph, steps, comm="torch", B=16):
     from cs744_pytorch_distributed_tutorial_amd.runtime.engine import NativeTrainer
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    tr = NativeTrainer(batch_size=16, device=dev, rank=rank, world=world, sync=sync, comm="torch", bucket_mb=2.0,
-                       graph=graph, train_size=512, test_size=32, autotune=False)
+    tr = NativeTrainer(batch_size=B, device=dev, rank=rank, world=world, sync=sync, comm=comm, bucket_mb=2.0,
+                       graph=graph, train_size=512, test_size=64, autotune=False, check_every=1)
     for _ in range(steps):
         tr.step()
     torch.cuda.synchronize()
-    return {"params": tr.params.cpu(), "bufs": tr.bufs.cpu(), "nbt": tr.nbt.cpu(), "loss": tr.last_loss(),
-            "buckets": len(tr.bucket_lows), "graph": tr.graph_mode}
+    ev = tr.evaluate(max_batches=2)
+    out = {"params": tr.params.cpu(), "mom": tr.mom.cpu(), "bufs": tr.bufs.cpu(), "nbt": tr.nbt.cpu(),
+           "loss": tr.last_loss(), "buckets": len(tr.bucket_lows), "graph": tr.graph_mode,
+           "calls": tr.native_comm.calls() if tr.native_comm is not None else -1,
+           "kind": tr.native_comm.kind if tr.native_comm is not None else "none", "eval": ev}
+    tr.close()
+    return out
 
 
 @pytest.fixture(scope="module")
@@ -29,6 +54,7 @@ def gpu():
         pytest.skip("no GPU")
 
 
+@pytest.mark.slow
 def test_ddp_segments_replicas_identical_and_match_eager(gpu):
     seg = run_world(_train, 2, "ddp", "segments", 4)
     eag = run_world(_train, 2, "ddp", "none", 4)
@@ -42,9 +68,156 @@ def test_ddp_segments_replicas_identical_and_match_eager(gpu):
     assert torch.equal(seg[1]["nbt"], seg[0]["nbt"])
 
 
+@pytest.mark.slow
+@pytest.mark.parametrize("world", [2, 4])
+def test_cpp_ddp_step_multi_rank_staged(gpu, world):
+    """The N>1 benchmark's C++ step (not _step_eager) with `world` ranks on one GPU."""
+    steps = 5
+    nat = run_world(_train, world, "ddp", "none", steps, "staged")
+    ref = run_world(_train, world, "ddp", "segments", steps, "torch")
+    nb = nat[0]["buckets"]
+    assert nb > 1 and nat[0]["kind"] == "staged"
+    # construction: 4 broadcasts; per step: one all-reduce per bucket + 2 buffer broadcasts
+    assert nat[0]["calls"] == steps * (nb + 2), nat[0]["calls"]
+    for r in range(world):
+        for k in ("params", "mom", "bufs", "nbt"):
+            assert torch.equal(nat[r][k], nat[0][k]), (r, k)
+        assert nat[r]["eval"]["global_correct"] == world * nat[r]["eval"]["correct"]
+    # same gradients, same averaging bytes, same SGD: the C++ step equals the Python-orchestrated one
+    assert torch.equal(nat[0]["params"], ref[0]["params"])
+    assert torch.equal(nat[0]["mom"], ref[0]["mom"])
+    assert nat[0]["loss"] == ref[0]["loss"]
+
+
+def _ragged(rank, world):
+    from cs744_pytorch_distributed_tutorial_amd.runtime.engine import NativeTrainer
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    tr = NativeTrainer(batch_size=16, device=dev, rank=rank, world=world, comm="staged", graph="none",
+                       train_size=80, test_size=16, autotune=False, drop_last=False)
+    assert tr.steps_per_epoch() == 3
+    for _ in range(3):
+        tr.step()
+    torch.cuda.synchronize()
+    out = {"params": tr.params.cpu(), "loss": tr.last_loss()}
+    tr.close()
+    return out
+
+
+@pytest.mark.slow
+def test_staged_ragged_last_batch(gpu):
+    """drop_last=False ragged batch through the multi-rank C++ step: 2 ranks x 40 samples at
+    B=16 -> batches 16, 16, 8."""
+    out = run_world(_ragged, 2)
+    assert torch.equal(out[0]["params"], out[1]["params"])
+    assert torch.isfinite(out[0]["params"]).all()
+
+
+@pytest.mark.slow
 def test_sync_modes_agree(gpu):
     ref = run_world(_train, 2, "ddp", "none", 2)[0]["params"]
     for mode in ("allreduce", "flat"):
         out = run_world(_train, 2, mode, "segments", 2)
         assert torch.equal(out[0]["params"], out[1]["params"]), mode
         torch.testing.assert_close(out[0]["params"], ref, rtol=1e-5, atol=1e-6, msg=mode)
+
+
+def _probe_run(probe, steps=6, skip=0, sgd_overlap=False):
+    from cs744_pytorch_distributed_tutorial_amd.runtime.engine import NativeTrainer
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    tr = NativeTrainer(batch_size=32, device=dev, bucket_mb=1.0, graph="none", train_size=512, test_size=32,
+                       autotune=False, probe=probe, probe_spin_us=40.0)
+    tr.engine.set_debug_skip(skip)
+    tr.engine.set_sgd_overlap(sgd_overlap)
+    for _ in range(steps):
+        tr.step()
+    torch.cuda.synchronize()
+    out = {k: getattr(tr, k).clone() for k in ("params", "mom", "bufs", "nbt")}
+    calls = tr.native_comm.calls() if tr.native_comm is not None else 0
+    tr.close()
+    return out, calls
+
+
+def test_probe_comm_ordering_bitwise(gpu):
+    base, _ = _probe_run("0")
+    probed, calls = _probe_run("order")
+    assert calls > 6
+    for k in base:
+        assert torch.equal(base[k], probed[k]), k
+    # per-bucket SGD on the optimizer stream must wait for each bucket's collective too
+    ovl, _ = _probe_run("order", sgd_overlap=True)
+    for k in base:
+        assert torch.equal(base[k], ovl[k]), ("sgd_overlap", k)
+
+
+def test_probe_comm_detects_missing_join(gpu):
+    """Negative control: without the join before SGD the scrambled gradients are consumed."""
+    base, _ = _probe_run("0")
+    bad, _ = _probe_run("order", skip=1)
+    assert not torch.equal(base["params"], bad["params"])
+
+
+def test_rccl_one_rank_abort_path(gpu):
+    """World-1 RCCL: async-error poll is clean, abort() makes the next collective raise
+    instead of touching a freed communicator."""
+    from cs744_pytorch_distributed_tutorial_amd.runtime.engine import NativeTrainer
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    tr = NativeTrainer(batch_size=16, device=dev, graph="none", train_size=128, test_size=16, autotune=False,
+                       probe="1", check_every=1)
+    tr.step()
+    tr.step()
+    torch.cuda.synchronize()
+    assert tr.native_comm.kind == "rccl" and tr.native_comm.async_error() == ""
+    tr.abort()
+    assert tr.native_comm.async_error() == "aborted"
+    with pytest.raises(RuntimeError, match="aborted"):
+        tr.step()
+    tr.native_comm = None  # aborted: nothing to join
+    tr.close()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.slow
+def test_killed_rank_fails_peer_promptly(gpu):
+    """CS744_FAULT kills rank 1 inside the native all-reduce of step 3: rank 0 must exit
+    non-zero within seconds (gloo sees the closed connection), not hang."""
+    port = _free_port()
+    code = textwrap.dedent(f"""
+        import os, sys
+        sys.path.insert(0, {ROOT!r})
+        import torch
+        from cs744_pytorch_distributed_tutorial_amd import distributed as D
+        rank = int(sys.argv[1])
+        if rank == 1:
+            os.environ["CS744_FAULT"] = "all_reduce@7:1:kill"
+        D.init_process_group("gloo", rank=rank, world_size=2, master_addr="127.0.0.1", master_port={port},
+                             timeout_s=60)
+        from cs744_pytorch_distributed_tutorial_amd.runtime.engine import NativeTrainer
+        torch.cuda.set_device(0)
+        tr = NativeTrainer(batch_size=16, rank=rank, world=2, comm="staged", graph="none", train_size=256,
+                           test_size=16, autotune=False, check_every=1)
+        for _ in range(10):
+            tr.step()
+        torch.cuda.synchronize()
+        print("finished", flush=True)
+    """)
+    procs = [subprocess.Popen([sys.executable, "-c", code, str(r)], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                              text=True) for r in range(2)]
+    try:
+        outs = [p.communicate(timeout=100) for p in procs]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    assert procs[1].returncode == 17, outs[1][1][-800:]
+    assert procs[0].returncode != 0 and "finished" not in outs[0][0], outs[0][1][-800:]
