@@ -62,6 +62,8 @@ def parse(argv=None):
     p.add_argument("--no-graph", action="store_true", help="native engine: same as --graph none")
     p.add_argument("--graph", type=str, default="auto", choices=["auto", "full", "segments", "none"])
     p.add_argument("--json-out", type=str, default=None)
+    p.add_argument("--watchdog-s", type=float, default=600.0,
+                   help="abort the communicator and exit(18) if one step stalls this long (0 = off)")
     p.add_argument("--phases", type=int, default=0,
                    help="native engine: after the timed steps, N more steps with per-phase device timing "
                         "(forward / bucket backward / all-reduce wait / SGD), printed to stderr as JSON")
@@ -112,19 +114,32 @@ def main(argv=None) -> int:
     device = D.device() if world > 1 else torch.device("cuda", 0)
     torch.cuda.set_device(device)
     trainer = make_trainer(args, device, rank, world)
+    # a dead peer leaves RCCL kernels spinning forever: the watchdog turns that into ncclCommAbort
+    # + a prompt non-zero exit; kicked once per step, nothing on the device
+    from cs744_pytorch_distributed_tutorial_amd.utils.faults import Watchdog
+    wd = Watchdog(args.watchdog_s, "bench step", on_timeout=getattr(trainer, "abort", None)).start() \
+        if args.watchdog_s > 0 else None
 
     for _ in range(args.warmup):
         trainer.step()
+        if wd is not None:
+            wd.kick()
     torch.cuda.synchronize()
     D.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         trainer.step()
+        if wd is not None:
+            wd.kick()
     torch.cuda.synchronize()
     D.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    if wd is not None:
+        wd.stop()
+    if hasattr(trainer, "check_comm"):
+        trainer.check_comm()  # async RCCL errors surface here instead of as a silent bad number
     elapsed = D.all_reduce_scalar(elapsed, op=D.ReduceOp.MAX) if world > 1 else elapsed
     loss = trainer.last_loss()
     metric, unit, gbatch, seq, baseline, data = describe(args, trainer, world)
@@ -155,6 +170,7 @@ def main(argv=None) -> int:
         # split-bf16 x6 kernels (3 bf16 pieces per operand, 6 MFMAs; f64-checked like the f32 path)
         maths = [t["math"] for t in trainer.tile_table()]
         out["config"]["conv_gemm_math"] = {m: maths.count(m) for m in sorted(set(maths))}
+        out["config"]["conv_tiles"] = getattr(trainer, "tile_source", None)
     if args.phases > 0 and hasattr(trainer, "phase_breakdown"):
         ph = trainer.phase_breakdown(args.phases)
         if rank == 0:

@@ -316,3 +316,122 @@ def test_bn_reduce_in_wgrad_launch_bitwise_equal(dev, keep, monkeypatch):
         out.append((t.params.clone(), t.mom.clone(), t.bufs.clone()))
     for a, b in zip(out[0], out[1]):
         assert torch.equal(a, b)
+
+
+class _FixedDecisionVGG(torch.nn.Module):
+    """float64 VGG whose ReLU masks and 2x2 max-pool argmaxes are the engine's own fp32
+    decisions (recomputed exactly from the engine's conv outputs y and BN coefficients:
+    sign(fma(y, scale, shift)) is the sign of the exact fp64 value y*scale + shift). A
+    pre-activation within fp32 rounding of 0 then cannot flip a mask between the engine and
+    the reference, so every gradient tensor is comparable at fp32 accuracy (with free
+    decisions about one such flip per million activations is expected at B=64)."""
+
+    def __init__(self, ref, tr, B):
+        super().__init__()
+        self.ref, self.specs = ref, tr.layout.specs
+        self.sel = []
+        for l, spec in enumerate(self.specs):
+            H, C = spec.hw, spec.cout
+            y = tr.engine.tensor(l, "y")[:B * H * H].double().cpu().view(B, H, H, C)
+            bn = tr.engine.tensor(l, "bn").double().cpu()
+            z = (y * bn[0] + bn[1]).float().clamp_min(0.0)  # the kernel's fmaxf(fma(y, sc, sh), 0)
+            if spec.pool:
+                w = z.view(B, H // 2, 2, H // 2, 2, C).permute(0, 1, 3, 5, 2, 4).reshape(B, H // 2, H // 2, C, 4)
+                am = torch.zeros(w.shape[:-1], dtype=torch.long)
+                for p in range(1, 4):  # first strict maximum in window order, as the kernel scans
+                    am = torch.where(w[..., p] > w.gather(-1, am[..., None])[..., 0], torch.full_like(am, p), am)
+                pos = w.gather(-1, am[..., None])[..., 0] > 0
+                one = torch.nn.functional.one_hot(am, 4).bool() & pos[..., None]
+                sel = one.view(B, H // 2, H // 2, C, 2, 2).permute(0, 3, 1, 4, 2, 5).reshape(B, C, H, H)
+            else:
+                sel = (z > 0).permute(0, 3, 1, 2)
+            self.sel.append(sel.double())
+
+    def forward(self, x):
+        L = self.ref.layers
+        for l, spec in enumerate(self.specs):
+            x = L[spec.bn_idx](L[spec.conv_idx](x)) * self.sel[l]
+            if spec.pool:
+                x = F.avg_pool2d(x, 2) * 4.0  # exactly one selected element per window
+        return self.ref.fc1(x.flatten(1))
+
+
+def _grads_vs_fp64(tr, B, offset=0):
+    """One forward + full backward of the engine at batch B (<= Bmax; B < Bmax is the ragged
+    last batch of an epoch) on the sampler's first B samples vs the decision-aligned float64
+    VGG11 on the same augmented inputs: loss, then every gradient tensor. Returns (n tensors
+    within 1e-4 relative, n checked, global relative L2 error, worst relative error)."""
+    from cs744_pytorch_distributed_tutorial_amd.models import VGG11
+    from cs744_pytorch_distributed_tutorial_amd.utils import data as dm
+    ref = VGG11().double()
+    ref.load_state_dict({k: v.double() if v.is_floating_point() else v for k, v in tr.state_dict().items()})
+    idx = torch.tensor(tr.sampler.indices()[offset:offset + B])
+    tr.engine.set_perm(idx)
+    tr.engine.forward_train(B)
+    tr.engine.backward(tr.layout.L - 1, 0, B)
+    torch.cuda.synchronize()
+    model = _FixedDecisionVGG(ref, tr, B)
+    x = dm.augment_reference(tr.train_set.data, idx, tr.aug_train.cpu()).double()
+    y = tr.train_set.targets[idx]
+    loss = F.cross_entropy(model(x), y)
+    loss.backward()
+    assert abs(tr.last_loss() - loss.item()) <= 1e-5 * max(1.0, abs(loss.item())), (tr.last_loss(), loss.item())
+    g = tr.grads_state()
+    conv_bias = {f"layers.{s.conv_idx}.bias" for s in tr.layout.specs}
+    tight = checked = 0
+    num = den = 0.0
+    worst = []
+    for n, p in ref.named_parameters():
+        if n in conv_bias:  # ~0 (BN removes it): absolute bound only
+            assert g[n].abs().max() < 1e-4, n
+            continue
+        checked += 1
+        r = _rel(g[n], p.grad)
+        worst.append((r, n))
+        tight += r < 1e-4
+        num += float(((g[n].double() - p.grad) ** 2).sum())
+        den += float((p.grad ** 2).sum())
+    worst.sort(reverse=True)
+    print("[parity] worst tensors:", ", ".join(f"{n} {r:.1e}" for r, n in worst[:6]))
+    return tight, checked, (num / den) ** 0.5, worst[0][0]
+
+
+def _force_x6s(tr):
+    """Every conv GEMM of the step on the split-bf16 X6S kernels (conv0's padded forward has
+    no X6S variant and stays f32)."""
+    n = 0
+    for l in range(tr.layout.L):
+        for m in range(3):
+            if (l == 0 and m == 1) or (l == 0 and m == 0):
+                continue
+            tr.engine.set_tile(l, m, 64, 64, 2 if m != 0 else 1, 64, 16 | 4)
+            n += 1
+    return n
+
+
+@pytest.mark.parametrize("variant", ["autotuned", "x6s_everywhere", "f32_only"])
+def test_bench_config_b64_matches_fp64(dev, variant):
+    """The benchmarked configuration (B=64; tuned tiles = 22 of 23 GEMMs on X6S split-bf16
+    maths), every X6S GEMM, and f32-MFMA-only tiles vs the decision-aligned fp64 model: every
+    gradient tensor within 1e-4 relative (max-abs normalised)."""
+    tr = _trainer(dev, batch_size=64, train_size=1024, autotune=variant == "autotuned")
+    if variant == "x6s_everywhere":
+        assert _force_x6s(tr) == 22
+        assert sum(t["math"] == "x6s" for t in tr.tile_table()) == 22
+    if variant == "autotuned":
+        assert sum(t["math"] == "x6s" for t in tr.tile_table()) >= 1
+    tight, checked, rel, worst = _grads_vs_fp64(tr, 64)
+    print(f"[parity] B=64 {variant}: {tight}/{checked} tensors within 1e-4 rel, global rel L2 {rel:.3e}")
+    assert tight == checked and worst < 1e-4, (tight, checked, worst)
+    assert rel < 1e-5, rel
+
+
+@pytest.mark.parametrize("B,Bmax", [(20, 64), (80, 128)])
+def test_ragged_batches_match_fp64(dev, B, Bmax):
+    """The reference's ragged last batches (20 at N=4, B=64; 80 in part1 at B=256, SURVEY.md
+    Appendix B) through forward_train / backward with the B=Bmax tile table (X6S where tuned)."""
+    tr = _trainer(dev, batch_size=Bmax, train_size=512, autotune=True)
+    tight, checked, rel, worst = _grads_vs_fp64(tr, B)
+    print(f"[parity] ragged B={B} (Bmax {Bmax}): {tight}/{checked} tensors within 1e-4 rel, global rel L2 {rel:.3e}")
+    assert tight == checked and worst < 1e-4, (tight, checked, worst)
+    assert rel < 1e-5, rel
