@@ -120,6 +120,12 @@ def main(argv=None) -> int:
     wd = Watchdog(args.watchdog_s, "bench step", on_timeout=getattr(trainer, "abort", None)).start() \
         if args.watchdog_s > 0 else None
 
+    import contextlib
+    step_stream = torch.cuda.Stream(device) if os.environ.get("CS_STEP_STREAM", "0") == "1" else None
+    ctx = torch.cuda.stream(step_stream) if step_stream is not None else contextlib.nullcontext()
+    if step_stream is not None:
+        step_stream.wait_stream(torch.cuda.current_stream())
+    ctx.__enter__()
     for _ in range(args.warmup):
         trainer.step()
         if wd is not None:
@@ -136,6 +142,7 @@ def main(argv=None) -> int:
     D.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    ctx.__exit__(None, None, None)
     if wd is not None:
         wd.stop()
     if hasattr(trainer, "check_comm"):

@@ -225,7 +225,8 @@ class NativeTrainer:
                 # ordering test: every collective = spin + exact scramble/unscramble on the comm
                 # stream (parallel/staged.py ProbeComm); a missing fork/join is a bitwise mismatch
                 from ..parallel.staged import ProbeComm
-                self._probe = ProbeComm(self.device.index or 0, probe_spin_us)
+                spin = float(os.environ.get("CS_PROBE_SPIN", probe_spin_us))  # < 0: fork/join only
+                self._probe = ProbeComm(self.device.index or 0, spin)
             else:
                 # measurement only: a one-rank RCCL communicator so the engine's bucketed all-reduce,
                 # buffer broadcast and stream fork/join run (and cost what they cost) on one GPU
@@ -420,7 +421,7 @@ class NativeTrainer:
         ranges = [v for r in self.bucket_ranges for v in r]
         probe = self.world == 1 and self.native_comm is not None
         self.engine.step(B, self.native_comm, self.bucket_lows, ranges,
-                         self.broadcast_buffers and (self.world > 1 or probe),
+                         self.broadcast_buffers and (self.world > 1 or probe) and not os.environ.get("CS_NO_BCAST"),
                          self.lr, self.momentum, self.wd, self.damp)
 
     def _pre_forward_sync(self) -> None:

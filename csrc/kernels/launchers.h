@@ -157,6 +157,13 @@ hipError_t cs_comm_spin(double us, hipStream_t stream);
 // exact invertible scramble: floats x2 (inverse x0.5), integers +1 (inverse -1)
 hipError_t cs_comm_scramble(void* buf, int64_t n, int kind, int inverse, hipStream_t stream);
 
+// ---------------------------------------------------------------- stream links (stream_link.hip)
+// signal: count += 1 on `stream`; wait: ++*expect, then poll until count >= *expect (bounded by
+// timeout_s; on timeout *err = 1 in host-mapped memory). count / expect: device memory, zeroed.
+hipError_t cs_link_signal(unsigned long long* count, hipStream_t stream);
+hipError_t cs_link_wait(const unsigned long long* count, unsigned long long* expect, int* err, double timeout_s,
+                        hipStream_t stream);
+
 // ---------------------------------------------------------------- decoder-LM elementwise ops (lm.hip)
 enum { CS_F32 = 0, CS_BF16 = 1 };
 int cs_rmsnorm_bwd_partials(int rows);

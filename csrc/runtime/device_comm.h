@@ -23,6 +23,7 @@
 #include <rccl/rccl.h>
 
 #include <string>
+#include <vector>
 
 namespace cs {
 
@@ -42,6 +43,37 @@ class DeviceComm {
   virtual void abort() {}
   // collectives issued so far (tests / fault injection)
   virtual int64_t calls() const { return 0; }
+};
+
+// The fork / join machinery every communicator shares (CS_COMM_FORK selects it):
+//  2 = kernel stream links (default; stream_link.hip: a one-lane signal kernel on the
+//      producer, a bounded one-lane wait kernel on the consumer — no HIP event at all);
+//  0 = HIP events (record on the producer stream, wait on the consumer stream).
+// Measured on MI355X, VGG-11 B=64 C++ step at world 1, fork/join only (no collective
+// kernels), profiles/r2_dp_plumbing.md: no comm 0.755 ms; events 0.855 ms with ONE bucket
+// and 0.872 ms with six (any event pair on the compute stream costs ~100 us per step);
+// links 0.757 / 0.765 ms; one-rank RCCL with six bucket all-reduces 0.867 (events) vs
+// 0.786 ms (links).
+// Graph-capturable in both modes. A link's timeout shows up in error().
+class StreamBridge {
+ public:
+  explicit StreamBridge(unsigned event_flags = hipEventDisableTiming);
+  ~StreamBridge();
+  StreamBridge(const StreamBridge&) = delete;
+  StreamBridge& operator=(const StreamBridge&) = delete;
+  void fork(hipStream_t compute, hipStream_t comm);  // comm waits for compute
+  void join(hipStream_t comm, hipStream_t compute);  // compute waits for comm
+  std::string error() const;
+  int mode() const { return mode_; }
+
+ private:
+  int mode_ = 0;
+  std::vector<hipEvent_t> fork_events_;
+  size_t next_fork_ = 0;
+  hipEvent_t join_event_ = nullptr;
+  unsigned long long* dev_ = nullptr;  // [fork count, fork expect, join count, join expect]
+  int* err_ = nullptr;                 // host-mapped timeout word
+  double timeout_s_ = 10.0;
 };
 
 inline size_t comm_dtype_bytes(ncclDataType_t dt) {

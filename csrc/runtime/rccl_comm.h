@@ -3,8 +3,9 @@
 // Replaces the reference's gloo/TCP process group as the gradient data plane
 // (SURVEY.md §2.2 N17-N21, §5.8): one ncclComm_t built from a unique id that the
 // Python side shares through the c10d TCPStore, a dedicated high-priority comm
-// stream, and HIP-event fork/join between the caller's compute stream and the
-// comm stream — so every collective is stream-ordered, never blocks the host,
+// stream, and fork/join between the caller's compute stream and the comm stream
+// (StreamBridge: HIP events or kernel stream links, device_comm.h) — so every
+// collective is stream-ordered, never blocks the host,
 // overlaps with whatever the compute stream does next, and can be captured into
 // a hipGraph. Averaging uses ncclAvg (the reference divides by 4 in a separate
 // pass, master/part2b/part2b.py:44).
@@ -61,16 +62,10 @@ class RcclComm final : public DeviceComm {
   void fork(hipStream_t compute);
   ncclComm_t comm_ = nullptr;
   hipStream_t stream_ = nullptr;
-  std::vector<hipEvent_t> fork_events_;
-  hipEvent_t join_event_ = nullptr;
-  // CS_COMM_FORK=1: fork/join by stream memory operations on two signal-memory counters
-  // (hipStreamWriteValue64 / hipStreamWaitValue64) instead of event record + wait. Off: on the
-  // one-rank probe it measured 59.7k img/s vs 70.3-73.3k with events (profiles/r1_dp_plumbing_probe.md)
-  bool value_sync_ = false;
-  uint64_t* fork_ctr_ = nullptr;
-  uint64_t* join_ctr_ = nullptr;
-  uint64_t fork_seq_ = 0, join_seq_ = 0;
-  size_t next_fork_ = 0;
+  // (CS_COMM_FORK=1, stream memory operations hipStreamWriteValue64 / hipStreamWaitValue64 on
+  // signal memory, was measured and dropped: 59.7k img/s vs 70.3-73.3k with events on the
+  // one-rank probe, profiles/r1_dp_plumbing_probe.md)
+  StreamBridge bridge_;
   int rank_ = 0, world_ = 1, device_ = 0;
   int group_depth_ = 0;
   bool aborted_ = false;

@@ -13,7 +13,6 @@ namespace {
 void hip_ok(hipError_t e, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string("StagedComm/ProbeComm: ") + what + ": " + hipGetErrorString(e));
 }
-constexpr size_t kForkEvents = 64;
 
 at::ScalarType torch_dtype(ncclDataType_t dt) {
   switch (dt) {
@@ -29,18 +28,9 @@ at::ScalarType torch_dtype(ncclDataType_t dt) {
   }
 }
 
-void make_stream_and_events(int device, hipStream_t* s, std::vector<hipEvent_t>* forks, hipEvent_t* join) {
+void make_stream(int device, hipStream_t* s) {
   hip_ok(hipSetDevice(device), "hipSetDevice");
   hip_ok(hipStreamCreateWithFlags(s, hipStreamNonBlocking), "stream");
-  forks->resize(kForkEvents);
-  for (auto& e : *forks) hip_ok(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event");
-  hip_ok(hipEventCreateWithFlags(join, hipEventDisableTiming), "event");
-}
-
-void fork_on(hipStream_t compute, hipStream_t comm, std::vector<hipEvent_t>& forks, size_t& next) {
-  hipEvent_t e = forks[next++ % forks.size()];
-  hip_ok(hipEventRecord(e, compute), "hipEventRecord(fork)");
-  hip_ok(hipStreamWaitEvent(comm, e, 0), "hipStreamWaitEvent(fork)");
 }
 }  // namespace
 
@@ -51,18 +41,14 @@ StagedComm::StagedComm(const std::string& group_name, int device) : device_(devi
   TORCH_CHECK(pg_, "StagedComm: no process group named ", group_name);
   rank_ = pg_->getRank();
   world_ = pg_->getSize();
-  make_stream_and_events(device, &stream_, &fork_events_, &join_event_);
+  make_stream(device, &stream_);
 }
 
 StagedComm::~StagedComm() {
   if (stream_) hipStreamSynchronize(stream_);
-  for (auto& e : fork_events_) hipEventDestroy(e);
-  if (join_event_) hipEventDestroy(join_event_);
   if (pinned_) hipHostFree(pinned_);
   if (stream_) hipStreamDestroy(stream_);
 }
-
-void StagedComm::fork(hipStream_t compute) { fork_on(compute, stream_, fork_events_, next_fork_); }
 
 at::Tensor StagedComm::stage_in(const void* buf, size_t count, ncclDataType_t dt) {
   const size_t bytes = count * comm_dtype_bytes(dt);
@@ -88,7 +74,7 @@ void StagedComm::all_reduce(void* buf, size_t count, ncclDataType_t dt, ncclRedO
   TORCH_CHECK(!aborted_, "StagedComm: communicator aborted");
   ++calls_;
   fault_point("all_reduce", rank_);
-  if (do_fork) fork(compute);
+  if (do_fork) bridge_.fork(compute, stream_);
   at::Tensor t = stage_in(buf, count, dt);
   c10d::AllreduceOptions o;
   switch (op) {
@@ -117,7 +103,7 @@ void StagedComm::broadcast(void* buf, size_t count, ncclDataType_t dt, int root,
   TORCH_CHECK(!aborted_, "StagedComm: communicator aborted");
   ++calls_;
   fault_point("broadcast", rank_);
-  if (do_fork) fork(compute);
+  if (do_fork) bridge_.fork(compute, stream_);
   at::Tensor t = stage_in(buf, count, dt);
   c10d::BroadcastOptions o;
   o.rootRank = root;
@@ -131,10 +117,7 @@ void StagedComm::broadcast(void* buf, size_t count, ncclDataType_t dt, int root,
   if (rank_ != root) stage_out(buf, count, dt);
 }
 
-void StagedComm::join(hipStream_t compute) {
-  hip_ok(hipEventRecord(join_event_, stream_), "hipEventRecord(join)");
-  hip_ok(hipStreamWaitEvent(compute, join_event_, 0), "hipStreamWaitEvent(join)");
-}
+void StagedComm::join(hipStream_t compute) { bridge_.join(stream_, compute); }
 
 void StagedComm::abort() {
   if (aborted_) return;
@@ -145,18 +128,15 @@ void StagedComm::abort() {
 
 // ------------------------------------------------------------------------------ ProbeComm
 
-ProbeComm::ProbeComm(int device, double spin_us) : spin_us_(spin_us) {
-  make_stream_and_events(device, &stream_, &fork_events_, &join_event_);
-}
+ProbeComm::ProbeComm(int device, double spin_us) : spin_us_(spin_us) { make_stream(device, &stream_); }
 
 ProbeComm::~ProbeComm() {
   if (stream_) hipStreamSynchronize(stream_);
-  for (auto& e : fork_events_) hipEventDestroy(e);
-  if (join_event_) hipEventDestroy(join_event_);
   if (stream_) hipStreamDestroy(stream_);
 }
 
 void ProbeComm::scramble(void* buf, size_t count, ncclDataType_t dt) {
+  if (spin_us_ < 0.0) return;  // fork/join only: prices the stream plumbing alone
   int kind;
   switch (dt) {
     case ncclFloat32: kind = CS_SCRAMBLE_F32; break;
@@ -176,20 +156,17 @@ void ProbeComm::all_reduce(void* buf, size_t count, ncclDataType_t dt, ncclRedOp
                            bool do_fork) {
   ++calls_;
   fault_point("all_reduce", 0);
-  if (do_fork) fork_on(compute, stream_, fork_events_, next_fork_);
+  if (do_fork) bridge_.fork(compute, stream_);
   scramble(buf, count, dt);
 }
 
 void ProbeComm::broadcast(void* buf, size_t count, ncclDataType_t dt, int, hipStream_t compute, bool do_fork) {
   ++calls_;
   fault_point("broadcast", 0);
-  if (do_fork) fork_on(compute, stream_, fork_events_, next_fork_);
+  if (do_fork) bridge_.fork(compute, stream_);
   scramble(buf, count, dt);
 }
 
-void ProbeComm::join(hipStream_t compute) {
-  hip_ok(hipEventRecord(join_event_, stream_), "hipEventRecord(join)");
-  hip_ok(hipStreamWaitEvent(compute, join_event_, 0), "hipStreamWaitEvent(join)");
-}
+void ProbeComm::join(hipStream_t compute) { bridge_.join(stream_, compute); }
 
 }  // namespace cs

@@ -40,18 +40,15 @@ class StagedComm final : public DeviceComm {
                   bool fork = true) override;
   void broadcast(void* buf, size_t count, ncclDataType_t dt, int root, hipStream_t compute, bool fork = true) override;
   void join(hipStream_t compute) override;
-  std::string async_error() override { return error_; }
+  std::string async_error() override { return error_.empty() ? bridge_.error() : error_; }
   void abort() override;
 
  private:
-  void fork(hipStream_t compute);
   at::Tensor stage_in(const void* buf, size_t count, ncclDataType_t dt);
   void stage_out(void* buf, size_t count, ncclDataType_t dt);
   c10::intrusive_ptr<c10d::ProcessGroup> pg_;
   hipStream_t stream_ = nullptr;
-  std::vector<hipEvent_t> fork_events_;
-  size_t next_fork_ = 0;
-  hipEvent_t join_event_ = nullptr;
+  StreamBridge bridge_;
   void* pinned_ = nullptr;
   size_t pinned_bytes_ = 0;
   int rank_ = 0, world_ = 1, device_ = 0;
@@ -62,7 +59,8 @@ class StagedComm final : public DeviceComm {
 
 // World-1 ordering probe: every collective becomes, on the comm stream, an exact scramble
 // of the buffer (x2 for floats, +1 for integers), a spin of `spin_us` microseconds, and
-// the exact inverse. A correct caller (fork before, join
+// the exact inverse (spin_us < 0: no kernels at all — the fork/join plumbing alone, for
+// measurement). A correct caller (fork before, join
 // after) sees the buffer unchanged, so a probe run is bitwise equal to a no-comm run;
 // a missing fork lets the scramble race the producer, a missing join lets the consumer
 // read a scrambled or stale buffer — either shows up as a mismatch.
@@ -81,13 +79,12 @@ class ProbeComm final : public DeviceComm {
                   bool fork = true) override;
   void broadcast(void* buf, size_t count, ncclDataType_t dt, int root, hipStream_t compute, bool fork = true) override;
   void join(hipStream_t compute) override;
+  std::string async_error() override { return bridge_.error(); }
 
  private:
   void scramble(void* buf, size_t count, ncclDataType_t dt);
   hipStream_t stream_ = nullptr;
-  std::vector<hipEvent_t> fork_events_;
-  size_t next_fork_ = 0;
-  hipEvent_t join_event_ = nullptr;
+  StreamBridge bridge_;
   double spin_us_ = 0.0;
   int64_t calls_ = 0;
 };
