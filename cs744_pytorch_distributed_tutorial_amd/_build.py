@@ -40,8 +40,9 @@ def _torch_paths():
 
 
 def _sources():
-    hip = sorted(glob.glob(os.path.join(CSRC, "**", "*.hip"), recursive=True))
-    cpp = sorted(glob.glob(os.path.join(CSRC, "**", "*.cpp"), recursive=True))
+    tests = os.path.join(CSRC, "tests") + os.sep
+    hip = sorted(f for f in glob.glob(os.path.join(CSRC, "**", "*.hip"), recursive=True) if not f.startswith(tests))
+    cpp = sorted(f for f in glob.glob(os.path.join(CSRC, "**", "*.cpp"), recursive=True) if not f.startswith(tests))
     return hip, cpp
 
 
@@ -141,13 +142,82 @@ def _check_stubs(so: str) -> None:
         raise RuntimeError("undefined kernel stubs (add explicit instantiations):\n" + "\n".join(bad[:10]))
 
 
+ASAN_OUT = os.path.join(PKG_DIR, "bin", "asan_runtime_test")
+# host code only: device code is never sanitized (each -fsanitize right after -Xarch_host)
+ASAN_FLAGS = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fno-omit-frame-pointer", "-O1", "-g"]
+
+
+def build_asan(jobs: int = 0, verbose: bool = False) -> str:
+    """Standalone AddressSanitizer build of the C++ runtime (runtime/*.cpp + the kernels' host
+    launchers) and csrc/tests/asan_runtime_test.cpp. A separate object tree
+    (build/asan); the product _C.so is untouched."""
+    obj_dir = os.path.join(ROOT, "build", "asan")
+    os.makedirs(obj_dir, exist_ok=True)
+    os.makedirs(os.path.dirname(ASAN_OUT), exist_ok=True)
+    hip = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
+    cpp = sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp"))) + [os.path.join(CSRC, "tests", "asan_runtime_test.cpp")]
+    _, tinc, tlib = _torch_paths()
+    incs = [f"-I{p}" for p in tinc] + [f"-I{sysconfig.get_paths()['include']}", f"-I{ROCM}/include"]
+    todo, objs = [], []
+    for src in hip + cpp:
+        o = os.path.join(obj_dir, os.path.relpath(src, CSRC).replace(os.sep, "__") + ".o")
+        objs.append(o)
+        if not os.path.exists(o) or os.path.getmtime(o) < max(os.path.getmtime(src), _deps_mtime(o)):
+            if src.endswith(".hip"):
+                cmd = [HIPCC, f"--offload-arch={ARCH}", *_common_flags(), *ASAN_FLAGS, "-MD", "-MF", o + ".d", "-c",
+                       src, "-o", o]
+            else:
+                cmd = [HIPCC, *_common_flags(), *ASAN_FLAGS, *incs, "-D_GLIBCXX_USE_CXX11_ABI=1", "-DUSE_ROCM=1",
+                       "-MD", "-MF", o + ".d", "-x", "c++", "-c", src, "-o", o]
+            todo.append((src, cmd))
+
+    def run(item):
+        src, cmd = item
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"asan compile failed: {os.path.relpath(src, ROOT)}\n{r.stdout}\n{r.stderr}")
+        return src
+    with cf.ThreadPoolExecutor(jobs or min(8, os.cpu_count() or 4)) as ex:
+        for src in ex.map(run, todo):
+            print(f"[build:asan] compiled {os.path.relpath(src, ROOT)}", flush=True)
+    # One copy of every ROCm runtime library: torch ships them under file names without the
+    # soname's version suffix, so a standalone program's NEEDED "libamdhip64.so.7" would resolve
+    # to /opt/rocm while libtorch_hip loads torch's copy (two HIP / RCCL / SMI runtimes; ASan
+    # then reports the SMI library's static map freed twice at exit). bin/libs/<soname> ->
+    # torch's file, searched first through $ORIGIN (same torch install on the GPU box).
+    libs = os.path.join(os.path.dirname(ASAN_OUT), "libs")
+    os.makedirs(libs, exist_ok=True)
+    for f in glob.glob(os.path.join(tlib, "*.so")):
+        r = subprocess.run([os.path.join(ROCM, "lib", "llvm", "bin", "llvm-readelf"), "-d", f], capture_output=True,
+                           text=True)
+        son = [l.split("[")[-1].rstrip("]") for l in r.stdout.splitlines() if "SONAME" in l]
+        if son and son[0] != os.path.basename(f):
+            link = os.path.join(libs, son[0])
+            if os.path.lexists(link):
+                os.remove(link)
+            os.symlink(f, link)
+    cmd = [HIPCC, f"--offload-arch={ARCH}", *ASAN_FLAGS, "-o", ASAN_OUT, *objs, f"-L{tlib}", "-ltorch", "-ltorch_cpu",
+           "-ltorch_hip", "-lc10", "-lc10_hip", "-l:libamdhip64.so", "-l:librccl.so", "-Wl,--disable-new-dtags",
+           "-Wl,-rpath,$ORIGIN/libs", f"-Wl,-rpath,{tlib}", "-Wl,--no-as-needed"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"asan link failed\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    print(f"[build:asan] linked {os.path.relpath(ASAN_OUT, ROOT)}", flush=True)
+    return ASAN_OUT
+
+
 def main(argv=None) -> int:
     p = argparse.ArgumentParser()
     p.add_argument("-j", "--jobs", type=int, default=0)
     p.add_argument("--force", action="store_true")
     p.add_argument("-v", "--verbose", action="store_true")
+    p.add_argument("--asan", action="store_true", help="also build the host-ASan runtime test program")
     a = p.parse_args(argv)
     build(a.jobs, a.force, a.verbose)
+    if a.asan:
+        build_asan(a.jobs, a.verbose)
     return 0
 
 
