@@ -30,11 +30,13 @@ import os
 import sys
 import time
 
-import torch
-
 ROOT = os.path.dirname(os.path.abspath(__file__))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
+
+# the package raises GPU_MAX_HW_QUEUES before anything initialises HIP (see its __init__)
+import cs744_pytorch_distributed_tutorial_amd  # noqa: E402,F401
+import torch  # noqa: E402
 
 from cs744_pytorch_distributed_tutorial_amd import distributed as D  # noqa: E402
 
@@ -120,12 +122,6 @@ def main(argv=None) -> int:
     wd = Watchdog(args.watchdog_s, "bench step", on_timeout=getattr(trainer, "abort", None)).start() \
         if args.watchdog_s > 0 else None
 
-    import contextlib
-    step_stream = torch.cuda.Stream(device) if os.environ.get("CS_STEP_STREAM", "0") == "1" else None
-    ctx = torch.cuda.stream(step_stream) if step_stream is not None else contextlib.nullcontext()
-    if step_stream is not None:
-        step_stream.wait_stream(torch.cuda.current_stream())
-    ctx.__enter__()
     for _ in range(args.warmup):
         trainer.step()
         if wd is not None:
@@ -142,7 +138,6 @@ def main(argv=None) -> int:
     D.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    ctx.__exit__(None, None, None)
     if wd is not None:
         wd.stop()
     if hasattr(trainer, "check_comm"):
@@ -178,6 +173,7 @@ def main(argv=None) -> int:
         maths = [t["math"] for t in trainer.tile_table()]
         out["config"]["conv_gemm_math"] = {m: maths.count(m) for m in sorted(set(maths))}
         out["config"]["conv_tiles"] = getattr(trainer, "tile_source", None)
+        out["config"]["wgrad_side_stream"] = getattr(trainer, "overlap_wgrad", None)
     if args.phases > 0 and hasattr(trainer, "phase_breakdown"):
         ph = trainer.phase_breakdown(args.phases)
         if rank == 0:

@@ -11,4 +11,29 @@ Subpackages:
 """
 __version__ = "0.1.0"
 
-from . import distributed  # noqa: F401
+import os as _os
+
+
+def _raise_hw_queues(minimum: int = 8) -> int:
+    """HIP hardware queues per process (GPU_MAX_HW_QUEUES, read once at HIP init; HIP's default
+    is 4). The native engine runs the compute stream, a side stream for weight gradients, the
+    communicator's stream and RCCL's own streams, and its cross-stream waits are small kernels
+    (kernel stream links): streams that share a hardware queue serialise behind such a wait
+    (measured: VGG-11 step with side-stream weight gradients + one-rank RCCL 1.69 ms at 4 queues,
+    0.717 ms at 8). Raised before HIP initialises; returns the count in effect."""
+    cur = int(_os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4)
+    try:
+        import torch
+        if torch.cuda.is_initialized():  # too late to change it in this process
+            return cur
+    except Exception:  # pragma: no cover - torch missing
+        return cur
+    if cur < minimum:
+        _os.environ["GPU_MAX_HW_QUEUES"] = str(minimum)
+        cur = minimum
+    return cur
+
+
+HW_QUEUES = _raise_hw_queues()
+
+from . import distributed  # noqa: F401,E402

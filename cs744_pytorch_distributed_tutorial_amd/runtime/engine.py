@@ -263,6 +263,20 @@ class NativeTrainer:
         self._probe = getattr(self, "_probe", None)
         self.engine = C.VggEngine(self.B, lay.desc(), lay.offs(), lay.buf_offs(), lay.feat, lay.ncls,
                                   self.params, self.grads, self.mom, self.bufs, self.nbt)
+        # weight gradients on a side stream (off the backward's critical chain; bit-identical):
+        # on unless CS_OVERLAP_WGRAD=0, or a communicator runs with too few HIP hardware queues
+        # (their cross-stream waits would serialise behind each other, package __init__). Only
+        # for steps the engine orders itself: with collectives issued from Python through
+        # torch.distributed (comm="torch"), a gloo all-reduce of a bucket whose weight
+        # gradients came from the side stream intermittently read a stale gradient
+        # (measured: layers.25.weight wrong at step 3 of 4, world 2, whether the side stream
+        # was joined by a stream link or a HIP event; only a host sync of the side stream
+        # avoided it), so that path keeps the serial backward.
+        from .. import HW_QUEUES
+        python_collectives = world > 1 and self.native_comm is None
+        self.overlap_wgrad = os.environ.get("CS_OVERLAP_WGRAD", "1") != "0" and not python_collectives and (
+            self.native_comm is None or HW_QUEUES >= 8)
+        self.engine.set_overlap_wgrad(self.overlap_wgrad)
         self.engine.set_data(0, self.train_data, self.train_labels, self.aug_train)
         self.engine.set_data(1, self.test_data, self.test_labels, self.aug_test)
         self.idx_buf = self.engine.idx()

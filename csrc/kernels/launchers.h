@@ -158,11 +158,12 @@ hipError_t cs_comm_spin(double us, hipStream_t stream);
 hipError_t cs_comm_scramble(void* buf, int64_t n, int kind, int inverse, hipStream_t stream);
 
 // ---------------------------------------------------------------- stream links (stream_link.hip)
-// signal: count += 1 on `stream`; wait: ++*expect, then poll until count >= *expect (bounded by
-// timeout_s; on timeout *err = 1 in host-mapped memory). count / expect: device memory, zeroed.
+// signal: count += 1 on `stream`; wait: *expect += delta, then poll until count >= *expect
+// (bounded by timeout_s; on timeout *err = 1 in host-mapped memory). count / expect: device
+// memory, zeroed.
 hipError_t cs_link_signal(unsigned long long* count, hipStream_t stream);
 hipError_t cs_link_wait(const unsigned long long* count, unsigned long long* expect, int* err, double timeout_s,
-                        hipStream_t stream);
+                        hipStream_t stream, unsigned long long delta = 1);
 
 // ---------------------------------------------------------------- decoder-LM elementwise ops (lm.hip)
 enum { CS_F32 = 0, CS_BF16 = 1 };

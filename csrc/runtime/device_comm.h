@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -45,6 +46,31 @@ class DeviceComm {
   virtual int64_t calls() const { return 0; }
 };
 
+// whether `s` is being captured into a graph (links fall back to events there)
+bool stream_capturing(hipStream_t s);
+
+// One-direction kernel stream link (stream_link.hip): signal(producer) enqueues a one-lane
+// counter bump; wait(consumer) makes the consumer wait for EVERY signal issued so far (the
+// host counts them; the device keeps the expected count, so captured graphs replay
+// correctly). Bounded waits: a timeout sets error().
+class StreamLink {
+ public:
+  StreamLink();
+  ~StreamLink();
+  StreamLink(const StreamLink&) = delete;
+  StreamLink& operator=(const StreamLink&) = delete;
+  void signal(hipStream_t producer);
+  void wait(hipStream_t consumer);
+  std::string error() const;
+
+ private:
+  unsigned long long* dev_ = nullptr;  // [count, expect]
+  int* err_ = nullptr;                 // host-mapped timeout word
+  unsigned long long pending_ = 0;     // signals issued since the last wait
+  double timeout_s_ = 10.0;
+  hipEvent_t ev_ = nullptr;            // CS_LINK_EVENTS=1 (diagnostic): the same link through an event
+};
+
 // The fork / join machinery every communicator shares (CS_COMM_FORK selects it):
 //  2 = kernel stream links (default; stream_link.hip: a one-lane signal kernel on the
 //      producer, a bounded one-lane wait kernel on the consumer — no HIP event at all);
@@ -54,7 +80,8 @@ class DeviceComm {
 // and 0.872 ms with six (any event pair on the compute stream costs ~100 us per step);
 // links 0.757 / 0.765 ms; one-rank RCCL with six bucket all-reduces 0.867 (events) vs
 // 0.786 ms (links).
-// Graph-capturable in both modes. A link's timeout shows up in error().
+// Inside a graph capture the bridge always uses events (how a second stream joins a capture).
+// A link's timeout shows up in error().
 class StreamBridge {
  public:
   explicit StreamBridge(unsigned event_flags = hipEventDisableTiming);
@@ -71,9 +98,7 @@ class StreamBridge {
   std::vector<hipEvent_t> fork_events_;
   size_t next_fork_ = 0;
   hipEvent_t join_event_ = nullptr;
-  unsigned long long* dev_ = nullptr;  // [fork count, fork expect, join count, join expect]
-  int* err_ = nullptr;                 // host-mapped timeout word
-  double timeout_s_ = 10.0;
+  std::unique_ptr<StreamLink> fork_link_, join_link_;
 };
 
 inline size_t comm_dtype_bytes(ncclDataType_t dt) {

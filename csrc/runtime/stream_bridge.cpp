@@ -14,39 +14,82 @@ void hip_ok(hipError_t e, const char* what) {
 constexpr size_t kForkEvents = 64;
 }  // namespace
 
+StreamLink::StreamLink() {
+  if (const char* e = getenv("CS_COMM_LINK_TIMEOUT_S")) timeout_s_ = atof(e);
+  void* p = nullptr;
+  hip_ok(hipMalloc(&p, 2 * sizeof(unsigned long long)), "hipMalloc(link counters)");
+  hip_ok(hipMemset(p, 0, 2 * sizeof(unsigned long long)), "hipMemset(link counters)");
+  dev_ = static_cast<unsigned long long*>(p);
+  void* h = nullptr;
+  hip_ok(hipHostMalloc(&h, sizeof(int), hipHostMallocMapped), "hipHostMalloc(link error word)");
+  err_ = static_cast<int*>(h);
+  *err_ = 0;
+  if (const char* e = getenv("CS_LINK_EVENTS"))
+    if (atoi(e) != 0) hip_ok(hipEventCreateWithFlags(&ev_, hipEventDisableTiming), "event");
+  hip_ok(hipDeviceSynchronize(), "sync");
+}
+
+StreamLink::~StreamLink() {
+  if (dev_) hipFree(dev_);
+  if (err_) hipHostFree(err_);
+  if (ev_) hipEventDestroy(ev_);
+}
+
+void StreamLink::signal(hipStream_t producer) {
+  if (ev_) {
+    hip_ok(hipEventRecord(ev_, producer), "link event record");
+  } else {
+    hip_ok(cs_link_signal(dev_, producer), "link signal");
+  }
+  ++pending_;
+}
+
+void StreamLink::wait(hipStream_t consumer) {
+  if (pending_ == 0) return;  // nothing signalled since the last wait
+  if (ev_) {
+    hip_ok(hipStreamWaitEvent(consumer, ev_, 0), "link event wait");
+  } else {
+    hip_ok(cs_link_wait(dev_, dev_ + 1, err_, timeout_s_, consumer, pending_), "link wait");
+  }
+  pending_ = 0;
+}
+
+std::string StreamLink::error() const {
+  if (err_ != nullptr && __atomic_load_n(err_, __ATOMIC_ACQUIRE) != 0)
+    return "stream link wait timed out (a signal never arrived)";
+  return std::string();
+}
+
+bool stream_capturing(hipStream_t s) {
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  return hipStreamIsCapturing(s, &st) == hipSuccess && st != hipStreamCaptureStatusNone;
+}
+
 StreamBridge::StreamBridge(unsigned event_flags) {
   mode_ = 2;
   if (const char* e = getenv("CS_COMM_FORK")) mode_ = atoi(e);
   if (mode_ != 0 && mode_ != 2) throw std::runtime_error("CS_COMM_FORK: 0 (HIP events) or 2 (kernel stream links)");
-  if (const char* e = getenv("CS_COMM_LINK_TIMEOUT_S")) timeout_s_ = atof(e);
-  if (mode_ == 0) {
-    fork_events_.resize(kForkEvents);
-    for (auto& ev : fork_events_) hip_ok(hipEventCreateWithFlags(&ev, event_flags), "event");
-    hip_ok(hipEventCreateWithFlags(&join_event_, event_flags), "event");
-  } else {
-    void* p = nullptr;
-    hip_ok(hipMalloc(&p, 4 * sizeof(unsigned long long)), "hipMalloc(link counters)");
-    hip_ok(hipMemset(p, 0, 4 * sizeof(unsigned long long)), "hipMemset(link counters)");
-    dev_ = static_cast<unsigned long long*>(p);
-    void* h = nullptr;
-    hip_ok(hipHostMalloc(&h, sizeof(int), hipHostMallocMapped), "hipHostMalloc(link error word)");
-    err_ = static_cast<int*>(h);
-    *err_ = 0;
-    hip_ok(hipDeviceSynchronize(), "sync");
+  // events always exist: a fork/join inside a graph capture must be an event edge (a stream
+  // joins a capture only through an event; a link's kernels on a non-capturing stream would run
+  // at once instead of being recorded)
+  fork_events_.resize(kForkEvents);
+  for (auto& ev : fork_events_) hip_ok(hipEventCreateWithFlags(&ev, event_flags), "event");
+  hip_ok(hipEventCreateWithFlags(&join_event_, event_flags), "event");
+  if (mode_ == 2) {
+    fork_link_ = std::make_unique<StreamLink>();
+    join_link_ = std::make_unique<StreamLink>();
   }
 }
 
 StreamBridge::~StreamBridge() {
   for (auto& ev : fork_events_) hipEventDestroy(ev);
   if (join_event_) hipEventDestroy(join_event_);
-  if (dev_) hipFree(dev_);
-  if (err_) hipHostFree(err_);
 }
 
 void StreamBridge::fork(hipStream_t compute, hipStream_t comm) {
-  if (mode_ == 2) {
-    hip_ok(cs_link_signal(dev_ + 0, compute), "link signal (fork)");
-    hip_ok(cs_link_wait(dev_ + 0, dev_ + 1, err_, timeout_s_, comm), "link wait (fork)");
+  if (mode_ == 2 && !stream_capturing(compute)) {
+    fork_link_->signal(compute);
+    fork_link_->wait(comm);
     return;
   }
   hipEvent_t e = fork_events_[next_fork_++ % fork_events_.size()];
@@ -55,9 +98,9 @@ void StreamBridge::fork(hipStream_t compute, hipStream_t comm) {
 }
 
 void StreamBridge::join(hipStream_t comm, hipStream_t compute) {
-  if (mode_ == 2) {
-    hip_ok(cs_link_signal(dev_ + 2, comm), "link signal (join)");
-    hip_ok(cs_link_wait(dev_ + 2, dev_ + 3, err_, timeout_s_, compute), "link wait (join)");
+  if (mode_ == 2 && !stream_capturing(compute)) {
+    join_link_->signal(comm);
+    join_link_->wait(compute);
     return;
   }
   hip_ok(hipEventRecord(join_event_, comm), "hipEventRecord(join)");
@@ -65,8 +108,11 @@ void StreamBridge::join(hipStream_t comm, hipStream_t compute) {
 }
 
 std::string StreamBridge::error() const {
-  if (err_ != nullptr && __atomic_load_n(err_, __ATOMIC_ACQUIRE) != 0)
-    return "stream link wait timed out (a fork/join signal never arrived)";
+  if (fork_link_) {
+    std::string e = fork_link_->error();
+    if (e.empty()) e = join_link_->error();
+    return e;
+  }
   return std::string();
 }
 

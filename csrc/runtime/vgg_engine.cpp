@@ -157,17 +157,19 @@ VggEngine::VggEngine(int64_t Bmax, std::vector<int64_t> desc, std::vector<int64_
   ws_elems_ = kWsElems;
   ws_ = torch::zeros({ws_elems_}, fo);
   ws_side_ = torch::zeros({ws_elems_}, fo);
-  ok(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking), "side stream");
+  {
+    int least = 0, greatest = 0;
+    ok(hipDeviceGetStreamPriorityRange(&least, &greatest), "stream priorities");
+    ok(hipStreamCreateWithPriority(&side_, hipStreamNonBlocking, least), "side stream");
+  }
+  dz_link_ = std::make_unique<StreamLink>();
+  wg_link_ = std::make_unique<StreamLink>();
   ok(hipStreamCreateWithFlags(&opt_, hipStreamNonBlocking), "optimizer stream");
   ev_opt_.resize(64);
   for (auto& e : ev_opt_) ok(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event");
   if (const char* e = getenv("CS_SGD_OVERLAP")) sgd_overlap_ = atoi(e) != 0;
-  ev_bn_.resize(L);
-  ev_wg_.resize(L);
-  for (int64_t l = 0; l < L; ++l) {
-    ok(hipEventCreateWithFlags(&ev_bn_[l], hipEventDisableTiming), "event");
-    ok(hipEventCreateWithFlags(&ev_wg_[l], hipEventDisableTiming), "event");
-  }
+  if (const char* e = getenv("CS_OVERLAP_WGRAD")) set_overlap_wgrad(atoi(e) != 0);
+  if (const char* e = getenv("CS_WGRAD_AFTER_DGRAD")) wgrad_after_dgrad_ = atoi(e) != 0;
   // split-K tile tickets for the in-launch combine: one zeroed region per (block, mode) call site
   tiles_max_ = 1;
   for (int64_t l = 0; l < L; ++l)
@@ -188,6 +190,18 @@ VggEngine::VggEngine(int64_t Bmax, std::vector<int64_t> desc, std::vector<int64_
   bn_eval_ = torch::zeros({2, cmax}, fo);
   TORCH_CHECK(feat % 4 == 0, "VggEngine: feature size must be a multiple of 4");
   head_ws_ = torch::zeros({cs_linear_xent_ws((int)Bmax, (int)ncls)}, fo);
+}
+
+bool VggEngine::side_wgrad(hipStream_t s) const { return overlap_wgrad_ && !stream_capturing(s); }
+
+void VggEngine::join_side(hipStream_t s) { wg_link_->wait(s); }
+
+void VggEngine::set_overlap_wgrad(bool on) {
+  overlap_wgrad_ = on;
+  if (on && dz_blk_.empty()) {
+    const auto fo = params_.options();
+    for (const VggBlock& b : blocks_) dz_blk_.push_back(torch::zeros({Bmax_ * b.H * b.H * b.cout}, fo));
+  }
 }
 
 torch::Tensor VggEngine::tensor(int64_t block, const std::string& name) const {
@@ -358,13 +372,15 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
   TORCH_CHECK(0 <= lo && lo <= hi && hi < L, "backward: need 0 <= lo <= hi < num_blocks");
   TORCH_CHECK(B > 0 && B <= Bmax_, "backward: 0 < B <= Bmax");
   hipStream_t s = cur_stream();
+  // side-stream weight gradients, except while a graph is captured (the side stream would not
+  // join the capture; the serial order computes the same bits)
+  const bool ovl = side_wgrad(s);
   for (int l = (int)hi; l >= (int)lo; --l) {
     VggBlock& b = blocks_[l];
     float* bn = b.bn.data_ptr<float>();
-    float* dz = dz_[l & 1].data_ptr<float>();
-    // WAR: block l+2's weight-gradient GEMM (side stream) reads the same dz buffer; it may
-    // belong to an earlier backward() call of this step that did not join (bucketed step)
-    if (overlap_wgrad_ && l + 2 < L) ok(hipStreamWaitEvent(s, ev_wg_[l + 2], 0), "wait wgrad");
+    // with the side-stream weight gradients every block has its own dz buffer (no WAR wait
+    // on a wgrad that may still be reading it)
+    float* dz = ovl ? dz_blk_[l].data_ptr<float>() : dz_[l & 1].data_ptr<float>();
     // this block's output gradient: gbuf_, or the split-K slabs the dgrad above left in ws_
     const int gs = g_slabs_;
     const float* Gin = gs > 1 ? ws_.data_ptr<float>() : gbuf_[(L - 1 - l) % 2].data_ptr<float>();
@@ -390,11 +406,11 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
     }
     g_slabs_ = 1;
     red_pending_ = -1;
-    if (!overlap_wgrad_ && dual_ok(l)) {  // wgrad + dgrad in one launch
+    if (!ovl && dual_ok(l)) {  // wgrad + dgrad in one launch
       conv_dual(l, (int)B, s, dz);
       continue;
     }
-    if (fuse_red_ && !overlap_wgrad_ && bn_path_ == 0 && l > 0 && !bn_fused(l - 1, B)) {
+    if (fuse_red_ && !ovl && bn_path_ == 0 && l > 0 && !bn_fused(l - 1, B)) {
       // dgrad(l) first, then wgrad(l) carrying block l-1's BN partial-sum pass
       const ConvTile& t = b.tile[CS_CONV_DGRAD];
       const Dims d = dims(b, CS_CONV_DGRAD, B);
@@ -427,12 +443,14 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
       red_P_ = r.P;
       continue;
     }
-    if (overlap_wgrad_) {
-      ok(hipEventRecord(ev_bn_[l], s), "record bn");
-      ok(hipStreamWaitEvent(side_, ev_bn_[l], 0), "side wait");
+    if (ovl && !wgrad_after_dgrad_) {
+      // the weight gradient leaves the critical chain: it runs on the (low-priority) side
+      // stream once dz(l) exists, beside this block's dgrad and the BN backward below
+      dz_link_->signal(s);
+      dz_link_->wait(side_);
       conv(l, CS_CONV_WGRAD, (int)B, b.tile[CS_CONV_WGRAD], side_, false, ws_side_.data_ptr<float>(), dz);
-      ok(hipEventRecord(ev_wg_[l], side_), "record wgrad");
-    } else {
+      wg_link_->signal(side_);
+    } else if (!ovl) {
       conv(l, CS_CONV_WGRAD, (int)B, b.tile[CS_CONV_WGRAD], s, false, ws_side_.data_ptr<float>(), dz);
     }
     if (l > 0) {
@@ -446,8 +464,17 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
         g_stride_ = d.M * d.N;
       }
     }
+    if (ovl && wgrad_after_dgrad_) {
+      // (default) fork the weight gradient only after this block's data gradient: the
+      // critical dgrad keeps the whole chip, and the wgrad fills it while the main stream
+      // runs the latency-bound split-K combine / BN backward kernels of the block below
+      dz_link_->signal(s);
+      dz_link_->wait(side_);
+      conv(l, CS_CONV_WGRAD, (int)B, b.tile[CS_CONV_WGRAD], side_, false, ws_side_.data_ptr<float>(), dz);
+      wg_link_->signal(side_);
+    }
   }
-  if (join && overlap_wgrad_) ok(hipStreamWaitEvent(s, ev_wg_[lo], 0), "join side");
+  if (join && ovl) join_side(s);
 }
 
 VggEngine::~VggEngine() {
@@ -461,8 +488,6 @@ VggEngine::~VggEngine() {
   }
   for (auto e : ev_opt_) hipEventDestroy(e);
   for (auto e : tev_) hipEventDestroy(e);
-  for (auto e : ev_bn_) hipEventDestroy(e);
-  for (auto e : ev_wg_) hipEventDestroy(e);
 }
 
 void VggEngine::sgd(double lr, double momentum, double wd, double dampening, int64_t off, int64_t n) {
@@ -521,7 +546,7 @@ void VggEngine::sgd_bucket(DeviceComm* comm, int64_t lo_block, int64_t off, int6
   hipEvent_t e = opt_event();
   ok(hipEventRecord(e, s), "record main");
   ok(hipStreamWaitEvent(opt_, e, 0), "opt wait main");
-  if (overlap_wgrad_) ok(hipStreamWaitEvent(opt_, ev_wg_[lo_block], 0), "opt wait wgrad");
+  TORCH_CHECK(!overlap_wgrad_, "sgd_bucket: per-bucket SGD and side-stream weight gradients are exclusive");
   if (comm != nullptr) {
     hipEvent_t c = opt_event();
     ok(hipEventRecord(c, comm->stream()), "record comm");
@@ -578,12 +603,13 @@ void VggEngine::step(int64_t B, DeviceComm* comm, const std::vector<int64_t>& bu
   // the caller passes a communicator only when the step is data-parallel (a one-rank
   // communicator too: the CS_COMM_PROBE measurement and the ProbeComm ordering test)
   const bool dp = comm != nullptr;
+  const bool ovl = side_wgrad(s);
   tn_ = 0;
   mark("start");
   forward_train(B);
   mark("forward");
   // per-bucket SGD needs the buckets to tile the flat buffer exactly
-  bool tiled = sgd_overlap_;
+  bool tiled = sgd_overlap_ && !ovl;
   for (size_t k = 0, at = 0; k < nb && tiled; ++k) {
     tiled = bucket_ranges[2 * k] == (int64_t)at;
     at += bucket_ranges[2 * k + 1];
@@ -602,7 +628,7 @@ void VggEngine::step(int64_t B, DeviceComm* comm, const std::vector<int64_t>& bu
     // all-reduce from there, so it overlaps the rest of the backward on the main stream
     if (dp)
       comm->all_reduce(G(bucket_ranges[2 * k]), bucket_ranges[2 * k + 1], ncclFloat32, ncclAvg,
-                       overlap_wgrad_ ? side_ : s, /*fork=*/!(debug_skip_ & 2));
+                       ovl ? side_ : s, /*fork=*/!(debug_skip_ & 2));
     if (dp && broadcast_buffers && k == 0) {
       // DDP broadcast_buffers (rank 0's BN running stats before every training forward), issued
       // for the NEXT forward right behind the first bucket: this forward has produced the
@@ -618,7 +644,7 @@ void VggEngine::step(int64_t B, DeviceComm* comm, const std::vector<int64_t>& bu
     if (tiled)
       sgd_bucket(comm, lo, bucket_ranges[2 * k], bucket_ranges[2 * k + 1], lr, momentum, wd, dampening, k + 1 == nb);
   }
-  if (overlap_wgrad_) ok(hipStreamWaitEvent(s, ev_wg_[0], 0), "join side");
+  if (ovl) join_side(s);
   if (dp && !(debug_skip_ & 1)) comm->join(s);
   mark("allreduce_wait");
   if (tiled) join_opt();

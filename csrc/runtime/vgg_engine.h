@@ -78,7 +78,9 @@ class VggEngine {
   // running them together only shares CUs, and each cross-stream event wait inside the
   // graph cost a 10-20 us bubble (1.16 -> 1.26 ms/step).
   void backward(int64_t hi, int64_t lo, int64_t B, bool join = true);
-  void set_overlap_wgrad(bool on) { overlap_wgrad_ = on; }
+  void set_overlap_wgrad(bool on);
+  bool side_wgrad(hipStream_t s) const;  // overlap on and `s` not capturing a graph
+  void join_side(hipStream_t s);          // `s` waits for every side-stream weight gradient so far
   void set_fixup(bool on) { fixup_ = on; }
   void set_dual(bool on) { dual_ = on; }
   void set_bn_fused_rows(int64_t r) { bn_fused_rows_ = r; }
@@ -204,7 +206,12 @@ class VggEngine {
   std::vector<std::string> tnames_;      // phase ending at tev_[i + 1]
   size_t tn_ = 0;                        // events recorded in the last step
   void mark(const char* phase);           // record the next timing event (timing_ only)
-  std::vector<hipEvent_t> ev_bn_, ev_wg_;  // per block: BN-backward done (main), wgrad done (side)
+  // side-stream weight gradients (CS_OVERLAP_WGRAD=1): kernel stream links (device_comm.h),
+  // main -> side "dz(l) ready" and side -> main "weight gradients done", and one dz buffer
+  // per block
+  std::unique_ptr<StreamLink> dz_link_, wg_link_;
+  bool wgrad_after_dgrad_ = true;  // fork point of the side wgrad (CS_WGRAD_AFTER_DGRAD=0: before dgrad)
+  std::vector<torch::Tensor> dz_blk_;
 
  public:
   ~VggEngine();

@@ -435,3 +435,36 @@ def test_ragged_batches_match_fp64(dev, B, Bmax):
     print(f"[parity] ragged B={B} (Bmax {Bmax}): {tight}/{checked} tensors within 1e-4 rel, global rel L2 {rel:.3e}")
     assert tight == checked and worst < 1e-4, (tight, checked, worst)
     assert rel < 1e-5, rel
+
+
+def test_wgrad_side_stream_bitwise_and_graph(dev):
+    """Weight gradients on the side stream (kernel stream links, the default) compute exactly
+    what the serial backward does; a full-step graph of the two-stream step replays it exactly."""
+    runs = []
+    for ovl, graph in ((False, "none"), (True, "none"), (True, "full")):
+        t = _trainer(dev, batch_size=32, train_size=256, graph=graph)
+        t.engine.set_overlap_wgrad(ovl)
+        for _ in range(5):
+            t.step()
+        torch.cuda.synchronize()
+        runs.append((t.params.clone(), t.mom.clone(), t.bufs.clone()))
+        t.close()
+    for r in runs[1:]:
+        for a, b in zip(runs[0], r):
+            assert torch.equal(a, b)
+
+
+def test_wgrad_side_stream_long_run_no_syncs(dev):
+    """30 back-to-back steps (the host far ahead of the GPU, epoch boundary crossed) with the
+    side-stream weight gradients == the serial backward, bit for bit."""
+    out = []
+    for ovl in (False, True):
+        t = _trainer(dev, batch_size=32, train_size=640)
+        t.engine.set_overlap_wgrad(ovl)
+        for _ in range(30):
+            t.step()
+        torch.cuda.synchronize()
+        out.append((t.params.clone(), t.mom.clone(), t.bufs.clone()))
+        t.close()
+    for a, b in zip(*out):
+        assert torch.equal(a, b)
