@@ -178,6 +178,23 @@ VggEngine::VggEngine(int64_t Bmax, std::vector<int64_t> desc, std::vector<int64_
       tiles_max_ = std::max(tiles_max_, cdiv(d.M, 64) * cdiv(d.N, 64));
     }
   counters_ = torch::zeros({3 * L * tiles_max_}, fo.dtype(at::kInt));
+  // per-block parameter ranges for the side-stream SGD: the backward-ready layout puts fc first,
+  // then blocks L-1..0, each {w, bias, gamma, beta} inside [w_off, next block's w_off)
+  {
+    bool contiguous = fc_w_ + ncls * feat <= blocks_[L - 1].w_off && fc_b_ + ncls <= blocks_[L - 1].w_off;
+    for (int64_t l = 0; l < L && contiguous; ++l) {
+      const VggBlock& b = blocks_[l];
+      const int64_t lo = l == L - 1 ? 0 : b.w_off;
+      const int64_t hi = l == 0 ? P : blocks_[l - 1].w_off;
+      const int64_t wn = (l == 0 && b.cin == 4) ? b.cout * 27 : b.cout * 9 * b.cin;
+      contiguous = l == 0 || blocks_[l - 1].w_off > b.w_off;  // blocks laid out last -> first
+      for (int64_t o : {b.b_off, b.g_off, b.be_off}) contiguous = contiguous && o >= b.w_off && o + b.cout <= hi;
+      contiguous = contiguous && b.w_off + wn <= hi;
+      blk_range_.emplace_back(lo, hi - lo);
+    }
+    if (!contiguous) blk_range_.clear();
+  }
+  if (const char* e = getenv("CS_SGD_SIDE")) sgd_side_ = atoi(e) != 0;
   if (const char* e = getenv("CS_CONV_FIXUP")) fixup_ = atoi(e) != 0;
   if (const char* e = getenv("CS_CONV_DUAL")) dual_ = atoi(e) != 0;
   if (const char* e = getenv("CS_BN_FUSED_ROWS")) bn_fused_rows_ = atoll(e);
@@ -464,13 +481,21 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
         g_stride_ = d.M * d.N;
       }
     }
-    if (ovl && wgrad_after_dgrad_) {
+    if (ovl && wgrad_after_dgrad_ && l == 0) {
+      // block 0's weight gradient is the step's last GEMM: nothing is left to overlap it with,
+      // so it runs on this stream (main's split-K workspace is free once the BN backward above
+      // has read the dgrad result) without a fork/join round trip
+      conv(l, CS_CONV_WGRAD, (int)B, b.tile[CS_CONV_WGRAD], s, false, ws_.data_ptr<float>(), dz);
+      if (bwd_sgd_) sgd_on(s, blk_range_[0].first, blk_range_[0].second, true);
+    } else if (ovl && wgrad_after_dgrad_) {
       // (default) fork the weight gradient only after this block's data gradient: the
       // critical dgrad keeps the whole chip, and the wgrad fills it while the main stream
       // runs the latency-bound split-K combine / BN backward kernels of the block below
       dz_link_->signal(s);
       dz_link_->wait(side_);
       conv(l, CS_CONV_WGRAD, (int)B, b.tile[CS_CONV_WGRAD], side_, false, ws_side_.data_ptr<float>(), dz);
+      // block l's dgrad (the last reader of its weights) and BN backward ran before the fork
+      if (bwd_sgd_) sgd_on(side_, blk_range_[l].first, blk_range_[l].second, false);
       wg_link_->signal(side_);
     }
   }
@@ -488,6 +513,14 @@ VggEngine::~VggEngine() {
   }
   for (auto e : ev_opt_) hipEventDestroy(e);
   for (auto e : tev_) hipEventDestroy(e);
+}
+
+void VggEngine::sgd_on(hipStream_t st, int64_t off, int64_t n, bool cursor) {
+  if (n == 0) return;
+  ok(cs_sgd_flat(P(off), G(off), mom_.data_ptr<float>() + off, n, (float)hp_[0], (float)hp_[1], (float)hp_[2],
+                 (float)hp_[3], 1.0f, sgd_first_ ? 1 : 0, st,
+                 cursor && perm_len_ > 0 ? cursor_.data_ptr<int64_t>() : nullptr),
+     "sgd_flat(side)");
 }
 
 void VggEngine::sgd(double lr, double momentum, double wd, double dampening, int64_t off, int64_t n) {
@@ -615,6 +648,19 @@ void VggEngine::step(int64_t B, DeviceComm* comm, const std::vector<int64_t>& bu
     at += bucket_ranges[2 * k + 1];
     if (k + 1 == nb) tiled = tiled && (int64_t)at == params_.numel();
   }
+  // SGD behind the weight gradients (sgd_side_): per block on the side stream (world 1), or per
+  // bucket on the comm stream behind its all-reduce; the buckets must tile the flat buffer
+  bool side_sgd = ovl && sgd_side_ && wgrad_after_dgrad_ && !blk_range_.empty();
+  for (size_t k = 0, at = 0; k < nb && side_sgd; ++k) {
+    side_sgd = bucket_ranges[2 * k] == (int64_t)at;
+    at += bucket_ranges[2 * k + 1];
+    if (k + 1 == nb) side_sgd = side_sgd && (int64_t)at == params_.numel();
+  }
+  hp_[0] = lr;
+  hp_[1] = momentum;
+  hp_[2] = wd;
+  hp_[3] = dampening;
+  bwd_sgd_ = side_sgd && !dp;
   int64_t hi = L - 1;
   for (size_t k = 0; k < nb; ++k) {
     const int64_t lo = bucket_blocks[k];
@@ -625,10 +671,17 @@ void VggEngine::step(int64_t B, DeviceComm* comm, const std::vector<int64_t>& bu
     mark(k < 8 ? kBwd[k] : "backward_bucket8+");
     hi = lo - 1;
     // a bucket is complete once its last weight-gradient GEMM (side stream) is: fork the
-    // all-reduce from there, so it overlaps the rest of the backward on the main stream
+    // all-reduce from there, so it overlaps the rest of the backward on the main stream. The
+    // last bucket also holds block 0, whose weight gradient ran on the main stream: join the
+    // side stream into main and fork from main
+    hipStream_t src = ovl ? side_ : s;
+    if (ovl && lo == 0 && wgrad_after_dgrad_) {
+      join_side(s);
+      src = s;
+    }
     if (dp)
-      comm->all_reduce(G(bucket_ranges[2 * k]), bucket_ranges[2 * k + 1], ncclFloat32, ncclAvg,
-                       ovl ? side_ : s, /*fork=*/!(debug_skip_ & 2));
+      comm->all_reduce(G(bucket_ranges[2 * k]), bucket_ranges[2 * k + 1], ncclFloat32, ncclAvg, src,
+                       /*fork=*/!(debug_skip_ & 2));
     if (dp && broadcast_buffers && k == 0) {
       // DDP broadcast_buffers (rank 0's BN running stats before every training forward), issued
       // for the NEXT forward right behind the first bucket: this forward has produced the
@@ -643,12 +696,17 @@ void VggEngine::step(int64_t B, DeviceComm* comm, const std::vector<int64_t>& bu
     // gradient (the last reader of these weights) is done, beside the backward below
     if (tiled)
       sgd_bucket(comm, lo, bucket_ranges[2 * k], bucket_ranges[2 * k + 1], lr, momentum, wd, dampening, k + 1 == nb);
+    // the comm stream runs this bucket's SGD right behind its all-reduce (every reader of the
+    // bucket's weights — its blocks' data gradients — was enqueued before the fork)
+    if (side_sgd && dp) sgd_on(comm->stream(), bucket_ranges[2 * k], bucket_ranges[2 * k + 1], k + 1 == nb);
   }
+  bwd_sgd_ = false;
   if (ovl) join_side(s);
   if (dp && !(debug_skip_ & 1)) comm->join(s);
   mark("allreduce_wait");
   if (tiled) join_opt();
-  else sgd(lr, momentum, wd, dampening, 0, params_.numel());
+  else if (!side_sgd) sgd(lr, momentum, wd, dampening, 0, params_.numel());
+  if (side_sgd) sgd_first_ = false;
   mark("sgd");
 }
 

@@ -71,12 +71,10 @@ class VggEngine {
   // augment + conv/BN/ReLU/pool chain + fused linear/xent fwd+bwd (train) for B <= Bmax samples
   void forward_train(int64_t B);
   // backward of blocks hi..lo (inclusive, hi >= lo), writing their gradients into `grads`.
-  // With overlap_wgrad the weight-gradient GEMM of a block runs on a side stream
-  // concurrently with its data-gradient GEMM (they only share read-only inputs); join =
-  // true makes the caller's stream wait for the side stream before returning. Off by
-  // default: measured on MI355X at B=64 both split-K GEMMs already fill the 256 CUs, so
-  // running them together only shares CUs, and each cross-stream event wait inside the
-  // graph cost a 10-20 us bubble (1.16 -> 1.26 ms/step).
+  // With overlap_wgrad the weight-gradient GEMM of block l > 0 runs on a low-priority side
+  // stream once block l's data gradient is enqueued, beside the rest of the backward; block
+  // 0's (the last GEMM of the step, nothing left to overlap) stays on the caller's stream.
+  // join = true makes the caller's stream wait for the side stream before returning.
   void backward(int64_t hi, int64_t lo, int64_t B, bool join = true);
   void set_overlap_wgrad(bool on);
   bool side_wgrad(hipStream_t s) const;  // overlap on and `s` not capturing a graph
@@ -97,6 +95,7 @@ class VggEngine {
                   double dampening, bool advance_cursor);
   void join_opt();
   void set_sgd_overlap(bool on) { sgd_overlap_ = on; }
+  void set_sgd_side(bool on) { sgd_side_ = on; }
   // torch.optim.SGD's first step sets buf = d (no dampening): the next step's SGD launches
   // use first = 1 (only matters with dampening != 0); cleared once that step's SGD is enqueued
   void set_sgd_first(bool on) { sgd_first_ = on; }
@@ -212,6 +211,17 @@ class VggEngine {
   std::unique_ptr<StreamLink> dz_link_, wg_link_;
   bool wgrad_after_dgrad_ = true;  // fork point of the side wgrad (CS_WGRAD_AFTER_DGRAD=0: before dgrad)
   std::vector<torch::Tensor> dz_blk_;
+  // SGD behind the weight gradients (CS_SGD_SIDE=0 disables; needs overlap_wgrad, the
+  // dgrad-first fork and a block-contiguous flat layout): at world 1 each block's parameters
+  // are updated on the side stream right after its weight gradient (block 0's on the main
+  // stream), with a communicator each bucket's SGD runs on the comm stream right behind its
+  // all-reduce — the 28 us optimizer pass leaves the end of the step. Bit-identical: every
+  // element gets the same update, only its launch differs.
+  bool sgd_side_ = true;
+  bool bwd_sgd_ = false;  // set by step(): backward() issues the per-block SGD
+  double hp_[4] = {0, 0, 0, 0};  // lr, momentum, wd, dampening of the step in flight
+  std::vector<std::pair<int64_t, int64_t>> blk_range_;  // block l's [off, off + n) (block L-1 from 0: fc)
+  void sgd_on(hipStream_t st, int64_t off, int64_t n, bool cursor);
 
  public:
   ~VggEngine();
