@@ -28,7 +28,9 @@ mode                reference                                                  p
 
 Ranges are visited in the reference's ``model.parameters()`` order. Runs on
 CPU tensors over gloo too, which is how the multi-rank logic is unit-tested
-without GPUs.
+without GPUs. On GPU buffers the root's combines are gfx950 kernels
+(``csrc/kernels/flat_ops.hip``: rank-ordered mean of the gathered rows, add-then-divide of
+the star), not ATen elementwise ops.
 """
 from __future__ import annotations
 
@@ -39,6 +41,11 @@ import torch
 from .comm import Comm
 
 FLAT_MODES = ("gather_scatter", "p2p", "allreduce", "flat", "ddp", "none")
+
+
+def _native():
+    from ..ops.native import C  # the compiled extension; raises if it is missing
+    return C()
 
 
 class FlatGradSync:
@@ -78,7 +85,10 @@ class FlatGradSync:
             out = self._tmp(w * maxn, g)[:w * n] if r == self.root else None
             self.comm.gather_flat(g, out, self.root)
             if r == self.root:
-                torch.mean(out.view(w, n), 0, out=g)
+                if g.is_cuda:
+                    _native().rows_mean(out, w, g)
+                else:
+                    torch.mean(out.view(w, n), 0, out=g)
             self.comm.broadcast(g, self.root)
 
     def _p2p(self, flat_grad: torch.Tensor) -> None:
@@ -87,12 +97,16 @@ class FlatGradSync:
             g = flat_grad[off:off + n]
             if r == self.root:
                 tmp = self._tmp(n, g)
-                for src in range(w):
-                    if src == self.root:
-                        continue
+                peers = [src for src in range(w) if src != self.root]
+                for i, src in enumerate(peers):
                     self.comm.recv(tmp, src)
-                    g.add_(tmp)
-                g.div_(w)
+                    last = i == len(peers) - 1
+                    if g.is_cuda:
+                        _native().accumulate(g, tmp, float(w) if last else 0.0)
+                    else:
+                        g.add_(tmp)
+                        if last:
+                            g.div_(w)
                 for dst in range(w):
                     if dst != self.root:
                         self.comm.send(g, dst)

@@ -85,6 +85,22 @@ void sgd_multi(torch::Tensor table, int64_t ntens, int64_t nchunks, double lr, d
                          (float)lr, (float)mom, (float)wd, (float)damp, (float)scale, first ? 1 : 0, cur_stream()));
 }
 
+// part2a root combine: dst[n] = mean over rows of src[rows * n] (rank order)
+void rows_mean(torch::Tensor src, int64_t rows, torch::Tensor dst) {
+  for (auto* t : {&src, &dst}) { CS_CHECK_CUDA(*t); CS_CHECK_F32(*t); CS_CHECK_CONTIG(*t); }
+  TORCH_CHECK(rows >= 1 && src.numel() == rows * dst.numel(), "rows_mean: src must hold rows * dst.numel()");
+  DevGuard gd(dst.device());
+  CS_LAUNCH(cs_rows_mean(src.data_ptr<float>(), (int)rows, dst.numel(), dst.data_ptr<float>(), cur_stream()));
+}
+
+// part2a_extra root combine: g += t (then g /= div when div > 0)
+void accumulate(torch::Tensor g, torch::Tensor t, double div) {
+  for (auto* x : {&g, &t}) { CS_CHECK_CUDA(*x); CS_CHECK_F32(*x); CS_CHECK_CONTIG(*x); }
+  TORCH_CHECK(g.numel() == t.numel(), "accumulate: size mismatch");
+  DevGuard gd(g.device());
+  CS_LAUNCH(cs_accumulate(g.data_ptr<float>(), t.data_ptr<float>(), g.numel(), (float)div, cur_stream()));
+}
+
 std::vector<torch::Tensor> linear_xent(torch::Tensor feat, torch::Tensor W, torch::Tensor bias, torch::Tensor labels,
                                        double gscale, bool backward) {
   for (auto* t : {&feat, &W, &bias}) { CS_CHECK_CUDA(*t); CS_CHECK_F32(*t); CS_CHECK_CONTIG(*t); }
@@ -143,6 +159,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("sgd_flat", &sgd_flat, "fused SGD on flat buffers");
   m.def("sgd_multi_table", &sgd_multi_table, "build the multi-tensor SGD table");
   m.def("sgd_multi", &sgd_multi, "multi-tensor fused SGD");
+  m.def("rows_mean", &rows_mean, "mean over the rows of a [rows, n] buffer (part2a root)");
+  m.def("accumulate", &accumulate, "g += t, optionally then g /= div (part2a_extra root)");
   m.def("linear_xent", &linear_xent, "fused Linear + softmax cross-entropy fwd(+bwd)");
   m.def("softmax_xent", &softmax_xent, "softmax cross-entropy fwd+bwd");
   register_conv_ops(m);

@@ -1,0 +1,71 @@
+// Elementwise combines for the tutorial's faithful gradient-sync modes on the native
+// engine's flat gradient buffer (parallel/flat_sync.py), replacing ATen's mean / add_ / div_
+// on that path:
+//  * rows_mean — part2a's gather -> mean on the root (`master/part2a/part2a.py:42-52`):
+//    dst[i] = (sum_r src[r][i]) / rows, rows summed in rank order 0..rows-1 (fixed order: the
+//    root's result does not depend on the launch shape);
+//  * accumulate — part2a_extra's star on the root (`master/part2a/part2a_extra.py:41-58`):
+//    g += t for each received peer buffer, and on the last one g = (g + t) / div (the same two
+//    roundings as the reference's add then divide).
+// Both are HBM-streaming: float4 grid-stride loops, a few waves per CU, scalar tail.
+#include "common.h"
+#include "launchers.h"
+
+namespace {
+
+__global__ __launch_bounds__(256) void rows_mean_kernel(const float* __restrict__ src, int rows, int64_t n,
+                                                        float* __restrict__ dst) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const float fr = (float)rows;
+  const int64_t n4 = n >> 2;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 s = reinterpret_cast<const float4*>(src)[i];
+    for (int r = 1; r < rows; ++r) {
+      const float4 v = reinterpret_cast<const float4*>(src + (int64_t)r * n)[i];
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    reinterpret_cast<float4*>(dst)[i] = make_float4(s.x / fr, s.y / fr, s.z / fr, s.w / fr);
+  }
+  for (int64_t i = (n4 << 2) + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    float s = src[i];
+    for (int r = 1; r < rows; ++r) s += src[(int64_t)r * n + i];
+    dst[i] = s / fr;
+  }
+}
+
+__global__ __launch_bounds__(256) void accumulate_kernel(float* __restrict__ g, const float* __restrict__ t,
+                                                         int64_t n, float div) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t n4 = n >> 2;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 a = reinterpret_cast<float4*>(g)[i];
+    const float4 b = reinterpret_cast<const float4*>(t)[i];
+    a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    if (div > 0.f) { a.x /= div; a.y /= div; a.z /= div; a.w /= div; }
+    reinterpret_cast<float4*>(g)[i] = a;
+  }
+  for (int64_t i = (n4 << 2) + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    float a = g[i] + t[i];
+    if (div > 0.f) a /= div;
+    g[i] = a;
+  }
+}
+
+int grid_for(int64_t n) {
+  const int64_t b = ((n + 3) / 4 + 255) / 256;
+  return (int)(b < 1 ? 1 : (b > 2048 ? 2048 : b));
+}
+
+}  // namespace
+
+hipError_t cs_rows_mean(const float* src, int rows, int64_t n, float* dst, hipStream_t stream) {
+  if (n <= 0 || rows <= 0) return hipSuccess;
+  hipLaunchKernelGGL(rows_mean_kernel, dim3(grid_for(n)), dim3(256), 0, stream, src, rows, n, dst);
+  return hipGetLastError();
+}
+
+hipError_t cs_accumulate(float* g, const float* t, int64_t n, float div, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(accumulate_kernel, dim3(grid_for(n)), dim3(256), 0, stream, g, t, n, div);
+  return hipGetLastError();
+}

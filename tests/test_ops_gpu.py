@@ -107,3 +107,23 @@ def test_softmax_xent_matches_torch(dev):
     l, dl, c = native.softmax_xent(lg.detach(), y)
     torch.testing.assert_close(l, loss.detach(), rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(dl, lg.grad, rtol=1e-5, atol=1e-7)
+
+
+def test_flat_sync_root_combines_match_torch(dev):
+    """part2a / part2a_extra root combines on the flat buffer (flat_ops.hip) vs ATen."""
+    from cs744_pytorch_distributed_tutorial_amd import _C
+    torch.manual_seed(3)
+    for w, n in ((2, 1), (4, 1003), (8, 65536 + 3)):
+        src = torch.randn(w * n, device="cuda")
+        dst = torch.empty(n, device="cuda")
+        _C.rows_mean(src, w, dst)
+        ref = src.view(w, n).double().mean(0).float()
+        torch.testing.assert_close(dst, ref, rtol=1e-6, atol=1e-7)
+        g = torch.randn(n, device="cuda")
+        ts = [torch.randn(n, device="cuda") for _ in range(w - 1)]
+        exp = g.clone()
+        for i, t in enumerate(ts):
+            _C.accumulate(g, t, float(w) if i == len(ts) - 1 else 0.0)
+            exp.add_(t)
+        exp.div_(w)
+        assert torch.equal(g, exp)
