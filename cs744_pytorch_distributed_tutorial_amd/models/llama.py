@@ -9,10 +9,11 @@ the full replica (8.03 B parameters = 16 GB in bf16, fits the 288 GB HBM3E of on
 MI355X with gradients and optimizer state), and the step's 16 GB of bf16
 gradients is the xGMI all-reduce stress the config names.
 
-Hot elementwise ops (RMSNorm fwd/bwd, SwiGLU fwd/bwd, RoPE) have hand-written
-gfx950 kernels in ``ops.lm`` used on the GPU; GEMMs go to hipBLASLt through
-``torch.matmul`` (plain library GEMMs) and attention to
-``scaled_dot_product_attention``.
+Hot ops have hand-written gfx950 kernels used on the GPU: RMSNorm fwd/bwd, SwiGLU
+fwd/bwd and RoPE in ``ops.lm``, and causal grouped-query flash attention (forward and a
+deterministic backward, bf16, head dim 64/128) in ``ops.attention`` — called on the
+[B, S, H, D] projections directly, no transposes. The projection GEMMs are plain library
+GEMMs (hipBLASLt through ``nn.Linear``).
 """
 from __future__ import annotations
 
@@ -82,9 +83,13 @@ class Attention(nn.Module):
         k = self.wk(x).view(B, S, self.nkv, self.hd)
         v = self.wv(x).view(B, S, self.nkv, self.hd)
         q, k = _ops().rope(q, cos, sin), _ops().rope(k, cos, sin)
-        q, k, v = q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2)
-        o = F.scaled_dot_product_attention(q, k, v, is_causal=True, enable_gqa=self.nkv != self.nh)
-        return self.wo(o.transpose(1, 2).reshape(B, S, self.nh * self.hd))
+        from ..ops.attention import attention, native_ok
+        if native_ok(q, k, v):
+            o = attention(q, k, v, causal=True)  # [B, S, Hq, hd], gfx950 flash attention
+        else:  # CPU / fp32: PyTorch's attention
+            q, k, v = q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2)
+            o = F.scaled_dot_product_attention(q, k, v, is_causal=True, enable_gqa=self.nkv != self.nh).transpose(1, 2)
+        return self.wo(o.reshape(B, S, self.nh * self.hd))
 
 
 class FeedForward(nn.Module):

@@ -80,6 +80,44 @@ torch::Tensor rope(torch::Tensor x, torch::Tensor cosv, torch::Tensor sinv, bool
   return out;
 }
 
+// q [B, S, Hq, D], k/v [B, S, Hkv, D] bf16 contiguous -> {o [B, S, Hq, D], lse f32 [B, Hq, S]}
+void attn_check(const torch::Tensor& q, const torch::Tensor& k, const torch::Tensor& v) {
+  for (auto* t : {&q, &k, &v}) {
+    check(*t, "attention input");
+    TORCH_CHECK(t->scalar_type() == at::kBFloat16 && t->dim() == 4, "attention: bf16 [B, S, H, D] tensors");
+  }
+  TORCH_CHECK(k.sizes() == v.sizes() && q.size(0) == k.size(0) && q.size(1) == k.size(1) && q.size(3) == k.size(3),
+              "attention: q/k/v shapes");
+  TORCH_CHECK(q.size(3) == 64 || q.size(3) == 128, "attention: head dim 64 or 128");
+  TORCH_CHECK(q.size(2) % k.size(2) == 0, "attention: query heads must be a multiple of kv heads");
+}
+
+std::vector<torch::Tensor> attn_fwd(torch::Tensor q, torch::Tensor k, torch::Tensor v, double scale, bool causal) {
+  attn_check(q, k, v);
+  DevGuard g(q.device());
+  auto o = torch::empty_like(q);
+  auto lse = torch::empty({q.size(0), q.size(2), q.size(1)}, q.options().dtype(at::kFloat));
+  CS_LAUNCH(cs_attn_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(), q.size(0),
+                        q.size(1), q.size(2), k.size(2), q.size(3), (float)scale, causal ? 1 : 0, cur_stream()));
+  return {o, lse};
+}
+
+std::vector<torch::Tensor> attn_bwd(torch::Tensor q, torch::Tensor k, torch::Tensor v, torch::Tensor o,
+                                    torch::Tensor lse, torch::Tensor dout, double scale, bool causal) {
+  attn_check(q, k, v);
+  check(o, "o"); check(dout, "dout"); check(lse, "lse");
+  TORCH_CHECK(o.sizes() == q.sizes() && dout.sizes() == q.sizes() && o.scalar_type() == at::kBFloat16 &&
+                  dout.scalar_type() == at::kBFloat16, "attn_bwd: o / dout must match q");
+  TORCH_CHECK(lse.scalar_type() == at::kFloat && lse.numel() == q.size(0) * q.size(2) * q.size(1), "attn_bwd: lse");
+  DevGuard g(q.device());
+  auto dq = torch::empty_like(q), dk = torch::empty_like(k), dv = torch::empty_like(v);
+  auto delta = torch::empty_like(lse);
+  CS_LAUNCH(cs_attn_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), dout.data_ptr(), lse.data_ptr<float>(),
+                        delta.data_ptr<float>(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), q.size(0), q.size(1),
+                        q.size(2), k.size(2), q.size(3), (float)scale, causal ? 1 : 0, cur_stream()));
+  return {dq, dk, dv};
+}
+
 }  // namespace
 
 void register_lm_ops(pybind11::module& m) {
@@ -88,4 +126,6 @@ void register_lm_ops(pybind11::module& m) {
   m.def("swiglu_fwd", &swiglu_fwd);
   m.def("swiglu_bwd", &swiglu_bwd);
   m.def("rope", &rope);
+  m.def("attn_fwd", &attn_fwd, "flash attention forward (bf16 [B,S,H,D], GQA, causal)");
+  m.def("attn_bwd", &attn_bwd, "flash attention backward -> dq, dk, dv");
 }

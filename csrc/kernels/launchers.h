@@ -181,5 +181,12 @@ hipError_t cs_swiglu_fwd(int dt, const void* a, const void* b, void* out, size_t
 hipError_t cs_swiglu_bwd(int dt, const void* a, const void* b, const void* g, void* da, void* db, size_t n,
                          hipStream_t s);
 // x/out: [B, S, H, hd] contiguous; cos/sin: [S, hd/2] fp32; inverse rotates by -angle (backward)
+// causal / full grouped-query flash attention, bf16 [B, S, H, D] (attention.hip); lse: f32 [B, Hq, S]
+// base-2 row log-sum-exp of the scaled scores; delta: f32 [B, Hq, S] scratch of the backward
+hipError_t cs_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int S, int Hq, int Hkv,
+                       int D, float scale, int causal, hipStream_t stream);
+hipError_t cs_attn_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout, const float* lse,
+                       float* delta, void* dq, void* dk, void* dv, int B, int S, int Hq, int Hkv, int D, float scale,
+                       int causal, hipStream_t stream);
 hipError_t cs_rope(int dt, const void* x, const float* cosv, const float* sinv, void* out, int B, int S, int H, int hd,
                    int inverse, hipStream_t s);
