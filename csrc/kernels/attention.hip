@@ -15,7 +15,7 @@
 // both the ds_read_b128 row reads and the transposed reads.
 //
 // Forward: one workgroup = 4 waves = 128 queries of one (batch, head); K/V tiles of 64 keys,
-// register-staged into a double-buffered LDS image (one barrier per tile); online softmax in
+// LDS-DMA-staged into a double-buffered LDS image (one barrier per tile); online softmax in
 // base 2 (c = log2(e)/sqrt(D)); writes O and the row log-sum-exp L2 = m + log2(l) (base 2).
 // Backward (deterministic, no float atomics):
 //   attn_delta: delta = rowsum(dO * O) per (b, head, query);
@@ -116,31 +116,44 @@ __device__ __forceinline__ void store_rowT(const f32x16 (&acc)[D / 32], float mu
 constexpr int kBM = 128;  // queries per workgroup (fwd, dq) / keys per workgroup (dkdv)
 constexpr int kBN = 64;   // keys per K/V tile (fwd, dq) / queries per Q/dO tile (dkdv)
 
-// Register-staged copy of a 64-row [rows][D] global tile (row stride `stride` elements, rows
-// >= nrows zero) into an LDS image: 256 threads, CPT 16-byte chunks each.
+// LDS-DMA copy (buffer_load ... lds) of a 64-row [rows][D] global tile into an LDS image, no
+// registers: each wave-instruction writes 64 16-byte pieces = 1 KiB of the image contiguously,
+// so the swizzle is applied on the SOURCE side (image piece (row, pc) <- global chunk
+// pc ^ swz(row)); rows >= nrows get an out-of-range offset and land as zeros.
+constexpr int kOOB = 0x7ffffff0;
+
 template <int D>
-struct Stager {
-  static constexpr int NCH = D / 8, CPT = kBN * NCH / 256;
-  uint4 r[CPT];
-  __device__ void load(const __bf16* base, size_t stride, int row0, int nrows) {
-#pragma unroll
-    for (int i = 0; i < CPT; ++i) {
-      const int c = threadIdx.x + 256 * i, row = c / NCH, ch = c % NCH;
-      r[i] = row0 + row < nrows ? *reinterpret_cast<const uint4*>(base + (size_t)(row0 + row) * stride + 8 * ch)
-                                : make_uint4(0u, 0u, 0u, 0u);
-    }
+struct Dma {
+  static constexpr int NCH = D / 8, PER_WAVE = kBN * NCH / (4 * 64);  // instructions per wave
+  __amdgpu_buffer_rsrc_t rs;
+  size_t stride;  // bytes between rows
+  int nrows;
+  __device__ Dma(const __bf16* base, size_t stride_elems, int nrows_) : stride(stride_elems * 2), nrows(nrows_) {
+    const int64_t bytes = nrows_ > 0 ? (int64_t)(nrows_ - 1) * (int64_t)stride + 2 * D : 0;
+    rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<__bf16*>(base), (short)0, (int)bytes, 0x00020000);
   }
-  __device__ void store(char* img) const {
+  __device__ __forceinline__ void issue(char* img, int row0) const {
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
 #pragma unroll
-    for (int i = 0; i < CPT; ++i) {
-      const int c = threadIdx.x + 256 * i, row = c / NCH, ch = c % NCH;
-      *reinterpret_cast<uint4*>(img + Img<D>::off(row, ch)) = r[i];
+    for (int i = 0; i < PER_WAVE; ++i) {
+      const int slot = (wv * PER_WAVE + i) * 64 + lane, row = slot / NCH, pc = slot % NCH;
+      const int sw = (((row & 3) << 2) | ((row >> 2) & 3)) & (NCH - 1);
+      const int grow = row0 + row;
+      const int off = grow < nrows ? (int)((size_t)grow * stride) + 16 * (pc ^ sw) : kOOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(img + (wv * PER_WAVE + i) * 1024),
+                                               16, off, 0, 0, 0);
     }
   }
 };
 
+// every wave's LDS-DMA has landed and every wave is past its reads of the other buffer
+__device__ __forceinline__ void dma_barrier() {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+}
+
 template <int D>
-__global__ __launch_bounds__(256) void attn_fwd_kernel(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
+__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
                                                        const __bf16* __restrict__ v, __bf16* __restrict__ o,
                                                        float* __restrict__ lse, int S, int Hq, int Hkv, float c,
                                                        int causal) {
@@ -166,17 +179,16 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const __bf16* __restrict_
 
   const int kend = causal ? min(S, q0 + kBM) : S;
   const int nkt = (kend + kBN - 1) / kBN;
-  Stager<D> sk, sv;
-  sk.load(K, ks, 0, S);
-  sv.load(V, ks, 0, S);
-  sk.store(smem);
-  sv.store(smem + TILE);
-  __syncthreads();
+  const Dma<D> dk(K, ks, S), dv(V, ks, S);
+  dk.issue(smem, 0);
+  dv.issue(smem + TILE, 0);
+  dma_barrier();
   for (int kt = 0; kt < nkt; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < nkt) {
-      sk.load(K, ks, (kt + 1) * kBN, S);
-      sv.load(V, ks, (kt + 1) * kBN, S);
+    if (kt + 1 < nkt) {  // the other buffer: every wave finished reading it before the last barrier
+      char* nx = smem + (cur ^ 1) * 2 * TILE;
+      dk.issue(nx, (kt + 1) * kBN);
+      dv.issue(nx + TILE, (kt + 1) * kBN);
     }
     const char* Kl = smem + cur * 2 * TILE;
     const char* Vl = Kl + TILE;
@@ -235,12 +247,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const __bf16* __restrict_
 #pragma unroll
           for (int ss = 0; ss < 2; ++ss) acc[dt] = mfma(tr_frag<D>(Vl, 32 * t + 16 * ss, 32 * dt, lane), pf[t][ss], acc[dt]);
     }
-    if (kt + 1 < nkt) {
-      char* nx = smem + (cur ^ 1) * 2 * TILE;
-      sk.store(nx);
-      sv.store(nx + TILE);
-    }
-    __syncthreads();
+    dma_barrier();
   }
   if (qi < S) {
     store_rowT<D>(acc, l > 0.f ? 1.f / l : 0.f, o + ((size_t)b * S + qi) * qs + (size_t)hq * D, h);
@@ -274,7 +281,7 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(const __bf16* __restric
 }
 
 template <int D>
-__global__ __launch_bounds__(256) void attn_dq_kernel(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
+__global__ __launch_bounds__(256, 2) void attn_dq_kernel(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
                                                       const __bf16* __restrict__ v, const __bf16* __restrict__ dout,
                                                       const float* __restrict__ lse, const float* __restrict__ delta,
                                                       __bf16* __restrict__ dq, int S, int Hq, int Hkv, float c,
@@ -304,59 +311,48 @@ __global__ __launch_bounds__(256) void attn_dq_kernel(const __bf16* __restrict__
 
   const int kend = causal ? min(S, q0 + kBM) : S;
   const int nkt = (kend + kBN - 1) / kBN;
-  Stager<D> sk, sv;
-  sk.load(K, ks, 0, S);
-  sv.load(V, ks, 0, S);
-  sk.store(smem);
-  sv.store(smem + TILE);
-  __syncthreads();
+  const Dma<D> dmk(K, ks, S), dmv(V, ks, S);
+  dmk.issue(smem, 0);
+  dmv.issue(smem + TILE, 0);
+  dma_barrier();
   for (int kt = 0; kt < nkt; ++kt) {
     const int cur = kt & 1;
     if (kt + 1 < nkt) {
-      sk.load(K, ks, (kt + 1) * kBN, S);
-      sv.load(V, ks, (kt + 1) * kBN, S);
+      char* nx = smem + (cur ^ 1) * 2 * TILE;
+      dmk.issue(nx, (kt + 1) * kBN);
+      dmv.issue(nx + TILE, (kt + 1) * kBN);
     }
     const char* Kl = smem + cur * 2 * TILE;
     const char* Vl = Kl + TILE;
     const int k0 = kt * kBN;
-    if (!causal || k0 <= q0w + 31) {
-      f32x16 s[2], dp[2];
+    // one 32-key half of the tile at a time (no running max here: P = exp2(S c - L2) is final),
+    // which keeps two score tiles live instead of four: two waves per SIMD fit
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        s[t] = zero16();
-        dp[t] = zero16();
+    for (int t = 0; t < 2; ++t) {
+      if (causal && k0 + 32 * t > q0w + 31) continue;  // wave-uniform: the half is above the diagonal
+      f32x16 s = zero16(), dp = zero16();
 #pragma unroll
-        for (int kk = 0; kk < KK; ++kk) {
-          s[t] = mfma(row_frag<D>(Kl, 32 * t + r, kk, h), qf[kk], s[t]);
-          dp[t] = mfma(row_frag<D>(Vl, 32 * t + r, kk, h), gf[kk], dp[t]);
-        }
+      for (int kk = 0; kk < KK; ++kk) {
+        s = mfma(row_frag<D>(Kl, 32 * t + r, kk, h), qf[kk], s);
+        dp = mfma(row_frag<D>(Vl, 32 * t + r, kk, h), gf[kk], dp);
       }
-      const bool edge = (causal && k0 + kBN - 1 > q0w) || k0 + kBN > S;
+      const bool edge = (causal && k0 + 32 * t + 31 > q0w) || k0 + 32 * t + 32 > S;
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          float p = __builtin_amdgcn_exp2f(s[t][e] * c - L2);
-          if (edge) {
-            const int key = k0 + 32 * t + acc_row(e, h);
-            if ((causal && key > qi) || key >= S) p = 0.f;
-          }
-          s[t][e] = p * (dp[t][e] - dl);  // dS^T
+      for (int e = 0; e < 16; ++e) {
+        float p = __builtin_amdgcn_exp2f(s[e] * c - L2);
+        if (edge) {
+          const int key = k0 + 32 * t + acc_row(e, h);
+          if ((causal && key > qi) || key >= S) p = 0.f;
         }
+        s[e] = p * (dp[e] - dl);  // dS^T
+      }
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-          for (int ss = 0; ss < 2; ++ss)
-            acc[dt] = mfma(tr_frag<D>(Kl, 32 * t + 16 * ss, 32 * dt, lane), acc_frag(s[t], ss), acc[dt]);
+        for (int ss = 0; ss < 2; ++ss)
+          acc[dt] = mfma(tr_frag<D>(Kl, 32 * t + 16 * ss, 32 * dt, lane), acc_frag(s, ss), acc[dt]);
     }
-    if (kt + 1 < nkt) {
-      char* nx = smem + (cur ^ 1) * 2 * TILE;
-      sk.store(nx);
-      sv.store(nx + TILE);
-    }
-    __syncthreads();
+    dma_barrier();
   }
   if (qi < S) store_rowT<D>(acc, scale, dq + qrow, h);
 }
@@ -394,18 +390,15 @@ __global__ __launch_bounds__(256) void attn_dkdv_kernel(const __bf16* __restrict
   const int qt0 = causal ? (kb * kBM) / kBN : 0;
   const int nqt = (S + kBN - 1) / kBN - qt0;
   const int total = nqt * grp;
-  Stager<D> sq, sg;
-  auto load = [&](int it) {
-    const int hq = hk * grp + it / nqt, q0 = (qt0 + it % nqt) * kBN;
-    const __bf16* Q = q + (size_t)b * S * qs + (size_t)hq * D;
-    const __bf16* G = dout + (size_t)b * S * qs + (size_t)hq * D;
-    sq.load(Q, qs, q0, S);
-    sg.load(G, qs, q0, S);
-  };
+  // Q / dO tiles by LDS-DMA; L2 / delta (64 floats each) through registers
   auto store = [&](int it, int buf) {
     char* base = smem + buf * BUF;
-    sq.store(base);
-    sg.store(base + TILE);
+    {
+      const int hq = hk * grp + it / nqt, q0 = (qt0 + it % nqt) * kBN;
+      const Dma<D> dq_(q + (size_t)b * S * qs + (size_t)hq * D, qs, S), dg(dout + (size_t)b * S * qs + (size_t)hq * D, qs, S);
+      dq_.issue(base, q0);
+      dg.issue(base + TILE, q0);
+    }
     if (threadIdx.x < 2 * kBN) {  // L2 and delta of the tile's 64 queries
       const int hq = hk * grp + it / nqt, q0 = (qt0 + it % nqt) * kBN;
       const int qq = q0 + (threadIdx.x & (kBN - 1));
@@ -414,14 +407,11 @@ __global__ __launch_bounds__(256) void attn_dkdv_kernel(const __bf16* __restrict
           qq < S ? src[((size_t)b * Hq + hq) * S + qq] : 0.f;
     }
   };
-  if (total > 0) {
-    load(0);
-    store(0, 0);
-  }
-  __syncthreads();
+  if (total > 0) store(0, 0);
+  dma_barrier();
   for (int it = 0; it < total; ++it) {
     const int cur = it & 1;
-    if (it + 1 < total) load(it + 1);
+    if (it + 1 < total) store(it + 1, cur ^ 1);  // the other buffer: its readers passed the last barrier
     const char* Ql = smem + cur * BUF;
     const char* Gl = Ql + TILE;
     const float* L2s = reinterpret_cast<const float*>(Ql + 2 * TILE);
@@ -456,8 +446,7 @@ __global__ __launch_bounds__(256) void attn_dkdv_kernel(const __bf16* __restrict
           adk[dt] = mfma(tr_frag<D>(Ql, 32 * u + 16 * ss, 32 * dt, lane), acc_frag(ds, ss), adk[dt]);
         }
     }
-    if (it + 1 < total) store(it + 1, cur ^ 1);
-    __syncthreads();
+    dma_barrier();
   }
   if (kj < S) {
     store_rowT<D>(adk, scale, dk + krow, h);
