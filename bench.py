@@ -59,7 +59,9 @@ def parse(argv=None):
     p.add_argument("--bucket-mb", type=float, default=4.0,
                    help="DDP bucket cap; buckets close at layer boundaries (VGG-11: 9|9|9|4.5|3.7 MiB)")
     p.add_argument("--bucket-policy", type=str, default="layer", choices=["size", "layer", "single"])
-    p.add_argument("--dtype", type=str, default="fp32", choices=["fp32", "bf16"])
+    p.add_argument("--dtype", type=str, default=None, choices=["fp32", "bf16"],
+                   help="compute dtype (default: fp32 for the CNNs, the reference's; bf16 for the Llama LMs, "
+                        "the BASELINE config's)")
     p.add_argument("--seq-len", type=int, default=0, help="decoder LM sequence length")
     p.add_argument("--no-graph", action="store_true", help="native engine: same as --graph none")
     p.add_argument("--graph", type=str, default="auto", choices=["auto", "full", "segments", "none"])
@@ -107,6 +109,10 @@ def main(argv=None) -> int:
         # B = 1 / 2 / 4 — the fp32 master-weight SGD step amortises over more tokens)
         m = args.model.lower()
         args.batch_size = 64 if is_vgg(args.model) else (4 if "8b" in m else (8 if "llama" in m else 128))
+    if args.dtype is None:
+        args.dtype = "bf16" if "llama" in args.model.lower() else "fp32"
+    if args.seq_len == 0 and "8b" in args.model.lower():
+        args.seq_len = 2048  # the round-1 measurements' context (the model's max_seq is 8192)
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
     if world_env > 1:
         D.init_process_group(backend="nccl")
