@@ -456,6 +456,14 @@ struct TileXS {
 
 __device__ __forceinline__ void split4(const float4 v, bf16x4& h, bf16x4& m, bf16x4& l) {
   const float x[4] = {v.x, v.y, v.z, v.w};
+#ifdef CS_X6_PROBE  // measurement only (wrong numbers): prices the split arithmetic of the X6S store
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const __bf16 hj = (__bf16)x[j];
+    h[j] = hj; m[j] = hj; l[j] = hj;
+  }
+  return;
+#endif
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const __bf16 hj = (__bf16)x[j];
