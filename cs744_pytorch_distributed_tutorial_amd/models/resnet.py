@@ -9,10 +9,11 @@ layout of the widely used ImageNet implementation (``conv1``, ``bn1``,
 interchangeable with it. ResNet-50 has 25,557,032 parameters (97.5 MiB of fp32
 gradients per step — the all-reduce payload of the scaling benchmark).
 
-MI355X notes: the model is meant to run ``channels_last`` (NHWC, the layout the
-MFMA implicit-GEMM convolutions want) under optional bf16 autocast, trained by
-``parallel.ddp.DistributedDataParallel`` (flat bucketed gradients, RCCL all-reduce
-overlapped with backward) and ``ops.optim.FusedSGD`` (one HIP launch per step).
+MI355X notes: every BatchNorm with its ReLU and the bottleneck's residual add is one fused
+gfx950 pass forward and two backward (``ops.cnn.bn_act``, ``csrc/kernels/bn_nchw.hip``) on
+NCHW activations, fp32 or bf16 under autocast; convolutions are MIOpen's. Trained by
+``parallel.ddp.DistributedDataParallel`` (flat bucketed gradients, RCCL all-reduce overlapped
+with backward) and ``ops.optim.FusedSGD`` (one HIP launch per step).
 """
 from __future__ import annotations
 
@@ -21,6 +22,8 @@ from typing import List, Optional, Type, Union
 import torch
 import torch.nn as nn
 
+from ..ops.cnn import bn_act
+
 
 def conv3x3(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
     return nn.Conv2d(cin, cout, 3, stride=stride, padding=1, bias=False)
@@ -28,6 +31,11 @@ def conv3x3(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
 
 def conv1x1(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
     return nn.Conv2d(cin, cout, 1, stride=stride, bias=False)
+
+
+def _downsample(ds: nn.Sequential, x: torch.Tensor) -> torch.Tensor:
+    """the projection shortcut: conv1x1 + BN (no ReLU), the BN through the fused kernel"""
+    return bn_act(ds[1], ds[0](x), relu=False)
 
 
 class BasicBlock(nn.Module):
@@ -43,10 +51,9 @@ class BasicBlock(nn.Module):
         self.downsample = downsample
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        idt = x if self.downsample is None else self.downsample(x)
-        y = self.relu(self.bn1(self.conv1(x)))
-        y = self.bn2(self.conv2(y))
-        return self.relu(y + idt)
+        idt = x if self.downsample is None else _downsample(self.downsample, x)
+        y = bn_act(self.bn1, self.conv1(x))
+        return bn_act(self.bn2, self.conv2(y), residual=idt)
 
 
 class Bottleneck(nn.Module):
@@ -64,11 +71,10 @@ class Bottleneck(nn.Module):
         self.downsample = downsample
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        idt = x if self.downsample is None else self.downsample(x)
-        y = self.relu(self.bn1(self.conv1(x)))
-        y = self.relu(self.bn2(self.conv2(y)))
-        y = self.bn3(self.conv3(y))
-        return self.relu(y + idt)
+        idt = x if self.downsample is None else _downsample(self.downsample, x)
+        y = bn_act(self.bn1, self.conv1(x))
+        y = bn_act(self.bn2, self.conv2(y))
+        return bn_act(self.bn3, self.conv3(y), residual=idt)
 
 
 class ResNet(nn.Module):
@@ -109,7 +115,7 @@ class ResNet(nn.Module):
         return nn.Sequential(*layers)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
+        x = self.maxpool(bn_act(self.bn1, self.conv1(x)))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         return self.fc(torch.flatten(self.avgpool(x), 1))
 

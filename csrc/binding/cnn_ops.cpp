@@ -1,0 +1,86 @@
+// torch bindings of the CNN-extension kernels (csrc/kernels/bn_nchw.hip): fused training
+// BatchNorm2d (+ residual add, + ReLU) on NCHW activations; shapes/dtypes validated on the host.
+#include "binding/torch_util.h"
+#include "kernels/launchers.h"
+
+namespace {
+
+using csb::cur_stream;
+using csb::DevGuard;
+
+int act_dt(const torch::Tensor& t) {
+  if (t.scalar_type() == at::kFloat) return CS_F32;
+  if (t.scalar_type() == at::kBFloat16) return CS_BF16;
+  TORCH_CHECK(false, "bn_act: activations must be float32 or bfloat16, got ", t.scalar_type());
+  return -1;
+}
+
+void check_act(const torch::Tensor& t, const torch::Tensor& like, const char* n) {
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.sizes() == like.sizes() && t.scalar_type() == like.scalar_type(),
+              n, " must be a contiguous NCHW GPU tensor shaped and typed like x");
+}
+
+void check_param(const torch::Tensor& t, int64_t C, const char* n) {
+  if (!t.defined()) return;
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.scalar_type() == at::kFloat && t.numel() == C, n,
+              " must be a contiguous float32 GPU tensor of C elements");
+}
+
+template <typename T>
+T* opt_ptr(const c10::optional<torch::Tensor>& t) {
+  return t.has_value() && t->defined() ? t->data_ptr<T>() : nullptr;
+}
+
+// -> {y, stat [4, C]}
+std::vector<torch::Tensor> bn_act_fwd(torch::Tensor x, c10::optional<torch::Tensor> res, c10::optional<torch::Tensor> w,
+                                      c10::optional<torch::Tensor> b, c10::optional<torch::Tensor> rm,
+                                      c10::optional<torch::Tensor> rv, double momentum, double eps, bool relu) {
+  TORCH_CHECK(x.is_cuda() && x.is_contiguous() && x.dim() == 4, "bn_act: x must be a contiguous NCHW GPU tensor");
+  const int64_t N = x.size(0), C = x.size(1), HW = x.size(2) * x.size(3);
+  if (res.has_value() && res->defined()) check_act(*res, x, "res");
+  for (auto* t : {&w, &b, &rm, &rv})
+    if (t->has_value()) check_param(**t, C, "bn parameter");
+  TORCH_CHECK(rm.has_value() == rv.has_value(), "bn_act: running mean and var go together");
+  TORCH_CHECK(N * HW > 0, "bn_act: empty batch");
+  DevGuard g(x.device());
+  auto fo = x.options().dtype(at::kFloat);
+  auto y = torch::empty_like(x);
+  auto stat = torch::empty({4, C}, fo);
+  auto part = torch::empty({cs_bn_nchw_partials((int)N, (int)C)}, fo);
+  CS_LAUNCH(cs_bn_nchw_fwd(act_dt(x), x.data_ptr(), res.has_value() && res->defined() ? res->data_ptr() : nullptr,
+                           opt_ptr<float>(w), opt_ptr<float>(b), opt_ptr<float>(rm), opt_ptr<float>(rv),
+                           (float)momentum, (float)eps, relu ? 1 : 0, y.data_ptr(), stat.data_ptr<float>(),
+                           part.data_ptr<float>(), (int)N, (int)C, (int)HW, cur_stream()));
+  return {y, stat};
+}
+
+// -> {dx, dres (or undefined), dw, db}
+std::vector<torch::Tensor> bn_act_bwd(torch::Tensor dy, torch::Tensor x, c10::optional<torch::Tensor> res,
+                                      c10::optional<torch::Tensor> w, torch::Tensor stat, bool relu, bool need_dres) {
+  TORCH_CHECK(x.is_cuda() && x.is_contiguous() && x.dim() == 4, "bn_act_bwd: x must be a contiguous NCHW GPU tensor");
+  check_act(dy, x, "dy");
+  const bool has_res = res.has_value() && res->defined();
+  if (has_res) check_act(*res, x, "res");
+  const int64_t N = x.size(0), C = x.size(1), HW = x.size(2) * x.size(3);
+  if (w.has_value()) check_param(*w, C, "weight");
+  TORCH_CHECK(stat.is_cuda() && stat.scalar_type() == at::kFloat && stat.numel() == 4 * C, "bn_act_bwd: stat");
+  DevGuard g(x.device());
+  auto fo = x.options().dtype(at::kFloat);
+  auto dx = torch::empty_like(x);
+  torch::Tensor dres = need_dres ? torch::empty_like(x) : torch::Tensor();
+  auto dw = torch::empty({C}, fo), db = torch::empty({C}, fo);
+  auto coef = torch::empty({3, C}, fo);
+  auto part = torch::empty({cs_bn_nchw_partials((int)N, (int)C)}, fo);
+  CS_LAUNCH(cs_bn_nchw_bwd(act_dt(x), dy.data_ptr(), x.data_ptr(), has_res ? res->data_ptr() : nullptr,
+                           opt_ptr<float>(w), stat.data_ptr<float>(), relu ? 1 : 0, dx.data_ptr(),
+                           need_dres ? dres.data_ptr() : nullptr, dw.data_ptr<float>(), db.data_ptr<float>(),
+                           coef.data_ptr<float>(), part.data_ptr<float>(), (int)N, (int)C, (int)HW, cur_stream()));
+  return {dx, dres, dw, db};
+}
+
+}  // namespace
+
+void register_cnn_ops(pybind11::module& m) {
+  m.def("bn_act_fwd", &bn_act_fwd, "fused training BatchNorm2d (+residual) (+ReLU), NCHW fp32/bf16 -> (y, stat)");
+  m.def("bn_act_bwd", &bn_act_bwd, "its backward -> (dx, dres, dweight, dbias)");
+}

@@ -152,6 +152,7 @@ std::vector<torch::Tensor> softmax_xent(torch::Tensor logits, torch::Tensor labe
 void register_conv_ops(pybind11::module& m);
 void register_runtime(pybind11::module& m);
 void register_lm_ops(pybind11::module& m);
+void register_cnn_ops(pybind11::module& m);
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "gfx950 (MI355X) kernels + native runtime for cs744_pytorch_distributed_tutorial_amd";
@@ -166,4 +167,5 @@ PYBIND11_MODULE(_C, m) {
   register_conv_ops(m);
   register_runtime(m);
   register_lm_ops(m);
+  register_cnn_ops(m);
 }
