@@ -22,7 +22,7 @@ from typing import List, Optional, Type, Union
 import torch
 import torch.nn as nn
 
-from ..ops.cnn import bn_act
+from ..ops.cnn import bn_act, max_pool3s2
 
 
 def conv3x3(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
@@ -115,7 +115,7 @@ class ResNet(nn.Module):
         return nn.Sequential(*layers)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        x = self.maxpool(bn_act(self.bn1, self.conv1(x)))
+        x = max_pool3s2(bn_act(self.bn1, self.conv1(x)))  # self.maxpool's op, on the gfx950 kernel
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         return self.fc(torch.flatten(self.avgpool(x), 1))
 

@@ -57,3 +57,25 @@ def bn_act(bn: nn.BatchNorm2d, x: torch.Tensor, relu: bool = True,
     if residual is not None:
         y = y + residual
     return F.relu(y) if relu else y
+
+
+class _MaxPool3s2(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        y, pos = native.C().maxpool3s2_fwd(x)
+        ctx.save_for_backward(pos)
+        ctx.hw = (x.shape[2], x.shape[3])
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (pos,) = ctx.saved_tensors
+        return native.C().maxpool3s2_bwd(dy.contiguous(), pos, *ctx.hw)
+
+
+def max_pool3s2(x: torch.Tensor) -> torch.Tensor:
+    """``F.max_pool2d(x, 3, 2, 1)``: the gfx950 kernels for contiguous NCHW fp32 / bf16 GPU
+    tensors (gather-style deterministic backward), ATen otherwise."""
+    if x.is_cuda and x.dim() == 4 and x.is_contiguous() and x.dtype in (torch.float32, torch.bfloat16):
+        return _MaxPool3s2.apply(x)
+    return F.max_pool2d(x, 3, 2, 1)

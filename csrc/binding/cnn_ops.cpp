@@ -78,9 +78,34 @@ std::vector<torch::Tensor> bn_act_bwd(torch::Tensor dy, torch::Tensor x, c10::op
   return {dx, dres, dw, db};
 }
 
+// 3x3/2 max-pool, padding 1: -> {y, pos (uint8 window position)}
+std::vector<torch::Tensor> maxpool3s2_fwd(torch::Tensor x) {
+  TORCH_CHECK(x.is_cuda() && x.is_contiguous() && x.dim() == 4, "maxpool3s2: x must be a contiguous NCHW GPU tensor");
+  const int64_t H = x.size(2), W = x.size(3), Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+  DevGuard g(x.device());
+  auto y = torch::empty({x.size(0), x.size(1), Ho, Wo}, x.options());
+  auto pos = torch::empty({x.size(0), x.size(1), Ho, Wo}, x.options().dtype(at::kByte));
+  CS_LAUNCH(cs_maxpool3s2_fwd(act_dt(x), x.data_ptr(), y.data_ptr(), pos.data_ptr<uint8_t>(), x.size(0) * x.size(1),
+                              (int)H, (int)W, (int)Ho, (int)Wo, cur_stream()));
+  return {y, pos};
+}
+
+torch::Tensor maxpool3s2_bwd(torch::Tensor dy, torch::Tensor pos, int64_t H, int64_t W) {
+  TORCH_CHECK(dy.is_cuda() && dy.is_contiguous() && dy.dim() == 4 && pos.sizes() == dy.sizes() &&
+                  pos.scalar_type() == at::kByte && pos.is_contiguous(), "maxpool3s2_bwd: dy / pos");
+  TORCH_CHECK(dy.size(2) == (H - 1) / 2 + 1 && dy.size(3) == (W - 1) / 2 + 1, "maxpool3s2_bwd: input size");
+  DevGuard g(dy.device());
+  auto dx = torch::empty({dy.size(0), dy.size(1), H, W}, dy.options());
+  CS_LAUNCH(cs_maxpool3s2_bwd(act_dt(dy), dy.data_ptr(), pos.data_ptr<uint8_t>(), dx.data_ptr(), dy.size(0) * dy.size(1),
+                              (int)H, (int)W, (int)dy.size(2), (int)dy.size(3), cur_stream()));
+  return dx;
+}
+
 }  // namespace
 
 void register_cnn_ops(pybind11::module& m) {
   m.def("bn_act_fwd", &bn_act_fwd, "fused training BatchNorm2d (+residual) (+ReLU), NCHW fp32/bf16 -> (y, stat)");
   m.def("bn_act_bwd", &bn_act_bwd, "its backward -> (dx, dres, dweight, dbias)");
+  m.def("maxpool3s2_fwd", &maxpool3s2_fwd, "3x3/2 pad-1 max-pool, NCHW -> (y, window position)");
+  m.def("maxpool3s2_bwd", &maxpool3s2_bwd, "its gather-style backward");
 }

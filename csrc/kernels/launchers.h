@@ -199,5 +199,11 @@ hipError_t cs_bn_nchw_fwd(int dt, const void* x, const void* res, const float* w
 hipError_t cs_bn_nchw_bwd(int dt, const void* dy, const void* x, const void* res, const float* w, const float* stat,
                           int relu, void* dx, void* dres, float* dw, float* db, float* coef, float* part, int N, int C,
                           int HW, hipStream_t stream);
+// 3x3 / stride 2 / pad 1 max-pool on NCHW planes (pool_nchw.hip); pos: uint8 winning window
+// position per output (0..8), consumed by the gather-style backward
+hipError_t cs_maxpool3s2_fwd(int dt, const void* x, void* y, unsigned char* pos, int64_t planes, int H, int W, int Ho,
+                             int Wo, hipStream_t stream);
+hipError_t cs_maxpool3s2_bwd(int dt, const void* dy, const unsigned char* pos, void* dx, int64_t planes, int H, int W,
+                             int Ho, int Wo, hipStream_t stream);
 hipError_t cs_rope(int dt, const void* x, const float* cosv, const float* sinv, void* out, int B, int S, int H, int hd,
                    int inverse, hipStream_t s);
