@@ -7,7 +7,7 @@ statistics and running stats (momentum not None), and ``x`` is a contiguous NCHW
 GPU tensor: one statistics pass, one normalise/add/ReLU pass, and in the backward one reduction
 pass and one dx (+ residual gradient) pass, with the ReLU mask recomputed from the saved input
 instead of stored. Running mean / var and ``num_batches_tracked`` are updated like
-``nn.BatchNorm2d``. Anything else (CPU, eval mode, channels_last) runs the module itself.
+``nn.BatchNorm2d``, inside the statistics launch. Anything else (CPU, eval mode, channels_last) runs the module itself.
 """
 from __future__ import annotations
 
@@ -22,8 +22,9 @@ from . import native
 
 class _BnAct(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, residual, running_mean, running_var, momentum, eps, relu):
-        y, stat = native.C().bn_act_fwd(x, residual, weight, bias, running_mean, running_var, momentum, eps, relu)
+    def forward(ctx, x, weight, bias, residual, running_mean, running_var, nbt, momentum, eps, relu):
+        y, stat = native.C().bn_act_fwd(x, residual, weight, bias, running_mean, running_var, nbt, momentum, eps,
+                                        relu)
         ctx.save_for_backward(x, residual, weight, stat)
         ctx.relu = relu
         ctx.has_res = residual is not None
@@ -34,7 +35,7 @@ class _BnAct(torch.autograd.Function):
         x, residual, weight, stat = ctx.saved_tensors
         dx, dres, dw, db = native.C().bn_act_bwd(dy.contiguous(), x, residual, weight, stat, ctx.relu, ctx.has_res)
         return (dx, dw if weight is not None else None, db if weight is not None else None,
-                dres if ctx.has_res else None, None, None, None, None, None)
+                dres if ctx.has_res else None, None, None, None, None, None, None)
 
 
 def native_ok(bn: nn.BatchNorm2d, x: torch.Tensor, residual: Optional[torch.Tensor]) -> bool:
@@ -49,10 +50,8 @@ def bn_act(bn: nn.BatchNorm2d, x: torch.Tensor, relu: bool = True,
     if native_ok(bn, x, residual):
         if residual is not None:
             residual = residual.contiguous()
-        y = _BnAct.apply(x, bn.weight, bn.bias, residual, bn.running_mean, bn.running_var, float(bn.momentum),
-                         float(bn.eps), relu)
-        bn.num_batches_tracked.add_(1)
-        return y
+        return _BnAct.apply(x, bn.weight, bn.bias, residual, bn.running_mean, bn.running_var,
+                            bn.num_batches_tracked, float(bn.momentum), float(bn.eps), relu)
     y = bn(x)
     if residual is not None:
         y = y + residual

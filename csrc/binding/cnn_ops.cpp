@@ -34,13 +34,16 @@ T* opt_ptr(const c10::optional<torch::Tensor>& t) {
 // -> {y, stat [4, C]}
 std::vector<torch::Tensor> bn_act_fwd(torch::Tensor x, c10::optional<torch::Tensor> res, c10::optional<torch::Tensor> w,
                                       c10::optional<torch::Tensor> b, c10::optional<torch::Tensor> rm,
-                                      c10::optional<torch::Tensor> rv, double momentum, double eps, bool relu) {
+                                      c10::optional<torch::Tensor> rv, c10::optional<torch::Tensor> nbt, double momentum,
+                                      double eps, bool relu) {
   TORCH_CHECK(x.is_cuda() && x.is_contiguous() && x.dim() == 4, "bn_act: x must be a contiguous NCHW GPU tensor");
   const int64_t N = x.size(0), C = x.size(1), HW = x.size(2) * x.size(3);
   if (res.has_value() && res->defined()) check_act(*res, x, "res");
   for (auto* t : {&w, &b, &rm, &rv})
     if (t->has_value()) check_param(**t, C, "bn parameter");
   TORCH_CHECK(rm.has_value() == rv.has_value(), "bn_act: running mean and var go together");
+  if (nbt.has_value())
+    TORCH_CHECK(nbt->is_cuda() && nbt->scalar_type() == at::kLong && nbt->numel() == 1, "bn_act: num_batches_tracked");
   TORCH_CHECK(N * HW > 0, "bn_act: empty batch");
   DevGuard g(x.device());
   auto fo = x.options().dtype(at::kFloat);
@@ -49,7 +52,7 @@ std::vector<torch::Tensor> bn_act_fwd(torch::Tensor x, c10::optional<torch::Tens
   auto part = torch::empty({cs_bn_nchw_partials((int)N, (int)C)}, fo);
   CS_LAUNCH(cs_bn_nchw_fwd(act_dt(x), x.data_ptr(), res.has_value() && res->defined() ? res->data_ptr() : nullptr,
                            opt_ptr<float>(w), opt_ptr<float>(b), opt_ptr<float>(rm), opt_ptr<float>(rv),
-                           (float)momentum, (float)eps, relu ? 1 : 0, y.data_ptr(), stat.data_ptr<float>(),
+                           opt_ptr<int64_t>(nbt), (float)momentum, (float)eps, relu ? 1 : 0, y.data_ptr(), stat.data_ptr<float>(),
                            part.data_ptr<float>(), (int)N, (int)C, (int)HW, cur_stream()));
   return {y, stat};
 }

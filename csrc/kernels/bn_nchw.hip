@@ -110,8 +110,10 @@ __global__ __launch_bounds__(256) void finalize_fwd_kernel(const T* __restrict__
                                                            int P, int C, int HW, double M, const float* __restrict__ w,
                                                            const float* __restrict__ b, float* __restrict__ rm,
                                                            float* __restrict__ rv, float momentum, float eps,
-                                                           float* __restrict__ stat /* [4][C] */) {
+                                                           float* __restrict__ stat /* [4][C] */,
+                                                           int64_t* __restrict__ nbt) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c == 0 && nbt != nullptr) *nbt += 1;  // num_batches_tracked
   if (c >= C) return;
   double s1 = 0.0, s2 = 0.0;
   for (int p = 0; p < P; ++p) {
@@ -255,12 +257,13 @@ int apply_grid(int64_t nvec) {
 }
 
 template <typename T, int V>
-void fwd_t(const void* x, const void* res, const float* w, const float* b, float* rm, float* rv, float momentum,
-           float eps, int relu, void* y, float* stat, float* part, int N, int C, int HW, hipStream_t st) {
+void fwd_t(const void* x, const void* res, const float* w, const float* b, float* rm, float* rv, int64_t* nbt,
+           float momentum, float eps, int relu, void* y, float* stat, float* part, int N, int C, int HW,
+           hipStream_t st) {
   const int P = chunks(N, C), npb = (N + P - 1) / P;
   hipLaunchKernelGGL((stats_kernel<T, V>), dim3(P, C), dim3(256), 0, st, (const T*)x, N, C, HW, npb, part);
   hipLaunchKernelGGL(finalize_fwd_kernel<T>, dim3((C + 255) / 256), dim3(256), 0, st, (const T*)x, part, P, C, HW,
-                     (double)N * HW, w, b, rm, rv, momentum, eps, stat);
+                     (double)N * HW, w, b, rm, rv, momentum, eps, stat, nbt);
   const int64_t nvec = (int64_t)N * C * HW / V;
   hipLaunchKernelGGL((apply_fwd_kernel<T, V>), dim3(apply_grid(nvec)), dim3(256), 0, st, (const T*)x, (const T*)res,
                      stat, (T*)y, C, HW, nvec, relu);
@@ -284,18 +287,18 @@ void bwd_t(const void* dy, const void* x, const void* res, const float* w, const
 int cs_bn_nchw_partials(int N, int C) { return chunks(N, C) * C * 2; }
 
 hipError_t cs_bn_nchw_fwd(int dt, const void* x, const void* res, const float* w, const float* b, float* rm, float* rv,
-                          float momentum, float eps, int relu, void* y, float* stat, float* part, int N, int C, int HW,
-                          hipStream_t stream) {
+                          int64_t* nbt, float momentum, float eps, int relu, void* y, float* stat, float* part, int N,
+                          int C, int HW, hipStream_t stream) {
   if ((int64_t)N * C * HW == 0) return hipSuccess;
   if (dt == CS_BF16) {
     const int V = vec_width(HW, 2);
-    if (V == 8) fwd_t<__hip_bfloat16, 8>(x, res, w, b, rm, rv, momentum, eps, relu, y, stat, part, N, C, HW, stream);
-    else if (V == 4) fwd_t<__hip_bfloat16, 4>(x, res, w, b, rm, rv, momentum, eps, relu, y, stat, part, N, C, HW, stream);
-    else fwd_t<__hip_bfloat16, 1>(x, res, w, b, rm, rv, momentum, eps, relu, y, stat, part, N, C, HW, stream);
+    if (V == 8) fwd_t<__hip_bfloat16, 8>(x, res, w, b, rm, rv, nbt, momentum, eps, relu, y, stat, part, N, C, HW, stream);
+    else if (V == 4) fwd_t<__hip_bfloat16, 4>(x, res, w, b, rm, rv, nbt, momentum, eps, relu, y, stat, part, N, C, HW, stream);
+    else fwd_t<__hip_bfloat16, 1>(x, res, w, b, rm, rv, nbt, momentum, eps, relu, y, stat, part, N, C, HW, stream);
   } else {
     const int V = vec_width(HW, 4);
-    if (V == 4) fwd_t<float, 4>(x, res, w, b, rm, rv, momentum, eps, relu, y, stat, part, N, C, HW, stream);
-    else fwd_t<float, 1>(x, res, w, b, rm, rv, momentum, eps, relu, y, stat, part, N, C, HW, stream);
+    if (V == 4) fwd_t<float, 4>(x, res, w, b, rm, rv, nbt, momentum, eps, relu, y, stat, part, N, C, HW, stream);
+    else fwd_t<float, 1>(x, res, w, b, rm, rv, nbt, momentum, eps, relu, y, stat, part, N, C, HW, stream);
   }
   return hipGetLastError();
 }

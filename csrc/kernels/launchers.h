@@ -191,11 +191,11 @@ hipError_t cs_attn_bwd(const void* q, const void* k, const void* v, const void* 
 // training BatchNorm2d (+ residual add, + ReLU) on NCHW fp32 / bf16 activations (bn_nchw.hip).
 // stat: f32 [4, C] = scale, shift, mean, invstd (written by the forward, read by the backward);
 // part: f32 scratch of cs_bn_nchw_partials(N, C) floats; coef: f32 [3, C] scratch (backward).
-// rm / rv (running stats, updated with `momentum`), w / b, res, dres, dw, db may be null.
+// rm / rv (running stats, updated with `momentum`; nbt += 1), w / b, res, dres, dw, db, nbt may be null.
 int cs_bn_nchw_partials(int N, int C);
 hipError_t cs_bn_nchw_fwd(int dt, const void* x, const void* res, const float* w, const float* b, float* rm, float* rv,
-                          float momentum, float eps, int relu, void* y, float* stat, float* part, int N, int C, int HW,
-                          hipStream_t stream);
+                          int64_t* nbt, float momentum, float eps, int relu, void* y, float* stat, float* part, int N,
+                          int C, int HW, hipStream_t stream);
 hipError_t cs_bn_nchw_bwd(int dt, const void* dy, const void* x, const void* res, const float* w, const float* stat,
                           int relu, void* dx, void* dres, float* dw, float* db, float* coef, float* part, int N, int C,
                           int HW, hipStream_t stream);
