@@ -272,10 +272,13 @@ class NativeTrainer:
         # (measured: layers.25.weight wrong at step 3 of 4, world 2, whether the side stream
         # was joined by a stream link or a HIP event; only a host sync of the side stream
         # avoided it), so that path keeps the serial backward.
+        # Also off under rocprofv3 counter collection, which serialises every dispatch: a side-stream
+        # link wait would spin to its timeout waiting for a signal that cannot run.
         from .. import HW_QUEUES
         python_collectives = world > 1 and self.native_comm is None
+        counters = bool(os.environ.get("ROCPROF_COUNTERS") or os.environ.get("ROCPROF_COUNTER_COLLECTION"))
         self.overlap_wgrad = os.environ.get("CS_OVERLAP_WGRAD", "1") != "0" and not python_collectives and (
-            self.native_comm is None or HW_QUEUES >= 8)
+            self.native_comm is None or HW_QUEUES >= 8) and not counters
         self.engine.set_overlap_wgrad(self.overlap_wgrad)
         self.engine.set_data(0, self.train_data, self.train_labels, self.aug_train)
         self.engine.set_data(1, self.test_data, self.test_labels, self.aug_test)
