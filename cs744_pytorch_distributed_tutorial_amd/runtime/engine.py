@@ -523,7 +523,11 @@ class NativeTrainer:
     def check_comm(self) -> None:
         """Async-error poll of the native communicator (ncclCommGetAsyncError for RCCL): on an
         error the communicator is aborted (ncclCommAbort) and the step raises, so a dead peer
-        becomes a prompt failure instead of a hang."""
+        becomes a prompt failure instead of a hang. Also raises when one of the
+        engine's own side-stream links timed out (its ordering can no longer be trusted)."""
+        link = self.engine.link_error()
+        if link:
+            raise RuntimeError(f"rank {self.rank}: engine stream link failed: {link}")
         if self.native_comm is None:
             return
         err = self.native_comm.async_error()

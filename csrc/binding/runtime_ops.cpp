@@ -163,6 +163,7 @@ void register_runtime(pybind11::module& m) {
       .def("set_overlap_wgrad", &cs::VggEngine::set_overlap_wgrad)
       .def("set_sgd_overlap", &cs::VggEngine::set_sgd_overlap)
       .def("set_sgd_side", &cs::VggEngine::set_sgd_side)
+      .def("link_error", &cs::VggEngine::link_error)
       .def("set_sgd_first", &cs::VggEngine::set_sgd_first)
       .def("set_debug_skip", &cs::VggEngine::set_debug_skip)
       .def("set_timing", &cs::VggEngine::set_timing)

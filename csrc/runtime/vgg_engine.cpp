@@ -213,6 +213,11 @@ bool VggEngine::side_wgrad(hipStream_t s) const { return overlap_wgrad_ && !stre
 
 void VggEngine::join_side(hipStream_t s) { wg_link_->wait(s); }
 
+std::string VggEngine::link_error() const {
+  std::string e = dz_link_->error();
+  return e.empty() ? wg_link_->error() : e;
+}
+
 void VggEngine::set_overlap_wgrad(bool on) {
   overlap_wgrad_ = on;
   if (on && dz_blk_.empty()) {

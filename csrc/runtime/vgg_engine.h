@@ -79,6 +79,8 @@ class VggEngine {
   void set_overlap_wgrad(bool on);
   bool side_wgrad(hipStream_t s) const;  // overlap on and `s` not capturing a graph
   void join_side(hipStream_t s);          // `s` waits for every side-stream weight gradient so far
+  // "" unless a side-stream link wait timed out (device_comm.h StreamLink: bounded waits)
+  std::string link_error() const;
   void set_fixup(bool on) { fixup_ = on; }
   void set_dual(bool on) { dual_ = on; }
   void set_bn_fused_rows(int64_t r) { bn_fused_rows_ = r; }

@@ -17,10 +17,19 @@ def main():
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--window", type=int, default=20)
     p.add_argument("--windows", type=int, default=15)
+    p.add_argument("--extra-streams", type=int, default=0,
+                   help="create and use this many extra HIP streams first (more streams than hardware "
+                        "queues: do the side-stream links still make progress when queues are shared?)")
     a = p.parse_args()
     from cs744_pytorch_distributed_tutorial_amd.runtime.engine import NativeTrainer
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
+    extra = [torch.cuda.Stream() for _ in range(a.extra_streams)]
+    scratch = torch.zeros(1024, device=dev)
+    for st in extra:  # a kernel on every stream, so each is bound to a hardware queue
+        with torch.cuda.stream(st):
+            scratch.add_(1.0)
+    torch.cuda.synchronize()
     t = NativeTrainer(batch_size=64, device=dev, graph="auto")
     for _ in range(a.warmup):
         t.step()
@@ -33,9 +42,15 @@ def main():
         t1 = time.perf_counter()
         torch.cuda.synchronize()
         t2 = time.perf_counter()
+        if extra:  # keep the extra streams busy between windows too
+            for st in extra:
+                with torch.cuda.stream(st):
+                    scratch.add_(1.0)
         rows.append({"window": w, "ms_per_step": round((t2 - t0) * 1e3 / a.window, 4),
                      "host_enqueue_ms_per_step": round((t1 - t0) * 1e3 / a.window, 4)})
         print(json.dumps(rows[-1]), flush=True)
+    t.check_comm()  # raises if a side-stream link wait timed out
+    print("links ok", flush=True)
 
 
 if __name__ == "__main__":
