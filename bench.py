@@ -114,6 +114,12 @@ def main(argv=None) -> int:
     if args.seq_len == 0 and "8b" in args.model.lower():
         args.seq_len = 2048  # the round-1 measurements' context (the model's max_seq is 8192)
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.engine == "native" and is_vgg(args.model):
+        # before the process group or anything else creates streams: the native engine's side
+        # stream must own a hardware queue (measured 4x slower steps when it shares one)
+        from cs744_pytorch_distributed_tutorial_amd.ops import native
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+        native.C().reserve_streams()
     if world_env > 1:
         D.init_process_group(backend="nccl")
     rank, world = D.get_rank(), D.get_world_size()

@@ -194,6 +194,8 @@ class NativeTrainer:
                  check_every: int = 0):
         C = native.C()
         self.device = device or torch.device("cuda", torch.cuda.current_device())
+        with torch.cuda.device(self.device):
+            C.reserve_streams()  # the engine's side stream gets its own hardware queue (device_comm.h)
         self.rank, self.world = rank, world
         self.B = batch_size
         self.lr, self.momentum, self.wd, self.damp = lr, momentum, weight_decay, dampening

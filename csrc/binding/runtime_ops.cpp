@@ -41,6 +41,9 @@ void check_gpu(const torch::Tensor& t, const char* name) {
 }  // namespace
 
 void register_runtime(pybind11::module& m) {
+  m.def("reserve_streams", &cs::reserve_streams,
+        "create (once per process) the native engine's side stream and bind it to a hardware queue; call it "
+        "before other code creates streams");
   namespace py = pybind11;
   m.def("rccl_unique_id", []() { return py::bytes(cs::RcclComm::unique_id()); });
   m.def("rccl_version", []() {

@@ -49,6 +49,16 @@ class DeviceComm {
 // whether `s` is being captured into a graph (links fall back to events there)
 bool stream_capturing(hipStream_t s);
 
+// The engine's side stream (weight gradients + their SGD), created once per process and bound to
+// a hardware queue on creation (one tiny fill runs on it). Measured on MI355X: when the side
+// stream is created after other streams have already taken the process's hardware queues
+// (GPU_MAX_HW_QUEUES), it shares a queue and every side/main link handoff stalls — the VGG-11
+// step went from 0.72 to 2.8 ms with 8-40 busy streams created first (at 8, 16 or 32 queues), and
+// stayed at 0.72 ms when those streams came after it. reserve_streams() creates it now: call it
+// before anything else creates streams (NativeTrainer and bench.py do).
+hipStream_t reserved_side_stream();
+void reserve_streams();
+
 // One-direction kernel stream link (stream_link.hip): signal(producer) enqueues a one-lane
 // counter bump; wait(consumer) makes the consumer wait for EVERY signal issued so far (the
 // host counts them; the device keeps the expected count, so captured graphs replay

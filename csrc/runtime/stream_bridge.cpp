@@ -60,6 +60,24 @@ std::string StreamLink::error() const {
   return std::string();
 }
 
+hipStream_t reserved_side_stream() {
+  static hipStream_t side = [] {
+    int least = 0, greatest = 0;
+    hip_ok(hipDeviceGetStreamPriorityRange(&least, &greatest), "stream priorities");
+    hipStream_t s = nullptr;
+    hip_ok(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, least), "side stream");
+    void* scratch = nullptr;
+    hip_ok(hipMalloc(&scratch, 256), "side stream scratch");
+    hip_ok(hipMemsetAsync(scratch, 0, 256, s), "bind side stream");
+    hip_ok(hipStreamSynchronize(s), "bind side stream");
+    hip_ok(hipFree(scratch), "side stream scratch");
+    return s;
+  }();
+  return side;
+}
+
+void reserve_streams() { (void)reserved_side_stream(); }
+
 bool stream_capturing(hipStream_t s) {
   hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
   return hipStreamIsCapturing(s, &st) == hipSuccess && st != hipStreamCaptureStatusNone;

@@ -157,11 +157,7 @@ VggEngine::VggEngine(int64_t Bmax, std::vector<int64_t> desc, std::vector<int64_
   ws_elems_ = kWsElems;
   ws_ = torch::zeros({ws_elems_}, fo);
   ws_side_ = torch::zeros({ws_elems_}, fo);
-  {
-    int least = 0, greatest = 0;
-    ok(hipDeviceGetStreamPriorityRange(&least, &greatest), "stream priorities");
-    ok(hipStreamCreateWithPriority(&side_, hipStreamNonBlocking, least), "side stream");
-  }
+  side_ = reserved_side_stream();  // process-wide, created early (device_comm.h)
   dz_link_ = std::make_unique<StreamLink>();
   wg_link_ = std::make_unique<StreamLink>();
   ok(hipStreamCreateWithFlags(&opt_, hipStreamNonBlocking), "optimizer stream");
@@ -508,10 +504,7 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
 }
 
 VggEngine::~VggEngine() {
-  if (side_ != nullptr) {
-    hipStreamSynchronize(side_);
-    hipStreamDestroy(side_);
-  }
+  if (side_ != nullptr) hipStreamSynchronize(side_);  // shared process-wide stream: not destroyed
   if (opt_ != nullptr) {
     hipStreamSynchronize(opt_);
     hipStreamDestroy(opt_);

@@ -20,17 +20,41 @@ def main():
     p.add_argument("--extra-streams", type=int, default=0,
                    help="create and use this many extra HIP streams first (more streams than hardware "
                         "queues: do the side-stream links still make progress when queues are shared?)")
+    p.add_argument("--extra-after", action="store_true", help="create the extra streams after the trainer")
+    p.add_argument("--reserve-first", action="store_true", help="reserve the engine's side stream before anything")
+    p.add_argument("--nccl-pg", action="store_true",
+                   help="first bring up a one-rank NCCL (RCCL) process group and run a barrier and an all-reduce "
+                        "through it, as a multi-GPU job does before building its trainer")
     a = p.parse_args()
+    if a.reserve_first:
+        from cs744_pytorch_distributed_tutorial_amd.ops import native
+        torch.cuda.set_device(0)
+        native.C().reserve_streams()
+    if a.nccl_pg:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        torch.cuda.set_device(0)
+        torch.distributed.init_process_group("nccl", rank=0, world_size=1)
+        torch.distributed.barrier(device_ids=[0])
+        x = torch.ones(4, device="cuda")
+        torch.distributed.all_reduce(x)
+        torch.cuda.synchronize()
     from cs744_pytorch_distributed_tutorial_amd.runtime.engine import NativeTrainer
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    extra = [torch.cuda.Stream() for _ in range(a.extra_streams)]
+    def make_extra():
+        ex = [torch.cuda.Stream() for _ in range(a.extra_streams)]
+        for st in ex:  # a kernel on every stream, so each is bound to a hardware queue
+            with torch.cuda.stream(st):
+                scratch.add_(1.0)
+        torch.cuda.synchronize()
+        return ex
+
     scratch = torch.zeros(1024, device=dev)
-    for st in extra:  # a kernel on every stream, so each is bound to a hardware queue
-        with torch.cuda.stream(st):
-            scratch.add_(1.0)
-    torch.cuda.synchronize()
+    extra = [] if a.extra_after else make_extra()
     t = NativeTrainer(batch_size=64, device=dev, graph="auto")
+    if a.extra_after:
+        extra = make_extra()
     for _ in range(a.warmup):
         t.step()
     torch.cuda.synchronize()
