@@ -56,7 +56,10 @@ bool stream_capturing(hipStream_t s);
 // step went from 0.72 to 2.8 ms with 8-40 busy streams created first (at 8, 16 or 32 queues), and
 // stayed at 0.72 ms when those streams came after it. reserve_streams() creates it now: call it
 // before anything else creates streams (NativeTrainer and bench.py do).
+// reserved_comm_stream(): the same for RcclComm's (high-priority) stream, whose fork/join links
+// stall the same way when it shares a queue.
 hipStream_t reserved_side_stream();
+hipStream_t reserved_comm_stream();
 void reserve_streams();
 
 // One-direction kernel stream link (stream_link.hip): signal(producer) enqueues a one-lane

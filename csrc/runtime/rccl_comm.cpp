@@ -42,9 +42,14 @@ RcclComm::RcclComm(const std::string& uid, int rank, int world, int device, bool
   if (uid.size() != sizeof(ncclUniqueId)) throw std::runtime_error("RcclComm: unique id must be 128 bytes");
   if (rank < 0 || rank >= world) throw std::runtime_error("RcclComm: bad rank");
   hip_ok(hipSetDevice(device), "hipSetDevice");
-  int lo = 0, hi = 0;
-  hip_ok(hipDeviceGetStreamPriorityRange(&lo, &hi), "hipDeviceGetStreamPriorityRange");
-  hip_ok(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, high_priority ? hi : lo), "stream");
+  if (high_priority) {  // the process-wide reserved comm stream: its own hardware queue (device_comm.h)
+    stream_ = reserved_comm_stream();
+    own_stream_ = false;
+  } else {
+    int lo = 0, hi = 0;
+    hip_ok(hipDeviceGetStreamPriorityRange(&lo, &hi), "hipDeviceGetStreamPriorityRange");
+    hip_ok(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, lo), "stream");
+  }
   ncclUniqueId id;
   std::memcpy(&id, uid.data(), sizeof(id));
   nccl_ok(ncclCommInitRank(&comm_, world, id, rank), "ncclCommInitRank");
@@ -57,7 +62,7 @@ RcclComm::~RcclComm() {
       ncclCommDestroy(comm_);
     }
   }
-  if (stream_) hipStreamDestroy(stream_);
+  if (stream_ && own_stream_) hipStreamDestroy(stream_);
 }
 
 void RcclComm::fork(hipStream_t compute) {

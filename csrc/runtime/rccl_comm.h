@@ -62,6 +62,7 @@ class RcclComm final : public DeviceComm {
   void fork(hipStream_t compute);
   ncclComm_t comm_ = nullptr;
   hipStream_t stream_ = nullptr;
+  bool own_stream_ = true;  // false: the process-wide reserved comm stream (never destroyed)
   // (CS_COMM_FORK=1, stream memory operations hipStreamWriteValue64 / hipStreamWaitValue64 on
   // signal memory, was measured and dropped: 59.7k img/s vs 70.3-73.3k with events on the
   // one-rank probe, profiles/r1_dp_plumbing_probe.md)

@@ -60,23 +60,37 @@ std::string StreamLink::error() const {
   return std::string();
 }
 
+namespace {
+// a non-blocking stream at the lowest (or highest) priority, bound to a hardware queue by one
+// tiny fill (queues are taken when a stream first runs work)
+hipStream_t bound_stream(bool high) {
+  int least = 0, greatest = 0;
+  hip_ok(hipDeviceGetStreamPriorityRange(&least, &greatest), "stream priorities");
+  hipStream_t s = nullptr;
+  hip_ok(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, high ? greatest : least), "reserved stream");
+  void* scratch = nullptr;
+  hip_ok(hipMalloc(&scratch, 256), "reserved stream scratch");
+  hip_ok(hipMemsetAsync(scratch, 0, 256, s), "bind reserved stream");
+  hip_ok(hipStreamSynchronize(s), "bind reserved stream");
+  hip_ok(hipFree(scratch), "reserved stream scratch");
+  return s;
+}
+}  // namespace
+
 hipStream_t reserved_side_stream() {
-  static hipStream_t side = [] {
-    int least = 0, greatest = 0;
-    hip_ok(hipDeviceGetStreamPriorityRange(&least, &greatest), "stream priorities");
-    hipStream_t s = nullptr;
-    hip_ok(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, least), "side stream");
-    void* scratch = nullptr;
-    hip_ok(hipMalloc(&scratch, 256), "side stream scratch");
-    hip_ok(hipMemsetAsync(scratch, 0, 256, s), "bind side stream");
-    hip_ok(hipStreamSynchronize(s), "bind side stream");
-    hip_ok(hipFree(scratch), "side stream scratch");
-    return s;
-  }();
+  static hipStream_t side = bound_stream(false);
   return side;
 }
 
-void reserve_streams() { (void)reserved_side_stream(); }
+hipStream_t reserved_comm_stream() {
+  static hipStream_t comm = bound_stream(true);
+  return comm;
+}
+
+void reserve_streams() {
+  (void)reserved_side_stream();
+  (void)reserved_comm_stream();
+}
 
 bool stream_capturing(hipStream_t s) {
   hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
