@@ -18,6 +18,8 @@ from __future__ import annotations
 
 from typing import Optional
 
+import os
+
 import torch
 import torch.nn as nn
 
@@ -77,11 +79,15 @@ class TorchTrainer:
                  seq_len: int = 0, fused_sgd: bool = True):
         from ..ops.optim import FusedSGD
         torch.manual_seed(seed)
+        # MIOpen find mode for the CNN convolutions (CS744_CONV_BENCHMARK=1): time every solver
+        # once per shape instead of taking the heuristic pick (opt-in: for ResNet-50 the search ran
+        # for more than 3 minutes on MI355X before the first step finished)
+        if os.environ.get("CS744_CONV_BENCHMARK", "0") == "1":
+            torch.backends.cudnn.benchmark = True
         self.device, self.world, self.B = device, world, batch_size
         self.model_name = model
         self.module = build_model(model).to(device)
         self.is_lm = hasattr(self.module, "vocab_size")
-        import os
         self.channels_last = not self.is_lm and os.environ.get("CS744_CHANNELS_LAST", "0") == "1"
         if self.channels_last:
             self.module = self.module.to(memory_format=torch.channels_last)
