@@ -62,6 +62,11 @@ class Comm:
         """``out`` (on ``dst`` only) receives ``world * buf.numel()`` elements, rank-major."""
         raise NotImplementedError
 
+    def scatter_flat(self, buf: torch.Tensor, rows: Optional[torch.Tensor], src: int = 0) -> None:
+        """``buf`` receives row ``rank`` of ``rows`` (``world * buf.numel()`` elements, on ``src``
+        only)."""
+        raise NotImplementedError
+
     def send(self, buf: torch.Tensor, dst: int) -> None:
         raise NotImplementedError
 
@@ -113,6 +118,14 @@ class TorchComm(Comm):
             return
         lst = list(out.view(self.world_size, -1).unbind(0)) if self.rank == dst else None
         D.gather(buf, lst, dst=dst, group=self.group)
+
+    def scatter_flat(self, buf: torch.Tensor, rows: Optional[torch.Tensor], src: int = 0) -> None:
+        if self.world_size == 1:
+            if rows is not None:
+                buf.copy_(rows.reshape(-1)[:buf.numel()])
+            return
+        lst = list(rows.view(self.world_size, -1).unbind(0)) if self.rank == src else None
+        D.scatter(buf, lst, src=src, group=self.group)
 
     def send(self, buf: torch.Tensor, dst: int) -> None:
         D.isend(buf, dst, group=self.group).wait()

@@ -10,9 +10,9 @@ native C++ RCCL communicator):
 mode                reference                                                  pattern here
 ==================  =========================================================  ==============================
 ``gather_scatter``  part2a (`master/part2a/part2a.py:42-52`)                   per tensor: gather to rank 0,
-                                                                               mean on rank 0, send the mean
-                                                                               back (a scatter of N identical
-                                                                               shards == a broadcast)
+                                                                               mean on rank 0, scatter the
+                                                                               mean back (N identical shards,
+                                                                               as the reference does)
 ``p2p``             part2a_extra (`master/part2a/part2a_extra.py:41-58`)       per tensor star: rank 0 recvs
                                                                                from 1..N-1, averages, sends
                                                                                back; every message waited
@@ -84,12 +84,13 @@ class FlatGradSync:
             g = flat_grad[off:off + n]
             out = self._tmp(w * maxn, g)[:w * n] if r == self.root else None
             self.comm.gather_flat(g, out, self.root)
-            if r == self.root:
+            if r == self.root:  # the mean, then every gathered row overwritten by it: the scatter list
                 if g.is_cuda:
-                    _native().rows_mean(out, w, g)
+                    _native().rows_mean(out, w, g, True)
                 else:
                     torch.mean(out.view(w, n), 0, out=g)
-            self.comm.broadcast(g, self.root)
+                    out.view(w, n).copy_(g.expand(w, n))
+            self.comm.scatter_flat(g, out, self.root)
 
     def _p2p(self, flat_grad: torch.Tensor) -> None:
         w, r = self.comm.world_size, self.comm.rank

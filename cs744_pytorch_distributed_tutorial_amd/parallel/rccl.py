@@ -87,6 +87,10 @@ class RcclComm(Comm):
         self.native.gather(buf, out, dst)
         self.native.join()
 
+    def scatter_flat(self, buf: torch.Tensor, rows: Optional[torch.Tensor], src: int = 0) -> None:
+        self.native.scatter(rows if self.rank == src else None, buf, src)
+        self.native.join()
+
     def send(self, buf: torch.Tensor, dst: int) -> None:
         self.native.send(buf, dst)
         self.native.join()

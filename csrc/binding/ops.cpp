@@ -86,11 +86,13 @@ void sgd_multi(torch::Tensor table, int64_t ntens, int64_t nchunks, double lr, d
 }
 
 // part2a root combine: dst[n] = mean over rows of src[rows * n] (rank order)
-void rows_mean(torch::Tensor src, int64_t rows, torch::Tensor dst) {
+// (bcast: the mean is also written over every row of src)
+void rows_mean(torch::Tensor src, int64_t rows, torch::Tensor dst, bool bcast) {
   for (auto* t : {&src, &dst}) { CS_CHECK_CUDA(*t); CS_CHECK_F32(*t); CS_CHECK_CONTIG(*t); }
   TORCH_CHECK(rows >= 1 && src.numel() == rows * dst.numel(), "rows_mean: src must hold rows * dst.numel()");
   DevGuard gd(dst.device());
-  CS_LAUNCH(cs_rows_mean(src.data_ptr<float>(), (int)rows, dst.numel(), dst.data_ptr<float>(), cur_stream()));
+  CS_LAUNCH(cs_rows_mean(src.data_ptr<float>(), (int)rows, dst.numel(), dst.data_ptr<float>(), bcast ? 1 : 0,
+                         cur_stream()));
 }
 
 // part2a_extra root combine: g += t (then g /= div when div > 0)
@@ -160,7 +162,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("sgd_flat", &sgd_flat, "fused SGD on flat buffers");
   m.def("sgd_multi_table", &sgd_multi_table, "build the multi-tensor SGD table");
   m.def("sgd_multi", &sgd_multi, "multi-tensor fused SGD");
-  m.def("rows_mean", &rows_mean, "mean over the rows of a [rows, n] buffer (part2a root)");
+  m.def("rows_mean", &rows_mean, "mean over the rows of a [rows, n] buffer (part2a root)", pybind11::arg("src"),
+        pybind11::arg("rows"), pybind11::arg("dst"), pybind11::arg("bcast") = false);
   m.def("accumulate", &accumulate, "g += t, optionally then g /= div (part2a_extra root)");
   m.def("linear_xent", &linear_xent, "fused Linear + softmax cross-entropy fwd(+bwd)");
   m.def("softmax_xent", &softmax_xent, "softmax cross-entropy fwd+bwd");

@@ -3,7 +3,8 @@
 // on that path:
 //  * rows_mean — part2a's gather -> mean on the root (`master/part2a/part2a.py:42-52`):
 //    dst[i] = (sum_r src[r][i]) / rows, rows summed in rank order 0..rows-1 (fixed order: the
-//    root's result does not depend on the launch shape);
+//    root's result does not depend on the launch shape); optionally the mean is also written
+//    over every gathered row, which then is the scatter list the root sends back;
 //  * accumulate — part2a_extra's star on the root (`master/part2a/part2a_extra.py:41-58`):
 //    g += t for each received peer buffer, and on the last one g = (g + t) / div (the same two
 //    roundings as the reference's add then divide).
@@ -13,8 +14,10 @@
 
 namespace {
 
-__global__ __launch_bounds__(256) void rows_mean_kernel(const float* __restrict__ src, int rows, int64_t n,
-                                                        float* __restrict__ dst) {
+// bcast: also write the mean back over every row of src (the root's scatter list: every rank
+// receives the mean); each thread reads all rows of its elements before writing any of them
+__global__ __launch_bounds__(256) void rows_mean_kernel(float* __restrict__ src, int rows, int64_t n,
+                                                        float* __restrict__ dst, int bcast) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const float fr = (float)rows;
   const int64_t n4 = n >> 2;
@@ -24,12 +27,17 @@ __global__ __launch_bounds__(256) void rows_mean_kernel(const float* __restrict_
       const float4 v = reinterpret_cast<const float4*>(src + (int64_t)r * n)[i];
       s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
     }
-    reinterpret_cast<float4*>(dst)[i] = make_float4(s.x / fr, s.y / fr, s.z / fr, s.w / fr);
+    const float4 m = make_float4(s.x / fr, s.y / fr, s.z / fr, s.w / fr);
+    reinterpret_cast<float4*>(dst)[i] = m;
+    if (bcast)
+      for (int r = 0; r < rows; ++r) reinterpret_cast<float4*>(src + (int64_t)r * n)[i] = m;
   }
   for (int64_t i = (n4 << 2) + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     float s = src[i];
     for (int r = 1; r < rows; ++r) s += src[(int64_t)r * n + i];
     dst[i] = s / fr;
+    if (bcast)
+      for (int r = 0; r < rows; ++r) src[(int64_t)r * n + i] = s / fr;
   }
 }
 
@@ -58,9 +66,9 @@ int grid_for(int64_t n) {
 
 }  // namespace
 
-hipError_t cs_rows_mean(const float* src, int rows, int64_t n, float* dst, hipStream_t stream) {
+hipError_t cs_rows_mean(float* src, int rows, int64_t n, float* dst, int bcast, hipStream_t stream) {
   if (n <= 0 || rows <= 0) return hipSuccess;
-  hipLaunchKernelGGL(rows_mean_kernel, dim3(grid_for(n)), dim3(256), 0, stream, src, rows, n, dst);
+  hipLaunchKernelGGL(rows_mean_kernel, dim3(grid_for(n)), dim3(256), 0, stream, src, rows, n, dst, bcast);
   return hipGetLastError();
 }
 

@@ -26,7 +26,7 @@ hipError_t cs_sgd_flat(float* p, const float* g, float* m, int64_t n, float lr, 
                        float scale, int first, hipStream_t stream, int64_t* counter = nullptr);
 // faithful sync modes on flat gradients (flat_ops.hip): dst = mean over `rows` rows of src [rows][n];
 // g = g + t, then / div when div > 0
-hipError_t cs_rows_mean(const float* src, int rows, int64_t n, float* dst, hipStream_t stream);
+hipError_t cs_rows_mean(float* src, int rows, int64_t n, float* dst, int bcast, hipStream_t stream);
 hipError_t cs_accumulate(float* g, const float* t, int64_t n, float div, hipStream_t stream);
 hipError_t cs_sgd_multi(const CsTensorEntry* tab_dev, int ntens, const int64_t* chunk_start_dev, int nchunks,
                         float lr, float mom, float wd, float damp, float scale, int first, hipStream_t stream);

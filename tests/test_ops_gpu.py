@@ -119,6 +119,10 @@ def test_flat_sync_root_combines_match_torch(dev):
         _C.rows_mean(src, w, dst)
         ref = src.view(w, n).double().mean(0).float()
         torch.testing.assert_close(dst, ref, rtol=1e-6, atol=1e-7)
+        rows = src.clone()
+        dst2 = torch.empty(n, device="cuda")
+        _C.rows_mean(rows, w, dst2, True)  # the mean also over every row: the scatter list
+        assert torch.equal(dst2, dst) and torch.equal(rows.view(w, n), dst.expand(w, n))
         g = torch.randn(n, device="cuda")
         ts = [torch.randn(n, device="cuda") for _ in range(w - 1)]
         exp = g.clone()
