@@ -213,6 +213,12 @@ class NativeTrainer:
             init_state = VGG(model).state_dict()
         lay.pack(init_state, self.params, self.bufs, self.nbt)
 
+        # under rocprofv3 counter collection every dispatch is serialised, which a kernel stream
+        # link (a wait kernel spinning for another stream's signal) cannot survive: the
+        # communicators fork/join with HIP events instead (device_comm.h StreamBridge mode 0)
+        self._counters = bool(os.environ.get("ROCPROF_COUNTERS") or os.environ.get("ROCPROF_COUNTER_COLLECTION"))
+        if self._counters:
+            os.environ["CS_COMM_FORK"] = "0"
         # communicator + DDP construction-time sync (params + buffers from rank 0)
         self.comm = None
         self.comm_kind = comm if world > 1 else "none"
@@ -278,9 +284,8 @@ class NativeTrainer:
         # link wait would spin to its timeout waiting for a signal that cannot run.
         from .. import HW_QUEUES
         python_collectives = world > 1 and self.native_comm is None
-        counters = bool(os.environ.get("ROCPROF_COUNTERS") or os.environ.get("ROCPROF_COUNTER_COLLECTION"))
         self.overlap_wgrad = os.environ.get("CS_OVERLAP_WGRAD", "1") != "0" and not python_collectives and (
-            self.native_comm is None or HW_QUEUES >= 8) and not counters
+            self.native_comm is None or HW_QUEUES >= 8) and not self._counters
         self.engine.set_overlap_wgrad(self.overlap_wgrad)
         self.engine.set_data(0, self.train_data, self.train_labels, self.aug_train)
         self.engine.set_data(1, self.test_data, self.test_labels, self.aug_test)
