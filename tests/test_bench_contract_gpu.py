@@ -1,0 +1,35 @@
+"""bench.py's one-line JSON contract on an MI355X: the metric/config BASELINE.json names, the
+whole-job value consistent with ms_per_step, exactly the requested steps/warmup."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+pytestmark = [pytest.mark.gpu]
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_bench_json_line():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    r = subprocess.run([sys.executable, "bench.py", "--steps", "7", "--warmup", "3"], cwd=ROOT, capture_output=True,
+                       text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-1500:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    with open(os.path.join(ROOT, "BASELINE.json")) as f:
+        base = json.load(f)
+    assert d["metric"].startswith("images/sec (whole node) VGG-11 CIFAR-shape")
+    assert base["metric"].startswith(d["metric"])
+    assert d["unit"] == "images/s" and d["n_gpus"] == 1 and d["steps"] == 7 and d["warmup"] == 3
+    assert d["higher_is_better"] is True and d["scaling"] == "weak" and d["dtype"] == "fp32"
+    assert "synthetic" in d["data"]
+    c = d["config"]
+    assert c["model"] == "VGG11" and c["global_batch"] == 64 and c["parallelism"] == "dp1" and c["seq_len"] is None
+    assert d["value"] > 0 and abs(d["value"] - 64 * 1e3 / d["ms_per_step"]) / d["value"] < 1e-3
+    assert d["vs_baseline"] == pytest.approx(d["value"] / 554.0, rel=1e-2)
