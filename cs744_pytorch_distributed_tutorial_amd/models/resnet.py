@@ -9,9 +9,18 @@ layout of the widely used ImageNet implementation (``conv1``, ``bn1``,
 interchangeable with it. ResNet-50 has 25,557,032 parameters (97.5 MiB of fp32
 gradients per step — the all-reduce payload of the scaling benchmark).
 
-MI355X notes: every BatchNorm with its ReLU and the bottleneck's residual add is one fused
-gfx950 pass forward and two backward (``ops.cnn.bn_act``, ``csrc/kernels/bn_nchw.hip``) on
-NCHW activations, fp32 or bf16 under autocast; convolutions are MIOpen's. Trained by
+MI355X notes: two layouts, one parameter set.
+
+* ``layout="nhwc"`` (default on GPU): activations stay channels-last end to end and every
+  layer is the framework's (``ops.cnn_nhwc``): each convolution one hipBLASLt GEMM on the
+  matrix cores (1x1: the activation itself; k x k / strided: a gfx950 im2col gather, and the
+  gather-style col2im in the backward), BatchNorm (+ residual) (+ ReLU) and the stem's max-pool
+  gfx950 kernels (``csrc/kernels/cnn_nhwc.hip``) — no layout transposes in the step.
+* ``layout="nchw"``: MIOpen convolutions, with every BatchNorm + ReLU (+ the bottleneck's
+  residual add) one fused gfx950 pass forward and two backward (``ops.cnn.bn_act``,
+  ``csrc/kernels/bn_nchw.hip``). CPU runs always take this layout.
+
+fp32, or bf16 under autocast (fp32 master weights and BN statistics). Trained by
 ``parallel.ddp.DistributedDataParallel`` (flat bucketed gradients, RCCL all-reduce overlapped
 with backward) and ``ops.optim.FusedSGD`` (one HIP launch per step).
 """
@@ -23,6 +32,7 @@ import torch
 import torch.nn as nn
 
 from ..ops.cnn import bn_act, max_pool3s2
+from ..ops.cnn_nhwc import act_dtype, bn_act_nhwc, conv_nhwc, max_pool3s2_nhwc, to_nhwc
 
 
 def conv3x3(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
@@ -36,6 +46,10 @@ def conv1x1(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
 def _downsample(ds: nn.Sequential, x: torch.Tensor) -> torch.Tensor:
     """the projection shortcut: conv1x1 + BN (no ReLU), the BN through the fused kernel"""
     return bn_act(ds[1], ds[0](x), relu=False)
+
+
+def _downsample_nhwc(ds: nn.Sequential, x: torch.Tensor) -> torch.Tensor:
+    return bn_act_nhwc(ds[1], conv_nhwc(x, ds[0]), relu=False)
 
 
 class BasicBlock(nn.Module):
@@ -54,6 +68,11 @@ class BasicBlock(nn.Module):
         idt = x if self.downsample is None else _downsample(self.downsample, x)
         y = bn_act(self.bn1, self.conv1(x))
         return bn_act(self.bn2, self.conv2(y), residual=idt)
+
+    def forward_nhwc(self, x: torch.Tensor) -> torch.Tensor:
+        idt = x if self.downsample is None else _downsample_nhwc(self.downsample, x)
+        y = bn_act_nhwc(self.bn1, conv_nhwc(x, self.conv1))
+        return bn_act_nhwc(self.bn2, conv_nhwc(y, self.conv2), residual=idt)
 
 
 class Bottleneck(nn.Module):
@@ -76,11 +95,19 @@ class Bottleneck(nn.Module):
         y = bn_act(self.bn2, self.conv2(y))
         return bn_act(self.bn3, self.conv3(y), residual=idt)
 
+    def forward_nhwc(self, x: torch.Tensor) -> torch.Tensor:
+        idt = x if self.downsample is None else _downsample_nhwc(self.downsample, x)
+        y = bn_act_nhwc(self.bn1, conv_nhwc(x, self.conv1))
+        y = bn_act_nhwc(self.bn2, conv_nhwc(y, self.conv2))
+        return bn_act_nhwc(self.bn3, conv_nhwc(y, self.conv3), residual=idt)
+
 
 class ResNet(nn.Module):
     def __init__(self, block: Type[Union[BasicBlock, Bottleneck]], layers: List[int], num_classes: int = 1000,
-                 zero_init_residual: bool = False):
+                 zero_init_residual: bool = False, layout: str = "nhwc"):
         super().__init__()
+        assert layout in ("nhwc", "nchw"), layout
+        self.layout = layout
         self.inplanes = 64
         self.conv1 = nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False)
         self.bn1 = nn.BatchNorm2d(64)
@@ -115,22 +142,33 @@ class ResNet(nn.Module):
         return nn.Sequential(*layers)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if self.layout == "nhwc" and x.is_cuda:
+            return self.forward_nhwc(x)
         x = max_pool3s2(bn_act(self.bn1, self.conv1(x)))  # self.maxpool's op, on the gfx950 kernel
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         return self.fc(torch.flatten(self.avgpool(x), 1))
 
-
-def resnet18(num_classes: int = 1000) -> ResNet:
-    return ResNet(BasicBlock, [2, 2, 2, 2], num_classes)
-
-
-def resnet34(num_classes: int = 1000) -> ResNet:
-    return ResNet(BasicBlock, [3, 4, 6, 3], num_classes)
-
-
-def resnet50(num_classes: int = 1000) -> ResNet:
-    return ResNet(Bottleneck, [3, 4, 6, 3], num_classes)
+    def forward_nhwc(self, x: torch.Tensor) -> torch.Tensor:
+        """the same network on channels-last activations (input: [B, 3, H, W], any memory format)"""
+        x = to_nhwc(x, act_dtype(x))
+        x = max_pool3s2_nhwc(bn_act_nhwc(self.bn1, conv_nhwc(x, self.conv1)))
+        for layer in (self.layer1, self.layer2, self.layer3, self.layer4):
+            for blk in layer:
+                x = blk.forward_nhwc(x)
+        return self.fc(x.mean(dim=(1, 2)))
 
 
-def resnet101(num_classes: int = 1000) -> ResNet:
-    return ResNet(Bottleneck, [3, 4, 23, 3], num_classes)
+def resnet18(num_classes: int = 1000, layout: str = "nhwc") -> ResNet:
+    return ResNet(BasicBlock, [2, 2, 2, 2], num_classes, layout=layout)
+
+
+def resnet34(num_classes: int = 1000, layout: str = "nhwc") -> ResNet:
+    return ResNet(BasicBlock, [3, 4, 6, 3], num_classes, layout=layout)
+
+
+def resnet50(num_classes: int = 1000, layout: str = "nhwc") -> ResNet:
+    return ResNet(Bottleneck, [3, 4, 6, 3], num_classes, layout=layout)
+
+
+def resnet101(num_classes: int = 1000, layout: str = "nhwc") -> ResNet:
+    return ResNet(Bottleneck, [3, 4, 23, 3], num_classes, layout=layout)

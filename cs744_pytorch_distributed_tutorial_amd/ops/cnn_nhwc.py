@@ -1,0 +1,154 @@
+"""Channels-last (NHWC) convolution, BatchNorm(+residual)(+ReLU) and 3x3/2 max-pool for the
+ResNet family's native path (``csrc/kernels/cnn_nhwc.hip``; models/resnet.py ``layout="nhwc"``).
+
+Activations are contiguous ``[B, H, W, C]`` tensors (fp32, or bf16 under autocast). A
+convolution is one GEMM on MI355X's matrix cores (hipBLASLt via ``torch.mm``):
+
+* 1x1 / stride 1: the activation *is* the ``[B*H*W, Cin]`` operand, no copy;
+* anything else (3x3, the 7x7 stem, strided 1x1 shortcuts): the gfx950 ``im2col_nhwc`` gather
+  builds ``[B*Ho*Wo, Kp]`` (columns ordered (r, s, c), K padded to a 16-byte multiple), kept
+  for the weight gradient; the data gradient is ``dcol = dy @ W`` folded back by the
+  gather-style ``col2im_nhwc`` (deterministic, no atomics).
+
+No NCHW<->NHWC transposes anywhere in the step (MIOpen's NCHW path spends ~20 % of a ResNet-50
+bf16 step in them, ``profiles/r2_resnet50_bf16_kernels.txt``). BatchNorm follows
+``nn.BatchNorm2d`` training semantics (batch statistics, biased variance for normalisation,
+unbiased for the running variance, ``num_batches_tracked`` += 1); eval mode and CPU tensors use
+the module's running statistics through plain torch ops.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import native
+
+
+def act_dtype(x: torch.Tensor) -> torch.dtype:
+    """bf16 under CUDA autocast (its dtype), else the input's dtype"""
+    if x.is_cuda and torch.is_autocast_enabled("cuda"):
+        return torch.get_autocast_dtype("cuda")
+    return x.dtype
+
+
+def to_nhwc(x: torch.Tensor, dtype: Optional[torch.dtype] = None) -> torch.Tensor:
+    """[B, C, H, W] (any memory format) -> contiguous [B, H, W, C]"""
+    x = x.permute(0, 2, 3, 1)
+    return x.to(dtype).contiguous() if dtype is not None else x.contiguous()
+
+
+def _kpad(k: int, dtype: torch.dtype) -> int:
+    v = 8 if dtype == torch.bfloat16 else 4
+    return (k + v - 1) // v * v
+
+
+class _ConvNHWC(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, stride: int, pad: int):
+        B, H, W, C = x.shape
+        Co, Ci, R, S = weight.shape
+        assert Ci == C, f"conv_nhwc: {C} input channels for a {Ci}-channel weight"
+        Ho, Wo = (H + 2 * pad - R) // stride + 1, (W + 2 * pad - S) // stride + 1
+        K = R * S * C
+        wf = weight.permute(0, 2, 3, 1).reshape(Co, K).to(x.dtype)  # [Co, K], columns (r, s, c)
+        direct = R == 1 and S == 1 and stride == 1 and pad == 0
+        if direct:
+            col = x.view(B * H * W, C)
+        else:
+            Kp = _kpad(K, x.dtype)
+            col = native.C().im2col_nhwc(x, R, S, stride, pad, Kp)
+            if Kp != K:
+                wf = F.pad(wf, (0, Kp - K))
+        wf = wf.contiguous()
+        with torch.autocast("cuda", enabled=False):
+            y = torch.mm(col, wf.t())
+        ctx.save_for_backward(col, wf)
+        ctx.geo = (B, H, W, C, Co, R, S, stride, pad, K, direct)
+        ctx.wdtype = weight.dtype
+        return y.view(B, Ho, Wo, Co)
+
+    @staticmethod
+    def backward(ctx, dy):
+        col, wf = ctx.saved_tensors
+        B, H, W, C, Co, R, S, stride, pad, K, direct = ctx.geo
+        dy2 = dy.reshape(-1, Co)
+        if not dy2.is_contiguous():
+            dy2 = dy2.contiguous()
+        dx = dw = None
+        with torch.autocast("cuda", enabled=False):
+            if ctx.needs_input_grad[1]:
+                dwf = torch.mm(dy2.t(), col)  # [Co, Kp]
+                dw = dwf[:, :K].reshape(Co, R, S, C).permute(0, 3, 1, 2).to(ctx.wdtype).contiguous()
+            if ctx.needs_input_grad[0]:
+                dcol = torch.mm(dy2, wf)  # [M, Kp]
+                dx = dcol.view(B, H, W, C) if direct else native.C().col2im_nhwc(dcol, B, H, W, C, R, S, stride, pad)
+        return dx, dw, None, None
+
+
+def conv_nhwc(x: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
+    """``conv(x)`` for a bias-free, ungrouped, undilated Conv2d on a [B, H, W, C] tensor"""
+    assert conv.bias is None and conv.groups == 1 and conv.dilation == (1, 1), "conv_nhwc: unsupported Conv2d"
+    assert conv.stride[0] == conv.stride[1] and conv.padding[0] == conv.padding[1], "conv_nhwc: square stride/pad"
+    if not x.is_cuda:
+        y = F.conv2d(x.permute(0, 3, 1, 2), conv.weight.to(x.dtype), None, conv.stride, conv.padding)
+        return y.permute(0, 2, 3, 1).contiguous()
+    return _ConvNHWC.apply(x, conv.weight, int(conv.stride[0]), int(conv.padding[0]))
+
+
+class _BnActNHWC(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, residual, running_mean, running_var, nbt, momentum, eps, relu):
+        y, stat = native.C().bn_nhwc_fwd(x, residual, weight, bias, running_mean, running_var, nbt, momentum, eps, relu)
+        ctx.save_for_backward(x, residual, weight, stat)
+        ctx.relu = relu
+        ctx.has_res = residual is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, residual, weight, stat = ctx.saved_tensors
+        dx, dres, dw, db = native.C().bn_nhwc_bwd(dy.contiguous(), x, residual, weight, stat, ctx.relu, ctx.has_res)
+        return (dx, dw, db, dres if ctx.has_res else None, None, None, None, None, None, None)
+
+
+def bn_act_nhwc(bn: nn.BatchNorm2d, x: torch.Tensor, relu: bool = True,
+                residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``relu(bn(x) + residual)`` on [B, H, W, C] activations"""
+    if (bn.training and bn.track_running_stats and bn.momentum is not None and bn.affine and x.is_cuda
+            and x.dtype in (torch.float32, torch.bfloat16) and x.shape[0] * x.shape[1] * x.shape[2] > 1):
+        if residual is not None:
+            residual = residual.contiguous()
+        return _BnActNHWC.apply(x.contiguous(), bn.weight, bn.bias, residual, bn.running_mean, bn.running_var,
+                                bn.num_batches_tracked, float(bn.momentum), float(bn.eps), relu)
+    if bn.training:  # CPU training: the module itself on an NCHW view
+        y = bn(x.permute(0, 3, 1, 2)).permute(0, 2, 3, 1)
+    else:
+        scale = bn.weight * torch.rsqrt(bn.running_var + bn.eps)
+        y = x * scale.to(x.dtype) + (bn.bias - bn.running_mean * scale).to(x.dtype)
+    if residual is not None:
+        y = y + residual
+    return (F.relu(y) if relu else y).contiguous()
+
+
+class _MaxPoolNHWC(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        y, pos = native.C().maxpool3s2_nhwc_fwd(x)
+        ctx.save_for_backward(pos)
+        ctx.hw = (x.shape[1], x.shape[2])
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (pos,) = ctx.saved_tensors
+        return native.C().maxpool3s2_nhwc_bwd(dy.contiguous(), pos, *ctx.hw)
+
+
+def max_pool3s2_nhwc(x: torch.Tensor) -> torch.Tensor:
+    """``F.max_pool2d(., 3, 2, 1)`` on a [B, H, W, C] tensor"""
+    if x.is_cuda and x.dtype in (torch.float32, torch.bfloat16):
+        return _MaxPoolNHWC.apply(x.contiguous())
+    return F.max_pool2d(x.permute(0, 3, 1, 2), 3, 2, 1).permute(0, 2, 3, 1).contiguous()

@@ -8,10 +8,13 @@ framework's own data-parallel runtime around them.
   ``RcclComm`` (``comm="rccl"``) or ProcessGroupNCCL (``comm="torch"``);
   or any explicit strategy of ``parallel.sync`` (part2a / part2a_extra / part2b);
 * optimizer = ``ops.optim.FusedSGD`` (one multi-tensor HIP launch per step);
-* CNNs run NCHW by default: measured on MI355X (torch 2.10+rocm7.0, MIOpen FAST find) the
-  channels_last (NHWC) ResNet-50 step is 10-18x SLOWER (its composable_kernel weight-gradient
-  kernels take up to 225 ms each; 210 vs 1923 img/s bf16, 115 vs 2131 img/s fp32), so NHWC
-  is opt-in (``CS744_CHANNELS_LAST=1``); optionally under bf16 autocast (``dtype="bf16"``; master weights and the optimizer stay fp32);
+* ResNets run the framework's channels-last path by default (``models.resnet`` ``layout="nhwc"``:
+  hipBLASLt GEMM convolutions over gfx950 im2col / BatchNorm / pool kernels, no MIOpen);
+  ``CS744_RESNET_LAYOUT=nchw`` selects MIOpen convolutions on NCHW with the fused NCHW
+  BatchNorm kernels. MIOpen's own channels_last kernels (``CS744_CHANNELS_LAST=1`` with the
+  NCHW layout) measured 10-18x SLOWER on MI355X (torch 2.10+rocm7.0: composable_kernel
+  weight-gradient kernels up to 225 ms each). Optionally under bf16 autocast
+  (``dtype="bf16"``; master weights and the optimizer stay fp32);
 * data = device-resident synthetic batches of the named shape (no host traffic).
 """
 from __future__ import annotations
@@ -32,7 +35,7 @@ def build_model(name: str) -> nn.Module:
     if n.startswith("vgg"):
         return vgg.VGG(n.upper())
     if n in ("resnet18", "resnet34", "resnet50", "resnet101"):
-        return getattr(resnet, n)()
+        return getattr(resnet, n)(layout=os.environ.get("CS744_RESNET_LAYOUT", "nhwc"))
     if n.startswith("llama") or n.startswith("decoder"):
         from ..models import llama
         return llama.build(name.lower())
@@ -109,8 +112,10 @@ class TorchTrainer:
         else:
             shape = (3, 32, 32) if model.lower().startswith("vgg") else (3, 224, 224)
             classes = 10 if model.lower().startswith("vgg") else 1000
+            # the NHWC ResNet reads the batch channels-last (its permute to [B, H, W, C] is then free)
+            nhwc = getattr(self.module, "layout", "nchw") == "nhwc"
             self.data = SyntheticBatches("image", batch_size, device, shape=shape, classes=classes, seed=seed,
-                                         channels_last=self.channels_last)
+                                         channels_last=self.channels_last or nhwc)
         self.loss: Optional[torch.Tensor] = None
 
     def step(self) -> None:

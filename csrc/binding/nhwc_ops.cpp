@@ -1,0 +1,167 @@
+// torch bindings of the channels-last CNN kernels (csrc/kernels/cnn_nhwc.hip). Activations are
+// contiguous [B, H, W, C] fp32 / bf16 GPU tensors; shapes, dtypes and the vector-width
+// preconditions are validated here, before any launch.
+#include "binding/torch_util.h"
+#include "kernels/launchers.h"
+
+namespace {
+
+using csb::cur_stream;
+using csb::DevGuard;
+
+int act_dt(const torch::Tensor& t, const char* who) {
+  if (t.scalar_type() == at::kFloat) return CS_F32;
+  if (t.scalar_type() == at::kBFloat16) return CS_BF16;
+  TORCH_CHECK(false, who, ": activations must be float32 or bfloat16, got ", t.scalar_type());
+  return -1;
+}
+
+void check_nhwc(const torch::Tensor& t, const char* who) {
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.dim() == 4, who, ": expected a contiguous [B, H, W, C] GPU tensor");
+}
+
+void check_like(const torch::Tensor& t, const torch::Tensor& like, const char* n) {
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.sizes() == like.sizes() && t.scalar_type() == like.scalar_type(),
+              n, " must be a contiguous [B, H, W, C] GPU tensor shaped and typed like x");
+}
+
+void check_param(const c10::optional<torch::Tensor>& t, int64_t C, const char* n) {
+  if (!t.has_value() || !t->defined()) return;
+  TORCH_CHECK(t->is_cuda() && t->is_contiguous() && t->scalar_type() == at::kFloat && t->numel() == C, n,
+              " must be a contiguous float32 GPU tensor of C elements");
+}
+
+template <typename T>
+T* opt_ptr(const c10::optional<torch::Tensor>& t) {
+  return t.has_value() && t->defined() ? t->data_ptr<T>() : nullptr;
+}
+
+// -> {y, stat [4, C] = scale, shift, mean, invstd}
+std::vector<torch::Tensor> bn_nhwc_fwd(torch::Tensor x, c10::optional<torch::Tensor> res,
+                                       c10::optional<torch::Tensor> w, c10::optional<torch::Tensor> b,
+                                       c10::optional<torch::Tensor> rm, c10::optional<torch::Tensor> rv,
+                                       c10::optional<torch::Tensor> nbt, double momentum, double eps, bool relu) {
+  check_nhwc(x, "bn_nhwc_fwd");
+  const int dt = act_dt(x, "bn_nhwc_fwd");
+  const int64_t C = x.size(3), M = x.numel() / C;
+  TORCH_CHECK(M > 0 && C > 0, "bn_nhwc_fwd: empty input");
+  const bool has_res = res.has_value() && res->defined();
+  if (has_res) check_like(*res, x, "res");
+  check_param(w, C, "weight");
+  check_param(b, C, "bias");
+  check_param(rm, C, "running_mean");
+  check_param(rv, C, "running_var");
+  TORCH_CHECK(rm.has_value() == rv.has_value(), "bn_nhwc_fwd: running mean and var go together");
+  if (nbt.has_value())
+    TORCH_CHECK(nbt->is_cuda() && nbt->scalar_type() == at::kLong && nbt->numel() == 1, "bn_nhwc_fwd: num_batches_tracked");
+  DevGuard g(x.device());
+  auto fo = x.options().dtype(at::kFloat);
+  auto y = torch::empty_like(x);
+  auto stat = torch::empty({4, C}, fo);
+  auto part = torch::empty({cs_bn_nhwc_partials(M, (int)C, dt)}, fo);
+  CS_LAUNCH(cs_bn_nhwc_fwd(dt, x.data_ptr(), has_res ? res->data_ptr() : nullptr, opt_ptr<float>(w), opt_ptr<float>(b),
+                           opt_ptr<float>(rm), opt_ptr<float>(rv), opt_ptr<int64_t>(nbt), (float)momentum, (float)eps,
+                           relu ? 1 : 0, y.data_ptr(), stat.data_ptr<float>(), part.data_ptr<float>(), M, (int)C,
+                           cur_stream()));
+  return {y, stat};
+}
+
+// -> {dx, dres (or undefined), dweight, dbias}
+std::vector<torch::Tensor> bn_nhwc_bwd(torch::Tensor dy, torch::Tensor x, c10::optional<torch::Tensor> res,
+                                       c10::optional<torch::Tensor> w, torch::Tensor stat, bool relu, bool need_dres) {
+  check_nhwc(x, "bn_nhwc_bwd");
+  const int dt = act_dt(x, "bn_nhwc_bwd");
+  check_like(dy, x, "dy");
+  const bool has_res = res.has_value() && res->defined();
+  if (has_res) check_like(*res, x, "res");
+  const int64_t C = x.size(3), M = x.numel() / C;
+  check_param(w, C, "weight");
+  TORCH_CHECK(stat.is_cuda() && stat.scalar_type() == at::kFloat && stat.numel() == 4 * C, "bn_nhwc_bwd: stat");
+  DevGuard g(x.device());
+  auto fo = x.options().dtype(at::kFloat);
+  auto dx = torch::empty_like(x);
+  torch::Tensor dres = need_dres ? torch::empty_like(x) : torch::Tensor();
+  auto dw = torch::empty({C}, fo), db = torch::empty({C}, fo);
+  auto coef = torch::empty({3, C}, fo);
+  auto part = torch::empty({cs_bn_nhwc_partials(M, (int)C, dt)}, fo);
+  CS_LAUNCH(cs_bn_nhwc_bwd(dt, dy.data_ptr(), x.data_ptr(), has_res ? res->data_ptr() : nullptr, opt_ptr<float>(w),
+                           stat.data_ptr<float>(), relu ? 1 : 0, dx.data_ptr(), need_dres ? dres.data_ptr() : nullptr,
+                           dw.data_ptr<float>(), db.data_ptr<float>(), coef.data_ptr<float>(), part.data_ptr<float>(),
+                           M, (int)C, cur_stream()));
+  return {dx, dres, dw, db};
+}
+
+// 3x3 / 2 pad-1 max-pool -> {y, pos (uint8 window position per output element)}
+std::vector<torch::Tensor> maxpool3s2_nhwc_fwd(torch::Tensor x) {
+  check_nhwc(x, "maxpool3s2_nhwc_fwd");
+  const int dt = act_dt(x, "maxpool3s2_nhwc_fwd");
+  const int64_t B = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int64_t Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+  DevGuard g(x.device());
+  auto y = torch::empty({B, Ho, Wo, C}, x.options());
+  auto pos = torch::empty({B, Ho, Wo, C}, x.options().dtype(at::kByte));
+  CS_LAUNCH(cs_maxpool3s2_nhwc_fwd(dt, x.data_ptr(), y.data_ptr(), pos.data_ptr<uint8_t>(), (int)B, (int)H, (int)W,
+                                   (int)C, (int)Ho, (int)Wo, cur_stream()));
+  return {y, pos};
+}
+
+torch::Tensor maxpool3s2_nhwc_bwd(torch::Tensor dy, torch::Tensor pos, int64_t H, int64_t W) {
+  check_nhwc(dy, "maxpool3s2_nhwc_bwd");
+  const int dt = act_dt(dy, "maxpool3s2_nhwc_bwd");
+  TORCH_CHECK(pos.sizes() == dy.sizes() && pos.scalar_type() == at::kByte && pos.is_contiguous(),
+              "maxpool3s2_nhwc_bwd: pos must match dy");
+  TORCH_CHECK(dy.size(1) == (H - 1) / 2 + 1 && dy.size(2) == (W - 1) / 2 + 1, "maxpool3s2_nhwc_bwd: input size");
+  DevGuard g(dy.device());
+  auto dx = torch::empty({dy.size(0), H, W, dy.size(3)}, dy.options());
+  CS_LAUNCH(cs_maxpool3s2_nhwc_bwd(dt, dy.data_ptr(), pos.data_ptr<uint8_t>(), dx.data_ptr(), (int)dy.size(0), (int)H,
+                                   (int)W, (int)dy.size(3), (int)dy.size(1), (int)dy.size(2), cur_stream()));
+  return dx;
+}
+
+int vec_of(int64_t C, int dt) {
+  const int v16 = dt == CS_BF16 ? 8 : 4;
+  if (C % v16 == 0) return v16;
+  return C % 4 == 0 ? 4 : 1;
+}
+
+// x [B, H, W, C] -> col [B*Ho*Wo, Kp] (Kp >= R*S*C, a multiple of the channel vector width)
+torch::Tensor im2col_nhwc(torch::Tensor x, int64_t R, int64_t S, int64_t stride, int64_t pad, int64_t Kp) {
+  check_nhwc(x, "im2col_nhwc");
+  const int dt = act_dt(x, "im2col_nhwc");
+  const int64_t B = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  TORCH_CHECK(R > 0 && S > 0 && stride > 0 && pad >= 0 && Kp >= R * S * C && Kp % vec_of(C, dt) == 0,
+              "im2col_nhwc: bad geometry");
+  const int64_t Ho = (H + 2 * pad - R) / stride + 1, Wo = (W + 2 * pad - S) / stride + 1;
+  TORCH_CHECK(Ho > 0 && Wo > 0, "im2col_nhwc: empty output");
+  DevGuard g(x.device());
+  auto col = torch::empty({B * Ho * Wo, Kp}, x.options());
+  CS_LAUNCH(cs_im2col_nhwc(dt, x.data_ptr(), col.data_ptr(), (int)B, (int)H, (int)W, (int)C, (int)R, (int)S,
+                           (int)stride, (int)pad, (int)Ho, (int)Wo, (int)Kp, cur_stream()));
+  return col;
+}
+
+// dcol [B*Ho*Wo, Kp] -> dx [B, H, W, C] (the adjoint of im2col_nhwc)
+torch::Tensor col2im_nhwc(torch::Tensor dcol, int64_t B, int64_t H, int64_t W, int64_t C, int64_t R, int64_t S,
+                          int64_t stride, int64_t pad) {
+  TORCH_CHECK(dcol.is_cuda() && dcol.is_contiguous() && dcol.dim() == 2, "col2im_nhwc: dcol must be a contiguous 2-D GPU tensor");
+  const int dt = act_dt(dcol, "col2im_nhwc");
+  const int64_t Ho = (H + 2 * pad - R) / stride + 1, Wo = (W + 2 * pad - S) / stride + 1, Kp = dcol.size(1);
+  TORCH_CHECK(R > 0 && S > 0 && stride > 0 && pad >= 0 && Ho > 0 && Wo > 0, "col2im_nhwc: bad geometry");
+  TORCH_CHECK(dcol.size(0) == B * Ho * Wo && Kp >= R * S * C && Kp % vec_of(C, dt) == 0, "col2im_nhwc: dcol shape");
+  DevGuard g(dcol.device());
+  auto dx = torch::empty({B, H, W, C}, dcol.options());
+  CS_LAUNCH(cs_col2im_nhwc(dt, dcol.data_ptr(), dx.data_ptr(), (int)B, (int)H, (int)W, (int)C, (int)R, (int)S,
+                           (int)stride, (int)pad, (int)Ho, (int)Wo, (int)Kp, cur_stream()));
+  return dx;
+}
+
+}  // namespace
+
+void register_nhwc_ops(pybind11::module& m) {
+  m.def("bn_nhwc_fwd", &bn_nhwc_fwd, "training BatchNorm2d (+residual) (+ReLU), NHWC fp32/bf16 -> (y, stat)");
+  m.def("bn_nhwc_bwd", &bn_nhwc_bwd, "its backward -> (dx, dres, dweight, dbias)");
+  m.def("maxpool3s2_nhwc_fwd", &maxpool3s2_nhwc_fwd, "3x3/2 pad-1 max-pool, NHWC -> (y, window position)");
+  m.def("maxpool3s2_nhwc_bwd", &maxpool3s2_nhwc_bwd, "its gather-style backward");
+  m.def("im2col_nhwc", &im2col_nhwc, "NHWC im2col -> [B*Ho*Wo, Kp], columns (r, s, c)");
+  m.def("col2im_nhwc", &col2im_nhwc, "adjoint of im2col_nhwc (gather, deterministic)");
+}

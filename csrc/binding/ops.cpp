@@ -155,6 +155,7 @@ void register_conv_ops(pybind11::module& m);
 void register_runtime(pybind11::module& m);
 void register_lm_ops(pybind11::module& m);
 void register_cnn_ops(pybind11::module& m);
+void register_nhwc_ops(pybind11::module& m);
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "gfx950 (MI355X) kernels + native runtime for cs744_pytorch_distributed_tutorial_amd";
@@ -171,4 +172,5 @@ PYBIND11_MODULE(_C, m) {
   register_runtime(m);
   register_lm_ops(m);
   register_cnn_ops(m);
+  register_nhwc_ops(m);
 }

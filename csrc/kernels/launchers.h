@@ -207,3 +207,21 @@ hipError_t cs_maxpool3s2_bwd(int dt, const void* dy, const unsigned char* pos, v
                              int Ho, int Wo, hipStream_t stream);
 hipError_t cs_rope(int dt, const void* x, const float* cosv, const float* sinv, void* out, int B, int S, int H, int hd,
                    int inverse, hipStream_t s);
+// channels-last (NHWC) CNN kernels (cnn_nhwc.hip), fp32 / bf16 activations, M = B*H*W rows of C.
+// BatchNorm: stat / coef / part exactly as the NCHW kernels above (part: cs_bn_nhwc_partials floats).
+int cs_bn_nhwc_partials(int64_t M, int C, int dt);
+hipError_t cs_bn_nhwc_fwd(int dt, const void* x, const void* res, const float* w, const float* b, float* rm, float* rv,
+                          int64_t* nbt, float momentum, float eps, int relu, void* y, float* stat, float* part,
+                          int64_t M, int C, hipStream_t stream);
+hipError_t cs_bn_nhwc_bwd(int dt, const void* dy, const void* x, const void* res, const float* w, const float* stat,
+                          int relu, void* dx, void* dres, float* dw, float* db, float* coef, float* part, int64_t M,
+                          int C, hipStream_t stream);
+hipError_t cs_maxpool3s2_nhwc_fwd(int dt, const void* x, void* y, unsigned char* pos, int B, int H, int W, int C,
+                                  int Ho, int Wo, hipStream_t stream);
+hipError_t cs_maxpool3s2_nhwc_bwd(int dt, const void* dy, const unsigned char* pos, void* dx, int B, int H, int W,
+                                  int C, int Ho, int Wo, hipStream_t stream);
+// col: [B*Ho*Wo, Kp], columns (r*S + s)*C + c, zero for k >= R*S*C; col2im is its adjoint (gather)
+hipError_t cs_im2col_nhwc(int dt, const void* x, void* col, int B, int H, int W, int C, int R, int S, int stride,
+                          int pad, int Ho, int Wo, int Kp, hipStream_t stream);
+hipError_t cs_col2im_nhwc(int dt, const void* dcol, void* dx, int B, int H, int W, int C, int R, int S, int stride,
+                          int pad, int Ho, int Wo, int Kp, hipStream_t stream);

@@ -1,0 +1,13 @@
+# round-2: channels-last ResNet path — its GPU tests, then ResNet-50 B=128 bench (nhwc vs nchw, bf16 / fp32)
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest tests/test_cnn_nhwc_gpu.py tests/test_bn_nchw_gpu.py -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/pytest_nhwc.log 2>&1
+rc=$?; echo "pytest exit $rc"; tail -15 gpurun_out/pytest_nhwc.log
+[ $rc -eq 0 ] || exit $rc
+for lay in nhwc nchw; do
+  for dt in bf16 fp32; do
+    CS744_RESNET_LAYOUT=$lay timeout -k 10 300 python bench.py --model resnet50 --dtype $dt --steps 10 --warmup 3 > gpurun_out/bench_rn50_${lay}_${dt}.log 2>&1 || exit $?
+    echo "$lay $dt: $(tail -1 gpurun_out/bench_rn50_${lay}_${dt}.log | cut -c1-200)"
+  done
+done

@@ -84,8 +84,8 @@ def test_resnet_native_bn_matches_module_path(dev, monkeypatch):
     from cs744_pytorch_distributed_tutorial_amd.models.resnet import resnet18
     from cs744_pytorch_distributed_tutorial_amd.ops import cnn
     torch.manual_seed(0)
-    a = resnet18(num_classes=10).to(dev)
-    b = resnet18(num_classes=10).to(dev)
+    a = resnet18(num_classes=10, layout="nchw").to(dev)
+    b = resnet18(num_classes=10, layout="nchw").to(dev)
     b.load_state_dict(a.state_dict())
     x = torch.randn(4, 3, 64, 64, device=dev)
     ya = a(x)

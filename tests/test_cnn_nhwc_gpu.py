@@ -1,0 +1,184 @@
+"""Channels-last CNN path (csrc/kernels/cnn_nhwc.hip, ops/cnn_nhwc.py) against plain PyTorch
+fp64/fp32 references: convolution through im2col + GEMM (forward, data and weight gradients)
+for every geometry ResNet uses, training BatchNorm (+residual) (+ReLU) with running statistics,
+the 3x3/2 max-pool, bitwise run-to-run determinism, and a whole ResNet-18 step against the
+NCHW module path."""
+import pytest
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from cs744_pytorch_distributed_tutorial_amd.ops import native
+    native.C()
+    return torch.device("cuda", 0)
+
+
+def nhwc(x):
+    return x.permute(0, 2, 3, 1).contiguous()
+
+
+def nchw(x):
+    return x.permute(0, 3, 1, 2)
+
+
+# (B, Cin, H, W, Cout, k, stride, pad): every ResNet geometry (stem, 1x1, strided 1x1, 3x3, 3x3/2)
+CONVS = [(2, 3, 32, 32, 16, 7, 2, 3), (2, 16, 14, 14, 32, 1, 1, 0), (2, 16, 14, 14, 32, 1, 2, 0),
+         (3, 8, 9, 11, 16, 3, 1, 1), (2, 32, 14, 14, 16, 3, 2, 1), (1, 4, 5, 5, 8, 3, 1, 1)]
+
+
+@pytest.mark.parametrize("geo", CONVS)
+def test_conv_nhwc_matches_fp64(dev, geo):
+    from cs744_pytorch_distributed_tutorial_amd.ops.cnn_nhwc import conv_nhwc
+    B, Ci, H, W, Co, k, st, pad = geo
+    torch.manual_seed(sum(geo))
+    conv = nn.Conv2d(Ci, Co, k, stride=st, padding=pad, bias=False).to(dev)
+    x = torch.randn(B, Ci, H, W, device=dev)
+    xh = nhwc(x).requires_grad_()
+    y = conv_nhwc(xh, conv)
+    xr = x.double().requires_grad_()
+    wr = conv.weight.detach().double().requires_grad_()
+    yr = F.conv2d(xr, wr, None, st, pad)
+    torch.testing.assert_close(nchw(y).double(), yr, rtol=1e-4, atol=1e-4)
+    g = torch.randn(yr.shape, device=dev)
+    y.backward(nhwc(g))
+    yr.backward(g.double())
+    torch.testing.assert_close(nchw(xh.grad).double(), xr.grad, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(conv.weight.grad.double(), wr.grad, rtol=1e-4, atol=1e-3)
+
+
+def test_conv_nhwc_bf16_close(dev):
+    from cs744_pytorch_distributed_tutorial_amd.ops.cnn_nhwc import conv_nhwc
+    torch.manual_seed(3)
+    conv = nn.Conv2d(64, 64, 3, padding=1, bias=False).to(dev)
+    x = torch.randn(4, 64, 14, 14, device=dev)
+    xh = nhwc(x).bfloat16().requires_grad_()
+    y = conv_nhwc(xh, conv)
+    assert y.dtype == torch.bfloat16
+    yr = F.conv2d(xh.detach().float().permute(0, 3, 1, 2), conv.weight.bfloat16().float(), None, 1, 1)
+    torch.testing.assert_close(nchw(y).float(), yr, rtol=2e-2, atol=3e-2)
+    y.float().square().sum().backward()
+    assert conv.weight.grad.dtype == torch.float32 and torch.isfinite(conv.weight.grad).all()
+
+
+@pytest.mark.parametrize("shape", [(4, 56, 56, 64), (8, 7, 7, 2048), (3, 14, 14, 24), (2, 5, 3, 6), (64, 3, 3, 512)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("relu,residual", [(True, False), (True, True), (False, False)])
+def test_bn_act_nhwc_matches_fp64(dev, shape, dtype, relu, residual):
+    from cs744_pytorch_distributed_tutorial_amd.ops.cnn_nhwc import bn_act_nhwc
+    torch.manual_seed(hash((shape, relu, residual)) % 1000)
+    C = shape[3]
+    bn = nn.BatchNorm2d(C).to(dev)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+        bn.running_mean.uniform_(-0.1, 0.1)
+    rm0, rv0 = bn.running_mean.clone().double(), bn.running_var.clone().double()
+    x = (torch.randn(shape, device=dev) * 2 + 0.7).to(dtype).requires_grad_()
+    res = torch.randn(shape, device=dev).to(dtype).requires_grad_() if residual else None
+    y = bn_act_nhwc(bn, x, relu, res)
+    assert y.shape == x.shape and y.dtype == dtype
+    xr = x.detach().double().requires_grad_()
+    rr = res.detach().double().requires_grad_() if residual else None
+    wr = bn.weight.detach().double().requires_grad_()
+    br = bn.bias.detach().double().requires_grad_()
+    yr = F.batch_norm(nchw(xr), rm0.clone(), rv0.clone(), wr, br, True, 0.1, 1e-5).permute(0, 2, 3, 1)
+    if residual:
+        yr = yr + rr
+    if relu:
+        yr = F.relu(yr)
+    tol = dict(rtol=1e-4, atol=1e-4) if dtype == torch.float32 else dict(rtol=2e-2, atol=3e-2)
+    torch.testing.assert_close(y.double(), yr, **tol)
+    xd = x.detach().double().reshape(-1, C)
+    M = xd.shape[0]
+    torch.testing.assert_close(bn.running_mean.double(), 0.9 * rm0 + 0.1 * xd.mean(0), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(bn.running_var.double(), 0.9 * rv0 + 0.1 * xd.var(0, unbiased=M > 1), rtol=1e-4,
+                               atol=1e-5)
+    assert int(bn.num_batches_tracked) == 1
+    g = torch.randn(shape, device=dev).to(dtype)
+    y.backward(g)
+    yr.backward(g.double())
+    gt = dict(rtol=1e-3, atol=1e-3) if dtype == torch.float32 else dict(rtol=5e-2, atol=5e-2)
+    torch.testing.assert_close(x.grad.double(), xr.grad, **gt)
+    pt = dict(rtol=1e-3, atol=1e-2 if dtype == torch.bfloat16 else 1e-3)
+    torch.testing.assert_close(bn.weight.grad.double(), wr.grad, **pt)
+    torch.testing.assert_close(bn.bias.grad.double(), br.grad, **pt)
+    if residual:
+        torch.testing.assert_close(res.grad.double(), rr.grad, **gt)
+
+
+@pytest.mark.parametrize("shape", [(2, 112, 112, 64), (3, 7, 9, 5), (1, 2, 3, 8)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_max_pool_nhwc_matches_torch(dev, shape, dtype):
+    from cs744_pytorch_distributed_tutorial_amd.ops.cnn_nhwc import max_pool3s2_nhwc
+    torch.manual_seed(1)
+    x = torch.randn(shape, device=dev).to(dtype).requires_grad_()
+    y = max_pool3s2_nhwc(x)
+    xr = nchw(x.detach()).contiguous().requires_grad_()
+    yr = F.max_pool2d(xr, 3, 2, 1)
+    assert torch.equal(nchw(y), yr)
+    g = torch.randn(yr.shape, device=dev).to(dtype)
+    y.backward(nhwc(g))
+    yr.backward(g)
+    torch.testing.assert_close(nchw(x.grad).float(), xr.grad.float(), rtol=1e-2 if dtype == torch.bfloat16 else 1e-6,
+                               atol=1e-2 if dtype == torch.bfloat16 else 1e-6)
+
+
+def _step(model, x):
+    model.zero_grad(set_to_none=True)
+    y = model(x)
+    y.square().mean().backward()
+    return y.detach().clone(), [p.grad.clone() for p in model.parameters()]
+
+
+def test_resnet18_nhwc_matches_nchw_module_path(dev):
+    """a whole ResNet-18 forward/backward on the channels-last kernels == MIOpen + nn.BatchNorm2d (fp32),
+    and bitwise equal to itself on a re-run"""
+    from cs744_pytorch_distributed_tutorial_amd.models.resnet import resnet18
+    from cs744_pytorch_distributed_tutorial_amd.ops import cnn
+    torch.manual_seed(0)
+    a = resnet18(num_classes=10, layout="nhwc").to(dev)
+    b = resnet18(num_classes=10, layout="nchw").to(dev)
+    b.load_state_dict(a.state_dict())
+    a2 = resnet18(num_classes=10, layout="nhwc").to(dev)
+    a2.load_state_dict(a.state_dict())
+    x = torch.randn(4, 3, 64, 64, device=dev)
+    ya, ga = _step(a, x)
+    ya2, ga2 = _step(a2, x)
+    assert torch.equal(ya, ya2) and all(torch.equal(p, q) for p, q in zip(ga, ga2))
+    orig = cnn.native_ok
+    cnn.native_ok = lambda *args: False
+    try:
+        yb, gb = _step(b, x)
+    finally:
+        cnn.native_ok = orig
+    torch.testing.assert_close(ya, yb, rtol=2e-3, atol=2e-3)
+    for (n, _), pa, pb in zip(a.named_parameters(), ga, gb):
+        torch.testing.assert_close(pa, pb, rtol=2e-2, atol=2e-3, msg=n)
+    for (n, ba), (_, bb) in zip(a.named_buffers(), b.named_buffers()):
+        torch.testing.assert_close(ba.double(), bb.double(), rtol=1e-4, atol=1e-5, msg=n)
+
+
+def test_resnet50_nhwc_bf16_step_trains(dev):
+    """ResNet-50 under bf16 autocast on the channels-last path: finite loss that drops over a few SGD steps"""
+    from cs744_pytorch_distributed_tutorial_amd.models.resnet import resnet50
+    torch.manual_seed(0)
+    m = resnet50(num_classes=10).to(dev)
+    opt = torch.optim.SGD(m.parameters(), lr=0.01)
+    x = torch.randn(8, 3, 64, 64, device=dev)
+    t = torch.randint(0, 10, (8,), device=dev)
+    losses = []
+    for _ in range(8):
+        opt.zero_grad()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            loss = F.cross_entropy(m(x).float(), t)
+        loss.backward()
+        opt.step()
+        losses.append(float(loss.detach()))
+    assert all(l == l for l in losses) and losses[-1] < losses[0], losses
