@@ -81,7 +81,13 @@ class _ConvNHWC(torch.autograd.Function):
         with torch.autocast("cuda", enabled=False):
             if ctx.needs_input_grad[1]:
                 dwf = torch.mm(dy2.t(), col)  # [Co, Kp]
-                dw = dwf[:, :K].reshape(Co, R, S, C).permute(0, 3, 1, 2).to(ctx.wdtype).contiguous()
+                # a fresh standard-strided [Co, Ci, R, S] tensor (a permuted view of a 1x1 kernel would
+                # pass is_contiguous() with non-standard strides for its size-1 dims)
+                if R == 1 and S == 1 and dwf.shape[1] == K:
+                    dw = dwf.view(Co, C, 1, 1).to(ctx.wdtype)
+                else:
+                    dw = torch.empty((Co, C, R, S), dtype=ctx.wdtype, device=dy.device)
+                    dw.copy_(dwf[:, :K].reshape(Co, R, S, C).permute(0, 3, 1, 2))
             if ctx.needs_input_grad[0]:
                 dcol = torch.mm(dy2, wf)  # [M, Kp]
                 dx = dcol.view(B, H, W, C) if direct else native.C().col2im_nhwc(dcol, B, H, W, C, R, S, stride, pad)

@@ -11,3 +11,8 @@ for lay in nhwc nchw; do
     echo "$lay $dt: $(tail -1 gpurun_out/bench_rn50_${lay}_${dt}.log | cut -c1-200)"
   done
 done
+export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT
+(cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_rn50_nhwc -o run -- python3 $R/bench.py --model resnet50 --dtype bf16 --steps 5 --warmup 2 > $R/gpurun_out/prof_rn50_nhwc.log 2>&1) || exit $?
+python3 scripts/prof_summary.py gpurun_out/prof_rn50_nhwc --steps 7 > gpurun_out/prof_rn50_nhwc_summary.txt 2>&1
+head -40 gpurun_out/prof_rn50_nhwc_summary.txt | cut -c1-180

@@ -165,20 +165,33 @@ def test_resnet18_nhwc_matches_nchw_module_path(dev):
         torch.testing.assert_close(ba.double(), bb.double(), rtol=1e-4, atol=1e-5, msg=n)
 
 
-def test_resnet50_nhwc_bf16_step_trains(dev):
-    """ResNet-50 under bf16 autocast on the channels-last path: finite loss that drops over a few SGD steps"""
+def test_resnet50_nhwc_bf16_as_accurate_as_miopen_bf16(dev):
+    """ResNet-50 under bf16 autocast, channels-last kernels vs MIOpen + the NCHW module path, both
+    measured against the fp32 NCHW step on the same weights and batch: the native path's logit error
+    and per-parameter gradient alignment are no worse than MIOpen's bf16 (bf16 error compounds over
+    50 layers, so the two bf16 paths are compared through the fp32 reference, not to each other)"""
     from cs744_pytorch_distributed_tutorial_amd.models.resnet import resnet50
     torch.manual_seed(0)
-    m = resnet50(num_classes=10).to(dev)
-    opt = torch.optim.SGD(m.parameters(), lr=0.01)
+    nets = {k: resnet50(num_classes=10, layout=k.split("_")[0]).to(dev) for k in ("nhwc_bf16", "nchw_bf16", "nchw_fp32")}
+    sd = nets["nhwc_bf16"].state_dict()
+    for m in nets.values():
+        m.load_state_dict(sd)
     x = torch.randn(8, 3, 64, 64, device=dev)
     t = torch.randint(0, 10, (8,), device=dev)
-    losses = []
-    for _ in range(8):
-        opt.zero_grad()
-        with torch.autocast("cuda", dtype=torch.bfloat16):
-            loss = F.cross_entropy(m(x).float(), t)
+    out = {}
+    for k, m in nets.items():
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=k.endswith("bf16")):
+            y = m(x).float()
+            loss = F.cross_entropy(y, t)
         loss.backward()
-        opt.step()
-        losses.append(float(loss.detach()))
-    assert all(l == l for l in losses) and losses[-1] < losses[0], losses
+        out[k] = (y.detach().double(), [p.grad.double().flatten() for p in m.parameters()])
+    yref, gref = out["nchw_fp32"]
+
+    def err(k):
+        y, g = out[k]
+        cos = [float(a @ b / (a.norm() * b.norm())) for a, b in zip(g, gref) if b.norm() > 1e-6]
+        return float((y - yref).norm() / yref.norm()), sum(cos) / len(cos), min(cos)
+
+    e_nat, e_mio = err("nhwc_bf16"), err("nchw_bf16")
+    assert e_nat[0] <= 2 * e_mio[0] + 0.02, (e_nat, e_mio)
+    assert e_nat[1] >= e_mio[1] - 0.02 and e_nat[2] >= e_mio[2] - 0.1, (e_nat, e_mio)
