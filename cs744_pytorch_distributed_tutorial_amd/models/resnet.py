@@ -150,7 +150,8 @@ class ResNet(nn.Module):
 
     def forward_nhwc(self, x: torch.Tensor) -> torch.Tensor:
         """the same network on channels-last activations (input: [B, 3, H, W], any memory format)"""
-        x = to_nhwc(x, act_dtype(x))
+        # the 3-channel image gets a zero 4th channel: the stem's im2col then moves 4-channel vectors
+        x = to_nhwc(x, act_dtype(x), pad_c=1 if x.shape[1] == 3 else 0)
         x = max_pool3s2_nhwc(bn_act_nhwc(self.bn1, conv_nhwc(x, self.conv1)))
         for layer in (self.layer1, self.layer2, self.layer3, self.layer4):
             for blk in layer:

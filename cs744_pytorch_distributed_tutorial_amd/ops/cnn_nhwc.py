@@ -34,10 +34,12 @@ def act_dtype(x: torch.Tensor) -> torch.dtype:
     return x.dtype
 
 
-def to_nhwc(x: torch.Tensor, dtype: Optional[torch.dtype] = None) -> torch.Tensor:
-    """[B, C, H, W] (any memory format) -> contiguous [B, H, W, C]"""
+def to_nhwc(x: torch.Tensor, dtype: Optional[torch.dtype] = None, pad_c: int = 0) -> torch.Tensor:
+    """[B, C, H, W] (any memory format) -> contiguous [B, H, W, C (+ pad_c zero channels)]"""
     x = x.permute(0, 2, 3, 1)
-    return x.to(dtype).contiguous() if dtype is not None else x.contiguous()
+    if dtype is not None:
+        x = x.to(dtype)
+    return F.pad(x, (0, pad_c)).contiguous() if pad_c else x.contiguous()
 
 
 def _kpad(k: int, dtype: torch.dtype) -> int:
@@ -45,15 +47,44 @@ def _kpad(k: int, dtype: torch.dtype) -> int:
     return (k + v - 1) // v * v
 
 
+def _wgrad_splits(M: int, Co: int, Kp: int) -> int:
+    """row chunks for the weight-gradient GEMM dW = dY^T @ col ([Co, M] x [M, Kp]): its output is
+    small and its reduction long (M = B*Ho*Wo rows: 401k for ResNet-50's first stage at B=128), so
+    one GEMM fills few of the 256 CUs (hipBLASLt measured ~30 TFLOP/s on it); S chunks run as one
+    batched GEMM with fp32 partials, summed after"""
+    tiles = max(1, (Co // 128) * (Kp // 128))
+    s = 1
+    while s < 64 and tiles * s * 2 <= 1024 and M % (2 * s) == 0 and M // (2 * s) >= 2048:
+        s *= 2
+    return s
+
+
+def _wgrad(dy2: torch.Tensor, col: torch.Tensor) -> torch.Tensor:
+    """fp32 dY^T @ col, split over row chunks when the output alone cannot fill the chip"""
+    M, Co = dy2.shape
+    Kp = col.shape[1]
+    S = _wgrad_splits(M, Co, Kp)
+    if S == 1:
+        return torch.mm(dy2.t(), col, out_dtype=torch.float32) if col.dtype != torch.float32 else torch.mm(dy2.t(), col)
+    a = dy2.view(S, M // S, Co).transpose(1, 2)
+    b = col.view(S, M // S, Kp)
+    part = torch.bmm(a, b, out_dtype=torch.float32) if col.dtype != torch.float32 else torch.bmm(a, b)
+    return part.sum(0)
+
+
 class _ConvNHWC(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, stride: int, pad: int):
         B, H, W, C = x.shape
         Co, Ci, R, S = weight.shape
-        assert Ci == C, f"conv_nhwc: {C} input channels for a {Ci}-channel weight"
+        # x may carry zero channels beyond the weight's (the stem's 3 -> 4, for vector access)
+        assert Ci <= C, f"conv_nhwc: {C} input channels for a {Ci}-channel weight"
         Ho, Wo = (H + 2 * pad - R) // stride + 1, (W + 2 * pad - S) // stride + 1
         K = R * S * C
-        wf = weight.permute(0, 2, 3, 1).reshape(Co, K).to(x.dtype)  # [Co, K], columns (r, s, c)
+        w4 = weight.permute(0, 2, 3, 1)
+        if Ci < C:
+            w4 = F.pad(w4, (0, C - Ci))
+        wf = w4.reshape(Co, K).to(x.dtype)  # [Co, K], columns (r, s, c)
         direct = R == 1 and S == 1 and stride == 1 and pad == 0
         if direct:
             col = x.view(B * H * W, C)
@@ -66,29 +97,30 @@ class _ConvNHWC(torch.autograd.Function):
         with torch.autocast("cuda", enabled=False):
             y = torch.mm(col, wf.t())
         ctx.save_for_backward(col, wf)
-        ctx.geo = (B, H, W, C, Co, R, S, stride, pad, K, direct)
+        ctx.geo = (B, H, W, C, Ci, Co, R, S, stride, pad, K, direct)
         ctx.wdtype = weight.dtype
         return y.view(B, Ho, Wo, Co)
 
     @staticmethod
     def backward(ctx, dy):
         col, wf = ctx.saved_tensors
-        B, H, W, C, Co, R, S, stride, pad, K, direct = ctx.geo
+        B, H, W, C, Ci, Co, R, S, stride, pad, K, direct = ctx.geo
         dy2 = dy.reshape(-1, Co)
         if not dy2.is_contiguous():
             dy2 = dy2.contiguous()
         dx = dw = None
         with torch.autocast("cuda", enabled=False):
             if ctx.needs_input_grad[1]:
-                dwf = torch.mm(dy2.t(), col)  # [Co, Kp]
+                dwf = _wgrad(dy2, col)  # [Co, Kp] fp32
                 # a fresh standard-strided [Co, Ci, R, S] tensor (a permuted view of a 1x1 kernel would
                 # pass is_contiguous() with non-standard strides for its size-1 dims)
-                if R == 1 and S == 1 and dwf.shape[1] == K:
+                if R == 1 and S == 1 and dwf.shape[1] == K and Ci == C:
                     dw = dwf.view(Co, C, 1, 1).to(ctx.wdtype)
                 else:
-                    dw = torch.empty((Co, C, R, S), dtype=ctx.wdtype, device=dy.device)
-                    dw.copy_(dwf[:, :K].reshape(Co, R, S, C).permute(0, 3, 1, 2))
+                    dw = torch.empty((Co, Ci, R, S), dtype=ctx.wdtype, device=dy.device)
+                    dw.copy_(dwf[:, :K].reshape(Co, R, S, C)[..., :Ci].permute(0, 3, 1, 2))
             if ctx.needs_input_grad[0]:
+                assert Ci == C, "conv_nhwc: no data gradient through padded input channels"
                 dcol = torch.mm(dy2, wf)  # [M, Kp]
                 dx = dcol.view(B, H, W, C) if direct else native.C().col2im_nhwc(dcol, B, H, W, C, R, S, stride, pad)
         return dx, dw, None, None

@@ -134,19 +134,21 @@ __global__ __launch_bounds__(256) void stats_kernel(const T* __restrict__ x, int
   lanes_to_part<V>(s, s1, s2, sh, part, C);
 }
 
-// 256 threads = 32 channels x 8 partial lanes, f64 sums in lane order: mean / biased var
-// (normalisation) / unbiased var (running stats); stat = [scale, shift, mean, invstd][C]
+// 256 threads = 8 channels x 32 partial lanes (f64 sums, lanes combined in a fixed tree):
+// mean / biased var (normalisation) / unbiased var (running stats); stat = [scale, shift, mean,
+// invstd][C]. 32 lanes keep even 1024 partials to 32 dependent adds per thread.
 template <typename T>
 __global__ __launch_bounds__(256) void finalize_fwd_kernel(const T* __restrict__ x, const float* __restrict__ part,
                                                            int P, int C, double M, const float* __restrict__ w,
                                                            const float* __restrict__ b, float* __restrict__ rm,
                                                            float* __restrict__ rv, float momentum, float eps,
                                                            float* __restrict__ stat, int64_t* __restrict__ nbt) {
-  __shared__ double sh[8][32][2];
-  const int cl = threadIdx.x & 31, pl = threadIdx.x >> 5, c = blockIdx.x * 32 + cl;
+  __shared__ double sh[32][8][2];
+  const int cl = threadIdx.x & 7, pl = threadIdx.x >> 3, c = blockIdx.x * 8 + cl;
   double s1 = 0.0, s2 = 0.0;
   if (c < C)
-    for (int p = pl; p < P; p += 8) {
+#pragma unroll 4
+    for (int p = pl; p < P; p += 32) {
       const float2 v = *reinterpret_cast<const float2*>(part + ((size_t)p * C + c) * 2);
       s1 += (double)v.x;
       s2 += (double)v.y;
@@ -154,13 +156,18 @@ __global__ __launch_bounds__(256) void finalize_fwd_kernel(const T* __restrict__
   sh[pl][cl][0] = s1;
   sh[pl][cl][1] = s2;
   __syncthreads();
+#pragma unroll
+  for (int h = 16; h > 0; h >>= 1) {
+    if (pl < h) {
+      sh[pl][cl][0] += sh[pl + h][cl][0];
+      sh[pl][cl][1] += sh[pl + h][cl][1];
+    }
+    __syncthreads();
+  }
   if (blockIdx.x == 0 && threadIdx.x == 0 && nbt != nullptr) *nbt += 1;  // num_batches_tracked
   if (pl != 0 || c >= C) return;
-  s1 = s2 = 0.0;
-  for (int l = 0; l < 8; ++l) {
-    s1 += sh[l][cl][0];
-    s2 += sh[l][cl][1];
-  }
+  s1 = sh[0][cl][0];
+  s2 = sh[0][cl][1];
   const double K = (double)E<T>::ld(x + c);
   const double dm = s1 / M;
   double var = s2 / M - dm * dm;
@@ -179,20 +186,30 @@ __global__ __launch_bounds__(256) void finalize_fwd_kernel(const T* __restrict__
   }
 }
 
+// Block (p, g): rows [p*rpb, ...) x this block's channel vectors (the stats kernel's split): each
+// thread keeps its V channels' scale / shift in registers and walks rows.
 template <typename T, int V>
 __global__ __launch_bounds__(256) void apply_fwd_kernel(const T* __restrict__ x, const T* __restrict__ res,
-                                                        const float* __restrict__ stat, T* __restrict__ y, int C,
-                                                        int64_t nvec, int relu) {
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += stride) {
-    const int64_t e = i * V;
-    const int c = (int)(e % C);
-    float v[V], r[V];
+                                                        const float* __restrict__ stat, T* __restrict__ y,
+                                                        int64_t M, int C, int rpb, int relu) {
+  const RowSplit s = row_split(C, V);
+  if (s.rl >= s.lanes) return;
+  float sc[V], sf[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) {
+    sc[j] = stat[s.c0 + j];
+    sf[j] = stat[C + s.c0 + j];
+  }
+  const int64_t r0 = (int64_t)blockIdx.x * rpb, r1 = min(M, r0 + rpb);
+#pragma unroll 2
+  for (int64_t r = r0 + s.rl; r < r1; r += s.lanes) {
+    const int64_t e = r * C + s.c0;
+    float v[V], rr[V];
     ldv<T, V>(x + e, v);
-    if (res != nullptr) ldv<T, V>(res + e, r);
+    if (res != nullptr) ldv<T, V>(res + e, rr);
 #pragma unroll
     for (int j = 0; j < V; ++j) {
-      const float z = preact(v[j], stat[c + j], stat[C + c + j], res != nullptr ? r[j] : 0.f);
+      const float z = preact(v[j], sc[j], sf[j], res != nullptr ? rr[j] : 0.f);
       v[j] = relu && !(z > 0.f) ? 0.f : z;
     }
     stv<T, V>(y + e, v);
@@ -237,16 +254,18 @@ __global__ __launch_bounds__(256) void bwd_reduce_kernel(const T* __restrict__ d
   lanes_to_part<V>(s, sg, sgx, sh, part, C);
 }
 
-// dbeta = sum g, dgamma = sum g*xhat; coef = [gamma*invstd, sum g / M, sum g*xhat / M][C]
+// dbeta = sum g, dgamma = sum g*xhat (8 channels x 32 partial lanes, as the forward finalize);
+// coef = [gamma*invstd, sum g / M, sum g*xhat / M][C]
 __global__ __launch_bounds__(256) void finalize_bwd_kernel(const float* __restrict__ part, int P, int C, double M,
                                                            const float* __restrict__ w, const float* __restrict__ stat,
                                                            float* __restrict__ dw, float* __restrict__ db,
                                                            float* __restrict__ coef) {
-  __shared__ double sh[8][32][2];
-  const int cl = threadIdx.x & 31, pl = threadIdx.x >> 5, c = blockIdx.x * 32 + cl;
+  __shared__ double sh[32][8][2];
+  const int cl = threadIdx.x & 7, pl = threadIdx.x >> 3, c = blockIdx.x * 8 + cl;
   double sg = 0.0, sgx = 0.0;
   if (c < C)
-    for (int p = pl; p < P; p += 8) {
+#pragma unroll 4
+    for (int p = pl; p < P; p += 32) {
       const float2 v = *reinterpret_cast<const float2*>(part + ((size_t)p * C + c) * 2);
       sg += (double)v.x;
       sgx += (double)v.y;
@@ -254,12 +273,17 @@ __global__ __launch_bounds__(256) void finalize_bwd_kernel(const float* __restri
   sh[pl][cl][0] = sg;
   sh[pl][cl][1] = sgx;
   __syncthreads();
-  if (pl != 0 || c >= C) return;
-  sg = sgx = 0.0;
-  for (int l = 0; l < 8; ++l) {
-    sg += sh[l][cl][0];
-    sgx += sh[l][cl][1];
+#pragma unroll
+  for (int h = 16; h > 0; h >>= 1) {
+    if (pl < h) {
+      sh[pl][cl][0] += sh[pl + h][cl][0];
+      sh[pl][cl][1] += sh[pl + h][cl][1];
+    }
+    __syncthreads();
   }
+  if (pl != 0 || c >= C) return;
+  sg = sh[0][cl][0];
+  sgx = sh[0][cl][1];
   if (dw != nullptr) dw[c] = (float)sgx;
   if (db != nullptr) db[c] = (float)sg;
   coef[c] = (w != nullptr ? w[c] : 1.f) * stat[3 * C + c];
@@ -267,25 +291,40 @@ __global__ __launch_bounds__(256) void finalize_bwd_kernel(const float* __restri
   coef[2 * C + c] = (float)(sgx / M);
 }
 
+// dx = k*(g - mean(g) - xhat*mean(g*xhat)), dres = g; per-channel operands in registers, rows walked
+// as in apply_fwd_kernel
 template <typename T, int V>
 __global__ __launch_bounds__(256) void apply_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                         const T* __restrict__ res, const float* __restrict__ stat,
                                                         const float* __restrict__ coef, T* __restrict__ dx,
-                                                        T* __restrict__ dres, int C, int64_t nvec, int relu) {
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += stride) {
-    const int64_t e = i * V;
-    const int c = (int)(e % C);
-    float g[V], v[V], r[V];
+                                                        T* __restrict__ dres, int64_t M, int C, int rpb, int relu) {
+  const RowSplit s = row_split(C, V);
+  if (s.rl >= s.lanes) return;
+  float sc[V], sf[V], mu[V], is[V], k[V], mg[V], mgx[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) {
+    const int c = s.c0 + j;
+    sc[j] = stat[c];
+    sf[j] = stat[C + c];
+    mu[j] = stat[2 * C + c];
+    is[j] = stat[3 * C + c];
+    k[j] = coef[c];
+    mg[j] = coef[C + c];
+    mgx[j] = coef[2 * C + c];
+  }
+  const int64_t r0 = (int64_t)blockIdx.x * rpb, r1 = min(M, r0 + rpb);
+#pragma unroll 2
+  for (int64_t r = r0 + s.rl; r < r1; r += s.lanes) {
+    const int64_t e = r * C + s.c0;
+    float g[V], v[V], rr[V];
     ldv<T, V>(dy + e, g);
     ldv<T, V>(x + e, v);
-    if (relu && res != nullptr) ldv<T, V>(res + e, r);
+    if (relu && res != nullptr) ldv<T, V>(res + e, rr);
 #pragma unroll
     for (int j = 0; j < V; ++j) {
-      const int cj = c + j;
-      if (relu && !(preact(v[j], stat[cj], stat[C + cj], res != nullptr ? r[j] : 0.f) > 0.f)) g[j] = 0.f;
-      const float xhat = (v[j] - stat[2 * C + cj]) * stat[3 * C + cj];
-      v[j] = coef[cj] * (g[j] - coef[C + cj] - xhat * coef[2 * C + cj]);
+      if (relu && !(preact(v[j], sc[j], sf[j], res != nullptr ? rr[j] : 0.f) > 0.f)) g[j] = 0.f;
+      const float xhat = (v[j] - mu[j]) * is[j];
+      v[j] = k[j] * (g[j] - mg[j] - xhat * mgx[j]);
     }
     stv<T, V>(dx + e, v);
     if (dres != nullptr) stv<T, V>(dres + e, g);
@@ -452,17 +491,31 @@ BnGrid bn_grid(int64_t M, int C, int V) {
   return g;
 }
 
+// elementwise passes: ~2048 blocks of >= 4 rows per row lane
+BnGrid apply_grid(int64_t M, int C, int V) {
+  BnGrid g;
+  const int CV = C / V;
+  g.CG = (CV + 255) / 256;
+  const int lanes = 256 / (CV < 256 ? CV : 256);
+  const int64_t want = (2048 + g.CG - 1) / g.CG;
+  int64_t rpb = (M + want - 1) / want;
+  if (rpb < 4 * (int64_t)lanes) rpb = 4 * (int64_t)lanes;
+  g.rpb = (int)rpb;
+  g.P = (int)((M + rpb - 1) / rpb);
+  return g;
+}
+
 template <typename T, int V>
 void bn_fwd_t(const void* x, const void* res, const float* w, const float* b, float* rm, float* rv, int64_t* nbt,
               float momentum, float eps, int relu, void* y, float* stat, float* part, int64_t M, int C,
               hipStream_t st) {
   const BnGrid g = bn_grid(M, C, V);
   hipLaunchKernelGGL((stats_kernel<T, V>), dim3(g.P, g.CG), dim3(256), 0, st, (const T*)x, M, C, g.rpb, part);
-  hipLaunchKernelGGL(finalize_fwd_kernel<T>, dim3((C + 31) / 32), dim3(256), 0, st, (const T*)x, part, g.P, C,
+  hipLaunchKernelGGL(finalize_fwd_kernel<T>, dim3((C + 7) / 8), dim3(256), 0, st, (const T*)x, part, g.P, C,
                      (double)M, w, b, rm, rv, momentum, eps, stat, nbt);
-  const int64_t nvec = M * C / V;
-  hipLaunchKernelGGL((apply_fwd_kernel<T, V>), dim3(grid_for(nvec)), dim3(256), 0, st, (const T*)x, (const T*)res,
-                     stat, (T*)y, C, nvec, relu);
+  const BnGrid a = apply_grid(M, C, V);
+  hipLaunchKernelGGL((apply_fwd_kernel<T, V>), dim3(a.P, a.CG), dim3(256), 0, st, (const T*)x, (const T*)res, stat,
+                     (T*)y, M, C, a.rpb, relu);
 }
 
 template <typename T, int V>
@@ -471,11 +524,11 @@ void bn_bwd_t(const void* dy, const void* x, const void* res, const float* w, co
   const BnGrid g = bn_grid(M, C, V);
   hipLaunchKernelGGL((bwd_reduce_kernel<T, V>), dim3(g.P, g.CG), dim3(256), 0, st, (const T*)dy, (const T*)x,
                      (const T*)res, stat, M, C, g.rpb, relu, part);
-  hipLaunchKernelGGL(finalize_bwd_kernel, dim3((C + 31) / 32), dim3(256), 0, st, part, g.P, C, (double)M, w, stat, dw,
+  hipLaunchKernelGGL(finalize_bwd_kernel, dim3((C + 7) / 8), dim3(256), 0, st, part, g.P, C, (double)M, w, stat, dw,
                      db, coef);
-  const int64_t nvec = M * C / V;
-  hipLaunchKernelGGL((apply_bwd_kernel<T, V>), dim3(grid_for(nvec)), dim3(256), 0, st, (const T*)dy, (const T*)x,
-                     (const T*)res, stat, coef, (T*)dx, (T*)dres, C, nvec, relu);
+  const BnGrid a = apply_grid(M, C, V);
+  hipLaunchKernelGGL((apply_bwd_kernel<T, V>), dim3(a.P, a.CG), dim3(256), 0, st, (const T*)dy, (const T*)x,
+                     (const T*)res, stat, coef, (T*)dx, (T*)dres, M, C, a.rpb, relu);
 }
 
 // dispatch on (dtype, V) for a functor F<T, V>::run(args...)

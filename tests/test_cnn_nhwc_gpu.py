@@ -30,7 +30,8 @@ def nchw(x):
 
 # (B, Cin, H, W, Cout, k, stride, pad): every ResNet geometry (stem, 1x1, strided 1x1, 3x3, 3x3/2)
 CONVS = [(2, 3, 32, 32, 16, 7, 2, 3), (2, 16, 14, 14, 32, 1, 1, 0), (2, 16, 14, 14, 32, 1, 2, 0),
-         (3, 8, 9, 11, 16, 3, 1, 1), (2, 32, 14, 14, 16, 3, 2, 1), (1, 4, 5, 5, 8, 3, 1, 1)]
+         (3, 8, 9, 11, 16, 3, 1, 1), (2, 32, 14, 14, 16, 3, 2, 1), (1, 4, 5, 5, 8, 3, 1, 1),
+         (8, 16, 32, 32, 16, 3, 1, 1), (16, 8, 32, 32, 32, 1, 1, 0)]  # the last two: split weight-gradient GEMM
 
 
 @pytest.mark.parametrize("geo", CONVS)
@@ -51,6 +52,28 @@ def test_conv_nhwc_matches_fp64(dev, geo):
     yr.backward(g.double())
     torch.testing.assert_close(nchw(xh.grad).double(), xr.grad, rtol=1e-4, atol=1e-4)
     torch.testing.assert_close(conv.weight.grad.double(), wr.grad, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_conv_nhwc_padded_stem(dev, dtype):
+    """the stem's 3-channel weight on a 4-channel input whose last channel is zero (vector im2col)"""
+    from cs744_pytorch_distributed_tutorial_amd.ops.cnn_nhwc import conv_nhwc, to_nhwc
+    torch.manual_seed(7)
+    conv = nn.Conv2d(3, 16, 7, stride=2, padding=3, bias=False).to(dev)
+    x = torch.randn(2, 3, 40, 40, device=dev)
+    xh = to_nhwc(x, dtype, pad_c=1)
+    assert xh.shape == (2, 40, 40, 4) and bool((xh[..., 3] == 0).all())
+    y = conv_nhwc(xh, conv)
+    wr = conv.weight.detach().to(dtype).double().requires_grad_()
+    yr = F.conv2d(x.to(dtype).double(), wr, None, 2, 3)
+    tol = dict(rtol=1e-4, atol=1e-4) if dtype == torch.float32 else dict(rtol=2e-2, atol=3e-2)
+    torch.testing.assert_close(nchw(y).double(), yr, **tol)
+    g = torch.randn(yr.shape, device=dev)
+    y.backward(nhwc(g).to(dtype))
+    yr.backward(g.to(dtype).double())
+    assert conv.weight.grad.shape == (16, 3, 7, 7) and conv.weight.grad.is_contiguous()
+    torch.testing.assert_close(conv.weight.grad.double(), wr.grad, rtol=1e-4 if dtype == torch.float32 else 2e-2,
+                               atol=1e-3 if dtype == torch.float32 else 0.5)
 
 
 def test_conv_nhwc_bf16_close(dev):
