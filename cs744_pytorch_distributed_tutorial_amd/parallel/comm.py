@@ -134,6 +134,35 @@ class TorchComm(Comm):
         D.irecv(buf, src, group=self.group).wait()
 
 
+def _agreed(build, group, what: str) -> Comm:
+    """Build a native communicator on every rank, or on none: each rank reports whether its
+    construction succeeded (one MIN all-reduce over the process group), and if any rank failed
+    all of them fall back to the torch.distributed communicator — a rank that cannot join the
+    native RCCL communicator must not leave its peers waiting inside the first collective."""
+    import sys
+
+    import torch.distributed as dist
+    comm, err = None, None
+    try:
+        comm = build()
+    except Exception as e:  # noqa: BLE001 - reported, then agreed on below
+        err = e
+    if not dist.is_initialized():
+        if err is not None:
+            raise err
+        return comm
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else "cpu"
+    ok = torch.tensor([0 if err is not None else 1], dtype=torch.int32, device=dev)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)
+    if int(ok.item()) == 1:
+        return comm
+    print(f"[comm] native {what} communicator unavailable on some rank ({err!r} here); "
+          "every rank falls back to torch.distributed", file=sys.stderr, flush=True)
+    if comm is not None and hasattr(comm, "close"):
+        comm.close()
+    return TorchComm(group)
+
+
 def make_comm(kind: Optional[str] = None, group=None) -> Comm:
     """``kind``: ``"torch"`` (default), ``"rccl"`` (native C++ RCCL communicator, one GPU per
     rank) or ``"staged"`` (native C++ communicator over a gloo group with host staging: the
@@ -143,7 +172,7 @@ def make_comm(kind: Optional[str] = None, group=None) -> Comm:
         return TorchComm(group)
     if kind == "rccl":
         from .rccl import RcclComm
-        return RcclComm.from_process_group(group)
+        return _agreed(lambda: RcclComm.from_process_group(group), group, "rccl")
     if kind == "staged":
         from .staged import StagedComm
         return StagedComm(group)

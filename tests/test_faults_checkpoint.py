@@ -124,3 +124,31 @@ def test_checkpoint_roundtrip_resume_matches_uninterrupted(tmp_path):
     run(m2, o2, batches[2:])
     for a, b in zip(m_ref.state_dict().values(), m2.state_dict().values()):
         assert torch.equal(a, b)
+
+
+def _native_comm_fallback_worker(rank, world):
+    import torch
+    from cs744_pytorch_distributed_tutorial_amd.parallel import comm as cm
+    # rank 1 cannot build the native communicator; rank 0 (pretend) can: all must agree on torch
+    built = []
+
+    def build():
+        if rank == 1:
+            raise RuntimeError("no RCCL on this rank")
+        built.append(rank)
+        return cm.TorchComm()
+
+    c = cm._agreed(build, None, "rccl")
+    t = torch.full((4,), float(rank + 1))
+    c.all_reduce(t, "sum")
+    return {"kind": type(c).__name__, "sum": t, "built": len(built)}
+
+
+def test_native_comm_failure_on_one_rank_falls_back_on_all():
+    """a rank that cannot build the native RCCL communicator takes every rank to torch.distributed
+    (agreed by one all-reduce) instead of leaving its peers inside the first native collective"""
+    from mp_util import run_world
+    out = run_world(_native_comm_fallback_worker, 2)
+    for r in range(2):
+        assert out[r]["kind"] == "TorchComm"
+        assert list(out[r]["sum"]) == [3.0] * 4
