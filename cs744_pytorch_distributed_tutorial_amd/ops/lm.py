@@ -36,17 +36,20 @@ def rope_ref(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Ten
 # ------------------------------------------------------------------ autograd functions
 class _RMSNorm(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, eps):
+    def forward(ctx, x, w, eps, out_bf16):
         xc = x.contiguous()
-        y, rstd = native.C().rmsnorm_fwd(xc, w.contiguous(), eps)
+        y, rstd = native.C().rmsnorm_fwd(xc, w.contiguous(), eps, out_bf16)
         ctx.save_for_backward(xc, w, rstd)
         return y
 
     @staticmethod
     def backward(ctx, gy):
         x, w, rstd = ctx.saved_tensors
-        dx, dw = native.C().rmsnorm_bwd(x, w.contiguous(), rstd, gy.contiguous().to(x.dtype))
-        return dx, dw, None
+        gy = gy.contiguous()
+        if gy.dtype != x.dtype and x.shape[-1] % 4 != 0:
+            gy = gy.to(x.dtype)
+        dx, dw = native.C().rmsnorm_bwd(x, w.contiguous(), rstd, gy)
+        return dx, dw, None, None
 
 
 class _SwiGLU(torch.autograd.Function):
@@ -82,9 +85,12 @@ def _native_ok(*ts) -> bool:
 
 def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float = 1e-5) -> torch.Tensor:
     if _native_ok(x, w):
-        if torch.is_autocast_enabled() and x.dtype == torch.float32:
-            pass  # residual stream stays fp32; the following Linear casts under autocast
-        return _RMSNorm.apply(x, w, eps)
+        # under bf16 autocast the fp32 residual stream is normalised straight into bf16: the
+        # projections that follow read it without a cast pass each (5 per block), and their input
+        # gradients come back in bf16 into the backward kernel, again without a cast
+        out_bf16 = (torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16
+                    and x.shape[-1] % 4 == 0)
+        return _RMSNorm.apply(x, w, eps, out_bf16)
     return rms_norm_ref(x, w, eps)
 
 

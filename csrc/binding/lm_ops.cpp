@@ -18,30 +18,33 @@ void check(const torch::Tensor& t, const char* n) {
   TORCH_CHECK(t.is_cuda() && t.is_contiguous(), n, " must be a contiguous GPU tensor");
 }
 
-std::vector<torch::Tensor> rmsnorm_fwd(torch::Tensor x, torch::Tensor w, double eps) {
+// out_bf16: write y in bf16 whatever x's dtype (the fp32 residual stream feeding bf16 GEMMs)
+std::vector<torch::Tensor> rmsnorm_fwd(torch::Tensor x, torch::Tensor w, double eps, bool out_bf16) {
   check(x, "x"); check(w, "w");
   const int64_t D = w.numel();
   TORCH_CHECK(x.size(-1) == D, "rmsnorm: last dim must match the weight");
+  TORCH_CHECK(!out_bf16 || x.scalar_type() == at::kBFloat16 || D % 4 == 0, "rmsnorm: bf16 output of fp32 input needs D % 4 == 0");
   const int64_t rows = x.numel() / D;
   DevGuard g(x.device());
-  auto y = torch::empty_like(x);
+  auto y = out_bf16 ? torch::empty_like(x, x.options().dtype(at::kBFloat16)) : torch::empty_like(x);
   auto rstd = torch::empty({rows}, x.options().dtype(at::kFloat));
-  CS_LAUNCH(cs_rmsnorm_fwd(dt_of(x), dt_of(w), x.data_ptr(), w.data_ptr(), y.data_ptr(), rstd.data_ptr<float>(),
-                           (int)rows, (int)D, (float)eps, cur_stream()));
+  CS_LAUNCH(cs_rmsnorm_fwd(dt_of(x), dt_of(w), dt_of(y), x.data_ptr(), w.data_ptr(), y.data_ptr(),
+                           rstd.data_ptr<float>(), (int)rows, (int)D, (float)eps, cur_stream()));
   return {y, rstd};
 }
 
 std::vector<torch::Tensor> rmsnorm_bwd(torch::Tensor x, torch::Tensor w, torch::Tensor rstd, torch::Tensor gy) {
   check(x, "x"); check(w, "w"); check(rstd, "rstd"); check(gy, "gy");
   const int64_t D = w.numel(), rows = x.numel() / D;
-  TORCH_CHECK(gy.sizes() == x.sizes() && gy.scalar_type() == x.scalar_type() && rstd.numel() == rows,
-              "rmsnorm_bwd: shapes");
+  TORCH_CHECK(gy.sizes() == x.sizes() && rstd.numel() == rows, "rmsnorm_bwd: shapes");
+  TORCH_CHECK(gy.scalar_type() == x.scalar_type() || D % 4 == 0, "rmsnorm_bwd: mixed dtypes need D % 4 == 0");
   DevGuard g(x.device());
   auto dx = torch::empty_like(x);
   auto dw = torch::empty_like(w);
-  auto part = torch::empty({(int64_t)cs_rmsnorm_bwd_partials((int)rows), D}, x.options().dtype(at::kFloat));
-  CS_LAUNCH(cs_rmsnorm_bwd(dt_of(x), dt_of(w), x.data_ptr(), w.data_ptr(), rstd.data_ptr<float>(), gy.data_ptr(),
-                           dx.data_ptr(), dw.data_ptr(), part.data_ptr<float>(), (int)rows, (int)D, cur_stream()));
+  auto part = torch::empty({(int64_t)cs_rmsnorm_bwd_partials((int)rows, (int)D), D}, x.options().dtype(at::kFloat));
+  CS_LAUNCH(cs_rmsnorm_bwd(dt_of(x), dt_of(w), dt_of(gy), x.data_ptr(), w.data_ptr(), rstd.data_ptr<float>(),
+                           gy.data_ptr(), dx.data_ptr(), dw.data_ptr(), part.data_ptr<float>(), (int)rows, (int)D,
+                           cur_stream()));
   return {dx, dw};
 }
 

@@ -171,12 +171,13 @@ hipError_t cs_link_wait(const unsigned long long* count, unsigned long long* exp
 
 // ---------------------------------------------------------------- decoder-LM elementwise ops (lm.hip)
 enum { CS_F32 = 0, CS_BF16 = 1 };
-int cs_rmsnorm_bwd_partials(int rows);
-hipError_t cs_rmsnorm_fwd(int dt, int wdt, const void* x, const void* w, void* y, float* rstd, int rows, int D,
-                          float eps, hipStream_t s);
-// part: [cs_rmsnorm_bwd_partials(rows)][D] fp32 scratch; dw has the weight's dtype
-hipError_t cs_rmsnorm_bwd(int dt, int wdt, const void* x, const void* w, const float* rstd, const void* g, void* dx,
-                          void* dw, float* part, int rows, int D, hipStream_t s);
+int cs_rmsnorm_bwd_partials(int rows, int D);
+// y has dtype odt (e.g. bf16 out of an fp32 residual stream under autocast; odt != dt needs D % 4 == 0)
+hipError_t cs_rmsnorm_fwd(int dt, int wdt, int odt, const void* x, const void* w, void* y, float* rstd, int rows,
+                          int D, float eps, hipStream_t s);
+// part: [cs_rmsnorm_bwd_partials(rows, D)][D] fp32 scratch; dw has the weight's dtype, g dtype gdt, dx x's
+hipError_t cs_rmsnorm_bwd(int dt, int wdt, int gdt, const void* x, const void* w, const float* rstd, const void* g,
+                          void* dx, void* dw, float* part, int rows, int D, hipStream_t s);
 hipError_t cs_swiglu_fwd(int dt, const void* a, const void* b, void* out, size_t n, hipStream_t s);
 hipError_t cs_swiglu_bwd(int dt, const void* a, const void* b, const void* g, void* da, void* db, size_t n,
                          hipStream_t s);

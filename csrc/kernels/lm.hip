@@ -69,6 +69,137 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(const T* __restrict__ 
   }
 }
 
+// ---- 4-wide path (D % 4 == 0, D <= 4 * 256 * kMaxQ): 16/8-byte accesses, the row held in
+// registers between the reduction and the scaling pass, the weight-gradient partial of a block
+// kept in registers across its rows (one store per block instead of a read-modify-write per row)
+constexpr int kMaxQ = 8, kRows4 = 16;
+
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ float4 ld4(const __hip_bfloat16* p) {
+  const uint2 r = *reinterpret_cast<const uint2*>(p);
+  return make_float4(__uint_as_float(r.x << 16), __uint_as_float(r.x & 0xffff0000u), __uint_as_float(r.y << 16),
+                     __uint_as_float(r.y & 0xffff0000u));
+}
+__device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+__device__ __forceinline__ void st4(__hip_bfloat16* p, float4 v) {
+  __hip_bfloat16 e[4] = {__float2bfloat16(v.x), __float2bfloat16(v.y), __float2bfloat16(v.z), __float2bfloat16(v.w)};
+  *reinterpret_cast<uint2*>(p) = *reinterpret_cast<const uint2*>(e);
+}
+
+template <typename T, typename W, typename O>
+__global__ __launch_bounds__(256) void rmsnorm_fwd4_kernel(const T* __restrict__ x, const W* __restrict__ w,
+                                                           O* __restrict__ y, float* __restrict__ rstd, int rows,
+                                                           int D, float eps) {
+  __shared__ float red[16];
+  const int row = blockIdx.x, DQ = D >> 2;
+  const T* xr = x + (size_t)row * D;
+  float4 v[kMaxQ];
+  float ss = 0.f;
+#pragma unroll
+  for (int k = 0; k < kMaxQ; ++k) {
+    const int q = threadIdx.x + k * 256;
+    if (q < DQ) {
+      v[k] = ld4(xr + 4 * q);
+      ss += v[k].x * v[k].x + v[k].y * v[k].y + v[k].z * v[k].z + v[k].w * v[k].w;
+    }
+  }
+  ss = cs::block_sum(ss, red);
+  const float r = rsqrtf(ss / (float)D + eps);
+  if (threadIdx.x == 0) rstd[row] = r;
+  O* yr = y + (size_t)row * D;
+#pragma unroll
+  for (int k = 0; k < kMaxQ; ++k) {
+    const int q = threadIdx.x + k * 256;
+    if (q < DQ) {
+      const float4 wv = ld4(w + 4 * q);
+      st4(yr + 4 * q, make_float4(v[k].x * r * wv.x, v[k].y * r * wv.y, v[k].z * r * wv.z, v[k].w * r * wv.w));
+    }
+  }
+}
+
+// kRows4 rows per block; dw_part[block][D] = sum over the block's rows of g*x*r
+template <typename T, typename W, typename G>
+__global__ __launch_bounds__(256) void rmsnorm_bwd4_kernel(const T* __restrict__ x, const W* __restrict__ w,
+                                                           const float* __restrict__ rstd, const G* __restrict__ g,
+                                                           T* __restrict__ dx, float* __restrict__ dw_part, int rows,
+                                                           int D) {
+  __shared__ float red[16];
+  const int DQ = D >> 2;
+  float4 wv[kMaxQ], acc[kMaxQ];
+#pragma unroll
+  for (int k = 0; k < kMaxQ; ++k) {
+    const int q = threadIdx.x + k * 256;
+    wv[k] = q < DQ ? ld4(w + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
+    acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  const int r0 = blockIdx.x * kRows4;
+  for (int rr = 0; rr < kRows4; ++rr) {
+    const int row = r0 + rr;
+    if (row >= rows) break;  // uniform across the block
+    const T* xr = x + (size_t)row * D;
+    const G* gr = g + (size_t)row * D;
+    float4 xv[kMaxQ], gv[kMaxQ];
+    float dot = 0.f;
+#pragma unroll
+    for (int k = 0; k < kMaxQ; ++k) {
+      const int q = threadIdx.x + k * 256;
+      if (q < DQ) {
+        xv[k] = ld4(xr + 4 * q);
+        gv[k] = ld4(gr + 4 * q);
+        dot += wv[k].x * gv[k].x * xv[k].x + wv[k].y * gv[k].y * xv[k].y + wv[k].z * gv[k].z * xv[k].z +
+               wv[k].w * gv[k].w * xv[k].w;
+      }
+    }
+    dot = cs::block_sum(dot, red);
+    const float r = rstd[row];
+    const float c = r * r * r * dot / (float)D;
+    T* dxr = dx + (size_t)row * D;
+#pragma unroll
+    for (int k = 0; k < kMaxQ; ++k) {
+      const int q = threadIdx.x + k * 256;
+      if (q < DQ) {
+        st4(dxr + 4 * q, make_float4(r * wv[k].x * gv[k].x - c * xv[k].x, r * wv[k].y * gv[k].y - c * xv[k].y,
+                                     r * wv[k].z * gv[k].z - c * xv[k].z, r * wv[k].w * gv[k].w - c * xv[k].w));
+        acc[k].x += gv[k].x * xv[k].x * r;
+        acc[k].y += gv[k].y * xv[k].y * r;
+        acc[k].z += gv[k].z * xv[k].z * r;
+        acc[k].w += gv[k].w * xv[k].w * r;
+      }
+    }
+  }
+  float* part = dw_part + (size_t)blockIdx.x * D;
+#pragma unroll
+  for (int k = 0; k < kMaxQ; ++k) {
+    const int q = threadIdx.x + k * 256;
+    if (q < DQ) st4(part + 4 * q, acc[k]);
+  }
+}
+
+// dw[4q..4q+3] = sum_p part[p][4q..]: 16 column quads x 16 partial lanes per block, lanes
+// combined through LDS in lane order (deterministic)
+template <typename W>
+__global__ __launch_bounds__(256) void colsum4_kernel(const float* __restrict__ part, int P, int D,
+                                                      W* __restrict__ dw) {
+  __shared__ float4 sh[16][16];
+  const int cq = threadIdx.x & 15, pl = threadIdx.x >> 4, q = blockIdx.x * 16 + cq;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (4 * q < D) {
+#pragma unroll 8
+    for (int p = pl; p < P; p += 16) {
+      const float4 v = ld4(part + (size_t)p * D + 4 * q);
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+  }
+  sh[pl][cq] = s;
+  __syncthreads();
+  if (pl != 0 || 4 * q >= D) return;
+  float4 t = sh[0][cq];
+  for (int l = 1; l < 16; ++l) {
+    t.x += sh[l][cq].x; t.y += sh[l][cq].y; t.z += sh[l][cq].z; t.w += sh[l][cq].w;
+  }
+  st4(dw + 4 * q, t);
+}
+
 template <typename W>
 __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ part, int P, int D,
                                                      W* __restrict__ dw) {
@@ -124,9 +255,13 @@ int grid_for(size_t n) {
   return (int)(b > 16384 ? 16384 : (b == 0 ? 1 : b));
 }
 
+bool use4(int D) { return D % 4 == 0 && D / 4 <= 256 * kMaxQ; }
+
 }  // namespace
 
-int cs_rmsnorm_bwd_partials(int rows) { return (rows + kRowsPerBlock - 1) / kRowsPerBlock; }
+int cs_rmsnorm_bwd_partials(int rows, int D) {
+  return use4(D) ? (rows + kRows4 - 1) / kRows4 : (rows + kRowsPerBlock - 1) / kRowsPerBlock;
+}
 
 #define CS_DT_DISPATCH(dt, ...)                                         \
   do {                                                                  \
@@ -141,9 +276,29 @@ int cs_rmsnorm_bwd_partials(int rows) { return (rows + kRowsPerBlock - 1) / kRow
     }                                                                   \
   } while (0)
 
-hipError_t cs_rmsnorm_fwd(int dt, int wdt, const void* x, const void* w, void* y, float* rstd, int rows, int D,
-                          float eps, hipStream_t s) {
+#define CS_DT_DISPATCH2(dt, U, ...)                                    \
+  do {                                                                  \
+    if ((dt) == CS_F32) {                                               \
+      using U = float;                                                  \
+      __VA_ARGS__;                                                      \
+    } else if ((dt) == CS_BF16) {                                       \
+      using U = __hip_bfloat16;                                         \
+      __VA_ARGS__;                                                      \
+    } else {                                                            \
+      return hipErrorInvalidValue;                                      \
+    }                                                                   \
+  } while (0)
+
+hipError_t cs_rmsnorm_fwd(int dt, int wdt, int odt, const void* x, const void* w, void* y, float* rstd, int rows,
+                          int D, float eps, hipStream_t s) {
   if (rows <= 0) return hipSuccess;
+  if (use4(D)) {
+    CS_DT_DISPATCH2(dt, T, CS_DT_DISPATCH2(wdt, Wt, CS_DT_DISPATCH2(odt, O,
+        hipLaunchKernelGGL((rmsnorm_fwd4_kernel<T, Wt, O>), dim3(rows), dim3(256), 0, s, (const T*)x, (const Wt*)w,
+                           (O*)y, rstd, rows, D, eps))));
+    return hipGetLastError();
+  }
+  if (odt != dt) return hipErrorInvalidValue;  // the scalar path writes the input's dtype
   if (wdt == CS_F32) {
     CS_DT_DISPATCH(dt, hipLaunchKernelGGL((rmsnorm_fwd_kernel<T, float>), dim3(rows), dim3(256), 0, s,
                                           (const T*)x, (const float*)w, (T*)y, rstd, rows, D, eps));
@@ -154,10 +309,19 @@ hipError_t cs_rmsnorm_fwd(int dt, int wdt, const void* x, const void* w, void* y
   return hipGetLastError();
 }
 
-hipError_t cs_rmsnorm_bwd(int dt, int wdt, const void* x, const void* w, const float* rstd, const void* g, void* dx,
-                          void* dw, float* part, int rows, int D, hipStream_t s) {
+hipError_t cs_rmsnorm_bwd(int dt, int wdt, int gdt, const void* x, const void* w, const float* rstd, const void* g,
+                          void* dx, void* dw, float* part, int rows, int D, hipStream_t s) {
   if (rows <= 0) return hipSuccess;
-  const int P = cs_rmsnorm_bwd_partials(rows);
+  const int P = cs_rmsnorm_bwd_partials(rows, D);
+  if (use4(D)) {
+    CS_DT_DISPATCH2(dt, T, CS_DT_DISPATCH2(wdt, Wt, CS_DT_DISPATCH2(gdt, G,
+        hipLaunchKernelGGL((rmsnorm_bwd4_kernel<T, Wt, G>), dim3(P), dim3(256), 0, s, (const T*)x, (const Wt*)w,
+                           rstd, (const G*)g, (T*)dx, part, rows, D))));
+    CS_DT_DISPATCH2(wdt, Wt, hipLaunchKernelGGL((colsum4_kernel<Wt>), dim3((D / 4 + 15) / 16), dim3(256), 0, s,
+                                                part, P, D, (Wt*)dw));
+    return hipGetLastError();
+  }
+  if (gdt != dt) return hipErrorInvalidValue;  // the scalar path reads the gradient in the input's dtype
   if (wdt == CS_F32) {
     CS_DT_DISPATCH(dt, hipLaunchKernelGGL((rmsnorm_bwd_kernel<T, float>), dim3(P), dim3(256), 0, s, (const T*)x,
                                           (const float*)w, rstd, (const T*)g, (T*)dx, part, rows, D));

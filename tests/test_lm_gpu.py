@@ -43,6 +43,26 @@ def test_rmsnorm(dev, dtype, shape):
                                atol=5e-2 if dtype == torch.bfloat16 else 1e-4)
 
 
+@pytest.mark.parametrize("shape", [(2, 9, 4096), (3, 1000), (5, 8192)])
+def test_rmsnorm_fp32_stream_bf16_out(dev, shape):
+    """under bf16 autocast: fp32 residual stream in, bf16 normalised activations out (no cast pass),
+    bf16 incoming gradient, fp32 dx and weight gradient"""
+    from cs744_pytorch_distributed_tutorial_amd.ops import lm
+    torch.manual_seed(1)
+    x = torch.randn(*shape, device=dev).requires_grad_()
+    w = (torch.rand(shape[-1], device=dev) + 0.5).requires_grad_()
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = lm.rms_norm(x, w, 1e-5)
+    assert y.dtype == torch.bfloat16
+    gy = torch.randn(shape, device=dev).bfloat16()
+    y.backward(gy)
+    assert x.grad.dtype == torch.float32 and w.grad.dtype == torch.float32
+    ry, (rgx, rgw) = _ref_grads(lambda a, b: lm.rms_norm_ref(a, b, 1e-5), [x, w], gy.float())
+    torch.testing.assert_close(y.float(), ry, rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(x.grad, rgx, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(w.grad, rgw, rtol=1e-4, atol=1e-3)
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_swiglu(dev, dtype):
     from cs744_pytorch_distributed_tutorial_amd.ops import lm
