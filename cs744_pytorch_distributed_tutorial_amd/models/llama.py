@@ -13,7 +13,9 @@ Hot ops have hand-written gfx950 kernels used on the GPU: RMSNorm fwd/bwd, SwiGL
 fwd/bwd and RoPE in ``ops.lm``, and causal grouped-query flash attention (forward and a
 deterministic backward, bf16, head dim 64/128) in ``ops.attention`` — called on the
 [B, S, H, D] projections directly, no transposes. The projection GEMMs are plain library
-GEMMs (hipBLASLt through ``nn.Linear``).
+GEMMs (hipBLASLt), run on bf16 copies of the fp32 master weights that the fused SGD pass
+rewrites (``ops.lm.ShadowLinear``): no per-step weight casts, fp32 weight gradients straight out
+of the GEMM.
 """
 from __future__ import annotations
 
@@ -51,6 +53,13 @@ def _ops():
     return lm
 
 
+def _Linear(*args, **kwargs) -> nn.Linear:
+    """bias-free projection: ``ops.lm.ShadowLinear`` (nn.Linear with a bf16 weight copy kept in step
+    with the fp32 master by the fused optimizer)"""
+    from ..ops.lm import ShadowLinear
+    return ShadowLinear(*args, **kwargs)
+
+
 class RMSNorm(nn.Module):
     def __init__(self, dim: int, eps: float = 1e-5):
         super().__init__()
@@ -72,10 +81,10 @@ class Attention(nn.Module):
         super().__init__()
         self.nh, self.nkv = cfg.n_heads, cfg.n_kv_heads
         self.hd = cfg.dim // cfg.n_heads
-        self.wq = nn.Linear(cfg.dim, self.nh * self.hd, bias=False)
-        self.wk = nn.Linear(cfg.dim, self.nkv * self.hd, bias=False)
-        self.wv = nn.Linear(cfg.dim, self.nkv * self.hd, bias=False)
-        self.wo = nn.Linear(self.nh * self.hd, cfg.dim, bias=False)
+        self.wq = _Linear(cfg.dim, self.nh * self.hd, bias=False)
+        self.wk = _Linear(cfg.dim, self.nkv * self.hd, bias=False)
+        self.wv = _Linear(cfg.dim, self.nkv * self.hd, bias=False)
+        self.wo = _Linear(self.nh * self.hd, cfg.dim, bias=False)
 
     def forward(self, x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
         B, S, _ = x.shape
@@ -95,9 +104,9 @@ class Attention(nn.Module):
 class FeedForward(nn.Module):
     def __init__(self, cfg: LlamaConfig):
         super().__init__()
-        self.w1 = nn.Linear(cfg.dim, cfg.ffn_dim, bias=False)  # gate
-        self.w3 = nn.Linear(cfg.dim, cfg.ffn_dim, bias=False)  # up
-        self.w2 = nn.Linear(cfg.ffn_dim, cfg.dim, bias=False)  # down
+        self.w1 = _Linear(cfg.dim, cfg.ffn_dim, bias=False)  # gate
+        self.w3 = _Linear(cfg.dim, cfg.ffn_dim, bias=False)  # up
+        self.w2 = _Linear(cfg.ffn_dim, cfg.dim, bias=False)  # down
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         return self.w2(_ops().swiglu(self.w1(x), self.w3(x)))
@@ -124,7 +133,7 @@ class Llama(nn.Module):
         self.tok_embeddings = nn.Embedding(cfg.vocab_size, cfg.dim)
         self.layers = nn.ModuleList(Block(cfg) for _ in range(cfg.n_layers))
         self.norm = RMSNorm(cfg.dim, cfg.norm_eps)
-        self.output = nn.Linear(cfg.dim, cfg.vocab_size, bias=False)
+        self.output = _Linear(cfg.dim, cfg.vocab_size, bias=False)
         std = 0.02
         for m in self.modules():
             if isinstance(m, nn.Linear):

@@ -104,3 +104,83 @@ def rope(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
     if _native_ok(x):
         return _RoPE.apply(x, cos, sin)
     return rope_ref(x, cos, sin)
+
+
+# ------------------------------------------------------------------ bf16 projections with fp32 masters
+class _LinearShadow(torch.autograd.Function):
+    """y = x @ W^T on the bf16 shadow of the fp32 master W; dW straight out of the GEMM in fp32"""
+
+    @staticmethod
+    def forward(ctx, x, weight, shadow):
+        x2 = x.reshape(-1, x.shape[-1])
+        with torch.autocast("cuda", enabled=False):
+            y = torch.mm(x2, shadow.t())
+        ctx.save_for_backward(x2, shadow)
+        ctx.xshape = x.shape
+        return y.view(*x.shape[:-1], shadow.shape[0])
+
+    @staticmethod
+    def backward(ctx, gy):
+        x2, shadow = ctx.saved_tensors
+        g2 = gy.reshape(-1, gy.shape[-1])
+        if g2.dtype != shadow.dtype:
+            g2 = g2.to(shadow.dtype)
+        dx = dw = None
+        with torch.autocast("cuda", enabled=False):
+            if ctx.needs_input_grad[0]:
+                dx = torch.mm(g2, shadow).view(ctx.xshape)
+            if ctx.needs_input_grad[1]:
+                dw = torch.mm(g2.t(), x2, out_dtype=torch.float32)
+        return dx, dw, None
+
+
+class ShadowLinear(torch.nn.Linear):
+    """``nn.Linear`` (same parameters and state_dict) whose bf16-autocast forward reads a bf16 copy
+    of the fp32 weight kept alongside it instead of casting the weight at every use. ``FusedSGD``
+    rewrites the copy in its update pass (``sgd_multi`` shadow column), so a training step spends no
+    cast kernel on the weights at all, and the weight gradient leaves the GEMM in fp32 (no bf16
+    round trip, no cast back). Any other in-place change of the weight (load_state_dict, a DDP
+    broadcast, another optimizer) bumps its version and the copy is re-made on the next forward."""
+
+    def _shadow(self) -> torch.Tensor:
+        w = self.weight
+        sh = getattr(w, "_cs_bf16_shadow", None)
+        if sh is None or getattr(w, "_cs_bf16_shadow_version", -1) != w._version or sh.device != w.device \
+                or sh.shape != w.shape:
+            with torch.no_grad():
+                sh = w.detach().to(torch.bfloat16)
+            w._cs_bf16_shadow = sh
+            w._cs_bf16_shadow_version = w._version
+        return sh
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if (self.bias is None and x.is_cuda and self.weight.dtype == torch.float32 and torch.is_autocast_enabled("cuda")
+                and torch.get_autocast_dtype("cuda") == torch.bfloat16):
+            return _LinearShadow.apply(x.to(torch.bfloat16), self.weight, self._shadow())
+        return super().forward(x)
+
+
+# ------------------------------------------------------------------ LM loss
+class _CrossEntropy(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, targets):
+        loss, lse = native.C().xent_fwd(logits, targets)
+        ctx.save_for_backward(logits, targets, lse)
+        return loss.sum() / logits.shape[0]
+
+    @staticmethod
+    def backward(ctx, g):
+        logits, targets, lse = ctx.saved_tensors
+        d = native.C().xent_bwd(logits, targets, lse, g.float().reshape(1).contiguous(), 1.0 / logits.shape[0])
+        return d, None
+
+
+def cross_entropy(logits: torch.Tensor, targets: torch.Tensor) -> torch.Tensor:
+    """``F.cross_entropy(logits.float(), targets)`` (mean over rows) for [R, V] logits: on GPU one
+    fused gfx950 pass forward and one backward over the logits in their own dtype (no fp32 upcast of
+    the [tokens, vocab] matrix, no separate log-softmax / nll / cast kernels). Targets must lie in
+    [0, V) (no ignore index; the LM's synthetic tokens always do)."""
+    if (logits.is_cuda and logits.dim() == 2 and logits.shape[1] % 8 == 0
+            and logits.dtype in (torch.float32, torch.bfloat16)):
+        return _CrossEntropy.apply(logits.contiguous(), targets.contiguous())
+    return torch.nn.functional.cross_entropy(logits.float(), targets)

@@ -12,6 +12,20 @@ import torch
 from . import native
 
 
+_NO_SHADOW = {}
+
+
+def _shadow_of(p: torch.Tensor) -> torch.Tensor:
+    """the live bf16 shadow of ``p`` (registered by ``ops.lm.ShadowLinear``), or an empty tensor"""
+    sh = getattr(p, "_cs_bf16_shadow", None)
+    if sh is not None and getattr(p, "_cs_bf16_shadow_version", -1) == p._version and sh.numel() == p.numel():
+        return sh
+    dev = p.device
+    if dev not in _NO_SHADOW:
+        _NO_SHADOW[dev] = torch.empty(0, device=dev, dtype=torch.bfloat16)
+    return _NO_SHADOW[dev]
+
+
 class FusedSGD(torch.optim.SGD):
     def __init__(self, params, lr=0.1, momentum=0.0, dampening=0.0, weight_decay=0.0, nesterov=False,
                  grad_scale: float = 1.0):
@@ -44,10 +58,13 @@ class FusedSGD(torch.optim.SGD):
                     first = True
                 bufs.append(st["momentum_buffer"])
             gs = [p.grad for p in ps]
-            key = tuple((p.data_ptr(), g.data_ptr(), b.data_ptr()) for p, g, b in zip(ps, gs, bufs))
+            # a parameter with a live bf16 shadow (ops.lm.ShadowLinear) gets it rewritten by the same pass
+            shs = [_shadow_of(p) for p in ps]
+            key = tuple((p.data_ptr(), g.data_ptr(), b.data_ptr(), s.data_ptr() if s.numel() else 0)
+                        for p, g, b, s in zip(ps, gs, bufs, shs))
             tab = self._tables.get(id(group))
             if tab is None or tab[0] != key:
-                t = native.C().sgd_multi_table(ps, gs, bufs)
+                t = native.C().sgd_multi_table(ps, gs, bufs, shs)
                 nchunks = int(t[-1].item())
                 tab = (key, t, nchunks)
                 self._tables[id(group)] = tab

@@ -123,8 +123,9 @@ class TorchTrainer:
         self.opt.zero_grad()  # DDP re-attaches its bucket views (and zeroes them) in forward
         with torch.autocast("cuda", dtype=torch.bfloat16, enabled=self.dtype == "bf16"):
             out = self.net(x)
-            if self.is_lm:
-                loss = self.crit(out.float().view(-1, out.shape[-1]), y.view(-1))
+            if self.is_lm:  # fused gfx950 softmax cross-entropy over the bf16 logits (ops.lm)
+                from ..ops.lm import cross_entropy
+                loss = cross_entropy(out.view(-1, out.shape[-1]), y.view(-1))
             else:
                 loss = self.crit(out.float(), y)
         loss.backward()

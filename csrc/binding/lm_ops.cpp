@@ -48,6 +48,34 @@ std::vector<torch::Tensor> rmsnorm_bwd(torch::Tensor x, torch::Tensor w, torch::
   return {dx, dw};
 }
 
+// logits [R, V], targets [R] int64 -> {loss_rows [R] f32, lse [R] f32}
+std::vector<torch::Tensor> xent_fwd(torch::Tensor logits, torch::Tensor tgt) {
+  check(logits, "logits");
+  TORCH_CHECK(logits.dim() == 2 && logits.size(1) % 8 == 0, "xent: logits [R, V] with V % 8 == 0");
+  TORCH_CHECK(tgt.is_cuda() && tgt.is_contiguous() && tgt.scalar_type() == at::kLong && tgt.numel() == logits.size(0),
+              "xent: targets [R] int64");
+  DevGuard g(logits.device());
+  auto fo = logits.options().dtype(at::kFloat);
+  auto loss = torch::empty({logits.size(0)}, fo), lse = torch::empty({logits.size(0)}, fo);
+  CS_LAUNCH(cs_xent_fwd(dt_of(logits), logits.data_ptr(), tgt.data_ptr<int64_t>(), loss.data_ptr<float>(),
+                        lse.data_ptr<float>(), (int)logits.size(0), (int)logits.size(1), cur_stream()));
+  return {loss, lse};
+}
+
+torch::Tensor xent_bwd(torch::Tensor logits, torch::Tensor tgt, torch::Tensor lse, torch::Tensor gscale, double inv_n) {
+  check(logits, "logits");
+  check(lse, "lse");
+  TORCH_CHECK(logits.dim() == 2 && logits.size(1) % 8 == 0 && lse.numel() == logits.size(0), "xent_bwd: shapes");
+  TORCH_CHECK(tgt.is_cuda() && tgt.scalar_type() == at::kLong && tgt.numel() == logits.size(0), "xent_bwd: targets");
+  TORCH_CHECK(gscale.is_cuda() && gscale.scalar_type() == at::kFloat && gscale.numel() == 1, "xent_bwd: g");
+  DevGuard g(logits.device());
+  auto d = torch::empty_like(logits);
+  CS_LAUNCH(cs_xent_bwd(dt_of(logits), logits.data_ptr(), tgt.data_ptr<int64_t>(), lse.data_ptr<float>(),
+                        gscale.data_ptr<float>(), (float)inv_n, d.data_ptr(), (int)logits.size(0), (int)logits.size(1),
+                        cur_stream()));
+  return d;
+}
+
 torch::Tensor swiglu_fwd(torch::Tensor a, torch::Tensor b) {
   check(a, "a"); check(b, "b");
   TORCH_CHECK(a.sizes() == b.sizes() && a.scalar_type() == b.scalar_type(), "swiglu: a/b mismatch");
@@ -126,6 +154,8 @@ std::vector<torch::Tensor> attn_bwd(torch::Tensor q, torch::Tensor k, torch::Ten
 void register_lm_ops(pybind11::module& m) {
   m.def("rmsnorm_fwd", &rmsnorm_fwd);
   m.def("rmsnorm_bwd", &rmsnorm_bwd);
+  m.def("xent_fwd", &xent_fwd, "softmax cross-entropy rows -> (loss, lse)");
+  m.def("xent_bwd", &xent_bwd, "its backward -> dlogits");
   m.def("swiglu_fwd", &swiglu_fwd);
   m.def("swiglu_bwd", &swiglu_bwd);
   m.def("rope", &rope);

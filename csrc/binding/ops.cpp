@@ -47,11 +47,14 @@ void sgd_flat(torch::Tensor p, torch::Tensor g, torch::Tensor m, double lr, doub
 
 // Builds the device table {p,g,m,n} + chunk prefix once per distinct pointer set; returns it
 // as an int64 tensor the caller caches. Layout: [ntens*4 entries | ntens chunk starts | nchunks].
+// shadows (optional): per parameter a bf16 tensor of the same layout that the update rewrites
+// with the new value, or an empty tensor for none
 torch::Tensor sgd_multi_table(std::vector<torch::Tensor> ps, std::vector<torch::Tensor> gs,
-                              std::vector<torch::Tensor> ms) {
+                              std::vector<torch::Tensor> ms, c10::optional<std::vector<torch::Tensor>> shadows) {
   TORCH_CHECK(ps.size() == gs.size() && ps.size() == ms.size() && !ps.empty(), "sgd_multi_table: list sizes");
+  TORCH_CHECK(!shadows.has_value() || shadows->size() == ps.size(), "sgd_multi_table: shadow list size");
   const int64_t nt = ps.size();
-  auto host = torch::empty({nt * 4 + nt + 1}, torch::kLong);
+  auto host = torch::empty({nt * 5 + nt + 1}, torch::kLong);
   int64_t* h = host.data_ptr<int64_t>();
   int64_t chunks = 0;
   for (int64_t i = 0; i < nt; ++i) {
@@ -64,24 +67,34 @@ torch::Tensor sgd_multi_table(std::vector<torch::Tensor> ps, std::vector<torch::
     TORCH_CHECK(ps[i].strides() == gs[i].strides() && ps[i].strides() == ms[i].strides(),
                 "sgd_multi_table: param, grad and momentum must share one memory layout");
     TORCH_CHECK(ps[i].numel() == gs[i].numel() && ps[i].numel() == ms[i].numel(), "sgd_multi_table: numel");
-    h[i * 4 + 0] = (int64_t)ps[i].data_ptr<float>();
-    h[i * 4 + 1] = (int64_t)gs[i].data_ptr<float>();
-    h[i * 4 + 2] = (int64_t)ms[i].data_ptr<float>();
-    h[i * 4 + 3] = ps[i].numel();
-    h[nt * 4 + i] = chunks;
+    int64_t sh = 0;
+    if (shadows.has_value() && (*shadows)[i].numel() > 0) {
+      const auto& t = (*shadows)[i];
+      CS_CHECK_CUDA(t);
+      TORCH_CHECK(t.scalar_type() == at::kBFloat16 && t.numel() == ps[i].numel() && t.strides() == ps[i].strides(),
+                  "sgd_multi_table: a shadow must be a bf16 tensor laid out like its parameter");
+      sh = (int64_t)t.data_ptr();
+    }
+    h[i * 5 + 0] = (int64_t)ps[i].data_ptr<float>();
+    h[i * 5 + 1] = (int64_t)gs[i].data_ptr<float>();
+    h[i * 5 + 2] = (int64_t)ms[i].data_ptr<float>();
+    h[i * 5 + 3] = ps[i].numel();
+    h[i * 5 + 4] = sh;
+    h[nt * 5 + i] = chunks;
     chunks += (ps[i].numel() + 4095) / 4096;
   }
-  h[nt * 5] = chunks;
+  h[nt * 6] = chunks;
   return host.to(ps[0].device());
 }
 
 void sgd_multi(torch::Tensor table, int64_t ntens, int64_t nchunks, double lr, double mom, double wd, double damp,
                double scale, bool first) {
   CS_CHECK_CUDA(table);
-  TORCH_CHECK(table.scalar_type() == at::kLong && table.numel() == ntens * 5 + 1, "sgd_multi: bad table");
+  TORCH_CHECK(table.scalar_type() == at::kLong && table.numel() == ntens * 6 + 1, "sgd_multi: bad table");
+  static_assert(sizeof(CsTensorEntry) == 5 * sizeof(int64_t), "CsTensorEntry: five 8-byte fields");
   DevGuard gd(table.device());
   const int64_t* t = table.data_ptr<int64_t>();
-  CS_LAUNCH(cs_sgd_multi(reinterpret_cast<const CsTensorEntry*>(t), (int)ntens, t + ntens * 4, (int)nchunks,
+  CS_LAUNCH(cs_sgd_multi(reinterpret_cast<const CsTensorEntry*>(t), (int)ntens, t + ntens * 5, (int)nchunks,
                          (float)lr, (float)mom, (float)wd, (float)damp, (float)scale, first ? 1 : 0, cur_stream()));
 }
 
@@ -161,7 +174,8 @@ PYBIND11_MODULE(_C, m) {
   m.doc() = "gfx950 (MI355X) kernels + native runtime for cs744_pytorch_distributed_tutorial_amd";
   m.def("augment", &augment, "fused CIFAR gather+crop+flip+normalize");
   m.def("sgd_flat", &sgd_flat, "fused SGD on flat buffers");
-  m.def("sgd_multi_table", &sgd_multi_table, "build the multi-tensor SGD table");
+  m.def("sgd_multi_table", &sgd_multi_table, "build the multi-tensor SGD table", pybind11::arg("ps"), pybind11::arg("gs"),
+        pybind11::arg("ms"), pybind11::arg("shadows") = pybind11::none());
   m.def("sgd_multi", &sgd_multi, "multi-tensor fused SGD");
   m.def("rows_mean", &rows_mean, "mean over the rows of a [rows, n] buffer (part2a root)", pybind11::arg("src"),
         pybind11::arg("rows"), pybind11::arg("dst"), pybind11::arg("bcast") = false);

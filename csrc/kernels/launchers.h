@@ -9,6 +9,7 @@ struct CsTensorEntry {
   float* g;
   float* m;
   int64_t n;
+  uint16_t* shadow;  // optional bf16 copy of p, rewritten by the update (the bf16 GEMMs' operand)
 };
 
 // data pipeline
@@ -178,6 +179,12 @@ hipError_t cs_rmsnorm_fwd(int dt, int wdt, int odt, const void* x, const void* w
 // part: [cs_rmsnorm_bwd_partials(rows, D)][D] fp32 scratch; dw has the weight's dtype, g dtype gdt, dx x's
 hipError_t cs_rmsnorm_bwd(int dt, int wdt, int gdt, const void* x, const void* w, const float* rstd, const void* g,
                           void* dx, void* dw, float* part, int rows, int D, hipStream_t s);
+// softmax cross-entropy, logits [R, V] fp32/bf16 with V % 8 == 0, targets in [0, V): per-row loss and
+// log-sum-exp; backward dlogits = (softmax - onehot) * g[0] * inv_n in the logits' dtype
+hipError_t cs_xent_fwd(int dt, const void* logits, const int64_t* tgt, float* loss, float* lse, int R, int V,
+                       hipStream_t s);
+hipError_t cs_xent_bwd(int dt, const void* logits, const int64_t* tgt, const float* lse, const float* g, float inv_n,
+                       void* dlogits, int R, int V, hipStream_t s);
 hipError_t cs_swiglu_fwd(int dt, const void* a, const void* b, void* out, size_t n, hipStream_t s);
 hipError_t cs_swiglu_bwd(int dt, const void* a, const void* b, const void* g, void* da, void* db, size_t n,
                          hipStream_t s);

@@ -255,6 +255,93 @@ int grid_for(size_t n) {
   return (int)(b > 16384 ? 16384 : (b == 0 ? 1 : b));
 }
 
+// ---- softmax cross-entropy over bf16 / fp32 logits [R, V] (V % 8 == 0), mean over rows:
+// forward = one read of the logits (online max / sum-exp per row: 8-element vectors, wave
+// shuffles, then the 4 waves in order) -> per-row loss and log-sum-exp; backward = one more read
+// and one write: dlogits = (softmax - onehot) * g / R, with the upstream scalar g read on device.
+// Replaces the fp32 upcast + log_softmax + nll (and their backward) of nn.CrossEntropyLoss.
+__device__ __forceinline__ void ms_combine(float& m, float& s, float m2, float s2) {
+  if (m2 == -INFINITY) return;
+  if (m == -INFINITY) {
+    m = m2;
+    s = s2;
+    return;
+  }
+  if (m2 > m) {
+    s = s * __expf(m - m2) + s2;
+    m = m2;
+  } else {
+    s += s2 * __expf(m2 - m);
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void ld8(const T* p, float (&v)[8]) {
+  const float4 a = ld4(p), b = ld4(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void xent_fwd_kernel(const T* __restrict__ logits, const int64_t* __restrict__ tgt,
+                                                       float* __restrict__ loss, float* __restrict__ lse, int V) {
+  __shared__ float sm[4], ss[4];
+  const int row = blockIdx.x;
+  const T* x = logits + (size_t)row * V;
+  float m = -INFINITY, s = 0.f;
+  for (int i = threadIdx.x * 8; i < V; i += 256 * 8) {
+    float v[8];
+    ld8(x + i, v);
+    float vm = v[0];
+#pragma unroll
+    for (int j = 1; j < 8; ++j) vm = fmaxf(vm, v[j]);
+    float vs = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) vs += __expf(v[j] - vm);
+    ms_combine(m, s, vm, vs);
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const float m2 = __shfl_xor(m, off, 64), s2 = __shfl_xor(s, off, 64);
+    ms_combine(m, s, m2, s2);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    sm[threadIdx.x >> 6] = m;
+    ss[threadIdx.x >> 6] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  m = sm[0];
+  s = ss[0];
+  for (int w = 1; w < 4; ++w) ms_combine(m, s, sm[w], ss[w]);
+  const float l = m + __logf(s);
+  lse[row] = l;
+  const int64_t t = tgt[row];
+  loss[row] = (t >= 0 && t < V) ? l - ld(x, (size_t)t) : NAN;  // an out-of-range target poisons the loss
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void xent_bwd_kernel(const T* __restrict__ logits, const int64_t* __restrict__ tgt,
+                                                       const float* __restrict__ lse, const float* __restrict__ g,
+                                                       float inv_n, T* __restrict__ dlogits, int V) {
+  const int row = blockIdx.x;
+  const T* x = logits + (size_t)row * V;
+  T* d = dlogits + (size_t)row * V;
+  const float l = lse[row], scale = g[0] * inv_n;
+  const int64_t t = tgt[row];
+  for (int i = threadIdx.x * 8; i < V; i += 256 * 8) {
+    float v[8];
+    ld8(x + i, v);
+    float4 a, b;
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (__expf(v[j] - l) - (i + j == t ? 1.f : 0.f)) * scale;
+    a = make_float4(o[0], o[1], o[2], o[3]);
+    b = make_float4(o[4], o[5], o[6], o[7]);
+    st4(d + i, a);
+    st4(d + i + 4, b);
+  }
+}
+
 bool use4(int D) { return D % 4 == 0 && D / 4 <= 256 * kMaxQ; }
 
 }  // namespace
@@ -333,6 +420,24 @@ hipError_t cs_rmsnorm_bwd(int dt, int wdt, int gdt, const void* x, const void* w
     hipLaunchKernelGGL((colsum_kernel<__hip_bfloat16>), dim3((D + 255) / 256), dim3(256), 0, s, part, P, D,
                        (__hip_bfloat16*)dw);
   }
+  return hipGetLastError();
+}
+
+hipError_t cs_xent_fwd(int dt, const void* logits, const int64_t* tgt, float* loss, float* lse, int R, int V,
+                       hipStream_t s) {
+  if (R <= 0) return hipSuccess;
+  if (V % 8 != 0) return hipErrorInvalidValue;
+  CS_DT_DISPATCH(dt, hipLaunchKernelGGL((xent_fwd_kernel<T>), dim3(R), dim3(256), 0, s, (const T*)logits, tgt, loss,
+                                        lse, V));
+  return hipGetLastError();
+}
+
+hipError_t cs_xent_bwd(int dt, const void* logits, const int64_t* tgt, const float* lse, const float* g, float inv_n,
+                       void* dlogits, int R, int V, hipStream_t s) {
+  if (R <= 0) return hipSuccess;
+  if (V % 8 != 0) return hipErrorInvalidValue;
+  CS_DT_DISPATCH(dt, hipLaunchKernelGGL((xent_bwd_kernel<T>), dim3(R), dim3(256), 0, s, (const T*)logits, tgt, lse, g,
+                                        inv_n, (T*)dlogits, V));
   return hipGetLastError();
 }
 

@@ -75,6 +75,10 @@ __global__ __launch_bounds__(256) void sgd_multi_kernel(const CsTensorEntry* __r
       sgd1(pv, e.g[i], mv, a);
       e.p[i] = pv;
       if (a.mom != 0.f) e.m[i] = mv;
+      if (e.shadow != nullptr) {  // round-to-nearest-even bf16 of the new value (NaN kept quiet)
+        const uint32_t u = __float_as_uint(pv);
+        e.shadow[i] = (pv != pv) ? (uint16_t)((u >> 16) | 0x40u) : (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+      }
     }
   }
 }

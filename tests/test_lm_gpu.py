@@ -109,3 +109,57 @@ def test_resnet50_step(dev):
     tr.step()
     tr.step()
     assert tr.last_loss() == tr.last_loss()
+
+
+def test_shadow_linear_matches_autocast_linear_and_sgd_keeps_shadow(dev):
+    """ShadowLinear under bf16 autocast == nn.Linear under autocast (same bf16 GEMM), fp32 weight
+    gradient at least as accurate; FusedSGD rewrites the bf16 shadow with the updated weight (bit-equal
+    to a fresh cast), and an in-place weight change outside the optimizer invalidates it"""
+    from cs744_pytorch_distributed_tutorial_amd.ops.lm import ShadowLinear
+    from cs744_pytorch_distributed_tutorial_amd.ops.optim import FusedSGD
+    torch.manual_seed(3)
+    a = ShadowLinear(256, 384, bias=False).to(dev)
+    b = torch.nn.Linear(256, 384, bias=False).to(dev)
+    b.load_state_dict(a.state_dict())
+    x = torch.randn(2, 64, 256, device=dev)
+    gy = torch.randn(2, 64, 384, device=dev)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        ya, yb = a(x), b(x)
+    assert ya.dtype == yb.dtype == torch.bfloat16
+    assert torch.equal(ya, yb)
+    ya.backward(gy.bfloat16())
+    yb.backward(gy.bfloat16())
+    ref = gy.bfloat16().reshape(-1, 384).t().double() @ x.bfloat16().double().reshape(-1, 256)
+    assert a.weight.grad.dtype == torch.float32
+    err_a = (a.weight.grad.double() - ref).norm() / ref.norm()
+    err_b = (b.weight.grad.double() - ref).norm() / ref.norm()
+    assert err_a <= err_b + 1e-6 and err_a < 1e-5, (float(err_a), float(err_b))
+    opt = FusedSGD(a.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+    opt.step()
+    sh = a.weight._cs_bf16_shadow
+    assert torch.equal(sh, a.weight.detach().to(torch.bfloat16))
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        a(x)
+    assert a.weight._cs_bf16_shadow is sh  # still valid: the fused pass kept it in step
+    with torch.no_grad():
+        a.weight.mul_(0.5)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        a(x)
+    assert torch.equal(a.weight._cs_bf16_shadow, a.weight.detach().to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("R,V", [(64, 1024), (7, 128256), (33, 8)])
+def test_cross_entropy_matches_torch(dev, dtype, R, V):
+    from cs744_pytorch_distributed_tutorial_amd.ops.lm import cross_entropy
+    torch.manual_seed(R)
+    x = (torch.randn(R, V, device=dev) * 3).to(dtype).requires_grad_()
+    t = torch.randint(0, V, (R,), device=dev)
+    loss = cross_entropy(x, t)
+    xr = x.detach().double().requires_grad_()
+    ref = torch.nn.functional.cross_entropy(xr, t)
+    torch.testing.assert_close(loss.double(), ref, rtol=1e-5, atol=1e-5)
+    (2.5 * loss).backward()
+    (2.5 * ref).backward()
+    tol = dict(rtol=1e-4, atol=1e-6) if dtype == torch.float32 else dict(rtol=1e-2, atol=1e-4)
+    torch.testing.assert_close(x.grad.double(), xr.grad, **tol)
