@@ -193,8 +193,6 @@ def main(argv=None) -> int:
         out["config"]["conv_gemm_math"] = {m: maths.count(m) for m in sorted(set(maths))}
         out["config"]["conv_tiles"] = getattr(trainer, "tile_source", None)
         out["config"]["wgrad_side_stream"] = getattr(trainer, "overlap_wgrad", None)
-    if getattr(trainer, "gemm_table", None):
-        out["config"]["gemm_table"] = os.path.relpath(trainer.gemm_table, os.path.dirname(os.path.abspath(__file__)))
     if args.phases > 0 and hasattr(trainer, "phase_breakdown"):
         ph = trainer.phase_breakdown(args.phases)
         if rank == 0:

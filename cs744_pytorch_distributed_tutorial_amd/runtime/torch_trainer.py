@@ -42,31 +42,6 @@ def build_model(name: str) -> nn.Module:
     raise ValueError(f"unknown model {name!r}")
 
 
-GEMM_TABLES = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemm_tables")
-
-
-def load_gemm_table(model: str) -> Optional[str]:
-    """Offline-tuned GEMM solutions for ``model`` on gfx950 (PyTorch TunableOp: per GEMM shape, the
-    fastest of the hipBLASLt / rocBLAS solutions, timed on MI355X; ``scripts/gpu_r2_tune2.sh``): enabled
-    read-only, so the step never searches. Measured isolated on MI355X: the Llama-3-8B [8192 x 4096] x
-    [4096 x 4096] forward GEMM 224.6 us with hipBLASLt's heuristic pick vs 134.5 us tuned. A table whose
-    validators (HIP / hipBLASLt / rocBLAS versions, arch) do not match the runtime is ignored by torch.
-    ``CS744_GEMM_TABLE=0`` turns it off."""
-    if os.environ.get("CS744_GEMM_TABLE", "1") == "0" or not torch.cuda.is_available():
-        return None
-    arch = torch.cuda.get_device_properties(torch.cuda.current_device()).gcnArchName.split(":")[0]
-    path = os.path.join(GEMM_TABLES, f"tunableop_{arch}_{model.lower().replace('-', '')}.csv")
-    if not os.path.exists(path):
-        return None
-    import tempfile
-    import torch.cuda.tunable as tunable
-    tunable.enable(True)
-    tunable.tuning_enable(False)
-    # results are written back at exit: keep that copy out of the repository
-    tunable.set_filename(os.path.join(tempfile.gettempdir(), f"cs744_tunableop_{os.getpid()}_%d.csv"))
-    return path if tunable.read_file(path) else None
-
-
 class SyntheticBatches:
     """A pool of random, fixed, device-resident samples; each step gathers a random batch.
 
@@ -116,7 +91,6 @@ class TorchTrainer:
         self.model_name = model
         self.module = build_model(model).to(device)
         self.is_lm = hasattr(self.module, "vocab_size")
-        self.gemm_table = load_gemm_table(model) if device.type == "cuda" else None
         self.channels_last = not self.is_lm and os.environ.get("CS744_CHANNELS_LAST", "0") == "1"
         if self.channels_last:
             self.module = self.module.to(memory_format=torch.channels_last)
