@@ -281,16 +281,16 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(const __bf16* __restric
 }
 
 template <int D>
-__global__ __launch_bounds__(256, 2) void attn_dq_kernel(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
+__device__ __forceinline__ void dq_body(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
                                                       const __bf16* __restrict__ v, const __bf16* __restrict__ dout,
                                                       const float* __restrict__ lse, const float* __restrict__ delta,
                                                       __bf16* __restrict__ dq, int S, int Hq, int Hkv, float c,
-                                                      float scale, int causal) {
+                                                      float scale, int causal, int bx, int by, int bz) {
   constexpr int KK = D / 16, DT = D / 32, TILE = kBN * D * 2;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nqb = (S + kBM - 1) / kBM;
-  const int qb = nqb - 1 - (int)blockIdx.x;
-  const int hq = blockIdx.y, b = blockIdx.z, hk = hq / (Hq / Hkv);
+  const int qb = nqb - 1 - bx;
+  const int hq = by, b = bz, hk = hq / (Hq / Hkv);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
   const int q0 = qb * kBM, q0w = q0 + 32 * w, qi = q0w + r;
   const size_t qs = (size_t)Hq * D, ks = (size_t)Hkv * D;
@@ -358,18 +358,27 @@ __global__ __launch_bounds__(256, 2) void attn_dq_kernel(const __bf16* __restric
 }
 
 template <int D>
-__global__ __launch_bounds__(256) void attn_dkdv_kernel(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
+__global__ __launch_bounds__(256, 2) void attn_dq_kernel(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
+                                                      const __bf16* __restrict__ v, const __bf16* __restrict__ dout,
+                                                      const float* __restrict__ lse, const float* __restrict__ delta,
+                                                      __bf16* __restrict__ dq, int S, int Hq, int Hkv, float c,
+                                                      float scale, int causal) {
+  dq_body<D>(q, k, v, dout, lse, delta, dq, S, Hq, Hkv, c, scale, causal, blockIdx.x, blockIdx.y, blockIdx.z);
+}
+
+template <int D>
+__device__ __forceinline__ void dkdv_body(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
                                                         const __bf16* __restrict__ v, const __bf16* __restrict__ dout,
                                                         const float* __restrict__ lse, const float* __restrict__ delta,
                                                         __bf16* __restrict__ dk, __bf16* __restrict__ dv, int S, int Hq,
-                                                        int Hkv, float c, float scale, int causal) {
+                                                        int Hkv, float c, float scale, int causal, int bx, int by, int bz) {
   constexpr int KK = D / 16, DT = D / 32, TILE = kBN * D * 2;
   // [2 buffers][Q image, dO image, L2[64], delta[64]]
   constexpr int BUF = 2 * TILE + 2 * kBN * 4;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nkb = (S + kBM - 1) / kBM;
-  const int kb = causal ? (int)blockIdx.x : nkb - 1 - (int)blockIdx.x;  // causal: early keys see the most queries
-  const int hk = blockIdx.y, b = blockIdx.z, grp = Hq / Hkv;
+  const int kb = causal ? bx : nkb - 1 - bx;  // causal: early keys see the most queries
+  const int hk = by, b = bz, grp = Hq / Hkv;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
   const int kw0 = kb * kBM + 32 * w, kj = kw0 + r;  // this lane's key (the accumulator column)
   const size_t qs = (size_t)Hq * D, ks = (size_t)Hkv * D;
@@ -455,6 +464,56 @@ __global__ __launch_bounds__(256) void attn_dkdv_kernel(const __bf16* __restrict
 }
 
 template <int D>
+__global__ __launch_bounds__(256) void attn_dkdv_kernel(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
+                                                        const __bf16* __restrict__ v, const __bf16* __restrict__ dout,
+                                                        const float* __restrict__ lse, const float* __restrict__ delta,
+                                                        __bf16* __restrict__ dk, __bf16* __restrict__ dv, int S, int Hq,
+                                                        int Hkv, int B, float c, float scale, int causal) {
+  // 1-D grid, key block slowest-varying: every head's heaviest (earliest, causal) key blocks dispatch
+  // first. At one wave per SIMD (356 VGPR+AGPR) the 512 blocks of the Llama-3-8B shape run in two
+  // rounds on 256 CUs; heaviest-first keeps the second round from starting with a 16x-longer block.
+  const int L = (int)blockIdx.x;
+  dkdv_body<D>(q, k, v, dout, lse, delta, dk, dv, S, Hq, Hkv, c, scale, causal, L / (Hkv * B), L % Hkv,
+               (L / Hkv) % B);
+}
+
+// Causal backward in ONE launch: the dK/dV blocks first (key block ascending = most query tiles
+// first), then the dQ blocks (latest query block first). A dK/dV block of an early key block
+// walks up to 16x the query tiles of a late one, so run alone that kernel leaves most CUs idle
+// in its tail; here the dQ blocks (independent: they write only dQ) fill those CUs as the short
+// dK/dV blocks retire. Same bodies, same arithmetic, same results as the two launches.
+template <int D>
+__global__ __launch_bounds__(256) void attn_bwd_fused_kernel(const __bf16* __restrict__ q, const __bf16* __restrict__ k,
+                                                             const __bf16* __restrict__ v,
+                                                             const __bf16* __restrict__ dout,
+                                                             const float* __restrict__ lse,
+                                                             const float* __restrict__ delta, __bf16* __restrict__ dq,
+                                                             __bf16* __restrict__ dk, __bf16* __restrict__ dv, int S,
+                                                             int Hq, int Hkv, int B, float c, float scale, int causal) {
+  const int nb = (S + kBM - 1) / kBM;
+  const int n_kv = nb * Hkv * B;
+  int L = (int)blockIdx.x;
+  if (L < n_kv) {  // key block slowest-varying: all heads' heaviest key blocks dispatch first
+    dkdv_body<D>(q, k, v, dout, lse, delta, dk, dv, S, Hq, Hkv, c, scale, causal, L / (Hkv * B), L % Hkv,
+                 (L / Hkv) % B);
+  } else {
+    L -= n_kv;
+    dq_body<D>(q, k, v, dout, lse, delta, dq, S, Hq, Hkv, c, scale, causal, L / (Hq * B), L % Hq, (L / Hq) % B);
+  }
+}
+
+// The causal backward runs as one launch (attn_bwd_fused_kernel) by default; CS_ATTN_BWD_FUSED=0 gives
+// dQ then dK/dV (heaviest-first grid). Llama-3-8B step on MI355X: two launches in grid order 18.79k
+// tokens/s (dK/dV 1156 us), heaviest-first 19.76k (dK/dV 645 us), one launch 20.12k.
+bool attn_bwd_fused() {
+  static const bool on = [] {
+    const char* e = getenv("CS_ATTN_BWD_FUSED");
+    return e == nullptr || atoi(e) != 0;
+  }();
+  return on;
+}
+
+template <int D>
 size_t fwd_lds() { return 2 * 2 * (size_t)kBN * D * 2; }
 template <int D>
 size_t dkdv_lds() { return 2 * (2 * (size_t)kBN * D * 2 + 2 * kBN * 4); }
@@ -476,12 +535,20 @@ hipError_t launch_bwd(const void* q, const void* k, const void* v, const void* o
   hipLaunchKernelGGL(attn_delta_kernel<D>, dim3((rows + 15) / 16), dim3(256), 0, st, (const __bf16*)o,
                      (const __bf16*)dout, delta, B, S, Hq);
   const float c = scale * 1.4426950408889634f;
-  hipLaunchKernelGGL(attn_dq_kernel<D>, dim3((S + kBM - 1) / kBM, Hq, B), dim3(256), fwd_lds<D>(), st,
+  const int nb = (S + kBM - 1) / kBM;
+  if (causal && attn_bwd_fused()) {
+    const size_t lds = dkdv_lds<D>() > fwd_lds<D>() ? dkdv_lds<D>() : fwd_lds<D>();
+    hipLaunchKernelGGL(attn_bwd_fused_kernel<D>, dim3(nb * (Hkv + Hq) * B), dim3(256), lds, st, (const __bf16*)q,
+                       (const __bf16*)k, (const __bf16*)v, (const __bf16*)dout, lse, delta, (__bf16*)dq, (__bf16*)dk,
+                       (__bf16*)dv, S, Hq, Hkv, B, c, scale, causal);
+    return hipGetLastError();
+  }
+  hipLaunchKernelGGL(attn_dq_kernel<D>, dim3(nb, Hq, B), dim3(256), fwd_lds<D>(), st,
                      (const __bf16*)q, (const __bf16*)k, (const __bf16*)v, (const __bf16*)dout, lse, delta,
                      (__bf16*)dq, S, Hq, Hkv, c, scale, causal);
-  hipLaunchKernelGGL(attn_dkdv_kernel<D>, dim3((S + kBM - 1) / kBM, Hkv, B), dim3(256), dkdv_lds<D>(), st,
+  hipLaunchKernelGGL(attn_dkdv_kernel<D>, dim3(nb * Hkv * B), dim3(256), dkdv_lds<D>(), st,
                      (const __bf16*)q, (const __bf16*)k, (const __bf16*)v, (const __bf16*)dout, lse, delta,
-                     (__bf16*)dk, (__bf16*)dv, S, Hq, Hkv, c, scale, causal);
+                     (__bf16*)dk, (__bf16*)dv, S, Hq, Hkv, B, c, scale, causal);
   return hipGetLastError();
 }
 
