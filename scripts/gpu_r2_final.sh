@@ -14,3 +14,7 @@ timeout -k 10 300 python bench.py > gpurun_out/bench_default.log 2>&1 || exit $?
 tail -1 gpurun_out/bench_default.log | cut -c1-300
 timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_driver_shape.log 2>&1 || exit $?
 tail -1 gpurun_out/bench_driver_shape.log | cut -c1-300
+timeout -k 10 300 python bench.py --model llama3-8b --steps 4 --warmup 2 > gpurun_out/bench_llama_final.log 2>&1 || exit $?
+tail -1 gpurun_out/bench_llama_final.log | cut -c1-200
+timeout -k 10 300 python bench.py --model resnet50 --dtype bf16 --steps 10 --warmup 3 > gpurun_out/bench_rn50_final.log 2>&1 || exit $?
+tail -1 gpurun_out/bench_rn50_final.log | cut -c1-200

@@ -64,10 +64,11 @@ def test_rmsnorm_fp32_stream_bf16_out(dev, shape):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_swiglu(dev, dtype):
+@pytest.mark.parametrize("shape", [(3, 17, 352), (5, 7, 9)])  # 4-wide kernels / scalar kernels
+def test_swiglu(dev, dtype, shape):
     from cs744_pytorch_distributed_tutorial_amd.ops import lm
-    a = torch.randn(3, 17, 352, device=dev).to(dtype).requires_grad_()
-    b = torch.randn(3, 17, 352, device=dev).to(dtype).requires_grad_()
+    a = torch.randn(*shape, device=dev).to(dtype).requires_grad_()
+    b = torch.randn(*shape, device=dev).to(dtype).requires_grad_()
     y = lm.swiglu(a, b)
     gy = torch.randn_like(y)
     y.backward(gy)
