@@ -105,10 +105,11 @@ def describe(args, trainer, world):
 def main(argv=None) -> int:
     args = parse(argv)
     if args.batch_size is None:
-        # Llama-3-8B: 4 x 2048 tokens per GPU (measured on MI355X: 11.6k / 14.3k / 15.8k tokens/s at
-        # B = 1 / 2 / 4 — the fp32 master-weight SGD step amortises over more tokens)
+        # Llama-3-8B: 8 x 2048 tokens per GPU (measured on MI355X with the round-2 kernels: 19.8-20.1k /
+        # 20.0k / 20.7k tokens/s at B = 4 / 6 / 8 — the fp32 master-weight SGD step and, at N > 1, the
+        # gradient all-reduce amortise over more tokens)
         m = args.model.lower()
-        args.batch_size = 64 if is_vgg(args.model) else (4 if "8b" in m else (8 if "llama" in m else 128))
+        args.batch_size = 64 if is_vgg(args.model) else (8 if "8b" in m else (8 if "llama" in m else 128))
     if args.dtype is None:
         args.dtype = "bf16" if "llama" in args.model.lower() else "fp32"
     if args.seq_len == 0 and "8b" in args.model.lower():
