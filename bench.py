@@ -109,7 +109,7 @@ def main(argv=None) -> int:
         # 20.0k / 20.7k tokens/s at B = 4 / 6 / 8 — the fp32 master-weight SGD step and, at N > 1, the
         # gradient all-reduce amortise over more tokens)
         m = args.model.lower()
-        args.batch_size = 64 if is_vgg(args.model) else (8 if "8b" in m else (8 if "llama" in m else 128))
+        args.batch_size = 64 if is_vgg(args.model) else (8 if "llama" in m or "8b" in m else 128)
     if args.dtype is None:
         args.dtype = "bf16" if "llama" in args.model.lower() else "fp32"
     if args.seq_len == 0 and "8b" in args.model.lower():
