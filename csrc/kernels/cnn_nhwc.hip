@@ -341,9 +341,9 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const T* __restrict__ 
   const int CV = C / V;
   const int64_t total = (int64_t)B * Ho * Wo * CV;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    const int cv = (int)(i % CV);
-    const int64_t o = i / CV;
-    const int ow = (int)(o % Wo), oh = (int)((o / Wo) % Ho), b = (int)(o / ((int64_t)Wo * Ho));
+    const int ii = (int)i, cv = ii % CV, o32 = ii / CV;  // total < 2^31 (host check): 32-bit index math
+    const int64_t o = o32;
+    const int ow = o32 % Wo, oh = (o32 / Wo) % Ho, b = o32 / (Wo * Ho);
     float best[V];
     int bp[V];
 #pragma unroll
@@ -380,9 +380,9 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const T* __restrict__ 
   const int CV = C / V;
   const int64_t total = (int64_t)B * H * W * CV;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    const int cv = (int)(i % CV);
-    const int64_t q = i / CV;
-    const int iw = (int)(q % W), ih = (int)((q / W) % H), b = (int)(q / ((int64_t)W * H));
+    const int ii = (int)i, cv = ii % CV, q32 = ii / CV;  // 32-bit index math (host check)
+    const int64_t q = q32;
+    const int iw = q32 % W, ih = (q32 / W) % H, b = q32 / (W * H);
     // outputs whose window [2o-1, 2o+1] holds this input, in row-major order
     const int oh0 = ih / 2, oh1 = min(Ho - 1, (ih + 1) / 2);
     const int ow0 = iw / 2, ow1 = min(Wo - 1, (iw + 1) / 2);
@@ -413,14 +413,14 @@ __global__ __launch_bounds__(256) void im2col_kernel(const T* __restrict__ x, T*
   const int KV = Kp / V, K = R * S * C;
   const int64_t total = (int64_t)B * Ho * Wo * KV;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    const int k = (int)(i % KV) * V;
-    const int64_t m = i / KV;
+    const int ii = (int)i, k = (ii % KV) * V, m32 = ii / KV;  // 32-bit index math (host check)
+    const int64_t m = m32;
     float v[V];
 #pragma unroll
     for (int j = 0; j < V; ++j) v[j] = 0.f;
     if (k < K) {
       const int c = k % C, rs = k / C, s = rs % S, r = rs / S;
-      const int ow = (int)(m % Wo), oh = (int)((m / Wo) % Ho), b = (int)(m / ((int64_t)Wo * Ho));
+      const int ow = m32 % Wo, oh = (m32 / Wo) % Ho, b = m32 / (Wo * Ho);
       const int ih = oh * st - pad + r, iw = ow * st - pad + s;
       if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W) ldv<T, V>(x + (((int64_t)b * H + ih) * W + iw) * C + c, v);
     }
@@ -436,9 +436,9 @@ __global__ __launch_bounds__(256) void col2im_kernel(const T* __restrict__ dcol,
   const int CV = C / V;
   const int64_t total = (int64_t)B * H * W * CV;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    const int c = (int)(i % CV) * V;
-    const int64_t q = i / CV;
-    const int iw = (int)(q % W), ih = (int)((q / W) % H), b = (int)(q / ((int64_t)W * H));
+    const int ii = (int)i, c = (ii % CV) * V, q32 = ii / CV;  // 32-bit index math (host check)
+    const int64_t q = q32;
+    const int iw = q32 % W, ih = (q32 / W) % H, b = q32 / (W * H);
     float acc[V];
 #pragma unroll
     for (int j = 0; j < V; ++j) acc[j] = 0.f;
@@ -461,6 +461,9 @@ __global__ __launch_bounds__(256) void col2im_kernel(const T* __restrict__ dcol,
 }
 
 // ------------------------------------------------------------------------------ host side
+// the gather kernels index their work items in 32 bits (64-bit integer division is emulated)
+constexpr int64_t kMaxItems = (int64_t)1 << 31;
+
 int grid_for(int64_t n) {
   const int64_t b = (n + 255) / 256;
   return (int)(b < 1 ? 1 : (b > 65536 ? 65536 : b));
@@ -575,6 +578,7 @@ hipError_t cs_maxpool3s2_nhwc_fwd(int dt, const void* x, void* y, unsigned char*
                                   int Ho, int Wo, hipStream_t stream) {
   const int64_t n = (int64_t)B * Ho * Wo * C;
   if (n == 0) return hipSuccess;
+  if (n >= kMaxItems) return hipErrorInvalidValue;
   CS_NHWC_DISPATCH(dt, C, hipLaunchKernelGGL((maxpool_fwd_kernel<T, V>), dim3(grid_for(n / V)), dim3(256), 0, stream,
                                        (const T*)x, (T*)y, pos, B, H, W, C, Ho, Wo));
   return hipGetLastError();
@@ -584,6 +588,7 @@ hipError_t cs_maxpool3s2_nhwc_bwd(int dt, const void* dy, const unsigned char* p
                                   int C, int Ho, int Wo, hipStream_t stream) {
   const int64_t n = (int64_t)B * H * W * C;
   if (n == 0) return hipSuccess;
+  if (n >= kMaxItems) return hipErrorInvalidValue;
   CS_NHWC_DISPATCH(dt, C, hipLaunchKernelGGL((maxpool_bwd_kernel<T, V>), dim3(grid_for(n / V)), dim3(256), 0, stream,
                                        (const T*)dy, pos, (T*)dx, B, H, W, C, Ho, Wo));
   return hipGetLastError();
@@ -593,6 +598,7 @@ hipError_t cs_im2col_nhwc(int dt, const void* x, void* col, int B, int H, int W,
                           int pad, int Ho, int Wo, int Kp, hipStream_t stream) {
   const int64_t n = (int64_t)B * Ho * Wo * Kp;
   if (n == 0) return hipSuccess;
+  if (n >= kMaxItems) return hipErrorInvalidValue;
   // V must divide C (a vector stays inside one tap) and Kp
   const int vc = vec_for(C, dt == CS_BF16 ? 2 : 4);
   if (vc > 1 && Kp % vc != 0) return hipErrorInvalidValue;
@@ -605,6 +611,7 @@ hipError_t cs_col2im_nhwc(int dt, const void* dcol, void* dx, int B, int H, int 
                           int pad, int Ho, int Wo, int Kp, hipStream_t stream) {
   const int64_t n = (int64_t)B * H * W * C;
   if (n == 0) return hipSuccess;
+  if (n >= kMaxItems) return hipErrorInvalidValue;
   const int vc = vec_for(C, dt == CS_BF16 ? 2 : 4);
   if (vc > 1 && Kp % vc != 0) return hipErrorInvalidValue;
   CS_NHWC_DISPATCH(dt, C, hipLaunchKernelGGL((col2im_kernel<T, V>), dim3(grid_for(n / V)), dim3(256), 0, stream,
