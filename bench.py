@@ -34,8 +34,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
-# the package raises GPU_MAX_HW_QUEUES before anything initialises HIP (see its __init__)
-import cs744_pytorch_distributed_tutorial_amd  # noqa: E402,F401
+# raise GPU_MAX_HW_QUEUES before anything initialises HIP (package ensure_hw_queues)
+import cs744_pytorch_distributed_tutorial_amd as _pkg  # noqa: E402
+
+_pkg.ensure_hw_queues()
 import torch  # noqa: E402
 
 from cs744_pytorch_distributed_tutorial_amd import distributed as D  # noqa: E402

@@ -12,28 +12,40 @@ Subpackages:
 __version__ = "0.1.0"
 
 import os as _os
+import warnings as _warnings
+
+_HW_QUEUES_DEFAULT = 4  # HIP's default GPU_MAX_HW_QUEUES
 
 
-def _raise_hw_queues(minimum: int = 8) -> int:
-    """HIP hardware queues per process (GPU_MAX_HW_QUEUES, read once at HIP init; HIP's default
-    is 4). The native engine runs the compute stream, a side stream for weight gradients, the
-    communicator's stream and RCCL's own streams, and its cross-stream waits are small kernels
-    (kernel stream links): streams that share a hardware queue serialise behind such a wait
-    (measured: VGG-11 step with side-stream weight gradients + one-rank RCCL 1.69 ms at 4 queues,
-    0.717 ms at 8). Raised before HIP initialises; returns the count in effect."""
-    cur = int(_os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4)
+def hw_queues() -> int:
+    """HIP hardware queues per process in effect (GPU_MAX_HW_QUEUES; read once at HIP init)."""
+    try:
+        return int(_os.environ.get("GPU_MAX_HW_QUEUES", str(_HW_QUEUES_DEFAULT)) or _HW_QUEUES_DEFAULT)
+    except ValueError:
+        return _HW_QUEUES_DEFAULT
+
+
+def ensure_hw_queues(minimum: int = 8) -> int:
+    """Raise GPU_MAX_HW_QUEUES to `minimum` for THIS process before HIP initialises; returns the
+    count in effect. Opt-in: called by the entry points (bench.py, train.py, entrypoints/*),
+    never at import. The native engine runs the compute stream, a side stream for weight
+    gradients, the communicator's stream and RCCL's own streams, and its cross-stream waits are
+    small kernels (kernel stream links): streams that share a hardware queue serialise behind
+    such a wait (measured: VGG-11 step with side-stream weight gradients + one-rank RCCL 1.69 ms
+    at 4 queues, 0.717 ms at 8). Too late once HIP is up: then it warns and changes nothing."""
+    cur = hw_queues()
+    if cur >= minimum:
+        return cur
     try:
         import torch
-        if torch.cuda.is_initialized():  # too late to change it in this process
+        if torch.cuda.is_initialized():
+            _warnings.warn(f"HIP already initialised with GPU_MAX_HW_QUEUES={cur} (< {minimum}); the native "
+                           "engine keeps weight gradients on the main stream when a communicator runs")
             return cur
     except Exception:  # pragma: no cover - torch missing
         return cur
-    if cur < minimum:
-        _os.environ["GPU_MAX_HW_QUEUES"] = str(minimum)
-        cur = minimum
-    return cur
+    _os.environ["GPU_MAX_HW_QUEUES"] = str(minimum)
+    return minimum
 
-
-HW_QUEUES = _raise_hw_queues()
 
 from . import distributed  # noqa: F401,E402

@@ -96,6 +96,47 @@ def conv_wgrad(dz: torch.Tensor, x: torch.Tensor, cout: int, *, w_oihw: bool = F
     return dw.view(cout, 3, 3, 3) if w_oihw else dw.view(cout, 3, 3, cin)
 
 
+def split3(t: torch.Tensor) -> torch.Tensor:
+    """fp32 tensor -> P3 bf16 chunks ``[numel/8, 3, 8]`` (h, m, l of every 8 elements, t = h + m + l
+    to 2^-26 |t|): the operand format of the pre-split ("XP") conv GEMMs
+    (``csrc/kernels/conv_xp.hip``)."""
+    t = t.contiguous()
+    out = torch.empty(t.numel() // 8, 3, 8, device=t.device, dtype=torch.bfloat16)
+    native.C().split3(t, out)
+    return out
+
+
+def conv_fwd_xp(x3: torch.Tensor, w3: torch.Tensor, bias: Optional[torch.Tensor], B: int, H: int, W: int, cin: int,
+                cout: int, *, bm: int = 128, bn: int = 64, bk: int = 32, kg: int = 1, splits: int = 1,
+                stats: bool = False, nb: int = 0):
+    """``conv_fwd`` on pre-split operands: x3 = split3(x NHWC), w3 = split3(w OHWI)."""
+    y = torch.empty(B * H * W, cout, device=x3.device, dtype=torch.float32)
+    R = native.C().conv_stat_rows(9 * cin, bm, bn, bk, splits, False)
+    T = (B * H * W + R - 1) // R
+    st = torch.empty(T, cout, 2, device=x3.device, dtype=torch.float32) if stats else None
+    rows = native.C().conv_gemm_xp(FWD, x3, w3, None, bias, y, _ws(FWD, B, H, W, cin, cout, splits, x3.device), st,
+                                   B, H, W, cin, cout, bm, bn, splits, bk, kg, nb)
+    return (y, st, rows) if stats else y
+
+
+def conv_dgrad_xp(dz3: torch.Tensor, w3: torch.Tensor, B: int, H: int, W: int, cin: int, cout: int, *,
+                  bm: int = 128, bn: int = 64, bk: int = 32, kg: int = 1, splits: int = 1,
+                  nb: int = 0) -> torch.Tensor:
+    dx = torch.empty(B * H * W, cin, device=dz3.device, dtype=torch.float32)
+    native.C().conv_gemm_xp(DGRAD, None, w3, dz3, None, dx, _ws(DGRAD, B, H, W, cin, cout, splits, dz3.device), None,
+                            B, H, W, cin, cout, bm, bn, splits, bk, kg, nb)
+    return dx
+
+
+def conv_wgrad_xp(dz3: torch.Tensor, x3: torch.Tensor, B: int, H: int, W: int, cin: int, cout: int, *,
+                  bm: int = 128, bn: int = 64, bk: int = 32, kg: int = 1, splits: int = 1,
+                  nb: int = 0) -> torch.Tensor:
+    dw = torch.empty(cout * 9 * cin, device=x3.device, dtype=torch.float32)
+    native.C().conv_gemm_xp(WGRAD, x3, None, dz3, None, dw, _ws(WGRAD, B, H, W, cin, cout, splits, x3.device), None,
+                            B, H, W, cin, cout, bm, bn, splits, bk, kg, nb)
+    return dw.view(cout, 3, 3, cin)
+
+
 class BNState:
     """Per-channel tensors one BN layer needs between forward and backward."""
 

@@ -191,8 +191,12 @@ class NativeTrainer:
                  test_size: Optional[int] = None, autotune: bool = True, broadcast_buffers: bool = True,
                  drop_last: bool = True, init_state: Optional[Dict[str, torch.Tensor]] = None,
                  dtype: str = "fp32", probe: Optional[str] = None, probe_spin_us: float = 20.0,
-                 check_every: int = 0):
+                 check_every: int = 0, timeout_s: float = 1800.0):
         C = native.C()
+        # a stream-link wait (side-stream joins, communicator fork/join) releases its consumer
+        # early only after the communicator timeout or on abort(): never before a late peer
+        C.set_link_timeout(float(timeout_s))
+        C.reset_link_abort()
         self.device = device or torch.device("cuda", torch.cuda.current_device())
         with torch.cuda.device(self.device):
             C.reserve_streams()  # the engine's side stream gets its own hardware queue (device_comm.h)
@@ -282,10 +286,10 @@ class NativeTrainer:
         # avoided it), so that path keeps the serial backward.
         # Also off under rocprofv3 counter collection, which serialises every dispatch: a side-stream
         # link wait would spin to its timeout waiting for a signal that cannot run.
-        from .. import HW_QUEUES
+        from .. import hw_queues
         python_collectives = world > 1 and self.native_comm is None
         self.overlap_wgrad = os.environ.get("CS_OVERLAP_WGRAD", "1") != "0" and not python_collectives and (
-            self.native_comm is None or HW_QUEUES >= 8) and not self._counters
+            self.native_comm is None or hw_queues() >= 8) and not self._counters
         self.engine.set_overlap_wgrad(self.overlap_wgrad)
         self.engine.set_data(0, self.train_data, self.train_labels, self.aug_train)
         self.engine.set_data(1, self.test_data, self.test_labels, self.aug_test)
@@ -543,9 +547,11 @@ class NativeTrainer:
             raise RuntimeError(f"rank {self.rank}: {self.native_comm.kind} communicator failed: {err}")
 
     def abort(self) -> None:
-        """Abort the native communicator (from a watchdog thread: unblocks RCCL kernels)."""
+        """Abort the native communicator (from a watchdog thread: unblocks RCCL kernels) and
+        release every waiting stream-link kernel (they record an error the next check raises)."""
         if self.native_comm is not None:
             self.native_comm.abort()
+        native.C().abort_links()
 
     def step(self) -> None:
         """One training iteration: next batch -> forward -> backward (+grad sync) -> SGD."""
@@ -697,7 +703,7 @@ def run_native(cfg, device, logger) -> dict:
                        world=world, sync=mode, comm=cfg.resolved_comm(world), bucket_mb=cfg.bucket_mb, lr=cfg.lr,
                        momentum=cfg.momentum, weight_decay=cfg.weight_decay, seed=cfg.seed, data_seed=cfg.data_seed,
                        train_size=cfg.train_size, test_size=cfg.test_size, drop_last=False,
-                       check_every=cfg.check_comm_every)
+                       check_every=cfg.check_comm_every, timeout_s=cfg.timeout_s)
     start_epoch, start_iter = 0, 0
     if cfg.resume:
         from ..utils.checkpoint import load_checkpoint

@@ -137,6 +137,8 @@ def init_from_config(cfg: TrainConfig) -> None:
 
 def run(cfg: TrainConfig) -> dict:
     """Build data/model/optimizer/sync for ``cfg.part`` and train + evaluate."""
+    from . import ensure_hw_queues
+    ensure_hw_queues()  # before anything below initialises HIP (no-op with a warning if too late)
     if cfg.threads:
         torch.set_num_threads(cfg.threads)
     init_from_config(cfg)

@@ -77,6 +77,67 @@ int64_t conv_gemm(int64_t mode, c10::optional<torch::Tensor> x, c10::optional<to
   return cs_conv_stat_rows(a.K, bm, bn, bk, splits, counters.has_value());
 }
 
+// P3 operand: contiguous bfloat16 [n/8, 3, 8] chunks (h, m, l per 8 elements, split3)
+const uint16_t* planes(const c10::optional<torch::Tensor>& t, int64_t need, int64_t& ps, const char* name) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kBFloat16 && t->is_contiguous() && t->numel() >= 3 * need,
+              name, ": must be a contiguous bfloat16 GPU tensor of >= 3 x ", need, " elements (P3 chunks, split3)");
+  ps = need;
+  return reinterpret_cast<const uint16_t*>(t->data_ptr<at::BFloat16>());
+}
+
+// pre-split ("XP") conv GEMM: operands as bf16 planes [3][n] (split3); returns FWD stats rows
+int64_t conv_gemm_xp(int64_t mode, c10::optional<torch::Tensor> x3, c10::optional<torch::Tensor> w3,
+                     c10::optional<torch::Tensor> dz3, c10::optional<torch::Tensor> bias, torch::Tensor out,
+                     c10::optional<torch::Tensor> ws, c10::optional<torch::Tensor> stats, int64_t B, int64_t H,
+                     int64_t W, int64_t Cin, int64_t Cout, int64_t bm, int64_t bn, int64_t splits, int64_t bk,
+                     int64_t kg, int64_t nb) {
+  TORCH_CHECK(mode >= 0 && mode <= 2, "conv_gemm_xp: bad mode");
+  TORCH_CHECK(pow2(H) && pow2(W) && pow2(Cin) && pow2(Cout) && Cin >= 64 && Cout >= 64 && B > 0,
+              "conv_gemm_xp: H, W, Cin, Cout powers of two, Cin/Cout >= 64");
+  TORCH_CHECK(cs_conv_xp_ok((int)bm, (int)bn, (int)bk, (int)kg, (int)nb) && splits >= 1,
+              "conv_gemm_xp: no kernel for ", bm, "x", bn, " bk ", bk, " kg ", kg, " nb ", nb);
+  const int64_t pix = B * H * W, wnum = Cout * 9 * Cin;
+  CsConvArgs a{};
+  a.B = B; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout;
+  cs_conv_fill_dims(&a, (int)mode);
+  if (mode != CS_CONV_DGRAD) {
+    TORCH_CHECK(x3.has_value(), "conv_gemm_xp: needs x3");
+    a.x3 = planes(x3, pix * Cin, a.x3s, "x3");
+  }
+  if (mode != CS_CONV_WGRAD) {
+    TORCH_CHECK(w3.has_value(), "conv_gemm_xp: needs w3");
+    a.w3 = planes(w3, wnum, a.w3s, "w3");
+  }
+  if (mode != CS_CONV_FWD) {
+    TORCH_CHECK(dz3.has_value(), "conv_gemm_xp: needs dz3");
+    a.dz3 = planes(dz3, pix * Cout, a.dz3s, "dz3");
+  }
+  check_t(bias, Cout, "bias");
+  check_t(out, mode == CS_CONV_FWD ? pix * Cout : (mode == CS_CONV_DGRAD ? pix * Cin : wnum), "out");
+  const int64_t R = cs_conv_stat_rows(a.K, bm, bn, bk, splits, false);
+  if (mode == CS_CONV_FWD) check_t(stats, ((pix + R - 1) / R) * Cout * 2, "stats");
+  const int64_t sp = cs_conv_effective_splits(a.K, bk, splits);
+  if (sp > 1) {
+    TORCH_CHECK(ws.has_value() && ws->defined(), "conv_gemm_xp: split-K needs a workspace");
+    check_t(ws, sp * (int64_t)a.M * a.N, "ws");
+  }
+  DevGuard g(out.device());
+  a.bias = cptr(bias);
+  a.out = out.data_ptr<float>(); a.ws = mptr(ws); a.stats = mode == CS_CONV_FWD ? mptr(stats) : nullptr;
+  CS_LAUNCH(cs_conv_xp(a, (int)mode, (int)bm, (int)bn, (int)bk, (int)splits, (int)kg, (int)nb, cur_stream()));
+  return R;
+}
+
+void split3(torch::Tensor x, torch::Tensor out) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat && x.is_contiguous() && x.numel() % 8 == 0,
+              "split3: x must be a contiguous float32 GPU tensor with numel % 8 == 0");
+  int64_t ps = 0;
+  const uint16_t* o = planes(out, x.numel(), ps, "out");
+  DevGuard g(x.device());
+  CS_LAUNCH(cs_split3(x.data_ptr<float>(), const_cast<uint16_t*>(o), x.numel(), cur_stream()));
+}
+
 void bn_finalize(torch::Tensor part, int64_t T, int64_t R, int64_t M, torch::Tensor gamma, torch::Tensor beta,
                  c10::optional<torch::Tensor> running_mean, c10::optional<torch::Tensor> running_var,
                  c10::optional<torch::Tensor> nbt, double momentum, double eps, torch::Tensor scale,
@@ -211,6 +272,15 @@ void register_conv_ops(pybind11::module& m) {
   m.def("conv_stat_rows", [](int64_t K, int64_t bm, int64_t bn, int64_t bk, int64_t splits, bool counters) {
     return cs_conv_stat_rows((int)K, (int)bm, (int)bn, (int)bk, (int)splits, counters);
   }, "FWD BN-statistics tile height of a conv_gemm launch");
+  m.def("conv_gemm_xp", &conv_gemm_xp, "pre-split (bf16 planes) implicit-GEMM 3x3 conv, six-product split-bf16 MFMA",
+        py::arg("mode"), py::arg("x3"), py::arg("w3"), py::arg("dz3"), py::arg("bias"), py::arg("out"), py::arg("ws"),
+        py::arg("stats"), py::arg("B"), py::arg("H"), py::arg("W"), py::arg("Cin"), py::arg("Cout"), py::arg("bm"),
+        py::arg("bn"), py::arg("splits"), py::arg("bk"), py::arg("kg"), py::arg("nb") = 0);
+  m.def("conv_xp_ok", [](int64_t bm, int64_t bn, int64_t bk, int64_t kg, int64_t nb) {
+    return cs_conv_xp_ok((int)bm, (int)bn, (int)bk, (int)kg, (int)nb);
+  }, "whether a pre-split conv GEMM variant exists", py::arg("bm"), py::arg("bn"), py::arg("bk"), py::arg("kg"),
+        py::arg("nb") = 0);
+  m.def("split3", &split3, "fp32 -> P3 bf16 chunks [n/8][3][8] (h, m, l: x = h + m + l to 2^-26)");
   m.def("bn_finalize", &bn_finalize);
   m.def("bn_eval_coeffs", &bn_eval_coeffs);
   m.def("bn_apply", &bn_apply);

@@ -72,6 +72,11 @@ void register_runtime(pybind11::module& m) {
       .def("join", [](cs::DeviceComm& c) { c.join(cur_stream()); })
       .def("async_error", &cs::DeviceComm::async_error)
       .def("abort", &cs::DeviceComm::abort);
+  m.def("set_link_timeout", &cs::set_link_timeout,
+        "stream-link wait timeout in seconds (the communicator timeout; CS_COMM_LINK_TIMEOUT_S overrides)");
+  m.def("link_timeout", &cs::link_timeout);
+  m.def("abort_links", &cs::abort_links, "release every waiting stream-link kernel with an error (watchdog path)");
+  m.def("reset_link_abort", &cs::reset_link_abort);
   py::class_<cs::StagedComm, cs::DeviceComm>(m, "StagedComm")
       .def(py::init<const std::string&, int>(), py::arg("group_name"), py::arg("device"));
   py::class_<cs::ProbeComm, cs::DeviceComm>(m, "ProbeComm")

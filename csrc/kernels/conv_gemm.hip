@@ -34,40 +34,10 @@
 
 #include <algorithm>
 
-#include "bn_device.h"
-#include "common.h"
-#include "launchers.h"
+#include "conv_common.h"
 
 namespace {
 
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef __amdgpu_buffer_rsrc_t rsrc_t;
-
-// byte offset past every descriptor's range: loads return 0, stores are dropped
-constexpr int kOOB = 0x7ffffff0;
-
-__device__ __forceinline__ rsrc_t make_rsrc(const void* p, int64_t bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
-}
-// the whole offset goes in voffset: the range check is only guaranteed to cover it
-__device__ __forceinline__ float4 bload4(rsrc_t r, int voff) {
-  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, 0));
-}
-__device__ __forceinline__ void bstore1(rsrc_t r, float v, int voff) {
-  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, voff, 0, 0);
-}
-
-// 9-bit mask of the 3x3 taps whose source pixel (h + s*dh, w + s*dw) is inside the image
-// (s = +1 for FWD / WGRAD, -1 for DGRAD's flipped kernel); bit t = tap t = 3*(dh+1)+(dw+1)
-__device__ __forceinline__ unsigned tap_mask(int h, int w, int H, int W, int s) {
-  unsigned m = 0;
-#pragma unroll
-  for (int t = 0; t < 9; ++t) {
-    const int hh = h + s * (t / 3 - 1), ww = w + s * (t % 3 - 1);
-    if ((unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W) m |= 1u << t;
-  }
-  return m;
-}
 
 template <int MODE>
 struct Traits;
@@ -618,134 +588,6 @@ __device__ __forceinline__ void kstep(Loader<BM, BN, MODE, BK, C4, false, KG>& l
   }
 }
 
-// In-launch split-K combine (cdna_hip_programming.md §5 "In-launch split-K reduction"):
-// every split block has stored its fp32 slab; it publishes it (vmcnt drain, barrier, one
-// agent-scope release) and takes a ticket on the tile's counter. The block that draws the
-// last ticket resets the counter, acquires, and sums the tile's slabs in split order
-// z = 0..S-1 (the same fixed order as the separate reduce kernel: deterministic and
-// independent of which block arrives last), then runs the epilogue: bias + output (+ this
-// tile's BN (mean, M2) over its BM rows for FWD; the OIHW scatter for conv0's wgrad).
-// Saves the reduce launch and the slab round trip for GEMMs whose S * BM * BN slabs are
-// small enough for one block to read (cs_conv_fixup_ok).
-template <int BM, int BN, int MODE>
-__device__ void splitk_fixup(const CsConvArgs& a, int tile, int mt, int nt, int nsplit, float* smem) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  int* flag = reinterpret_cast<int*>(smem);
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const int t = __hip_atomic_fetch_add(a.counters + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = t == nsplit - 1;
-    if (last) {
-      __hip_atomic_store(a.counters + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    flag[0] = last;
-  }
-  __syncthreads();
-  const int last = flag[0];
-  __syncthreads();  // flag is read by every wave before smem is reused below
-  if (!last) return;
-  constexpr int CG = BN / 4, RL = 256 / CG, RPT = BM / RL;
-  const int cg = threadIdx.x % CG, rl = threadIdx.x / CG;
-  const int m0 = mt * BM, n0 = nt * BN, n = n0 + 4 * cg;
-  const int S = nsplit;
-  const size_t slab = (size_t)a.M * a.N;
-  const bool nok = n < a.N;
-  float4 v[RPT];
-#pragma unroll
-  for (int k = 0; k < RPT; ++k) v[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-  const float* base = a.ws + n;
-  int z = 0;
-  for (; z + 4 <= S; z += 4) {  // 4 slabs per trip: RPT * 4 loads in flight, added in z order
-    float4 t[4][RPT];
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-#pragma unroll
-      for (int k = 0; k < RPT; ++k) {
-        const int m = m0 + rl + k * RL;
-        t[u][k] = (m < a.M && nok) ? *reinterpret_cast<const float4*>(base + (size_t)(z + u) * slab + (size_t)m * a.N)
-                                   : make_float4(0.f, 0.f, 0.f, 0.f);
-      }
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-#pragma unroll
-      for (int k = 0; k < RPT; ++k) {
-        v[k].x += t[u][k].x; v[k].y += t[u][k].y; v[k].z += t[u][k].z; v[k].w += t[u][k].w;
-      }
-  }
-  for (; z < S; ++z)
-#pragma unroll
-    for (int k = 0; k < RPT; ++k) {
-      const int m = m0 + rl + k * RL;
-      if (m < a.M && nok) {
-        const float4 t = *reinterpret_cast<const float4*>(base + (size_t)z * slab + (size_t)m * a.N);
-        v[k].x += t.x; v[k].y += t.y; v[k].z += t.z; v[k].w += t.w;
-      }
-    }
-  if constexpr (MODE == CS_CONV_FWD) {
-    if (a.bias != nullptr && nok) {
-      const float4 bv = *reinterpret_cast<const float4*>(a.bias + n);
-#pragma unroll
-      for (int k = 0; k < RPT; ++k) { v[k].x += bv.x; v[k].y += bv.y; v[k].z += bv.z; v[k].w += bv.w; }
-    }
-  }
-  if (MODE == CS_CONV_WGRAD && a.w_oihw) {
-#pragma unroll
-    for (int k = 0; k < RPT; ++k) {
-      const int m = m0 + rl + k * RL;
-      const float vals[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
-      if (m < a.M)
-        for (int q = 0; q < 4; ++q) {
-          const int nn = n + q, tap = nn >> 2, ci = nn & 3;
-          if (nn < a.N && ci < 3) a.out[(size_t)m * 27 + ci * 9 + tap] = vals[q];
-        }
-    }
-    return;
-  }
-#pragma unroll
-  for (int k = 0; k < RPT; ++k) {
-    const int m = m0 + rl + k * RL;
-    if (m < a.M && nok) *reinterpret_cast<float4*>(a.out + (size_t)m * a.N + n) = v[k];
-  }
-  if constexpr (MODE == CS_CONV_FWD) {
-    if (a.stats == nullptr) return;
-    // per-column (mean, M2) over the tile's valid rows, two passes through LDS
-    float* red = smem;             // [RL][BN]
-    float* meanv = smem + RL * BN;  // [BN]
-    const int cnt = (a.M - m0) < BM ? (a.M - m0) : BM;
-    float4 cs = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-    for (int k = 0; k < RPT; ++k)
-      if (m0 + rl + k * RL < a.M) { cs.x += v[k].x; cs.y += v[k].y; cs.z += v[k].z; cs.w += v[k].w; }
-    *reinterpret_cast<float4*>(red + rl * BN + 4 * cg) = cs;
-    __syncthreads();
-    if (threadIdx.x < BN) {
-      float sum = 0.f;
-      for (int q = 0; q < RL; ++q) sum += red[q * BN + threadIdx.x];
-      meanv[threadIdx.x] = sum / (float)cnt;
-    }
-    __syncthreads();
-    const float4 mu = *reinterpret_cast<const float4*>(meanv + 4 * cg);
-    float4 sq = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-    for (int k = 0; k < RPT; ++k)
-      if (m0 + rl + k * RL < a.M) {
-        const float dx = v[k].x - mu.x, dy = v[k].y - mu.y, dz = v[k].z - mu.z, dw = v[k].w - mu.w;
-        sq.x += dx * dx; sq.y += dy * dy; sq.z += dz * dz; sq.w += dw * dw;
-      }
-    *reinterpret_cast<float4*>(red + rl * BN + 4 * cg) = sq;
-    __syncthreads();
-    if (threadIdx.x < BN && n0 + (int)threadIdx.x < a.N) {
-      float m2 = 0.f;
-      for (int q = 0; q < RL; ++q) m2 += red[q * BN + threadIdx.x];
-      a.stats[((size_t)mt * a.N + n0 + threadIdx.x) * 2 + 0] = meanv[threadIdx.x];
-      a.stats[((size_t)mt * a.N + n0 + threadIdx.x) * 2 + 1] = m2;
-    }
-  }
-}
 
 // One K-step's MFMA chain on a staged LDS-DMA tile (GL): fragment reads one chunk ahead.
 template <int BM, int BN, int MODE, int BK, bool X6 = false>
@@ -776,12 +618,6 @@ __device__ __forceinline__ void kcompute_gl(const float* cur,
   }
 }
 
-// s_waitcnt vmcnt(N) alone (expcnt / lgkmcnt left at their maxima), gfx9 encoding
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-  static_assert(N >= 0 && N < 64, "vmcnt range");
-  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
-}
 
 // GL > 0: LDS-DMA staging through a GL-deep ring of LDS images — tile t+GL-1 is fetched
 // while tile t is multiplied, one raw s_barrier per K-step after a counted vmcnt (tile t
@@ -894,133 +730,7 @@ __device__ __forceinline__ void gemm_body(const CsConvArgs& a, const int tile, c
   }
   }
 
-  if constexpr (KG > 1) {
-    // K-group partials -> group 0, summed in group order through LDS (the main loop ended on
-    // a barrier; every group's last LDS reads are done)
-    float* red = smem;  // [KG-1][4 spatial waves][RM*RN*16][64 lanes]
-    constexpr int PER = T::RM * T::RN * 16 * 64;
-    if (kg > 0) {
-#pragma unroll
-      for (int i = 0; i < T::RM; ++i)
-#pragma unroll
-        for (int j = 0; j < T::RN; ++j)
-#pragma unroll
-          for (int e = 0; e < 16; ++e) red[((kg - 1) * 4 + wsp) * PER + ((i * T::RN + j) * 16 + e) * 64 + lane] = acc[i][j][e];
-    }
-    __syncthreads();
-    if (kg == 0) {
-#pragma unroll
-      for (int q = 0; q < KG - 1; ++q)
-#pragma unroll
-        for (int i = 0; i < T::RM; ++i)
-#pragma unroll
-          for (int j = 0; j < T::RN; ++j)
-#pragma unroll
-            for (int e = 0; e < 16; ++e) acc[i][j][e] += red[(q * 4 + wsp) * PER + ((i * T::RN + j) * 16 + e) * 64 + lane];
-    }
-    __syncthreads();
-  }
-  const bool owner = kg == 0;  // only K-group 0 holds the full sums; the others' stores are dropped
-
-  // ------------------------------------------------------------------ epilogue
-  // C/D map (32x32 f32 MFMA): col = lane & 31, row = (reg&3) + 8*(reg>>2) + 4*(lane>>5).
-  // Stores go through a buffer descriptor: rows/cols outside the GEMM get kOOB (dropped).
-  const bool slab = nsplit > 1;
-  if (slab || MODE == CS_CONV_DGRAD || (MODE == CS_CONV_WGRAD && !a.w_oihw)) {
-    float* dst = slab ? a.ws + (size_t)split * a.M * a.N : a.out;
-    const rsrc_t ro = make_rsrc(dst, (int64_t)a.M * a.N * 4);
-#pragma unroll
-    for (int i = 0; i < T::RM; ++i)
-#pragma unroll
-      for (int j = 0; j < T::RN; ++j) {
-        const int n = n0 + wn * T::WN + j * 32 + r;
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int m = m0 + wm * T::WM + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * hh;
-          bstore1(ro, acc[i][j][e], (owner && m < a.M && n < a.N) ? (m * a.N + n) * 4 : kOOB);
-        }
-      }
-    if constexpr (KG == 1) {
-      if (slab && a.counters != nullptr) splitk_fixup<BM, BN, MODE>(a, tile, mt, nt, nsplit, smem);
-    }
-    if (slab || MODE != CS_CONV_FWD) return;
-  }
-  if constexpr (MODE == CS_CONV_WGRAD) {  // conv0: scatter the padded (tap, ci) columns to OIHW
-#pragma unroll
-    for (int i = 0; i < T::RM; ++i)
-#pragma unroll
-      for (int j = 0; j < T::RN; ++j) {
-        const int n = n0 + wn * T::WN + j * 32 + r;
-        const int tap = n >> 2, ci = n & 3;
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int m = m0 + wm * T::WM + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * hh;
-          if (owner && m < a.M && n < a.N && ci < 3) a.out[(size_t)m * 27 + ci * 9 + tap] = acc[i][j][e];
-        }
-      }
-    return;
-  }
-  if constexpr (MODE == CS_CONV_FWD) {
-    // bias, store, and this tile's per-channel (mean, M2) for the BN statistics
-    float* red = smem;  // [2][BN] after the main loop's final barrier
-    const int cnt = (a.M - m0) < BM ? (a.M - m0) : BM;
-    const rsrc_t ro = make_rsrc(a.out, (int64_t)a.M * a.N * 4);
-    float colsum[T::RN];
-#pragma unroll
-    for (int j = 0; j < T::RN; ++j) {
-      const int n = n0 + wn * T::WN + j * 32 + r;
-      const float bv = (a.bias != nullptr && n < a.N) ? a.bias[n] : 0.f;
-      float s = 0.f;
-#pragma unroll
-      for (int i = 0; i < T::RM; ++i)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int m = m0 + wm * T::WM + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * hh;
-          const float v = acc[i][j][e] + bv;
-          acc[i][j][e] = v;
-          s += m < a.M ? v : 0.f;
-          bstore1(ro, v, (owner && m < a.M && n < a.N) ? (m * a.N + n) * 4 : kOOB);
-        }
-      colsum[j] = s + __shfl_xor(s, 32, 64);
-    }
-    if (a.stats == nullptr) return;
-#pragma unroll
-    for (int j = 0; j < T::RN; ++j)
-      if (owner && hh == 0) red[wm * BN + wn * T::WN + j * 32 + r] = colsum[j];
-    __syncthreads();
-    float mean[T::RN];
-#pragma unroll
-    for (int j = 0; j < T::RN; ++j) {
-      const int c = wn * T::WN + j * 32 + r;
-      mean[j] = (red[c] + red[BN + c]) / (float)cnt;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < T::RN; ++j) {
-      float s = 0.f;
-#pragma unroll
-      for (int i = 0; i < T::RM; ++i)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int m = m0 + wm * T::WM + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * hh;
-          const float d = acc[i][j][e] - mean[j];
-          s += m < a.M ? d * d : 0.f;
-        }
-      s += __shfl_xor(s, 32, 64);
-      if (owner && hh == 0) red[wm * BN + wn * T::WN + j * 32 + r] = s;
-    }
-    __syncthreads();
-    if (owner && wm == 0 && hh == 0) {
-#pragma unroll
-      for (int j = 0; j < T::RN; ++j) {
-        const int c = wn * T::WN + j * 32 + r, n = n0 + c;
-        if (n < a.N) {
-          a.stats[((size_t)mt * a.N + n) * 2 + 0] = mean[j];
-          a.stats[((size_t)mt * a.N + n) * 2 + 1] = red[c] + red[BN + c];
-        }
-      }
-    }
-  }
+  conv_epilogue<BM, BN, MODE, KG>(a, acc, tile, split, nsplit, smem);
 }
 
 template <int BM, int BN, int MODE, int BK, int SCHED, bool C4, int GL, int KG = 1>
@@ -1370,6 +1080,10 @@ int ilog2(int v) {
 }  // namespace
 
 int cs_conv_lg(int v) { return ilog2(v); }
+
+hipError_t cs_conv_splitk_reduce(const CsConvArgs& a, int mode, int splits, hipStream_t stream) {
+  return launch_reduce(a, mode, splits, stream);
+}
 
 void cs_conv_fill_dims(CsConvArgs* a, int mode) {
   a->lgH = ilog2(a->H);

@@ -68,6 +68,11 @@ struct CsConvArgs {
   // extra blocks after the GEMM tiles (dispatched last, they fill the GEMM's tail): an
   // independent BN-backward reduce (the block below's), red.P blocks; red.P == 0: none
   CsBnRed red;
+  // pre-split operands (conv_xp.hip): P3 bf16 chunks [n/8][3][8] (h, m, l of every 8 elements)
+  const uint16_t* x3;   // FWD / WGRAD: split conv input
+  const uint16_t* w3;   // FWD / DGRAD: split OHWI weights
+  const uint16_t* dz3;  // DGRAD / WGRAD: split output gradient
+  int64_t x3s, w3s, dz3s;  // element counts n (informational; the kernels derive the extents)
   // filled by the launcher:
   int lgH, lgW, lgCin, lgCout, M, N, K, ksteps_per_split, total_ksteps;
 };
@@ -106,6 +111,9 @@ inline bool cs_conv_dual_ok(int wstage, int wbk, int dstage, int dbk) {
   return ((wstage == (CS_STAGE_X6S | CS_STAGE_KG4) || wstage == (CS_STAGE_X6S | CS_STAGE_KG2)) && wbk == 64) ||
          (wstage == (CS_STAGE_X6S | CS_STAGE_REGS) && wbk == 16);
 }
+// deterministic split-K combine of `splits` fp32 slabs in a.ws (dims filled): sum in split order
+// (+bias and BN tile statistics of CS_SPLITK_STAT_ROWS rows for FWD; conv0's OIHW scatter for WGRAD)
+hipError_t cs_conv_splitk_reduce(const CsConvArgs& a, int mode, int splits, hipStream_t stream);
 // the split count cs_conv_gemm actually launches (K-steps re-balanced over splits)
 int cs_conv_effective_splits(int K, int bk, int splits);
 // split-K slabs of one tile a single block combines in-launch (S * BM * BN * 4 bytes)
@@ -113,6 +121,16 @@ int cs_conv_effective_splits(int K, int bk, int splits);
 bool cs_conv_fixup_ok(int splits, int bm, int bn);
 // FWD statistics tile height for a launch (bm, or CS_SPLITK_STAT_ROWS behind the reduce kernel)
 int cs_conv_stat_rows(int K, int bm, int bn, int bk, int splits, bool counters);
+
+// pre-split ("XP") conv GEMMs (conv_xp.hip): operands as three bf16 planes (x = h + m + l),
+// fp32-accurate six-product split-bf16 MFMA maths, LDS-DMA ring staging. bm, bn in {64, 128},
+// bk in {32, 64}, kg K-groups of 4 waves in {1, 2}, nb LDS ring stages (0 = as many as fit one
+// block per CU; 2-3 on some bk-32 tiles so two blocks share a CU) — cs_conv_xp_ok; layers with
+// Cin, Cout >= 64.
+bool cs_conv_xp_ok(int bm, int bn, int bk, int kg, int nb = 0);
+hipError_t cs_conv_xp(CsConvArgs a, int mode, int bm, int bn, int bk, int splits, int kg, int nb, hipStream_t stream);
+// fp32 x[n] (n % 8 == 0) -> P3 bf16 chunks out[n/8][3][8] (h, m, l)
+hipError_t cs_split3(const float* x, uint16_t* out, int64_t n, hipStream_t stream);
 
 // ---------------------------------------------------------------- BatchNorm + ReLU (+ 2x2 max-pool), NHWC
 hipError_t cs_bn_finalize(const float* part, int T, int R, int M, int C, const float* gamma, const float* beta,
@@ -163,12 +181,13 @@ hipError_t cs_comm_spin(double us, hipStream_t stream);
 hipError_t cs_comm_scramble(void* buf, int64_t n, int kind, int inverse, hipStream_t stream);
 
 // ---------------------------------------------------------------- stream links (stream_link.hip)
-// signal: count += 1 on `stream`; wait: *expect += delta, then poll until count >= *expect
-// (bounded by timeout_s; on timeout *err = 1 in host-mapped memory). count / expect: device
-// memory, zeroed.
+// signal: count += 1 on `stream`; wait: *expect += delta, then poll until count >= *expect.
+// The wait ends early only when the host sets *abort (host-mapped; *err = 2) or after timeout_s
+// (*err = 1; the engine sets it to the communicator timeout, so the step watchdog fires
+// first). count / expect: device memory, zeroed; err / abort: host-mapped.
 hipError_t cs_link_signal(unsigned long long* count, hipStream_t stream);
-hipError_t cs_link_wait(const unsigned long long* count, unsigned long long* expect, int* err, double timeout_s,
-                        hipStream_t stream, unsigned long long delta = 1);
+hipError_t cs_link_wait(const unsigned long long* count, unsigned long long* expect, int* err, const int* abort,
+                        double timeout_s, hipStream_t stream, unsigned long long delta = 1);
 
 // ---------------------------------------------------------------- decoder-LM elementwise ops (lm.hip)
 enum { CS_F32 = 0, CS_BF16 = 1 };

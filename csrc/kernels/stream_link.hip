@@ -11,8 +11,14 @@
 // The producers' writes are already released by the AQL kernel-boundary fence before the
 // signal kernel starts (in-order queue), and the consumer's next kernel starts with its own
 // acquire. Counters are monotonic and the expected count lives on the device, so a link is
-// graph-capturable. Every wait is bounded (timeout -> error word in host-mapped memory, the
-// host's async_error() sees it): a lost signal can never hang the GPU.
+// graph-capturable. A wait never releases its consumer before the signal except
+//  * on the host's abort word (host-mapped, set by the step watchdog / communicator abort:
+//    the run is failing anyway) -> error word 2, or
+//  * after timeout_s -> error word 1. The engine ties timeout_s to the communicator timeout
+//    (cfg.timeout_s, >= the step watchdog), so a late peer is waited for, not raced: an early
+//    release would let SGD read a bucket that an all-reduce is still writing.
+// Either error makes the host's next check raise; a lost signal can never hang the GPU for
+// longer than the timeout.
 #include "common.h"
 #include "launchers.h"
 
@@ -26,7 +32,7 @@ __global__ __launch_bounds__(64) void link_signal_kernel(unsigned long long* cou
 }
 
 __global__ __launch_bounds__(64) void link_wait_kernel(unsigned long long* count, unsigned long long* expect,
-                                                       int* err, unsigned long long timeout_ticks,
+                                                       int* err, const int* abort, unsigned long long timeout_ticks,
                                                        unsigned long long delta, unsigned long long zero) {
   if (threadIdx.x != 0) return;
   // Both words are read with atomic read-modify-writes, never plain or sc1 loads: consecutive
@@ -40,10 +46,16 @@ __global__ __launch_bounds__(64) void link_wait_kernel(unsigned long long* count
   const unsigned long long t0 = wall_clock64();
   // (`zero` is a kernel argument, 0 at run time: with a literal 0 the compiler turns the
   // read-modify-write back into a plain load)
-  while (__hip_atomic_fetch_add(count, zero, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < e) {
-    if (wall_clock64() - t0 > timeout_ticks) {
-      __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      break;
+  for (unsigned it = 0; __hip_atomic_fetch_add(count, zero, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < e; ++it) {
+    if ((it & 255) == 255) {  // host-side checks every 256 polls (a PCIe read each)
+      if (__hip_atomic_load(abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) {
+        __hip_atomic_store(err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+      if (wall_clock64() - t0 > timeout_ticks) {
+        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
     }
     __builtin_amdgcn_s_sleep(1);
   }
@@ -57,10 +69,10 @@ hipError_t cs_link_signal(unsigned long long* count, hipStream_t stream) {
   return hipGetLastError();
 }
 
-hipError_t cs_link_wait(const unsigned long long* count, unsigned long long* expect, int* err, double timeout_s,
-                        hipStream_t stream, unsigned long long delta) {
-  const double t = timeout_s < 1e-3 ? 1e-3 : (timeout_s > 60.0 ? 60.0 : timeout_s);
+hipError_t cs_link_wait(const unsigned long long* count, unsigned long long* expect, int* err, const int* abort,
+                        double timeout_s, hipStream_t stream, unsigned long long delta) {
+  const double t = timeout_s < 1e-3 ? 1e-3 : (timeout_s > 86400.0 ? 86400.0 : timeout_s);
   hipLaunchKernelGGL(link_wait_kernel, dim3(1), dim3(64), 0, stream, const_cast<unsigned long long*>(count), expect, err,
-                     (unsigned long long)(t * 1e8), delta, 0ull);  // wall_clock64: 100 MHz
+                     abort, (unsigned long long)(t * 1e8), delta, 0ull);  // wall_clock64: 100 MHz
   return hipGetLastError();
 }

@@ -65,7 +65,16 @@ void reserve_streams();
 // One-direction kernel stream link (stream_link.hip): signal(producer) enqueues a one-lane
 // counter bump; wait(consumer) makes the consumer wait for EVERY signal issued so far (the
 // host counts them; the device keeps the expected count, so captured graphs replay
-// correctly). Bounded waits: a timeout sets error().
+// correctly). A wait releases its consumer early only on abort_links() or after the
+// process-wide link timeout; either sets error().
+// Link timeout: set_link_timeout(s) (the trainer passes its communicator timeout,
+// cfg.timeout_s; CS_COMM_LINK_TIMEOUT_S overrides; default 1800 s), read at each wait's enqueue.
+void set_link_timeout(double seconds);
+double link_timeout();
+// host abort word polled by every link wait: set by the step watchdog / communicator abort so
+// waiting kernels end (error 2) instead of spinning to the timeout; reset_link_abort() re-arms
+void abort_links();
+void reset_link_abort();
 class StreamLink {
  public:
   StreamLink();
@@ -78,9 +87,8 @@ class StreamLink {
 
  private:
   unsigned long long* dev_ = nullptr;  // [count, expect]
-  int* err_ = nullptr;                 // host-mapped timeout word
+  int* err_ = nullptr;                 // host-mapped error word: 1 timeout, 2 aborted
   unsigned long long pending_ = 0;     // signals issued since the last wait
-  double timeout_s_ = 10.0;
   hipEvent_t ev_ = nullptr;            // CS_LINK_EVENTS=1 (diagnostic): the same link through an event
 };
 

@@ -12,10 +12,33 @@ void hip_ok(hipError_t e, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string("StreamBridge: ") + what + ": " + hipGetErrorString(e));
 }
 constexpr size_t kForkEvents = 64;
+
+double g_link_timeout = [] {
+  const char* e = getenv("CS_COMM_LINK_TIMEOUT_S");
+  return e ? atof(e) : 1800.0;
+}();
+
+int* abort_word() {
+  static int* w = [] {
+    void* h = nullptr;
+    hip_ok(hipHostMalloc(&h, sizeof(int), hipHostMallocMapped), "hipHostMalloc(link abort word)");
+    *static_cast<int*>(h) = 0;
+    return static_cast<int*>(h);
+  }();
+  return w;
+}
 }  // namespace
 
+void set_link_timeout(double seconds) {
+  if (getenv("CS_COMM_LINK_TIMEOUT_S") != nullptr) return;  // the environment wins
+  g_link_timeout = seconds > 0.0 ? seconds : 1800.0;
+}
+double link_timeout() { return g_link_timeout; }
+void abort_links() { __atomic_store_n(abort_word(), 1, __ATOMIC_RELEASE); }
+void reset_link_abort() { __atomic_store_n(abort_word(), 0, __ATOMIC_RELEASE); }
+
 StreamLink::StreamLink() {
-  if (const char* e = getenv("CS_COMM_LINK_TIMEOUT_S")) timeout_s_ = atof(e);
+  (void)abort_word();
   void* p = nullptr;
   hip_ok(hipMalloc(&p, 2 * sizeof(unsigned long long)), "hipMalloc(link counters)");
   hip_ok(hipMemset(p, 0, 2 * sizeof(unsigned long long)), "hipMemset(link counters)");
@@ -49,14 +72,17 @@ void StreamLink::wait(hipStream_t consumer) {
   if (ev_) {
     hip_ok(hipStreamWaitEvent(consumer, ev_, 0), "link event wait");
   } else {
-    hip_ok(cs_link_wait(dev_, dev_ + 1, err_, timeout_s_, consumer, pending_), "link wait");
+    hip_ok(cs_link_wait(dev_, dev_ + 1, err_, abort_word(), g_link_timeout, consumer, pending_), "link wait");
   }
   pending_ = 0;
 }
 
 std::string StreamLink::error() const {
-  if (err_ != nullptr && __atomic_load_n(err_, __ATOMIC_ACQUIRE) != 0)
-    return "stream link wait timed out (a signal never arrived)";
+  const int e = err_ != nullptr ? __atomic_load_n(err_, __ATOMIC_ACQUIRE) : 0;
+  if (e == 1)
+    return "stream link wait timed out after " + std::to_string(g_link_timeout) +
+           " s (its signal never arrived; the consumer ran unordered)";
+  if (e == 2) return "stream link wait aborted (abort_links)";
   return std::string();
 }
 

@@ -171,6 +171,62 @@ def test_probe_comm_detects_missing_join(gpu):
     assert not torch.equal(base["params"], bad["params"])
 
 
+def test_link_timeout_fails_loudly(gpu):
+    """A link wait released by its timeout (here shorter than the probe collective it waits
+    for) must surface: the next communicator check raises instead of training on."""
+    from cs744_pytorch_distributed_tutorial_amd.runtime.engine import NativeTrainer
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    tr = NativeTrainer(batch_size=32, device=dev, bucket_mb=1.0, graph="none", train_size=256, test_size=32,
+                       autotune=False, probe="order", probe_spin_us=50000.0, timeout_s=0.002)
+    try:
+        tr.step()
+        torch.cuda.synchronize()
+        with pytest.raises(RuntimeError, match="stream link"):
+            tr.check_comm()
+    finally:
+        tr.close()
+
+
+def test_link_default_timeout_waits_for_slow_collective(gpu):
+    """The link timeout is the communicator timeout (1800 s default, was a fixed 10 s): slow
+    collectives (60 ms each here) are waited for and the probe run stays bitwise equal to the
+    no-comm run."""
+    from cs744_pytorch_distributed_tutorial_amd.ops import native
+    base, _ = _probe_run("0", steps=2)
+    from cs744_pytorch_distributed_tutorial_amd.runtime.engine import NativeTrainer
+    dev = torch.device("cuda", 0)
+    tr = NativeTrainer(batch_size=32, device=dev, bucket_mb=1.0, graph="none", train_size=512, test_size=32,
+                       autotune=False, probe="order", probe_spin_us=60000.0)
+    if "CS_COMM_LINK_TIMEOUT_S" not in os.environ:
+        assert native.C().link_timeout() == 1800.0
+    for _ in range(2):
+        tr.step()
+    torch.cuda.synchronize()
+    tr.check_comm()
+    for k in ("params", "mom", "bufs", "nbt"):
+        assert torch.equal(base[k], getattr(tr, k)), k
+    tr.close()
+
+
+def test_link_abort_releases_waits(gpu):
+    """abort() (the watchdog path) releases a waiting link kernel; the error is reported."""
+    from cs744_pytorch_distributed_tutorial_amd.ops import native
+    from cs744_pytorch_distributed_tutorial_amd.runtime.engine import NativeTrainer
+    dev = torch.device("cuda", 0)
+    tr = NativeTrainer(batch_size=32, device=dev, bucket_mb=1.0, graph="none", train_size=256, test_size=32,
+                       autotune=False, probe="order", probe_spin_us=80000.0)
+    try:
+        tr.abort()
+        tr.step()
+        torch.cuda.synchronize()
+        with pytest.raises(RuntimeError, match="aborted"):
+            tr.check_comm()
+    finally:
+        native.C().reset_link_abort()
+        tr.close()
+
+
 def test_rccl_one_rank_abort_path(gpu):
     """World-1 RCCL: async-error poll is clean, abort() makes the next collective raise
     instead of touching a freed communicator."""
