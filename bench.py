@@ -104,6 +104,24 @@ def describe(args, trainer, world):
             "synthetic (ImageNet shape 3x224x224 uint8 pool on device), random-init weights")
 
 
+def comm_kind(trainer, world: int) -> str:
+    """The gradient transport the timed steps actually used."""
+    if world == 1:
+        return "none"
+    if getattr(trainer, "comm_kind", None):  # native engine
+        return trainer.comm_kind
+    net = getattr(trainer, "net", None)
+    comm = getattr(net, "comm", None)  # framework DDP (TorchTrainer)
+    return getattr(comm, "kind", "torch") if comm is not None else "torch"
+
+
+def comm_ctas_used(trainer):
+    native = getattr(trainer, "native_comm", None)
+    if native is None:
+        native = getattr(getattr(getattr(trainer, "net", None), "comm", None), "native", None)
+    return getattr(native, "max_ctas", None)
+
+
 def main(argv=None) -> int:
     args = parse(argv)
     if args.batch_size is None:
@@ -166,6 +184,7 @@ def main(argv=None) -> int:
     if hasattr(trainer, "check_comm"):
         trainer.check_comm()  # async RCCL errors surface here instead of as a silent bad number
     elapsed = D.all_reduce_scalar(elapsed, op=D.ReduceOp.MAX) if world > 1 else elapsed
+    comm_used = comm_kind(trainer, world)
     loss = trainer.last_loss()
     metric, unit, gbatch, seq, baseline, data = describe(args, trainer, world)
     per_step = gbatch * (seq or 1)
@@ -186,7 +205,8 @@ def main(argv=None) -> int:
         "data": data,
         "config": {"model": args.model, "global_batch": gbatch, "per_gpu_batch": args.batch_size, "seq_len": seq,
                    "parallelism": f"dp{world}", "sync": args.sync if world > 1 else "none", "engine": engine,
-                   "comm": args.comm, "bucket_mb": args.bucket_mb,
+                   "comm": comm_used, "comm_requested": args.comm if world > 1 else None,
+                   "comm_ctas": comm_ctas_used(trainer), "hw_queues": _pkg.hw_queues(), "bucket_mb": args.bucket_mb,
                    "optimizer": "SGD(lr=0.1, momentum=0.9, wd=1e-4)", "final_loss": round(loss, 4),
                    "baseline_img_s": baseline},
     }
@@ -213,6 +233,11 @@ def main(argv=None) -> int:
     if world > 1:
         D.barrier()
         D.destroy_process_group()
+    if world > 1 and args.comm == "rccl" and comm_used != "rccl":
+        # the number above ran on the fallback transport, not the RCCL data plane it claims to price
+        print(f"[bench] --comm rccl requested but the job ran on {comm_used!r} (native communicator "
+              "construction failed on some rank)", file=sys.stderr, flush=True)
+        return 3
     return 0
 
 

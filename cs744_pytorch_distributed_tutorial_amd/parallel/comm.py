@@ -81,6 +81,8 @@ _OPS = {"sum": D.ReduceOp.SUM, "avg": D.ReduceOp.AVG, "max": D.ReduceOp.MAX, "mi
 
 
 class TorchComm(Comm):
+    kind = "torch"
+
     def __init__(self, group=None):
         self.group = group
         self.rank = D.get_rank(group)
@@ -134,36 +136,71 @@ class TorchComm(Comm):
         D.irecv(buf, src, group=self.group).wait()
 
 
-def _agreed(build, group, what: str) -> Comm:
-    """Build a native communicator on every rank, or on none: each rank reports whether its
-    construction succeeded (one MIN all-reduce over the process group), and if any rank failed
-    all of them fall back to the torch.distributed communicator — a rank that cannot join the
-    native RCCL communicator must not leave its peers waiting inside the first collective."""
+def _all_ok(ok: bool, group) -> bool:
+    """One MIN all-reduce of a per-rank success flag over ``group`` (its backend's device)."""
+    import torch.distributed as dist
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else "cpu"
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    return int(t.item()) == 1
+
+
+def _agreed(build, group, what: str, prepare=None, share=None) -> Comm:
+    """Build a native communicator on every rank, or on none, in two agreed phases (a rank that
+    cannot join must not leave its peers waiting inside a collective):
+
+    1. ``prepare()`` — purely local (load the extension, create the RCCL unique id on rank 0, set
+       the device); every rank reports success in one MIN all-reduce, and only if ALL succeeded
+    2. ``share(ctx)`` — the collective exchange (the unique id's broadcast), then ``build(shared)``
+       (``ncclCommInitRankConfig``), and a second MIN all-reduce on the outcome.
+    Any failure in either phase takes every rank to the torch.distributed communicator.
+    ``prepare``/``share`` default to no-ops, so ``build()`` alone gets the one-phase agreement."""
     import sys
 
     import torch.distributed as dist
-    comm, err = None, None
+
+    def fallback(err):
+        print(f"[comm] native {what} communicator unavailable on some rank ({err!r} here); "
+              "every rank falls back to torch.distributed", file=sys.stderr, flush=True)
+        return TorchComm(group)
+
+    ctx, err = None, None
     try:
-        comm = build()
+        ctx = prepare() if prepare is not None else None
     except Exception as e:  # noqa: BLE001 - reported, then agreed on below
         err = e
     if not dist.is_initialized():
         if err is not None:
             raise err
+        shared = share(ctx) if share is not None else ctx
+        return build(shared) if prepare is not None else build()
+    if prepare is not None and not _all_ok(err is None, group):
+        return fallback(err)
+    comm = None
+    try:
+        if prepare is not None:
+            shared = share(ctx) if share is not None else ctx
+            comm = build(shared)
+        else:
+            comm = build()
+    except Exception as e:  # noqa: BLE001
+        err = e
+    if _all_ok(err is None, group):
         return comm
-    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else "cpu"
-    ok = torch.tensor([0 if err is not None else 1], dtype=torch.int32, device=dev)
-    dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)
-    if int(ok.item()) == 1:
-        return comm
-    print(f"[comm] native {what} communicator unavailable on some rank ({err!r} here); "
-          "every rank falls back to torch.distributed", file=sys.stderr, flush=True)
     if comm is not None and hasattr(comm, "close"):
         comm.close()
-    return TorchComm(group)
+    return fallback(err)
 
 
-def make_comm(kind: Optional[str] = None, group=None) -> Comm:
+def comm_ctas() -> int:
+    """RCCL compute budget (ncclConfig_t maxCTAs) for the native communicator: CS_COMM_CTAS, default
+    16 — the bucketed all-reduces that overlap the backward then take at most 16 of the 256 CUs
+    from the conv GEMMs; 0 leaves the choice to RCCL."""
+    import os
+    return int(os.environ.get("CS_COMM_CTAS", "16"))
+
+
+def make_comm(kind: Optional[str] = None, group=None, max_ctas: Optional[int] = None) -> Comm:
     """``kind``: ``"torch"`` (default), ``"rccl"`` (native C++ RCCL communicator, one GPU per
     rank) or ``"staged"`` (native C++ communicator over a gloo group with host staging: the
     engine's C++ step with several ranks on one GPU, ``parallel.staged``)."""
@@ -172,7 +209,9 @@ def make_comm(kind: Optional[str] = None, group=None) -> Comm:
         return TorchComm(group)
     if kind == "rccl":
         from .rccl import RcclComm
-        return _agreed(lambda: RcclComm.from_process_group(group), group, "rccl")
+        ctas = comm_ctas() if max_ctas is None else max_ctas
+        return _agreed(lambda uid: RcclComm.build(uid, group, ctas), group, "rccl",
+                       prepare=lambda: RcclComm.prepare(group), share=lambda uid: RcclComm.share_uid(uid, group))
     if kind == "staged":
         from .staged import StagedComm
         return StagedComm(group)

@@ -38,21 +38,37 @@ class RcclComm(Comm):
         self.world_size = native_comm.world_size
 
     @classmethod
-    def create(cls, rank: int, world: int, device: int, uid: Optional[bytes] = None) -> "RcclComm":
+    def create(cls, rank: int, world: int, device: int, uid: Optional[bytes] = None, max_ctas: int = 0) -> "RcclComm":
         if uid is None:
             if world != 1:
                 raise ValueError("RcclComm.create: a shared unique id is required for world > 1")
             uid = native.C().rccl_unique_id()
-        return cls(native.C().RcclComm(uid, rank, world, device))
+        return cls(native.C().RcclComm(uid, rank, world, device, True, int(max_ctas)))
+
+    # construction in the three steps comm._agreed agrees on: local preparation, the collective
+    # exchange of the unique id, then ncclCommInitRankConfig
+    @staticmethod
+    def prepare(group=None) -> Optional[bytes]:
+        """Local only: load the extension, select the device; rank 0 creates the unique id."""
+        C = native.C()
+        torch.cuda.current_device()
+        return C.rccl_unique_id() if D.get_rank(group) == 0 else None
+
+    @staticmethod
+    def share_uid(uid: Optional[bytes], group=None) -> bytes:
+        obj = [uid]
+        if D.get_world_size(group) > 1:
+            torch.distributed.broadcast_object_list(obj, src=0, group=group)
+        return obj[0]
 
     @classmethod
-    def from_process_group(cls, group=None) -> "RcclComm":
+    def build(cls, uid: bytes, group=None, max_ctas: int = 0) -> "RcclComm":
         rank, world = D.get_rank(group), D.get_world_size(group)
-        obj = [native.C().rccl_unique_id() if rank == 0 else None]
-        if world > 1:
-            torch.distributed.broadcast_object_list(obj, src=0, group=group)
-        dev = torch.cuda.current_device()
-        return cls(native.C().RcclComm(obj[0], rank, world, dev))
+        return cls(native.C().RcclComm(uid, rank, world, torch.cuda.current_device(), True, int(max_ctas)))
+
+    @classmethod
+    def from_process_group(cls, group=None, max_ctas: int = 0) -> "RcclComm":
+        return cls.build(cls.share_uid(cls.prepare(group), group), group, max_ctas)
 
     # ---- Comm interface (all stream-ordered; handles join the comm stream back)
     def all_reduce_avg(self, buf: torch.Tensor, async_op: bool = True) -> Handle:

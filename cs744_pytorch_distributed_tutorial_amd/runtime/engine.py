@@ -225,11 +225,13 @@ class NativeTrainer:
             os.environ["CS_COMM_FORK"] = "0"
         # communicator + DDP construction-time sync (params + buffers from rank 0)
         self.comm = None
-        self.comm_kind = comm if world > 1 else "none"
         if world > 1:
             from ..parallel.comm import make_comm
             self.comm = make_comm(comm)
             self.sync_from_root()
+        # the communicator actually in use (make_comm falls back to torch.distributed on every rank
+        # when one cannot build the native one)
+        self.comm_kind = getattr(self.comm, "kind", "torch") if self.comm is not None else "none"
         self.native_comm = getattr(self.comm, "native", None)
         probe = probe if probe is not None else os.environ.get("CS_COMM_PROBE", "0")
         if world == 1 and probe not in (None, "", "0"):

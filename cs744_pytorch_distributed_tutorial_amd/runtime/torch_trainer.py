@@ -27,6 +27,7 @@ import torch
 import torch.nn as nn
 
 from ..parallel import DistributedDataParallel, make_comm, make_sync
+from ..utils.metrics import roctx_range
 
 
 def build_model(name: str) -> nn.Module:
@@ -121,16 +122,19 @@ class TorchTrainer:
     def step(self) -> None:
         x, y = self.data.next()
         self.opt.zero_grad()  # DDP re-attaches its bucket views (and zeroes them) in forward
-        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=self.dtype == "bf16"):
+        with roctx_range("cs.forward"), torch.autocast("cuda", dtype=torch.bfloat16, enabled=self.dtype == "bf16"):
             out = self.net(x)
             if self.is_lm:  # fused gfx950 softmax cross-entropy over the bf16 logits (ops.lm)
                 from ..ops.lm import cross_entropy
                 loss = cross_entropy(out.view(-1, out.shape[-1]), y.view(-1))
             else:
                 loss = self.crit(out.float(), y)
-        loss.backward()
-        self.sync()
-        self.opt.step()
+        with roctx_range("cs.backward"):  # DDP's bucket all-reduces are enqueued from its hooks in here
+            loss.backward()
+        with roctx_range("cs.sync"):
+            self.sync()
+        with roctx_range("cs.sgd"):
+            self.opt.step()
         self.loss = loss.detach()
 
     def last_loss(self) -> float:

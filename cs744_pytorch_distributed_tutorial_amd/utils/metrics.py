@@ -147,10 +147,31 @@ def reduce_eval(comm, loss_sum: float, correct: int, total: int, batches: int,
     return {"global_avg_loss": ls / max(nb, 1.0), "global_correct": int(c), "global_total": int(n)}
 
 
-def roctx_range(name: str):
-    """Context manager emitting a roctx range (visible in rocprofv3 marker traces)."""
-    try:
-        return torch.cuda.nvtx.range(name)  # maps to roctx on ROCm builds
-    except Exception:  # pragma: no cover - no GPU profiler
-        import contextlib
-        return contextlib.nullcontext()
+class roctx_range:
+    """Context manager emitting a roctx range through the native extension's marker hook
+    (rocprofiler-sdk-roctx, the library ``rocprofv3 --marker-trace`` records; csrc/runtime/markers.h),
+    so the autograd-path trainers' phases (forward / backward / sync / optimizer) line up with the
+    native engine's ``cs.*`` ranges in one trace. A no-op without the extension or the library."""
+
+    _C = None
+
+    def __init__(self, name: str):
+        self.name = name
+
+    def __enter__(self):
+        C = roctx_range._C
+        if C is None:
+            try:
+                from ..ops import native
+                C = native.C() if native.available() else False
+            except Exception:  # pragma: no cover - no extension
+                C = False
+            roctx_range._C = C
+        if C:
+            C.roctx_push(self.name)
+        return self
+
+    def __exit__(self, *exc):
+        if roctx_range._C:
+            roctx_range._C.roctx_pop()
+        return False

@@ -1,6 +1,7 @@
 // pybind11 bindings of the native runtime: the RCCL communicator and the VGG engine.
 // Collectives take torch tensors and run stream-ordered w.r.t. torch's current stream.
 #include "binding/torch_util.h"
+#include "runtime/markers.h"
 #include "runtime/rccl_comm.h"
 #include "runtime/staged_comm.h"
 #include "runtime/vgg_engine.h"
@@ -72,6 +73,15 @@ void register_runtime(pybind11::module& m) {
       .def("join", [](cs::DeviceComm& c) { c.join(cur_stream()); })
       .def("async_error", &cs::DeviceComm::async_error)
       .def("abort", &cs::DeviceComm::abort);
+  m.def("roctx_available", &cs::roctx_available, "whether the native step emits roctx phase ranges");
+  m.def("roctx_push", [](const std::string& n) {
+    const auto& r = cs::Roctx::get();
+    if (r.push) r.push(n.c_str());
+  });
+  m.def("roctx_pop", []() {
+    const auto& r = cs::Roctx::get();
+    if (r.pop) r.pop();
+  });
   m.def("set_link_timeout", &cs::set_link_timeout,
         "stream-link wait timeout in seconds (the communicator timeout; CS_COMM_LINK_TIMEOUT_S overrides)");
   m.def("link_timeout", &cs::link_timeout);
@@ -82,10 +92,12 @@ void register_runtime(pybind11::module& m) {
   py::class_<cs::ProbeComm, cs::DeviceComm>(m, "ProbeComm")
       .def(py::init<int, double>(), py::arg("device"), py::arg("spin_us") = 20.0);
   py::class_<cs::RcclComm, cs::DeviceComm>(m, "RcclComm")
-      .def(py::init([](py::bytes uid, int rank, int world, int device, bool high_priority) {
-             return new cs::RcclComm(std::string(uid), rank, world, device, high_priority);
+      .def(py::init([](py::bytes uid, int rank, int world, int device, bool high_priority, int max_ctas) {
+             return new cs::RcclComm(std::string(uid), rank, world, device, high_priority, max_ctas);
            }),
-           py::arg("uid"), py::arg("rank"), py::arg("world"), py::arg("device"), py::arg("high_priority") = true)
+           py::arg("uid"), py::arg("rank"), py::arg("world"), py::arg("device"), py::arg("high_priority") = true,
+           py::arg("max_ctas") = 0)
+      .def_property_readonly("max_ctas", &cs::RcclComm::max_ctas)
       .def("all_gather",
            [](cs::RcclComm& c, torch::Tensor in, torch::Tensor out) {
              check_gpu(in, "in"); check_gpu(out, "out");

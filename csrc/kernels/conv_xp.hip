@@ -34,6 +34,8 @@
 // multiplies sub-steps [g*NG/KG, (g+1)*NG/KG) of every staged K-step and the groups' partial
 // sums meet in the shared epilogue (conv_common.h). Split-K slabs are combined by the same
 // deterministic reduce as conv_gemm.hip.
+#include <stdlib.h>
+
 #include "conv_common.h"
 
 namespace {
@@ -271,7 +273,10 @@ __device__ __forceinline__ void wait_ahead(int ahead) {
   wait_vmcnt<0>();
 }
 
-template <int BM, int BN, int MODE, int BK, int KG, int NBX>
+// PROBE (measurement only, wrong numbers; CS_XP_PROBE): 1 = no LDS-DMA in the K-loop (fragment
+// reads + MFMAs + barriers on stale stages), 2 = no MFMAs (operands kept live), 3 = no fragment
+// reads and no MFMAs (DMA + barriers only)
+template <int BM, int BN, int MODE, int BK, int KG, int NBX, int PROBE = 0>
 __device__ __forceinline__ void xp_body(const CsConvArgs& a, const int tile, const int split, const int nsplit,
                                         char* smem) {
   using T = XpTile<BM, BN, MODE, BK, KG, NBX>;
@@ -302,23 +307,35 @@ __device__ __forceinline__ void xp_body(const CsConvArgs& a, const int tile, con
     wait_ahead<T::NI, NB - 2>(min(NB - 2, nks - 1 - t));
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    if (t + NB - 1 < nks) {
+    if (PROBE != 1 && t + NB - 1 < nks) {
       const int nx = cur == 0 ? NB - 1 : cur - 1;  // (t + NB - 1) % NB: the stage read at step t-1
       ld.issue(a, (ks_begin + t + NB - 1) * BK, smem + nx * T::STAGE);
     }
     const char* As = smem + cur * T::STAGE;
     const char* Bs = As + T::SA * 16;
-    bf16x8 fa[2][3][T::RM], fb[2][3][T::RN];
-    const int s0 = kg * T::NGK;
-    xp_frags<T::A_KC, BM, BK, T::RM>(As, wm * T::WM, s0, lane, fa[0]);
-    xp_frags<T::B_KC, BN, BK, T::RN>(Bs, wn * T::WN, s0, lane, fb[0]);
+    if constexpr (PROBE != 3) {
+      bf16x8 fa[2][3][T::RM], fb[2][3][T::RN];
+      const int s0 = kg * T::NGK;
+      xp_frags<T::A_KC, BM, BK, T::RM>(As, wm * T::WM, s0, lane, fa[0]);
+      xp_frags<T::B_KC, BN, BK, T::RN>(Bs, wn * T::WN, s0, lane, fb[0]);
 #pragma unroll
-    for (int s = 0; s < T::NGK; ++s) {
-      if (s + 1 < T::NGK) {
-        xp_frags<T::A_KC, BM, BK, T::RM>(As, wm * T::WM, s0 + s + 1, lane, fa[(s + 1) & 1]);
-        xp_frags<T::B_KC, BN, BK, T::RN>(Bs, wn * T::WN, s0 + s + 1, lane, fb[(s + 1) & 1]);
+      for (int s = 0; s < T::NGK; ++s) {
+        if (s + 1 < T::NGK) {
+          xp_frags<T::A_KC, BM, BK, T::RM>(As, wm * T::WM, s0 + s + 1, lane, fa[(s + 1) & 1]);
+          xp_frags<T::B_KC, BN, BK, T::RN>(Bs, wn * T::WN, s0 + s + 1, lane, fb[(s + 1) & 1]);
+        }
+        if constexpr (PROBE == 2) {
+#pragma unroll
+          for (int q = 0; q < 3; ++q) {
+#pragma unroll
+            for (int i = 0; i < T::RM; ++i) asm volatile("" ::"v"(fa[s & 1][q][i]));
+#pragma unroll
+            for (int j = 0; j < T::RN; ++j) asm volatile("" ::"v"(fb[s & 1][q][j]));
+          }
+        } else {
+          xp_mma<T::RM, T::RN>(fa[s & 1], fb[s & 1], acc);
+        }
       }
-      xp_mma<T::RM, T::RN>(fa[s & 1], fb[s & 1], acc);
     }
     cur = cur == NB - 1 ? 0 : cur + 1;
   }
@@ -326,7 +343,7 @@ __device__ __forceinline__ void xp_body(const CsConvArgs& a, const int tile, con
   conv_epilogue<BM, BN, MODE, KG>(a, acc, tile, split, nsplit, reinterpret_cast<float*>(smem));
 }
 
-template <int BM, int BN, int MODE, int BK, int KG, int NBX>
+template <int BM, int BN, int MODE, int BK, int KG, int NBX, int PROBE = 0>
 __global__ __launch_bounds__(256 * KG) void conv_xp_kernel(CsConvArgs a) {
   extern __shared__ __attribute__((aligned(16))) char xsm[];
   const int ntiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
@@ -337,7 +354,7 @@ __global__ __launch_bounds__(256 * KG) void conv_xp_kernel(CsConvArgs a) {
     else cs_bn::bn_red_body<false>(a.red, lin - ng, a.red.P, reinterpret_cast<float*>(xsm));
     return;
   }
-  xp_body<BM, BN, MODE, BK, KG, NBX>(a, cs::xcd_remap(lin % ntiles, ntiles), lin / ntiles, nsplit, xsm);
+  xp_body<BM, BN, MODE, BK, KG, NBX, PROBE>(a, cs::xcd_remap(lin % ntiles, ntiles), lin / ntiles, nsplit, xsm);
 }
 
 // ---------------------------------------------------------------- producers
@@ -369,7 +386,7 @@ __global__ __launch_bounds__(256) void split3_kernel(const float* __restrict__ x
   }
 }
 
-template <int BM, int BN, int MODE, int BK, int KG, int NBX>
+template <int BM, int BN, int MODE, int BK, int KG, int NBX, int PROBE = 0>
 hipError_t launch_xp(const CsConvArgs& a, int splits, hipStream_t stream) {
   using T = XpTile<BM, BN, MODE, BK, KG, NBX>;
   const int ntiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
@@ -377,7 +394,7 @@ hipError_t launch_xp(const CsConvArgs& a, int splits, hipStream_t stream) {
   const size_t red = (size_t)(KG - 1) * 4 * T::RM * T::RN * 16 * 64 * sizeof(float);
   if (red > lds) lds = red;
   if (a.red.P > 0) lds = std::max(lds, cs_bn_red_lds(a.red.C));
-  hipLaunchKernelGGL((conv_xp_kernel<BM, BN, MODE, BK, KG, NBX>), dim3(ntiles * splits + a.red.P), dim3(256 * KG), lds,
+  hipLaunchKernelGGL((conv_xp_kernel<BM, BN, MODE, BK, KG, NBX, PROBE>), dim3(ntiles * splits + a.red.P), dim3(256 * KG), lds,
                      stream, a);
   return hipGetLastError();
 }
@@ -432,6 +449,18 @@ hipError_t cs_conv_xp(CsConvArgs a, int mode, int bm, int bn, int bk, int splits
   if (splits > 1 && (a.ws == nullptr || (int64_t)splits * a.M * a.N * 4 >= 0x7ffffff0ll)) return hipErrorInvalidValue;
   a.counters = nullptr;
   hipError_t e = hipErrorInvalidValue;
+  static const int probe = [] {
+    const char* v = getenv("CS_XP_PROBE");
+    return v ? atoi(v) : 0;
+  }();
+  if (probe > 0 && mode == CS_CONV_FWD && kg == 2 && nb == 0 && bm == bn && bm + bk == 128) {
+#define CS_XPP(BM_, BK_, P_)                                                                                 \
+  if (bm == BM_ && probe == P_) e = launch_xp<BM_, BM_, CS_CONV_FWD, BK_, 2, 0, P_>(a, splits, stream);
+    CS_XPP(64, 64, 1) CS_XPP(64, 64, 2) CS_XPP(64, 64, 3) CS_XPP(128, 32, 1) CS_XPP(128, 32, 2) CS_XPP(128, 32, 3)
+#undef CS_XPP
+    if (e != hipSuccess || splits == 1) return e;
+    return cs_conv_splitk_reduce(a, mode, splits, stream);
+  }
 #define CS_XP(BM_, BN_, BK_, KG_, NB_)                                  \
   if (bm == BM_ && bn == BN_ && bk == BK_ && kg == KG_ && nb == NB_) \
     e = launch_xp_mode<BM_, BN_, BK_, KG_, NB_>(a, mode, splits, stream);

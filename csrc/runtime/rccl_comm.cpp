@@ -37,8 +37,8 @@ unsigned comm_event_flags() {
 }
 }  // namespace
 
-RcclComm::RcclComm(const std::string& uid, int rank, int world, int device, bool high_priority)
-    : bridge_(comm_event_flags()), rank_(rank), world_(world), device_(device) {
+RcclComm::RcclComm(const std::string& uid, int rank, int world, int device, bool high_priority, int max_ctas)
+    : bridge_(comm_event_flags()), rank_(rank), world_(world), device_(device), max_ctas_(max_ctas) {
   if (uid.size() != sizeof(ncclUniqueId)) throw std::runtime_error("RcclComm: unique id must be 128 bytes");
   if (rank < 0 || rank >= world) throw std::runtime_error("RcclComm: bad rank");
   hip_ok(hipSetDevice(device), "hipSetDevice");
@@ -52,7 +52,15 @@ RcclComm::RcclComm(const std::string& uid, int rank, int world, int device, bool
   }
   ncclUniqueId id;
   std::memcpy(&id, uid.data(), sizeof(id));
-  nccl_ok(ncclCommInitRank(&comm_, world, id, rank), "ncclCommInitRank");
+  // ncclCommInitRankConfig: the header is ROCm 7.2's RCCL 2.27, the runtime torch's 2.26 — the
+  // library copies min(config.size, its own sizeof) bytes, and every field set here predates both
+  ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+  cfg.blocking = 1;
+  if (max_ctas > 0) {
+    cfg.maxCTAs = max_ctas;
+    cfg.minCTAs = max_ctas < 4 ? max_ctas : 4;
+  }
+  nccl_ok(ncclCommInitRankConfig(&comm_, world, id, rank, &cfg), "ncclCommInitRankConfig");
 }
 
 RcclComm::~RcclComm() {

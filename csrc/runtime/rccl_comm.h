@@ -24,7 +24,11 @@ class RcclComm final : public DeviceComm {
  public:
   static std::string unique_id();  // 128 raw bytes (NCCL_UNIQUE_ID_BYTES)
 
-  RcclComm(const std::string& uid, int rank, int world, int device, bool high_priority = true);
+  // max_ctas > 0: RCCL compute budget (ncclConfig_t maxCTAs, minCTAs <= it) so the bucketed
+  // all-reduces overlapping the backward take at most that many CUs from the conv GEMMs
+  // (SURVEY.md §5.8); 0 = RCCL's own choice
+  RcclComm(const std::string& uid, int rank, int world, int device, bool high_priority = true, int max_ctas = 0);
+  int max_ctas() const { return max_ctas_; }
   ~RcclComm();
   RcclComm(const RcclComm&) = delete;
   RcclComm& operator=(const RcclComm&) = delete;
@@ -67,7 +71,7 @@ class RcclComm final : public DeviceComm {
   // signal memory, was measured and dropped: 59.7k img/s vs 70.3-73.3k with events on the
   // one-rank probe, profiles/r1_dp_plumbing_probe.md)
   StreamBridge bridge_;
-  int rank_ = 0, world_ = 1, device_ = 0;
+  int rank_ = 0, world_ = 1, device_ = 0, max_ctas_ = 0;
   int group_depth_ = 0;
   bool aborted_ = false;
   int64_t calls_ = 0;

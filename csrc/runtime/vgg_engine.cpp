@@ -1,5 +1,7 @@
 #include "runtime/vgg_engine.h"
 
+#include "runtime/markers.h"
+
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 
 #include <stdio.h>
@@ -636,8 +638,12 @@ void VggEngine::step(int64_t B, DeviceComm* comm, const std::vector<int64_t>& bu
   const bool dp = comm != nullptr;
   const bool ovl = side_wgrad(s);
   tn_ = 0;
+  Range step_range("cs.step");
   mark("start");
-  forward_train(B);
+  {
+    Range r("cs.forward");
+    forward_train(B);
+  }
   mark("forward");
   // per-bucket SGD needs the buckets to tile the flat buffer exactly
   bool tiled = sgd_overlap_ && !ovl;
@@ -663,7 +669,12 @@ void VggEngine::step(int64_t B, DeviceComm* comm, const std::vector<int64_t>& bu
   for (size_t k = 0; k < nb; ++k) {
     const int64_t lo = bucket_blocks[k];
     TORCH_CHECK(lo <= hi, "step: bucket blocks must decrease");
+    static const char* kBwdR[] = {"cs.backward.bucket0", "cs.backward.bucket1", "cs.backward.bucket2",
+                                  "cs.backward.bucket3", "cs.backward.bucket4", "cs.backward.bucket5",
+                                  "cs.backward.bucket6", "cs.backward.bucket7"};
+    Range bwd_range(k < 8 ? kBwdR[k] : "cs.backward.bucket8+");
     backward(hi, lo, B, /*join=*/false);
+    bwd_range.end();
     static const char* kBwd[] = {"backward_bucket0", "backward_bucket1", "backward_bucket2", "backward_bucket3",
                                  "backward_bucket4", "backward_bucket5", "backward_bucket6", "backward_bucket7"};
     mark(k < 8 ? kBwd[k] : "backward_bucket8+");
@@ -677,9 +688,11 @@ void VggEngine::step(int64_t B, DeviceComm* comm, const std::vector<int64_t>& bu
       join_side(s);
       src = s;
     }
-    if (dp)
+    if (dp) {
+      Range r("cs.allreduce.enqueue");
       comm->all_reduce(G(bucket_ranges[2 * k]), bucket_ranges[2 * k + 1], ncclFloat32, ncclAvg, src,
                        /*fork=*/!(debug_skip_ & 2));
+    }
     if (dp && broadcast_buffers && k == 0) {
       // DDP broadcast_buffers (rank 0's BN running stats before every training forward), issued
       // for the NEXT forward right behind the first bucket: this forward has produced the
@@ -699,12 +712,18 @@ void VggEngine::step(int64_t B, DeviceComm* comm, const std::vector<int64_t>& bu
     if (side_sgd && dp) sgd_on(comm->stream(), bucket_ranges[2 * k], bucket_ranges[2 * k + 1], k + 1 == nb);
   }
   bwd_sgd_ = false;
-  if (ovl) join_side(s);
-  if (dp && !(debug_skip_ & 1)) comm->join(s);
+  {
+    Range r("cs.comm.join");
+    if (ovl) join_side(s);
+    if (dp && !(debug_skip_ & 1)) comm->join(s);
+  }
   mark("allreduce_wait");
-  if (tiled) join_opt();
-  else if (!side_sgd) sgd(lr, momentum, wd, dampening, 0, params_.numel());
-  if (side_sgd) sgd_first_ = false;
+  {
+    Range r("cs.sgd");
+    if (tiled) join_opt();
+    else if (!side_sgd) sgd(lr, momentum, wd, dampening, 0, params_.numel());
+    if (side_sgd) sgd_first_ = false;
+  }
   mark("sgd");
 }
 

@@ -144,6 +144,54 @@ def _native_comm_fallback_worker(rank, world):
     return {"kind": type(c).__name__, "sum": t, "built": len(built)}
 
 
+def _two_phase_fallback_worker(rank, world, fail_at):
+    import torch
+    import torch.distributed as dist
+    from cs744_pytorch_distributed_tutorial_amd.parallel import comm as cm
+    log = []
+
+    def prepare():
+        if fail_at == "prepare" and rank == 1:
+            raise RuntimeError("cannot load the extension on this rank")
+        log.append("prepare")
+        return b"uid" if rank == 0 else None
+
+    def share(uid):
+        log.append("share")
+        obj = [uid]
+        dist.broadcast_object_list(obj, src=0)  # the real path's collective exchange
+        return obj[0]
+
+    def build(uid):
+        if fail_at == "build" and rank == 1:
+            raise RuntimeError("ncclCommInitRankConfig failed on this rank")
+        log.append("build:" + uid.decode())
+        return cm.TorchComm()
+
+    c = cm._agreed(build, None, "rccl", prepare=prepare, share=share)
+    t = torch.full((4,), float(rank + 1))
+    c.all_reduce(t, "sum")  # every rank reaches the same collectives: no hang, no mismatch
+    return {"kind": type(c).__name__, "sum": t, "log": log}
+
+
+@pytest.mark.parametrize("fail_at", ["prepare", "build", "none"])
+def test_native_comm_two_phase_agreement(fail_at):
+    """a rank failing BEFORE the unique-id broadcast must not leave its peers inside
+    broadcast_object_list — phase 1 agrees first; a failure in ncclCommInitRankConfig is agreed
+    after it. Both end with every rank on torch.distributed."""
+    from mp_util import run_world
+    out = run_world(_two_phase_fallback_worker, 2, fail_at)
+    for r in range(2):
+        assert out[r]["kind"] == "TorchComm"
+        assert list(out[r]["sum"]) == [3.0] * 4
+    if fail_at == "prepare":  # nobody entered the collective exchange
+        assert all("share" not in out[r]["log"] for r in range(2))
+    else:
+        assert all("share" in out[r]["log"] for r in range(2))
+    if fail_at == "none":
+        assert out[0]["log"][-1] == "build:uid" and out[1]["log"][-1] == "build:uid"
+
+
 def test_native_comm_failure_on_one_rank_falls_back_on_all():
     """a rank that cannot build the native RCCL communicator takes every rank to torch.distributed
     (agreed by one all-reduce) instead of leaving its peers inside the first native collective"""

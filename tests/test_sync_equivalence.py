@@ -63,11 +63,41 @@ def test_all_modes_agree(world):
             assert _max_diff(res[r][0], res[0][0]) < 1e-6, (mode, opts, r)
 
 
+def _bn_prefwd(rank, world, broadcast):
+    """Rank 1's BN buffers are pushed away from rank 0's; the buffers each rank's module sees
+    at the START of its next training forward are captured by a forward pre-hook."""
+    import torch.nn as nn
+    from cs744_pytorch_distributed_tutorial_amd.models import VGG11
+    from cs744_pytorch_distributed_tutorial_amd.parallel import DistributedDataParallel, make_comm
+    torch.manual_seed(5000)
+    model = VGG11()
+    net = DistributedDataParallel(model, comm=make_comm("torch"), broadcast_buffers=broadcast)
+    opt = torch.optim.SGD(net.parameters(), lr=0.1, momentum=0.9)
+    g = torch.Generator().manual_seed(100 + rank)
+    seen = []
+    model.register_forward_pre_hook(
+        lambda m, inp: seen.append(torch.cat([b.detach().double().reshape(-1) for b in m.buffers()])))
+    for step in range(2):
+        if step == 1 and rank == 1:
+            with torch.no_grad():
+                for b in model.buffers():
+                    b.add_(3)  # rank-local drift: per-rank BN statistics (and any local edit)
+        x = torch.randn(8, 3, 32, 32, generator=g)
+        y = torch.randint(0, 10, (8,), generator=g)
+        opt.zero_grad()
+        nn.CrossEntropyLoss()(net(x), y).backward()
+        opt.step()
+    return seen[1]  # buffers entering the second training forward
+
+
 def test_ddp_broadcasts_bn_buffers_from_rank0():
-    res = run_world(_train, 2, "ddp", 1, {})
-    # buffers synced before each training forward: after one step rank-local BN stats differ,
-    # but both ranks started the step from rank 0's buffers
-    assert res[0][1].shape == res[1][1].shape
+    """part3 DDP semantics (broadcast_buffers=True, `master/part3/part3.py:116`): every training
+    forward starts from rank 0's BN buffers, so rank 1's drifted buffers are overwritten before
+    its forward; the negative control (broadcast_buffers=False) keeps them apart."""
+    res = run_world(_bn_prefwd, 2, True)
+    assert torch.equal(torch.as_tensor(res[0]), torch.as_tensor(res[1]))
+    off = run_world(_bn_prefwd, 2, False)
+    assert _max_diff(torch.as_tensor(off[0]), torch.as_tensor(off[1])) >= 2.0
 
 
 def test_single_process_differs_from_dp_due_to_per_rank_bn():
