@@ -137,6 +137,17 @@ def conv_wgrad_xp(dz3: torch.Tensor, x3: torch.Tensor, B: int, H: int, W: int, c
     return dw.view(cout, 3, 3, cin)
 
 
+_GRID_BARS = {}
+
+
+def _grid_bar(device) -> torch.Tensor:
+    """Zeroed grid-barrier counters of the one-launch BN kernels (left zeroed by every launch)."""
+    key = str(device)
+    if key not in _GRID_BARS:
+        _GRID_BARS[key] = torch.zeros(4, dtype=torch.int32, device=device)
+    return _GRID_BARS[key]
+
+
 class BNState:
     """Per-channel tensors one BN layer needs between forward and backward."""
 
@@ -156,6 +167,15 @@ def bn_relu_pool_fwd(y: torch.Tensor, stats: torch.Tensor, rows: int, B: int, H:
     C = gamma.numel()
     M = B * H * W
     T = stats.shape[0]
+    if fused == "grid":  # one grid-barrier launch (the engine's default for the larger layers)
+        bnv = torch.empty(4, C, device=y.device, dtype=torch.float32)
+        Ho, Wo = (H // 2, W // 2) if pool else (H, W)
+        out = torch.empty(B, Ho, Wo, C, device=y.device, dtype=torch.float32)
+        native.C().bn_grid_fwd(stats, T, rows, M, gamma, beta, running_mean, running_var, nbt, momentum, eps, bnv,
+                               y, out, B, H, W, pool, _grid_bar(y.device))
+        st = BNState(C, y.device)
+        st.scale, st.shift, st.mean, st.invstd = bnv[0], bnv[1], bnv[2], bnv[3]
+        return out, st
     if fused:
         bnv = torch.empty(4, C, device=y.device, dtype=torch.float32)
         Ho, Wo = (H // 2, W // 2) if pool else (H, W)
@@ -191,6 +211,15 @@ def bn_relu_pool_bwd(y: torch.Tensor, G: torch.Tensor, st: BNState, gamma: torch
     """-> (dz [B*H*W, C], dgamma, dbeta, dbias) for z = maxpool?(relu(bn(y))).
     ``fused``: True = one launch (small layers), "two" = chunk partials + finalize-in-apply."""
     C = gamma.numel()
+    if fused == "grid":
+        bnv = torch.stack([st.scale, st.shift, st.mean, st.invstd]).contiguous()
+        part = torch.empty(native.C().bn_bwd_blocks(B, H, W, C, pool) * C * 3, device=y.device)
+        coef = torch.empty(C * 3, device=y.device)
+        dgamma, dbeta, dbias = (torch.empty(C, device=y.device) for _ in range(3))
+        dz = torch.empty(B * H * W, C, device=y.device)
+        native.C().bn_grid_bwd(y, G, B, H, W, C, pool, bnv, gamma, part, coef, dgamma, dbeta, dbias, dz,
+                               _grid_bar(y.device))
+        return dz, dgamma, dbeta, dbias
     if fused == "two":
         bnv = torch.stack([st.scale, st.shift, st.mean, st.invstd]).contiguous()
         part = torch.empty(native.C().bn_bwd_chunks(B, H, W, C, pool) * C * 3, device=y.device)

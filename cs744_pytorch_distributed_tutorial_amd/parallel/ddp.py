@@ -21,6 +21,13 @@ What it keeps from DDP:
 MI355X-native differences: bucket policy ``"layer"`` (xGMI-sized layer-aligned
 buckets, `parallel.buckets`), ``ReduceOp.AVG`` (``ncclAvg``) instead of a separate
 divide, and a pluggable communicator (``TorchComm`` or the native ``RcclComm``).
+
+``grad_comm_dtype=torch.bfloat16`` (the default for the decoder-LM configs, runtime/torch_trainer.py):
+each ready bucket's fp32 gradients are cast to bf16 (round to nearest even,
+``csrc/kernels/flat_ops.hip`` cast_grad) on the compute stream, the all-reduce(AVG) runs on the
+bf16 copy, and the average is widened back into the fp32 gradient view before the optimizer
+reads it — half the bytes on the wire (Llama-3-8B pure DP: 16 GB instead of 32 GB of gradients
+per step).
 """
 from __future__ import annotations
 
@@ -34,10 +41,21 @@ from .buckets import Bucket, build_buckets
 from .comm import Comm, make_comm
 
 
+def _cast(src: torch.Tensor, dst: torch.Tensor) -> None:
+    """fp32 <-> bf16 copy of one gradient bucket: the gfx950 cast kernel on the GPU (fails
+    loudly if the extension is missing there), torch's copy_ (same rounding) on the CPU."""
+    if src.is_cuda:
+        from ..ops import native
+        native.C().cast_grad(src, dst)
+    else:
+        dst.copy_(src)
+
+
 class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, comm: Optional[Comm] = None, bucket_cap_mb: float = 25.0,
                  first_bucket_cap_mb: float = 1.0, bucket_policy: str = "size",
-                 broadcast_buffers: bool = True, sync_on_init: bool = True):
+                 broadcast_buffers: bool = True, sync_on_init: bool = True,
+                 grad_comm_dtype: Optional[torch.dtype] = None):
         super().__init__()
         self.module = module
         self.comm = comm if comm is not None else make_comm("torch")
@@ -53,6 +71,13 @@ class DistributedDataParallel(nn.Module):
         p0 = self._params[0]
         total = sum(b.numel for b in self.buckets)
         self.flat_grad = torch.zeros(total, dtype=p0.dtype, device=p0.device)
+        # bf16 transport: the wire copy of every bucket (None: all-reduce the gradients in place)
+        self.grad_comm_dtype = grad_comm_dtype if grad_comm_dtype not in (None, p0.dtype) else None
+        if self.grad_comm_dtype is not None and (p0.dtype != torch.float32 or self.grad_comm_dtype != torch.bfloat16):
+            raise ValueError("grad_comm_dtype: only bfloat16 transport of float32 gradients")
+        self.flat_comm = torch.empty(total, dtype=self.grad_comm_dtype, device=p0.device) \
+            if self.grad_comm_dtype is not None else None
+        self._casts: List = []
         self._views: List[Optional[torch.Tensor]] = [None] * len(self._params)
         self._bucket_of = [0] * len(self._params)
         for b in self.buckets:
@@ -161,7 +186,13 @@ class DistributedDataParallel(nn.Module):
             if not self._ready[b.index]:
                 break  # keep identical launch order across ranks
             view = self.flat_grad[b.offset:b.offset + b.numel]
-            self._handles.append(self.comm.all_reduce_avg(view, async_op=True))
+            if self.flat_comm is not None:
+                wire = self.flat_comm[b.offset:b.offset + b.numel]
+                _cast(view, wire)  # on the compute stream: the comm stream's fork orders it
+                self._handles.append(self.comm.all_reduce_avg(wire, async_op=True))
+                self._casts.append((wire, view))
+            else:
+                self._handles.append(self.comm.all_reduce_avg(view, async_op=True))
             self._launched[b.index] = True
 
     def _finalize(self) -> None:
@@ -171,6 +202,9 @@ class DistributedDataParallel(nn.Module):
             raise RuntimeError(f"DDP: buckets {missing} never became ready (unused parameters?)")
         for h in self._handles:
             h.wait()
+        for wire, view in self._casts:  # after the join: the averaged bf16 bucket -> fp32 grads
+            _cast(wire, view)
+        self._casts = []
         self._reset_counts()
 
     # ------------------------------------------------------------------ forward

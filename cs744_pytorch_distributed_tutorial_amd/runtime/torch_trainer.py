@@ -97,8 +97,11 @@ class TorchTrainer:
             self.module = self.module.to(memory_format=torch.channels_last)
         self.dtype = dtype
         if world > 1 and sync == "ddp":
+            # decoder LMs all-reduce bf16 gradients by default (CS744_GRAD_COMM_DTYPE=fp32 | bf16)
+            gdt = os.environ.get("CS744_GRAD_COMM_DTYPE", "bf16" if self.is_lm else "fp32")
             self.net = DistributedDataParallel(self.module, comm=make_comm(comm), bucket_cap_mb=bucket_mb,
-                                               bucket_policy=bucket_policy)
+                                               bucket_policy=bucket_policy,
+                                               grad_comm_dtype=torch.bfloat16 if gdt == "bf16" else None)
             self.sync = make_sync("none", [])
         else:
             self.net = self.module

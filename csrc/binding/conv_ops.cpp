@@ -221,6 +221,55 @@ void bn_fused_fwd(torch::Tensor part, int64_t T, int64_t R, int64_t M, torch::Te
                             cur_stream()));
 }
 
+// one-launch grid-barrier BN (bn_grid.hip); bar: zeroed int32 counters (>= 3), left zeroed
+void bn_grid_fwd(torch::Tensor part, int64_t T, int64_t R, int64_t M, torch::Tensor gamma, torch::Tensor beta,
+                 c10::optional<torch::Tensor> running_mean, c10::optional<torch::Tensor> running_var,
+                 c10::optional<torch::Tensor> nbt, double momentum, double eps, torch::Tensor bnv, torch::Tensor y,
+                 torch::Tensor out, int64_t B, int64_t H, int64_t W, bool pool, torch::Tensor bar) {
+  const int64_t C = gamma.numel();
+  TORCH_CHECK(C % 4 == 0 && (!pool || (H % 2 == 0 && W % 2 == 0)) && M == B * H * W && T == (M + R - 1) / R,
+              "bn_grid_fwd: shape");
+  check_t(part, T * C * 2, "part"); check_t(beta, C, "beta"); check_t(bnv, 4 * C, "bnv");
+  check_t(running_mean, C, "running_mean"); check_t(running_var, C, "running_var");
+  check_t(y, M * C, "y"); check_t(out, B * (pool ? H / 2 : H) * (pool ? W / 2 : W) * C, "out");
+  TORCH_CHECK(bar.is_cuda() && bar.scalar_type() == at::kInt && bar.numel() >= 3, "bn_grid: bar int32 [>= 3]");
+  if (nbt.has_value()) TORCH_CHECK(nbt->scalar_type() == at::kLong && nbt->is_cuda(), "nbt: int64 GPU scalar");
+  CsBnGridFwd g{};
+  g.part = part.data_ptr<float>(); g.gamma = gamma.data_ptr<float>(); g.beta = beta.data_ptr<float>();
+  g.y = y.data_ptr<float>(); g.running_mean = mptr(running_mean); g.running_var = mptr(running_var);
+  g.bnv = bnv.data_ptr<float>(); g.out = out.data_ptr<float>();
+  g.nbt = nbt.has_value() ? nbt->data_ptr<int64_t>() : nullptr;
+  g.momentum = (float)momentum; g.eps = (float)eps;
+  g.T = T; g.R = R; g.M = M; g.B = B; g.H = H; g.W = W; g.C = C; g.pool = pool ? 1 : 0;
+  g.bar = reinterpret_cast<unsigned*>(bar.data_ptr<int>());
+  DevGuard dg(y.device());
+  CS_LAUNCH(cs_bn_grid_fwd(g, cur_stream()));
+}
+
+void bn_grid_bwd(torch::Tensor y, torch::Tensor G, int64_t B, int64_t H, int64_t W, int64_t C, bool pool,
+                 torch::Tensor bnv, torch::Tensor gamma, torch::Tensor part, torch::Tensor coef,
+                 c10::optional<torch::Tensor> dgamma, c10::optional<torch::Tensor> dbeta,
+                 c10::optional<torch::Tensor> dbias, torch::Tensor dz, torch::Tensor bar) {
+  TORCH_CHECK(C % 4 == 0 && C <= 1024 && (!pool || (H % 2 == 0 && W % 2 == 0)), "bn_grid_bwd: shape");
+  check_t(y, B * H * W * C, "y");
+  check_t(G, B * (pool ? H / 2 : H) * (pool ? W / 2 : W) * C, "G");
+  check_t(bnv, 4 * C, "bnv"); check_t(gamma, C, "gamma"); check_t(coef, 3 * C, "coef");
+  check_t(part, (int64_t)cs_bn_bwd_blocks(B, H, W, C, pool) * C * 3, "part");
+  check_t(dgamma, C, "dgamma"); check_t(dbeta, C, "dbeta"); check_t(dbias, C, "dbias");
+  check_t(dz, B * H * W * C, "dz");
+  TORCH_CHECK(bar.is_cuda() && bar.scalar_type() == at::kInt && bar.numel() >= 3, "bn_grid: bar int32 [>= 3]");
+  CsBnGridBwd g{};
+  const float* bv = bnv.data_ptr<float>();
+  g.y = y.data_ptr<float>(); g.G = G.data_ptr<float>();
+  g.scale = bv; g.shift = bv + C; g.mean = bv + 2 * C; g.invstd = bv + 3 * C; g.gamma = gamma.data_ptr<float>();
+  g.part = part.data_ptr<float>(); g.coef = coef.data_ptr<float>();
+  g.dgamma = mptr(dgamma); g.dbeta = mptr(dbeta); g.dbias = mptr(dbias); g.dz = dz.data_ptr<float>();
+  g.B = B; g.H = H; g.W = W; g.C = C; g.pool = pool ? 1 : 0; g.gslabs = 1;
+  g.bar = reinterpret_cast<unsigned*>(bar.data_ptr<int>());
+  DevGuard dg(y.device());
+  CS_LAUNCH(cs_bn_grid_bwd(g, cur_stream()));
+}
+
 void bn_fused_bwd(torch::Tensor y, torch::Tensor G, int64_t B, int64_t H, int64_t W, int64_t C, bool pool,
                   torch::Tensor bnv, torch::Tensor gamma, torch::Tensor coef, c10::optional<torch::Tensor> dgamma,
                   c10::optional<torch::Tensor> dbeta, c10::optional<torch::Tensor> dbias, torch::Tensor dz) {
@@ -260,6 +309,8 @@ void register_conv_ops(pybind11::module& m) {
     return cs_bn_bwd_chunks(B, H, W, C, pool ? 1 : 0);
   });
   m.def("bn_fused_fwd", &bn_fused_fwd, "single-launch BN finalize + normalize/ReLU(/pool) (small layers)");
+  m.def("bn_grid_fwd", &bn_grid_fwd, "one-launch grid-barrier BN finalize + normalize/ReLU(/pool)");
+  m.def("bn_grid_bwd", &bn_grid_bwd, "one-launch grid-barrier BN backward: partials | finalize | apply");
   m.def("bn_fused_bwd", &bn_fused_bwd, "single-launch BN backward: reduce + finalize + apply (small layers)");
   m.def("conv_gemm", &conv_gemm, "implicit-GEMM 3x3 conv (mode 0 fwd / 1 dgrad / 2 wgrad), fp32 MFMA",
         py::arg("mode"), py::arg("x"), py::arg("w"), py::arg("dz"), py::arg("bias"), py::arg("out"), py::arg("ws"),

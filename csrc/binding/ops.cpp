@@ -109,6 +109,17 @@ void rows_mean(torch::Tensor src, int64_t rows, torch::Tensor dst, bool bcast) {
 }
 
 // part2a_extra root combine: g += t (then g /= div when div > 0)
+void cast_grad(torch::Tensor src, torch::Tensor dst) {
+  TORCH_CHECK(src.is_cuda() && dst.is_cuda() && src.is_contiguous() && dst.is_contiguous() &&
+                  src.numel() == dst.numel(),
+              "cast_grad: contiguous GPU tensors of equal size");
+  const bool to_bf16 = src.scalar_type() == at::kFloat && dst.scalar_type() == at::kBFloat16;
+  TORCH_CHECK(to_bf16 || (src.scalar_type() == at::kBFloat16 && dst.scalar_type() == at::kFloat),
+              "cast_grad: float32 -> bfloat16 or bfloat16 -> float32");
+  DevGuard g(src.device());
+  CS_LAUNCH(cs_cast_grad(src.data_ptr(), dst.data_ptr(), src.numel(), to_bf16 ? 1 : 0, cur_stream()));
+}
+
 void accumulate(torch::Tensor g, torch::Tensor t, double div) {
   for (auto* x : {&g, &t}) { CS_CHECK_CUDA(*x); CS_CHECK_F32(*x); CS_CHECK_CONTIG(*x); }
   TORCH_CHECK(g.numel() == t.numel(), "accumulate: size mismatch");
@@ -180,6 +191,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("rows_mean", &rows_mean, "mean over the rows of a [rows, n] buffer (part2a root)", pybind11::arg("src"),
         pybind11::arg("rows"), pybind11::arg("dst"), pybind11::arg("bcast") = false);
   m.def("accumulate", &accumulate, "g += t, optionally then g /= div (part2a_extra root)");
+  m.def("cast_grad", &cast_grad, "gradient bucket fp32 <-> bf16 (bf16 gradient transport of the DDP)");
   m.def("linear_xent", &linear_xent, "fused Linear + softmax cross-entropy fwd(+bwd)");
   m.def("softmax_xent", &softmax_xent, "softmax cross-entropy fwd+bwd");
   register_conv_ops(m);

@@ -467,9 +467,14 @@ __global__ __launch_bounds__(256) void bn_fused_bwd_kernel(const float* __restri
                                                            const float* __restrict__ gamma, float* __restrict__ coef,
                                                            float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                            float* __restrict__ dbias, float* __restrict__ dz,
-                                                           int gslabs, int64_t gstride) {
+                                                           int gslabs, int64_t gstride,
+                                                           unsigned long long* __restrict__ signal) {
   __shared__ float lds[4 * 4 * 3 * 4];
   __shared__ float coef_sh[3 * kFusedCh];  // this block's 16 channels' dZ coefficients
+  // a deferred stream-link signal (device_comm.h StreamLink::defer): this launch started, so the
+  // kernels before it on the stream completed
+  if (signal != nullptr && blockIdx.x == 0 && threadIdx.x == 0)
+    __hip_atomic_fetch_add(signal, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int cq = threadIdx.x & 3, rl = threadIdx.x >> 2;
   const int cqg = blockIdx.x * 4 + cq;
   const float* scale = bnv;
@@ -720,13 +725,13 @@ hipError_t cs_bn_fused_fwd(const float* part, int T, int R, int M, int C, const 
 
 hipError_t cs_bn_fused_bwd(const float* y, const float* G, int B, int H, int W, int C, int pool, const float* bnv,
                            const float* gamma, float* coef, float* dgamma, float* dbeta, float* dbias, float* dz,
-                           hipStream_t stream, int gslabs, int64_t gstride) {
+                           hipStream_t stream, int gslabs, int64_t gstride, unsigned long long* signal) {
   if (C % kFusedCh != 0 || (pool && ((H | W) & 1)) || gslabs < 1) return hipErrorInvalidValue;
   if (pool)
     hipLaunchKernelGGL((bn_fused_bwd_kernel<true>), dim3(C / kFusedCh), dim3(256), 0, stream, y, G, B, H, W, C, bnv,
-                       gamma, coef, dgamma, dbeta, dbias, dz, gslabs, gstride);
+                       gamma, coef, dgamma, dbeta, dbias, dz, gslabs, gstride, signal);
   else
     hipLaunchKernelGGL((bn_fused_bwd_kernel<false>), dim3(C / kFusedCh), dim3(256), 0, stream, y, G, B, H, W, C, bnv,
-                       gamma, coef, dgamma, dbeta, dbias, dz, gslabs, gstride);
+                       gamma, coef, dgamma, dbeta, dbias, dz, gslabs, gstride, signal);
   return hipGetLastError();
 }

@@ -461,8 +461,17 @@ __global__ __launch_bounds__(256) void col2im_kernel(const T* __restrict__ dcol,
 }
 
 // ------------------------------------------------------------------------------ host side
-// the gather kernels index their work items in 32 bits (64-bit integer division is emulated)
+// the gather kernels index their work items in 32 bits (64-bit integer division is emulated):
+// a launch covers at most kMaxItems items, larger tensors go in batch chunks (every image's
+// gather is independent) — e.g. the 224-px stem im2col passes 2^31 items near B = 850
 constexpr int64_t kMaxItems = (int64_t)1 << 31;
+
+// images per launch so that one launch stays below kMaxItems items (>= 1: one image always fits
+// for every shape these kernels serve; the callers check per_image < kMaxItems)
+int batch_chunk(int B, int64_t per_image) {
+  const int64_t c = (kMaxItems - 1) / per_image;
+  return (int)(c < 1 ? 1 : (c > B ? B : c));
+}
 
 int grid_for(int64_t n) {
   const int64_t b = (n + 255) / 256;
@@ -576,45 +585,71 @@ hipError_t cs_bn_nhwc_bwd(int dt, const void* dy, const void* x, const void* res
 
 hipError_t cs_maxpool3s2_nhwc_fwd(int dt, const void* x, void* y, unsigned char* pos, int B, int H, int W, int C,
                                   int Ho, int Wo, hipStream_t stream) {
-  const int64_t n = (int64_t)B * Ho * Wo * C;
-  if (n == 0) return hipSuccess;
-  if (n >= kMaxItems) return hipErrorInvalidValue;
-  CS_NHWC_DISPATCH(dt, C, hipLaunchKernelGGL((maxpool_fwd_kernel<T, V>), dim3(grid_for(n / V)), dim3(256), 0, stream,
-                                       (const T*)x, (T*)y, pos, B, H, W, C, Ho, Wo));
+  const int64_t per = (int64_t)Ho * Wo * C;
+  if (per * B == 0) return hipSuccess;
+  if (per >= kMaxItems) return hipErrorInvalidValue;
+  const int cb = batch_chunk(B, per);
+  for (int b0 = 0; b0 < B; b0 += cb) {
+    const int nb = B - b0 < cb ? B - b0 : cb;
+    const int64_t xo = (int64_t)b0 * H * W * C, yo = (int64_t)b0 * per;
+    CS_NHWC_DISPATCH(dt, C, hipLaunchKernelGGL((maxpool_fwd_kernel<T, V>), dim3(grid_for(nb * per / V)), dim3(256),
+                                               0, stream, (const T*)x + xo, (T*)y + yo, pos + yo, nb, H, W, C, Ho,
+                                               Wo));
+  }
   return hipGetLastError();
 }
 
 hipError_t cs_maxpool3s2_nhwc_bwd(int dt, const void* dy, const unsigned char* pos, void* dx, int B, int H, int W,
                                   int C, int Ho, int Wo, hipStream_t stream) {
-  const int64_t n = (int64_t)B * H * W * C;
-  if (n == 0) return hipSuccess;
-  if (n >= kMaxItems) return hipErrorInvalidValue;
-  CS_NHWC_DISPATCH(dt, C, hipLaunchKernelGGL((maxpool_bwd_kernel<T, V>), dim3(grid_for(n / V)), dim3(256), 0, stream,
-                                       (const T*)dy, pos, (T*)dx, B, H, W, C, Ho, Wo));
+  const int64_t per = (int64_t)H * W * C;
+  if (per * B == 0) return hipSuccess;
+  if (per >= kMaxItems) return hipErrorInvalidValue;
+  const int cb = batch_chunk(B, per);
+  for (int b0 = 0; b0 < B; b0 += cb) {
+    const int nb = B - b0 < cb ? B - b0 : cb;
+    const int64_t yo = (int64_t)b0 * Ho * Wo * C, xo = (int64_t)b0 * per;
+    CS_NHWC_DISPATCH(dt, C, hipLaunchKernelGGL((maxpool_bwd_kernel<T, V>), dim3(grid_for(nb * per / V)), dim3(256),
+                                               0, stream, (const T*)dy + yo, pos + yo, (T*)dx + xo, nb, H, W, C, Ho,
+                                               Wo));
+  }
   return hipGetLastError();
 }
 
 hipError_t cs_im2col_nhwc(int dt, const void* x, void* col, int B, int H, int W, int C, int R, int S, int stride,
                           int pad, int Ho, int Wo, int Kp, hipStream_t stream) {
-  const int64_t n = (int64_t)B * Ho * Wo * Kp;
-  if (n == 0) return hipSuccess;
-  if (n >= kMaxItems) return hipErrorInvalidValue;
+  const int64_t per = (int64_t)Ho * Wo * Kp;
+  if (per * B == 0) return hipSuccess;
+  if (per >= kMaxItems) return hipErrorInvalidValue;
   // V must divide C (a vector stays inside one tap) and Kp
   const int vc = vec_for(C, dt == CS_BF16 ? 2 : 4);
   if (vc > 1 && Kp % vc != 0) return hipErrorInvalidValue;
-  CS_NHWC_DISPATCH(dt, C, hipLaunchKernelGGL((im2col_kernel<T, V>), dim3(grid_for(n / V)), dim3(256), 0, stream,
-                                       (const T*)x, (T*)col, B, H, W, C, R, S, stride, pad, Ho, Wo, Kp));
+  const int cb = batch_chunk(B, per);
+  for (int b0 = 0; b0 < B; b0 += cb) {
+    const int nb = B - b0 < cb ? B - b0 : cb;
+    const int64_t xo = (int64_t)b0 * H * W * C, co = (int64_t)b0 * per;
+    CS_NHWC_DISPATCH(dt, C, hipLaunchKernelGGL((im2col_kernel<T, V>), dim3(grid_for(nb * per / V)), dim3(256), 0,
+                                               stream, (const T*)x + xo, (T*)col + co, nb, H, W, C, R, S, stride, pad,
+                                               Ho, Wo, Kp));
+  }
   return hipGetLastError();
 }
 
 hipError_t cs_col2im_nhwc(int dt, const void* dcol, void* dx, int B, int H, int W, int C, int R, int S, int stride,
                           int pad, int Ho, int Wo, int Kp, hipStream_t stream) {
-  const int64_t n = (int64_t)B * H * W * C;
-  if (n == 0) return hipSuccess;
-  if (n >= kMaxItems) return hipErrorInvalidValue;
+  const int64_t per = (int64_t)H * W * C;
+  if (per * B == 0) return hipSuccess;
+  if (per >= kMaxItems || (int64_t)Ho * Wo * Kp >= kMaxItems) return hipErrorInvalidValue;
   const int vc = vec_for(C, dt == CS_BF16 ? 2 : 4);
   if (vc > 1 && Kp % vc != 0) return hipErrorInvalidValue;
-  CS_NHWC_DISPATCH(dt, C, hipLaunchKernelGGL((col2im_kernel<T, V>), dim3(grid_for(n / V)), dim3(256), 0, stream,
-                                       (const T*)dcol, (T*)dx, B, H, W, C, R, S, stride, pad, Ho, Wo, Kp));
+  // chunk so both the dx items and the dcol rows a launch reads stay within 32-bit indices
+  const int64_t per_col = (int64_t)Ho * Wo * Kp;
+  const int cb = batch_chunk(B, per > per_col ? per : per_col);
+  for (int b0 = 0; b0 < B; b0 += cb) {
+    const int nb = B - b0 < cb ? B - b0 : cb;
+    const int64_t xo = (int64_t)b0 * per, co = (int64_t)b0 * per_col;
+    CS_NHWC_DISPATCH(dt, C, hipLaunchKernelGGL((col2im_kernel<T, V>), dim3(grid_for(nb * per / V)), dim3(256), 0,
+                                               stream, (const T*)dcol + co, (T*)dx + xo, nb, H, W, C, R, S, stride,
+                                               pad, Ho, Wo, Kp));
+  }
   return hipGetLastError();
 }

@@ -8,7 +8,11 @@
 //  * accumulate — part2a_extra's star on the root (`master/part2a/part2a_extra.py:41-58`):
 //    g += t for each received peer buffer, and on the last one g = (g + t) / div (the same two
 //    roundings as the reference's add then divide).
-// Both are HBM-streaming: float4 grid-stride loops, a few waves per CU, scalar tail.
+//  * cast_grad — bf16 gradient transport of the framework DDP (parallel/ddp.py grad_comm_dtype):
+//    a bucket's fp32 gradients -> bf16 (round to nearest even, the wire format of the bf16
+//    all-reduce: half the xGMI bytes, SURVEY.md §2.3 / §7.1's 16 GB per Llama-3-8B step), and the
+//    averaged bf16 bucket back into the fp32 gradient view the optimizer reads.
+// All are HBM-streaming: float4 grid-stride loops, a few waves per CU, scalar tail.
 #include "common.h"
 #include "launchers.h"
 
@@ -59,6 +63,37 @@ __global__ __launch_bounds__(256) void accumulate_kernel(float* __restrict__ g, 
   }
 }
 
+__device__ __forceinline__ unsigned short bf16_rne(float x) {
+  const __bf16 h = (__bf16)x;  // v_cvt_pk_bf16_f32: round to nearest even, NaN stays NaN
+  return __builtin_bit_cast(unsigned short, h);
+}
+
+__global__ __launch_bounds__(256) void f32_to_bf16_kernel(const float* __restrict__ x, unsigned short* __restrict__ y,
+                                                          int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t n4 = n >> 2;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    const float4 v = reinterpret_cast<const float4*>(x)[i];
+    ushort4 o;
+    o.x = bf16_rne(v.x); o.y = bf16_rne(v.y); o.z = bf16_rne(v.z); o.w = bf16_rne(v.w);
+    reinterpret_cast<ushort4*>(y)[i] = o;
+  }
+  for (int64_t i = (n4 << 2) + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) y[i] = bf16_rne(x[i]);
+}
+
+__global__ __launch_bounds__(256) void bf16_to_f32_kernel(const unsigned short* __restrict__ x, float* __restrict__ y,
+                                                          int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t n4 = n >> 2;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    const ushort4 v = reinterpret_cast<const ushort4*>(x)[i];
+    reinterpret_cast<float4*>(y)[i] = make_float4(__uint_as_float((unsigned)v.x << 16), __uint_as_float((unsigned)v.y << 16),
+                                                  __uint_as_float((unsigned)v.z << 16), __uint_as_float((unsigned)v.w << 16));
+  }
+  for (int64_t i = (n4 << 2) + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    y[i] = __uint_as_float((unsigned)x[i] << 16);
+}
+
 int grid_for(int64_t n) {
   const int64_t b = ((n + 3) / 4 + 255) / 256;
   return (int)(b < 1 ? 1 : (b > 2048 ? 2048 : b));
@@ -75,5 +110,16 @@ hipError_t cs_rows_mean(float* src, int rows, int64_t n, float* dst, int bcast, 
 hipError_t cs_accumulate(float* g, const float* t, int64_t n, float div, hipStream_t stream) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(accumulate_kernel, dim3(grid_for(n)), dim3(256), 0, stream, g, t, n, div);
+  return hipGetLastError();
+}
+
+hipError_t cs_cast_grad(const void* src, void* dst, int64_t n, int to_bf16, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  if (to_bf16)
+    hipLaunchKernelGGL(f32_to_bf16_kernel, dim3(grid_for(n)), dim3(256), 0, stream, static_cast<const float*>(src),
+                       static_cast<unsigned short*>(dst), n);
+  else
+    hipLaunchKernelGGL(bf16_to_f32_kernel, dim3(grid_for(n)), dim3(256), 0, stream,
+                       static_cast<const unsigned short*>(src), static_cast<float*>(dst), n);
   return hipGetLastError();
 }

@@ -29,6 +29,8 @@ hipError_t cs_sgd_flat(float* p, const float* g, float* m, int64_t n, float lr, 
 // g = g + t, then / div when div > 0
 hipError_t cs_rows_mean(float* src, int rows, int64_t n, float* dst, int bcast, hipStream_t stream);
 hipError_t cs_accumulate(float* g, const float* t, int64_t n, float div, hipStream_t stream);
+// bf16 gradient transport: to_bf16 = 1: fp32 src -> bf16 dst (round to nearest even); 0: bf16 -> fp32
+hipError_t cs_cast_grad(const void* src, void* dst, int64_t n, int to_bf16, hipStream_t stream);
 hipError_t cs_sgd_multi(const CsTensorEntry* tab_dev, int ntens, const int64_t* chunk_start_dev, int nchunks,
                         float lr, float mom, float wd, float damp, float scale, int first, hipStream_t stream);
 
@@ -150,6 +152,34 @@ hipError_t cs_bn_bwd_tail(const float* y, const float* G, int B, int H, int W, i
                           const float* shift, const float* mean, const float* invstd, const float* gamma,
                           const float* part, int P, float* coef, float* dgamma, float* dbeta, float* dbias, float* dz,
                           hipStream_t stream, int gslabs = 1, int64_t gstride = 0);
+// One-launch BN (bn_grid.hip): P <= 256 blocks (all resident) whose phases meet at in-kernel grid
+// barriers — backward: partials | per-channel finalize | dZ apply (replaces cs_bn_bwd's three
+// launches, same partials bit for bit); forward: finalize from the conv epilogue's tile partials |
+// normalize/ReLU/pool (replaces cs_bn_finalize + cs_bn_apply). bar: zeroed device counters the
+// kernels leave zeroed (3 for backward, 2 for forward; one set per stream); err: device word set
+// on a barrier timeout; signal: optional stream-link counter bumped when the launch starts.
+struct CsBnGridBwd {
+  const float *y, *G, *scale, *shift, *mean, *invstd, *gamma;
+  float *part, *coef, *dgamma, *dbeta, *dbias, *dz;
+  int64_t gstride;
+  int B, H, W, C, pool, gslabs;
+  unsigned* bar;
+  int* err;
+  unsigned long long* signal;
+};
+struct CsBnGridFwd {
+  const float *part, *gamma, *beta, *y;
+  float *running_mean, *running_var, *bnv, *out;  // bnv [4][C]: scale, shift, mean, invstd
+  int64_t* nbt;
+  float momentum, eps;
+  int T, R, M, B, H, W, C, pool;
+  unsigned* bar;
+  int* err;
+  unsigned long long* signal;
+};
+hipError_t cs_bn_grid_bwd(const CsBnGridBwd& a, hipStream_t stream);
+hipError_t cs_bn_grid_fwd(const CsBnGridFwd& a, hipStream_t stream);
+int cs_bn_grid_fwd_blocks(int B, int H, int W, int C, int pool);
 // G may be split-K slabs of the data-gradient GEMM: G = sum_{z < gslabs} G[z * gstride + i]
 // (summed in z order, bit-equal to the split-K combine launch it replaces)
 hipError_t cs_bn_bwd(const float* y, const float* G, int B, int H, int W, int C, int pool, const float* scale,
@@ -165,7 +195,8 @@ hipError_t cs_bn_fused_fwd(const float* part, int T, int R, int M, int C, const 
                            float* bnv, const float* y, float* out, int B, int H, int W, int pool, hipStream_t stream);
 hipError_t cs_bn_fused_bwd(const float* y, const float* G, int B, int H, int W, int C, int pool, const float* bnv,
                            const float* gamma, float* coef, float* dgamma, float* dbeta, float* dbias, float* dz,
-                           hipStream_t stream, int gslabs = 1, int64_t gstride = 0);
+                           hipStream_t stream, int gslabs = 1, int64_t gstride = 0,
+                           unsigned long long* signal = nullptr);
 // two-launch backward for larger layers (C % 16 == 0): channel-sliced chunk partials, then
 // finalize folded into the apply; part: [cs_bn_bwd_chunks][C][3] scratch
 int cs_bn_bwd_chunks(int B, int H, int W, int C, int pool);

@@ -82,6 +82,11 @@ class StreamLink {
   StreamLink(const StreamLink&) = delete;
   StreamLink& operator=(const StreamLink&) = delete;
   void signal(hipStream_t producer);
+  // signal folded into the NEXT kernel launched on the producer stream: returns the counter that
+  // kernel must bump (once, at its start: it starts only after everything before it on that
+  // stream completed and released — the same edge as a signal launch, without the launch).
+  // nullptr when the link runs on events (CS_LINK_EVENTS): then call signal() instead.
+  unsigned long long* defer();
   void wait(hipStream_t consumer);
   std::string error() const;
 

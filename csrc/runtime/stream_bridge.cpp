@@ -67,6 +67,12 @@ void StreamLink::signal(hipStream_t producer) {
   ++pending_;
 }
 
+unsigned long long* StreamLink::defer() {
+  if (ev_) return nullptr;
+  ++pending_;
+  return dev_;
+}
+
 void StreamLink::wait(hipStream_t consumer) {
   if (pending_ == 0) return;  // nothing signalled since the last wait
   if (ev_) {

@@ -198,8 +198,16 @@ VggEngine::VggEngine(int64_t Bmax, std::vector<int64_t> desc, std::vector<int64_
   if (const char* e = getenv("CS_BN_FUSED_ROWS")) bn_fused_rows_ = atoll(e);
   if (const char* e = getenv("CS_CONV_MATH")) math_ = atoi(e);
   if (const char* e = getenv("CS_BN_PATH")) bn_path_ = atoi(e);
+  if (const char* e = getenv("CS_DEFER_SIGNALS")) defer_signals_ = atoi(e) != 0;
   if (const char* e = getenv("CS_KEEP_SLABS")) keep_slabs_ = atoi(e) != 0;
   if (const char* e = getenv("CS_FUSE_BN_RED")) fuse_red_ = atoi(e) != 0;
+  grid_bar_ = torch::zeros({8}, fo.dtype(at::kInt));
+  {
+    void* h = nullptr;
+    ok(hipHostMalloc(&h, sizeof(int), hipHostMallocMapped), "hipHostMalloc(grid error word)");
+    grid_err_ = static_cast<int*>(h);
+    *grid_err_ = 0;
+  }
   bn_part_ = torch::zeros({partmax}, fo);
   bn_coef_ = torch::zeros({cmax * 3}, fo);
   bn_eval_ = torch::zeros({2, cmax}, fo);
@@ -213,7 +221,16 @@ void VggEngine::join_side(hipStream_t s) { wg_link_->wait(s); }
 
 std::string VggEngine::link_error() const {
   std::string e = dz_link_->error();
-  return e.empty() ? wg_link_->error() : e;
+  if (e.empty()) e = wg_link_->error();
+  if (e.empty() && grid_err_ != nullptr && __atomic_load_n(grid_err_, __ATOMIC_ACQUIRE) != 0)
+    e = "BN grid barrier timed out (a block of the one-launch BN kernel never arrived)";
+  return e;
+}
+
+void VggEngine::flush_signal(hipStream_t s) {
+  if (pending_sig_ == nullptr) return;
+  ok(cs_link_signal(pending_sig_, s), "link signal");
+  pending_sig_ = nullptr;
 }
 
 void VggEngine::set_overlap_wgrad(bool on) {
@@ -374,6 +391,31 @@ void VggEngine::forward_train(int64_t B) {
          "bn_fused_fwd");
       continue;
     }
+    if (bn_path_ == 2) {  // finalize + normalize/ReLU/pool in one grid-barrier launch
+      CsBnGridFwd g{};
+      g.part = b.stats.data_ptr<float>();
+      g.gamma = P(b.g_off);
+      g.beta = P(b.be_off);
+      g.y = b.y.data_ptr<float>();
+      g.running_mean = bufs + b.rm_off;
+      g.running_var = bufs + b.rv_off;
+      g.bnv = bn;
+      g.out = out;
+      g.nbt = nbt_.data_ptr<int64_t>() + l;
+      g.momentum = kBnMomentum;
+      g.eps = kBnEps;
+      g.T = (int)cdiv(M, rows);
+      g.R = rows;
+      g.M = (int)M;
+      g.B = (int)B;
+      g.H = g.W = b.H;
+      g.C = b.cout;
+      g.pool = b.pool;
+      g.bar = reinterpret_cast<unsigned*>(grid_bar_.data_ptr<int>()) + 4;
+      g.err = grid_err_;
+      ok(cs_bn_grid_fwd(g, s), "bn_grid_fwd");
+      continue;
+    }
     ok(cs_bn_finalize(b.stats.data_ptr<float>(), (int)cdiv(M, rows), rows, (int)M, b.cout, P(b.g_off), P(b.be_off),
                       bufs + b.rm_off, bufs + b.rv_off, nbt_.data_ptr<int64_t>() + l, kBnMomentum, kBnEps, bn,
                       bn + b.cout, bn + 2 * b.cout, bn + 3 * b.cout, s),
@@ -404,21 +446,52 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
     // this block's output gradient: gbuf_, or the split-K slabs the dgrad above left in ws_
     const int gs = g_slabs_;
     const float* Gin = gs > 1 ? ws_.data_ptr<float>() : gbuf_[(L - 1 - l) % 2].data_ptr<float>();
-    TORCH_CHECK(gs == 1 || bn_path_ == 0, "VggEngine: kept split-K slabs need the default BN path");
-    if (red_pending_ == l) {  // the partial sums already ran inside the weight-gradient launch above
+    TORCH_CHECK(gs == 1 || bn_path_ != 1, "VggEngine: kept split-K slabs need the grid or three-launch BN path");
+    if (red_pending_ != l && !bn_fused(l, B) && bn_path_ == 2) {  // reduce + finalize + apply: one launch
+      CsBnGridBwd g{};
+      g.y = b.y.data_ptr<float>();
+      g.G = Gin;
+      g.scale = bn;
+      g.shift = bn + b.cout;
+      g.mean = bn + 2 * b.cout;
+      g.invstd = bn + 3 * b.cout;
+      g.gamma = P(b.g_off);
+      g.part = bn_part_.data_ptr<float>();
+      g.coef = bn_coef_.data_ptr<float>();
+      g.dgamma = G(b.g_off);
+      g.dbeta = G(b.be_off);
+      g.dbias = G(b.b_off);
+      g.dz = dz;
+      g.gstride = g_stride_;
+      g.B = (int)B;
+      g.H = g.W = b.H;
+      g.C = b.cout;
+      g.pool = b.pool;
+      g.gslabs = gs;
+      g.bar = reinterpret_cast<unsigned*>(grid_bar_.data_ptr<int>());
+      g.err = grid_err_;
+      g.signal = pending_sig_;  // the previous block's dz-link signal rides this launch
+      pending_sig_ = nullptr;
+      ok(cs_bn_grid_bwd(g, s), "bn_grid_bwd");
+    } else if (red_pending_ == l) {  // the partial sums already ran inside the weight-gradient launch above
+      flush_signal(s);
       ok(cs_bn_bwd_tail(b.y.data_ptr<float>(), Gin, (int)B, b.H, b.H, b.cout, b.pool, bn, bn + b.cout,
                         bn + 2 * b.cout, bn + 3 * b.cout, P(b.g_off), bn_part_.data_ptr<float>(), red_P_,
                         bn_coef_.data_ptr<float>(), G(b.g_off), G(b.be_off), G(b.b_off), dz, s, gs, g_stride_),
          "bn_bwd_tail");
     } else if (bn_fused(l, B)) {  // reduce + finalize + apply in one launch
       ok(cs_bn_fused_bwd(b.y.data_ptr<float>(), Gin, (int)B, b.H, b.H, b.cout, b.pool, bn, P(b.g_off),
-                         bn_coef_.data_ptr<float>(), G(b.g_off), G(b.be_off), G(b.b_off), dz, s, gs, g_stride_),
+                         bn_coef_.data_ptr<float>(), G(b.g_off), G(b.be_off), G(b.b_off), dz, s, gs, g_stride_,
+                         pending_sig_),
          "bn_fused_bwd");
+      pending_sig_ = nullptr;
     } else if (bn_path_ == 1) {  // chunk partials, then finalize folded into the apply: two launches
+      flush_signal(s);
       ok(cs_bn_bwd2(b.y.data_ptr<float>(), gbuf_[(L - 1 - l) % 2].data_ptr<float>(), (int)B, b.H, b.H, b.cout, b.pool,
                     bn, P(b.g_off), bn_part_.data_ptr<float>(), G(b.g_off), G(b.be_off), G(b.b_off), dz, s),
          "bn_bwd2");
     } else {
+      flush_signal(s);
       ok(cs_bn_bwd(b.y.data_ptr<float>(), Gin, (int)B, b.H, b.H, b.cout, b.pool, bn, bn + b.cout,
                    bn + 2 * b.cout, bn + 3 * b.cout, P(b.g_off), bn_part_.data_ptr<float>(),
                    bn_coef_.data_ptr<float>(), G(b.g_off), G(b.be_off), G(b.b_off), dz, s, gs, g_stride_),
@@ -477,7 +550,7 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
       const ConvTile& t = b.tile[CS_CONV_DGRAD];
       const Dims d = dims(b, CS_CONV_DGRAD, B);
       const int sp = eff_splits(d.K, t.splits, t.bk);
-      const bool keep = keep_slabs_ && bn_path_ == 0 && sp > 1 && sp <= 32;
+      const bool keep = keep_slabs_ && bn_path_ != 1 && sp > 1 && sp <= 32;
       conv(l, CS_CONV_DGRAD, (int)B, t, s, false, nullptr, dz, keep);
       if (keep) {
         g_slabs_ = sp;
@@ -493,8 +566,11 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
     } else if (ovl && wgrad_after_dgrad_) {
       // (default) fork the weight gradient only after this block's data gradient: the
       // critical dgrad keeps the whole chip, and the wgrad fills it while the main stream
-      // runs the latency-bound split-K combine / BN backward kernels of the block below
-      dz_link_->signal(s);
+      // runs the latency-bound split-K combine / BN backward kernels of the block below.
+      // The signal rides the next main-stream launch (the BN backward of block l-1) instead of
+      // a launch of its own on the critical path (measured ~5.5 us each)
+      pending_sig_ = defer_signals_ ? dz_link_->defer() : nullptr;
+      if (pending_sig_ == nullptr) dz_link_->signal(s);
       dz_link_->wait(side_);
       conv(l, CS_CONV_WGRAD, (int)B, b.tile[CS_CONV_WGRAD], side_, false, ws_side_.data_ptr<float>(), dz);
       // block l's dgrad (the last reader of its weights) and BN backward ran before the fork
@@ -502,10 +578,15 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
       wg_link_->signal(side_);
     }
   }
+  flush_signal(s);  // nothing left on this stream to carry it
   if (join && ovl) join_side(s);
 }
 
 VggEngine::~VggEngine() {
+  if (grid_err_ != nullptr) {
+    hipDeviceSynchronize();
+    hipHostFree(grid_err_);
+  }
   if (side_ != nullptr) hipStreamSynchronize(side_);  // shared process-wide stream: not destroyed
   if (opt_ != nullptr) {
     hipStreamSynchronize(opt_);

@@ -179,7 +179,16 @@ class VggEngine {
   // 0 by measurement (MI355X, B=64): 80.7k img/s vs 77.1k — the channel-sliced blocks of the
   // folded launches stream NHWC rows as 64-B pieces and repeat the finalize in every block,
   // which costs more than the launch they save (e.g. block 0 forward 27.8 us vs 4.9 + 5.2 us)
-  int bn_path_ = 0;
+  // 2 (default) = one-launch grid-barrier BN forward / backward (bn_grid.hip) for the layers the
+  // single-block fused kernels do not serve: measured per-queue timeline (r3) had 197 us of BN
+  // launches on the critical path with the 2- / 3-launch paths.
+  int bn_path_ = 2;
+  torch::Tensor grid_bar_;     // zeroed grid-barrier counters of the BN kernels (main stream)
+  int* grid_err_ = nullptr;    // host-mapped: a grid barrier timed out
+  // a dz-link signal deferred into the next main-stream kernel (StreamLink::defer), or nullptr
+  unsigned long long* pending_sig_ = nullptr;
+  bool defer_signals_ = true;  // CS_DEFER_SIGNALS=0: every link signal as its own launch
+  void flush_signal(hipStream_t s);  // launch a pending deferred signal as its own kernel
   // CS_KEEP_SLABS=1: split-K data gradients leave their slabs in ws_ and the next BN backward
   // sums them (z order, bit-equal) while it reads G, instead of a separate combine launch.
   // Off: measured equal on MI355X (81.8-82.0k vs 82.0-82.1k img/s) — both BN passes then read

@@ -1,6 +1,8 @@
-set -o pipefail
-cd $GRAFT_REPO_ROOT
-mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
-echo "pytest exit $?"
-tail -30 gpurun_out/pytest_gpu.log
+#!/bin/bash
+# Selected GPU test files (args), one pytest process, each test bounded; then optional trace tag
+cd "${GRAFT_REPO_ROOT:-.}" && mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest -x -v --timeout 180 --timeout-method thread "$@" > gpurun_out/tests_sel.log 2>&1
+rc=$?
+grep -E "PASSED|FAILED|ERROR|passed|failed" gpurun_out/tests_sel.log | tail -40
+echo "pytest rc=$rc"
+exit $rc

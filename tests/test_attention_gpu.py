@@ -50,6 +50,57 @@ def test_flash_attention_matches_reference(dev, B, S, Hq, Hkv, D, causal):
         assert _rel(a, r) < 1.5e-2, (name, _rel(a, r))
 
 
+def _ref_per_head(q, k, v, do, causal):
+    """fp32 reference, one (batch, head) at a time (bounded memory at S = 4096): output and
+    dq/dk/dv, dk/dv summed over the query heads that share a KV head (GQA)."""
+    B, S, Hq, D = q.shape
+    Hkv = k.shape[2]
+    rep = Hq // Hkv
+    scale = 1.0 / math.sqrt(D)
+    o = torch.empty(B, S, Hq, D, device=q.device)
+    dq = torch.empty_like(o)
+    dk = torch.zeros(B, S, Hkv, D, device=q.device)
+    dv = torch.zeros_like(dk)
+    mask = torch.ones(S, S, dtype=torch.bool, device=q.device).triu(1) if causal else None
+    for b in range(B):
+        for h in range(Hq):
+            qh = q[b, :, h].float().requires_grad_()
+            kh = k[b, :, h // rep].float().requires_grad_()
+            vh = v[b, :, h // rep].float().requires_grad_()
+            s = (qh @ kh.t()) * scale
+            if mask is not None:
+                s = s.masked_fill(mask, float("-inf"))
+            oh = torch.softmax(s, -1) @ vh
+            oh.backward(do[b, :, h].float())
+            o[b, :, h] = oh.detach()
+            dq[b, :, h] = qh.grad
+            dk[b, :, h // rep] += kh.grad
+            dv[b, :, h // rep] += vh.grad
+    return o, dq, dk, dv
+
+
+@pytest.mark.parametrize("S", [2048, 4096])
+def test_flash_attention_llama3_8b_shape(dev, S):
+    """The shape the kernels are scheduled for (BASELINE.json config 5: Llama-3-8B, Hq 32 / Hkv 8,
+    D 128, causal): the one-launch causal backward dispatches dK/dV blocks heaviest key block first
+    with dQ blocks back-filling the CUs — only exercised with many (16 / 32) key blocks."""
+    from cs744_pytorch_distributed_tutorial_amd.ops.attention import attention, native_ok
+    B, Hq, Hkv, D = 1, 32, 8, 128
+    g = torch.Generator(device=dev).manual_seed(S)
+    q = torch.randn(B, S, Hq, D, device=dev, generator=g).bfloat16().requires_grad_()
+    k = torch.randn(B, S, Hkv, D, device=dev, generator=g).bfloat16().requires_grad_()
+    v = torch.randn(B, S, Hkv, D, device=dev, generator=g).bfloat16().requires_grad_()
+    do = torch.randn(B, S, Hq, D, device=dev, generator=g).bfloat16()
+    assert native_ok(q, k, v)
+    o = attention(q, k, v, True)
+    o.backward(do)
+    ro, rdq, rdk, rdv = _ref_per_head(q.detach(), k.detach(), v.detach(), do, True)
+    assert _rel(o, ro) < 8e-3, _rel(o, ro)
+    for name, a, r in (("dq", q.grad, rdq), ("dk", k.grad, rdk), ("dv", v.grad, rdv)):
+        assert torch.isfinite(a.float()).all(), name
+        assert _rel(a, r) < 1.5e-2, (name, _rel(a, r))
+
+
 def test_flash_attention_lse(dev):
     """The forward's row log-sum-exp (base 2, scaled scores) matches the reference."""
     from cs744_pytorch_distributed_tutorial_amd import _C

@@ -218,3 +218,33 @@ def test_resnet50_nhwc_bf16_as_accurate_as_miopen_bf16(dev):
     e_nat, e_mio = err("nhwc_bf16"), err("nchw_bf16")
     assert e_nat[0] <= 2 * e_mio[0] + 0.02, (e_nat, e_mio)
     assert e_nat[1] >= e_mio[1] - 0.02 and e_nat[2] >= e_mio[2] - 0.1, (e_nat, e_mio)
+
+
+def test_im2col_col2im_past_32bit_items(dev):
+    """the gathers index work items in 32 bits; tensors past 2^31 items run in batch
+    chunks instead of failing (the 224-px stem im2col crosses it near B = 850). 7300 images of
+    64x64x8 bf16 through a 3x3 im2col = 2.15e9 column elements; images on both sides of every
+    chunk boundary and the last one are checked against F.unfold, and col2im of the same columns
+    against the adjoint on those images."""
+    import torch.nn.functional as F
+    from cs744_pytorch_distributed_tutorial_amd.ops import native
+    C_ = native.C()
+    B, H, C, Kp = 7300, 64, 8, 72
+    g = torch.Generator(device=dev).manual_seed(0)
+    x = torch.randn(B, H, H, C, device=dev, generator=g).bfloat16()
+    col = C_.im2col_nhwc(x, 3, 3, 1, 1, Kp)
+    per = H * H * Kp
+    assert col.numel() == B * per and col.numel() > 2 ** 31
+    chunk = (2 ** 31 - 1) // per
+    for b in sorted({0, chunk - 1, chunk, min(2 * chunk, B - 1), B - 1}):
+        ref = F.unfold(x[b:b + 1].permute(0, 3, 1, 2).float(), 3, padding=1)  # [1, C*9 (c, r, s), HW]
+        ref = ref.view(C, 9, H * H).permute(2, 1, 0).reshape(H * H, 9 * C)  # columns (r, s, c)
+        got = col[b * H * H:(b + 1) * H * H, :9 * C].float()
+        assert torch.equal(got, ref), b
+    dx = C_.col2im_nhwc(col, B, H, H, C, 3, 3, 1, 1)
+    for b in sorted({0, chunk, B - 1}):
+        cb = col[b * H * H:(b + 1) * H * H, :9 * C].float().view(H * H, 9, C).permute(2, 1, 0).reshape(1, 9 * C, H * H)
+        ref = F.fold(cb, (H, H), 3, padding=1).permute(0, 2, 3, 1)[0]
+        torch.testing.assert_close(dx[b].float(), ref, rtol=1e-2, atol=1e-2)
+    del col, dx
+    torch.cuda.empty_cache()

@@ -175,10 +175,11 @@ def test_conv_wgrad(dev, shape, tile, fixup, stage):
                                         (64, 2, 512, True), (5, 16, 128, True), (8, 8, 256, False),
                                         (16, 8, 256, False), (8, 4, 512, False), (64, 8, 256, False),
                                         (64, 32, 64, True)])
-@pytest.mark.parametrize("fused", [False, True, "two"])
+@pytest.mark.parametrize("fused", [False, True, "two", "grid"])
 def test_bn_relu_pool_fwd_bwd(dev, B, H, C, pool, fused):
     # False: finalize / apply / reduce / finalize / apply launches; True: the single-launch kernels
-    # (forward row-chunked over blocks); "two": row-chunked forward + the two-launch backward
+    # (forward row-chunked over blocks); "two": row-chunked forward + the two-launch backward;
+    # "grid": the one-launch grid-barrier kernels (bn_grid.hip, the engine's default)
     from cs744_pytorch_distributed_tutorial_amd.ops import functional as Fn
     torch.manual_seed(B * C)
     y = (torch.randn(B, C, H, H, dtype=torch.float64) * 2 + 0.5).requires_grad_()
@@ -202,7 +203,8 @@ def test_bn_relu_pool_fwd_bwd(dev, B, H, C, pool, fused):
         seg = yd.double().view(-1, R, C)
         mu_t = seg.mean(1)
         st = torch.stack([mu_t, ((seg - mu_t[:, None]) ** 2).sum(1)], 2).float().contiguous()
-        out, bst = Fn.bn_relu_pool_fwd(yd, st, R, B, H, H, gd, bd, rmd, rvd, nbt, pool=pool, fused=True)
+        out, bst = Fn.bn_relu_pool_fwd(yd, st, R, B, H, H, gd, bd, rmd, rvd, nbt, pool=pool,
+                                       fused="grid" if fused == "grid" else True)
         # every row chunk of the forward computed the same coefficients: bnv matches a fresh finalize
         _close(bst.mean, yd.double().mean(0), 1e-5)
     else:

@@ -57,6 +57,36 @@ def _lm_ddp(rank, world, sync):
     return torch.cat([p.detach().reshape(-1) for p in tr.module.parameters()])
 
 
+def _lm_ddp_transport(rank, world, gdt):
+    import os
+    os.environ["CS744_GRAD_COMM_DTYPE"] = gdt
+    from cs744_pytorch_distributed_tutorial_amd.runtime.torch_trainer import TorchTrainer
+    torch.set_num_threads(1)
+    tr = TorchTrainer("llama-tiny", 4, torch.device("cpu"), rank, world, sync="ddp", comm="torch", bucket_mb=0.5,
+                      lr=0.05, weight_decay=0.0, seq_len=32, fused_sgd=False)
+    p0 = torch.cat([p.detach().reshape(-1) for p in tr.module.parameters()]).clone()
+    for _ in range(3):
+        tr.step()
+    return {"p": torch.cat([p.detach().reshape(-1) for p in tr.module.parameters()]), "p0": p0,
+            "wire": str(tr.net.grad_comm_dtype)}
+
+
+@pytest.mark.slow
+def test_lm_ddp_bf16_gradient_transport_matches_fp32():
+    """bf16 gradient transport (the LM default: half the xGMI bytes) vs fp32 transport, 2-rank gloo:
+    replicas stay identical and the trained weights agree to bf16 rounding of the gradients."""
+    bf = run_world(_lm_ddp_transport, 2, "bf16")
+    fp = run_world(_lm_ddp_transport, 2, "fp32")
+    assert bf[0]["wire"] == "torch.bfloat16" and fp[0]["wire"] == "None"
+    assert torch.equal(torch.as_tensor(bf[0]["p"]), torch.as_tensor(bf[1]["p"]))
+    pb, pf, p0 = (torch.as_tensor(t) for t in (bf[0]["p"], fp[0]["p"], fp[0]["p0"]))
+    step = (pf - p0).abs().max()
+    assert step > 0
+    # each gradient element is rounded to 8 significant bits once (+ the average): the weight
+    # difference stays a small fraction of the 3-step update, and not zero (the wire is bf16)
+    assert 0 < (pb - pf).abs().max() <= 2e-2 * step
+
+
 @pytest.mark.slow
 @pytest.mark.parametrize("sync", ["ddp", "allreduce"])
 def test_lm_data_parallel_replicas_identical(sync):

@@ -251,6 +251,44 @@ def test_single_launch_bn_matches_multi_kernel_bn(dev):
     torch.testing.assert_close(b.nbt, a.nbt)
 
 
+def test_grid_bn_matches_multi_launch_bn(dev, monkeypatch):
+    """The one-launch grid-barrier BN kernels (default, CS_BN_PATH=2) vs the 2/3-launch path
+    (CS_BN_PATH=0): same partials, different (fixed) finalize order -> a norm bound after two
+    steps, identical num_batches_tracked; and the grid path is deterministic run to run."""
+    out = []
+    for path in ("0", "2", "2"):
+        monkeypatch.setenv("CS_BN_PATH", path)
+        t = _trainer(dev, batch_size=32, train_size=256)
+        for _ in range(2):
+            t.step()
+        torch.cuda.synchronize()
+        assert not t.engine.link_error()
+        out.append((t.params.clone(), t.nbt.clone(), t.last_loss()))
+    a, b, c = out
+    assert abs(a[2] - b[2]) < 1e-3 * max(1.0, abs(a[2]))
+    d = (b[0].double() - a[0].double()).norm() / a[0].double().norm()
+    assert d.item() < 2e-3, d.item()
+    torch.testing.assert_close(a[1], b[1])
+    assert torch.equal(b[0], c[0])
+
+
+def test_deferred_link_signals_bitwise_equal(dev, monkeypatch):
+    """Side-stream weight gradients forked by a signal folded into the next main-stream BN launch
+    (CS_DEFER_SIGNALS=1, default) == a separate signal launch per block, bit for bit."""
+    out = []
+    for defer in ("0", "1"):
+        monkeypatch.setenv("CS_DEFER_SIGNALS", defer)
+        t = _trainer(dev, batch_size=32, train_size=256)
+        assert t.overlap_wgrad
+        for _ in range(4):
+            t.step()
+        torch.cuda.synchronize()
+        t.check_comm()
+        out.append((t.params.clone(), t.mom.clone(), t.bufs.clone()))
+    for a, b in zip(out[0], out[1]):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("stage", [0, 16 | 4])
 def test_kept_dgrad_slabs_bitwise_equal(dev, stage, monkeypatch):
     # CS_KEEP_SLABS=1 (opt-in): split-K data gradients left as slabs and summed (z order) by the
@@ -302,6 +340,7 @@ def test_bn_reduce_in_wgrad_launch_bitwise_equal(dev, keep, monkeypatch):
     # block l-1's BN partial-sum pass appended to block l's weight-gradient launch (extra blocks
     # after the GEMM tiles) == the standalone reduce launch, bit for bit (also with kept slabs)
     monkeypatch.setenv("CS_KEEP_SLABS", keep)
+    monkeypatch.setenv("CS_BN_PATH", "0")  # the appended reduce belongs to the three-launch BN path
     out = []
     for fuse in ("0", "1"):
         monkeypatch.setenv("CS_FUSE_BN_RED", fuse)
