@@ -1,0 +1,94 @@
+#!/bin/bash
+# One parametrised driver for every GPU measurement of this repo (replaces the round-1/2 one-off
+# lease scripts). Run on the box as one gpurun command, e.g.
+#   gpurun --timeout 1200 -- 'bash scripts/gpu.sh suite'
+#   gpurun --timeout 900  -- 'bash scripts/gpu.sh tests tests/test_conv_bn_gpu.py -k grid'
+#   gpurun --timeout 600  -- 'bash scripts/gpu.sh trace r3 --steps 10'
+# Every GPU step runs under its own timeout and the steps chain with && (a crash, abort or time
+# limit ends the command; nothing is retried). Results land in gpurun_out/.
+#
+#   suite                      every GPU test, smoke(), default bench   (the driver's round-end set)
+#   tests FILES... [pytest -k]  selected GPU tests, one pytest process
+#   bench [bench.py args]      one bench.py run (default: 20 timed / 5 warmup steps)
+#   trace TAG [bench args]     rocprofv3 kernel + marker trace -> per-kernel table and a one-step
+#                              per-queue timeline (scripts/prof_summary.py, scripts/step_timeline.py)
+#   pmc TAG "COUNTERS" [args]  one rocprofv3 counter pass over a short bench (kernel trace only,
+#                              never combined with other trace domains) -> scripts/pmc_summary.py
+#   xp                         pre-split conv GEMM tests + graph-timed sweep (scripts/xp_bench.py)
+#   probe                      XP K-loop ablation (scripts/xp_probe.py)
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-.}" || exit 1
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+R=$PWD
+what=${1:-suite}
+shift || true
+
+page_in() { timeout -k 10 300 python3 -c "import torch, cs744_pytorch_distributed_tutorial_amd" || exit $?; }
+
+case "$what" in
+  suite)
+    timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 240 \
+      --timeout-method thread > gpurun_out/pytest_gpu_full.log 2>&1
+    rc=$?; echo "pytest exit $rc"; tail -5 gpurun_out/pytest_gpu_full.log
+    [ $rc -eq 0 ] || exit $rc
+    timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+    rc=$?; echo "smoke exit $rc"; tail -3 gpurun_out/smoke.log
+    [ $rc -eq 0 ] || exit $rc
+    timeout -k 10 300 python -u bench.py > gpurun_out/bench_default.log 2>&1
+    rc=$?; tail -1 gpurun_out/bench_default.log; exit $rc
+    ;;
+  tests)
+    timeout -k 10 1000 python -u -m pytest -x -v --timeout 180 --timeout-method thread "$@" \
+      > gpurun_out/tests_sel.log 2>&1
+    rc=$?
+    grep -E "PASSED|FAILED|ERROR|passed|failed" gpurun_out/tests_sel.log | tail -60
+    echo "pytest rc=$rc"; exit $rc
+    ;;
+  bench)
+    [ $# -eq 0 ] && set -- --steps 20 --warmup 5
+    timeout -k 10 400 python -u bench.py "$@" > gpurun_out/bench.log 2>&1
+    rc=$?; grep -v amdgpu.ids gpurun_out/bench.log | tail -3; exit $rc
+    ;;
+  trace)
+    TAG=${1:-trace}; shift || true
+    [ $# -eq 0 ] && set -- --steps 10 --warmup 5
+    page_in
+    (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --marker-trace --stats -d $R/gpurun_out/$TAG -o run -- \
+      python3 $R/bench.py "$@" > $R/gpurun_out/$TAG.log 2>&1)
+    rc=$?; echo "rocprofv3 rc=$rc"; tail -1 gpurun_out/$TAG.log
+    [ $rc -eq 0 ] || exit $rc
+    python3 scripts/prof_summary.py gpurun_out/$TAG --steps 15 --top 45 > gpurun_out/${TAG}_kernels.txt 2>&1
+    python3 scripts/step_timeline.py gpurun_out/$TAG > gpurun_out/${TAG}_timeline.txt 2>&1
+    head -3 gpurun_out/${TAG}_kernels.txt
+    grep -E "^# one step|^## queue|^# queue|^# main" gpurun_out/${TAG}_timeline.txt
+    ;;
+  pmc)
+    TAG=${1:-pmc}; P=$2; shift 2 || true
+    [ $# -eq 0 ] && set -- --steps 3 --warmup 2
+    page_in
+    # counter collection serialises dispatches: the side-stream link waits cannot overlap
+    export CS_OVERLAP_WGRAD=0
+    (cd /tmp && timeout -s KILL 150 rocprofv3 --pmc $P --output-format csv -d $R/gpurun_out/$TAG -o run -- \
+      python3 $R/bench.py "$@" > $R/gpurun_out/$TAG.log 2>&1)
+    rc=$?; echo "pmc pass exit $rc"; tail -2 gpurun_out/$TAG.log
+    [ $rc -eq 0 ] || exit $rc
+    python3 scripts/pmc_summary.py gpurun_out/$TAG > gpurun_out/${TAG}_summary.txt 2>&1
+    head -40 gpurun_out/${TAG}_summary.txt
+    ;;
+  xp)
+    timeout -k 10 700 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_conv_xp_gpu.py \
+      > gpurun_out/xp_tests.log 2>&1
+    rc=$?; tail -5 gpurun_out/xp_tests.log; echo "pytest rc=$rc"
+    [ $rc -eq 0 ] || exit $rc
+    timeout -k 10 600 python -u scripts/xp_bench.py 64 10 > gpurun_out/xp_bench.log 2>&1
+    rc=$?; grep -v amdgpu.ids gpurun_out/xp_bench.log; exit $rc
+    ;;
+  probe)
+    timeout -k 10 400 python -u scripts/xp_probe.py > gpurun_out/xp_probe.log 2>&1
+    rc=$?; cat gpurun_out/xp_probe.log; exit $rc
+    ;;
+  *)
+    echo "usage: bash scripts/gpu.sh suite|tests|bench|trace|pmc|xp|probe ..."; exit 2
+    ;;
+esac
