@@ -12,6 +12,10 @@ if ROOT not in sys.path:
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (run via gpurun)")
     config.addinivalue_line("markers", "slow: multi-process or long-running test")
+    # the test session is an entry point like bench.py: HIP's hardware queues are raised before
+    # any test initialises HIP (the engine's side stream + a communicator need >= 8 queues)
+    import cs744_pytorch_distributed_tutorial_amd as pkg
+    pkg.ensure_hw_queues()
 
 
 def free_port() -> int:

@@ -33,6 +33,10 @@ def _entry(rank, world, port, fn, args, q):
     import torch
     torch.set_num_threads(1)
     try:
+        # each rank is an entry point: raise HIP's hardware queues before anything initialises HIP,
+        # as bench.py / train.py do (the side-stream weight-gradient path needs >= 8 with a comm)
+        import cs744_pytorch_distributed_tutorial_amd as pkg
+        pkg.ensure_hw_queues()
         from cs744_pytorch_distributed_tutorial_amd import distributed as D
         D.init_process_group(backend="gloo", rank=rank, world_size=world, master_addr="127.0.0.1",
                              master_port=port, timeout_s=120)

@@ -30,17 +30,20 @@ pytestmark = [pytest.mark.gpu]
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _train(rank, world, sync, graph, steps, comm="torch", B=16):
+def _train(rank, world, sync, graph, steps, comm="torch", B=16, autotune=False):
     from cs744_pytorch_distributed_tutorial_amd.runtime.engine import NativeTrainer
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     tr = NativeTrainer(batch_size=B, device=dev, rank=rank, world=world, sync=sync, comm=comm, bucket_mb=2.0,
-                       graph=graph, train_size=512, test_size=64, autotune=False, check_every=1)
+                       graph=graph, train_size=max(512, 8 * B * world), test_size=64, autotune=autotune,
+                       check_every=1)
     for _ in range(steps):
         tr.step()
     torch.cuda.synchronize()
     ev = tr.evaluate(max_batches=2)
+    maths = sorted({t["math"] for t in tr.tile_table()}) if autotune else []
     out = {"params": tr.params.cpu(), "mom": tr.mom.cpu(), "bufs": tr.bufs.cpu(), "nbt": tr.nbt.cpu(),
+           "tiles": tr.tile_source, "maths": maths,
            "loss": tr.last_loss(), "buckets": len(tr.bucket_lows), "graph": tr.graph_mode,
            "calls": tr.native_comm.calls() if tr.native_comm is not None else -1,
            "kind": tr.native_comm.kind if tr.native_comm is not None else "none", "eval": ev,
@@ -89,6 +92,21 @@ def test_cpp_ddp_step_multi_rank_staged(gpu, world):
     assert torch.equal(nat[0]["params"], ref[0]["params"])
     assert torch.equal(nat[0]["mom"], ref[0]["mom"])
     assert nat[0]["loss"] == ref[0]["loss"]
+
+
+@pytest.mark.slow
+def test_cpp_ddp_step_multi_rank_staged_bench_config(gpu):
+    """The same multi-rank C++ step at the benchmark's configuration: B = 64 per rank and the
+    shipped gfx950 tile table (split-bf16 X6S conv kernels, split-K), not the small default tiles."""
+    steps = 4
+    nat = run_world(_train, 2, "ddp", "none", steps, "staged", 64, True)
+    ref = run_world(_train, 2, "ddp", "segments", steps, "torch", 64, True)
+    assert nat[0]["tiles"] == "shipped" and "x6s" in nat[0]["maths"], (nat[0]["tiles"], nat[0]["maths"])
+    assert nat[0]["wgrad_side"] and nat[0]["kind"] == "staged"
+    for k in ("params", "mom", "bufs", "nbt"):
+        assert torch.equal(nat[1][k], nat[0][k]), k
+    assert torch.equal(nat[0]["params"], ref[0]["params"])
+    assert torch.equal(nat[0]["mom"], ref[0]["mom"])
 
 
 def _ragged(rank, world):
