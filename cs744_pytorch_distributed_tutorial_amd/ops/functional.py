@@ -144,7 +144,7 @@ def _grid_bar(device) -> torch.Tensor:
     """Zeroed grid-barrier counters of the one-launch BN kernels (left zeroed by every launch)."""
     key = str(device)
     if key not in _GRID_BARS:
-        _GRID_BARS[key] = torch.zeros(4, dtype=torch.int32, device=device)
+        _GRID_BARS[key] = torch.zeros(640, dtype=torch.int32, device=device)  # kCsBnGridBarInts
     return _GRID_BARS[key]
 
 

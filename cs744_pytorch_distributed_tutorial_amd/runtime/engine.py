@@ -279,20 +279,23 @@ class NativeTrainer:
                                   self.params, self.grads, self.mom, self.bufs, self.nbt)
         # weight gradients on a side stream (off the backward's critical chain; bit-identical):
         # on unless CS_OVERLAP_WGRAD=0, or a communicator runs with too few HIP hardware queues
-        # (their cross-stream waits would serialise behind each other, package __init__). Only
-        # for steps the engine orders itself: with collectives issued from Python through
-        # torch.distributed (comm="torch"), a gloo all-reduce of a bucket whose weight
-        # gradients came from the side stream intermittently read a stale gradient
-        # (measured: layers.25.weight wrong at step 3 of 4, world 2, whether the side stream
-        # was joined by a stream link or a HIP event; only a host sync of the side stream
-        # avoided it), so that path keeps the serial backward.
-        # Also off under rocprofv3 counter collection, which serialises every dispatch: a side-stream
-        # link wait would spin to its timeout waiting for a signal that cannot run.
+        # (their cross-stream waits would serialise behind each other, package __init__), or
+        # under rocprofv3 counter collection, which serialises every dispatch (a side-stream link
+        # wait would spin to its timeout waiting for a signal that cannot run).
+        # Collectives issued from Python (comm="torch": gloo copies each bucket to the host)
+        # additionally need the side stream's results released to SYSTEM scope before that copy:
+        # round 2 measured a stale layers.25.weight gradient at world 2 without it, so the join
+        # then also waits on a system-release event (VggEngine::join_side; CS_SYS_JOIN=0 drops it,
+        # and without it the overlap stays off for Python collectives unless CS_OVERLAP_WGRAD=force).
         from .. import hw_queues
         python_collectives = world > 1 and self.native_comm is None
-        self.overlap_wgrad = os.environ.get("CS_OVERLAP_WGRAD", "1") != "0" and not python_collectives and (
+        sj = os.environ.get("CS_SYS_JOIN")
+        self.sys_join = python_collectives if sj is None else sj != "0"
+        ow = os.environ.get("CS_OVERLAP_WGRAD", "1")
+        self.overlap_wgrad = ow != "0" and (ow == "force" or self.sys_join or not python_collectives) and (
             self.native_comm is None or hw_queues() >= 8) and not self._counters
         self.engine.set_overlap_wgrad(self.overlap_wgrad)
+        self.engine.set_sys_join(self.sys_join)
         self.engine.set_data(0, self.train_data, self.train_labels, self.aug_train)
         self.engine.set_data(1, self.test_data, self.test_labels, self.aug_test)
         self.idx_buf = self.engine.idx()

@@ -221,7 +221,7 @@ void bn_fused_fwd(torch::Tensor part, int64_t T, int64_t R, int64_t M, torch::Te
                             cur_stream()));
 }
 
-// one-launch grid-barrier BN (bn_grid.hip); bar: zeroed int32 counters (>= 3), left zeroed
+// one-launch grid-barrier BN (bn_grid.hip); bar: zeroed int32 counters (>= kCsBnGridBarInts), left zeroed
 void bn_grid_fwd(torch::Tensor part, int64_t T, int64_t R, int64_t M, torch::Tensor gamma, torch::Tensor beta,
                  c10::optional<torch::Tensor> running_mean, c10::optional<torch::Tensor> running_var,
                  c10::optional<torch::Tensor> nbt, double momentum, double eps, torch::Tensor bnv, torch::Tensor y,
@@ -232,7 +232,7 @@ void bn_grid_fwd(torch::Tensor part, int64_t T, int64_t R, int64_t M, torch::Ten
   check_t(part, T * C * 2, "part"); check_t(beta, C, "beta"); check_t(bnv, 4 * C, "bnv");
   check_t(running_mean, C, "running_mean"); check_t(running_var, C, "running_var");
   check_t(y, M * C, "y"); check_t(out, B * (pool ? H / 2 : H) * (pool ? W / 2 : W) * C, "out");
-  TORCH_CHECK(bar.is_cuda() && bar.scalar_type() == at::kInt && bar.numel() >= 3, "bn_grid: bar int32 [>= 3]");
+  TORCH_CHECK(bar.is_cuda() && bar.scalar_type() == at::kInt && bar.numel() >= kCsBnGridBarInts, "bn_grid: bar int32 [>= kCsBnGridBarInts]");
   if (nbt.has_value()) TORCH_CHECK(nbt->scalar_type() == at::kLong && nbt->is_cuda(), "nbt: int64 GPU scalar");
   CsBnGridFwd g{};
   g.part = part.data_ptr<float>(); g.gamma = gamma.data_ptr<float>(); g.beta = beta.data_ptr<float>();
@@ -257,7 +257,7 @@ void bn_grid_bwd(torch::Tensor y, torch::Tensor G, int64_t B, int64_t H, int64_t
   check_t(part, (int64_t)cs_bn_bwd_blocks(B, H, W, C, pool) * C * 3, "part");
   check_t(dgamma, C, "dgamma"); check_t(dbeta, C, "dbeta"); check_t(dbias, C, "dbias");
   check_t(dz, B * H * W * C, "dz");
-  TORCH_CHECK(bar.is_cuda() && bar.scalar_type() == at::kInt && bar.numel() >= 3, "bn_grid: bar int32 [>= 3]");
+  TORCH_CHECK(bar.is_cuda() && bar.scalar_type() == at::kInt && bar.numel() >= kCsBnGridBarInts, "bn_grid: bar int32 [>= kCsBnGridBarInts]");
   CsBnGridBwd g{};
   const float* bv = bnv.data_ptr<float>();
   g.y = y.data_ptr<float>(); g.G = G.data_ptr<float>();

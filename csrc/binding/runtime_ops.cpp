@@ -181,6 +181,7 @@ void register_runtime(pybind11::module& m) {
            py::arg("bucket_ranges"), py::arg("broadcast_buffers"), py::arg("lr"), py::arg("momentum"),
            py::arg("wd"), py::arg("dampening"))
       .def("set_overlap_wgrad", &cs::VggEngine::set_overlap_wgrad)
+      .def("set_sys_join", &cs::VggEngine::set_sys_join)
       .def("set_sgd_overlap", &cs::VggEngine::set_sgd_overlap)
       .def("set_sgd_side", &cs::VggEngine::set_sgd_side)
       .def("link_error", &cs::VggEngine::link_error)

@@ -21,6 +21,8 @@
 // `signal` (optional): a kernel stream link's counter bumped by block 0 as its first action —
 // this launch starts only after the previous kernel on its stream completed and released, so
 // that is the same "previous work done" edge as a separate link_signal launch, minus the launch.
+#include <type_traits>
+
 #include "bn_device.h"
 #include "common.h"
 #include "launchers.h"
@@ -34,23 +36,49 @@ __device__ __forceinline__ void link_bump(unsigned long long* signal) {
     __hip_atomic_fetch_add(signal, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// all P blocks arrive; returns after every block's earlier global stores are visible
-__device__ __forceinline__ void grid_barrier(unsigned* ctr, unsigned P, int* err) {
+// Counter layout (kBarInts ints, zeroed; every launch leaves it zeroed): barrier i owns
+// [i * kBarStride, (i + 1) * kBarStride): 8 group counters 32 ints (128 B) apart, then the top
+// counter at +256; the exit counter follows the last barrier.
+constexpr int kBarStride = 288;
+
+// all P blocks arrive; returns after every block's earlier global stores are visible.
+// BARV 0: one counter, every block polls it with memory-side read-modify-writes (round-3 first
+//         version: ~14 us per barrier at P = 256, measured — P RMWs serialise on one address).
+// BARV 1: one counter for arrival, polled with agent-scope atomic loads.
+// BARV 2: hierarchical arrival — block b counts into group (b & 7)'s counter (its own 128-B
+//         line); the last of a group bumps the top counter, which the blocks poll with loads.
+template <int BARV>
+__device__ __forceinline__ void grid_barrier(unsigned* bar, int i, unsigned P, int* err) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned* top = bar + i * kBarStride + 256;
+    unsigned target = P;
+    if (BARV == 2) {
+      const unsigned g = blockIdx.x & 7u, gs = (P - g + 7u) >> 3;
+      target = P < 8u ? P : 8u;
+      // acq_rel: releases this block's stores and acquires the earlier arrivals' of its group,
+      // so the group's last block releases all of them with its top bump
+      const unsigned t = __hip_atomic_fetch_add(bar + i * kBarStride + g * 32, 1u, __ATOMIC_ACQ_REL,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+      if (t == gs - 1u) __hip_atomic_fetch_add(top, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     const unsigned long long t0 = wall_clock64();
     unsigned zero = 0;
-    asm volatile("" : "+v"(zero));  // a run-time 0: keeps the poll a memory-side read-modify-write
-    while (__hip_atomic_fetch_add(ctr, zero, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < P) {
+    asm volatile("" : "+v"(zero));  // a run-time 0: keeps the BARV 0 poll a memory-side read-modify-write
+    for (;;) {
+      const unsigned v = BARV == 0 ? __hip_atomic_fetch_add(top, zero, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                   : __hip_atomic_load(top, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (v >= target) break;
       if (wall_clock64() - t0 > kSpinTicks) {
         if (err != nullptr) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
       }
-      __builtin_amdgcn_s_sleep(2);
+      __builtin_amdgcn_s_sleep(BARV == 0 ? 2 : 1);
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -58,12 +86,17 @@ __device__ __forceinline__ void grid_barrier(unsigned* ctr, unsigned P, int* err
   __syncthreads();
 }
 
-// the last block to finish resets the NB barrier counters (every block is past every barrier)
-__device__ __forceinline__ void grid_exit(unsigned* ctr, int NB, unsigned P) {
+// the last block to finish resets the NB barriers' counters (every block is past every barrier)
+__device__ __forceinline__ void grid_exit(unsigned* bar, int NB, unsigned P) {
   if (threadIdx.x == 0) {
-    const unsigned t = __hip_atomic_fetch_add(ctr + NB, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (t == P - 1)
-      for (int i = 0; i <= NB; ++i) __hip_atomic_store(ctr + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned t = __hip_atomic_fetch_add(bar + NB * kBarStride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t == P - 1) {
+      for (int i = 0; i < NB; ++i) {
+        for (int g = 0; g < 8; ++g) __hip_atomic_store(bar + i * kBarStride + g * 32, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(bar + i * kBarStride + 256, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      __hip_atomic_store(bar + NB * kBarStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 
@@ -123,7 +156,7 @@ __device__ __forceinline__ float4 bnrelu4(float4 y, float4 s, float4 t) {
 }
 
 // ------------------------------------------------------------------ backward
-template <bool POOL>
+template <bool POOL, int BARV>
 __global__ __launch_bounds__(256) void bn_bwd_grid_kernel(CsBnGridBwd a) {
   extern __shared__ __attribute__((aligned(16))) float red[];  // rows * C * 3 (phase 1), then scratch
   link_bump(a.signal);
@@ -133,7 +166,7 @@ __global__ __launch_bounds__(256) void bn_bwd_grid_kernel(CsBnGridBwd a) {
   const CsBnRed r{a.y, a.G, a.scale, a.shift, a.mean, a.invstd, a.part, a.gstride,
                   a.B, a.H, a.W, C, POOL ? 1 : 0, (int)P, a.gslabs};
   cs_bn::bn_red_body<POOL>(r, blockIdx.x, P, red);
-  grid_barrier(a.bar, P, a.err);
+  if (BARV >= 0) grid_barrier<BARV>(a.bar, 0, P, a.err);
   // phase 2: channels b, b + P, ...: sum the P partials (thread t holds p = t, t + 256, ...,
   // then a fixed tree), then the coefficients
   const int M = a.B * a.H * a.W;
@@ -156,7 +189,7 @@ __global__ __launch_bounds__(256) void bn_bwd_grid_kernel(CsBnGridBwd a) {
       a.coef[3 * c + 2] = k3;
     }
   }
-  grid_barrier(a.bar + 1, P, a.err);
+  if (BARV >= 0) grid_barrier<BARV>(a.bar, 1, P, a.err);
   // phase 3: dZ over this block's units (the apply pass of bn.hip, coefficients from global)
   const int C4 = C >> 2, rows = 256 / C4;
   const int cq = threadIdx.x % C4, rl = threadIdx.x / C4;
@@ -166,10 +199,11 @@ __global__ __launch_bounds__(256) void bn_bwd_grid_kernel(CsBnGridBwd a) {
     for (int u = blockIdx.x * rows + rl; u < units; u += P * rows)
       cs_bn::bwd_visit<true, POOL>(a.y, a.G, a.B, a.H, a.W, C, cq, u, a.scale, a.shift, a.mean, a.invstd, a.coef, a.dz,
                                    dummy, a.gslabs, a.gstride);
-  grid_exit(a.bar, 2, P);
+  if (BARV >= 0) grid_exit(a.bar, 2, P);
 }
 
 // ------------------------------------------------------------------ forward
+template <int BARV>
 __global__ __launch_bounds__(256) void bn_fwd_grid_kernel(CsBnGridFwd a) {
   __shared__ float lds[16];
   link_bump(a.signal);
@@ -201,7 +235,7 @@ __global__ __launch_bounds__(256) void bn_fwd_grid_kernel(CsBnGridFwd a) {
     }
   }
   if (a.nbt != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *a.nbt += 1;
-  grid_barrier(a.bar, P, a.err);
+  if (BARV >= 0) grid_barrier<BARV>(a.bar, 0, P, a.err);
   // phase 2: relu(y * scale + shift) (2x2 max with pooling), one thread per (unit, 4 channels)
   const int C4 = C >> 2;
   const int Ho = a.pool ? a.H >> 1 : a.H, Wo = a.pool ? a.W >> 1 : a.W;
@@ -225,16 +259,47 @@ __global__ __launch_bounds__(256) void bn_fwd_grid_kernel(CsBnGridFwd a) {
     }
     reinterpret_cast<float4*>(a.out)[t] = o;
   }
-  grid_exit(a.bar, 1, P);
+  if (BARV >= 0) grid_exit(a.bar, 1, P);
 }
 
 }  // namespace
+
+// experiment knobs (scripts/bn_grid_bench.py): CS_BN_GRID_PMUL = blocks per CU allowed for the
+// forward (1..4), CS_BN_GRID_BARV = barrier version (0, 1, 2; -1 skips the barriers: wrong
+// results, timing of the phases alone)
+static int grid_pmul() {
+  static const int v = [] {
+    const char* e = getenv("CS_BN_GRID_PMUL");
+    const int m = e ? atoi(e) : 1;
+    return m < 1 ? 1 : (m > 4 ? 4 : m);
+  }();
+  return v;
+}
+static int grid_barv() {
+  static const int v = [] {
+    const char* e = getenv("CS_BN_GRID_BARV");
+    const int b = e ? atoi(e) : 2;
+    return b < -1 ? -1 : (b > 2 ? 2 : b);
+  }();
+  return v;
+}
+
+template <typename F>
+static void with_barv(F&& f) {
+  switch (grid_barv()) {
+    case -1: f(std::integral_constant<int, -1>{}); break;
+    case 0: f(std::integral_constant<int, 0>{}); break;
+    case 1: f(std::integral_constant<int, 1>{}); break;
+    default: f(std::integral_constant<int, 2>{}); break;
+  }
+}
 
 int cs_bn_grid_fwd_blocks(int B, int H, int W, int C, int pool) {
   const int64_t total = (int64_t)B * (pool ? H / 2 : H) * (pool ? W / 2 : W) * (C / 4);
   int64_t p = (total + 255) / 256;
   if (p < C / 2) p = C / 2;  // at least half a block per channel for the finalize phase
-  return (int)(p > 256 ? 256 : (p < 1 ? 1 : p));
+  const int64_t cap = 256 * grid_pmul();
+  return (int)(p > cap ? cap : (p < 1 ? 1 : p));
 }
 
 hipError_t cs_bn_grid_bwd(const CsBnGridBwd& a, hipStream_t stream) {
@@ -242,16 +307,20 @@ hipError_t cs_bn_grid_bwd(const CsBnGridBwd& a, hipStream_t stream) {
     return hipErrorInvalidValue;
   const int P = cs_bn_bwd_blocks(a.B, a.H, a.W, a.C, a.pool);  // <= 256: every block resident
   const size_t lds = (size_t)(256 / (a.C / 4)) * a.C * 3 * sizeof(float);
-  if (a.pool)
-    hipLaunchKernelGGL((bn_bwd_grid_kernel<true>), dim3(P), dim3(256), lds, stream, a);
-  else
-    hipLaunchKernelGGL((bn_bwd_grid_kernel<false>), dim3(P), dim3(256), lds, stream, a);
+  with_barv([&](auto bv) {
+    if (a.pool)
+      hipLaunchKernelGGL((bn_bwd_grid_kernel<true, decltype(bv)::value>), dim3(P), dim3(256), lds, stream, a);
+    else
+      hipLaunchKernelGGL((bn_bwd_grid_kernel<false, decltype(bv)::value>), dim3(P), dim3(256), lds, stream, a);
+  });
   return hipGetLastError();
 }
 
 hipError_t cs_bn_grid_fwd(const CsBnGridFwd& a, hipStream_t stream) {
   if (a.C % 4 != 0 || (a.pool && ((a.H | a.W) & 1)) || a.bar == nullptr || a.T < 1) return hipErrorInvalidValue;
   const int P = cs_bn_grid_fwd_blocks(a.B, a.H, a.W, a.C, a.pool);
-  hipLaunchKernelGGL(bn_fwd_grid_kernel, dim3(P), dim3(256), 0, stream, a);
+  with_barv([&](auto bv) {
+    hipLaunchKernelGGL((bn_fwd_grid_kernel<decltype(bv)::value>), dim3(P), dim3(256), 0, stream, a);
+  });
   return hipGetLastError();
 }

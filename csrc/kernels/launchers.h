@@ -155,8 +155,8 @@ hipError_t cs_bn_bwd_tail(const float* y, const float* G, int B, int H, int W, i
 // One-launch BN (bn_grid.hip): P <= 256 blocks (all resident) whose phases meet at in-kernel grid
 // barriers — backward: partials | per-channel finalize | dZ apply (replaces cs_bn_bwd's three
 // launches, same partials bit for bit); forward: finalize from the conv epilogue's tile partials |
-// normalize/ReLU/pool (replaces cs_bn_finalize + cs_bn_apply). bar: zeroed device counters the
-// kernels leave zeroed (3 for backward, 2 for forward; one set per stream); err: device word set
+// normalize/ReLU/pool (replaces cs_bn_finalize + cs_bn_apply). bar: kCsBnGridBarInts zeroed device
+// ints the kernels leave zeroed (one set per stream and direction); err: device word set
 // on a barrier timeout; signal: optional stream-link counter bumped when the launch starts.
 struct CsBnGridBwd {
   const float *y, *G, *scale, *shift, *mean, *invstd, *gamma;
@@ -177,6 +177,7 @@ struct CsBnGridFwd {
   int* err;
   unsigned long long* signal;
 };
+constexpr int kCsBnGridBarInts = 640;  // 2 barriers x (8 group lines + top line) + exit counter
 hipError_t cs_bn_grid_bwd(const CsBnGridBwd& a, hipStream_t stream);
 hipError_t cs_bn_grid_fwd(const CsBnGridFwd& a, hipStream_t stream);
 int cs_bn_grid_fwd_blocks(int B, int H, int W, int C, int pool);

@@ -201,7 +201,7 @@ VggEngine::VggEngine(int64_t Bmax, std::vector<int64_t> desc, std::vector<int64_
   if (const char* e = getenv("CS_DEFER_SIGNALS")) defer_signals_ = atoi(e) != 0;
   if (const char* e = getenv("CS_KEEP_SLABS")) keep_slabs_ = atoi(e) != 0;
   if (const char* e = getenv("CS_FUSE_BN_RED")) fuse_red_ = atoi(e) != 0;
-  grid_bar_ = torch::zeros({8}, fo.dtype(at::kInt));
+  grid_bar_ = torch::zeros({2 * kCsBnGridBarInts}, fo.dtype(at::kInt));  // backward set, forward set
   {
     void* h = nullptr;
     ok(hipHostMalloc(&h, sizeof(int), hipHostMallocMapped), "hipHostMalloc(grid error word)");
@@ -217,7 +217,27 @@ VggEngine::VggEngine(int64_t Bmax, std::vector<int64_t> desc, std::vector<int64_
 
 bool VggEngine::side_wgrad(hipStream_t s) const { return overlap_wgrad_ && !stream_capturing(s); }
 
-void VggEngine::join_side(hipStream_t s) { wg_link_->wait(s); }
+// The link wait orders `s` after the side stream's weight gradients for kernels on this device:
+// each side-stream kernel ends with the device-scope release the next kernel's acquire pairs
+// with. A host-side reader is not covered: gloo copies a CUDA tensor to the host on its own
+// stream, ordered after `s` only, and without a system-scope release on the producing stream a
+// weight gradient can still sit in an L2 the copy does not see (measured round 2: a stale
+// layers.25.weight gradient at world 2, with a link or a plain event join alike; only a host
+// sync of the side stream avoided it). sys_join_ adds an event recorded with
+// hipEventReleaseToSystem on the side stream, which `s` (and so the copy behind it) waits on.
+void VggEngine::join_side(hipStream_t s) {
+  wg_link_->wait(s);
+  if (sys_join_) {
+    ok(hipEventRecord(sys_ev_, side_), "sys-join event record");
+    ok(hipStreamWaitEvent(s, sys_ev_, 0), "sys-join event wait");
+  }
+}
+
+void VggEngine::set_sys_join(bool on) {
+  if (on && sys_ev_ == nullptr)
+    ok(hipEventCreateWithFlags(&sys_ev_, hipEventDisableTiming | hipEventReleaseToSystem), "sys-join event");
+  sys_join_ = on;
+}
 
 std::string VggEngine::link_error() const {
   std::string e = dz_link_->error();
@@ -411,7 +431,7 @@ void VggEngine::forward_train(int64_t B) {
       g.H = g.W = b.H;
       g.C = b.cout;
       g.pool = b.pool;
-      g.bar = reinterpret_cast<unsigned*>(grid_bar_.data_ptr<int>()) + 4;
+      g.bar = reinterpret_cast<unsigned*>(grid_bar_.data_ptr<int>()) + kCsBnGridBarInts;
       g.err = grid_err_;
       ok(cs_bn_grid_fwd(g, s), "bn_grid_fwd");
       continue;
@@ -583,6 +603,10 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
 }
 
 VggEngine::~VggEngine() {
+  if (sys_ev_ != nullptr) {
+    hipEventSynchronize(sys_ev_);
+    hipEventDestroy(sys_ev_);
+  }
   if (grid_err_ != nullptr) {
     hipDeviceSynchronize();
     hipHostFree(grid_err_);

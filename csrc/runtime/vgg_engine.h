@@ -79,6 +79,10 @@ class VggEngine {
   void set_overlap_wgrad(bool on);
   bool side_wgrad(hipStream_t s) const;  // overlap on and `s` not capturing a graph
   void join_side(hipStream_t s);          // `s` waits for every side-stream weight gradient so far
+  // join_side also waits on an event recorded with a SYSTEM-scope release on the side stream:
+  // needed when a consumer outside the device's kernels reads the weight gradients (gloo's
+  // device-to-host copy of an all-reduce issued from Python; see join_side)
+  void set_sys_join(bool on);
   // "" unless a side-stream link wait timed out (device_comm.h StreamLink: bounded waits)
   std::string link_error() const;
   void set_fixup(bool on) { fixup_ = on; }
@@ -167,10 +171,11 @@ class VggEngine {
   int64_t ws_elems_ = 0;
   torch::Tensor counters_;  // split-K tile tickets, [3 * L][tiles_max_] int32
   int64_t tiles_max_ = 1;
-  // in-launch split-K combine where it fits (CS_CONV_FIXUP=1 enables). Off: measured on MI355X
-  // at B=64 every tuned GEMM was slower with it (the last block's serial slab read costs more
-  // than the separate reduce launch it saves): 64.8k vs 69.1k img/s.
-  bool fixup_ = false;
+  // in-launch split-K combine where it fits (the last block of a tile sums the slabs in z order;
+  // CS_CONV_FIXUP=0 restores the separate reduce launch). Round 2 measured it slower (64.8k vs
+  // 69.1k img/s, before the side-stream weight gradients and the retuned tiles); round 3 with the
+  // current step: 96.9k vs 92.3k img/s (100 timed steps each, same box, scripts/ab_bn.sh).
+  bool fixup_ = true;
   bool dual_ = true;
   // CS_BN_FUSED_ROWS; 0 disables. Measured on MI355X at B=64 (img/s): 0 -> 71.46k, 256 (blocks 6-7)
   // -> 71.64k, 1024 -> 69.85k, 4096 -> 63.07k: one block per 16 channels serialises too many rows
@@ -179,10 +184,12 @@ class VggEngine {
   // 0 by measurement (MI355X, B=64): 80.7k img/s vs 77.1k — the channel-sliced blocks of the
   // folded launches stream NHWC rows as 64-B pieces and repeat the finalize in every block,
   // which costs more than the launch they save (e.g. block 0 forward 27.8 us vs 4.9 + 5.2 us)
-  // 2 (default) = one-launch grid-barrier BN forward / backward (bn_grid.hip) for the layers the
-  // single-block fused kernels do not serve: measured per-queue timeline (r3) had 197 us of BN
-  // launches on the critical path with the 2- / 3-launch paths.
-  int bn_path_ = 2;
+  // 2 = one-launch grid-barrier BN forward / backward (bn_grid.hip) for the layers the
+  // single-block fused kernels do not serve. Measured round 3 (profiles/r3_bn_grid_barrier.txt):
+  // the phases alone beat the split launches by 1-2 us per layer, but each in-kernel grid barrier
+  // costs ~10-14 us on MI355X (256 blocks over 8 XCDs; hierarchical arrival + load polling still
+  // ~10 us), so the step is slower: 69.6k (2) vs 90.6k (0) img/s. Kept opt-in.
+  int bn_path_ = 0;
   torch::Tensor grid_bar_;     // zeroed grid-barrier counters of the BN kernels (main stream)
   int* grid_err_ = nullptr;    // host-mapped: a grid barrier timed out
   // a dz-link signal deferred into the next main-stream kernel (StreamLink::defer), or nullptr
@@ -201,6 +208,8 @@ class VggEngine {
   int64_t bn_fused_rows_ = 256;  // horizontal wgrad+dgrad fusion in backward (CS_CONV_DUAL=0 disables)
   hipStream_t side_ = nullptr;
   bool overlap_wgrad_ = false;
+  bool sys_join_ = false;
+  hipEvent_t sys_ev_ = nullptr;
   // per-bucket SGD on opt_ overlapping the backward of the blocks below (CS_SGD_OVERLAP=1 enables).
   // Off: measured on MI355X (B=64, full-step hipGraph) 66.0-66.6k img/s with it vs 81.2k without —
   // the graph's cross-stream fork/join edges cost far more than the 28 us SGD they hide

@@ -30,7 +30,8 @@ pytestmark = [pytest.mark.gpu]
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _train(rank, world, sync, graph, steps, comm="torch", B=16, autotune=False):
+def _train(rank, world, sync, graph, steps, comm="torch", B=16, autotune=False, env=None):
+    os.environ.update(env or {})
     from cs744_pytorch_distributed_tutorial_amd.runtime.engine import NativeTrainer
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -47,7 +48,7 @@ def _train(rank, world, sync, graph, steps, comm="torch", B=16, autotune=False):
            "loss": tr.last_loss(), "buckets": len(tr.bucket_lows), "graph": tr.graph_mode,
            "calls": tr.native_comm.calls() if tr.native_comm is not None else -1,
            "kind": tr.native_comm.kind if tr.native_comm is not None else "none", "eval": ev,
-           "wgrad_side": tr.overlap_wgrad}
+           "wgrad_side": tr.overlap_wgrad, "sys_join": tr.sys_join}
     tr.close()
     return out
 
@@ -70,6 +71,25 @@ def test_ddp_segments_replicas_identical_and_match_eager(gpu):
     assert torch.equal(seg[0]["params"], eag[0]["params"]), (seg[0]["params"] - eag[0]["params"]).abs().max()
     # DDP broadcast_buffers: rank 0's running stats win on every rank
     assert torch.equal(seg[1]["nbt"], seg[0]["nbt"])
+
+
+@pytest.mark.slow
+def test_python_gloo_collectives_with_side_stream_wgrad(gpu):
+    """Round-2 advisor finding: side-stream weight gradients + an all-reduce issued from Python
+    over gloo intermittently read a stale gradient (layers.25.weight at step 3 of 4). gloo moves a
+    CUDA tensor to the host with a copy ordered after the main stream only; the side stream's
+    last kernels had released at device scope, which does not cover that copy. The join of the
+    side stream into the main stream now also waits on a HIP event recorded with a system-scope
+    release (VggEngine::join_side, sys_join on for Python collectives). Eager steps (no graph:
+    the side stream runs every step), several repetitions, bitwise against the serial backward."""
+    ser = run_world(_train, 2, "ddp", "none", 6, "torch", 16, False, {"CS_OVERLAP_WGRAD": "0"})
+    assert not ser[0]["wgrad_side"]
+    for _ in range(3):
+        ovl = run_world(_train, 2, "ddp", "none", 6, "torch", 16, False, {})
+        assert ovl[0]["wgrad_side"] and ovl[0]["sys_join"]
+        for r in range(2):
+            for k in ("params", "mom", "bufs"):
+                assert torch.equal(ovl[r][k], ser[r][k]), (r, k, (ovl[r][k] - ser[r][k]).abs().max())
 
 
 @pytest.mark.slow
