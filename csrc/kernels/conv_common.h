@@ -77,12 +77,15 @@ __device__ void splitk_fixup(const CsConvArgs& a, int tile, int mt, int nt, int 
   const int last = flag[0];
   __syncthreads();  // flag is read by every wave before smem is reused below
   if (!last) return;
+  // the combine runs on the first 256 threads; K-group kernels (KG * 256 threads) keep their
+  // other waves idle here but at every barrier below
   constexpr int CG = BN / 4, RL = 256 / CG, RPT = BM / RL;
+  const bool act = threadIdx.x < 256;
   const int cg = threadIdx.x % CG, rl = threadIdx.x / CG;
   const int m0 = mt * BM, n0 = nt * BN, n = n0 + 4 * cg;
   const int S = nsplit;
   const size_t slab = (size_t)a.M * a.N;
-  const bool nok = n < a.N;
+  const bool nok = act && n < a.N;
   float4 v[RPT];
 #pragma unroll
   for (int k = 0; k < RPT; ++k) v[k] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -122,6 +125,7 @@ __device__ void splitk_fixup(const CsConvArgs& a, int tile, int mt, int nt, int 
     }
   }
   if (MODE == CS_CONV_WGRAD && a.w_oihw) {
+    if (!act) return;  // no barrier below
 #pragma unroll
     for (int k = 0; k < RPT; ++k) {
       const int m = m0 + rl + k * RL;
@@ -149,7 +153,7 @@ __device__ void splitk_fixup(const CsConvArgs& a, int tile, int mt, int nt, int 
 #pragma unroll
     for (int k = 0; k < RPT; ++k)
       if (m0 + rl + k * RL < a.M) { cs.x += v[k].x; cs.y += v[k].y; cs.z += v[k].z; cs.w += v[k].w; }
-    *reinterpret_cast<float4*>(red + rl * BN + 4 * cg) = cs;
+    if (act) *reinterpret_cast<float4*>(red + rl * BN + 4 * cg) = cs;
     __syncthreads();
     if (threadIdx.x < BN) {
       float sum = 0.f;
@@ -165,7 +169,7 @@ __device__ void splitk_fixup(const CsConvArgs& a, int tile, int mt, int nt, int 
         const float dx = v[k].x - mu.x, dy = v[k].y - mu.y, dz = v[k].z - mu.z, dw = v[k].w - mu.w;
         sq.x += dx * dx; sq.y += dy * dy; sq.z += dz * dz; sq.w += dw * dw;
       }
-    *reinterpret_cast<float4*>(red + rl * BN + 4 * cg) = sq;
+    if (act) *reinterpret_cast<float4*>(red + rl * BN + 4 * cg) = sq;
     __syncthreads();
     if (threadIdx.x < BN && n0 + (int)threadIdx.x < a.N) {
       float m2 = 0.f;
@@ -235,9 +239,8 @@ __device__ __forceinline__ void conv_epilogue(const CsConvArgs& a, f32x16 (&acc)
           bstore1(ro, acc[i][j][e], (owner && m < a.M && n < a.N) ? (m * a.N + n) * 4 : kOOB);
         }
       }
-    if constexpr (KG == 1) {
-      if (slab && a.counters != nullptr) splitk_fixup<BM, BN, MODE>(a, tile, mt, nt, nsplit, smem);
-    }
+    // (K-group kernels: every wave reaches this; the combine runs on the first 256 threads)
+    if (slab && a.counters != nullptr) splitk_fixup<BM, BN, MODE>(a, tile, mt, nt, nsplit, smem);
     if (slab || MODE != CS_CONV_FWD) return;
   }
   if constexpr (MODE == CS_CONV_WGRAD) {  // conv0: scatter the padded (tap, ci) columns to OIHW

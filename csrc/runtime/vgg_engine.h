@@ -172,10 +172,11 @@ class VggEngine {
   torch::Tensor counters_;  // split-K tile tickets, [3 * L][tiles_max_] int32
   int64_t tiles_max_ = 1;
   // in-launch split-K combine where it fits (the last block of a tile sums the slabs in z order;
-  // CS_CONV_FIXUP=0 restores the separate reduce launch). Round 2 measured it slower (64.8k vs
-  // 69.1k img/s, before the side-stream weight gradients and the retuned tiles); round 3 with the
-  // current step: 96.9k vs 92.3k img/s (100 timed steps each, same box, scripts/ab_bn.sh).
-  bool fixup_ = true;
+  // CS_CONV_FIXUP=1 enables). Off by measurement: round 2 64.8k vs 69.1k img/s; round 3, same
+  // box, 74.6k / 73.9k (on) vs 78.8k (off). (A first round-3 A/B showed it faster — 96.9k vs
+  // 92.3k — because the K-group kernels skipped the combine altogether: neither the in-launch
+  // combine nor the reduce launch ran, fixed in conv_common.h and covered by the KG fixup tests.)
+  bool fixup_ = false;
   bool dual_ = true;
   // CS_BN_FUSED_ROWS; 0 disables. Measured on MI355X at B=64 (img/s): 0 -> 71.46k, 256 (blocks 6-7)
   // -> 71.64k, 1024 -> 69.85k, 4096 -> 63.07k: one block per 16 channels serialises too many rows

@@ -36,6 +36,8 @@ TILES = [(64, 64, 1, 16), (128, 64, 1, 16), (64, 128, 3, 16), (128, 128, 2, 16),
 VARIANTS = [(False, 0), (True, 0), (False, 1), (True, 1), (False, 2), (False, 3), (False, 4),
             (False, 8), (True, 8), (False, 9), (False, 10), (False, 11), (False, 12),
             (False, 16), (True, 16), (False, 19), (False, 20)]
+# the in-launch combine in K-group kernels (KG * 256 threads; the combine runs on the first 256)
+VARIANTS += [(True, 3), (True, 4), (True, 11), (True, 12), (True, 19), (True, 20)]
 # +32 = bf16 operands, f32 accumulation (the engine's opt-in bf16 mode): bf16-level tolerance
 VARIANTS += [(False, 32), (False, 35), (False, 36)]
 
