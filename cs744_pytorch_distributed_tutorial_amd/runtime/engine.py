@@ -277,21 +277,25 @@ class NativeTrainer:
         self._probe = getattr(self, "_probe", None)
         self.engine = C.VggEngine(self.B, lay.desc(), lay.offs(), lay.buf_offs(), lay.feat, lay.ncls,
                                   self.params, self.grads, self.mom, self.bufs, self.nbt)
-        # weight gradients on a side stream (off the backward's critical chain; bit-identical):
-        # on unless CS_OVERLAP_WGRAD=0, or a communicator runs with too few HIP hardware queues
-        # (their cross-stream waits would serialise behind each other, package __init__), or
-        # under rocprofv3 counter collection, which serialises every dispatch (a side-stream link
-        # wait would spin to its timeout waiting for a signal that cannot run).
-        # Collectives issued from Python (comm="torch": gloo copies each bucket to the host)
-        # additionally need the side stream's results released to SYSTEM scope before that copy:
-        # round 2 measured a stale layers.25.weight gradient at world 2 without it, so the join
-        # then also waits on a system-release event (VggEngine::join_side; CS_SYS_JOIN=0 drops it,
-        # and without it the overlap stays off for Python collectives unless CS_OVERLAP_WGRAD=force).
+        # weight gradients on a side stream (bit-identical to the serial backward): opt-in
+        # (CS_OVERLAP_WGRAD=1). Round 3 measured the serial backward faster on MI355X (B=64, two
+        # boxes, interleaved runs): 81.7-81.8k img/s serial vs 76.3k with the side stream — a
+        # side-stream weight-gradient GEMM takes every CU it lands on (its blocks fill the whole
+        # register file), so the critical chain's next kernel waits for side blocks to drain,
+        # which costs more than the overlap wins (scripts/ab_matrix.sh; profiles/r3_overlap_ab.txt).
+        # With it on, it still needs >= 8 HIP hardware queues when a communicator runs, is off under
+        # rocprofv3 counter collection (which serialises every dispatch: a side-stream link wait
+        # would spin to its timeout), and collectives issued from Python (comm="torch": gloo copies
+        # each bucket to the host) need the side stream's results released to SYSTEM scope before
+        # that copy: round 2 measured a stale layers.25.weight gradient at world 2 without it, so
+        # the join then also waits on a system-release event (VggEngine::join_side; CS_SYS_JOIN=0
+        # drops it, and without it the overlap stays off for Python collectives unless
+        # CS_OVERLAP_WGRAD=force).
         from .. import hw_queues
         python_collectives = world > 1 and self.native_comm is None
         sj = os.environ.get("CS_SYS_JOIN")
         self.sys_join = python_collectives if sj is None else sj != "0"
-        ow = os.environ.get("CS_OVERLAP_WGRAD", "1")
+        ow = os.environ.get("CS_OVERLAP_WGRAD", "0")
         self.overlap_wgrad = ow != "0" and (ow == "force" or self.sys_join or not python_collectives) and (
             self.native_comm is None or hw_queues() >= 8) and not self._counters
         self.engine.set_overlap_wgrad(self.overlap_wgrad)

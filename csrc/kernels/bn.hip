@@ -243,7 +243,11 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
                                                               const float* __restrict__ gamma,
                                                               const float* __restrict__ invstd,
                                                               float* __restrict__ dgamma, float* __restrict__ dbeta,
-                                                              float* __restrict__ dbias, float* __restrict__ coef) {
+                                                              float* __restrict__ dbias, float* __restrict__ coef,
+                                                              unsigned long long* __restrict__ signal) {
+  // a deferred stream-link signal (the kernels before this launch on its stream completed)
+  if (signal != nullptr && blockIdx.x == 0 && threadIdx.x == 0)
+    __hip_atomic_fetch_add(signal, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int lane = threadIdx.x & 63;
   const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
   float sg = 0.f, sgx = 0.f, sx = 0.f;
@@ -688,12 +692,12 @@ hipError_t cs_bn_bwd(const float* y, const float* G, int B, int H, int W, int C,
 hipError_t cs_bn_bwd_tail(const float* y, const float* G, int B, int H, int W, int C, int pool, const float* scale,
                           const float* shift, const float* mean, const float* invstd, const float* gamma,
                           const float* part, int P, float* coef, float* dgamma, float* dbeta, float* dbias, float* dz,
-                          hipStream_t stream, int gslabs, int64_t gstride) {
+                          hipStream_t stream, int gslabs, int64_t gstride, unsigned long long* signal) {
   if (C % 4 != 0 || C > 1024 || (pool && ((H | W) & 1)) || gslabs < 1 || P < 1) return hipErrorInvalidValue;
   const int M = B * H * W;
   const int rows = 256 / (C / 4);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 3) / 4), dim3(256), 0, stream, part, P, C, M, gamma, invstd,
-                     dgamma, dbeta, dbias, coef);
+                     dgamma, dbeta, dbias, coef, signal);
   // the apply pass is sized for bandwidth, independent of the reduce's P
   const int units = pool ? B * (H / 2) * (W / 2) : B * H * W;
   int blocks = (units + rows - 1) / rows;

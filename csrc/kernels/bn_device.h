@@ -89,6 +89,88 @@ __device__ __forceinline__ void bwd_visit(const float* __restrict__ y, const flo
 }
 
 
+// The same per-element visit for ONE channel of one incoming-gradient value g, when the
+// gradient is still in the registers of the GEMM (or split-K combine) that produced it: i0 is
+// the element's index in y (the window's first element with pooling), C the channel count and
+// W2 y's width. Decisions and sums are bwd_visit's, so the partials only differ from the
+// standalone reduce pass in their (fixed) summation order.
+template <bool POOL>
+__device__ __forceinline__ void bwd_point(const float* __restrict__ y, size_t i0, int C, int W2, float g, float sc,
+                                          float sh, float mu, float is, float& s0, float& s1, float& s2) {
+  constexpr int NP = POOL ? 4 : 1;
+  float yv[NP];
+  yv[0] = y[i0];
+  if (POOL) {
+    yv[1 % NP] = y[i0 + C];
+    yv[2 % NP] = y[i0 + (size_t)W2 * C];
+    yv[3 % NP] = y[i0 + (size_t)W2 * C + C];
+  }
+  float z[NP];
+  int am = 0;
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    z[p] = fmaxf(yv[p] * sc + sh, 0.f);
+    if (p > 0 && z[p] > z[am]) am = p;
+  }
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const float gp = (p == am && z[p] > 0.f) ? g : 0.f;
+    const float xh = (yv[p] - mu) * is;
+    s0 += gp;
+    s1 += gp * xh;
+    s2 += xh;
+  }
+}
+
+__device__ __forceinline__ float f4get(const float4& v, int q) {
+  return q == 0 ? v.x : (q == 1 ? v.y : (q == 2 ? v.z : v.w));
+}
+
+// bwd_point for 4 consecutive channels (i0 16-B aligned): one float4 load of y per window
+// position, the per-channel BN vectors as float4; s[k][q] += the k-th term of channel q
+template <bool POOL>
+__device__ __forceinline__ void bwd_point4(const float* __restrict__ y, size_t i0, int C, int W2, float4 g,
+                                           float4 sc, float4 sh, float4 mu, float4 is, float (&s)[3][4]) {
+  constexpr int NP = POOL ? 4 : 1;
+  float4 yv[NP];
+  yv[0] = *reinterpret_cast<const float4*>(y + i0);
+  if (POOL) {
+    yv[1 % NP] = *reinterpret_cast<const float4*>(y + i0 + C);
+    yv[2 % NP] = *reinterpret_cast<const float4*>(y + i0 + (size_t)W2 * C);
+    yv[3 % NP] = *reinterpret_cast<const float4*>(y + i0 + (size_t)W2 * C + C);
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float scq = f4get(sc, q), shq = f4get(sh, q), muq = f4get(mu, q), isq = f4get(is, q), gq = f4get(g, q);
+    float yq[NP], z[NP];
+    int am = 0;
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      yq[p] = f4get(yv[p], q);
+      z[p] = fmaxf(yq[p] * scq + shq, 0.f);
+      if (p > 0 && z[p] > z[am]) am = p;
+    }
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      const float gp = (p == am && z[p] > 0.f) ? gq : 0.f;
+      const float xh = (yq[p] - muq) * isq;
+      s[0][q] += gp;
+      s[1][q] += gp * xh;
+      s[2][q] += xh;
+    }
+  }
+}
+
+// index in y (full resolution, NHWC, C channels) of output-gradient row m's first element;
+// the gradient rows are pixels of an H x W (= y's size halved with pooling) image
+template <bool POOL>
+__device__ __forceinline__ size_t bwd_point_index(int m, int n, int lgH, int lgW, int C) {
+  if (!POOL) return (size_t)m * C + n;
+  const int W = 1 << lgW, H = 1 << lgH;
+  const int wo = m & (W - 1), ho = (m >> lgW) & (H - 1), b = m >> (lgW + lgH);
+  return (((size_t)b * 2 * H + 2 * ho) * 2 * W + 2 * wo) * C + n;
+}
+
 // Partials of block `blk` of `nblk` (part [nblk][C][3]); 256 working threads (more are idle),
 // red = rows * C * 3 floats of LDS (cs_bn_red_lds)
 template <bool POOL>

@@ -180,6 +180,83 @@ __device__ void splitk_fixup(const CsConvArgs& a, int tile, int mt, int nt, int 
   }
 }
 
+// DGRAD epilogue with CsConvArgs::ered: this tile's BN-backward partial sums of the block below
+// (bn.hip's reduce pass, per channel: sum g, sum g*xhat, sum xhat over its full-resolution
+// elements) from the output gradient values of K-group 0. The tile goes through LDS first
+// (dgrad_bn_stage, inline), then a NON-inlined pass gathers y and sums: it runs after the
+// accumulators are dead and gets its own register allocation, so the main loop's does not
+// grow (inlined, it cost the 1024-thread tiles VGPR spills). Every wave of the block shares
+// the gathers: thread t owns column t % BN and every (NT/BN)-th row; the row groups' sums are
+// added in a fixed order -> ered.part [mt][N][3]. LDS: BM x (BN + 4) floats (launch_k sizes
+// the launch for it). Every thread of the block takes part (barriers inside).
+template <int BM, int BN>
+__device__ __forceinline__ void dgrad_bn_stage(const f32x16 (&acc)[BM / 64][BN / 64], bool owner, float* smem) {
+  constexpr int RM = BM / 64, RN = BN / 64, WM = BM / 2, WN = BN / 2, TP = BN + 4;
+  const int lane = threadIdx.x & 63, wsp = (threadIdx.x >> 6) & 3;
+  const int wm = wsp >> 1, wn = wsp & 1, r = lane & 31, hh = lane >> 5;
+  if (owner) {
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+      for (int j = 0; j < RN; ++j)
+#pragma unroll
+        for (int el = 0; el < 16; ++el)
+          smem[(wm * WM + i * 32 + (el & 3) + 8 * (el >> 2) + 4 * hh) * TP + wn * WN + j * 32 + r] = acc[i][j][el];
+  }
+  __syncthreads();
+}
+
+template <int BM, int BN, int NT, bool POOL>
+__device__ __noinline__ void dgrad_bn_partials(const float* __restrict__ y, const float* __restrict__ bnv_scale,
+                                               const float* __restrict__ bnv_shift, const float* __restrict__ bnv_mean,
+                                               const float* __restrict__ bnv_invstd, float* __restrict__ part, int M,
+                                               int N, int lgH, int lgW, int mt, int m0, int n0, float* img) {
+  // thread: channel quad cq (float4 loads of the image, y and the BN vectors), every RG-th row
+  constexpr int TP = BN + 4, CQ = BN / 4, RG = NT / CQ, NW = NT / 64;
+  static_assert(NT % CQ == 0 && 64 % CQ == 0 && NW * BN * 3 <= BM * TP, "wave partials must fit the tile image");
+  const int tid = threadIdx.x, lane = tid & 63, cq = tid % CQ, rg = tid / CQ, n = n0 + 4 * cq;
+  const bool nok = n < N;
+  const int nc = nok ? n : 0;
+  const float4 sc = *reinterpret_cast<const float4*>(bnv_scale + nc), sh = *reinterpret_cast<const float4*>(bnv_shift + nc);
+  const float4 mu = *reinterpret_cast<const float4*>(bnv_mean + nc), is = *reinterpret_cast<const float4*>(bnv_invstd + nc);
+  float s[3][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll 2
+  for (int row = rg; row < BM; row += RG) {
+    const int m = m0 + row;
+    const bool ok = nok && m < M;
+    float t[3][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    cs_bn::bwd_point4<POOL>(y, cs_bn::bwd_point_index<POOL>(ok ? m : 0, nc, lgH, lgW, N), N, 2 << lgW,
+                            *reinterpret_cast<const float4*>(img + row * TP + 4 * cq), sc, sh, mu, is, t);
+    if (ok)
+#pragma unroll
+      for (int k = 0; k < 3; ++k)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) s[k][q] += t[k][q];
+  }
+  // the wave's row groups (lane / CQ), then the waves in order
+#pragma unroll
+  for (int off = CQ; off < 64; off <<= 1)
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) s[k][q] += __shfl_xor(s[k][q], off, 64);
+  __syncthreads();  // every image read done: the wave sums reuse the space
+  if (lane < CQ)
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) img[((tid >> 6) * BN + 4 * cq + q) * 3 + k] = s[k][q];
+  __syncthreads();
+  if (tid < BN && n0 + tid < N) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      float t = 0.f;
+      for (int w = 0; w < NW; ++w) t += img[(w * BN + tid) * 3 + k];
+      part[((size_t)mt * N + n0 + tid) * 3 + k] = t;
+    }
+  }
+}
+
 // Epilogue of one output tile: `acc` holds each spatial wave's (BM/2)x(BN/2) partial sums of
 // this block's K range (K-group kg's share when KG > 1). The caller's main loop has ended
 // on a barrier (every wave's LDS reads done): smem is free.
@@ -241,6 +318,18 @@ __device__ __forceinline__ void conv_epilogue(const CsConvArgs& a, f32x16 (&acc)
       }
     // (K-group kernels: every wave reaches this; the combine runs on the first 256 threads)
     if (slab && a.counters != nullptr) splitk_fixup<BM, BN, MODE>(a, tile, mt, nt, nsplit, smem);
+    if constexpr (MODE == CS_CONV_DGRAD) {
+      if (!slab && a.ered.part != nullptr) {  // (split-K: the combine launch takes them)
+        dgrad_bn_stage<BM, BN>(acc, owner, smem);
+        const CsBnRed& e = a.ered;
+        if (e.pool)
+          dgrad_bn_partials<BM, BN, 256 * KG, true>(e.y, e.scale, e.shift, e.mean, e.invstd, e.part, a.M, a.N, a.lgH,
+                                                    a.lgW, mt, m0, n0, smem);
+        else
+          dgrad_bn_partials<BM, BN, 256 * KG, false>(e.y, e.scale, e.shift, e.mean, e.invstd, e.part, a.M, a.N, a.lgH,
+                                                     a.lgW, mt, m0, n0, smem);
+      }
+    }
     if (slab || MODE != CS_CONV_FWD) return;
   }
   if constexpr (MODE == CS_CONV_WGRAD) {  // conv0: scatter the padded (tap, ci) columns to OIHW

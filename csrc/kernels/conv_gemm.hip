@@ -837,6 +837,35 @@ __device__ __forceinline__ void splitk_reduce_body(const CsConvArgs& a, int mode
       *reinterpret_cast<float4*>(a.out + (size_t)m * a.N + n) = acc;
     }
   }
+  if (mode == CS_CONV_DGRAD && a.ered.part != nullptr) {
+    // BN-backward partials of the block below over this 16-row tile (conv_common.h
+    // dgrad_bn_partials): each thread's 4 channels at its row, then the 16 rows in order
+    const CsBnRed& e = a.ered;
+    float s[3][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    if (in) {
+      const float4 sc = *reinterpret_cast<const float4*>(e.scale + n), sh = *reinterpret_cast<const float4*>(e.shift + n);
+      const float4 mu = *reinterpret_cast<const float4*>(e.mean + n), is = *reinterpret_cast<const float4*>(e.invstd + n);
+      if (e.pool)
+        cs_bn::bwd_point4<true>(e.y, cs_bn::bwd_point_index<true>(m, n, a.lgH, a.lgW, a.N), a.N, 2 * a.W, acc, sc, sh,
+                                mu, is, s);
+      else
+        cs_bn::bwd_point4<false>(e.y, cs_bn::bwd_point_index<false>(m, n, a.lgH, a.lgW, a.N), a.N, 2 * a.W, acc, sc,
+                                 sh, mu, is, s);
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) red[ty][4 * tx + q] = s[k][q];
+      __syncthreads();
+      if (threadIdx.x < 64 && n0 + (int)threadIdx.x < a.N) {
+        float t = 0.f;
+        for (int r = 0; r < kRedRows; ++r) t += red[r][threadIdx.x];
+        e.part[((size_t)mt * a.N + n0 + threadIdx.x) * 3 + k] = t;
+      }
+      __syncthreads();
+    }
+    return;
+  }
   if (mode != CS_CONV_FWD || a.stats == nullptr) return;
   // per-column (mean, M2) of this 16-row tile (two-pass inside the tile: robust)
   const int cnt = (a.M - m0) < kRedRows ? (a.M - m0) : kRedRows;
@@ -917,7 +946,8 @@ int conv_sched() {
 
 template <int BM, int BN, int MODE, int BK, int SCHED, bool C4, int GL, int KG = 1>
 hipError_t launch_k(dim3 grid, size_t lds, hipStream_t stream, const CsConvArgs& a) {
-  const size_t l = a.red.P > 0 ? std::max(lds, cs_bn_red_lds(a.red.C)) : lds;
+  size_t l = a.red.P > 0 ? std::max(lds, cs_bn_red_lds(a.red.C)) : lds;
+  if (MODE == CS_CONV_DGRAD && a.ered.part != nullptr) l = std::max(l, (size_t)BM * (BN + 4) * sizeof(float));
   hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, MODE, BK, SCHED, C4, GL, KG>), grid, dim3(256 * KG), l, stream, a);
   return hipGetLastError();
 }
@@ -1142,6 +1172,10 @@ int cs_conv_stat_rows(int K, int bm, int bn, int bk, int splits, bool counters) 
   return (s == 1 || (counters && cs_conv_fixup_ok(s, bm, bn))) ? bm : CS_SPLITK_STAT_ROWS;
 }
 
+int cs_conv_ered_rows(int K, int bm, int bk, int splits) {
+  return cs_conv_effective_splits(K, bk, splits) == 1 ? bm : CS_SPLITK_STAT_ROWS;
+}
+
 int cs_conv_effective_splits(int K, int bk, int splits) {
   const int ks = (K + bk - 1) / bk;
   int s = splits < 1 ? 1 : (splits > ks ? ks : splits);
@@ -1178,8 +1212,10 @@ hipError_t cs_conv_gemm_dual(CsConvArgs wg, int wbk, int wsplits, CsConvArgs dg,
   if (s1 > 1 && s2 > 1 && wg.ws == dg.ws) return hipErrorInvalidValue;  // slabs must not alias
   const int nt1 = ((wg.M + 63) / 64) * ((wg.N + 63) / 64), nt2 = ((dg.M + 63) / 64) * ((dg.N + 63) / 64);
   const int nb1 = nt1 * s1, nb = nb1 + nt2 * s2;
-  const size_t lds = 2 * (size_t)std::max(Tile<64, 64, CS_CONV_WGRAD, 32>::STAGE, Tile<64, 64, CS_CONV_DGRAD, 32>::STAGE) *
-                     sizeof(float);
+  // (>= the 64 x 68 float tile image of the dgrad epilogue's BN partials, CsConvArgs::ered)
+  const size_t lds = std::max<size_t>(
+      2 * (size_t)std::max(Tile<64, 64, CS_CONV_WGRAD, 32>::STAGE, Tile<64, 64, CS_CONV_DGRAD, 32>::STAGE) * sizeof(float),
+      64 * 68 * sizeof(float));
   if (stage == CS_STAGE_REGS) {
 #define CS_DUAL(B1, B2)                                                                                      \
   if (wbk == B1 && dbk == B2)                                                                                \
@@ -1224,7 +1260,8 @@ hipError_t cs_conv_gemm(CsConvArgs a, int mode, int bm, int bn, int bk, int spli
   if (!cs_conv_stage_ok(stage, bm, bn, bk, a.w_oihw && mode == CS_CONV_FWD)) return hipErrorInvalidValue;
   splits = prep_gemm(a, mode, bk, splits);
   if (splits < 0) return hipErrorInvalidValue;
-  if (!cs_conv_fixup_ok(splits, bm, bn)) a.counters = nullptr;
+  // (BN-backward partials from a split-K data gradient come out of the combine launch)
+  if (!cs_conv_fixup_ok(splits, bm, bn) || a.ered.part != nullptr) a.counters = nullptr;
 #define CS_DISPATCH(BM_, BN_, BK_)                                                                       \
   if (bm == BM_ && bn == BN_ && bk == BK_) {                                                             \
     hipError_t e;                                                                                        \
@@ -1232,7 +1269,7 @@ hipError_t cs_conv_gemm(CsConvArgs a, int mode, int bm, int bn, int bk, int spli
     else if (mode == CS_CONV_DGRAD) e = launch_gemm<BM_, BN_, CS_CONV_DGRAD, BK_>(a, splits, stage, stream); \
     else e = launch_gemm<BM_, BN_, CS_CONV_WGRAD, BK_>(a, splits, stage, stream);                       \
     if (e != hipSuccess || splits == 1 || a.counters != nullptr) return e;                               \
-    if (a.keep_slabs && splits <= 2 * kFold) return e; /* the consumer sums the slabs */                  \
+    if (a.keep_slabs && splits <= 2 * kFold && a.ered.part == nullptr) return e; /* consumer sums slabs */ \
     return launch_reduce(a, mode, splits, stream);                                                       \
   }
   CS_DISPATCH(64, 64, 16)

@@ -70,6 +70,12 @@ struct CsConvArgs {
   // extra blocks after the GEMM tiles (dispatched last, they fill the GEMM's tail): an
   // independent BN-backward reduce (the block below's), red.P blocks; red.P == 0: none
   CsBnRed red;
+  // DGRAD: the BN-backward partial sums of the block below (whose output gradient this GEMM
+  // produces), taken from the finished output values where they are still in registers — the
+  // GEMM epilogue, or the split-K combine — instead of a separate reduce pass over G and y.
+  // Uses y, scale, shift, mean, invstd, pool and part ([row tiles][N][3], row tiles of BM rows,
+  // or CS_SPLITK_STAT_ROWS behind the split-K combine: cs_conv_ered_rows); part == null: none
+  CsBnRed ered;
   // pre-split operands (conv_xp.hip): P3 bf16 chunks [n/8][3][8] (h, m, l of every 8 elements)
   const uint16_t* x3;   // FWD / WGRAD: split conv input
   const uint16_t* w3;   // FWD / DGRAD: split OHWI weights
@@ -123,6 +129,10 @@ int cs_conv_effective_splits(int K, int bk, int splits);
 bool cs_conv_fixup_ok(int splits, int bm, int bn);
 // FWD statistics tile height for a launch (bm, or CS_SPLITK_STAT_ROWS behind the reduce kernel)
 int cs_conv_stat_rows(int K, int bm, int bn, int bk, int splits, bool counters);
+// rows per BN-backward partial of a DGRAD launch carrying `ered` (bm, or CS_SPLITK_STAT_ROWS
+// when split-K: the combine launch computes them; such launches never use the in-launch combine
+// or kept slabs)
+int cs_conv_ered_rows(int K, int bm, int bk, int splits);
 
 // pre-split ("XP") conv GEMMs (conv_xp.hip): operands as three bf16 planes (x = h + m + l),
 // fp32-accurate six-product split-bf16 MFMA maths, LDS-DMA ring staging. bm, bn in {64, 128},
@@ -147,11 +157,14 @@ int cs_bn_bwd_blocks(int B, int H, int W, int C, int pool);
 // LDS bytes the BN-backward reduce body needs (C channels)
 inline size_t cs_bn_red_lds(int C) { return (size_t)(256 / (C / 4)) * C * 3 * sizeof(float); }
 // finalize + apply of the BN backward when the reduce already ran (part from P blocks, e.g.
-// appended to the weight-gradient GEMM launch of the block above)
+// appended to the weight-gradient GEMM launch of the block above, or P row tiles of the data-
+// gradient GEMM that produced G: CsConvArgs::ered); signal: optional stream-link counter the
+// finalize launch bumps when it starts
 hipError_t cs_bn_bwd_tail(const float* y, const float* G, int B, int H, int W, int C, int pool, const float* scale,
                           const float* shift, const float* mean, const float* invstd, const float* gamma,
                           const float* part, int P, float* coef, float* dgamma, float* dbeta, float* dbias, float* dz,
-                          hipStream_t stream, int gslabs = 1, int64_t gstride = 0);
+                          hipStream_t stream, int gslabs = 1, int64_t gstride = 0,
+                          unsigned long long* signal = nullptr);
 // One-launch BN (bn_grid.hip): P <= 256 blocks (all resident) whose phases meet at in-kernel grid
 // barriers — backward: partials | per-channel finalize | dZ apply (replaces cs_bn_bwd's three
 // launches, same partials bit for bit); forward: finalize from the conv epilogue's tile partials |

@@ -44,6 +44,9 @@ class DeviceComm {
   virtual void abort() {}
   // collectives issued so far (tests / fault injection)
   virtual int64_t calls() const { return 0; }
+  // the host waits inside a collective for the GPU to reach it (StagedComm's host staging):
+  // every stream-link signal must be launched before one is issued
+  virtual bool host_blocking() const { return false; }
 };
 
 // whether `s` is being captured into a graph (links fall back to events there)

@@ -25,6 +25,7 @@ namespace cs {
 
 class StagedComm final : public DeviceComm {
  public:
+  bool host_blocking() const override { return true; }
   // group_name: a registered c10d group (torch.distributed group.group_name)
   StagedComm(const std::string& group_name, int device);
   ~StagedComm() override;

@@ -1,6 +1,7 @@
 #include <stdlib.h>
 
 #include <stdexcept>
+#include <vector>
 
 #include "kernels/launchers.h"
 #include "runtime/device_comm.h"
@@ -93,13 +94,40 @@ std::string StreamLink::error() const {
 }
 
 namespace {
+// CS_SIDE_CU_SHARE = m (opt-in, default 0): the side stream may only use (m-1)/m of the CUs — one
+// block of 8 consecutive CU-mask bits in every 8*m is left out, which is the same share of
+// every XCD whether the driver numbers CUs XCD by XCD or interleaved (m = 4: 64 of 256 CUs).
+// Why: a side-stream weight-gradient GEMM fills every CU it lands on (1024 threads x 128
+// VGPRs, or 512 x 256: the whole register file), so a main-stream kernel of the critical chain
+// (the BN backward, the next data gradient) waits for side blocks to drain before it can
+// start at all. Reserved CUs keep the critical chain moving. 0 or 1: no mask.
+int side_cu_share() {
+  static const int m = [] {
+    const char* e = getenv("CS_SIDE_CU_SHARE");
+    return e ? atoi(e) : 0;
+  }();
+  return m;
+}
+
 // a non-blocking stream at the lowest (or highest) priority, bound to a hardware queue by one
-// tiny fill (queues are taken when a stream first runs work)
-hipStream_t bound_stream(bool high) {
+// tiny fill (queues are taken when a stream first runs work); masked: on a CU subset
+// (side_cu_share) at the default priority (a CU-masked stream takes no priority)
+hipStream_t bound_stream(bool high, bool masked = false) {
   int least = 0, greatest = 0;
   hip_ok(hipDeviceGetStreamPriorityRange(&least, &greatest), "stream priorities");
   hipStream_t s = nullptr;
-  hip_ok(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, high ? greatest : least), "reserved stream");
+  const int m = masked ? side_cu_share() : 0;
+  if (m > 1) {
+    int dev = 0, cus = 0;
+    hip_ok(hipGetDevice(&dev), "device");
+    hip_ok(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev), "CU count");
+    std::vector<uint32_t> mask((cus + 31) / 32, 0u);
+    for (int i = 0; i < cus; ++i)
+      if ((i / 8) % m != m - 1) mask[i / 32] |= 1u << (i % 32);
+    hip_ok(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()), "CU-masked side stream");
+  } else {
+    hip_ok(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, high ? greatest : least), "reserved stream");
+  }
   void* scratch = nullptr;
   hip_ok(hipMalloc(&scratch, 256), "reserved stream scratch");
   hip_ok(hipMemsetAsync(scratch, 0, 256, s), "bind reserved stream");
@@ -110,7 +138,7 @@ hipStream_t bound_stream(bool high) {
 }  // namespace
 
 hipStream_t reserved_side_stream() {
-  static hipStream_t side = bound_stream(false);
+  static hipStream_t side = bound_stream(false, true);
   return side;
 }
 

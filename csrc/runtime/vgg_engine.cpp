@@ -136,6 +136,8 @@ VggEngine::VggEngine(int64_t Bmax, std::vector<int64_t> desc, std::vector<int64_
     dzmax = std::max(dzmax, pix * b.cout);
     partmax = std::max<int64_t>(partmax, (int64_t)cs_bn_bwd_blocks(Bmax, b.H, b.H, b.cout, b.pool) * b.cout * 3);
     partmax = std::max<int64_t>(partmax, (int64_t)cs_bn_bwd_chunks(Bmax, b.H, b.H, b.cout, b.pool) * b.cout * 3);
+    // row-tile partials of block l-1 out of block l's data gradient (>= CS_SPLITK_STAT_ROWS rows each)
+    if (l > 0) partmax = std::max<int64_t>(partmax, cdiv(pix, CS_SPLITK_STAT_ROWS) * b.cin * 3);
     cmax = std::max<int64_t>(cmax, b.cout);
     for (int m = 0; m < 3; ++m) b.tile[m] = default_tile(b, m, Bmax);
   }
@@ -201,6 +203,7 @@ VggEngine::VggEngine(int64_t Bmax, std::vector<int64_t> desc, std::vector<int64_
   if (const char* e = getenv("CS_DEFER_SIGNALS")) defer_signals_ = atoi(e) != 0;
   if (const char* e = getenv("CS_KEEP_SLABS")) keep_slabs_ = atoi(e) != 0;
   if (const char* e = getenv("CS_FUSE_BN_RED")) fuse_red_ = atoi(e) != 0;
+  if (const char* e = getenv("CS_BN_EPI_RED")) epi_red_ = atoi(e) != 0;
   grid_bar_ = torch::zeros({2 * kCsBnGridBarInts}, fo.dtype(at::kInt));  // backward set, forward set
   {
     void* h = nullptr;
@@ -226,6 +229,7 @@ bool VggEngine::side_wgrad(hipStream_t s) const { return overlap_wgrad_ && !stre
 // sync of the side stream avoided it). sys_join_ adds an event recorded with
 // hipEventReleaseToSystem on the side stream, which `s` (and so the copy behind it) waits on.
 void VggEngine::join_side(hipStream_t s) {
+  flush_signal(s);  // the side stream may be waiting for it: never wait on side before it is out
   wg_link_->wait(s);
   if (sys_join_) {
     ok(hipEventRecord(sys_ev_, side_), "sys-join event record");
@@ -338,11 +342,15 @@ void VggEngine::set_perm(torch::Tensor perm) {
 }
 
 void VggEngine::conv(int l, int mode, int B, const ConvTile& t, hipStream_t s, bool with_stats, float* ws,
-                     float* dz, bool keep_slabs, const CsBnRed* red) {
+                     float* dz, bool keep_slabs, const CsBnRed* red, const CsBnRed* ered) {
   VggBlock& b = blocks_[l];
   CsConvArgs a = conv_args(l, mode, B, with_stats, ws, dz);
   a.keep_slabs = keep_slabs ? 1 : 0;
   if (red != nullptr) a.red = *red;
+  if (ered != nullptr) {
+    TORCH_CHECK(mode == CS_CONV_DGRAD && !keep_slabs, "VggEngine: BN partials ride a data gradient without kept slabs");
+    a.ered = *ered;
+  }
   const Dims d = dims(b, mode, B);
   const int sp = eff_splits(d.K, t.splits, t.bk);
   TORCH_CHECK(sp == 1 || (int64_t)sp * d.M * d.N <= ws_elems_, "VggEngine: split-K workspace too small");
@@ -361,12 +369,40 @@ bool VggEngine::dual_ok(int l) const {
   return w.bm == 64 && w.bn == 64 && d.bm == 64 && d.bn == 64 && cs_conv_dual_ok(w.stage, w.bk, d.stage, d.bk);
 }
 
-void VggEngine::conv_dual(int l, int B, hipStream_t s, float* dz) {
+void VggEngine::conv_dual(int l, int B, hipStream_t s, float* dz, const CsBnRed* ered) {
   const ConvTile& w = blocks_[l].tile[CS_CONV_WGRAD];
   const ConvTile& d = blocks_[l].tile[CS_CONV_DGRAD];
   CsConvArgs wa = conv_args(l, CS_CONV_WGRAD, B, false, ws_side_.data_ptr<float>(), dz);
   CsConvArgs da = conv_args(l, CS_CONV_DGRAD, B, false, nullptr, dz);
+  if (ered != nullptr) da.ered = *ered;
   ok(cs_conv_gemm_dual(wa, w.bk, w.splits, da, d.bk, d.splits, s, w.stage), "conv_gemm_dual");
+}
+
+bool VggEngine::epi_red_ok(int l, int64_t B) const {
+  return epi_red_ && bn_path_ == 0 && !fixup_ && !keep_slabs_ && l > 0 && !bn_fused(l - 1, B);
+}
+
+CsBnRed VggEngine::epi_red_args(int l, int B) {
+  VggBlock& c = blocks_[l - 1];
+  float* cb = c.bn.data_ptr<float>();
+  CsBnRed r{};
+  r.y = c.y.data_ptr<float>();
+  r.scale = cb;
+  r.shift = cb + c.cout;
+  r.mean = cb + 2 * c.cout;
+  r.invstd = cb + 3 * c.cout;
+  r.part = bn_part_.data_ptr<float>();
+  r.B = B;
+  r.H = r.W = (int)c.H;
+  r.C = (int)c.cout;
+  r.pool = c.pool;
+  r.gslabs = 1;
+  // P = row tiles of block l's data gradient (M = B * H_l * W_l rows)
+  const ConvTile& t = blocks_[l].tile[CS_CONV_DGRAD];
+  const Dims d = dims(blocks_[l], CS_CONV_DGRAD, B);
+  r.P = (int)cdiv(d.M, cs_conv_ered_rows((int)d.K, t.bm, t.bk, t.splits));
+  TORCH_CHECK((int64_t)r.P * c.cout * 3 <= bn_part_.numel(), "VggEngine: BN partial buffer");
+  return r;
 }
 
 void VggEngine::forward_train(int64_t B) {
@@ -376,6 +412,7 @@ void VggEngine::forward_train(int64_t B) {
   const int L = (int)blocks_.size();
   g_slabs_ = 1;  // the head writes the top block's gradient to gbuf_
   red_pending_ = -1;
+  flush_signal(s);
   // one launch: sampler index (device cursor into the epoch permutation, or idx_ when no
   // permutation is set), label gather, crop/flip/normalize into block 0's NHWC input
   const bool use_perm = perm_len_ > 0;
@@ -493,12 +530,15 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
       g.signal = pending_sig_;  // the previous block's dz-link signal rides this launch
       pending_sig_ = nullptr;
       ok(cs_bn_grid_bwd(g, s), "bn_grid_bwd");
-    } else if (red_pending_ == l) {  // the partial sums already ran inside the weight-gradient launch above
-      flush_signal(s);
+    } else if (red_pending_ == l) {
+      // the partial sums already ran: in block l+1's data-gradient GEMM (epilogue / split-K
+      // combine) or inside the weight-gradient launch above; the pending signal rides the finalize
       ok(cs_bn_bwd_tail(b.y.data_ptr<float>(), Gin, (int)B, b.H, b.H, b.cout, b.pool, bn, bn + b.cout,
                         bn + 2 * b.cout, bn + 3 * b.cout, P(b.g_off), bn_part_.data_ptr<float>(), red_P_,
-                        bn_coef_.data_ptr<float>(), G(b.g_off), G(b.be_off), G(b.b_off), dz, s, gs, g_stride_),
+                        bn_coef_.data_ptr<float>(), G(b.g_off), G(b.be_off), G(b.b_off), dz, s, gs, g_stride_,
+                        pending_sig_),
          "bn_bwd_tail");
+      pending_sig_ = nullptr;
     } else if (bn_fused(l, B)) {  // reduce + finalize + apply in one launch
       ok(cs_bn_fused_bwd(b.y.data_ptr<float>(), Gin, (int)B, b.H, b.H, b.cout, b.pool, bn, P(b.g_off),
                          bn_coef_.data_ptr<float>(), G(b.g_off), G(b.be_off), G(b.b_off), dz, s, gs, g_stride_,
@@ -519,11 +559,19 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
     }
     g_slabs_ = 1;
     red_pending_ = -1;
+    // block l-1's BN partials out of this block's data gradient (no reduce launch of their own)
+    const bool er = epi_red_ok(l, B);
+    CsBnRed erv{};
+    if (er) erv = epi_red_args(l, (int)B);
     if (!ovl && dual_ok(l)) {  // wgrad + dgrad in one launch
-      conv_dual(l, (int)B, s, dz);
+      conv_dual(l, (int)B, s, dz, er ? &erv : nullptr);
+      if (er) {
+        red_pending_ = l - 1;
+        red_P_ = erv.P;
+      }
       continue;
     }
-    if (fuse_red_ && !ovl && bn_path_ == 0 && l > 0 && !bn_fused(l - 1, B)) {
+    if (!er && fuse_red_ && !ovl && bn_path_ == 0 && l > 0 && !bn_fused(l - 1, B)) {
       // dgrad(l) first, then wgrad(l) carrying block l-1's BN partial-sum pass
       const ConvTile& t = b.tile[CS_CONV_DGRAD];
       const Dims d = dims(b, CS_CONV_DGRAD, B);
@@ -570,11 +618,15 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
       const ConvTile& t = b.tile[CS_CONV_DGRAD];
       const Dims d = dims(b, CS_CONV_DGRAD, B);
       const int sp = eff_splits(d.K, t.splits, t.bk);
-      const bool keep = keep_slabs_ && bn_path_ != 1 && sp > 1 && sp <= 32;
-      conv(l, CS_CONV_DGRAD, (int)B, t, s, false, nullptr, dz, keep);
+      const bool keep = !er && keep_slabs_ && bn_path_ != 1 && sp > 1 && sp <= 32;
+      conv(l, CS_CONV_DGRAD, (int)B, t, s, false, nullptr, dz, keep, nullptr, er ? &erv : nullptr);
       if (keep) {
         g_slabs_ = sp;
         g_stride_ = d.M * d.N;
+      }
+      if (er) {
+        red_pending_ = l - 1;
+        red_P_ = erv.P;
       }
     }
     if (ovl && wgrad_after_dgrad_ && l == 0) {
@@ -598,7 +650,7 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
       wg_link_->signal(side_);
     }
   }
-  flush_signal(s);  // nothing left on this stream to carry it
+  if (!in_step_ || join) flush_signal(s);  // nothing left on this stream to carry it
   if (join && ovl) join_side(s);
 }
 
@@ -770,6 +822,7 @@ void VggEngine::step(int64_t B, DeviceComm* comm, const std::vector<int64_t>& bu
   hp_[2] = wd;
   hp_[3] = dampening;
   bwd_sgd_ = side_sgd && !dp;
+  in_step_ = true;
   int64_t hi = L - 1;
   for (size_t k = 0; k < nb; ++k) {
     const int64_t lo = bucket_blocks[k];
@@ -795,6 +848,7 @@ void VggEngine::step(int64_t B, DeviceComm* comm, const std::vector<int64_t>& bu
     }
     if (dp) {
       Range r("cs.allreduce.enqueue");
+      if (comm->host_blocking()) flush_signal(s);
       comm->all_reduce(G(bucket_ranges[2 * k]), bucket_ranges[2 * k + 1], ncclFloat32, ncclAvg, src,
                        /*fork=*/!(debug_skip_ & 2));
     }
@@ -817,6 +871,8 @@ void VggEngine::step(int64_t B, DeviceComm* comm, const std::vector<int64_t>& bu
     if (side_sgd && dp) sgd_on(comm->stream(), bucket_ranges[2 * k], bucket_ranges[2 * k + 1], k + 1 == nb);
   }
   bwd_sgd_ = false;
+  in_step_ = false;
+  flush_signal(s);
   {
     Range r("cs.comm.join");
     if (ovl) join_side(s);

@@ -86,6 +86,7 @@ class VggEngine {
   // "" unless a side-stream link wait timed out (device_comm.h StreamLink: bounded waits)
   std::string link_error() const;
   void set_fixup(bool on) { fixup_ = on; }
+  void set_epi_red(bool on) { epi_red_ = on; }
   void set_dual(bool on) { dual_ = on; }
   void set_bn_fused_rows(int64_t r) { bn_fused_rows_ = r; }
   bool block_dual(int64_t l) const { return blocks_.at(l).use_dual; }
@@ -144,7 +145,16 @@ class VggEngine {
 
  private:
   void conv(int l, int mode, int B, const ConvTile& t, hipStream_t s, bool with_stats, float* ws = nullptr,
-            float* dz = nullptr, bool keep_slabs = false, const CsBnRed* red = nullptr);
+            float* dz = nullptr, bool keep_slabs = false, const CsBnRed* red = nullptr,
+            const CsBnRed* ered = nullptr);
+  // Block l-1's BN-backward partial sums computed where block l's data gradient is finished —
+  // in the dgrad GEMM's epilogue, or in its split-K combine (CsConvArgs::ered) — instead of a
+  // reduce launch re-reading G and y; the BN backward of block l-1 is then finalize + apply,
+  // with the deferred side-stream signal riding the finalize launch (CS_BN_EPI_RED=0 disables).
+  // Only with the three-launch BN path (bn_path_ 0), no in-launch combine and no kept slabs.
+  bool epi_red_ = true;
+  bool epi_red_ok(int l, int64_t B) const;  // block l's dgrad can carry block l-1's partials
+  CsBnRed epi_red_args(int l, int B);       // ... and their arguments (part = bn_part_)
   // Backward order dgrad(l) -> wgrad(l) with block l-1's BN partial-sum pass appended to the
   // wgrad launch (extra blocks dispatched after the GEMM tiles, filling its tail): one launch
   // per block fewer on the critical chain, bit-identical partials (CS_FUSE_BN_RED=0 disables)
@@ -156,7 +166,7 @@ class VggEngine {
   bool dual_ok(int l) const;
   // single-launch BN forward / backward for layers with at most bn_fused_rows_ rows (B*H*W)
   bool bn_fused(int l, int64_t B) const;
-  void conv_dual(int l, int B, hipStream_t s, float* dz);
+  void conv_dual(int l, int B, hipStream_t s, float* dz, const CsBnRed* ered = nullptr);
   float* P(int64_t off) { return params_.data_ptr<float>() + off; }
   float* G(int64_t off) { return grads_.data_ptr<float>() + off; }
   int64_t Bmax_, feat_, ncls_;
@@ -197,6 +207,10 @@ class VggEngine {
   unsigned long long* pending_sig_ = nullptr;
   bool defer_signals_ = true;  // CS_DEFER_SIGNALS=0: every link signal as its own launch
   void flush_signal(hipStream_t s);  // launch a pending deferred signal as its own kernel
+  // set by step(): a signal still pending at the end of one bucket's backward() rides the first
+  // launch of the next bucket's (with layer-aligned buckets every backward() call is one block,
+  // so flushing there put every signal on a launch of its own); step() flushes before any wait
+  bool in_step_ = false;
   // CS_KEEP_SLABS=1: split-K data gradients leave their slabs in ws_ and the next BN backward
   // sums them (z order, bit-equal) while it reads G, instead of a separate combine launch.
   // Off: measured equal on MI355X (81.8-82.0k vs 82.0-82.1k img/s) — both BN passes then read

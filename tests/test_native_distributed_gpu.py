@@ -85,7 +85,7 @@ def test_python_gloo_collectives_with_side_stream_wgrad(gpu):
     ser = run_world(_train, 2, "ddp", "none", 6, "torch", 16, False, {"CS_OVERLAP_WGRAD": "0"})
     assert not ser[0]["wgrad_side"]
     for _ in range(3):
-        ovl = run_world(_train, 2, "ddp", "none", 6, "torch", 16, False, {})
+        ovl = run_world(_train, 2, "ddp", "none", 6, "torch", 16, False, {"CS_OVERLAP_WGRAD": "1"})
         assert ovl[0]["wgrad_side"] and ovl[0]["sys_join"]
         for r in range(2):
             for k in ("params", "mom", "bufs"):

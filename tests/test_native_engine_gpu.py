@@ -276,6 +276,7 @@ def test_deferred_link_signals_bitwise_equal(dev, monkeypatch):
     """Side-stream weight gradients forked by a signal folded into the next main-stream BN launch
     (CS_DEFER_SIGNALS=1, default) == a separate signal launch per block, bit for bit."""
     out = []
+    monkeypatch.setenv("CS_OVERLAP_WGRAD", "1")
     for defer in ("0", "1"):
         monkeypatch.setenv("CS_DEFER_SIGNALS", defer)
         t = _trainer(dev, batch_size=32, train_size=256)
@@ -294,6 +295,7 @@ def test_kept_dgrad_slabs_bitwise_equal(dev, stage, monkeypatch):
     # CS_KEEP_SLABS=1 (opt-in): split-K data gradients left as slabs and summed (z order) by the
     # next BN backward while it reads G == the separate split-K combine launch, bit for bit
     out = []
+    monkeypatch.setenv("CS_BN_EPI_RED", "0")  # kept slabs leave the BN partials to the reduce pass
     for keep in ("0", "1"):
         monkeypatch.setenv("CS_KEEP_SLABS", keep)
         t = _trainer(dev, batch_size=32, train_size=256)
@@ -335,12 +337,51 @@ def test_bf16_mode_tracks_fp32(dev):
     assert (ga @ gb / (ga.norm() * gb.norm())).item() > 0.95
 
 
+@pytest.mark.parametrize("tiles", ["shipped", "split", "nosplit", "dual"])
+def test_bn_partials_from_dgrad_match_reduce_pass(dev, tiles, monkeypatch):
+    """Block l-1's BN-backward partial sums taken from block l's data gradient — in the dgrad
+    GEMM epilogue (no split-K) or in its split-K combine (CS_BN_EPI_RED=1, default) — vs the
+    separate reduce launch (=0): same per-element terms, a different fixed summation order ->
+    a norm bound after two steps at B=64; run to run bitwise."""
+    monkeypatch.setenv("CS_BN_PATH", "0")
+    if tiles == "dual":
+        monkeypatch.setenv("CS_OVERLAP_WGRAD", "0")
+    out = []
+    for er in ("0", "1", "1"):
+        monkeypatch.setenv("CS_BN_EPI_RED", er)
+        t = _trainer(dev, batch_size=64, train_size=256, autotune=tiles == "shipped")
+        if tiles != "shipped":
+            for l in range(1, t.layout.L):
+                if tiles == "split":  # split-K 3/4 dgrads, f32 and X6S kernels (partials in the combine)
+                    t.engine.set_tile(l, 1, 64, 64, 4 if l % 2 else 3, 64 if l % 2 else 16, (16 | 4) if l % 2 else 0)
+                elif tiles == "nosplit":  # epilogue partials: 64x64 / 128x64 tiles, 256 / 1024 threads
+                    t.engine.set_tile(l, 1, 64 if l % 2 else 128, 64, 1, 64 if l % 2 else 32,
+                                      (16 | 4) if l % 2 else 0)
+                else:  # one wgrad + dgrad launch
+                    t.engine.set_tile(l, 1, 64, 64, 1 + (l % 2), 16, 0)
+                    t.engine.set_tile(l, 2, 64, 64, 2, 16, 0)
+                    t.engine.set_block_dual(l, True)
+        for _ in range(2):
+            t.step()
+        torch.cuda.synchronize()
+        assert not t.engine.link_error()
+        out.append((t.params.clone(), t.mom.clone(), t.bufs.clone(), t.last_loss()))
+    a, b, c = out
+    assert abs(a[3] - b[3]) < 1e-4 * max(1.0, abs(a[3]))
+    for x, y in zip(a[:2], b[:2]):
+        d = (y.double() - x.double()).norm() / x.double().norm()
+        assert d.item() < 1e-3, d.item()
+    for x, y in zip(b[:3], c[:3]):
+        assert torch.equal(x, y)
+
+
 @pytest.mark.parametrize("keep", ["0", "1"])
 def test_bn_reduce_in_wgrad_launch_bitwise_equal(dev, keep, monkeypatch):
     # block l-1's BN partial-sum pass appended to block l's weight-gradient launch (extra blocks
     # after the GEMM tiles) == the standalone reduce launch, bit for bit (also with kept slabs)
     monkeypatch.setenv("CS_KEEP_SLABS", keep)
     monkeypatch.setenv("CS_BN_PATH", "0")  # the appended reduce belongs to the three-launch BN path
+    monkeypatch.setenv("CS_BN_EPI_RED", "0")  # (partials out of the dgrad would take precedence)
     out = []
     for fuse in ("0", "1"):
         monkeypatch.setenv("CS_FUSE_BN_RED", fuse)
@@ -477,7 +518,7 @@ def test_ragged_batches_match_fp64(dev, B, Bmax):
 
 
 def test_wgrad_side_stream_bitwise_and_graph(dev):
-    """Weight gradients on the side stream (kernel stream links, the default) compute exactly
+    """Weight gradients on the side stream (kernel stream links, CS_OVERLAP_WGRAD=1) compute exactly
     what the serial backward does; a full-step graph of the two-stream step replays it exactly."""
     runs = []
     for ovl, graph in ((False, "none"), (True, "none"), (True, "full")):
