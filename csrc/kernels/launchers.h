@@ -31,6 +31,19 @@ hipError_t cs_rows_mean(float* src, int rows, int64_t n, float* dst, int bcast, 
 hipError_t cs_accumulate(float* g, const float* t, int64_t n, float div, hipStream_t stream);
 // bf16 gradient transport: to_bf16 = 1: fp32 src -> bf16 dst (round to nearest even); 0: bf16 -> fp32
 hipError_t cs_cast_grad(const void* src, void* dst, int64_t n, int to_bf16, hipStream_t stream);
+// SGD whose gradient for some ranges still sits in split-K slabs (weight gradients whose
+// combine launch was skipped): range k = [off[k], off[k] + len[k]) of the flat buffers has its
+// gradient in slab[k][z * stride[k] + i - off[k]], z < ns[k], summed in z order (bit-equal to
+// the combine launch) and written to g before the update. Offsets / lengths multiples of 4.
+constexpr int kCsSgdSlabsMax = 16;
+struct CsSgdSlabs {
+  int n;
+  int64_t off[kCsSgdSlabsMax], len[kCsSgdSlabsMax], stride[kCsSgdSlabsMax];
+  const float* slab[kCsSgdSlabsMax];
+  int ns[kCsSgdSlabsMax];
+};
+hipError_t cs_sgd_flat_slabs(float* p, float* g, float* m, int64_t n, float lr, float mom, float wd, float damp,
+                             float scale, int first, hipStream_t stream, int64_t* counter, const CsSgdSlabs& slabs);
 hipError_t cs_sgd_multi(const CsTensorEntry* tab_dev, int ntens, const int64_t* chunk_start_dev, int nchunks,
                         float lr, float mom, float wd, float damp, float scale, int first, hipStream_t stream);
 

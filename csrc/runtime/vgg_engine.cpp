@@ -204,6 +204,7 @@ VggEngine::VggEngine(int64_t Bmax, std::vector<int64_t> desc, std::vector<int64_
   if (const char* e = getenv("CS_KEEP_SLABS")) keep_slabs_ = atoi(e) != 0;
   if (const char* e = getenv("CS_FUSE_BN_RED")) fuse_red_ = atoi(e) != 0;
   if (const char* e = getenv("CS_BN_EPI_RED")) epi_red_ = atoi(e) != 0;
+  if (const char* e = getenv("CS_SGD_SLABS")) sgd_slabs_on_ = atoi(e) != 0;
   grid_bar_ = torch::zeros({2 * kCsBnGridBarInts}, fo.dtype(at::kInt));  // backward set, forward set
   {
     void* h = nullptr;
@@ -612,7 +613,25 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
       conv(l, CS_CONV_WGRAD, (int)B, b.tile[CS_CONV_WGRAD], side_, false, ws_side_.data_ptr<float>(), dz);
       wg_link_->signal(side_);
     } else if (!ovl) {
-      conv(l, CS_CONV_WGRAD, (int)B, b.tile[CS_CONV_WGRAD], s, false, ws_side_.data_ptr<float>(), dz);
+      const ConvTile& tw = b.tile[CS_CONV_WGRAD];
+      const Dims dw = dims(b, CS_CONV_WGRAD, B);
+      const int spw = eff_splits(dw.K, tw.splits, tw.bk);
+      const int64_t slab = dw.M * dw.N;
+      if (keep_wg_ && l > 0 && spw > 1 && spw <= 32 && sgd_slabs_.n < kCsSgdSlabsMax &&
+          keep_used_ + spw * slab <= keep_ws_.numel()) {
+        // slabs stay for the step's SGD launch to sum (no combine launch)
+        float* w = keep_ws_.data_ptr<float>() + keep_used_;
+        conv(l, CS_CONV_WGRAD, (int)B, tw, s, false, w, dz, /*keep_slabs=*/true);
+        const int k = sgd_slabs_.n++;
+        sgd_slabs_.off[k] = b.w_off;
+        sgd_slabs_.len[k] = slab;
+        sgd_slabs_.stride[k] = slab;
+        sgd_slabs_.slab[k] = w;
+        sgd_slabs_.ns[k] = spw;
+        keep_used_ += spw * slab;
+      } else {
+        conv(l, CS_CONV_WGRAD, (int)B, tw, s, false, ws_side_.data_ptr<float>(), dz);
+      }
     }
     if (l > 0) {
       const ConvTile& t = b.tile[CS_CONV_DGRAD];
@@ -823,6 +842,22 @@ void VggEngine::step(int64_t B, DeviceComm* comm, const std::vector<int64_t>& bu
   hp_[3] = dampening;
   bwd_sgd_ = side_sgd && !dp;
   in_step_ = true;
+  // kept weight-gradient slabs for the final SGD (world 1, serial backward, one flat SGD launch)
+  sgd_slabs_.n = 0;
+  keep_used_ = 0;
+  keep_wg_ = sgd_slabs_on_ && !dp && !ovl && !tiled && !side_sgd;
+  if (keep_wg_) {
+    int64_t need = 0;
+    for (int64_t l = 1; l < L; ++l) {
+      const ConvTile& tw = blocks_[l].tile[CS_CONV_WGRAD];
+      const Dims dw = dims(blocks_[l], CS_CONV_WGRAD, B);
+      const int spw = eff_splits(dw.K, tw.splits, tw.bk);
+      if (spw > 1 && spw <= 32) need += spw * dw.M * dw.N;
+    }
+    if ((!keep_ws_.defined() || keep_ws_.numel() < need) && !stream_capturing(s))
+      keep_ws_ = torch::zeros({std::max<int64_t>(need, 4)}, params_.options());
+    keep_wg_ = keep_ws_.defined() && keep_ws_.numel() >= need;
+  }
   int64_t hi = L - 1;
   for (size_t k = 0; k < nb; ++k) {
     const int64_t lo = bucket_blocks[k];
@@ -881,8 +916,19 @@ void VggEngine::step(int64_t B, DeviceComm* comm, const std::vector<int64_t>& bu
   mark("allreduce_wait");
   {
     Range r("cs.sgd");
-    if (tiled) join_opt();
-    else if (!side_sgd) sgd(lr, momentum, wd, dampening, 0, params_.numel());
+    if (tiled) {
+      join_opt();
+    } else if (!side_sgd && sgd_slabs_.n > 0) {
+      ok(cs_sgd_flat_slabs(P(0), G(0), mom_.data_ptr<float>(), params_.numel(), (float)lr, (float)momentum, (float)wd,
+                           (float)dampening, 1.0f, sgd_first_ ? 1 : 0, s,
+                           perm_len_ > 0 ? cursor_.data_ptr<int64_t>() : nullptr, sgd_slabs_),
+         "sgd_flat_slabs");
+      sgd_first_ = false;
+    } else if (!side_sgd) {
+      sgd(lr, momentum, wd, dampening, 0, params_.numel());
+    }
+    sgd_slabs_.n = 0;
+    keep_wg_ = false;
     if (side_sgd) sgd_first_ = false;
   }
   mark("sgd");

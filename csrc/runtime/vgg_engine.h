@@ -211,6 +211,17 @@ class VggEngine {
   // launch of the next bucket's (with layer-aligned buckets every backward() call is one block,
   // so flushing there put every signal on a launch of its own); step() flushes before any wait
   bool in_step_ = false;
+  // World-1 serial step: split-K weight gradients (blocks > 0, <= 32 slabs) leave their slabs in
+  // keep_ws_ and the step's one SGD launch sums them (z order: bit-equal) while it updates —
+  // no combine launch, no gradient round trip (CS_SGD_SLABS=1 enables). Off with a
+  // communicator (the all-reduce needs the combined gradient) and outside step(). Opt-in
+  // (CS_SGD_SLABS=1): measured even on MI355X (82.3-82.8k vs 82.8-83.6k img/s) — the SGD pass
+  // then walks each range's slabs one float4 at a time, which costs what the saved launches did.
+  bool sgd_slabs_on_ = false;
+  bool keep_wg_ = false;     // set by step() for the step in flight
+  torch::Tensor keep_ws_;
+  int64_t keep_used_ = 0;
+  CsSgdSlabs sgd_slabs_{};
   // CS_KEEP_SLABS=1: split-K data gradients leave their slabs in ws_ and the next BN backward
   // sums them (z order, bit-equal) while it reads G, instead of a separate combine launch.
   // Off: measured equal on MI355X (81.8-82.0k vs 82.0-82.1k img/s) — both BN passes then read

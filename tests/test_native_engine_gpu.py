@@ -375,6 +375,27 @@ def test_bn_partials_from_dgrad_match_reduce_pass(dev, tiles, monkeypatch):
         assert torch.equal(x, y)
 
 
+@pytest.mark.parametrize("tiles", ["shipped", "split"])
+def test_wgrad_slabs_summed_by_sgd_bitwise_equal(dev, tiles, monkeypatch):
+    """World-1 serial step: split-K weight gradients left as slabs and summed (z order) by the
+    step's SGD launch (CS_SGD_SLABS=1, opt-in) == the combine launch + plain SGD, bit for bit —
+    parameters, momentum and the gradient buffer itself."""
+    out = []
+    for on in ("0", "1"):
+        monkeypatch.setenv("CS_SGD_SLABS", on)
+        t = _trainer(dev, batch_size=64, train_size=512, autotune=tiles == "shipped")
+        if tiles == "split":  # f32 and X6S weight gradients, 2..32 slabs
+            for l in range(1, t.layout.L):
+                t.engine.set_tile(l, 2, 64, 64, [2, 32, 16, 8, 5, 3, 4][l - 1], 32 if l % 2 else 64,
+                                  0 if l % 2 else (16 | 4))
+        for _ in range(3):
+            t.step()
+        torch.cuda.synchronize()
+        out.append((t.params.clone(), t.mom.clone(), t.grads.clone(), t.bufs.clone()))
+    for a, b in zip(*out):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("keep", ["0", "1"])
 def test_bn_reduce_in_wgrad_launch_bitwise_equal(dev, keep, monkeypatch):
     # block l-1's BN partial-sum pass appended to block l's weight-gradient launch (extra blocks
