@@ -1,8 +1,11 @@
 """Channels-last (NHWC) convolution, BatchNorm(+residual)(+ReLU) and 3x3/2 max-pool for the
 ResNet family's native path (``csrc/kernels/cnn_nhwc.hip``; models/resnet.py ``layout="nhwc"``).
 
-Activations are contiguous ``[B, H, W, C]`` tensors (fp32, or bf16 under autocast). A
-convolution is one GEMM on MI355X's matrix cores (hipBLASLt via ``torch.mm``):
+Activations are contiguous ``[B, H, W, C]`` tensors (fp32, or bf16 under autocast). A bf16
+convolution with C, Cout % 32 == 0 that is not a plain 1x1/stride-1 one runs as the gfx950
+implicit-GEMM kernel (``csrc/kernels/conv_nhwc.hip``: forward, data and weight gradient gather
+their operands straight from the activations, no patch matrix in memory); the others are one
+GEMM on MI355X's matrix cores (hipBLASLt via ``torch.mm``):
 
 * 1x1 / stride 1: the activation *is* the ``[B*H*W, Cin]`` operand, no copy;
 * anything else (3x3, the 7x7 stem, strided 1x1 shortcuts): the gfx950 ``im2col_nhwc`` gather
@@ -18,6 +21,7 @@ the module's running statistics through plain torch ops.
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -70,6 +74,46 @@ def _wgrad(dy2: torch.Tensor, col: torch.Tensor) -> torch.Tensor:
     b = col.view(S, M // S, Kp)
     part = torch.bmm(a, b, out_dtype=torch.float32) if col.dtype != torch.float32 else torch.bmm(a, b)
     return part.sum(0)
+
+
+def _implicit_ok(dt: torch.dtype, C: int, Ci: int, Co: int, R: int, S: int, stride: int, pad: int) -> bool:
+    """the bf16 implicit-GEMM kernel serves this conv (every bf16 ResNet conv but the 4-channel
+    stem and the plain 1x1/stride-1 ones, which already are a GEMM on the activation itself);
+    CS_CONV_IMPLICIT=0 keeps the im2col + GEMM path"""
+    return (dt == torch.bfloat16 and C == Ci and Ci % 32 == 0 and Co % 32 == 0
+            and not (R == 1 and S == 1 and stride == 1 and pad == 0)
+            and os.environ.get("CS_CONV_IMPLICIT", "0") != "0")
+
+
+class _ConvImplicitNHWC(torch.autograd.Function):
+    """bf16 implicit-GEMM convolution (csrc/kernels/conv_nhwc.hip): no patch matrix in memory
+    forward or backward; saves x and the [Co, R, S, C] weight"""
+
+    @staticmethod
+    def forward(ctx, x, weight, stride: int, pad: int):
+        Co, Ci, R, S = weight.shape
+        w4 = weight.permute(0, 2, 3, 1).to(torch.bfloat16).contiguous()  # [Co, R, S, C]
+        y = native.C().conv_nhwc_bf16(0, x, w4, R, S, stride, pad, 0, 0)
+        ctx.save_for_backward(x, w4)
+        ctx.geo = (R, S, stride, pad)
+        ctx.wdtype = weight.dtype
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w4 = ctx.saved_tensors
+        R, S, stride, pad = ctx.geo
+        dy = dy.to(torch.bfloat16).contiguous()
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            wt = w4.permute(3, 1, 2, 0).contiguous()  # [C, R, S, Co]
+            dx = native.C().conv_nhwc_bf16(1, dy, wt, R, S, stride, pad, x.shape[1], x.shape[2])
+        if ctx.needs_input_grad[1]:
+            dwf = native.C().conv_nhwc_bf16(2, dy, x, R, S, stride, pad, 0, 0)  # fp32 [Co, R*S*C]
+            Co, C = w4.shape[0], w4.shape[3]
+            dw = torch.empty((Co, C, R, S), dtype=ctx.wdtype, device=dy.device)
+            dw.copy_(dwf.view(Co, R, S, C).permute(0, 3, 1, 2))
+        return dx, dw, None, None
 
 
 class _ConvNHWC(torch.autograd.Function):
@@ -133,7 +177,11 @@ def conv_nhwc(x: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
     if not x.is_cuda:
         y = F.conv2d(x.permute(0, 3, 1, 2), conv.weight.to(x.dtype), None, conv.stride, conv.padding)
         return y.permute(0, 2, 3, 1).contiguous()
-    return _ConvNHWC.apply(x, conv.weight, int(conv.stride[0]), int(conv.padding[0]))
+    Co, Ci, R, S = conv.weight.shape
+    st, pad = int(conv.stride[0]), int(conv.padding[0])
+    if _implicit_ok(act_dtype(x), x.shape[3], Ci, Co, R, S, st, pad):
+        return _ConvImplicitNHWC.apply(x.to(torch.bfloat16).contiguous(), conv.weight, st, pad)
+    return _ConvNHWC.apply(x, conv.weight, st, pad)
 
 
 class _BnActNHWC(torch.autograd.Function):

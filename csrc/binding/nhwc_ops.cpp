@@ -36,6 +36,59 @@ T* opt_ptr(const c10::optional<torch::Tensor>& t) {
   return t.has_value() && t->defined() ? t->data_ptr<T>() : nullptr;
 }
 
+// bf16 NHWC implicit-GEMM convolution (conv_nhwc.hip). mode 0: a = x [B,H,W,C], b = w
+// [Co,R,S,C] -> y [B,Ho,Wo,Co]; mode 1: a = dy [B,Ho,Wo,Co], b = wt [C,R,S,Co] -> dx [B,H,W,C]
+// (H, W given); mode 2: a = dy, b = x -> fp32 dW [Co, R*S*C]
+torch::Tensor conv_nhwc_bf16(int64_t mode, torch::Tensor a, torch::Tensor b, int64_t R, int64_t S, int64_t stride,
+                             int64_t pad, int64_t H, int64_t W) {
+  TORCH_CHECK(mode >= 0 && mode <= 2, "conv_nhwc_bf16: mode 0 fwd, 1 dgrad, 2 wgrad");
+  for (const auto* t : {&a, &b})
+    TORCH_CHECK(t->is_cuda() && t->is_contiguous() && t->scalar_type() == at::kBFloat16 && t->dim() == 4,
+                "conv_nhwc_bf16: operands must be contiguous 4-D bfloat16 GPU tensors");
+  TORCH_CHECK(R >= 1 && S >= 1 && stride >= 1 && pad >= 0, "conv_nhwc_bf16: geometry");
+  CsConvNhwcArgs p{};
+  p.R = (int)R;
+  p.S = (int)S;
+  p.st = (int)stride;
+  p.pad = (int)pad;
+  DevGuard g(a.device());
+  torch::Tensor out, ws;
+  if (mode == 0) {
+    p.B = (int)a.size(0), p.H = (int)a.size(1), p.W = (int)a.size(2), p.C = (int)a.size(3), p.Co = (int)b.size(0);
+    TORCH_CHECK(b.size(1) == R && b.size(2) == S && b.size(3) == p.C, "conv_nhwc_bf16: weight [Co, R, S, C]");
+    const int64_t Ho = (p.H + 2 * pad - R) / stride + 1, Wo = (p.W + 2 * pad - S) / stride + 1;
+    out = torch::empty({p.B, Ho, Wo, p.Co}, a.options());
+    p.x = a.data_ptr();
+    p.w = b.data_ptr();
+    p.y = out.data_ptr();
+  } else if (mode == 1) {
+    p.B = (int)a.size(0), p.H = (int)H, p.W = (int)W, p.Co = (int)a.size(3), p.C = (int)b.size(0);
+    TORCH_CHECK(b.size(1) == R && b.size(2) == S && b.size(3) == p.Co, "conv_nhwc_bf16: transposed weight [C, R, S, Co]");
+    TORCH_CHECK(a.size(1) == (H + 2 * pad - R) / stride + 1 && a.size(2) == (W + 2 * pad - S) / stride + 1,
+                "conv_nhwc_bf16: dy spatial size does not match H, W");
+    out = torch::empty({p.B, H, W, p.C}, a.options());
+    p.dy = a.data_ptr();
+    p.w = b.data_ptr();
+    p.y = out.data_ptr();
+  } else {
+    p.B = (int)b.size(0), p.H = (int)b.size(1), p.W = (int)b.size(2), p.C = (int)b.size(3), p.Co = (int)a.size(3);
+    TORCH_CHECK(a.size(0) == p.B && a.size(1) == (p.H + 2 * pad - R) / stride + 1 &&
+                    a.size(2) == (p.W + 2 * pad - S) / stride + 1,
+                "conv_nhwc_bf16: dy / x shapes");
+    const int sp = cs_conv_nhwc_splits(2, p.B, p.H, p.W, p.C, p.Co, p.R, p.S, p.st, p.pad);
+    ws = torch::empty({(int64_t)sp * p.Co * R * S * p.C}, a.options().dtype(at::kFloat));
+    out = torch::empty({p.Co, R * S * p.C}, a.options().dtype(at::kFloat));
+    p.dy = a.data_ptr();
+    p.x = b.data_ptr();
+    p.dw = ws.data_ptr<float>();
+    p.dw_out = out.data_ptr<float>();
+    CS_LAUNCH(cs_conv_nhwc(2, p, sp, cur_stream()));
+    return out;
+  }
+  CS_LAUNCH(cs_conv_nhwc((int)mode, p, 1, cur_stream()));
+  return out;
+}
+
 // -> {y, stat [4, C] = scale, shift, mean, invstd}
 std::vector<torch::Tensor> bn_nhwc_fwd(torch::Tensor x, c10::optional<torch::Tensor> res,
                                        c10::optional<torch::Tensor> w, c10::optional<torch::Tensor> b,
@@ -158,6 +211,9 @@ torch::Tensor col2im_nhwc(torch::Tensor dcol, int64_t B, int64_t H, int64_t W, i
 }  // namespace
 
 void register_nhwc_ops(pybind11::module& m) {
+  m.def("conv_nhwc_bf16", &conv_nhwc_bf16,
+        "bf16 NHWC implicit-GEMM conv: mode 0 fwd (a=x, b=w[Co,R,S,C]) -> y; 1 dgrad (a=dy, b=wt[C,R,S,Co]) -> dx; "
+        "2 wgrad (a=dy, b=x) -> fp32 dW [Co, R*S*C]");
   m.def("bn_nhwc_fwd", &bn_nhwc_fwd, "training BatchNorm2d (+residual) (+ReLU), NHWC fp32/bf16 -> (y, stat)");
   m.def("bn_nhwc_bwd", &bn_nhwc_bwd, "its backward -> (dx, dres, dweight, dbias)");
   m.def("maxpool3s2_nhwc_fwd", &maxpool3s2_nhwc_fwd, "3x3/2 pad-1 max-pool, NHWC -> (y, window position)");

@@ -305,6 +305,23 @@ hipError_t cs_maxpool3s2_nhwc_fwd(int dt, const void* x, void* y, unsigned char*
                                   int Ho, int Wo, hipStream_t stream);
 hipError_t cs_maxpool3s2_nhwc_bwd(int dt, const void* dy, const unsigned char* pos, void* dx, int B, int H, int W,
                                   int C, int Ho, int Wo, hipStream_t stream);
+// bf16 NHWC implicit-GEMM convolution (conv_nhwc.hip; C, Co % 32 == 0, any R x S / stride / pad):
+// FWD y[B,Ho,Wo,Co] = conv(x, w [Co][R][S][C]); DGRAD dx = y-shaped dy through wt [C][R][S][Co]
+// (the weight transposed by the caller), written to y; WGRAD: split-K fp32 slabs in dw
+// ([splits][Co][R*S*C], cs_conv_nhwc_splits) summed in split order into dw_out [Co][R*S*C] fp32.
+struct CsConvNhwcArgs {
+  const void* x;   // FWD / WGRAD: bf16 [B, H, W, C]
+  const void* w;   // FWD: bf16 [Co][R][S][C]; DGRAD: bf16 [C][R][S][Co]
+  const void* dy;  // DGRAD / WGRAD: bf16 [B, Ho, Wo, Co]
+  void* y;         // FWD: y; DGRAD: dx (bf16 [B, H, W, C])
+  float* dw;       // WGRAD: slab workspace
+  float* dw_out;   // WGRAD: fp32 [Co][R*S*C]
+  int B, H, W, C, Co, R, S, st, pad;
+  // filled by the launcher
+  int Ho, Wo, M, N, K, ksteps, ksteps_per_split;
+};
+int cs_conv_nhwc_splits(int mode, int B, int H, int W, int C, int Co, int R, int S, int st, int pad);
+hipError_t cs_conv_nhwc(int mode, const CsConvNhwcArgs& a, int splits, hipStream_t stream);
 // col: [B*Ho*Wo, Kp], columns (r*S + s)*C + c, zero for k >= R*S*C; col2im is its adjoint (gather)
 hipError_t cs_im2col_nhwc(int dt, const void* x, void* col, int B, int H, int W, int C, int R, int S, int stride,
                           int pad, int Ho, int Wo, int Kp, hipStream_t stream);

@@ -97,21 +97,24 @@ def test_python_gloo_collectives_with_side_stream_wgrad(gpu):
 def test_cpp_ddp_step_multi_rank_staged(gpu, world):
     """The N>1 benchmark's C++ step (not _step_eager) with `world` ranks on one GPU."""
     steps = 8
-    nat = run_world(_train, world, "ddp", "none", steps, "staged")
     ref = run_world(_train, world, "ddp", "segments", steps, "torch")
-    nb = nat[0]["buckets"]
-    assert nb > 1 and nat[0]["kind"] == "staged"
-    # construction: 4 broadcasts; per step: one all-reduce per bucket + 2 buffer broadcasts
-    assert nat[0]["calls"] == steps * (nb + 2), nat[0]["calls"]
-    for r in range(world):
-        for k in ("params", "mom", "bufs", "nbt"):
-            assert torch.equal(nat[r][k], nat[0][k]), (r, k)
-        assert nat[r]["eval"]["global_correct"] == world * nat[r]["eval"]["correct"]
-        assert nat[r]["wgrad_side"]  # the C++ step ran with side-stream weight gradients
-    # same gradients, same averaging bytes, same SGD: the C++ step equals the Python-orchestrated one
-    assert torch.equal(nat[0]["params"], ref[0]["params"])
-    assert torch.equal(nat[0]["mom"], ref[0]["mom"])
-    assert nat[0]["loss"] == ref[0]["loss"]
+    # the serial backward (default) and the opt-in side-stream weight gradients
+    for side in (False, True):
+        nat = run_world(_train, world, "ddp", "none", steps, "staged", 16, False,
+                        {"CS_OVERLAP_WGRAD": "1" if side else "0"})
+        nb = nat[0]["buckets"]
+        assert nb > 1 and nat[0]["kind"] == "staged"
+        # construction: 4 broadcasts; per step: one all-reduce per bucket + 2 buffer broadcasts
+        assert nat[0]["calls"] == steps * (nb + 2), nat[0]["calls"]
+        for r in range(world):
+            for k in ("params", "mom", "bufs", "nbt"):
+                assert torch.equal(nat[r][k], nat[0][k]), (r, k)
+            assert nat[r]["eval"]["global_correct"] == world * nat[r]["eval"]["correct"]
+            assert nat[r]["wgrad_side"] == side
+        # same gradients, same averaging bytes, same SGD: the C++ step equals the Python-orchestrated one
+        assert torch.equal(nat[0]["params"], ref[0]["params"])
+        assert torch.equal(nat[0]["mom"], ref[0]["mom"])
+        assert nat[0]["loss"] == ref[0]["loss"]
 
 
 @pytest.mark.slow
@@ -122,7 +125,7 @@ def test_cpp_ddp_step_multi_rank_staged_bench_config(gpu):
     nat = run_world(_train, 2, "ddp", "none", steps, "staged", 64, True)
     ref = run_world(_train, 2, "ddp", "segments", steps, "torch", 64, True)
     assert nat[0]["tiles"] == "shipped" and "x6s" in nat[0]["maths"], (nat[0]["tiles"], nat[0]["maths"])
-    assert nat[0]["wgrad_side"] and nat[0]["kind"] == "staged"
+    assert not nat[0]["wgrad_side"] and nat[0]["kind"] == "staged"  # the bench default: serial backward
     for k in ("params", "mom", "bufs", "nbt"):
         assert torch.equal(nat[1][k], nat[0][k]), k
     assert torch.equal(nat[0]["params"], ref[0]["params"])
