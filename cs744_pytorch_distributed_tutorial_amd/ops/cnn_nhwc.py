@@ -77,12 +77,21 @@ def _wgrad(dy2: torch.Tensor, col: torch.Tensor) -> torch.Tensor:
 
 
 def _implicit_ok(dt: torch.dtype, C: int, Ci: int, Co: int, R: int, S: int, stride: int, pad: int) -> bool:
-    """the bf16 implicit-GEMM kernel serves this conv (every bf16 ResNet conv but the 4-channel
-    stem and the plain 1x1/stride-1 ones, which already are a GEMM on the activation itself);
-    CS_CONV_IMPLICIT=0 keeps the im2col + GEMM path"""
-    return (dt == torch.bfloat16 and C == Ci and Ci % 32 == 0 and Co % 32 == 0
-            and not (R == 1 and S == 1 and stride == 1 and pad == 0)
-            and os.environ.get("CS_CONV_IMPLICIT", "0") != "0")
+    """whether this conv runs as the bf16 implicit-GEMM kernel (csrc/kernels/conv_nhwc.hip).
+
+    It serves every bf16 conv with C, Cout % 32 == 0 (not the 4-channel stem; plain 1x1/stride-1
+    convs already are a GEMM on the activation). By default it takes the stride-1 convs with at
+    most 128 input channels — the memory-bound ones, where not writing and re-reading the patch
+    matrix wins: ResNet-50 at B=256, fwd+bwd per conv, 56x56x64 3x3 681 vs 1545 us and 28x28x128
+    3x3 603 vs 855 us; the deeper, compute-bound convs stay on im2col + hipBLASLt, which is faster
+    there (14x14x256 3x3 421 vs 615 us; profiles/r3_conv_nhwc_bench.jsonl).
+    CS_CONV_IMPLICIT: 0 never, 1 (default) that policy, 2 every conv it serves."""
+    mode = os.environ.get("CS_CONV_IMPLICIT", "1")
+    if mode == "0" or dt != torch.bfloat16 or C != Ci or Ci % 32 or Co % 32:
+        return False
+    if R == 1 and S == 1 and stride == 1 and pad == 0:
+        return False
+    return mode == "2" or (stride == 1 and Ci <= 128)
 
 
 class _ConvImplicitNHWC(torch.autograd.Function):

@@ -45,8 +45,8 @@ __device__ __forceinline__ uint4 bload16(rsrc_t r, int off) {
 
 template <int MODE>
 struct Ops {  // which operands are K-contiguous in memory (A_G, B_KC) and in their LDS image (A_KC, B_KC)
-  // WGRAD's A (dy^T) arrives pixel-major and is transposed on its way into a K-contiguous image
-  // (the transpose read measured wrong on this operand: every 4th column repeated)
+  // (WGRAD's A, dy^T, arrives pixel-major and is transposed on its way into a K-contiguous image:
+  // 8 two-byte LDS stores per chunk; the pixel-major image + transpose read is the B path)
   static constexpr bool A_G = MODE != CS_CONV_WGRAD, A_KC = true, B_KC = MODE != CS_CONV_WGRAD;
 };
 
@@ -293,7 +293,10 @@ __global__ __launch_bounds__(256) void conv_nhwc_kernel(CsConvNhwcArgs p) {
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
           const int m = m0 + wm * G::WM + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
-          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, acc[i][j][e]), ro,
+          // (copy the element first: hipcc 7.2 lowered bit_cast of an indexed f32x16 element
+          // to element 0 for every e — all 16 stores wrote a0)
+          const float v = acc[i][j][e];
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), ro,
                                                 (m < p.M && n < p.N) ? (m * p.N + n) * 4 : kOOB, 0, 0);
         }
       }

@@ -80,8 +80,8 @@ def test_conv_nhwc_rejects_bad_shapes(C):
 
 @pytest.mark.parametrize("stride,k", [(1, 3), (2, 3), (2, 1)])
 def test_resnet_conv_layer_implicit_vs_im2col(C, stride, k, monkeypatch):
-    """ops/cnn_nhwc.conv_nhwc under bf16 autocast: the implicit-GEMM path (default) and the
-    im2col + GEMM path (CS_CONV_IMPLICIT=0) agree on y, dx and dW to bf16 rounding."""
+    """ops/cnn_nhwc.conv_nhwc under bf16 autocast: the implicit-GEMM path (CS_CONV_IMPLICIT=2: every
+    conv it serves) and the im2col + GEMM path (=0) agree on y, dx and dW to bf16 rounding."""
     from cs744_pytorch_distributed_tutorial_amd.ops import cnn_nhwc
     dev = torch.device("cuda", 0)
     torch.manual_seed(2)
@@ -89,7 +89,7 @@ def test_resnet_conv_layer_implicit_vs_im2col(C, stride, k, monkeypatch):
     x0 = torch.randn(4, 16, 16, 64, device=dev).to(torch.bfloat16)
     g0 = torch.randn(4, 16 // stride, 16 // stride, 128, device=dev).to(torch.bfloat16)
     outs = []
-    for mode in ("0", "1"):
+    for mode in ("0", "2"):
         monkeypatch.setenv("CS_CONV_IMPLICIT", mode)
         x = x0.clone().requires_grad_()
         conv.weight.grad = None
