@@ -1,6 +1,6 @@
 """ResNet-50 convolutions (B=256, bf16, NHWC) that the implicit-GEMM kernel serves: forward +
 backward time of ops/cnn_nhwc.conv_nhwc with the implicit path vs the im2col + hipBLASLt path
-(CS_CONV_IMPLICIT=0), per layer shape, CUDA-event timed over repeated calls. One JSON line per
+(CS_CONV_IMPLICIT=0 vs 2), per layer shape, CUDA-event timed over repeated calls. One JSON line per
 shape; a weighted total over the convs of one ResNet-50 step at the end."""
 import json
 import os
@@ -44,12 +44,12 @@ def timed(H, Ci, Co, k, st, mode):
     return 1000.0 * e0.elapsed_time(e1) / ITERS
 
 
-tot = {"0": 0.0, "1": 0.0}
+tot = {"0": 0.0, "2": 0.0}
 for (H, Ci, Co, k, st, n) in SHAPES:
-    r = {m: timed(H, Ci, Co, k, st, m) for m in ("0", "1")}
+    r = {m: timed(H, Ci, Co, k, st, m) for m in ("0", "2")}
     for m in r:
         tot[m] += n * r[m]
     flop = 3 * 2.0 * B * ((H + 2 * (k // 2) - k) // st + 1) ** 2 * Co * Ci * k * k
     print(json.dumps({"H": H, "Cin": Ci, "Cout": Co, "k": k, "stride": st, "per_net": n, "im2col_us": round(r["0"], 1),
-                      "implicit_us": round(r["1"], 1), "implicit_tflops": round(flop / r["1"] / 1e6, 1)}), flush=True)
-print(json.dumps({"B": B, "total_im2col_us": round(tot["0"], 1), "total_implicit_us": round(tot["1"], 1)}), flush=True)
+                      "implicit_us": round(r["2"], 1), "implicit_tflops": round(flop / r["2"] / 1e6, 1)}), flush=True)
+print(json.dumps({"B": B, "total_im2col_us": round(tot["0"], 1), "total_implicit_us": round(tot["2"], 1)}), flush=True)
