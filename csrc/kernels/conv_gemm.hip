@@ -35,6 +35,7 @@
 #include <algorithm>
 
 #include "conv_common.h"
+#include "sgd_device.h"
 
 namespace {
 
@@ -743,8 +744,13 @@ __global__ __launch_bounds__(256 * KG) void conv_gemm_kernel(CsConvArgs a) {
   const int nsplit = (a.total_ksteps + a.ksteps_per_split - 1) / a.ksteps_per_split;
   const int ng = ntiles * nsplit, lin = blockIdx.x;
   if (lin >= ng) {
-    if (a.red.pool) cs_bn::bn_red_body<true>(a.red, lin - ng, a.red.P, smem);
-    else cs_bn::bn_red_body<false>(a.red, lin - ng, a.red.P, smem);
+    const int e = lin - ng;
+    if (e >= a.red.P) {  // (then a.sgd.P blocks of an independent SGD update)
+      cs_sgd::tail_body(a.sgd, e - a.red.P, a.sgd.P);
+      return;
+    }
+    if (a.red.pool) cs_bn::bn_red_body<true>(a.red, e, a.red.P, smem);
+    else cs_bn::bn_red_body<false>(a.red, e, a.red.P, smem);
     return;
   }
   gemm_body<BM, BN, MODE, BK, SCHED, C4, GL, KG>(a, cs::xcd_remap(lin % ntiles, ntiles), lin / ntiles, nsplit, smem);
@@ -962,7 +968,7 @@ hipError_t launch_gemm_m(const CsConvArgs& a, int splits, int stage, hipStream_t
   const size_t lds = MATH == 3   ? TileXS<BM, BN, MODE, BK>::BYTES
                      : MATH == 5 ? TileXS<BM, BN, MODE, BK, 1>::BYTES
                                  : 2 * T::STAGE * sizeof(float);
-  const dim3 grid(ntiles * splits + a.red.P);
+  const dim3 grid(ntiles * splits + a.red.P + a.sgd.P);
   constexpr bool deep_fits = (BM + BN) * BK * 4 * 5 < 160 * 1024;
   if constexpr (BK != 64 && MATH == 0) {
     if (MODE == CS_CONV_FWD && a.w_oihw)  // padded conv0: Cin = 4 < BK
@@ -1204,7 +1210,8 @@ int prep_gemm(CsConvArgs& a, int mode, int bk, int splits) {
 
 hipError_t cs_conv_gemm_dual(CsConvArgs wg, int wbk, int wsplits, CsConvArgs dg, int dbk, int dsplits,
                              hipStream_t stream, int stage) {
-  if (wg.red.P != 0 || dg.red.P != 0) return hipErrorInvalidValue;  // no appended reduce in dual launches
+  if (wg.red.P != 0 || dg.red.P != 0 || wg.sgd.n != 0 || dg.sgd.n != 0)
+    return hipErrorInvalidValue;  // no appended work in dual launches
   if (wg.w_oihw) return hipErrorInvalidValue;  // conv0 has no data gradient
   wg.counters = dg.counters = nullptr;
   const int s1 = prep_gemm(wg, CS_CONV_WGRAD, wbk, wsplits), s2 = prep_gemm(dg, CS_CONV_DGRAD, dbk, dsplits);
@@ -1260,6 +1267,7 @@ hipError_t cs_conv_gemm(CsConvArgs a, int mode, int bm, int bn, int bk, int spli
   if (!cs_conv_stage_ok(stage, bm, bn, bk, a.w_oihw && mode == CS_CONV_FWD)) return hipErrorInvalidValue;
   splits = prep_gemm(a, mode, bk, splits);
   if (splits < 0) return hipErrorInvalidValue;
+  a.sgd.P = a.sgd.n > 0 ? (int)std::min<int64_t>(256, (a.sgd.n / 4 + 255) / 256) : 0;
   // (BN-backward partials from a split-K data gradient come out of the combine launch)
   if (!cs_conv_fixup_ok(splits, bm, bn) || a.ered.part != nullptr) a.counters = nullptr;
 #define CS_DISPATCH(BM_, BN_, BK_)                                                                       \

@@ -68,6 +68,17 @@ struct CsBnRed {
   int B, H, W, C, pool, P, gslabs;
 };
 
+// An SGD update of one parameter range carried by extra blocks appended to a GEMM launch (after
+// its tiles, like CsBnRed): P blocks (the launcher sizes it when n > 0); n == 0: none.
+struct CsSgdTail {
+  float* p;
+  const float* g;
+  float* m;
+  int64_t n;
+  float lr, mom, wd, damp;
+  int first, P;
+};
+
 struct CsConvArgs {
   const float* x;     // FWD / WGRAD: conv input, NHWC [B,H,W,Cin] (Cin = 4 for the padded conv0 input)
   const float* w;     // FWD / DGRAD: weights, OHWI [Cout][9][Cin]; conv0 (w_oihw=1): OIHW [Cout][3][9]
@@ -89,6 +100,9 @@ struct CsConvArgs {
   // Uses y, scale, shift, mean, invstd, pool and part ([row tiles][N][3], row tiles of BM rows,
   // or CS_SPLITK_STAT_ROWS behind the split-K combine: cs_conv_ered_rows); part == null: none
   CsBnRed ered;
+  // an independent SGD update appended to the launch (the serial world-1 step: block l+1's
+  // parameters, whose last reader has run, ride block l's weight-gradient GEMM)
+  CsSgdTail sgd;
   // pre-split operands (conv_xp.hip): P3 bf16 chunks [n/8][3][8] (h, m, l of every 8 elements)
   const uint16_t* x3;   // FWD / WGRAD: split conv input
   const uint16_t* w3;   // FWD / DGRAD: split OHWI weights

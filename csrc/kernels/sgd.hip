@@ -11,6 +11,7 @@
 // bound, not latency-bound, and stays this simple loop.)
 #include "common.h"
 #include "launchers.h"
+#include "sgd_device.h"
 
 namespace {
 
@@ -20,13 +21,7 @@ struct SgdArgs {
 };
 
 __device__ __forceinline__ void sgd1(float& p, float g, float& m, const SgdArgs& a) {
-  float d = g * a.scale;
-  if (a.wd != 0.f) d = d + a.wd * p;
-  if (a.mom != 0.f) {
-    m = a.first ? d : (m * a.mom + (1.f - a.damp) * d);
-    d = m;
-  }
-  p = p - a.lr * d;
+  cs_sgd::step1(p, g, m, a.lr, a.mom, a.wd, a.damp, a.scale, a.first);
 }
 
 __global__ __launch_bounds__(256) void sgd_flat_kernel(float* __restrict__ p, const float* __restrict__ g,

@@ -1,0 +1,49 @@
+// The SGD element update shared by the flat optimizer pass (sgd.hip) and the optimizer blocks
+// appended to a GEMM launch (conv_gemm.hip, CsConvArgs::sgd): one definition, so both are bit-equal.
+// torch.optim.SGD's order (master/part1/part1.py:98-99):
+//   d = g*scale + wd*p ; buf = first ? d : buf*mom + (1-damp)*d ; p = p - lr*buf
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "launchers.h"
+
+namespace cs_sgd {
+
+__device__ __forceinline__ void step1(float& p, float g, float& m, float lr, float mom, float wd, float damp,
+                                      float scale, int first) {
+  float d = g * scale;
+  if (wd != 0.f) d = d + wd * p;
+  if (mom != 0.f) {
+    m = first ? d : (m * mom + (1.f - damp) * d);
+    d = m;
+  }
+  p = p - lr * d;
+}
+
+// the update of [0, t.n) of t's range by block `blk` of `nblk` (grid-stride, float4 + scalar tail)
+__device__ __forceinline__ void tail_body(const CsSgdTail& t, int blk, int nblk) {
+  const int64_t n4 = t.n >> 2, stride = (int64_t)nblk * blockDim.x;
+  float4* p4 = reinterpret_cast<float4*>(t.p);
+  const float4* g4 = reinterpret_cast<const float4*>(t.g);
+  float4* m4 = reinterpret_cast<float4*>(t.m);
+  for (int64_t i = (int64_t)blk * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 pv = p4[i];
+    const float4 gv = g4[i];
+    float4 mv = t.first ? make_float4(0.f, 0.f, 0.f, 0.f) : m4[i];
+    step1(pv.x, gv.x, mv.x, t.lr, t.mom, t.wd, t.damp, 1.0f, t.first);
+    step1(pv.y, gv.y, mv.y, t.lr, t.mom, t.wd, t.damp, 1.0f, t.first);
+    step1(pv.z, gv.z, mv.z, t.lr, t.mom, t.wd, t.damp, 1.0f, t.first);
+    step1(pv.w, gv.w, mv.w, t.lr, t.mom, t.wd, t.damp, 1.0f, t.first);
+    p4[i] = pv;
+    if (t.mom != 0.f) m4[i] = mv;
+  }
+  for (int64_t i = (n4 << 2) + (int64_t)blk * blockDim.x + threadIdx.x; i < t.n; i += stride) {
+    float pv = t.p[i], mv = t.first ? 0.f : t.m[i];
+    step1(pv, t.g[i], mv, t.lr, t.mom, t.wd, t.damp, 1.0f, t.first);
+    t.p[i] = pv;
+    if (t.mom != 0.f) t.m[i] = mv;
+  }
+}
+
+}  // namespace cs_sgd

@@ -205,6 +205,7 @@ VggEngine::VggEngine(int64_t Bmax, std::vector<int64_t> desc, std::vector<int64_
   if (const char* e = getenv("CS_FUSE_BN_RED")) fuse_red_ = atoi(e) != 0;
   if (const char* e = getenv("CS_BN_EPI_RED")) epi_red_ = atoi(e) != 0;
   if (const char* e = getenv("CS_SGD_SLABS")) sgd_slabs_on_ = atoi(e) != 0;
+  if (const char* e = getenv("CS_SGD_TAIL")) sgd_tail_on_ = atoi(e) != 0;
   grid_bar_ = torch::zeros({2 * kCsBnGridBarInts}, fo.dtype(at::kInt));  // backward set, forward set
   {
     void* h = nullptr;
@@ -343,7 +344,7 @@ void VggEngine::set_perm(torch::Tensor perm) {
 }
 
 void VggEngine::conv(int l, int mode, int B, const ConvTile& t, hipStream_t s, bool with_stats, float* ws,
-                     float* dz, bool keep_slabs, const CsBnRed* red, const CsBnRed* ered) {
+                     float* dz, bool keep_slabs, const CsBnRed* red, const CsBnRed* ered, const CsSgdTail* sgd) {
   VggBlock& b = blocks_[l];
   CsConvArgs a = conv_args(l, mode, B, with_stats, ws, dz);
   a.keep_slabs = keep_slabs ? 1 : 0;
@@ -352,6 +353,7 @@ void VggEngine::conv(int l, int mode, int B, const ConvTile& t, hipStream_t s, b
     TORCH_CHECK(mode == CS_CONV_DGRAD && !keep_slabs, "VggEngine: BN partials ride a data gradient without kept slabs");
     a.ered = *ered;
   }
+  if (sgd != nullptr) a.sgd = *sgd;
   const Dims d = dims(b, mode, B);
   const int sp = eff_splits(d.K, t.splits, t.bk);
   TORCH_CHECK(sp == 1 || (int64_t)sp * d.M * d.N <= ws_elems_, "VggEngine: split-K workspace too small");
@@ -377,6 +379,22 @@ void VggEngine::conv_dual(int l, int B, hipStream_t s, float* dz, const CsBnRed*
   CsConvArgs da = conv_args(l, CS_CONV_DGRAD, B, false, nullptr, dz);
   if (ered != nullptr) da.ered = *ered;
   ok(cs_conv_gemm_dual(wa, w.bk, w.splits, da, d.bk, d.splits, s, w.stage), "conv_gemm_dual");
+}
+
+CsSgdTail VggEngine::sgd_tail_args(int64_t block) {
+  CsSgdTail t{};
+  const int64_t off = blk_range_[block].first, n = blk_range_[block].second;
+  if (n <= 0 || off % 4 != 0) return t;  // float4 rows (otherwise the final pass takes it)
+  t.p = P(off);
+  t.g = G(off);
+  t.m = mom_.data_ptr<float>() + off;
+  t.n = n;
+  t.lr = (float)hp_[0];
+  t.mom = (float)hp_[1];
+  t.wd = (float)hp_[2];
+  t.damp = (float)hp_[3];
+  t.first = sgd_first_ ? 1 : 0;
+  return t;
 }
 
 bool VggEngine::epi_red_ok(int l, int64_t B) const {
@@ -565,6 +583,7 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
     CsBnRed erv{};
     if (er) erv = epi_red_args(l, (int)B);
     if (!ovl && dual_ok(l)) {  // wgrad + dgrad in one launch
+      if (sgd_tail_ && l + 1 < (int)blocks_.size()) sgd_on(s, blk_range_[l + 1].first, blk_range_[l + 1].second, false);
       conv_dual(l, (int)B, s, dz, er ? &erv : nullptr);
       if (er) {
         red_pending_ = l - 1;
@@ -600,6 +619,7 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
       r.pool = c.pool;
       r.P = cs_bn_bwd_blocks((int)B, (int)c.H, (int)c.H, (int)c.cout, c.pool);
       r.gslabs = g_slabs_;
+      if (sgd_tail_ && l + 1 < (int)blocks_.size()) sgd_on(s, blk_range_[l + 1].first, blk_range_[l + 1].second, false);
       conv(l, CS_CONV_WGRAD, (int)B, b.tile[CS_CONV_WGRAD], s, false, ws_side_.data_ptr<float>(), dz, false, &r);
       red_pending_ = l - 1;
       red_P_ = r.P;
@@ -613,6 +633,13 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
       conv(l, CS_CONV_WGRAD, (int)B, b.tile[CS_CONV_WGRAD], side_, false, ws_side_.data_ptr<float>(), dz);
       wg_link_->signal(side_);
     } else if (!ovl) {
+      // block l+1's SGD rides this launch (its BN backward and data gradient ran before it)
+      CsSgdTail tail{};
+      if (sgd_tail_ && l + 1 < (int)blocks_.size()) {
+        tail = sgd_tail_args(l + 1);
+        if (tail.n == 0) sgd_on(s, blk_range_[l + 1].first, blk_range_[l + 1].second, false);
+      }
+      const CsSgdTail* tp = tail.n > 0 ? &tail : nullptr;
       const ConvTile& tw = b.tile[CS_CONV_WGRAD];
       const Dims dw = dims(b, CS_CONV_WGRAD, B);
       const int spw = eff_splits(dw.K, tw.splits, tw.bk);
@@ -621,7 +648,7 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
           keep_used_ + spw * slab <= keep_ws_.numel()) {
         // slabs stay for the step's SGD launch to sum (no combine launch)
         float* w = keep_ws_.data_ptr<float>() + keep_used_;
-        conv(l, CS_CONV_WGRAD, (int)B, tw, s, false, w, dz, /*keep_slabs=*/true);
+        conv(l, CS_CONV_WGRAD, (int)B, tw, s, false, w, dz, /*keep_slabs=*/true, nullptr, nullptr, tp);
         const int k = sgd_slabs_.n++;
         sgd_slabs_.off[k] = b.w_off;
         sgd_slabs_.len[k] = slab;
@@ -630,7 +657,7 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
         sgd_slabs_.ns[k] = spw;
         keep_used_ += spw * slab;
       } else {
-        conv(l, CS_CONV_WGRAD, (int)B, tw, s, false, ws_side_.data_ptr<float>(), dz);
+        conv(l, CS_CONV_WGRAD, (int)B, tw, s, false, ws_side_.data_ptr<float>(), dz, false, nullptr, nullptr, tp);
       }
     }
     if (l > 0) {
@@ -846,6 +873,9 @@ void VggEngine::step(int64_t B, DeviceComm* comm, const std::vector<int64_t>& bu
   sgd_slabs_.n = 0;
   keep_used_ = 0;
   keep_wg_ = sgd_slabs_on_ && !dp && !ovl && !tiled && !side_sgd;
+  // per-block SGD in the weight-gradient launches' tails (not with the kept-slab SGD, which needs
+  // the whole pass at the end)
+  sgd_tail_ = sgd_tail_on_ && !keep_wg_ && !dp && !ovl && !tiled && !side_sgd && !blk_range_.empty();
   if (keep_wg_) {
     int64_t need = 0;
     for (int64_t l = 1; l < L; ++l) {
@@ -924,11 +954,16 @@ void VggEngine::step(int64_t B, DeviceComm* comm, const std::vector<int64_t>& bu
                            perm_len_ > 0 ? cursor_.data_ptr<int64_t>() : nullptr, sgd_slabs_),
          "sgd_flat_slabs");
       sgd_first_ = false;
+    } else if (sgd_tail_) {
+      // blocks 1.. rode the weight-gradient launches; block 0 (+ the cursor) here
+      sgd_on(s, blk_range_[0].first, blk_range_[0].second, true);
+      sgd_first_ = false;
     } else if (!side_sgd) {
       sgd(lr, momentum, wd, dampening, 0, params_.numel());
     }
     sgd_slabs_.n = 0;
     keep_wg_ = false;
+    sgd_tail_ = false;
     if (side_sgd) sgd_first_ = false;
   }
   mark("sgd");

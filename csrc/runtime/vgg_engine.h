@@ -146,7 +146,7 @@ class VggEngine {
  private:
   void conv(int l, int mode, int B, const ConvTile& t, hipStream_t s, bool with_stats, float* ws = nullptr,
             float* dz = nullptr, bool keep_slabs = false, const CsBnRed* red = nullptr,
-            const CsBnRed* ered = nullptr);
+            const CsBnRed* ered = nullptr, const CsSgdTail* sgd = nullptr);
   // Block l-1's BN-backward partial sums computed where block l's data gradient is finished —
   // in the dgrad GEMM's epilogue, or in its split-K combine (CsConvArgs::ered) — instead of a
   // reduce launch re-reading G and y; the BN backward of block l-1 is then finalize + apply,
@@ -218,6 +218,13 @@ class VggEngine {
   // (CS_SGD_SLABS=1): measured even on MI355X (82.3-82.8k vs 82.8-83.6k img/s) — the SGD pass
   // then walks each range's slabs one float4 at a time, which costs what the saved launches did.
   bool sgd_slabs_on_ = false;
+  // World-1 serial step: block l+1's SGD rides block l's weight-gradient GEMM launch as appended
+  // blocks (its parameters' last readers — block l+1's BN backward and data gradient — are done),
+  // in the GEMM's tail instead of one 9.2M-parameter pass at the end of the step; block 0's update
+  // (and the cursor) stays a launch of its own (CS_SGD_TAIL=0 disables)
+  bool sgd_tail_on_ = true;
+  bool sgd_tail_ = false;  // set by step() for the step in flight
+  CsSgdTail sgd_tail_args(int64_t block);
   bool keep_wg_ = false;     // set by step() for the step in flight
   torch::Tensor keep_ws_;
   int64_t keep_used_ = 0;

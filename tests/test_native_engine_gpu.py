@@ -375,6 +375,23 @@ def test_bn_partials_from_dgrad_match_reduce_pass(dev, tiles, monkeypatch):
         assert torch.equal(x, y)
 
 
+@pytest.mark.parametrize("tiles", ["shipped", "default"])
+def test_sgd_in_wgrad_tails_bitwise_equal(dev, tiles, monkeypatch):
+    """World-1 serial step: block l+1's SGD as blocks appended to block l's weight-gradient
+    launch (CS_SGD_TAIL=1, default) == one flat SGD pass at the end, bit for bit (parameters,
+    momentum incl. the first step's buf = d, BN buffers, the device cursor)."""
+    out = []
+    for on in ("0", "1"):
+        monkeypatch.setenv("CS_SGD_TAIL", on)
+        t = _trainer(dev, batch_size=64, train_size=512, autotune=tiles == "shipped")
+        for _ in range(4):
+            t.step()
+        torch.cuda.synchronize()
+        out.append((t.params.clone(), t.mom.clone(), t.bufs.clone(), t.engine.cursor().clone()))
+    for a, b in zip(*out):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("tiles", ["shipped", "split"])
 def test_wgrad_slabs_summed_by_sgd_bitwise_equal(dev, tiles, monkeypatch):
     """World-1 serial step: split-K weight gradients left as slabs and summed (z order) by the
