@@ -734,6 +734,8 @@ __device__ __forceinline__ void gemm_body(const CsConvArgs& a, const int tile, c
   conv_epilogue<BM, BN, MODE, KG>(a, acc, tile, split, nsplit, smem);
 }
 
+__device__ __forceinline__ void splitk_tail(const CsSplitkTail& k, int blk, float* smem);  // below
+
 template <int BM, int BN, int MODE, int BK, int SCHED, bool C4, int GL, int KG = 1>
 __global__ __launch_bounds__(256 * KG) void conv_gemm_kernel(CsConvArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -745,6 +747,10 @@ __global__ __launch_bounds__(256 * KG) void conv_gemm_kernel(CsConvArgs a) {
   const int ng = ntiles * nsplit, lin = blockIdx.x;
   if (lin >= ng) {
     const int e = lin - ng;
+    if (e >= a.red.P + a.sgd.P) {  // (last: a.ktail.P blocks of another GEMM's split-K combine)
+      splitk_tail(a.ktail, e - a.red.P - a.sgd.P, smem);
+      return;
+    }
     if (e >= a.red.P) {  // (then a.sgd.P blocks of an independent SGD update)
       cs_sgd::tail_body(a.sgd, e - a.red.P, a.sgd.P);
       return;
@@ -918,6 +924,20 @@ __global__ __launch_bounds__(256) void splitk_reduce_dual_kernel(CsConvArgs a1, 
   else splitk_reduce_body(a2, mode2, nslab2, zstep2, blockIdx.x - nb1, red, meanv);
 }
 
+// blocks appended to a GEMM launch running another GEMM's split-K combine (CsSplitkTail): the
+// same body, tiles and summation order as splitk_reduce_kernel (WGRAD mode: no statistics, no
+// barrier), on the first 256 threads of the block
+__device__ __forceinline__ void splitk_tail(const CsSplitkTail& k, int blk, float* smem) {
+  if (threadIdx.x >= 256) return;
+  CsConvArgs t{};
+  t.ws = const_cast<float*>(k.ws);
+  t.out = k.out;
+  t.M = k.M;
+  t.N = k.N;
+  splitk_reduce_body(t, CS_CONV_WGRAD, k.nslab, 1, blk, *reinterpret_cast<float(*)[kRedRows][64]>(smem),
+                     *reinterpret_cast<float(*)[64]>(smem + kRedRows * 64));
+}
+
 int reduce_blocks(const CsConvArgs& a) { return ((a.M + kRedRows - 1) / kRedRows) * ((a.N + 63) / 64); }
 
 // fold pre-pass for large split counts; returns (nslab, zstep) for the combine
@@ -968,7 +988,7 @@ hipError_t launch_gemm_m(const CsConvArgs& a, int splits, int stage, hipStream_t
   const size_t lds = MATH == 3   ? TileXS<BM, BN, MODE, BK>::BYTES
                      : MATH == 5 ? TileXS<BM, BN, MODE, BK, 1>::BYTES
                                  : 2 * T::STAGE * sizeof(float);
-  const dim3 grid(ntiles * splits + a.red.P + a.sgd.P);
+  const dim3 grid(ntiles * splits + a.red.P + a.sgd.P + a.ktail.P);
   constexpr bool deep_fits = (BM + BN) * BK * 4 * 5 < 160 * 1024;
   if constexpr (BK != 64 && MATH == 0) {
     if (MODE == CS_CONV_FWD && a.w_oihw)  // padded conv0: Cin = 4 < BK
@@ -1210,7 +1230,7 @@ int prep_gemm(CsConvArgs& a, int mode, int bk, int splits) {
 
 hipError_t cs_conv_gemm_dual(CsConvArgs wg, int wbk, int wsplits, CsConvArgs dg, int dbk, int dsplits,
                              hipStream_t stream, int stage) {
-  if (wg.red.P != 0 || dg.red.P != 0 || wg.sgd.n != 0 || dg.sgd.n != 0)
+  if (wg.red.P != 0 || dg.red.P != 0 || wg.sgd.n != 0 || dg.sgd.n != 0 || wg.ktail.M != 0 || dg.ktail.M != 0)
     return hipErrorInvalidValue;  // no appended work in dual launches
   if (wg.w_oihw) return hipErrorInvalidValue;  // conv0 has no data gradient
   wg.counters = dg.counters = nullptr;
@@ -1268,6 +1288,14 @@ hipError_t cs_conv_gemm(CsConvArgs a, int mode, int bm, int bn, int bk, int spli
   splits = prep_gemm(a, mode, bk, splits);
   if (splits < 0) return hipErrorInvalidValue;
   a.sgd.P = a.sgd.n > 0 ? (int)std::min<int64_t>(256, (a.sgd.n / 4 + 255) / 256) : 0;
+  if (a.ktail.M > 0) {
+    if (a.ktail.ws == nullptr || a.ktail.out == nullptr || a.ktail.N % 4 || a.ktail.nslab < 1 ||
+        a.ktail.nslab > 2 * kFold)
+      return hipErrorInvalidValue;
+    a.ktail.P = ((a.ktail.M + kRedRows - 1) / kRedRows) * ((a.ktail.N + 63) / 64);
+  } else {
+    a.ktail.P = 0;
+  }
   // (BN-backward partials from a split-K data gradient come out of the combine launch)
   if (!cs_conv_fixup_ok(splits, bm, bn) || a.ered.part != nullptr) a.counters = nullptr;
 #define CS_DISPATCH(BM_, BN_, BK_)                                                                       \

@@ -79,6 +79,15 @@ struct CsSgdTail {
   int first, P;
 };
 
+// The deterministic split-K combine of ANOTHER (weight-gradient, standard-layout) GEMM carried
+// by blocks appended to a launch: out[M][N] = sum over nslab slabs of ws (z order, bit-equal to
+// the combine launch); P blocks (the launcher sizes it when M > 0).
+struct CsSplitkTail {
+  const float* ws;
+  float* out;
+  int M, N, nslab, P;
+};
+
 struct CsConvArgs {
   const float* x;     // FWD / WGRAD: conv input, NHWC [B,H,W,Cin] (Cin = 4 for the padded conv0 input)
   const float* w;     // FWD / DGRAD: weights, OHWI [Cout][9][Cin]; conv0 (w_oihw=1): OIHW [Cout][3][9]
@@ -103,6 +112,9 @@ struct CsConvArgs {
   // an independent SGD update appended to the launch (the serial world-1 step: block l+1's
   // parameters, whose last reader has run, ride block l's weight-gradient GEMM)
   CsSgdTail sgd;
+  // the split-K combine of block l's weight gradient riding block l's data-gradient launch (the
+  // serial step: the two GEMMs are independent)
+  CsSplitkTail ktail;
   // pre-split operands (conv_xp.hip): P3 bf16 chunks [n/8][3][8] (h, m, l of every 8 elements)
   const uint16_t* x3;   // FWD / WGRAD: split conv input
   const uint16_t* w3;   // FWD / DGRAD: split OHWI weights

@@ -206,6 +206,7 @@ VggEngine::VggEngine(int64_t Bmax, std::vector<int64_t> desc, std::vector<int64_
   if (const char* e = getenv("CS_BN_EPI_RED")) epi_red_ = atoi(e) != 0;
   if (const char* e = getenv("CS_SGD_SLABS")) sgd_slabs_on_ = atoi(e) != 0;
   if (const char* e = getenv("CS_SGD_TAIL")) sgd_tail_on_ = atoi(e) != 0;
+  if (const char* e = getenv("CS_KTAIL")) ktail_on_ = atoi(e) != 0;
   grid_bar_ = torch::zeros({2 * kCsBnGridBarInts}, fo.dtype(at::kInt));  // backward set, forward set
   {
     void* h = nullptr;
@@ -344,7 +345,8 @@ void VggEngine::set_perm(torch::Tensor perm) {
 }
 
 void VggEngine::conv(int l, int mode, int B, const ConvTile& t, hipStream_t s, bool with_stats, float* ws,
-                     float* dz, bool keep_slabs, const CsBnRed* red, const CsBnRed* ered, const CsSgdTail* sgd) {
+                     float* dz, bool keep_slabs, const CsBnRed* red, const CsBnRed* ered, const CsSgdTail* sgd,
+                     const CsSplitkTail* ktail) {
   VggBlock& b = blocks_[l];
   CsConvArgs a = conv_args(l, mode, B, with_stats, ws, dz);
   a.keep_slabs = keep_slabs ? 1 : 0;
@@ -354,6 +356,7 @@ void VggEngine::conv(int l, int mode, int B, const ConvTile& t, hipStream_t s, b
     a.ered = *ered;
   }
   if (sgd != nullptr) a.sgd = *sgd;
+  if (ktail != nullptr) a.ktail = *ktail;
   const Dims d = dims(b, mode, B);
   const int sp = eff_splits(d.K, t.splits, t.bk);
   TORCH_CHECK(sp == 1 || (int64_t)sp * d.M * d.N <= ws_elems_, "VggEngine: split-K workspace too small");
@@ -657,7 +660,13 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
         sgd_slabs_.ns[k] = spw;
         keep_used_ += spw * slab;
       } else {
-        conv(l, CS_CONV_WGRAD, (int)B, tw, s, false, ws_side_.data_ptr<float>(), dz, false, nullptr, nullptr, tp);
+        // with a split K (no fold, not conv0's OIHW scatter) the combine rides this block's
+        // data-gradient launch below (independent of it) instead of a launch of its own
+        const bool kt = ktail_on_ && in_step_ && l > 0 && spw > 1 && spw <= 32 && !dual_ok(l);
+        conv(l, CS_CONV_WGRAD, (int)B, tw, s, false, ws_side_.data_ptr<float>(), dz, kt, nullptr, nullptr, tp);
+        if (kt) {
+          pend_ktail_ = CsSplitkTail{ws_side_.data_ptr<float>(), G(b.w_off), (int)dw.M, (int)dw.N, spw, 0};
+        }
       }
     }
     if (l > 0) {
@@ -665,7 +674,10 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
       const Dims d = dims(b, CS_CONV_DGRAD, B);
       const int sp = eff_splits(d.K, t.splits, t.bk);
       const bool keep = !er && keep_slabs_ && bn_path_ != 1 && sp > 1 && sp <= 32;
-      conv(l, CS_CONV_DGRAD, (int)B, t, s, false, nullptr, dz, keep, nullptr, er ? &erv : nullptr);
+      const CsSplitkTail kt = pend_ktail_;
+      pend_ktail_ = CsSplitkTail{};
+      conv(l, CS_CONV_DGRAD, (int)B, t, s, false, nullptr, dz, keep, nullptr, er ? &erv : nullptr, nullptr,
+           kt.M > 0 ? &kt : nullptr);
       if (keep) {
         g_slabs_ = sp;
         g_stride_ = d.M * d.N;

@@ -146,7 +146,14 @@ class VggEngine {
  private:
   void conv(int l, int mode, int B, const ConvTile& t, hipStream_t s, bool with_stats, float* ws = nullptr,
             float* dz = nullptr, bool keep_slabs = false, const CsBnRed* red = nullptr,
-            const CsBnRed* ered = nullptr, const CsSgdTail* sgd = nullptr);
+            const CsBnRed* ered = nullptr, const CsSgdTail* sgd = nullptr, const CsSplitkTail* ktail = nullptr);
+  // Serial step: block l's split-K weight-gradient combine rides block l's data-gradient launch as
+  // appended blocks (the GEMMs are independent; the combined gradient's first reader is block l's
+  // SGD, later) — one launch fewer per split-K weight gradient. Opt-in (CS_KTAIL=1): bit-equal, but
+  // measured 83.7k vs 84.1k img/s (profiles/r3_overlap_ab.txt) — the appended slab-summing blocks
+  // share the CUs with the data gradient on the critical chain.
+  bool ktail_on_ = false;
+  CsSplitkTail pend_ktail_{};
   // Block l-1's BN-backward partial sums computed where block l's data gradient is finished —
   // in the dgrad GEMM's epilogue, or in its split-K combine (CsConvArgs::ered) — instead of a
   // reduce launch re-reading G and y; the BN backward of block l-1 is then finalize + apply,

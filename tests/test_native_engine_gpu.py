@@ -375,6 +375,27 @@ def test_bn_partials_from_dgrad_match_reduce_pass(dev, tiles, monkeypatch):
         assert torch.equal(x, y)
 
 
+@pytest.mark.parametrize("tiles", ["shipped", "split"])
+def test_wgrad_combine_in_dgrad_launch_bitwise_equal(dev, tiles, monkeypatch):
+    """Serial step: block l's split-K weight-gradient combine as blocks appended to block l's
+    data-gradient launch (CS_KTAIL=1, opt-in) == its own combine launch, bit for bit."""
+    out = []
+    for on in ("0", "1"):
+        monkeypatch.setenv("CS_KTAIL", on)
+        t = _trainer(dev, batch_size=64, train_size=512, autotune=tiles == "shipped")
+        if tiles == "split":  # f32 and X6S weight gradients with 2..32 slabs, 256- and 1024-thread dgrads
+            for l in range(1, t.layout.L):
+                t.engine.set_tile(l, 2, 64, 64, [2, 32, 16, 8, 5, 3, 4][l - 1], 32 if l % 2 else 64,
+                                  0 if l % 2 else (16 | 4))
+                t.engine.set_tile(l, 1, 64, 64, 1, 64 if l % 2 else 16, (16 | 4) if l % 2 else 0)
+        for _ in range(3):
+            t.step()
+        torch.cuda.synchronize()
+        out.append((t.params.clone(), t.mom.clone(), t.grads.clone(), t.bufs.clone()))
+    for a, b in zip(*out):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("tiles", ["shipped", "default"])
 def test_sgd_in_wgrad_tails_bitwise_equal(dev, tiles, monkeypatch):
     """World-1 serial step: block l+1's SGD as blocks appended to block l's weight-gradient
