@@ -4,7 +4,8 @@ ResNet family's native path (``csrc/kernels/cnn_nhwc.hip``; models/resnet.py ``l
 Activations are contiguous ``[B, H, W, C]`` tensors (fp32, or bf16 under autocast). A bf16
 convolution with C, Cout % 32 == 0 that is not a plain 1x1/stride-1 one runs as the gfx950
 implicit-GEMM kernel (``csrc/kernels/conv_nhwc.hip``: forward, data and weight gradient gather
-their operands straight from the activations, no patch matrix in memory); the others are one
+their operands straight from the activations, no patch matrix in memory), and so does the
+4-channel stem (its C4 mode); the others are one
 GEMM on MI355X's matrix cores (hipBLASLt via ``torch.mm``):
 
 * 1x1 / stride 1: the activation *is* the ``[B*H*W, Cin]`` operand, no copy;
@@ -125,9 +126,66 @@ class _ConvImplicitNHWC(torch.autograd.Function):
         return dx, dw, None, None
 
 
-class _ConvNHWC(torch.autograd.Function):
+def _stem_ok(x: torch.Tensor, Ci: int, Co: int, S: int) -> bool:
+    """the 4-channel stem (image + a zero channel) as the implicit-GEMM kernel's C4 mode: forward and
+    weight gradient without the [B*Ho*Wo, R*S*4] patch matrix (1.3 GB for ResNet-50 at B=256, written
+    by im2col and read twice). The image needs no gradient. CS_CONV_IMPLICIT=0 or CS_CONV_STEM=0 disables."""
+    return (os.environ.get("CS_CONV_IMPLICIT", "1") != "0" and os.environ.get("CS_CONV_STEM", "1") != "0"
+            and act_dtype(x) == torch.bfloat16 and x.shape[3] == 4
+            and Ci <= 4 and S <= 8 and Co % 32 == 0 and not x.requires_grad)
+
+
+class _ConvStemNHWC(torch.autograd.Function):
+    """C4 mode of csrc/kernels/conv_nhwc.hip: kernel rows padded to 8 taps of 4 channels (K = R*32),
+    weight [Co, R, 8, 4]; saves only the image"""
+
     @staticmethod
     def forward(ctx, x, weight, stride: int, pad: int):
+        Co, Ci, R, S = weight.shape
+        w4 = F.pad(weight.permute(0, 2, 3, 1), (0, 4 - Ci, 0, 8 - S)).to(torch.bfloat16).contiguous()
+        y = native.C().conv_nhwc_bf16(0, x, w4, R, S, stride, pad, 0, 0)
+        ctx.save_for_backward(x)
+        ctx.geo = (Co, Ci, R, S, stride, pad)
+        ctx.wdtype = weight.dtype
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        Co, Ci, R, S, stride, pad = ctx.geo
+        dw = None
+        if ctx.needs_input_grad[1]:
+            dwf = native.C().conv_nhwc_bf16(2, dy.to(torch.bfloat16).contiguous(), x, R, S, stride, pad, 0, 0)
+            dw = torch.empty((Co, Ci, R, S), dtype=ctx.wdtype, device=dy.device)
+            dw.copy_(dwf.view(Co, R, 8, 4)[:, :, :S, :Ci].permute(0, 3, 1, 2))
+        return None, dw, None, None
+
+
+class ResidualGradSink(torch.autograd.Function):
+    """Identity on the residual branch of a block whose first conv is a plain 1x1 (ResNet
+    bottleneck): the residual's gradient is handed to that conv's backward through ``box``, which
+    adds it in its data-gradient GEMM (``addmm``, beta = 1) instead of autograd summing the two
+    gradients of the block input in a separate elementwise pass (3 activation-sized passes -> 1).
+    Whichever of the two backward nodes runs first decides: if the conv's backward already ran,
+    this one returns the gradient itself and autograd adds as usual."""
+
+    @staticmethod
+    def forward(ctx, x, box: dict):
+        ctx.box = box
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        box = ctx.box
+        if box.get("done"):
+            return g, None
+        box["g"] = g
+        return None, None
+
+
+class _ConvNHWC(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, stride: int, pad: int, box: Optional[dict] = None):
         B, H, W, C = x.shape
         Co, Ci, R, S = weight.shape
         # x may carry zero channels beyond the weight's (the stem's 3 -> 4, for vector access)
@@ -152,6 +210,7 @@ class _ConvNHWC(torch.autograd.Function):
         ctx.save_for_backward(col, wf)
         ctx.geo = (B, H, W, C, Ci, Co, R, S, stride, pad, K, direct)
         ctx.wdtype = weight.dtype
+        ctx.box = box
         return y.view(B, Ho, Wo, Co)
 
     @staticmethod
@@ -174,13 +233,25 @@ class _ConvNHWC(torch.autograd.Function):
                     dw.copy_(dwf[:, :K].reshape(Co, R, S, C)[..., :Ci].permute(0, 3, 1, 2))
             if ctx.needs_input_grad[0]:
                 assert Ci == C, "conv_nhwc: no data gradient through padded input channels"
-                dcol = torch.mm(dy2, wf)  # [M, Kp]
+                box = ctx.box
+                gres = box.pop("g", None) if box is not None and direct else None
+                if box is not None:
+                    box["done"] = True  # a ResidualGradSink running after this returns its gradient
+                    box["fused"] = gres is not None
+                if gres is not None and gres.dtype == dy2.dtype and gres.is_contiguous():
+                    dcol = torch.addmm(gres.view(-1, C), dy2, wf)  # dx + the residual's gradient, one GEMM
+                else:
+                    dcol = torch.mm(dy2, wf)  # [M, Kp]
+                    if gres is not None:
+                        dcol = dcol + gres.reshape(dcol.shape)
                 dx = dcol.view(B, H, W, C) if direct else native.C().col2im_nhwc(dcol, B, H, W, C, R, S, stride, pad)
-        return dx, dw, None, None
+        return dx, dw, None, None, None
 
 
-def conv_nhwc(x: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
-    """``conv(x)`` for a bias-free, ungrouped, undilated Conv2d on a [B, H, W, C] tensor"""
+def conv_nhwc(x: torch.Tensor, conv: nn.Conv2d, grad_box: Optional[dict] = None) -> torch.Tensor:
+    """``conv(x)`` for a bias-free, ungrouped, undilated Conv2d on a [B, H, W, C] tensor;
+    ``grad_box``: the box of a ResidualGradSink on the same input (plain 1x1 convs take its
+    gradient into their data-gradient GEMM)"""
     assert conv.bias is None and conv.groups == 1 and conv.dilation == (1, 1), "conv_nhwc: unsupported Conv2d"
     assert conv.stride[0] == conv.stride[1] and conv.padding[0] == conv.padding[1], "conv_nhwc: square stride/pad"
     if not x.is_cuda:
@@ -190,22 +261,37 @@ def conv_nhwc(x: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
     st, pad = int(conv.stride[0]), int(conv.padding[0])
     if _implicit_ok(act_dtype(x), x.shape[3], Ci, Co, R, S, st, pad):
         return _ConvImplicitNHWC.apply(x.to(torch.bfloat16).contiguous(), conv.weight, st, pad)
-    return _ConvNHWC.apply(x, conv.weight, st, pad)
+    if _stem_ok(x, Ci, Co, S):
+        return _ConvStemNHWC.apply(x.to(torch.bfloat16).contiguous(), conv.weight, st, pad)
+    return _ConvNHWC.apply(x, conv.weight, st, pad, grad_box)
+
+
+def residual_sink_ok(x: torch.Tensor, conv: nn.Conv2d) -> bool:
+    """whether the block input x can hand its residual gradient to the plain 1x1 ``conv`` on it"""
+    return (x.is_cuda and x.requires_grad and torch.is_grad_enabled() and os.environ.get("CS_RES_SINK", "1") != "0"
+            and tuple(conv.kernel_size) == (1, 1) and tuple(conv.stride) == (1, 1) and tuple(conv.padding) == (0, 0))
 
 
 class _BnActNHWC(torch.autograd.Function):
+    """relu(bn(x) + residual): with a residual and ReLU the forward also writes the ReLU mask (one
+    bit per element), and the backward's two passes read it instead of the residual to rebuild the
+    mask (CS_BN_MASK=0: recompute from x and the residual)"""
+
     @staticmethod
     def forward(ctx, x, weight, bias, residual, running_mean, running_var, nbt, momentum, eps, relu):
-        y, stat = native.C().bn_nhwc_fwd(x, residual, weight, bias, running_mean, running_var, nbt, momentum, eps, relu)
-        ctx.save_for_backward(x, residual, weight, stat)
+        use_mask = relu and residual is not None and os.environ.get("CS_BN_MASK", "1") != "0"
+        y, stat, mask = native.C().bn_nhwc_fwd(x, residual, weight, bias, running_mean, running_var, nbt, momentum,
+                                               eps, relu, use_mask)
+        ctx.save_for_backward(x, None if use_mask else residual, weight, stat, mask if use_mask else None)
         ctx.relu = relu
         ctx.has_res = residual is not None
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, residual, weight, stat = ctx.saved_tensors
-        dx, dres, dw, db = native.C().bn_nhwc_bwd(dy.contiguous(), x, residual, weight, stat, ctx.relu, ctx.has_res)
+        x, residual, weight, stat, mask = ctx.saved_tensors
+        dx, dres, dw, db = native.C().bn_nhwc_bwd(dy.contiguous(), x, residual, weight, stat, ctx.relu, ctx.has_res,
+                                                  mask)
         return (dx, dw, db, dres if ctx.has_res else None, None, None, None, None, None, None)
 
 

@@ -55,7 +55,9 @@ torch::Tensor conv_nhwc_bf16(int64_t mode, torch::Tensor a, torch::Tensor b, int
   torch::Tensor out, ws;
   if (mode == 0) {
     p.B = (int)a.size(0), p.H = (int)a.size(1), p.W = (int)a.size(2), p.C = (int)a.size(3), p.Co = (int)b.size(0);
-    TORCH_CHECK(b.size(1) == R && b.size(2) == S && b.size(3) == p.C, "conv_nhwc_bf16: weight [Co, R, S, C]");
+    // the 4-channel stem: kernel rows padded to 8 taps, weight [Co, R, 8, 4]
+    TORCH_CHECK(b.size(1) == R && b.size(2) == (p.C == 4 ? 8 : S) && b.size(3) == p.C,
+                "conv_nhwc_bf16: weight [Co, R, S, C] ([Co, R, 8, 4] for a 4-channel input)");
     const int64_t Ho = (p.H + 2 * pad - R) / stride + 1, Wo = (p.W + 2 * pad - S) / stride + 1;
     out = torch::empty({p.B, Ho, Wo, p.Co}, a.options());
     p.x = a.data_ptr();
@@ -76,8 +78,9 @@ torch::Tensor conv_nhwc_bf16(int64_t mode, torch::Tensor a, torch::Tensor b, int
                     a.size(2) == (p.W + 2 * pad - S) / stride + 1,
                 "conv_nhwc_bf16: dy / x shapes");
     const int sp = cs_conv_nhwc_splits(2, p.B, p.H, p.W, p.C, p.Co, p.R, p.S, p.st, p.pad);
-    ws = torch::empty({(int64_t)sp * p.Co * R * S * p.C}, a.options().dtype(at::kFloat));
-    out = torch::empty({p.Co, R * S * p.C}, a.options().dtype(at::kFloat));
+    const int64_t kc = p.C == 4 ? R * 32 : R * S * p.C;  // (r, s < 8, c < 4) columns for the stem
+    ws = torch::empty({(int64_t)sp * p.Co * kc}, a.options().dtype(at::kFloat));
+    out = torch::empty({p.Co, kc}, a.options().dtype(at::kFloat));
     p.dy = a.data_ptr();
     p.x = b.data_ptr();
     p.dw = ws.data_ptr<float>();
@@ -89,11 +92,12 @@ torch::Tensor conv_nhwc_bf16(int64_t mode, torch::Tensor a, torch::Tensor b, int
   return out;
 }
 
-// -> {y, stat [4, C] = scale, shift, mean, invstd}
+// -> {y, stat [4, C] = scale, shift, mean, invstd, ReLU mask (with_mask; else undefined)}
 std::vector<torch::Tensor> bn_nhwc_fwd(torch::Tensor x, c10::optional<torch::Tensor> res,
                                        c10::optional<torch::Tensor> w, c10::optional<torch::Tensor> b,
                                        c10::optional<torch::Tensor> rm, c10::optional<torch::Tensor> rv,
-                                       c10::optional<torch::Tensor> nbt, double momentum, double eps, bool relu) {
+                                       c10::optional<torch::Tensor> nbt, double momentum, double eps, bool relu,
+                                       bool with_mask) {
   check_nhwc(x, "bn_nhwc_fwd");
   const int dt = act_dt(x, "bn_nhwc_fwd");
   const int64_t C = x.size(3), M = x.numel() / C;
@@ -112,16 +116,19 @@ std::vector<torch::Tensor> bn_nhwc_fwd(torch::Tensor x, c10::optional<torch::Ten
   auto y = torch::empty_like(x);
   auto stat = torch::empty({4, C}, fo);
   auto part = torch::empty({cs_bn_nhwc_partials(M, (int)C, dt)}, fo);
+  torch::Tensor mask;
+  if (with_mask) mask = torch::empty({M * C / cs_bn_nhwc_vec((int)C, dt)}, x.options().dtype(at::kByte));
   CS_LAUNCH(cs_bn_nhwc_fwd(dt, x.data_ptr(), has_res ? res->data_ptr() : nullptr, opt_ptr<float>(w), opt_ptr<float>(b),
                            opt_ptr<float>(rm), opt_ptr<float>(rv), opt_ptr<int64_t>(nbt), (float)momentum, (float)eps,
                            relu ? 1 : 0, y.data_ptr(), stat.data_ptr<float>(), part.data_ptr<float>(), M, (int)C,
-                           cur_stream()));
-  return {y, stat};
+                           cur_stream(), with_mask ? mask.data_ptr<uint8_t>() : nullptr));
+  return {y, stat, mask};
 }
 
 // -> {dx, dres (or undefined), dweight, dbias}
 std::vector<torch::Tensor> bn_nhwc_bwd(torch::Tensor dy, torch::Tensor x, c10::optional<torch::Tensor> res,
-                                       c10::optional<torch::Tensor> w, torch::Tensor stat, bool relu, bool need_dres) {
+                                       c10::optional<torch::Tensor> w, torch::Tensor stat, bool relu, bool need_dres,
+                                       c10::optional<torch::Tensor> mask) {
   check_nhwc(x, "bn_nhwc_bwd");
   const int dt = act_dt(x, "bn_nhwc_bwd");
   check_like(dy, x, "dy");
@@ -130,6 +137,11 @@ std::vector<torch::Tensor> bn_nhwc_bwd(torch::Tensor dy, torch::Tensor x, c10::o
   const int64_t C = x.size(3), M = x.numel() / C;
   check_param(w, C, "weight");
   TORCH_CHECK(stat.is_cuda() && stat.scalar_type() == at::kFloat && stat.numel() == 4 * C, "bn_nhwc_bwd: stat");
+  const bool has_mask = mask.has_value() && mask->defined();
+  if (has_mask)
+    TORCH_CHECK(relu && mask->is_cuda() && mask->scalar_type() == at::kByte &&
+                    mask->numel() == M * C / cs_bn_nhwc_vec((int)C, dt),
+                "bn_nhwc_bwd: mask from bn_nhwc_fwd(with_mask=True) of this activation");
   DevGuard g(x.device());
   auto fo = x.options().dtype(at::kFloat);
   auto dx = torch::empty_like(x);
@@ -140,7 +152,7 @@ std::vector<torch::Tensor> bn_nhwc_bwd(torch::Tensor dy, torch::Tensor x, c10::o
   CS_LAUNCH(cs_bn_nhwc_bwd(dt, dy.data_ptr(), x.data_ptr(), has_res ? res->data_ptr() : nullptr, opt_ptr<float>(w),
                            stat.data_ptr<float>(), relu ? 1 : 0, dx.data_ptr(), need_dres ? dres.data_ptr() : nullptr,
                            dw.data_ptr<float>(), db.data_ptr<float>(), coef.data_ptr<float>(), part.data_ptr<float>(),
-                           M, (int)C, cur_stream()));
+                           M, (int)C, cur_stream(), has_mask ? mask->data_ptr<uint8_t>() : nullptr));
   return {dx, dres, dw, db};
 }
 
@@ -213,9 +225,14 @@ torch::Tensor col2im_nhwc(torch::Tensor dcol, int64_t B, int64_t H, int64_t W, i
 void register_nhwc_ops(pybind11::module& m) {
   m.def("conv_nhwc_bf16", &conv_nhwc_bf16,
         "bf16 NHWC implicit-GEMM conv: mode 0 fwd (a=x, b=w[Co,R,S,C]) -> y; 1 dgrad (a=dy, b=wt[C,R,S,Co]) -> dx; "
-        "2 wgrad (a=dy, b=x) -> fp32 dW [Co, R*S*C]");
-  m.def("bn_nhwc_fwd", &bn_nhwc_fwd, "training BatchNorm2d (+residual) (+ReLU), NHWC fp32/bf16 -> (y, stat)");
-  m.def("bn_nhwc_bwd", &bn_nhwc_bwd, "its backward -> (dx, dres, dweight, dbias)");
+        "2 wgrad (a=dy, b=x) -> fp32 dW [Co, R*S*C]; a 4-channel x (the stem, S <= 8) uses kernel rows padded "
+        "to 8 taps: weight [Co, R, 8, 4], dW [Co, R*32]");
+  m.def("bn_nhwc_fwd", &bn_nhwc_fwd, "training BatchNorm2d (+residual) (+ReLU), NHWC fp32/bf16 -> (y, stat, mask)",
+        pybind11::arg("x"), pybind11::arg("res"), pybind11::arg("w"), pybind11::arg("b"), pybind11::arg("rm"), pybind11::arg("rv"), pybind11::arg("nbt"),
+        pybind11::arg("momentum"), pybind11::arg("eps"), pybind11::arg("relu"), pybind11::arg("with_mask") = false);
+  m.def("bn_nhwc_bwd", &bn_nhwc_bwd, "its backward -> (dx, dres, dweight, dbias); mask: the forward's ReLU mask",
+        pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("res"), pybind11::arg("w"), pybind11::arg("stat"), pybind11::arg("relu"),
+        pybind11::arg("need_dres"), pybind11::arg("mask") = pybind11::none());
   m.def("maxpool3s2_nhwc_fwd", &maxpool3s2_nhwc_fwd, "3x3/2 pad-1 max-pool, NHWC -> (y, window position)");
   m.def("maxpool3s2_nhwc_bwd", &maxpool3s2_nhwc_bwd, "its gather-style backward");
   m.def("im2col_nhwc", &im2col_nhwc, "NHWC im2col -> [B*Ho*Wo, Kp], columns (r, s, c)");

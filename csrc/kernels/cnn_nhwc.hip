@@ -191,7 +191,8 @@ __global__ __launch_bounds__(256) void finalize_fwd_kernel(const T* __restrict__
 template <typename T, int V>
 __global__ __launch_bounds__(256) void apply_fwd_kernel(const T* __restrict__ x, const T* __restrict__ res,
                                                         const float* __restrict__ stat, T* __restrict__ y,
-                                                        int64_t M, int C, int rpb, int relu) {
+                                                        int64_t M, int C, int rpb, int relu,
+                                                        unsigned char* __restrict__ mask) {
   const RowSplit s = row_split(C, V);
   if (s.rl >= s.lanes) return;
   float sc[V], sf[V];
@@ -207,12 +208,15 @@ __global__ __launch_bounds__(256) void apply_fwd_kernel(const T* __restrict__ x,
     float v[V], rr[V];
     ldv<T, V>(x + e, v);
     if (res != nullptr) ldv<T, V>(res + e, rr);
+    unsigned live = 0;
 #pragma unroll
     for (int j = 0; j < V; ++j) {
       const float z = preact(v[j], sc[j], sf[j], res != nullptr ? rr[j] : 0.f);
+      live |= (z > 0.f ? 1u : 0u) << j;
       v[j] = relu && !(z > 0.f) ? 0.f : z;
     }
     stv<T, V>(y + e, v);
+    if (mask != nullptr) mask[e / V] = (unsigned char)live;
   }
 }
 
@@ -221,6 +225,7 @@ template <typename T, int V>
 __global__ __launch_bounds__(256) void bwd_reduce_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                          const T* __restrict__ res, const float* __restrict__ stat,
                                                          int64_t M, int C, int rpb, int relu,
+                                                         const unsigned char* __restrict__ mask,
                                                          float* __restrict__ part) {
   __shared__ float sh[256 * kMaxV * 2];
   const RowSplit s = row_split(C, V);
@@ -242,10 +247,13 @@ __global__ __launch_bounds__(256) void bwd_reduce_kernel(const T* __restrict__ d
       float g[V], v[V], rr[V];
       ldv<T, V>(dy + off, g);
       ldv<T, V>(x + off, v);
-      if (relu && res != nullptr) ldv<T, V>(res + off, rr);
+      unsigned live = 0;
+      if (mask != nullptr) live = mask[off / V];
+      else if (relu && res != nullptr) ldv<T, V>(res + off, rr);
 #pragma unroll
       for (int j = 0; j < V; ++j) {
-        if (relu && !(preact(v[j], sc[j], sf[j], res != nullptr ? rr[j] : 0.f) > 0.f)) g[j] = 0.f;
+        if (mask != nullptr ? !((live >> j) & 1u) : relu && !(preact(v[j], sc[j], sf[j], res != nullptr ? rr[j] : 0.f) > 0.f))
+          g[j] = 0.f;
         sg[j] += g[j];
         sgx[j] = fmaf(g[j], (v[j] - mu[j]) * is[j], sgx[j]);
       }
@@ -297,7 +305,8 @@ template <typename T, int V>
 __global__ __launch_bounds__(256) void apply_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                         const T* __restrict__ res, const float* __restrict__ stat,
                                                         const float* __restrict__ coef, T* __restrict__ dx,
-                                                        T* __restrict__ dres, int64_t M, int C, int rpb, int relu) {
+                                                        T* __restrict__ dres, int64_t M, int C, int rpb, int relu,
+                                                        const unsigned char* __restrict__ mask) {
   const RowSplit s = row_split(C, V);
   if (s.rl >= s.lanes) return;
   float sc[V], sf[V], mu[V], is[V], k[V], mg[V], mgx[V];
@@ -319,10 +328,13 @@ __global__ __launch_bounds__(256) void apply_bwd_kernel(const T* __restrict__ dy
     float g[V], v[V], rr[V];
     ldv<T, V>(dy + e, g);
     ldv<T, V>(x + e, v);
-    if (relu && res != nullptr) ldv<T, V>(res + e, rr);
+    unsigned live = 0;
+    if (mask != nullptr) live = mask[e / V];
+    else if (relu && res != nullptr) ldv<T, V>(res + e, rr);
 #pragma unroll
     for (int j = 0; j < V; ++j) {
-      if (relu && !(preact(v[j], sc[j], sf[j], res != nullptr ? rr[j] : 0.f) > 0.f)) g[j] = 0.f;
+      if (mask != nullptr ? !((live >> j) & 1u) : relu && !(preact(v[j], sc[j], sf[j], res != nullptr ? rr[j] : 0.f) > 0.f))
+        g[j] = 0.f;
       const float xhat = (v[j] - mu[j]) * is[j];
       v[j] = k[j] * (g[j] - mg[j] - xhat * mgx[j]);
     }
@@ -520,27 +532,28 @@ BnGrid apply_grid(int64_t M, int C, int V) {
 template <typename T, int V>
 void bn_fwd_t(const void* x, const void* res, const float* w, const float* b, float* rm, float* rv, int64_t* nbt,
               float momentum, float eps, int relu, void* y, float* stat, float* part, int64_t M, int C,
-              hipStream_t st) {
+              unsigned char* mask, hipStream_t st) {
   const BnGrid g = bn_grid(M, C, V);
   hipLaunchKernelGGL((stats_kernel<T, V>), dim3(g.P, g.CG), dim3(256), 0, st, (const T*)x, M, C, g.rpb, part);
   hipLaunchKernelGGL(finalize_fwd_kernel<T>, dim3((C + 7) / 8), dim3(256), 0, st, (const T*)x, part, g.P, C,
                      (double)M, w, b, rm, rv, momentum, eps, stat, nbt);
   const BnGrid a = apply_grid(M, C, V);
   hipLaunchKernelGGL((apply_fwd_kernel<T, V>), dim3(a.P, a.CG), dim3(256), 0, st, (const T*)x, (const T*)res, stat,
-                     (T*)y, M, C, a.rpb, relu);
+                     (T*)y, M, C, a.rpb, relu, mask);
 }
 
 template <typename T, int V>
 void bn_bwd_t(const void* dy, const void* x, const void* res, const float* w, const float* stat, int relu, void* dx,
-              void* dres, float* dw, float* db, float* coef, float* part, int64_t M, int C, hipStream_t st) {
+              void* dres, float* dw, float* db, float* coef, float* part, int64_t M, int C, const unsigned char* mask,
+              hipStream_t st) {
   const BnGrid g = bn_grid(M, C, V);
   hipLaunchKernelGGL((bwd_reduce_kernel<T, V>), dim3(g.P, g.CG), dim3(256), 0, st, (const T*)dy, (const T*)x,
-                     (const T*)res, stat, M, C, g.rpb, relu, part);
+                     (const T*)res, stat, M, C, g.rpb, relu, mask, part);
   hipLaunchKernelGGL(finalize_bwd_kernel, dim3((C + 7) / 8), dim3(256), 0, st, part, g.P, C, (double)M, w, stat, dw,
                      db, coef);
   const BnGrid a = apply_grid(M, C, V);
   hipLaunchKernelGGL((apply_bwd_kernel<T, V>), dim3(a.P, a.CG), dim3(256), 0, st, (const T*)dy, (const T*)x,
-                     (const T*)res, stat, coef, (T*)dx, (T*)dres, M, C, a.rpb, relu);
+                     (const T*)res, stat, coef, (T*)dx, (T*)dres, M, C, a.rpb, relu, mask);
 }
 
 // dispatch on (dtype, V) for a functor F<T, V>::run(args...)
@@ -562,6 +575,8 @@ void bn_bwd_t(const void* dy, const void* x, const void* res, const float* w, co
 
 }  // namespace
 
+int cs_bn_nhwc_vec(int C, int dt) { return vec_for(C, dt == CS_BF16 ? 2 : 4); }
+
 int cs_bn_nhwc_partials(int64_t M, int C, int dt) {
   const BnGrid g = bn_grid(M, C, vec_for(C, dt == CS_BF16 ? 2 : 4));
   return g.P * C * 2;
@@ -569,17 +584,17 @@ int cs_bn_nhwc_partials(int64_t M, int C, int dt) {
 
 hipError_t cs_bn_nhwc_fwd(int dt, const void* x, const void* res, const float* w, const float* b, float* rm, float* rv,
                           int64_t* nbt, float momentum, float eps, int relu, void* y, float* stat, float* part,
-                          int64_t M, int C, hipStream_t stream) {
+                          int64_t M, int C, hipStream_t stream, unsigned char* mask) {
   if (M * C == 0) return hipSuccess;
-  CS_NHWC_DISPATCH(dt, C, bn_fwd_t<T, V>(x, res, w, b, rm, rv, nbt, momentum, eps, relu, y, stat, part, M, C, stream));
+  CS_NHWC_DISPATCH(dt, C, bn_fwd_t<T, V>(x, res, w, b, rm, rv, nbt, momentum, eps, relu, y, stat, part, M, C, mask, stream));
   return hipGetLastError();
 }
 
 hipError_t cs_bn_nhwc_bwd(int dt, const void* dy, const void* x, const void* res, const float* w, const float* stat,
                           int relu, void* dx, void* dres, float* dw, float* db, float* coef, float* part, int64_t M,
-                          int C, hipStream_t stream) {
+                          int C, hipStream_t stream, const unsigned char* mask) {
   if (M * C == 0) return hipSuccess;
-  CS_NHWC_DISPATCH(dt, C, bn_bwd_t<T, V>(dy, x, res, w, stat, relu, dx, dres, dw, db, coef, part, M, C, stream));
+  CS_NHWC_DISPATCH(dt, C, bn_bwd_t<T, V>(dy, x, res, w, stat, relu, dx, dres, dw, db, coef, part, M, C, mask, stream));
   return hipGetLastError();
 }
 

@@ -12,6 +12,10 @@
 //          fp32 partial slabs [splits][Co][R*S*C], summed in split order by conv_nhwc_reduce
 //   k = (r, s, c) with c fastest (FWD / WGRAD), (r, s, co) for DGRAD; a 32-wide K-step never
 //   crosses a tap (C, Cout % 32 == 0), so its tap is wave-uniform.
+//   C4 (the stem: 4-channel image, FWD / WGRAD only): the taps of a kernel row are padded to 8, so
+//   k = (r, s < 8, c < 4), K = R*32 and a K-step is one kernel row r; a 16-byte chunk is two
+//   adjacent taps = two 8-byte pixel loads, each with its own bounds check (the weight's taps
+//   s >= S are zero; WGRAD's columns for them are computed and dropped by the caller).
 //
 // Tiling: 256 threads = 4 waves (2 x 2), block tile 128 x BN (BN 64 / 128), K-step 32, wave tile
 // 64 x BN/2 of 32x32 MFMA tiles. Global -> registers (next K-step's loads in flight during this
@@ -41,6 +45,16 @@ __device__ __forceinline__ rsrc_t rsrc(const void* p, int64_t bytes) {
 }
 __device__ __forceinline__ uint4 bload16(rsrc_t r, int off) {
   return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+__device__ __forceinline__ uint2 bload8(rsrc_t r, int off) {
+  return __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+}
+// two 4-channel pixels (iw, iw + 1) of image row (b*H + ih): 16 bytes, each half bounds-checked
+__device__ __forceinline__ uint4 pix_pair(rsrc_t r, bool okr, int rowbase, int iw, int W) {
+  const int o = (rowbase * W + iw) * 8;
+  const uint2 lo = bload8(r, okr && (unsigned)iw < (unsigned)W ? o : kOOB);
+  const uint2 hi = bload8(r, okr && (unsigned)(iw + 1) < (unsigned)W ? o + 8 : kOOB);
+  return make_uint4(lo.x, lo.y, hi.x, hi.y);
 }
 
 template <int MODE>
@@ -77,7 +91,7 @@ __device__ __forceinline__ void chunk_pos(int q, int& a, int& b) {
   }
 }
 
-template <int BM, int BN, int MODE>
+template <int BM, int BN, int MODE, bool C4>
 struct Stager {
   using G = Geo<BM, BN, MODE>;
   rsrc_t ra, rb;
@@ -144,7 +158,15 @@ struct Stager {
 
   // global -> registers for the K-step starting at k0 (GEMM K index)
   __device__ __forceinline__ void load(const CsConvNhwcArgs& p, int k0) {
-    if constexpr (MODE == CS_CONV_FWD) {
+    if constexpr (MODE == CS_CONV_FWD && C4) {
+      const int r = k0 >> 5;  // one kernel row per K-step; chunk cq = taps 2cq, 2cq + 1
+#pragma unroll
+      for (int i = 0; i < G::AC; ++i) {
+        const int ih = a1[i] + r, cq = (threadIdx.x + G::NT * i) & 3;
+        const bool okr = a0[i] >= 0 && (unsigned)ih < (unsigned)p.H;
+        va[i] = pix_pair(ra, okr, a0[i] + ih, a2[i] + 2 * cq, p.W);
+      }
+    } else if constexpr (MODE == CS_CONV_FWD) {
       const int tap = k0 / p.C, c0 = k0 - tap * p.C;
       const int r = tap / p.S, s = tap - r * p.S;
 #pragma unroll
@@ -177,6 +199,16 @@ struct Stager {
     if constexpr (MODE != CS_CONV_WGRAD) {
 #pragma unroll
       for (int i = 0; i < G::BC; ++i) vb[i] = bload16(rb, b0[i] >= 0 ? (b0[i] + k0) * 2 : kOOB);
+    } else if constexpr (C4) {
+#pragma unroll
+      for (int i = 0; i < G::BC; ++i) {
+        const int pix = k0 + (b0[i] >> 16), n = b0[i] & 0xffff;
+        const int ow = pix % p.Wo, t = pix / p.Wo, oh = t % p.Ho, b = t / p.Ho;
+        const int r = n >> 5, s = (n >> 2) & 7;  // n = (r, s, c): a chunk is taps s, s + 1 of row r
+        const int ih = oh * p.st - p.pad + r;
+        const bool okr = pix < p.K && n < p.N && (unsigned)ih < (unsigned)p.H;
+        vb[i] = pix_pair(rb, okr, b * p.H + ih, ow * p.st - p.pad + s, p.W);
+      }
     } else {
 #pragma unroll
       for (int i = 0; i < G::BC; ++i) {
@@ -232,7 +264,7 @@ __device__ __forceinline__ void frag(const __bf16* img, int base, int h, int lan
   }
 }
 
-template <int BM, int BN, int MODE>
+template <int BM, int BN, int MODE, bool C4>
 __global__ __launch_bounds__(256) void conv_nhwc_kernel(CsConvNhwcArgs p) {
   using G = Geo<BM, BN, MODE>;
   extern __shared__ __attribute__((aligned(16))) __bf16 lds[];
@@ -254,7 +286,7 @@ __global__ __launch_bounds__(256) void conv_nhwc_kernel(CsConvNhwcArgs p) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
-  Stager<BM, BN, MODE> st;
+  Stager<BM, BN, MODE, C4> st;
   st.init(p, m0, n0);
   if (kb < ke) {
     st.load(p, kb * BK);
@@ -318,25 +350,38 @@ __global__ __launch_bounds__(256) void conv_nhwc_kernel(CsConvNhwcArgs p) {
   }
 }
 
-// dW = sum of the split slabs in split order (deterministic), fp32 [M][N]
-__global__ __launch_bounds__(256) void conv_nhwc_reduce_kernel(const float* __restrict__ part, int splits, int64_t n4,
-                                                               float* __restrict__ out) {
+// dW = sum of the split slabs, fp32 [M][N]: a block is CB float4 columns x SL split lanes (CB*SL =
+// 256); lane l sums slabs l, l + SL, ... in order, then the SL lane sums are added in lane order
+// through LDS — a fixed order for a given split count (SL is a function of it): deterministic. The
+// stem's weight gradient has hundreds of slabs over a small [64][224] output, so the slabs are
+// spread over lanes as well as columns.
+__global__ __launch_bounds__(256) void conv_nhwc_reduce_kernel(const float* __restrict__ part, int splits, int SL,
+                                                               int64_t n4, float* __restrict__ out) {
+  __shared__ float4 sh[256];
+  const int CB = 256 / SL, cl = threadIdx.x % CB, sl = threadIdx.x / CB;
+  const int64_t i = (int64_t)blockIdx.x * CB + cl;
   const float4* p4 = reinterpret_cast<const float4*>(part);
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
-    float4 a = p4[i];
-    for (int z = 1; z < splits; ++z) {
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (i < n4)
+    for (int z = sl; z < splits; z += SL) {
       const float4 t = p4[(int64_t)z * n4 + i];
       a.x += t.x; a.y += t.y; a.z += t.z; a.w += t.w;
     }
-    reinterpret_cast<float4*>(out)[i] = a;
+  sh[threadIdx.x] = a;
+  __syncthreads();
+  if (sl != 0 || i >= n4) return;
+  for (int l = 1; l < SL; ++l) {
+    const float4 t = sh[l * CB + cl];
+    a.x += t.x; a.y += t.y; a.z += t.z; a.w += t.w;
   }
+  reinterpret_cast<float4*>(out)[i] = a;
 }
 
-template <int BM, int BN, int MODE>
+template <int BM, int BN, int MODE, bool C4 = false>
 hipError_t launch(const CsConvNhwcArgs& p, int splits, hipStream_t stream) {
   using G = Geo<BM, BN, MODE>;
   const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
-  hipLaunchKernelGGL((conv_nhwc_kernel<BM, BN, MODE>), dim3(tiles * splits), dim3(256), G::LDS, stream, p);
+  hipLaunchKernelGGL((conv_nhwc_kernel<BM, BN, MODE, C4>), dim3(tiles * splits), dim3(256), G::LDS, stream, p);
   return hipGetLastError();
 }
 
@@ -346,20 +391,23 @@ int cs_conv_nhwc_splits(int mode, int B, int H, int W, int C, int Co, int R, int
   if (mode != CS_CONV_WGRAD) return 1;
   const int Ho = (H + 2 * pad - R) / st + 1, Wo = (W + 2 * pad - S) / st + 1;
   const int64_t pix = (int64_t)B * Ho * Wo, ksteps = (pix + BK - 1) / BK;
-  const int64_t tiles = (int64_t)((Co + 127) / 128) * ((R * S * C + 127) / 128);
+  const int64_t kc = C == 4 ? (int64_t)R * 32 : (int64_t)R * S * C;
+  const int64_t tiles = (int64_t)((Co + 127) / 128) * ((kc + 127) / 128);
   int64_t s = 1;  // ~2 waves of 256 CUs, >= 8 K-steps per split, slabs within 1 GiB
-  while (tiles * s * 2 <= 1024 && ksteps / (2 * s) >= 8 && 2 * s * Co * (int64_t)R * S * C * 4 <= (1ll << 30)) s *= 2;
+  while (tiles * s * 2 <= 1024 && ksteps / (2 * s) >= 8 && 2 * s * Co * kc * 4 <= (1ll << 30)) s *= 2;
   return (int)s;
 }
 
 hipError_t cs_conv_nhwc(int mode, const CsConvNhwcArgs& in, int splits, hipStream_t stream) {
   CsConvNhwcArgs p = in;
-  if (p.C % 32 || p.Co % 32 || p.R < 1 || p.S < 1 || p.st < 1 || p.pad < 0) return hipErrorInvalidValue;
+  // C4: the 4-channel stem, forward and weight gradient, kernel rows of at most 8 taps
+  const bool c4 = p.C == 4 && p.S <= 8 && mode != CS_CONV_DGRAD;
+  if ((p.C % 32 && !c4) || p.Co % 32 || p.R < 1 || p.S < 1 || p.st < 1 || p.pad < 0) return hipErrorInvalidValue;
   p.Ho = (p.H + 2 * p.pad - p.R) / p.st + 1;
   p.Wo = (p.W + 2 * p.pad - p.S) / p.st + 1;
   if (p.Ho < 1 || p.Wo < 1) return hipErrorInvalidValue;
   const int64_t xe = (int64_t)p.B * p.H * p.W * p.C, ye = (int64_t)p.B * p.Ho * p.Wo * p.Co;
-  const int64_t kc = (int64_t)p.R * p.S * p.C;
+  const int64_t kc = c4 ? (int64_t)p.R * 32 : (int64_t)p.R * p.S * p.C;
   if (mode == CS_CONV_FWD) {
     p.M = (int)((int64_t)p.B * p.Ho * p.Wo);
     p.N = p.Co;
@@ -387,7 +435,12 @@ hipError_t cs_conv_nhwc(int mode, const CsConvNhwcArgs& in, int splits, hipStrea
   if (mode != CS_CONV_WGRAD && p.y == nullptr) return hipErrorInvalidValue;
   const bool wide = p.N >= 128 && p.N % 128 == 0;
   hipError_t e;
-  if (mode == CS_CONV_FWD)
+  if (c4 && mode == CS_CONV_FWD)
+    e = wide ? launch<128, 128, CS_CONV_FWD, true>(p, 1, stream) : launch<128, 64, CS_CONV_FWD, true>(p, 1, stream);
+  else if (c4)
+    e = p.M <= 64 ? launch<64, 64, CS_CONV_WGRAD, true>(p, splits, stream)
+                  : launch<128, 64, CS_CONV_WGRAD, true>(p, splits, stream);
+  else if (mode == CS_CONV_FWD)
     e = wide ? launch<128, 128, CS_CONV_FWD>(p, 1, stream) : launch<128, 64, CS_CONV_FWD>(p, 1, stream);
   else if (mode == CS_CONV_DGRAD)
     e = wide ? launch<128, 128, CS_CONV_DGRAD>(p, 1, stream) : launch<128, 64, CS_CONV_DGRAD>(p, 1, stream);
@@ -398,7 +451,10 @@ hipError_t cs_conv_nhwc(int mode, const CsConvNhwcArgs& in, int splits, hipStrea
   if (e != hipSuccess || mode != CS_CONV_WGRAD) return e;
   // the caller's dw_out receives the split-ordered sum (slabs in p.dw)
   const int64_t n4 = (int64_t)p.M * p.N / 4;
-  int blocks = (int)std::min<int64_t>((n4 + 255) / 256, 2048);
-  hipLaunchKernelGGL(conv_nhwc_reduce_kernel, dim3(blocks), dim3(256), 0, stream, p.dw, splits, n4, p.dw_out);
+  int SL = 1;  // split lanes per column: up to 16, about 32 slabs per lane
+  while (SL < 16 && SL * 32 < splits) SL *= 2;
+  const int64_t blocks = (n4 + 256 / SL - 1) / (256 / SL);
+  hipLaunchKernelGGL(conv_nhwc_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, p.dw, splits, SL, n4,
+                     p.dw_out);
   return hipGetLastError();
 }

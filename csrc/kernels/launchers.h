@@ -320,13 +320,17 @@ hipError_t cs_rope(int dt, const void* x, const float* cosv, const float* sinv, 
                    int inverse, hipStream_t s);
 // channels-last (NHWC) CNN kernels (cnn_nhwc.hip), fp32 / bf16 activations, M = B*H*W rows of C.
 // BatchNorm: stat / coef / part exactly as the NCHW kernels above (part: cs_bn_nhwc_partials floats).
+// mask (optional, M*C/V bytes, V = cs_bn_nhwc_vec): the forward writes each V-channel vector's
+// pre-activation > 0 bits; the backward then takes the ReLU mask from it instead of recomputing it
+// from x and the residual (one activation-sized read fewer per pass for a residual BatchNorm).
 int cs_bn_nhwc_partials(int64_t M, int C, int dt);
+int cs_bn_nhwc_vec(int C, int dt);
 hipError_t cs_bn_nhwc_fwd(int dt, const void* x, const void* res, const float* w, const float* b, float* rm, float* rv,
                           int64_t* nbt, float momentum, float eps, int relu, void* y, float* stat, float* part,
-                          int64_t M, int C, hipStream_t stream);
+                          int64_t M, int C, hipStream_t stream, unsigned char* mask = nullptr);
 hipError_t cs_bn_nhwc_bwd(int dt, const void* dy, const void* x, const void* res, const float* w, const float* stat,
                           int relu, void* dx, void* dres, float* dw, float* db, float* coef, float* part, int64_t M,
-                          int C, hipStream_t stream);
+                          int C, hipStream_t stream, const unsigned char* mask = nullptr);
 hipError_t cs_maxpool3s2_nhwc_fwd(int dt, const void* x, void* y, unsigned char* pos, int B, int H, int W, int C,
                                   int Ho, int Wo, hipStream_t stream);
 hipError_t cs_maxpool3s2_nhwc_bwd(int dt, const void* dy, const unsigned char* pos, void* dx, int B, int H, int W,

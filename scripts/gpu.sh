@@ -58,7 +58,7 @@ case "$what" in
       python3 $R/bench.py "$@" > $R/gpurun_out/$TAG.log 2>&1)
     rc=$?; echo "rocprofv3 rc=$rc"; tail -1 gpurun_out/$TAG.log
     [ $rc -eq 0 ] || exit $rc
-    python3 scripts/prof_summary.py gpurun_out/$TAG --steps 15 --top 45 > gpurun_out/${TAG}_kernels.txt 2>&1
+    python3 scripts/prof_summary.py gpurun_out/$TAG --steps ${PS_STEPS:-15} --top 45 > gpurun_out/${TAG}_kernels.txt 2>&1
     python3 scripts/step_timeline.py gpurun_out/$TAG > gpurun_out/${TAG}_timeline.txt 2>&1
     head -3 gpurun_out/${TAG}_kernels.txt
     grep -E "^# one step|^## queue|^# queue|^# main" gpurun_out/${TAG}_timeline.txt

@@ -136,6 +136,28 @@ def test_bn_act_nhwc_matches_fp64(dev, shape, dtype, relu, residual):
         torch.testing.assert_close(res.grad.double(), rr.grad, **gt)
 
 
+@pytest.mark.parametrize("shape", [(4, 14, 14, 256), (3, 14, 14, 24), (2, 5, 3, 6)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_bn_relu_mask_equals_recomputed_mask(dev, shape, dtype, monkeypatch):
+    """residual + ReLU BatchNorm: the backward reading the forward's ReLU bit mask (default) is
+    bitwise equal to recomputing the mask from x and the residual (CS_BN_MASK=0), for V = 8 / 4 / 1"""
+    from cs744_pytorch_distributed_tutorial_amd.ops.cnn_nhwc import bn_act_nhwc
+    torch.manual_seed(5)
+    x0 = torch.randn(shape, device=dev).to(dtype)
+    r0 = torch.randn(shape, device=dev).to(dtype)
+    g = torch.randn(shape, device=dev).to(dtype)
+    outs = []
+    for m in ("0", "1"):
+        monkeypatch.setenv("CS_BN_MASK", m)
+        bn = nn.BatchNorm2d(shape[3]).to(dev)
+        x, r = x0.clone().requires_grad_(), r0.clone().requires_grad_()
+        y = bn_act_nhwc(bn, x, True, r)
+        y.backward(g)
+        outs.append((y, x.grad, r.grad, bn.weight.grad, bn.bias.grad))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("shape", [(2, 112, 112, 64), (3, 7, 9, 5), (1, 2, 3, 8)])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_max_pool_nhwc_matches_torch(dev, shape, dtype):
@@ -186,6 +208,41 @@ def test_resnet18_nhwc_matches_nchw_module_path(dev):
         torch.testing.assert_close(pa, pb, rtol=2e-2, atol=2e-3, msg=n)
     for (n, ba), (_, bb) in zip(a.named_buffers(), b.named_buffers()):
         torch.testing.assert_close(ba.double(), bb.double(), rtol=1e-4, atol=1e-5, msg=n)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_bottleneck_residual_grad_sink_matches_autograd_sum(dev, dtype, monkeypatch):
+    """identity bottlenecks: the residual gradient taken into conv1's data-gradient GEMM
+    (ResidualGradSink, default) == autograd summing it (CS_RES_SINK=0), input and every parameter
+    gradient; and the sink really feeds the GEMM (its box is drained)"""
+    from cs744_pytorch_distributed_tutorial_amd.models import resnet as rn
+    from cs744_pytorch_distributed_tutorial_amd.ops import cnn_nhwc
+    torch.manual_seed(6)
+    layer = nn.Sequential(rn.Bottleneck(256, 64), rn.Bottleneck(256, 64)).to(dev)
+    x0 = torch.randn(4, 14, 14, 256, device=dev).to(dtype)
+    g = torch.randn(4, 14, 14, 256, device=dev).to(dtype)
+    boxes = []
+    orig = cnn_nhwc.ResidualGradSink.apply
+
+    def spy(x, box):
+        boxes.append(box)
+        return orig(x, box)
+
+    monkeypatch.setattr(rn.ResidualGradSink, "apply", spy)
+    outs = []
+    for m in ("0", "1"):
+        monkeypatch.setenv("CS_RES_SINK", m)
+        layer.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_()
+        y = x
+        for blk in layer:
+            y = blk.forward_nhwc(y)
+        y.backward(g)
+        outs.append([x.grad.float()] + [p.grad.float() for p in layer.parameters()])
+    assert len(boxes) == 2 and all(b.get("fused") and "g" not in b for b in boxes)
+    tol = 1e-5 if dtype == torch.float32 else 2e-2
+    for a, b in zip(*outs):
+        assert ((a - b).norm() / (b.norm() + 1e-30)).item() < tol
 
 
 def test_resnet50_nhwc_bf16_as_accurate_as_miopen_bf16(dev):

@@ -100,3 +100,49 @@ def test_resnet_conv_layer_implicit_vs_im2col(C, stride, k, monkeypatch):
         outs.append((y.detach().float(), x.grad.float(), conv.weight.grad.float()))
     for a, b in zip(*outs):
         assert _rel(a, b) < 1e-2
+
+
+@pytest.mark.parametrize("shape", [(2, 30, 30, 64, 7, 2, 3), (1, 17, 19, 32, 3, 1, 1), (2, 224, 224, 64, 7, 2, 3)],
+                         ids=lambda s: "x".join(map(str, s)))
+def test_conv_nhwc_stem_c4_matches_fp64(C, shape):
+    """C4 mode (the 4-channel stem): kernel rows padded to 8 taps, forward and weight gradient vs f64"""
+    B, H, W, Co, R, st, pad = shape
+    torch.manual_seed(3)
+    dev = torch.device("cuda", 0)
+    x = torch.randn(B, H, W, 4, device=dev).to(torch.bfloat16)
+    w = (torch.randn(Co, R, R, 4, device=dev) / (R * R * 4) ** 0.5).to(torch.bfloat16)
+    wp = torch.nn.functional.pad(w, (0, 0, 0, 8 - R)).contiguous()  # [Co, R, 8, 4], zero taps s >= R
+    xr = x.double().cpu().permute(0, 3, 1, 2)
+    wr = w.double().cpu().permute(0, 3, 1, 2).requires_grad_()
+    yr = F.conv2d(xr, wr, None, st, pad)
+    y = C.conv_nhwc_bf16(0, x, wp, R, R, st, pad, 0, 0)
+    torch.cuda.synchronize()
+    assert y.shape == (B, yr.shape[2], yr.shape[3], Co)
+    assert _rel(y.permute(0, 3, 1, 2), yr) < 5e-3
+    dy = torch.randn(*y.shape, device=dev).to(torch.bfloat16)
+    yr.backward(dy.double().cpu().permute(0, 3, 1, 2))
+    dw = C.conv_nhwc_bf16(2, dy, x, R, R, st, pad, 0, 0)
+    torch.cuda.synchronize()
+    assert dw.shape == (Co, R * 32)
+    assert _rel(dw.view(Co, R, 8, 4)[:, :, :R].permute(0, 3, 1, 2), wr.grad) < 1e-4
+
+
+def test_resnet_stem_implicit_vs_im2col(C, monkeypatch):
+    """the ResNet stem (3 -> 64, 7x7/2, image padded to 4 channels) through ops/cnn_nhwc.conv_nhwc:
+    C4 implicit path (default) vs im2col + GEMM (CS_CONV_IMPLICIT=0), y and dW"""
+    from cs744_pytorch_distributed_tutorial_amd.ops import cnn_nhwc
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(4)
+    conv = torch.nn.Conv2d(3, 64, 7, 2, 3, bias=False).to(dev)
+    x = cnn_nhwc.to_nhwc(torch.randn(4, 3, 64, 64, device=dev), torch.bfloat16, pad_c=1)
+    g0 = torch.randn(4, 32, 32, 64, device=dev).to(torch.bfloat16)
+    outs = []
+    for mode in ("0", "1"):
+        monkeypatch.setenv("CS_CONV_IMPLICIT", mode)
+        conv.weight.grad = None
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = cnn_nhwc.conv_nhwc(x, conv)
+        y.backward(g0)
+        outs.append((y.detach().float(), conv.weight.grad.float()))
+    for a, b in zip(*outs):
+        assert _rel(a, b) < 1e-2
