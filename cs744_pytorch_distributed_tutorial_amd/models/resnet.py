@@ -32,7 +32,8 @@ import torch
 import torch.nn as nn
 
 from ..ops.cnn import bn_act, max_pool3s2
-from ..ops.cnn_nhwc import act_dtype, bn_act_nhwc, conv_nhwc, max_pool3s2_nhwc, to_nhwc
+from ..ops.cnn_nhwc import (ResidualGradSink, act_dtype, bn_act_nhwc, conv_nhwc, max_pool3s2_nhwc,
+                            residual_sink_ok, to_nhwc)
 
 
 def conv3x3(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
@@ -96,6 +97,16 @@ class Bottleneck(nn.Module):
         return bn_act(self.bn3, self.conv3(y), residual=idt)
 
     def forward_nhwc(self, x: torch.Tensor) -> torch.Tensor:
+        if residual_sink_ok(x, self.conv1):
+            # the shortcut branch's gradient w.r.t. x joins conv1's data-gradient GEMM
+            # (ops/cnn_nhwc.ResidualGradSink); the sink (and the downsample after it) is created after
+            # conv1..conv3, so autograd runs that branch's backward first
+            box: dict = {}
+            y = bn_act_nhwc(self.bn1, conv_nhwc(x, self.conv1, grad_box=box))
+            z = conv_nhwc(bn_act_nhwc(self.bn2, conv_nhwc(y, self.conv2)), self.conv3)
+            xs = ResidualGradSink.apply(x, box)
+            idt = xs if self.downsample is None else _downsample_nhwc(self.downsample, xs)
+            return bn_act_nhwc(self.bn3, z, residual=idt)
         idt = x if self.downsample is None else _downsample_nhwc(self.downsample, x)
         y = bn_act_nhwc(self.bn1, conv_nhwc(x, self.conv1))
         y = bn_act_nhwc(self.bn2, conv_nhwc(y, self.conv2))

@@ -239,7 +239,9 @@ class _ConvNHWC(torch.autograd.Function):
                     box["done"] = True  # a ResidualGradSink running after this returns its gradient
                     box["fused"] = gres is not None
                 if gres is not None and gres.dtype == dy2.dtype and gres.is_contiguous():
-                    dcol = torch.addmm(gres.view(-1, C), dy2, wf)  # dx + the residual's gradient, one GEMM
+                    # dx + the residual's gradient in one GEMM (beta = 1), written over the residual
+                    # gradient itself (an out-of-place addmm would first copy it into a new buffer)
+                    dcol = gres.view(-1, C).addmm_(dy2, wf)
                 else:
                     dcol = torch.mm(dy2, wf)  # [M, Kp]
                     if gres is not None:

@@ -61,7 +61,7 @@ case "$what" in
     python3 scripts/prof_summary.py gpurun_out/$TAG --steps ${PS_STEPS:-15} --top 45 > gpurun_out/${TAG}_kernels.txt 2>&1
     python3 scripts/step_timeline.py gpurun_out/$TAG > gpurun_out/${TAG}_timeline.txt 2>&1
     head -3 gpurun_out/${TAG}_kernels.txt
-    grep -E "^# one step|^## queue|^# queue|^# main" gpurun_out/${TAG}_timeline.txt
+    grep -E "^# one step|^## queue|^# queue|^# main" gpurun_out/${TAG}_timeline.txt || true
     ;;
   pmc)
     TAG=${1:-pmc}; P=$2; shift 2 || true

@@ -212,14 +212,16 @@ def test_resnet18_nhwc_matches_nchw_module_path(dev):
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_bottleneck_residual_grad_sink_matches_autograd_sum(dev, dtype, monkeypatch):
-    """identity bottlenecks: the residual gradient taken into conv1's data-gradient GEMM
+    """bottlenecks (a downsampling one, two identity ones): the shortcut branch's gradient w.r.t.
+    the block input taken into conv1's data-gradient GEMM
     (ResidualGradSink, default) == autograd summing it (CS_RES_SINK=0), input and every parameter
     gradient; and the sink really feeds the GEMM (its box is drained)"""
     from cs744_pytorch_distributed_tutorial_amd.models import resnet as rn
     from cs744_pytorch_distributed_tutorial_amd.ops import cnn_nhwc
     torch.manual_seed(6)
-    layer = nn.Sequential(rn.Bottleneck(256, 64), rn.Bottleneck(256, 64)).to(dev)
-    x0 = torch.randn(4, 14, 14, 256, device=dev).to(dtype)
+    down = nn.Sequential(rn.conv1x1(128, 256, 2), nn.BatchNorm2d(256))
+    layer = nn.Sequential(rn.Bottleneck(128, 64, 2, down), rn.Bottleneck(256, 64), rn.Bottleneck(256, 64)).to(dev)
+    x0 = torch.randn(4, 28, 28, 128, device=dev).to(dtype)
     g = torch.randn(4, 14, 14, 256, device=dev).to(dtype)
     boxes = []
     orig = cnn_nhwc.ResidualGradSink.apply
@@ -239,7 +241,7 @@ def test_bottleneck_residual_grad_sink_matches_autograd_sum(dev, dtype, monkeypa
             y = blk.forward_nhwc(y)
         y.backward(g)
         outs.append([x.grad.float()] + [p.grad.float() for p in layer.parameters()])
-    assert len(boxes) == 2 and all(b.get("fused") and "g" not in b for b in boxes)
+    assert len(boxes) == 3 and all(b.get("fused") and "g" not in b for b in boxes)
     tol = 1e-5 if dtype == torch.float32 else 2e-2
     for a, b in zip(*outs):
         assert ((a - b).norm() / (b.norm() + 1e-30)).item() < tol
