@@ -32,7 +32,7 @@ import torch
 import torch.nn as nn
 
 from ..ops.cnn import bn_act, max_pool3s2
-from ..ops.cnn_nhwc import (ResidualGradSink, act_dtype, bn_act_nhwc, conv_nhwc, max_pool3s2_nhwc,
+from ..ops.cnn_nhwc import (ResidualGradSink, act_dtype, bn_act_nhwc, bn_relu_maxpool_nhwc, conv_nhwc,
                             residual_sink_ok, to_nhwc)
 
 
@@ -163,7 +163,7 @@ class ResNet(nn.Module):
         """the same network on channels-last activations (input: [B, 3, H, W], any memory format)"""
         # the 3-channel image gets a zero 4th channel: the stem's im2col then moves 4-channel vectors
         x = to_nhwc(x, act_dtype(x), pad_c=1 if x.shape[1] == 3 else 0)
-        x = max_pool3s2_nhwc(bn_act_nhwc(self.bn1, conv_nhwc(x, self.conv1)))
+        x = bn_relu_maxpool_nhwc(self.bn1, conv_nhwc(x, self.conv1))
         for layer in (self.layer1, self.layer2, self.layer3, self.layer4):
             for blk in layer:
                 x = blk.forward_nhwc(x)

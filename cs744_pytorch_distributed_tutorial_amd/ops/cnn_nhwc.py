@@ -316,6 +316,38 @@ def bn_act_nhwc(bn: nn.BatchNorm2d, x: torch.Tensor, relu: bool = True,
     return (F.relu(y) if relu else y).contiguous()
 
 
+class _BnReluPoolNHWC(torch.autograd.Function):
+    """max_pool3s2(relu(bn(x))) with the BatchNorm apply fused into the pool's window loads: the
+    full-resolution activation is never written (forward) — the ResNet stem's 112x112x64 one is
+    411 MB at B=256. Backward: the pool's gather to full resolution, then the BatchNorm backward
+    with the ReLU mask recomputed from x."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, nbt, momentum, eps):
+        y, pos, stat = native.C().bn_relu_maxpool_nhwc_fwd(x, weight, bias, running_mean, running_var, nbt, momentum,
+                                                           eps)
+        ctx.save_for_backward(x, weight, stat, pos)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight, stat, pos = ctx.saved_tensors
+        g = native.C().maxpool3s2_nhwc_bwd(dy.contiguous(), pos, x.shape[1], x.shape[2])
+        dx, _, dw, db = native.C().bn_nhwc_bwd(g, x, None, weight, stat, True, False)
+        return dx, dw, db, None, None, None, None, None
+
+
+def bn_relu_maxpool_nhwc(bn: nn.BatchNorm2d, x: torch.Tensor) -> torch.Tensor:
+    """``max_pool3s2(relu(bn(x)))`` on [B, H, W, C] activations (one fused op in training on the GPU;
+    CS_BN_POOL_FUSE=0: BN-apply and pool as two passes)"""
+    if (bn.training and bn.track_running_stats and bn.momentum is not None and bn.affine and x.is_cuda
+            and x.dtype in (torch.float32, torch.bfloat16) and x.shape[0] * x.shape[1] * x.shape[2] > 1
+            and os.environ.get("CS_BN_POOL_FUSE", "1") != "0"):
+        return _BnReluPoolNHWC.apply(x.contiguous(), bn.weight, bn.bias, bn.running_mean, bn.running_var,
+                                     bn.num_batches_tracked, float(bn.momentum), float(bn.eps))
+    return max_pool3s2_nhwc(bn_act_nhwc(bn, x))
+
+
 class _MaxPoolNHWC(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x):

@@ -156,6 +156,39 @@ std::vector<torch::Tensor> bn_nhwc_bwd(torch::Tensor dy, torch::Tensor x, c10::o
   return {dx, dres, dw, db};
 }
 
+// training BatchNorm2d + ReLU + 3x3/2 pad-1 max-pool (the ResNet stem) -> {y (pooled), pos, stat}:
+// statistics as bn_nhwc_fwd, then the pool applies BN + ReLU to its window loads (no full-size output)
+std::vector<torch::Tensor> bn_relu_maxpool_nhwc_fwd(torch::Tensor x, c10::optional<torch::Tensor> w,
+                                                    c10::optional<torch::Tensor> b, c10::optional<torch::Tensor> rm,
+                                                    c10::optional<torch::Tensor> rv, c10::optional<torch::Tensor> nbt,
+                                                    double momentum, double eps) {
+  check_nhwc(x, "bn_relu_maxpool_nhwc_fwd");
+  const int dt = act_dt(x, "bn_relu_maxpool_nhwc_fwd");
+  const int64_t B = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3), M = x.numel() / C;
+  TORCH_CHECK(M > 0 && C > 0, "bn_relu_maxpool_nhwc_fwd: empty input");
+  check_param(w, C, "weight");
+  check_param(b, C, "bias");
+  check_param(rm, C, "running_mean");
+  check_param(rv, C, "running_var");
+  TORCH_CHECK(rm.has_value() == rv.has_value(), "bn_relu_maxpool_nhwc_fwd: running mean and var go together");
+  if (nbt.has_value())
+    TORCH_CHECK(nbt->is_cuda() && nbt->scalar_type() == at::kLong && nbt->numel() == 1,
+                "bn_relu_maxpool_nhwc_fwd: num_batches_tracked");
+  DevGuard g(x.device());
+  auto fo = x.options().dtype(at::kFloat);
+  auto stat = torch::empty({4, C}, fo);
+  auto part = torch::empty({cs_bn_nhwc_partials(M, (int)C, dt)}, fo);
+  CS_LAUNCH(cs_bn_nhwc_fwd(dt, x.data_ptr(), nullptr, opt_ptr<float>(w), opt_ptr<float>(b), opt_ptr<float>(rm),
+                           opt_ptr<float>(rv), opt_ptr<int64_t>(nbt), (float)momentum, (float)eps, 1, nullptr,
+                           stat.data_ptr<float>(), part.data_ptr<float>(), M, (int)C, cur_stream()));
+  const int64_t Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+  auto y = torch::empty({B, Ho, Wo, C}, x.options());
+  auto pos = torch::empty({B, Ho, Wo, C}, x.options().dtype(at::kByte));
+  CS_LAUNCH(cs_maxpool3s2_nhwc_fwd(dt, x.data_ptr(), y.data_ptr(), pos.data_ptr<uint8_t>(), (int)B, (int)H, (int)W,
+                                   (int)C, (int)Ho, (int)Wo, cur_stream(), stat.data_ptr<float>()));
+  return {y, pos, stat};
+}
+
 // 3x3 / 2 pad-1 max-pool -> {y, pos (uint8 window position per output element)}
 std::vector<torch::Tensor> maxpool3s2_nhwc_fwd(torch::Tensor x) {
   check_nhwc(x, "maxpool3s2_nhwc_fwd");
@@ -233,6 +266,8 @@ void register_nhwc_ops(pybind11::module& m) {
   m.def("bn_nhwc_bwd", &bn_nhwc_bwd, "its backward -> (dx, dres, dweight, dbias); mask: the forward's ReLU mask",
         pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("res"), pybind11::arg("w"), pybind11::arg("stat"), pybind11::arg("relu"),
         pybind11::arg("need_dres"), pybind11::arg("mask") = pybind11::none());
+  m.def("bn_relu_maxpool_nhwc_fwd", &bn_relu_maxpool_nhwc_fwd,
+        "training BatchNorm2d + ReLU + 3x3/2 max-pool, NHWC, the apply fused into the pool -> (y, pos, stat)");
   m.def("maxpool3s2_nhwc_fwd", &maxpool3s2_nhwc_fwd, "3x3/2 pad-1 max-pool, NHWC -> (y, window position)");
   m.def("maxpool3s2_nhwc_bwd", &maxpool3s2_nhwc_bwd, "its gather-style backward");
   m.def("im2col_nhwc", &im2col_nhwc, "NHWC im2col -> [B*Ho*Wo, Kp], columns (r, s, c)");

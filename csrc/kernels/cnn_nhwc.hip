@@ -345,17 +345,27 @@ __global__ __launch_bounds__(256) void apply_bwd_kernel(const T* __restrict__ dy
 
 // ------------------------------------------------------------------------------ max-pool 3x3/2
 // one thread per (output position, V channels); ties keep the first maximum in row-major window
-// order and a NaN wins (ATen's rules)
+// order and a NaN wins (ATen's rules). stat != nullptr: the input is a BatchNorm's pre-activation
+// and each window element is first taken through that BatchNorm + ReLU and rounded to T — the
+// same arithmetic as apply_fwd_kernel, so the result equals BN-apply then max-pool bit for bit,
+// without the full-resolution activation ever being written (the ResNet stem).
 template <typename T, int V>
 __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const T* __restrict__ x, T* __restrict__ y,
                                                           unsigned char* __restrict__ pos, int B, int H, int W, int C,
-                                                          int Ho, int Wo) {
+                                                          int Ho, int Wo, const float* __restrict__ stat) {
   const int CV = C / V;
   const int64_t total = (int64_t)B * Ho * Wo * CV;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     const int ii = (int)i, cv = ii % CV, o32 = ii / CV;  // total < 2^31 (host check): 32-bit index math
     const int64_t o = o32;
     const int ow = o32 % Wo, oh = (o32 / Wo) % Ho, b = o32 / (Wo * Ho);
+    float sc[V], sf[V];
+    if (stat != nullptr)
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        sc[j] = stat[cv * V + j];
+        sf[j] = stat[C + cv * V + j];
+      }
     float best[V];
     int bp[V];
 #pragma unroll
@@ -371,6 +381,14 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const T* __restrict__ 
         if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W) {
           float v[V];
           ldv<T, V>(x + (((int64_t)b * H + ih) * W + iw) * C + cv * V, v);
+          if (stat != nullptr)
+#pragma unroll
+            for (int j = 0; j < V; ++j) {
+              const float z = preact(v[j], sc[j], sf[j], 0.f);
+              T t;
+              E<T>::st(&t, !(z > 0.f) ? 0.f : z);
+              v[j] = E<T>::ld(&t);
+            }
 #pragma unroll
           for (int j = 0; j < V; ++j)
             if (bp[j] < 0 || v[j] > best[j] || v[j] != v[j]) {
@@ -537,6 +555,7 @@ void bn_fwd_t(const void* x, const void* res, const float* w, const float* b, fl
   hipLaunchKernelGGL((stats_kernel<T, V>), dim3(g.P, g.CG), dim3(256), 0, st, (const T*)x, M, C, g.rpb, part);
   hipLaunchKernelGGL(finalize_fwd_kernel<T>, dim3((C + 7) / 8), dim3(256), 0, st, (const T*)x, part, g.P, C,
                      (double)M, w, b, rm, rv, momentum, eps, stat, nbt);
+  if (y == nullptr) return;  // statistics only (the apply is fused into the consumer)
   const BnGrid a = apply_grid(M, C, V);
   hipLaunchKernelGGL((apply_fwd_kernel<T, V>), dim3(a.P, a.CG), dim3(256), 0, st, (const T*)x, (const T*)res, stat,
                      (T*)y, M, C, a.rpb, relu, mask);
@@ -599,7 +618,7 @@ hipError_t cs_bn_nhwc_bwd(int dt, const void* dy, const void* x, const void* res
 }
 
 hipError_t cs_maxpool3s2_nhwc_fwd(int dt, const void* x, void* y, unsigned char* pos, int B, int H, int W, int C,
-                                  int Ho, int Wo, hipStream_t stream) {
+                                  int Ho, int Wo, hipStream_t stream, const float* stat) {
   const int64_t per = (int64_t)Ho * Wo * C;
   if (per * B == 0) return hipSuccess;
   if (per >= kMaxItems) return hipErrorInvalidValue;
@@ -609,7 +628,7 @@ hipError_t cs_maxpool3s2_nhwc_fwd(int dt, const void* x, void* y, unsigned char*
     const int64_t xo = (int64_t)b0 * H * W * C, yo = (int64_t)b0 * per;
     CS_NHWC_DISPATCH(dt, C, hipLaunchKernelGGL((maxpool_fwd_kernel<T, V>), dim3(grid_for(nb * per / V)), dim3(256),
                                                0, stream, (const T*)x + xo, (T*)y + yo, pos + yo, nb, H, W, C, Ho,
-                                               Wo));
+                                               Wo, stat));
   }
   return hipGetLastError();
 }

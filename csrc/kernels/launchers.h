@@ -331,8 +331,10 @@ hipError_t cs_bn_nhwc_fwd(int dt, const void* x, const void* res, const float* w
 hipError_t cs_bn_nhwc_bwd(int dt, const void* dy, const void* x, const void* res, const float* w, const float* stat,
                           int relu, void* dx, void* dres, float* dw, float* db, float* coef, float* part, int64_t M,
                           int C, hipStream_t stream, const unsigned char* mask = nullptr);
+// stat (optional, a BatchNorm's [4][C] from cs_bn_nhwc_fwd with y == nullptr = statistics only):
+// pool relu(BN(x)) — the BatchNorm apply fused into the pool's window loads
 hipError_t cs_maxpool3s2_nhwc_fwd(int dt, const void* x, void* y, unsigned char* pos, int B, int H, int W, int C,
-                                  int Ho, int Wo, hipStream_t stream);
+                                  int Ho, int Wo, hipStream_t stream, const float* stat = nullptr);
 hipError_t cs_maxpool3s2_nhwc_bwd(int dt, const void* dy, const unsigned char* pos, void* dx, int B, int H, int W,
                                   int C, int Ho, int Wo, hipStream_t stream);
 // bf16 NHWC implicit-GEMM convolution (conv_nhwc.hip; C, Co % 32 == 0, any R x S / stride / pad):
