@@ -77,6 +77,29 @@ def _wgrad(dy2: torch.Tensor, col: torch.Tensor) -> torch.Tensor:
     return part.sum(0)
 
 
+def weights_channels_last(model: nn.Module) -> nn.Module:
+    """Lay the k x k (k > 1) conv weights of a channels-last model out as [Co, R, S, Ci] in memory
+    (torch.channels_last; shape and state_dict keys unchanged): the NHWC convolutions then read
+    them without a permuting copy per forward, and their weight gradients come out of the GEMM in
+    that layout with no copy back (the fused SGD and the DDP flat buffer take any dense layout
+    shared by parameter and gradient). 1x1 weights keep the standard strides."""
+    for m in model.modules():
+        if isinstance(m, nn.Conv2d) and tuple(m.kernel_size) != (1, 1):
+            m.weight.data = m.weight.data.contiguous(memory_format=torch.channels_last)
+    return model
+
+
+def _weight_grad(v: torch.Tensor, ctx) -> torch.Tensor:
+    """a [Co, Ci, R, S] view of a GEMM's fp32 weight gradient -> the gradient in the weight's own
+    layout (autograd would otherwise copy it to match): the view itself when it already is that
+    layout, else one copy into it"""
+    if v.dtype == ctx.wdtype and v.stride() == ctx.wstride:
+        return v
+    dw = torch.empty_strided(v.shape, ctx.wstride, dtype=ctx.wdtype, device=v.device)
+    dw.copy_(v)
+    return dw
+
+
 def _implicit_ok(dt: torch.dtype, C: int, Ci: int, Co: int, R: int, S: int, stride: int, pad: int) -> bool:
     """whether this conv runs as the bf16 implicit-GEMM kernel (csrc/kernels/conv_nhwc.hip).
 
@@ -107,6 +130,7 @@ class _ConvImplicitNHWC(torch.autograd.Function):
         ctx.save_for_backward(x, w4)
         ctx.geo = (R, S, stride, pad)
         ctx.wdtype = weight.dtype
+        ctx.wstride = weight.stride()
         return y
 
     @staticmethod
@@ -121,8 +145,7 @@ class _ConvImplicitNHWC(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             dwf = native.C().conv_nhwc_bf16(2, dy, x, R, S, stride, pad, 0, 0)  # fp32 [Co, R*S*C]
             Co, C = w4.shape[0], w4.shape[3]
-            dw = torch.empty((Co, C, R, S), dtype=ctx.wdtype, device=dy.device)
-            dw.copy_(dwf.view(Co, R, S, C).permute(0, 3, 1, 2))
+            dw = _weight_grad(dwf.view(Co, R, S, C).permute(0, 3, 1, 2), ctx)
         return dx, dw, None, None
 
 
@@ -147,6 +170,7 @@ class _ConvStemNHWC(torch.autograd.Function):
         ctx.save_for_backward(x)
         ctx.geo = (Co, Ci, R, S, stride, pad)
         ctx.wdtype = weight.dtype
+        ctx.wstride = weight.stride()
         return y
 
     @staticmethod
@@ -156,8 +180,7 @@ class _ConvStemNHWC(torch.autograd.Function):
         dw = None
         if ctx.needs_input_grad[1]:
             dwf = native.C().conv_nhwc_bf16(2, dy.to(torch.bfloat16).contiguous(), x, R, S, stride, pad, 0, 0)
-            dw = torch.empty((Co, Ci, R, S), dtype=ctx.wdtype, device=dy.device)
-            dw.copy_(dwf.view(Co, R, 8, 4)[:, :, :S, :Ci].permute(0, 3, 1, 2))
+            dw = _weight_grad(dwf.view(Co, R, 8, 4)[:, :, :S, :Ci].permute(0, 3, 1, 2), ctx)
         return None, dw, None, None
 
 
@@ -210,6 +233,7 @@ class _ConvNHWC(torch.autograd.Function):
         ctx.save_for_backward(col, wf)
         ctx.geo = (B, H, W, C, Ci, Co, R, S, stride, pad, K, direct)
         ctx.wdtype = weight.dtype
+        ctx.wstride = weight.stride()
         ctx.box = box
         return y.view(B, Ho, Wo, Co)
 
@@ -229,8 +253,7 @@ class _ConvNHWC(torch.autograd.Function):
                 if R == 1 and S == 1 and dwf.shape[1] == K and Ci == C:
                     dw = dwf.view(Co, C, 1, 1).to(ctx.wdtype)
                 else:
-                    dw = torch.empty((Co, Ci, R, S), dtype=ctx.wdtype, device=dy.device)
-                    dw.copy_(dwf[:, :K].reshape(Co, R, S, C)[..., :Ci].permute(0, 3, 1, 2))
+                    dw = _weight_grad(dwf[:, :K].reshape(Co, R, S, C)[..., :Ci].permute(0, 3, 1, 2), ctx)
             if ctx.needs_input_grad[0]:
                 assert Ci == C, "conv_nhwc: no data gradient through padded input channels"
                 box = ctx.box

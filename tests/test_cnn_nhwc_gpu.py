@@ -273,6 +273,30 @@ def test_bottleneck_residual_grad_sink_matches_autograd_sum(dev, dtype, monkeypa
         assert ((a - b).norm() / (b.norm() + 1e-30)).item() < tol
 
 
+def test_resnet_channels_last_weights_grads_in_place(dev, monkeypatch):
+    """k x k conv weights laid out channels-last (CS_CONV_WEIGHT_CL=1, opt-in): every weight gradient
+    arrives in its parameter's own layout (no autograd re-layout copy), and the step's gradients
+    equal those of standard-layout weights (CS_CONV_WEIGHT_CL=0)"""
+    from cs744_pytorch_distributed_tutorial_amd.models.resnet import resnet50
+    x = torch.randn(2, 3, 64, 64, device=dev)
+    grads = []
+    for m in ("0", "1"):
+        monkeypatch.setenv("CS_CONV_WEIGHT_CL", m)
+        torch.manual_seed(11)
+        net = resnet50(num_classes=10).to(dev)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            out = net(x)
+        out.float().square().sum().backward()
+        for mod in net.modules():
+            if isinstance(mod, nn.Conv2d):
+                assert mod.weight.grad.stride() == mod.weight.stride()
+                if m == "1" and mod.kernel_size != (1, 1):
+                    assert mod.weight.is_contiguous(memory_format=torch.channels_last)
+        grads.append([p.grad.float().contiguous() for p in net.parameters()])
+    for a, b in zip(*grads):
+        assert ((a - b).norm() / (b.norm() + 1e-30)).item() < 1e-5
+
+
 def test_resnet50_nhwc_bf16_as_accurate_as_miopen_bf16(dev):
     """ResNet-50 under bf16 autocast, channels-last kernels vs MIOpen + the NCHW module path, both
     measured against the fp32 NCHW step on the same weights and batch: the native path's logit error
