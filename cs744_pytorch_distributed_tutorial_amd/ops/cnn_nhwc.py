@@ -342,8 +342,8 @@ def bn_act_nhwc(bn: nn.BatchNorm2d, x: torch.Tensor, relu: bool = True,
 class _BnReluPoolNHWC(torch.autograd.Function):
     """max_pool3s2(relu(bn(x))) with the BatchNorm apply fused into the pool's window loads: the
     full-resolution activation is never written (forward) — the ResNet stem's 112x112x64 one is
-    411 MB at B=256. Backward: the pool's gather to full resolution, then the BatchNorm backward
-    with the ReLU mask recomputed from x."""
+    411 MB at B=256. Backward: the pool's gather pass, then the BatchNorm backward with the ReLU mask
+    recomputed from x (CS_BN_POOL_FUSE_BWD=1: the gather inside both BatchNorm passes instead)."""
 
     @staticmethod
     def forward(ctx, x, weight, bias, running_mean, running_var, nbt, momentum, eps):
@@ -355,8 +355,13 @@ class _BnReluPoolNHWC(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, weight, stat, pos = ctx.saved_tensors
-        g = native.C().maxpool3s2_nhwc_bwd(dy.contiguous(), pos, x.shape[1], x.shape[2])
-        dx, _, dw, db = native.C().bn_nhwc_bwd(g, x, None, weight, stat, True, False)
+        # opt-in: the pool's gather inside both BN passes measured 0.2-0.4 % slower than a gather pass
+        # writing the full-resolution gradient (profiles/r3_resnet50_fusions_ab.txt)
+        if os.environ.get("CS_BN_POOL_FUSE_BWD", "0") == "1":
+            dx, dw, db = native.C().bn_relu_maxpool_nhwc_bwd(dy.contiguous(), pos, x, weight, stat)
+        else:
+            g = native.C().maxpool3s2_nhwc_bwd(dy.contiguous(), pos, x.shape[1], x.shape[2])
+            dx, _, dw, db = native.C().bn_nhwc_bwd(g, x, None, weight, stat, True, False)
         return dx, dw, db, None, None, None, None, None
 
 

@@ -220,13 +220,48 @@ __global__ __launch_bounds__(256) void apply_fwd_kernel(const T* __restrict__ x,
   }
 }
 
-// g = dy masked by the recomputed pre-activation; part[p][c] = {sum g, sum g*xhat}
+// POOL: the BatchNorm's output went through the 3x3/2 max-pool (the ResNet stem) and dy is the
+// pooled gradient: a row's incoming gradient is gathered from the <= 2x2 windows that hold it and
+// picked it (maxpool_bwd_kernel's arithmetic, rounded to T as that kernel stores it) instead of
+// being read from a full-resolution gradient tensor that would first have to be written.
+struct PoolG {
+  const unsigned char* pos;
+  int H, W, Ho, Wo;
+};
 template <typename T, int V>
+__device__ __forceinline__ void pool_grad(const T* __restrict__ dy, const PoolG& pg, int q, int C, int c0,
+                                          float (&g)[V]) {
+  const int iw = q % pg.W, ih = (q / pg.W) % pg.H, b = q / (pg.W * pg.H);
+  const int oh0 = ih / 2, oh1 = min(pg.Ho - 1, (ih + 1) / 2);
+  const int ow0 = iw / 2, ow1 = min(pg.Wo - 1, (iw + 1) / 2);
+#pragma unroll
+  for (int j = 0; j < V; ++j) g[j] = 0.f;
+  for (int oh = oh0; oh <= oh1; ++oh)
+    for (int ow = ow0; ow <= ow1; ++ow) {
+      const int dh = ih - (2 * oh - 1), dw = iw - (2 * ow - 1);
+      if (dh < 0 || dh > 2 || dw < 0 || dw > 2) continue;
+      const int64_t o = (((int64_t)b * pg.Ho + oh) * pg.Wo + ow) * C + c0;
+      float d[V];
+      ldv<T, V>(dy + o, d);
+#pragma unroll
+      for (int j = 0; j < V; ++j)
+        if (pg.pos[o + j] == dh * 3 + dw) g[j] += d[j];
+    }
+#pragma unroll
+  for (int j = 0; j < V; ++j) {
+    T t;
+    E<T>::st(&t, g[j]);
+    g[j] = E<T>::ld(&t);
+  }
+}
+
+// g = dy masked by the recomputed pre-activation; part[p][c] = {sum g, sum g*xhat}
+template <typename T, int V, bool POOL>
 __global__ __launch_bounds__(256) void bwd_reduce_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                          const T* __restrict__ res, const float* __restrict__ stat,
                                                          int64_t M, int C, int rpb, int relu,
                                                          const unsigned char* __restrict__ mask,
-                                                         float* __restrict__ part) {
+                                                         float* __restrict__ part, PoolG pg) {
   __shared__ float sh[256 * kMaxV * 2];
   const RowSplit s = row_split(C, V);
   float sg[V], sgx[V];
@@ -245,7 +280,10 @@ __global__ __launch_bounds__(256) void bwd_reduce_kernel(const T* __restrict__ d
     for (int64_t r = r0 + s.rl; r < r1; r += s.lanes) {
       const int64_t off = r * C + s.c0;
       float g[V], v[V], rr[V];
-      ldv<T, V>(dy + off, g);
+      if constexpr (POOL)
+        pool_grad<T, V>(dy, pg, (int)r, C, s.c0, g);
+      else
+        ldv<T, V>(dy + off, g);
       ldv<T, V>(x + off, v);
       unsigned live = 0;
       if (mask != nullptr) live = mask[off / V];
@@ -301,12 +339,12 @@ __global__ __launch_bounds__(256) void finalize_bwd_kernel(const float* __restri
 
 // dx = k*(g - mean(g) - xhat*mean(g*xhat)), dres = g; per-channel operands in registers, rows walked
 // as in apply_fwd_kernel
-template <typename T, int V>
+template <typename T, int V, bool POOL>
 __global__ __launch_bounds__(256) void apply_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                         const T* __restrict__ res, const float* __restrict__ stat,
                                                         const float* __restrict__ coef, T* __restrict__ dx,
                                                         T* __restrict__ dres, int64_t M, int C, int rpb, int relu,
-                                                        const unsigned char* __restrict__ mask) {
+                                                        const unsigned char* __restrict__ mask, PoolG pg) {
   const RowSplit s = row_split(C, V);
   if (s.rl >= s.lanes) return;
   float sc[V], sf[V], mu[V], is[V], k[V], mg[V], mgx[V];
@@ -326,7 +364,10 @@ __global__ __launch_bounds__(256) void apply_bwd_kernel(const T* __restrict__ dy
   for (int64_t r = r0 + s.rl; r < r1; r += s.lanes) {
     const int64_t e = r * C + s.c0;
     float g[V], v[V], rr[V];
-    ldv<T, V>(dy + e, g);
+    if constexpr (POOL)
+      pool_grad<T, V>(dy, pg, (int)r, C, s.c0, g);
+    else
+      ldv<T, V>(dy + e, g);
     ldv<T, V>(x + e, v);
     unsigned live = 0;
     if (mask != nullptr) live = mask[e / V];
@@ -564,15 +605,24 @@ void bn_fwd_t(const void* x, const void* res, const float* w, const float* b, fl
 template <typename T, int V>
 void bn_bwd_t(const void* dy, const void* x, const void* res, const float* w, const float* stat, int relu, void* dx,
               void* dres, float* dw, float* db, float* coef, float* part, int64_t M, int C, const unsigned char* mask,
-              hipStream_t st) {
+              const PoolG* pool, hipStream_t st) {
   const BnGrid g = bn_grid(M, C, V);
-  hipLaunchKernelGGL((bwd_reduce_kernel<T, V>), dim3(g.P, g.CG), dim3(256), 0, st, (const T*)dy, (const T*)x,
-                     (const T*)res, stat, M, C, g.rpb, relu, mask, part);
+  const PoolG pg = pool != nullptr ? *pool : PoolG{nullptr, 0, 0, 0, 0};
+  if (pool != nullptr)
+    hipLaunchKernelGGL((bwd_reduce_kernel<T, V, true>), dim3(g.P, g.CG), dim3(256), 0, st, (const T*)dy, (const T*)x,
+                       (const T*)res, stat, M, C, g.rpb, relu, mask, part, pg);
+  else
+    hipLaunchKernelGGL((bwd_reduce_kernel<T, V, false>), dim3(g.P, g.CG), dim3(256), 0, st, (const T*)dy,
+                       (const T*)x, (const T*)res, stat, M, C, g.rpb, relu, mask, part, pg);
   hipLaunchKernelGGL(finalize_bwd_kernel, dim3((C + 7) / 8), dim3(256), 0, st, part, g.P, C, (double)M, w, stat, dw,
                      db, coef);
   const BnGrid a = apply_grid(M, C, V);
-  hipLaunchKernelGGL((apply_bwd_kernel<T, V>), dim3(a.P, a.CG), dim3(256), 0, st, (const T*)dy, (const T*)x,
-                     (const T*)res, stat, coef, (T*)dx, (T*)dres, M, C, a.rpb, relu, mask);
+  if (pool != nullptr)
+    hipLaunchKernelGGL((apply_bwd_kernel<T, V, true>), dim3(a.P, a.CG), dim3(256), 0, st, (const T*)dy, (const T*)x,
+                       (const T*)res, stat, coef, (T*)dx, (T*)dres, M, C, a.rpb, relu, mask, pg);
+  else
+    hipLaunchKernelGGL((apply_bwd_kernel<T, V, false>), dim3(a.P, a.CG), dim3(256), 0, st, (const T*)dy, (const T*)x,
+                       (const T*)res, stat, coef, (T*)dx, (T*)dres, M, C, a.rpb, relu, mask, pg);
 }
 
 // dispatch on (dtype, V) for a functor F<T, V>::run(args...)
@@ -611,9 +661,15 @@ hipError_t cs_bn_nhwc_fwd(int dt, const void* x, const void* res, const float* w
 
 hipError_t cs_bn_nhwc_bwd(int dt, const void* dy, const void* x, const void* res, const float* w, const float* stat,
                           int relu, void* dx, void* dres, float* dw, float* db, float* coef, float* part, int64_t M,
-                          int C, hipStream_t stream, const unsigned char* mask) {
+                          int C, hipStream_t stream, const unsigned char* mask, const unsigned char* pool_pos,
+                          int H, int W, int Ho, int Wo) {
   if (M * C == 0) return hipSuccess;
-  CS_NHWC_DISPATCH(dt, C, bn_bwd_t<T, V>(dy, x, res, w, stat, relu, dx, dres, dw, db, coef, part, M, C, mask, stream));
+  if (pool_pos != nullptr && (M >= kMaxItems || (int64_t)H * W <= 0 || M % ((int64_t)H * W) != 0 ||
+                              Ho != (H - 1) / 2 + 1 || Wo != (W - 1) / 2 + 1))
+    return hipErrorInvalidValue;
+  const PoolG pg{pool_pos, H, W, Ho, Wo};
+  const PoolG* pp = pool_pos != nullptr ? &pg : nullptr;
+  CS_NHWC_DISPATCH(dt, C, bn_bwd_t<T, V>(dy, x, res, w, stat, relu, dx, dres, dw, db, coef, part, M, C, mask, pp, stream));
   return hipGetLastError();
 }
 

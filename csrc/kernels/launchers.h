@@ -330,7 +330,11 @@ hipError_t cs_bn_nhwc_fwd(int dt, const void* x, const void* res, const float* w
                           int64_t M, int C, hipStream_t stream, unsigned char* mask = nullptr);
 hipError_t cs_bn_nhwc_bwd(int dt, const void* dy, const void* x, const void* res, const float* w, const float* stat,
                           int relu, void* dx, void* dres, float* dw, float* db, float* coef, float* part, int64_t M,
-                          int C, hipStream_t stream, const unsigned char* mask = nullptr);
+                          int C, hipStream_t stream, const unsigned char* mask = nullptr,
+                          const unsigned char* pool_pos = nullptr, int H = 0, int W = 0, int Ho = 0, int Wo = 0);
+// (pool_pos: the BatchNorm's output was 3x3/2 max-pooled (cs_maxpool3s2_nhwc_fwd's window positions
+// for the [B, Ho, Wo, C] output; x is [B, H, W, C]) and dy is the pooled gradient — the pool's
+// backward gather is fused into both BatchNorm backward passes)
 // stat (optional, a BatchNorm's [4][C] from cs_bn_nhwc_fwd with y == nullptr = statistics only):
 // pool relu(BN(x)) — the BatchNorm apply fused into the pool's window loads
 hipError_t cs_maxpool3s2_nhwc_fwd(int dt, const void* x, void* y, unsigned char* pos, int B, int H, int W, int C,

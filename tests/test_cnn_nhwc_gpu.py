@@ -139,17 +139,19 @@ def test_bn_act_nhwc_matches_fp64(dev, shape, dtype, relu, residual):
 @pytest.mark.parametrize("shape", [(2, 112, 112, 64), (3, 9, 7, 24), (2, 5, 6, 6)])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_bn_relu_maxpool_fused_equals_two_passes(dev, shape, dtype, monkeypatch):
-    """the stem's BatchNorm + ReLU + 3x3/2 max-pool with the apply fused into the pool (default) is
-    bitwise equal to BN-apply then pool (CS_BN_POOL_FUSE=0): output, input / weight / bias gradients
-    and running statistics"""
+    """the stem's BatchNorm + ReLU + 3x3/2 max-pool with the apply fused into the pool and the pool's
+    backward gather fused into the BatchNorm backward (CS_BN_POOL_FUSE_BWD=1) is bitwise equal to the separate
+    passes (CS_BN_POOL_FUSE=0 / CS_BN_POOL_FUSE_BWD=0): output, input / weight / bias gradients and
+    running statistics"""
     from cs744_pytorch_distributed_tutorial_amd.ops.cnn_nhwc import bn_relu_maxpool_nhwc
     torch.manual_seed(8)
     x0 = torch.randn(shape, device=dev).to(dtype)
     outs = []
-    for m in ("0", "1"):
+    for m, mb in (("0", "0"), ("1", "0"), ("1", "1")):
         monkeypatch.setenv("CS_BN_POOL_FUSE", m)
+        monkeypatch.setenv("CS_BN_POOL_FUSE_BWD", mb)
         bn = nn.BatchNorm2d(shape[3]).to(dev)
-        torch.manual_seed(10)  # the same affine parameters for both runs
+        torch.manual_seed(10)  # the same affine parameters for every run
         with torch.no_grad():
             bn.weight.uniform_(0.5, 1.5)
             bn.bias.uniform_(-0.5, 0.5)
@@ -158,8 +160,9 @@ def test_bn_relu_maxpool_fused_equals_two_passes(dev, shape, dtype, monkeypatch)
         g = torch.randn(y.shape, generator=torch.Generator(device=dev).manual_seed(9), device=dev).to(dtype)
         y.backward(g)
         outs.append((y, x.grad, bn.weight.grad, bn.bias.grad, bn.running_mean, bn.running_var))
-    for a, b in zip(*outs):
-        assert torch.equal(a, b)
+    for o in outs[1:]:
+        for a, b in zip(o, outs[0]):
+            assert torch.equal(a, b)
 
 
 @pytest.mark.parametrize("shape", [(4, 14, 14, 256), (3, 14, 14, 24), (2, 5, 3, 6)])
