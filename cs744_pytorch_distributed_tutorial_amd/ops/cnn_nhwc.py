@@ -74,6 +74,8 @@ def _wgrad(dy2: torch.Tensor, col: torch.Tensor) -> torch.Tensor:
     a = dy2.view(S, M // S, Co).transpose(1, 2)
     b = col.view(S, M // S, Kp)
     part = torch.bmm(a, b, out_dtype=torch.float32) if col.dtype != torch.float32 else torch.bmm(a, b)
+    if Co * Kp % 4 == 0 and os.environ.get("CS_SLAB_SUM", "1") != "0":
+        return native.C().slab_sum(part)  # split-lane slab sum (csrc/kernels/conv_nhwc.hip)
     return part.sum(0)
 
 

@@ -92,6 +92,18 @@ torch::Tensor conv_nhwc_bf16(int64_t mode, torch::Tensor a, torch::Tensor b, int
   return out;
 }
 
+// [S, ...] fp32 partials -> their sum over dim 0 (fixed order: deterministic)
+torch::Tensor slab_sum(torch::Tensor part) {
+  TORCH_CHECK(part.is_cuda() && part.is_contiguous() && part.scalar_type() == at::kFloat && part.dim() >= 2,
+              "slab_sum: contiguous fp32 [S, ...] GPU tensor");
+  const int64_t S = part.size(0), n = part.numel() / std::max<int64_t>(S, 1);
+  TORCH_CHECK(S >= 1 && n % 4 == 0, "slab_sum: the slab size must be a multiple of 4");
+  DevGuard g(part.device());
+  auto out = torch::empty(part.sizes().slice(1), part.options());
+  CS_LAUNCH(cs_slab_sum(part.data_ptr<float>(), (int)S, n, out.data_ptr<float>(), cur_stream()));
+  return out;
+}
+
 // -> {y, stat [4, C] = scale, shift, mean, invstd, ReLU mask (with_mask; else undefined)}
 std::vector<torch::Tensor> bn_nhwc_fwd(torch::Tensor x, c10::optional<torch::Tensor> res,
                                        c10::optional<torch::Tensor> w, c10::optional<torch::Tensor> b,
@@ -288,6 +300,7 @@ void register_nhwc_ops(pybind11::module& m) {
         "bf16 NHWC implicit-GEMM conv: mode 0 fwd (a=x, b=w[Co,R,S,C]) -> y; 1 dgrad (a=dy, b=wt[C,R,S,Co]) -> dx; "
         "2 wgrad (a=dy, b=x) -> fp32 dW [Co, R*S*C]; a 4-channel x (the stem, S <= 8) uses kernel rows padded "
         "to 8 taps: weight [Co, R, 8, 4], dW [Co, R*32]");
+  m.def("slab_sum", &slab_sum, "sum of fp32 partial slabs over dim 0, deterministic");
   m.def("bn_nhwc_fwd", &bn_nhwc_fwd, "training BatchNorm2d (+residual) (+ReLU), NHWC fp32/bf16 -> (y, stat, mask)",
         pybind11::arg("x"), pybind11::arg("res"), pybind11::arg("w"), pybind11::arg("b"), pybind11::arg("rm"), pybind11::arg("rv"), pybind11::arg("nbt"),
         pybind11::arg("momentum"), pybind11::arg("eps"), pybind11::arg("relu"), pybind11::arg("with_mask") = false);

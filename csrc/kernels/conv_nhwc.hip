@@ -387,6 +387,20 @@ hipError_t launch(const CsConvNhwcArgs& p, int splits, hipStream_t stream) {
 
 }  // namespace
 
+// out[n] = sum over z of part[z][n] (z in order within each split lane, lanes in order): the
+// deterministic slab sum of the weight-gradient GEMMs, also used by ops/cnn_nhwc._wgrad for its
+// row-chunk partials (n % 4 == 0, 16-byte aligned buffers)
+hipError_t cs_slab_sum(const float* part, int splits, int64_t n, float* out, hipStream_t stream) {
+  if (n % 4 || splits < 1) return hipErrorInvalidValue;
+  const int64_t n4 = n / 4;
+  int SL = 1;
+  while (SL < 16 && SL * 32 < splits) SL *= 2;
+  const int64_t blocks = (n4 + 256 / SL - 1) / (256 / SL);
+  if (blocks == 0) return hipSuccess;
+  hipLaunchKernelGGL(conv_nhwc_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, part, splits, SL, n4, out);
+  return hipGetLastError();
+}
+
 int cs_conv_nhwc_splits(int mode, int B, int H, int W, int C, int Co, int R, int S, int st, int pad) {
   if (mode != CS_CONV_WGRAD) return 1;
   const int Ho = (H + 2 * pad - R) / st + 1, Wo = (W + 2 * pad - S) / st + 1;
@@ -450,11 +464,5 @@ hipError_t cs_conv_nhwc(int mode, const CsConvNhwcArgs& in, int splits, hipStrea
     e = wide ? launch<128, 128, CS_CONV_WGRAD>(p, splits, stream) : launch<128, 64, CS_CONV_WGRAD>(p, splits, stream);
   if (e != hipSuccess || mode != CS_CONV_WGRAD) return e;
   // the caller's dw_out receives the split-ordered sum (slabs in p.dw)
-  const int64_t n4 = (int64_t)p.M * p.N / 4;
-  int SL = 1;  // split lanes per column: up to 16, about 32 slabs per lane
-  while (SL < 16 && SL * 32 < splits) SL *= 2;
-  const int64_t blocks = (n4 + 256 / SL - 1) / (256 / SL);
-  hipLaunchKernelGGL(conv_nhwc_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, p.dw, splits, SL, n4,
-                     p.dw_out);
-  return hipGetLastError();
+  return cs_slab_sum(p.dw, splits, (int64_t)p.M * p.N, p.dw_out, stream);
 }

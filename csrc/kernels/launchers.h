@@ -356,6 +356,8 @@ struct CsConvNhwcArgs {
   // filled by the launcher
   int Ho, Wo, M, N, K, ksteps, ksteps_per_split;
 };
+// out[n] = deterministic sum of part[z][n] over z < splits (fp32; n % 4 == 0)
+hipError_t cs_slab_sum(const float* part, int splits, int64_t n, float* out, hipStream_t stream);
 int cs_conv_nhwc_splits(int mode, int B, int H, int W, int C, int Co, int R, int S, int st, int pad);
 hipError_t cs_conv_nhwc(int mode, const CsConvNhwcArgs& a, int splits, hipStream_t stream);
 // col: [B*Ho*Wo, Kp], columns (r*S + s)*C + c, zero for k >= R*S*C; col2im is its adjoint (gather)

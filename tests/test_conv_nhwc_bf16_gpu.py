@@ -146,3 +146,15 @@ def test_resnet_stem_implicit_vs_im2col(C, monkeypatch):
         outs.append((y.detach().float(), conv.weight.grad.float()))
     for a, b in zip(*outs):
         assert _rel(a, b) < 1e-2
+
+
+@pytest.mark.parametrize("S,shape", [(64, (64, 256)), (3, (5, 12)), (512, (64, 224)), (1, (8, 8))])
+def test_slab_sum_matches_fp64_and_is_deterministic(C, S, shape):
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(12)
+    part = torch.randn(S, *shape, device=dev)
+    a = C.slab_sum(part)
+    b = C.slab_sum(part)
+    torch.cuda.synchronize()
+    assert a.shape == shape and torch.equal(a, b)
+    assert _rel(a, part.double().sum(0)) < 1e-6
