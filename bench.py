@@ -122,6 +122,68 @@ def comm_ctas_used(trainer):
     return getattr(native, "max_ctas", None)
 
 
+def _sysfs_card(device) -> str | None:
+    """/sys/class/drm/cardN/device of the GPU torch calls `device` (matched by PCI address)."""
+    import glob
+    try:
+        p = torch.cuda.get_device_properties(device)
+        want = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}."
+    except Exception:  # noqa: BLE001
+        return None
+    for d in sorted(glob.glob("/sys/class/drm/card*/device")):
+        if os.path.basename(os.path.realpath(d)).startswith(want):
+            return d
+    return None
+
+
+def _dpm_current(path: str):
+    """The active level of a pp_dpm_* table ('1: 2400Mhz *' -> 2400)."""
+    try:
+        for line in open(path):
+            if line.rstrip().endswith("*"):
+                return int("".join(ch for ch in line.split(":", 1)[1] if ch.isdigit()))
+    except (OSError, ValueError, IndexError):
+        pass
+    return None
+
+
+def calibration(device) -> dict:
+    """Box fingerprint taken AFTER the timed steps (it never touches `value`): the GPU's current
+    shader / memory clock levels and power cap from sysfs, and the throughput of a fixed bf16 MFMA
+    GEMM (hipBLASLt, 4096^3, ~1 ms per call) — so a slow box and a slow code change can be told
+    apart when two runs of the same tree disagree."""
+    out = {}
+    card = _sysfs_card(device)
+    if card:
+        out["sclk_mhz"] = _dpm_current(os.path.join(card, "pp_dpm_sclk"))
+        out["mclk_mhz"] = _dpm_current(os.path.join(card, "pp_dpm_mclk"))
+        import glob
+        for h in glob.glob(os.path.join(card, "hwmon", "hwmon*")):
+            for key, name in (("power_cap_w", "power1_cap"), ("power_w", "power1_average")):
+                try:
+                    out[key] = round(int(open(os.path.join(h, name)).read()) / 1e6, 1)
+                except (OSError, ValueError):
+                    pass
+    try:
+        n = 4096
+        a = torch.randn(n, n, device=device, dtype=torch.bfloat16)
+        b = torch.randn(n, n, device=device, dtype=torch.bfloat16)
+        for _ in range(3):
+            torch.mm(a, b)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        reps = 20
+        e0.record()
+        for _ in range(reps):
+            torch.mm(a, b)
+        e1.record()
+        e1.synchronize()
+        ms = e0.elapsed_time(e1) / reps
+        out["mfma_bf16_gemm_tflops"] = round(2 * n ** 3 / (ms * 1e-3) / 1e12, 1)
+    except Exception as e:  # noqa: BLE001
+        out["mfma_error"] = str(e)[:80]
+    return out
+
+
 def main(argv=None) -> int:
     args = parse(argv)
     if args.batch_size is None:
@@ -217,6 +279,8 @@ def main(argv=None) -> int:
         out["config"]["conv_gemm_math"] = {m: maths.count(m) for m in sorted(set(maths))}
         out["config"]["conv_tiles"] = getattr(trainer, "tile_source", None)
         out["config"]["wgrad_side_stream"] = getattr(trainer, "overlap_wgrad", None)
+    if os.environ.get("CS744_BENCH_CALIBRATE", "1") != "0":
+        out["calibration"] = calibration(device)
     if args.phases > 0 and hasattr(trainer, "phase_breakdown"):
         ph = trainer.phase_breakdown(args.phases)
         if rank == 0:

@@ -53,6 +53,9 @@ def main():
     scratch = torch.zeros(1024, device=dev)
     extra = [] if a.extra_after else make_extra()
     t = NativeTrainer(batch_size=64, device=dev, graph="auto")
+    from bench import _dpm_current, _sysfs_card
+    card = _sysfs_card(dev)
+    print(json.dumps({"sysfs_card": card, "sclk_mhz_idle": _dpm_current(os.path.join(card, "pp_dpm_sclk")) if card else None}), flush=True)
     if a.extra_after:
         extra = make_extra()
     for _ in range(a.warmup):
@@ -71,7 +74,8 @@ def main():
                 with torch.cuda.stream(st):
                     scratch.add_(1.0)
         rows.append({"window": w, "ms_per_step": round((t2 - t0) * 1e3 / a.window, 4),
-                     "host_enqueue_ms_per_step": round((t1 - t0) * 1e3 / a.window, 4)})
+                     "host_enqueue_ms_per_step": round((t1 - t0) * 1e3 / a.window, 4),
+                     "sclk_mhz": _dpm_current(os.path.join(card, "pp_dpm_sclk")) if card else None})
         print(json.dumps(rows[-1]), flush=True)
     t.check_comm()  # raises if a side-stream link wait timed out
     print("links ok", flush=True)
