@@ -148,27 +148,26 @@ ASAN_FLAGS = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fno-omit-fra
 
 
 def build_asan(jobs: int = 0, verbose: bool = False) -> str:
-    """Standalone AddressSanitizer build of the C++ runtime (runtime/*.cpp + the kernels' host
-    launchers) and csrc/tests/asan_runtime_test.cpp. A separate object tree
-    (build/asan); the product _C.so is untouched."""
+    """Standalone AddressSanitizer build of the C++ runtime (runtime/*.cpp) and
+    csrc/tests/asan_runtime_test.cpp, linked against the product build's kernel
+    objects (device code is never sanitized, so the kernels and their launchers are the
+    ``build()`` objects as they are — a separate ASan object tree for the runtime only, and a
+    program a fraction of the size of an all-sanitized one). The product _C.so is untouched."""
+    build(jobs)  # the kernel objects (incremental)
     obj_dir = os.path.join(ROOT, "build", "asan")
     os.makedirs(obj_dir, exist_ok=True)
     os.makedirs(os.path.dirname(ASAN_OUT), exist_ok=True)
-    hip = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
+    hip_objs = [_obj_path(f) for f in sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))]
     cpp = sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp"))) + [os.path.join(CSRC, "tests", "asan_runtime_test.cpp")]
     _, tinc, tlib = _torch_paths()
     incs = [f"-I{p}" for p in tinc] + [f"-I{sysconfig.get_paths()['include']}", f"-I{ROCM}/include"]
-    todo, objs = [], []
-    for src in hip + cpp:
+    todo, objs = [], list(hip_objs)
+    for src in cpp:
         o = os.path.join(obj_dir, os.path.relpath(src, CSRC).replace(os.sep, "__") + ".o")
         objs.append(o)
         if not os.path.exists(o) or os.path.getmtime(o) < max(os.path.getmtime(src), _deps_mtime(o)):
-            if src.endswith(".hip"):
-                cmd = [HIPCC, f"--offload-arch={ARCH}", *_common_flags(), *ASAN_FLAGS, "-MD", "-MF", o + ".d", "-c",
-                       src, "-o", o]
-            else:
-                cmd = [HIPCC, *_common_flags(), *ASAN_FLAGS, *incs, "-D_GLIBCXX_USE_CXX11_ABI=1", "-DUSE_ROCM=1",
-                       "-MD", "-MF", o + ".d", "-x", "c++", "-c", src, "-o", o]
+            cmd = [HIPCC, *_common_flags(), *ASAN_FLAGS, *incs, "-D_GLIBCXX_USE_CXX11_ABI=1", "-DUSE_ROCM=1",
+                   "-MD", "-MF", o + ".d", "-x", "c++", "-c", src, "-o", o]
             todo.append((src, cmd))
 
     def run(item):

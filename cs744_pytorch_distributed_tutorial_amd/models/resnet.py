@@ -34,7 +34,7 @@ import torch.nn as nn
 
 from ..ops.cnn import bn_act, max_pool3s2
 from ..ops.cnn_nhwc import (ResidualGradSink, act_dtype, bn_act_nhwc, bn_relu_maxpool_nhwc, conv_nhwc,
-                            residual_sink_ok, to_nhwc, weights_channels_last)
+                            residual_sink_ok, to_nhwc)
 
 
 def conv3x3(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
@@ -142,10 +142,6 @@ class ResNet(nn.Module):
                 last = getattr(m, "bn3", None) if isinstance(m, Bottleneck) else getattr(m, "bn2", None)
                 if isinstance(m, (Bottleneck, BasicBlock)) and last is not None:
                     nn.init.zeros_(last.weight)
-        if layout == "nhwc" and os.environ.get("CS_CONV_WEIGHT_CL", "0") == "1":
-            # [Co, R, S, Ci] in memory: no per-step weight permutes; measured even at ResNet-50 B=256
-            # (8.82k vs 8.87k img/s, profiles/r3_resnet50_fusions_ab.txt), so opt-in
-            weights_channels_last(self)
 
     def _make_layer(self, block, width: int, blocks: int, stride: int = 1) -> nn.Sequential:
         down = None

@@ -79,18 +79,6 @@ def _wgrad(dy2: torch.Tensor, col: torch.Tensor) -> torch.Tensor:
     return part.sum(0)
 
 
-def weights_channels_last(model: nn.Module) -> nn.Module:
-    """Lay the k x k (k > 1) conv weights of a channels-last model out as [Co, R, S, Ci] in memory
-    (torch.channels_last; shape and state_dict keys unchanged): the NHWC convolutions then read
-    them without a permuting copy per forward, and their weight gradients come out of the GEMM in
-    that layout with no copy back (the fused SGD and the DDP flat buffer take any dense layout
-    shared by parameter and gradient). 1x1 weights keep the standard strides."""
-    for m in model.modules():
-        if isinstance(m, nn.Conv2d) and tuple(m.kernel_size) != (1, 1):
-            m.weight.data = m.weight.data.contiguous(memory_format=torch.channels_last)
-    return model
-
-
 def _weight_grad(v: torch.Tensor, ctx) -> torch.Tensor:
     """a [Co, Ci, R, S] view of a GEMM's fp32 weight gradient -> the gradient in the weight's own
     layout (autograd would otherwise copy it to match): the view itself when it already is that
@@ -345,7 +333,8 @@ class _BnReluPoolNHWC(torch.autograd.Function):
     """max_pool3s2(relu(bn(x))) with the BatchNorm apply fused into the pool's window loads: the
     full-resolution activation is never written (forward) — the ResNet stem's 112x112x64 one is
     411 MB at B=256. Backward: the pool's gather pass, then the BatchNorm backward with the ReLU mask
-    recomputed from x (CS_BN_POOL_FUSE_BWD=1: the gather inside both BatchNorm passes instead)."""
+    recomputed from x (the gather inside both BatchNorm passes measured 0.2-0.4 % slower,
+    profiles/r3_resnet50_fusions_ab.txt, and was dropped in round 4)."""
 
     @staticmethod
     def forward(ctx, x, weight, bias, running_mean, running_var, nbt, momentum, eps):
@@ -357,13 +346,8 @@ class _BnReluPoolNHWC(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, weight, stat, pos = ctx.saved_tensors
-        # opt-in: the pool's gather inside both BN passes measured 0.2-0.4 % slower than a gather pass
-        # writing the full-resolution gradient (profiles/r3_resnet50_fusions_ab.txt)
-        if os.environ.get("CS_BN_POOL_FUSE_BWD", "0") == "1":
-            dx, dw, db = native.C().bn_relu_maxpool_nhwc_bwd(dy.contiguous(), pos, x, weight, stat)
-        else:
-            g = native.C().maxpool3s2_nhwc_bwd(dy.contiguous(), pos, x.shape[1], x.shape[2])
-            dx, _, dw, db = native.C().bn_nhwc_bwd(g, x, None, weight, stat, True, False)
+        g = native.C().maxpool3s2_nhwc_bwd(dy.contiguous(), pos, x.shape[1], x.shape[2])
+        dx, _, dw, db = native.C().bn_nhwc_bwd(g, x, None, weight, stat, True, False)
         return dx, dw, db, None, None, None, None, None
 
 

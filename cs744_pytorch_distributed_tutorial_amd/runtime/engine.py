@@ -193,13 +193,13 @@ class NativeTrainer:
                  dtype: str = "fp32", probe: Optional[str] = None, probe_spin_us: float = 20.0,
                  check_every: int = 0, timeout_s: float = 1800.0):
         C = native.C()
-        # a stream-link wait (side-stream joins, communicator fork/join) releases its consumer
+        # a stream-link wait (communicator fork/join) releases its consumer
         # early only after the communicator timeout or on abort(): never before a late peer
         C.set_link_timeout(float(timeout_s))
         C.reset_link_abort()
         self.device = device or torch.device("cuda", torch.cuda.current_device())
         with torch.cuda.device(self.device):
-            C.reserve_streams()  # the engine's side stream gets its own hardware queue (device_comm.h)
+            C.reserve_streams()  # the communicator's stream gets its own hardware queue (device_comm.h)
         self.rank, self.world = rank, world
         self.B = batch_size
         self.lr, self.momentum, self.wd, self.damp = lr, momentum, weight_decay, dampening
@@ -241,6 +241,14 @@ class NativeTrainer:
                 from ..parallel.staged import ProbeComm
                 spin = float(os.environ.get("CS_PROBE_SPIN", probe_spin_us))  # < 0: fork/join only
                 self._probe = ProbeComm(self.device.index or 0, spin)
+            elif probe.startswith("xgmi"):
+                # N > 1 projection on one GPU: every collective = a spin as long as a ring all-reduce
+                # of its bytes over W GPUs at G GB/s bus bandwidth plus a latency term ("xgmi:G:W:us",
+                # defaults 150 GB/s, 8 GPUs, 25 us): the real step schedule with modelled collectives
+                from ..parallel.staged import ProbeComm
+                f = (probe.split(":") + ["", "", ""])[1:4]
+                self._probe = ProbeComm(self.device.index or 0, float(f[2] or 25.0), float(f[0] or 150.0),
+                                        int(f[1] or 8))
             else:
                 # measurement only: a one-rank RCCL communicator so the engine's bucketed all-reduce,
                 # buffer broadcast and stream fork/join run (and cost what they cost) on one GPU
@@ -256,8 +264,6 @@ class NativeTrainer:
             assert off == at, "bucket plan must tile the flat parameter buffer"
             at += n
         assert at == lay.total, "bucket plan must cover the flat parameter buffer"
-        # opt-in (CS_SGD_OVERLAP=1): per-bucket SGD on the engine's optimizer stream (see vgg_engine.h)
-        self.sgd_overlap = os.environ.get("CS_SGD_OVERLAP", "0") != "0"
         self.flat_sync = FlatGradSync(self.sync_mode if self.sync_mode != "ddp" else "none", self.comm,
                                       lay.param_ranges(), lay.total) if self.comm is not None else None
 
@@ -277,29 +283,6 @@ class NativeTrainer:
         self._probe = getattr(self, "_probe", None)
         self.engine = C.VggEngine(self.B, lay.desc(), lay.offs(), lay.buf_offs(), lay.feat, lay.ncls,
                                   self.params, self.grads, self.mom, self.bufs, self.nbt)
-        # weight gradients on a side stream (bit-identical to the serial backward): opt-in
-        # (CS_OVERLAP_WGRAD=1). Round 3 measured the serial backward faster on MI355X (B=64, two
-        # boxes, interleaved runs): 81.7-81.8k img/s serial vs 76.3k with the side stream — a
-        # side-stream weight-gradient GEMM takes every CU it lands on (its blocks fill the whole
-        # register file), so the critical chain's next kernel waits for side blocks to drain,
-        # which costs more than the overlap wins (scripts/ab_matrix.sh; profiles/r3_overlap_ab.txt).
-        # With it on, it still needs >= 8 HIP hardware queues when a communicator runs, is off under
-        # rocprofv3 counter collection (which serialises every dispatch: a side-stream link wait
-        # would spin to its timeout), and collectives issued from Python (comm="torch": gloo copies
-        # each bucket to the host) need the side stream's results released to SYSTEM scope before
-        # that copy: round 2 measured a stale layers.25.weight gradient at world 2 without it, so
-        # the join then also waits on a system-release event (VggEngine::join_side; CS_SYS_JOIN=0
-        # drops it, and without it the overlap stays off for Python collectives unless
-        # CS_OVERLAP_WGRAD=force).
-        from .. import hw_queues
-        python_collectives = world > 1 and self.native_comm is None
-        sj = os.environ.get("CS_SYS_JOIN")
-        self.sys_join = python_collectives if sj is None else sj != "0"
-        ow = os.environ.get("CS_OVERLAP_WGRAD", "0")
-        self.overlap_wgrad = ow != "0" and (ow == "force" or self.sys_join or not python_collectives) and (
-            self.native_comm is None or hw_queues() >= 8) and not self._counters
-        self.engine.set_overlap_wgrad(self.overlap_wgrad)
-        self.engine.set_sys_join(self.sys_join)
         self.engine.set_data(0, self.train_data, self.train_labels, self.aug_train)
         self.engine.set_data(1, self.test_data, self.test_labels, self.aug_test)
         self.idx_buf = self.engine.idx()
@@ -479,10 +462,6 @@ class NativeTrainer:
             early = self.native_comm is not None and self.broadcast_buffers
             if not early:
                 self._pre_forward_sync()
-            # native comm: each bucket's SGD runs on the engine's optimizer stream once its
-            # all-reduce is in (and its weights' last reader, the bucket's lowest dgrad, is
-            # done), overlapping the backward of the blocks below
-            sgd_overlap = self.native_comm is not None and self.sgd_overlap
             handles = []
             for k in range(nseg):
                 if graphs is not None:
@@ -493,15 +472,8 @@ class NativeTrainer:
                 if early and k == 0:
                     self.native_comm.broadcast(self.bufs, 0)
                     self.native_comm.broadcast(self.nbt, 0)
-                if sgd_overlap:
-                    off, n = self.bucket_ranges[k]
-                    self.engine.sgd_bucket(self.native_comm, self.bucket_lows[k], off, n, self.lr, self.momentum,
-                                           self.wd, self.damp, k == nseg - 1)
             for h in handles:
                 h.wait()
-            if sgd_overlap:
-                self.engine.join_opt()
-                return
         else:
             for k in range(nseg):
                 if graphs is not None:
@@ -544,10 +516,7 @@ class NativeTrainer:
         """Async-error poll of the native communicator (ncclCommGetAsyncError for RCCL): on an
         error the communicator is aborted (ncclCommAbort) and the step raises, so a dead peer
         becomes a prompt failure instead of a hang. Also raises when one of the
-        engine's own side-stream links timed out (its ordering can no longer be trusted)."""
-        link = self.engine.link_error()
-        if link:
-            raise RuntimeError(f"rank {self.rank}: engine stream link failed: {link}")
+        communicator's fork/join stream links timed out (its ordering can no longer be trusted)."""
         if self.native_comm is None:
             return
         err = self.native_comm.async_error()

@@ -201,34 +201,6 @@ std::vector<torch::Tensor> bn_relu_maxpool_nhwc_fwd(torch::Tensor x, c10::option
   return {y, pos, stat};
 }
 
-// its backward from the pooled gradient -> {dx, dweight, dbias} (the pool's gather fused into the
-// BatchNorm backward passes: no full-resolution gradient tensor)
-std::vector<torch::Tensor> bn_relu_maxpool_nhwc_bwd(torch::Tensor dy, torch::Tensor pos, torch::Tensor x,
-                                                    c10::optional<torch::Tensor> w, torch::Tensor stat) {
-  check_nhwc(x, "bn_relu_maxpool_nhwc_bwd");
-  check_nhwc(dy, "bn_relu_maxpool_nhwc_bwd");
-  const int dt = act_dt(x, "bn_relu_maxpool_nhwc_bwd");
-  const int64_t B = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3), M = x.numel() / C;
-  const int64_t Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
-  TORCH_CHECK(dy.scalar_type() == x.scalar_type() && dy.size(0) == B && dy.size(1) == Ho && dy.size(2) == Wo &&
-                  dy.size(3) == C, "bn_relu_maxpool_nhwc_bwd: dy must be the pooled [B, Ho, Wo, C] gradient");
-  TORCH_CHECK(pos.is_cuda() && pos.is_contiguous() && pos.scalar_type() == at::kByte && pos.sizes() == dy.sizes(),
-              "bn_relu_maxpool_nhwc_bwd: pos");
-  check_param(w, C, "weight");
-  TORCH_CHECK(stat.is_cuda() && stat.scalar_type() == at::kFloat && stat.numel() == 4 * C, "bn_relu_maxpool_nhwc_bwd: stat");
-  DevGuard g(x.device());
-  auto fo = x.options().dtype(at::kFloat);
-  auto dx = torch::empty_like(x);
-  auto dw = torch::empty({C}, fo), db = torch::empty({C}, fo);
-  auto coef = torch::empty({3, C}, fo);
-  auto part = torch::empty({cs_bn_nhwc_partials(M, (int)C, dt)}, fo);
-  CS_LAUNCH(cs_bn_nhwc_bwd(dt, dy.data_ptr(), x.data_ptr(), nullptr, opt_ptr<float>(w), stat.data_ptr<float>(), 1,
-                           dx.data_ptr(), nullptr, dw.data_ptr<float>(), db.data_ptr<float>(), coef.data_ptr<float>(),
-                           part.data_ptr<float>(), M, (int)C, cur_stream(), nullptr, pos.data_ptr<uint8_t>(), (int)H,
-                           (int)W, (int)Ho, (int)Wo));
-  return {dx, dw, db};
-}
-
 // 3x3 / 2 pad-1 max-pool -> {y, pos (uint8 window position per output element)}
 std::vector<torch::Tensor> maxpool3s2_nhwc_fwd(torch::Tensor x) {
   check_nhwc(x, "maxpool3s2_nhwc_fwd");
@@ -309,8 +281,6 @@ void register_nhwc_ops(pybind11::module& m) {
         pybind11::arg("need_dres"), pybind11::arg("mask") = pybind11::none());
   m.def("bn_relu_maxpool_nhwc_fwd", &bn_relu_maxpool_nhwc_fwd,
         "training BatchNorm2d + ReLU + 3x3/2 max-pool, NHWC, the apply fused into the pool -> (y, pos, stat)");
-  m.def("bn_relu_maxpool_nhwc_bwd", &bn_relu_maxpool_nhwc_bwd,
-        "its backward from the pooled gradient (pool gather fused into the BatchNorm passes) -> (dx, dw, db)");
   m.def("maxpool3s2_nhwc_fwd", &maxpool3s2_nhwc_fwd, "3x3/2 pad-1 max-pool, NHWC -> (y, window position)");
   m.def("maxpool3s2_nhwc_bwd", &maxpool3s2_nhwc_bwd, "its gather-style backward");
   m.def("im2col_nhwc", &im2col_nhwc, "NHWC im2col -> [B*Ho*Wo, Kp], columns (r, s, c)");

@@ -43,8 +43,8 @@ void check_gpu(const torch::Tensor& t, const char* name) {
 
 void register_runtime(pybind11::module& m) {
   m.def("reserve_streams", &cs::reserve_streams,
-        "create (once per process) the native engine's side stream and bind it to a hardware queue; call it "
-        "before other code creates streams");
+        "create (once per process) the native communicator's stream and bind it to a hardware queue; call "
+        "it before other code creates streams");
   namespace py = pybind11;
   m.def("rccl_unique_id", []() { return py::bytes(cs::RcclComm::unique_id()); });
   m.def("rccl_version", []() {
@@ -90,7 +90,8 @@ void register_runtime(pybind11::module& m) {
   py::class_<cs::StagedComm, cs::DeviceComm>(m, "StagedComm")
       .def(py::init<const std::string&, int>(), py::arg("group_name"), py::arg("device"));
   py::class_<cs::ProbeComm, cs::DeviceComm>(m, "ProbeComm")
-      .def(py::init<int, double>(), py::arg("device"), py::arg("spin_us") = 20.0);
+      .def(py::init<int, double, double, int>(), py::arg("device"), py::arg("spin_us") = 20.0, py::arg("gbps") = 0.0,
+           py::arg("world") = 8);
   py::class_<cs::RcclComm, cs::DeviceComm>(m, "RcclComm")
       .def(py::init([](py::bytes uid, int rank, int world, int device, bool high_priority, int max_ctas) {
              return new cs::RcclComm(std::string(uid), rank, world, device, high_priority, max_ctas);
@@ -173,28 +174,19 @@ void register_runtime(pybind11::module& m) {
       .def("num_blocks", &cs::VggEngine::num_blocks)
       .def("tensor", &cs::VggEngine::tensor)
       .def("forward_train", &cs::VggEngine::forward_train)
-      .def("backward", &cs::VggEngine::backward, py::arg("hi"), py::arg("lo"), py::arg("B"),
-           py::arg("join") = true)
+      .def("backward", &cs::VggEngine::backward, py::arg("hi"), py::arg("lo"), py::arg("B"))
       .def("sgd", &cs::VggEngine::sgd)
       .def("forward_eval", &cs::VggEngine::forward_eval)
       .def("step", &cs::VggEngine::step, py::arg("B"), py::arg("comm").none(true), py::arg("bucket_blocks"),
            py::arg("bucket_ranges"), py::arg("broadcast_buffers"), py::arg("lr"), py::arg("momentum"),
            py::arg("wd"), py::arg("dampening"))
-      .def("set_overlap_wgrad", &cs::VggEngine::set_overlap_wgrad)
-      .def("set_sys_join", &cs::VggEngine::set_sys_join)
-      .def("set_sgd_overlap", &cs::VggEngine::set_sgd_overlap)
-      .def("set_sgd_side", &cs::VggEngine::set_sgd_side)
-      .def("link_error", &cs::VggEngine::link_error)
       .def("set_sgd_first", &cs::VggEngine::set_sgd_first)
+      .def("set_sgd_tail", &cs::VggEngine::set_sgd_tail)
+      .def("set_fin", &cs::VggEngine::set_fin)
       .def("set_debug_skip", &cs::VggEngine::set_debug_skip)
       .def("set_timing", &cs::VggEngine::set_timing)
       .def("set_math", &cs::VggEngine::set_math)
       .def("phase_times", &cs::VggEngine::phase_times)
-      .def("join_opt", &cs::VggEngine::join_opt)
-      .def("sgd_bucket", &cs::VggEngine::sgd_bucket, py::arg("comm").none(true), py::arg("lo_block"), py::arg("off"),
-           py::arg("n"), py::arg("lr"), py::arg("momentum"), py::arg("wd"), py::arg("dampening"),
-           py::arg("advance_cursor"))
-      .def("set_fixup", &cs::VggEngine::set_fixup)
       .def("set_dual", &cs::VggEngine::set_dual)
       .def("set_bn_fused_rows", &cs::VggEngine::set_bn_fused_rows)
       .def("block_dual", &cs::VggEngine::block_dual)

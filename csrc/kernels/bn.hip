@@ -520,108 +520,7 @@ __global__ __launch_bounds__(256) void bn_fused_bwd_kernel(const float* __restri
                           c0);
 }
 
-// Two-launch backward for the larger layers (both channel-sliced like the fused kernel: 16
-// channels x a chunk of units per block): (1) per-chunk partial sums of (dy, dy*xhat, xhat)
-// -> part [chunks][C][3]; (2) every block re-sums the few chunk partials of its 16 channels
-// (fixed order, identical in every block), block row 0 publishes dgamma / dbeta / dbias, and
-// the block writes dZ for its own chunk of units — the finalize launch of the three-launch
-// path folded into the apply.
-template <bool POOL>
-__global__ __launch_bounds__(256) void bn_bwd_red_kernel(const float* __restrict__ y, const float* __restrict__ G,
-                                                         int B, int H, int W, int C, const float* __restrict__ bnv,
-                                                         float* __restrict__ part, int upb) {
-  __shared__ float lds[4 * 4 * 3 * 4];
-  const int cq = threadIdx.x & 3, rl = threadIdx.x >> 2;
-  const int cqg = blockIdx.x * 4 + cq;
-  const int units = POOL ? B * (H >> 1) * (W >> 1) : B * H * W;
-  const int u_end = min(units, (int)(blockIdx.y + 1) * upb);
-  float acc[3][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-  for (int u = blockIdx.y * upb + rl; u < u_end; u += 64)
-    bwd_visit<false, POOL>(y, G, B, H, W, C, cqg, u, bnv, bnv + C, bnv + 2 * C, bnv + 3 * C, nullptr, nullptr, acc);
-  sum_reduce_block(acc, lds);
-  if (threadIdx.x < 4)
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int k = 0; k < 3; ++k) part[((size_t)blockIdx.y * C + 4 * cqg + q) * 3 + k] = acc[k][q];
-}
-
-template <bool POOL>
-__global__ __launch_bounds__(256) void bn_bwd_fapply_kernel(const float* __restrict__ y, const float* __restrict__ G,
-                                                            int B, int H, int W, int C, const float* __restrict__ bnv,
-                                                            const float* __restrict__ gamma,
-                                                            const float* __restrict__ part, int nchunks,
-                                                            float* __restrict__ dgamma, float* __restrict__ dbeta,
-                                                            float* __restrict__ dbias, float* __restrict__ dz, int upb) {
-  __shared__ float lds[4 * 4 * 3 * 4];
-  __shared__ float coef[1024 * 3];  // indexed by global channel; this block fills its 16
-  const int cq = threadIdx.x & 3, rl = threadIdx.x >> 2;
-  const int cqg = blockIdx.x * 4 + cq;
-  float acc[3][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-  for (int p = rl; p < nchunks; p += 64)
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int k = 0; k < 3; ++k) acc[k][q] += part[((size_t)p * C + 4 * cqg + q) * 3 + k];
-  sum_reduce_block(acc, lds);
-  if (threadIdx.x < 4) {
-    const float Mf = (float)(B * H * W);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int c = 4 * cqg + q;
-      const float k1 = gamma[c] * bnv[3 * C + c], k2 = acc[0][q] / Mf, k3 = acc[1][q] / Mf;
-      if (blockIdx.y == 0) {
-        if (dgamma) dgamma[c] = acc[1][q];
-        if (dbeta) dbeta[c] = acc[0][q];
-        if (dbias) dbias[c] = -k1 * k3 * acc[2][q];
-      }
-      coef[3 * c] = k1;
-      coef[3 * c + 1] = k2;
-      coef[3 * c + 2] = k3;
-    }
-  }
-  __syncthreads();
-  const int units = POOL ? B * (H >> 1) * (W >> 1) : B * H * W;
-  const int u_end = min(units, (int)(blockIdx.y + 1) * upb);
-  float dummy[3][4];
-  for (int u = blockIdx.y * upb + rl; u < u_end; u += 64)
-    bwd_visit<true, POOL>(y, G, B, H, W, C, cqg, u, bnv, bnv + C, bnv + 2 * C, bnv + 3 * C, coef, dz, dummy);
-}
-
 }  // namespace
-
-int cs_bn_bwd_chunks(int B, int H, int W, int C, int pool) {
-  const int units = pool ? B * (H / 2) * (W / 2) : B * H * W;
-  const int want = std::max(1, std::min(64, 4096 / std::max(C, 1)));  // ~256 reduce blocks
-  const int upb = std::max(64, (units + want - 1) / want);
-  return (units + upb - 1) / upb;
-}
-
-hipError_t cs_bn_bwd2(const float* y, const float* G, int B, int H, int W, int C, int pool, const float* bnv,
-                      const float* gamma, float* part, float* dgamma, float* dbeta, float* dbias, float* dz,
-                      hipStream_t stream) {
-  if (C % kFusedCh != 0 || C > 1024 || (pool && ((H | W) & 1))) return hipErrorInvalidValue;
-  const int units = pool ? B * (H / 2) * (W / 2) : B * H * W;
-  const int cg = C / kFusedCh;
-  const int rc = cs_bn_bwd_chunks(B, H, W, C, pool);
-  const int upb_r = (units + rc - 1) / rc;
-  // apply chunks sized for bandwidth: >= 256 units per block, ~512 blocks at most
-  int ra = std::max(1, std::min((units + 255) / 256, std::max(1, 512 / cg)));
-  const int upb_a = (units + ra - 1) / ra;
-  ra = (units + upb_a - 1) / upb_a;
-  if (pool) {
-    hipLaunchKernelGGL((bn_bwd_red_kernel<true>), dim3(cg, rc), dim3(256), 0, stream, y, G, B, H, W, C, bnv, part,
-                       upb_r);
-    hipLaunchKernelGGL((bn_bwd_fapply_kernel<true>), dim3(cg, ra), dim3(256), 0, stream, y, G, B, H, W, C, bnv, gamma,
-                       part, rc, dgamma, dbeta, dbias, dz, upb_a);
-  } else {
-    hipLaunchKernelGGL((bn_bwd_red_kernel<false>), dim3(cg, rc), dim3(256), 0, stream, y, G, B, H, W, C, bnv, part,
-                       upb_r);
-    hipLaunchKernelGGL((bn_bwd_fapply_kernel<false>), dim3(cg, ra), dim3(256), 0, stream, y, G, B, H, W, C, bnv,
-                       gamma, part, rc, dgamma, dbeta, dbias, dz, upb_a);
-  }
-  return hipGetLastError();
-}
 
 int cs_bn_bwd_blocks(int B, int H, int W, int C, int pool) {
   const int units = pool ? B * (H / 2) * (W / 2) : B * H * W;
@@ -630,20 +529,13 @@ int cs_bn_bwd_blocks(int B, int H, int W, int C, int pool) {
   return blocks < 256 ? blocks : 256;
 }
 
-// CS_BN_FIN_WIDE: partial count from which the 8-channel / 1024-thread finalize runs (0 = never)
-static int bn_finalize_wide_min() {
-  static const int v = [] {
-    const char* e = getenv("CS_BN_FIN_WIDE");
-    const int x = e ? atoi(e) : 512;
-    return x > 0 ? x : (1 << 30);
-  }();
-  return v;
-}
+// partial count from which the 8-channel / 1024-thread finalize runs
+constexpr int kFinWideMin = 512;
 
 hipError_t cs_bn_finalize(const float* part, int T, int R, int M, int C, const float* gamma, const float* beta,
                           float* running_mean, float* running_var, int64_t* nbt, float momentum, float eps,
                           float* scale, float* shift, float* save_mean, float* save_invstd, hipStream_t stream) {
-  if (T >= bn_finalize_wide_min() && C % kFinWideC == 0)
+  if (T >= kFinWideMin && C % kFinWideC == 0)
     hipLaunchKernelGGL(bn_finalize_wide_kernel, dim3(C / kFinWideC), dim3(1024), 0, stream, part, T, R, M, C, gamma,
                        beta, running_mean, running_var, nbt, momentum, eps, scale, shift, save_mean, save_invstd);
   else
@@ -709,6 +601,23 @@ hipError_t cs_bn_bwd_tail(const float* y, const float* G, int B, int H, int W, i
     hipLaunchKernelGGL((bn_bwd_kernel<true, false>), dim3(blocks), dim3(256), 0, stream, y, G, B, H, W, C, scale,
                        shift, mean, invstd, coef, dz, nullptr, gslabs, gstride);
   }
+  return hipGetLastError();
+}
+
+hipError_t cs_bn_bwd_apply(const float* y, const float* G, int B, int H, int W, int C, int pool, const float* scale,
+                           const float* shift, const float* mean, const float* invstd, const float* coef, float* dz,
+                           hipStream_t stream) {
+  if (C % 4 != 0 || C > 1024 || (pool && ((H | W) & 1))) return hipErrorInvalidValue;
+  const int rows = 256 / (C / 4);
+  const int units = pool ? B * (H / 2) * (W / 2) : B * H * W;
+  int blocks = (units + rows - 1) / rows;
+  if (blocks > 2048) blocks = 2048;
+  if (pool)
+    hipLaunchKernelGGL((bn_bwd_kernel<true, true>), dim3(blocks), dim3(256), 0, stream, y, G, B, H, W, C, scale, shift,
+                       mean, invstd, coef, dz, nullptr, 1, (int64_t)0);
+  else
+    hipLaunchKernelGGL((bn_bwd_kernel<true, false>), dim3(blocks), dim3(256), 0, stream, y, G, B, H, W, C, scale,
+                       shift, mean, invstd, coef, dz, nullptr, 1, (int64_t)0);
   return hipGetLastError();
 }
 

@@ -6,6 +6,7 @@
 // 32x32 MFMA tiles) per K-group.
 #pragma once
 #include "bn_device.h"
+#include "bn_fin.h"
 #include "common.h"
 #include "launchers.h"
 
@@ -47,139 +48,6 @@ __device__ __forceinline__ void wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
 }
 
-// In-launch split-K combine (cdna_hip_programming.md §5 "In-launch split-K reduction"):
-// every split block has stored its fp32 slab; it publishes it (vmcnt drain, barrier, one
-// agent-scope release) and takes a ticket on the tile's counter. The block that draws the
-// last ticket resets the counter, acquires, and sums the tile's slabs in split order
-// z = 0..S-1 (the same fixed order as the separate reduce kernel: deterministic and
-// independent of which block arrives last), then runs the epilogue: bias + output (+ this
-// tile's BN (mean, M2) over its BM rows for FWD; the OIHW scatter for conv0's wgrad).
-// Saves the reduce launch and the slab round trip for GEMMs whose S * BM * BN slabs are
-// small enough for one block to read (cs_conv_fixup_ok).
-template <int BM, int BN, int MODE>
-__device__ void splitk_fixup(const CsConvArgs& a, int tile, int mt, int nt, int nsplit, float* smem) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  int* flag = reinterpret_cast<int*>(smem);
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const int t = __hip_atomic_fetch_add(a.counters + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = t == nsplit - 1;
-    if (last) {
-      __hip_atomic_store(a.counters + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    flag[0] = last;
-  }
-  __syncthreads();
-  const int last = flag[0];
-  __syncthreads();  // flag is read by every wave before smem is reused below
-  if (!last) return;
-  // the combine runs on the first 256 threads; K-group kernels (KG * 256 threads) keep their
-  // other waves idle here but at every barrier below
-  constexpr int CG = BN / 4, RL = 256 / CG, RPT = BM / RL;
-  const bool act = threadIdx.x < 256;
-  const int cg = threadIdx.x % CG, rl = threadIdx.x / CG;
-  const int m0 = mt * BM, n0 = nt * BN, n = n0 + 4 * cg;
-  const int S = nsplit;
-  const size_t slab = (size_t)a.M * a.N;
-  const bool nok = act && n < a.N;
-  float4 v[RPT];
-#pragma unroll
-  for (int k = 0; k < RPT; ++k) v[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-  const float* base = a.ws + n;
-  int z = 0;
-  for (; z + 4 <= S; z += 4) {  // 4 slabs per trip: RPT * 4 loads in flight, added in z order
-    float4 t[4][RPT];
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-#pragma unroll
-      for (int k = 0; k < RPT; ++k) {
-        const int m = m0 + rl + k * RL;
-        t[u][k] = (m < a.M && nok) ? *reinterpret_cast<const float4*>(base + (size_t)(z + u) * slab + (size_t)m * a.N)
-                                   : make_float4(0.f, 0.f, 0.f, 0.f);
-      }
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-#pragma unroll
-      for (int k = 0; k < RPT; ++k) {
-        v[k].x += t[u][k].x; v[k].y += t[u][k].y; v[k].z += t[u][k].z; v[k].w += t[u][k].w;
-      }
-  }
-  for (; z < S; ++z)
-#pragma unroll
-    for (int k = 0; k < RPT; ++k) {
-      const int m = m0 + rl + k * RL;
-      if (m < a.M && nok) {
-        const float4 t = *reinterpret_cast<const float4*>(base + (size_t)z * slab + (size_t)m * a.N);
-        v[k].x += t.x; v[k].y += t.y; v[k].z += t.z; v[k].w += t.w;
-      }
-    }
-  if constexpr (MODE == CS_CONV_FWD) {
-    if (a.bias != nullptr && nok) {
-      const float4 bv = *reinterpret_cast<const float4*>(a.bias + n);
-#pragma unroll
-      for (int k = 0; k < RPT; ++k) { v[k].x += bv.x; v[k].y += bv.y; v[k].z += bv.z; v[k].w += bv.w; }
-    }
-  }
-  if (MODE == CS_CONV_WGRAD && a.w_oihw) {
-    if (!act) return;  // no barrier below
-#pragma unroll
-    for (int k = 0; k < RPT; ++k) {
-      const int m = m0 + rl + k * RL;
-      const float vals[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
-      if (m < a.M)
-        for (int q = 0; q < 4; ++q) {
-          const int nn = n + q, tap = nn >> 2, ci = nn & 3;
-          if (nn < a.N && ci < 3) a.out[(size_t)m * 27 + ci * 9 + tap] = vals[q];
-        }
-    }
-    return;
-  }
-#pragma unroll
-  for (int k = 0; k < RPT; ++k) {
-    const int m = m0 + rl + k * RL;
-    if (m < a.M && nok) *reinterpret_cast<float4*>(a.out + (size_t)m * a.N + n) = v[k];
-  }
-  if constexpr (MODE == CS_CONV_FWD) {
-    if (a.stats == nullptr) return;
-    // per-column (mean, M2) over the tile's valid rows, two passes through LDS
-    float* red = smem;             // [RL][BN]
-    float* meanv = smem + RL * BN;  // [BN]
-    const int cnt = (a.M - m0) < BM ? (a.M - m0) : BM;
-    float4 cs = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-    for (int k = 0; k < RPT; ++k)
-      if (m0 + rl + k * RL < a.M) { cs.x += v[k].x; cs.y += v[k].y; cs.z += v[k].z; cs.w += v[k].w; }
-    if (act) *reinterpret_cast<float4*>(red + rl * BN + 4 * cg) = cs;
-    __syncthreads();
-    if (threadIdx.x < BN) {
-      float sum = 0.f;
-      for (int q = 0; q < RL; ++q) sum += red[q * BN + threadIdx.x];
-      meanv[threadIdx.x] = sum / (float)cnt;
-    }
-    __syncthreads();
-    const float4 mu = *reinterpret_cast<const float4*>(meanv + 4 * cg);
-    float4 sq = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-    for (int k = 0; k < RPT; ++k)
-      if (m0 + rl + k * RL < a.M) {
-        const float dx = v[k].x - mu.x, dy = v[k].y - mu.y, dz = v[k].z - mu.z, dw = v[k].w - mu.w;
-        sq.x += dx * dx; sq.y += dy * dy; sq.z += dz * dz; sq.w += dw * dw;
-      }
-    if (act) *reinterpret_cast<float4*>(red + rl * BN + 4 * cg) = sq;
-    __syncthreads();
-    if (threadIdx.x < BN && n0 + (int)threadIdx.x < a.N) {
-      float m2 = 0.f;
-      for (int q = 0; q < RL; ++q) m2 += red[q * BN + threadIdx.x];
-      a.stats[((size_t)mt * a.N + n0 + threadIdx.x) * 2 + 0] = meanv[threadIdx.x];
-      a.stats[((size_t)mt * a.N + n0 + threadIdx.x) * 2 + 1] = m2;
-    }
-  }
-}
-
 // DGRAD epilogue with CsConvArgs::ered: this tile's BN-backward partial sums of the block below
 // (bn.hip's reduce pass, per channel: sum g, sum g*xhat, sum xhat over its full-resolution
 // elements) from the output gradient values of K-group 0. The tile goes through LDS first
@@ -210,7 +78,7 @@ template <int BM, int BN, int NT, bool POOL>
 __device__ __noinline__ void dgrad_bn_partials(const float* __restrict__ y, const float* __restrict__ bnv_scale,
                                                const float* __restrict__ bnv_shift, const float* __restrict__ bnv_mean,
                                                const float* __restrict__ bnv_invstd, float* __restrict__ part, int M,
-                                               int N, int lgH, int lgW, int mt, int m0, int n0, float* img) {
+                                               int N, int lgH, int lgW, int mt, int m0, int n0, float* img, bool fin) {
   // thread: channel quad cq (float4 loads of the image, y and the BN vectors), every RG-th row
   constexpr int TP = BN + 4, CQ = BN / 4, RG = NT / CQ, NW = NT / 64;
   static_assert(NT % CQ == 0 && 64 % CQ == 0 && NW * BN * 3 <= BM * TP, "wave partials must fit the tile image");
@@ -248,11 +116,17 @@ __device__ __noinline__ void dgrad_bn_partials(const float* __restrict__ y, cons
       for (int q = 0; q < 4; ++q) img[((tid >> 6) * BN + 4 * cq + q) * 3 + k] = s[k][q];
   __syncthreads();
   if (tid < BN && n0 + tid < N) {
+    float t[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-      float t = 0.f;
-      for (int w = 0; w < NW; ++w) t += img[(w * BN + tid) * 3 + k];
-      part[((size_t)mt * N + n0 + tid) * 3 + k] = t;
+      t[k] = 0.f;
+      for (int w = 0; w < NW; ++w) t[k] += img[(w * BN + tid) * 3 + k];
+    }
+    if (fin) {  // [T][N][4], write-through for the launch's last arriver (bn_fin.h)
+      cs_fin::put_sums(part, N, mt, n0 + tid, t[0], t[1], t[2]);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) part[((size_t)mt * N + n0 + tid) * 3 + k] = t[k];
     }
   }
 }
@@ -316,18 +190,19 @@ __device__ __forceinline__ void conv_epilogue(const CsConvArgs& a, f32x16 (&acc)
           bstore1(ro, acc[i][j][e], (owner && m < a.M && n < a.N) ? (m * a.N + n) * 4 : kOOB);
         }
       }
-    // (K-group kernels: every wave reaches this; the combine runs on the first 256 threads)
-    if (slab && a.counters != nullptr) splitk_fixup<BM, BN, MODE>(a, tile, mt, nt, nsplit, smem);
     if constexpr (MODE == CS_CONV_DGRAD) {
       if (!slab && a.ered.part != nullptr) {  // (split-K: the combine launch takes them)
         dgrad_bn_stage<BM, BN>(acc, owner, smem);
         const CsBnRed& e = a.ered;
+        const bool fin = a.fin.cnt != nullptr;
         if (e.pool)
           dgrad_bn_partials<BM, BN, 256 * KG, true>(e.y, e.scale, e.shift, e.mean, e.invstd, e.part, a.M, a.N, a.lgH,
-                                                    a.lgW, mt, m0, n0, smem);
+                                                    a.lgW, mt, m0, n0, smem, fin);
         else
           dgrad_bn_partials<BM, BN, 256 * KG, false>(e.y, e.scale, e.shift, e.mean, e.invstd, e.part, a.M, a.N, a.lgH,
-                                                     a.lgW, mt, m0, n0, smem);
+                                                     a.lgW, mt, m0, n0, smem, fin);
+        // the last block of the column finalizes the block below's BN backward (coef, dgamma, ...)
+        if (fin) cs_fin::arrive<true, BN>(a.fin, e.part, a.N, mt, nt, n0, smem);
       }
     }
     if (slab || MODE != CS_CONV_FWD) return;
@@ -397,16 +272,24 @@ __device__ __forceinline__ void conv_epilogue(const CsConvArgs& a, f32x16 (&acc)
       if (owner && hh == 0) red[wm * BN + wn * WN + j * 32 + r] = s;
     }
     __syncthreads();
+    const bool fin = a.fin.cnt != nullptr;
     if (owner && wm == 0 && hh == 0) {
 #pragma unroll
       for (int j = 0; j < RN; ++j) {
         const int c = wn * WN + j * 32 + r, n = n0 + c;
         if (n < a.N) {
-          a.stats[((size_t)mt * a.N + n) * 2 + 0] = mean[j];
-          a.stats[((size_t)mt * a.N + n) * 2 + 1] = red[c] + red[BN + c];
+          if (fin) {  // write-through for the launch's last arriver (bn_fin.h)
+            cs_fin::put_stats(a.stats, a.N, mt, n, mean[j], red[c] + red[BN + c]);
+          } else {
+            a.stats[((size_t)mt * a.N + n) * 2 + 0] = mean[j];
+            a.stats[((size_t)mt * a.N + n) * 2 + 1] = red[c] + red[BN + c];
+          }
         }
       }
     }
+    // the last block of the column finalizes the BN forward: scale / shift / mean / invstd,
+    // running stats (the separate bn_finalize launch is gone)
+    if (fin) cs_fin::arrive<false, BN>(a.fin, a.stats, a.N, mt, nt, n0, smem);
   }
 }
 

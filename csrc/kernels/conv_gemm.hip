@@ -565,7 +565,6 @@ __device__ __forceinline__ void kstep_xs(Loader<BM, BN, MODE, BK, C4, false, KG>
 // SCHED 0: the MFMA chain runs one chunk behind its fragment reads; the global loads
 //          go out after the first chunk, the LDS store after the second (sched barriers
 //          pin the phases so hipcc cannot hoist every read ahead of the chain).
-// SCHED 1: same code order, compiler schedules freely.
 template <int BM, int BN, int MODE, int BK, int SCHED, int LS, int SS, bool C4, int KG>
 __device__ __forceinline__ void kstep(Loader<BM, BN, MODE, BK, C4, false, KG>& ld, const CsConvArgs& a,
                                       const float* cur, float* nxt,
@@ -734,29 +733,16 @@ __device__ __forceinline__ void gemm_body(const CsConvArgs& a, const int tile, c
   conv_epilogue<BM, BN, MODE, KG>(a, acc, tile, split, nsplit, smem);
 }
 
-__device__ __forceinline__ void splitk_tail(const CsSplitkTail& k, int blk, float* smem);  // below
-
 template <int BM, int BN, int MODE, int BK, int SCHED, bool C4, int GL, int KG = 1>
 __global__ __launch_bounds__(256 * KG) void conv_gemm_kernel(CsConvArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int ntiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
   // linear grid: ntiles x nsplit GEMM blocks (x fastest, as the old (ntiles, 1, nsplit) grid
-  // dispatched them), then red.P blocks of an independent BN-backward reduce that run in the
-  // GEMM's tail
+  // dispatched them), then sgd.P blocks of an independent SGD update that run in the GEMM's tail
   const int nsplit = (a.total_ksteps + a.ksteps_per_split - 1) / a.ksteps_per_split;
   const int ng = ntiles * nsplit, lin = blockIdx.x;
   if (lin >= ng) {
-    const int e = lin - ng;
-    if (e >= a.red.P + a.sgd.P) {  // (last: a.ktail.P blocks of another GEMM's split-K combine)
-      splitk_tail(a.ktail, e - a.red.P - a.sgd.P, smem);
-      return;
-    }
-    if (e >= a.red.P) {  // (then a.sgd.P blocks of an independent SGD update)
-      cs_sgd::tail_body(a.sgd, e - a.red.P, a.sgd.P);
-      return;
-    }
-    if (a.red.pool) cs_bn::bn_red_body<true>(a.red, e, a.red.P, smem);
-    else cs_bn::bn_red_body<false>(a.red, e, a.red.P, smem);
+    cs_sgd::tail_body(a.sgd, lin - ng, a.sgd.P);
     return;
   }
   gemm_body<BM, BN, MODE, BK, SCHED, C4, GL, KG>(a, cs::xcd_remap(lin % ntiles, ntiles), lin / ntiles, nsplit, smem);
@@ -809,8 +795,13 @@ __global__ __launch_bounds__(256) void splitk_fold_kernel(float* __restrict__ ws
   }
 }
 
+// smem: >= kRedLds floats (the row image, the column means, and bn_fin.h's combine space)
+constexpr int kRedLds = 1024 + 80;
 __device__ __forceinline__ void splitk_reduce_body(const CsConvArgs& a, int mode, int nslab, int zstep, int blk,
-                                                   float (&red)[kRedRows][64], float (&meanv)[64]) {
+                                                   float* smem) {
+  float(&red)[kRedRows][64] = *reinterpret_cast<float(*)[kRedRows][64]>(smem);
+  float* meanv = smem + kRedRows * 64;
+  const bool fin = a.fin.cnt != nullptr;
   const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
   const int ntn = (a.N + 63) / 64;
   const int mt = blk / ntn, nt = blk - mt * ntn;
@@ -853,6 +844,7 @@ __device__ __forceinline__ void splitk_reduce_body(const CsConvArgs& a, int mode
     // BN-backward partials of the block below over this 16-row tile (conv_common.h
     // dgrad_bn_partials): each thread's 4 channels at its row, then the 16 rows in order
     const CsBnRed& e = a.ered;
+    float tot[3] = {0.f, 0.f, 0.f};
     float s[3][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
     if (in) {
       const float4 sc = *reinterpret_cast<const float4*>(e.scale + n), sh = *reinterpret_cast<const float4*>(e.shift + n);
@@ -872,9 +864,15 @@ __device__ __forceinline__ void splitk_reduce_body(const CsConvArgs& a, int mode
       if (threadIdx.x < 64 && n0 + (int)threadIdx.x < a.N) {
         float t = 0.f;
         for (int r = 0; r < kRedRows; ++r) t += red[r][threadIdx.x];
-        e.part[((size_t)mt * a.N + n0 + threadIdx.x) * 3 + k] = t;
+        if (fin) tot[k] = t;
+        else e.part[((size_t)mt * a.N + n0 + threadIdx.x) * 3 + k] = t;
       }
       __syncthreads();
+    }
+    if (fin) {  // [T][N][4] write-through, then the launch's last arriver finalizes (bn_fin.h)
+      if (threadIdx.x < 64 && n0 + (int)threadIdx.x < a.N)
+        cs_fin::put_sums(e.part, a.N, mt, n0 + threadIdx.x, tot[0], tot[1], tot[2]);
+      cs_fin::arrive<true, 64>(a.fin, e.part, a.N, mt, nt, n0, smem);
     }
     return;
   }
@@ -903,39 +901,28 @@ __device__ __forceinline__ void splitk_reduce_body(const CsConvArgs& a, int mode
   if (threadIdx.x < 64 && n0 + (int)threadIdx.x < a.N) {
     float sq = 0.f;
     for (int k = 0; k < kRedRows; ++k) sq += red[k][threadIdx.x];
-    a.stats[((size_t)mt * a.N + n0 + threadIdx.x) * 2 + 0] = meanv[threadIdx.x];
-    a.stats[((size_t)mt * a.N + n0 + threadIdx.x) * 2 + 1] = sq;
+    if (fin) {
+      cs_fin::put_stats(a.stats, a.N, mt, n0 + threadIdx.x, meanv[threadIdx.x], sq);
+    } else {
+      a.stats[((size_t)mt * a.N + n0 + threadIdx.x) * 2 + 0] = meanv[threadIdx.x];
+      a.stats[((size_t)mt * a.N + n0 + threadIdx.x) * 2 + 1] = sq;
+    }
   }
+  if (fin) cs_fin::arrive<false, 64>(a.fin, a.stats, a.N, mt, nt, n0, smem);
 }
 
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(CsConvArgs a, int mode, int nslab, int zstep) {
-  __shared__ float red[kRedRows][64];
-  __shared__ float meanv[64];
-  splitk_reduce_body(a, mode, nslab, zstep, blockIdx.x, red, meanv);
+  __shared__ float smem[kRedLds];
+  splitk_reduce_body(a, mode, nslab, zstep, blockIdx.x, smem);
 }
 
 // both split-K combines of a dual launch in one grid
 __global__ __launch_bounds__(256) void splitk_reduce_dual_kernel(CsConvArgs a1, int mode1, int nslab1, int zstep1,
                                                                  int nb1, CsConvArgs a2, int mode2, int nslab2,
                                                                  int zstep2) {
-  __shared__ float red[kRedRows][64];
-  __shared__ float meanv[64];
-  if ((int)blockIdx.x < nb1) splitk_reduce_body(a1, mode1, nslab1, zstep1, blockIdx.x, red, meanv);
-  else splitk_reduce_body(a2, mode2, nslab2, zstep2, blockIdx.x - nb1, red, meanv);
-}
-
-// blocks appended to a GEMM launch running another GEMM's split-K combine (CsSplitkTail): the
-// same body, tiles and summation order as splitk_reduce_kernel (WGRAD mode: no statistics, no
-// barrier), on the first 256 threads of the block
-__device__ __forceinline__ void splitk_tail(const CsSplitkTail& k, int blk, float* smem) {
-  if (threadIdx.x >= 256) return;
-  CsConvArgs t{};
-  t.ws = const_cast<float*>(k.ws);
-  t.out = k.out;
-  t.M = k.M;
-  t.N = k.N;
-  splitk_reduce_body(t, CS_CONV_WGRAD, k.nslab, 1, blk, *reinterpret_cast<float(*)[kRedRows][64]>(smem),
-                     *reinterpret_cast<float(*)[64]>(smem + kRedRows * 64));
+  __shared__ float smem[kRedLds];
+  if ((int)blockIdx.x < nb1) splitk_reduce_body(a1, mode1, nslab1, zstep1, blockIdx.x, smem);
+  else splitk_reduce_body(a2, mode2, nslab2, zstep2, blockIdx.x - nb1, smem);
 }
 
 int reduce_blocks(const CsConvArgs& a) { return ((a.M + kRedRows - 1) / kRedRows) * ((a.N + 63) / 64); }
@@ -962,23 +949,15 @@ hipError_t launch_reduce(const CsConvArgs& a, int mode, int splits, hipStream_t 
   return hipGetLastError();
 }
 
-int conv_sched() {
-  static int v = [] {
-    const char* e = getenv("CS_CONV_SCHED");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
-
 template <int BM, int BN, int MODE, int BK, int SCHED, bool C4, int GL, int KG = 1>
 hipError_t launch_k(dim3 grid, size_t lds, hipStream_t stream, const CsConvArgs& a) {
-  size_t l = a.red.P > 0 ? std::max(lds, cs_bn_red_lds(a.red.C)) : lds;
+  size_t l = std::max(lds, (size_t)(1024 + 16) * sizeof(float));  // bn_fin.h's combine space
   if (MODE == CS_CONV_DGRAD && a.ered.part != nullptr) l = std::max(l, (size_t)BM * (BN + 4) * sizeof(float));
   hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, MODE, BK, SCHED, C4, GL, KG>), grid, dim3(256 * KG), l, stream, a);
   return hipGetLastError();
 }
 
-// MATH 0: f32 MFMA (register staging honours CS_CONV_SCHED); MATH 2: X6 split-bf16 kernels;
+// MATH 0: f32 MFMA; MATH 2: X6 split-bf16 kernels;
 // MATH 3: X6 split at the LDS store (register staging only)
 template <int BM, int BN, int MODE, int BK, int MATH>
 hipError_t launch_gemm_m(const CsConvArgs& a, int splits, int stage, hipStream_t stream) {
@@ -988,7 +967,7 @@ hipError_t launch_gemm_m(const CsConvArgs& a, int splits, int stage, hipStream_t
   const size_t lds = MATH == 3   ? TileXS<BM, BN, MODE, BK>::BYTES
                      : MATH == 5 ? TileXS<BM, BN, MODE, BK, 1>::BYTES
                                  : 2 * T::STAGE * sizeof(float);
-  const dim3 grid(ntiles * splits + a.red.P + a.sgd.P + a.ktail.P);
+  const dim3 grid(ntiles * splits + a.sgd.P);
   constexpr bool deep_fits = (BM + BN) * BK * 4 * 5 < 160 * 1024;
   if constexpr (BK != 64 && MATH == 0) {
     if (MODE == CS_CONV_FWD && a.w_oihw)  // padded conv0: Cin = 4 < BK
@@ -1021,7 +1000,6 @@ hipError_t launch_gemm_m(const CsConvArgs& a, int splits, int stage, hipStream_t
   } else if constexpr (MATH >= 2) {
     return launch_k<BM, BN, MODE, BK, MATH, false, 0>(grid, lds, stream, a);
   } else {
-    if (conv_sched() == 1) return launch_k<BM, BN, MODE, BK, 1, false, 0>(grid, lds, stream, a);
     return launch_k<BM, BN, MODE, BK, 0, false, 0>(grid, lds, stream, a);
   }
 }
@@ -1040,8 +1018,8 @@ hipError_t launch_gemm(const CsConvArgs& a, int splits, int stage, hipStream_t s
 #define CS_K(BM_, BN_, MODE_, BK_, SCHED_, C4_, GL_) \
   template __global__ void conv_gemm_kernel<BM_, BN_, MODE_, BK_, SCHED_, C4_, GL_>(CsConvArgs);
 #define CS_MODE(BM_, BN_, MODE_)                                            \
-  CS_K(BM_, BN_, MODE_, 16, 0, false, 0) CS_K(BM_, BN_, MODE_, 16, 1, false, 0) \
-  CS_K(BM_, BN_, MODE_, 32, 0, false, 0) CS_K(BM_, BN_, MODE_, 32, 1, false, 0) \
+  CS_K(BM_, BN_, MODE_, 16, 0, false, 0)                                      \
+  CS_K(BM_, BN_, MODE_, 32, 0, false, 0)                                      \
   CS_K(BM_, BN_, MODE_, 32, 0, false, 3)                                      \
   CS_K(BM_, BN_, MODE_, 16, 2, false, 0) CS_K(BM_, BN_, MODE_, 32, 2, false, 0) \
   CS_K(BM_, BN_, MODE_, 32, 2, false, 3)                                      \
@@ -1055,7 +1033,7 @@ CS_TILE(64, 128)
 CS_TILE(128, 64)
 CS_TILE(128, 128)
 #define CS_BK64(BM_, BN_, MODE_) \
-  CS_K(BM_, BN_, MODE_, 64, 0, false, 0) CS_K(BM_, BN_, MODE_, 64, 1, false, 0) CS_K(BM_, BN_, MODE_, 64, 2, false, 0)
+  CS_K(BM_, BN_, MODE_, 64, 0, false, 0) CS_K(BM_, BN_, MODE_, 64, 2, false, 0)
 #define CS_TILE64(BM_, BN_) CS_BK64(BM_, BN_, CS_CONV_FWD) CS_BK64(BM_, BN_, CS_CONV_DGRAD) CS_BK64(BM_, BN_, CS_CONV_WGRAD)
 CS_TILE64(64, 64)
 CS_TILE64(128, 64)
@@ -1189,13 +1167,8 @@ bool cs_conv_stage_ok(int stage, int bm, int bn, int bk, bool conv0_fwd) {
   }
 }
 
-bool cs_conv_fixup_ok(int splits, int bm, int bn) {
-  return splits > 1 && (int64_t)splits * bm * bn * 4 <= CS_FIXUP_MAX_BYTES;
-}
-
-int cs_conv_stat_rows(int K, int bm, int bn, int bk, int splits, bool counters) {
-  const int s = cs_conv_effective_splits(K, bk, splits);
-  return (s == 1 || (counters && cs_conv_fixup_ok(s, bm, bn))) ? bm : CS_SPLITK_STAT_ROWS;
+int cs_conv_stat_rows(int K, int bm, int bk, int splits) {
+  return cs_conv_effective_splits(K, bk, splits) == 1 ? bm : CS_SPLITK_STAT_ROWS;
 }
 
 int cs_conv_ered_rows(int K, int bm, int bk, int splits) {
@@ -1230,10 +1203,9 @@ int prep_gemm(CsConvArgs& a, int mode, int bk, int splits) {
 
 hipError_t cs_conv_gemm_dual(CsConvArgs wg, int wbk, int wsplits, CsConvArgs dg, int dbk, int dsplits,
                              hipStream_t stream, int stage) {
-  if (wg.red.P != 0 || dg.red.P != 0 || wg.sgd.n != 0 || dg.sgd.n != 0 || wg.ktail.M != 0 || dg.ktail.M != 0)
-    return hipErrorInvalidValue;  // no appended work in dual launches
+  if (wg.sgd.n != 0 || dg.sgd.n != 0) return hipErrorInvalidValue;  // no appended work in dual launches
   if (wg.w_oihw) return hipErrorInvalidValue;  // conv0 has no data gradient
-  wg.counters = dg.counters = nullptr;
+  if (wg.fin.cnt != nullptr) return hipErrorInvalidValue;  // (the weight gradient has no BN statistics)
   const int s1 = prep_gemm(wg, CS_CONV_WGRAD, wbk, wsplits), s2 = prep_gemm(dg, CS_CONV_DGRAD, dbk, dsplits);
   if (s1 < 0 || s2 < 0) return hipErrorInvalidValue;
   if (s1 > 1 && s2 > 1 && wg.ws == dg.ws) return hipErrorInvalidValue;  // slabs must not alias
@@ -1288,24 +1260,21 @@ hipError_t cs_conv_gemm(CsConvArgs a, int mode, int bm, int bn, int bk, int spli
   splits = prep_gemm(a, mode, bk, splits);
   if (splits < 0) return hipErrorInvalidValue;
   a.sgd.P = a.sgd.n > 0 ? (int)std::min<int64_t>(256, (a.sgd.n / 4 + 255) / 256) : 0;
-  if (a.ktail.M > 0) {
-    if (a.ktail.ws == nullptr || a.ktail.out == nullptr || a.ktail.N % 4 || a.ktail.nslab < 1 ||
-        a.ktail.nslab > 2 * kFold)
+  if (a.fin.cnt != nullptr) {  // last-arriver BN finalize: its statistics must exist in this launch pair
+    if (mode == CS_CONV_WGRAD || (mode == CS_CONV_FWD && a.stats == nullptr) ||
+        (mode == CS_CONV_DGRAD && a.ered.part == nullptr))
       return hipErrorInvalidValue;
-    a.ktail.P = ((a.ktail.M + kRedRows - 1) / kRedRows) * ((a.ktail.N + 63) / 64);
-  } else {
-    a.ktail.P = 0;
+    const int R = cs_conv_stat_rows(a.K, bm, bk, splits), nc = splits > 1 ? 64 : bn;
+    if (a.fin.R != R || a.fin.M != a.M || a.fin.T != (a.M + R - 1) / R || a.fin.grp == nullptr) return hipErrorInvalidValue;
+    (void)nc;
   }
-  // (BN-backward partials from a split-K data gradient come out of the combine launch)
-  if (!cs_conv_fixup_ok(splits, bm, bn) || a.ered.part != nullptr) a.counters = nullptr;
 #define CS_DISPATCH(BM_, BN_, BK_)                                                                       \
   if (bm == BM_ && bn == BN_ && bk == BK_) {                                                             \
     hipError_t e;                                                                                        \
     if (mode == CS_CONV_FWD) e = launch_gemm<BM_, BN_, CS_CONV_FWD, BK_>(a, splits, stage, stream);     \
     else if (mode == CS_CONV_DGRAD) e = launch_gemm<BM_, BN_, CS_CONV_DGRAD, BK_>(a, splits, stage, stream); \
     else e = launch_gemm<BM_, BN_, CS_CONV_WGRAD, BK_>(a, splits, stage, stream);                       \
-    if (e != hipSuccess || splits == 1 || a.counters != nullptr) return e;                               \
-    if (a.keep_slabs && splits <= 2 * kFold && a.ered.part == nullptr) return e; /* consumer sums slabs */ \
+    if (e != hipSuccess || splits == 1) return e;                                                        \
     return launch_reduce(a, mode, splits, stream);                                                       \
   }
   CS_DISPATCH(64, 64, 16)

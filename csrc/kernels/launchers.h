@@ -31,19 +31,6 @@ hipError_t cs_rows_mean(float* src, int rows, int64_t n, float* dst, int bcast, 
 hipError_t cs_accumulate(float* g, const float* t, int64_t n, float div, hipStream_t stream);
 // bf16 gradient transport: to_bf16 = 1: fp32 src -> bf16 dst (round to nearest even); 0: bf16 -> fp32
 hipError_t cs_cast_grad(const void* src, void* dst, int64_t n, int to_bf16, hipStream_t stream);
-// SGD whose gradient for some ranges still sits in split-K slabs (weight gradients whose
-// combine launch was skipped): range k = [off[k], off[k] + len[k]) of the flat buffers has its
-// gradient in slab[k][z * stride[k] + i - off[k]], z < ns[k], summed in z order (bit-equal to
-// the combine launch) and written to g before the update. Offsets / lengths multiples of 4.
-constexpr int kCsSgdSlabsMax = 16;
-struct CsSgdSlabs {
-  int n;
-  int64_t off[kCsSgdSlabsMax], len[kCsSgdSlabsMax], stride[kCsSgdSlabsMax];
-  const float* slab[kCsSgdSlabsMax];
-  int ns[kCsSgdSlabsMax];
-};
-hipError_t cs_sgd_flat_slabs(float* p, float* g, float* m, int64_t n, float lr, float mom, float wd, float damp,
-                             float scale, int first, hipStream_t stream, int64_t* counter, const CsSgdSlabs& slabs);
 hipError_t cs_sgd_multi(const CsTensorEntry* tab_dev, int ntens, const int64_t* chunk_start_dev, int nchunks,
                         float lr, float mom, float wd, float damp, float scale, int first, hipStream_t stream);
 
@@ -79,14 +66,27 @@ struct CsSgdTail {
   int first, P;
 };
 
-// The deterministic split-K combine of ANOTHER (weight-gradient, standard-layout) GEMM carried
-// by blocks appended to a launch: out[M][N] = sum over nslab slabs of ws (z order, bit-equal to
-// the combine launch); P blocks (the launcher sizes it when M > 0).
-struct CsSplitkTail {
-  const float* ws;
-  float* out;
-  int M, N, nslab, P;
+// BatchNorm finalize by the last-arriving block of the launch that produces the statistics
+// partials (bn_fin.h): FWD with CsConvArgs::stats (scale / shift / mean / invstd -> bnv [4][C],
+// running stats, num_batches_tracked), BWD with CsConvArgs::ered (coef [C][3], dgamma, dbeta,
+// dbias; ered.part is then [T][C][4]). cnt == null: off (the separate finalize launch runs).
+struct CsBnFin {
+  int* cnt;    // zeroed ticket counters, >= cs_bn_fin_ints(...) ints (left zeroed by the launch)
+  float* grp;  // level-1 group partials, >= cs_bn_fin_grp_floats(...) floats
+  int T, R, M;  // row tiles of the partials, rows per tile, rows (the last tile may be short)
+  int count;    // BWD: elements per channel of the BN layer (full resolution) for the means
+  const float *gamma, *beta, *invstd;  // invstd: BWD (the forward's)
+  float *rmean, *rvar;                 // FWD running stats (may be null)
+  int64_t* nbt;                        // FWD (may be null)
+  float momentum, eps;
+  float* bnv;                          // FWD out [4][C]
+  float *coef, *dgamma, *dbeta, *dbias;  // BWD out (dgamma / dbeta / dbias may be null)
 };
+// tickets and group-partial floats a launch needs for T row tiles of C channels in column
+// tiles of nc channels (64 or 128)
+inline int cs_bn_fin_groups(int T, int nc) { return (T + 8 * (256 / nc) - 1) / (8 * (256 / nc)); }
+inline int cs_bn_fin_ints(int T, int C, int nc) { return ((C + nc - 1) / nc) * (cs_bn_fin_groups(T, nc) + 1); }
+inline int64_t cs_bn_fin_grp_floats(int T, int C, int nc) { return (int64_t)cs_bn_fin_groups(T, nc) * C * 4; }
 
 struct CsConvArgs {
   const float* x;     // FWD / WGRAD: conv input, NHWC [B,H,W,Cin] (Cin = 4 for the padded conv0 input)
@@ -96,13 +96,8 @@ struct CsConvArgs {
   float* out;         // FWD: y [M][Cout]; DGRAD: dx [M][Cin]; WGRAD: dW (OHWI, or OIHW for conv0)
   float* ws;          // split-K slabs [splits][M][N] (required when splits > 1)
   float* stats;       // FWD: per-row-tile BN partials [tiles][Cout][2] = (mean, M2); may be null
-  int* counters;      // split-K tile tickets (zeroed, >= #tiles ints) for the in-launch combine; null = reduce kernel
   int B, H, W, Cin, Cout;
   int w_oihw;
-  int keep_slabs;  // split-K: leave the <= 32 fp32 slabs in ws for the consumer to sum (no reduce launch)
-  // extra blocks after the GEMM tiles (dispatched last, they fill the GEMM's tail): an
-  // independent BN-backward reduce (the block below's), red.P blocks; red.P == 0: none
-  CsBnRed red;
   // DGRAD: the BN-backward partial sums of the block below (whose output gradient this GEMM
   // produces), taken from the finished output values where they are still in registers — the
   // GEMM epilogue, or the split-K combine — instead of a separate reduce pass over G and y.
@@ -112,14 +107,9 @@ struct CsConvArgs {
   // an independent SGD update appended to the launch (the serial world-1 step: block l+1's
   // parameters, whose last reader has run, ride block l's weight-gradient GEMM)
   CsSgdTail sgd;
-  // the split-K combine of block l's weight gradient riding block l's data-gradient launch (the
-  // serial step: the two GEMMs are independent)
-  CsSplitkTail ktail;
-  // pre-split operands (conv_xp.hip): P3 bf16 chunks [n/8][3][8] (h, m, l of every 8 elements)
-  const uint16_t* x3;   // FWD / WGRAD: split conv input
-  const uint16_t* w3;   // FWD / DGRAD: split OHWI weights
-  const uint16_t* dz3;  // DGRAD / WGRAD: split output gradient
-  int64_t x3s, w3s, dz3s;  // element counts n (informational; the kernels derive the extents)
+  // FWD (with stats) / DGRAD (with ered): the BN finalize by the launch's last-arriving block
+  // (or the split-K combine's); fin.cnt == null: off
+  CsBnFin fin;
   // filled by the launcher:
   int lgH, lgW, lgCin, lgCout, M, N, K, ksteps_per_split, total_ksteps;
 };
@@ -163,25 +153,11 @@ inline bool cs_conv_dual_ok(int wstage, int wbk, int dstage, int dbk) {
 hipError_t cs_conv_splitk_reduce(const CsConvArgs& a, int mode, int splits, hipStream_t stream);
 // the split count cs_conv_gemm actually launches (K-steps re-balanced over splits)
 int cs_conv_effective_splits(int K, int bk, int splits);
-// split-K slabs of one tile a single block combines in-launch (S * BM * BN * 4 bytes)
-#define CS_FIXUP_MAX_BYTES (256 << 10)
-bool cs_conv_fixup_ok(int splits, int bm, int bn);
 // FWD statistics tile height for a launch (bm, or CS_SPLITK_STAT_ROWS behind the reduce kernel)
-int cs_conv_stat_rows(int K, int bm, int bn, int bk, int splits, bool counters);
+int cs_conv_stat_rows(int K, int bm, int bk, int splits);
 // rows per BN-backward partial of a DGRAD launch carrying `ered` (bm, or CS_SPLITK_STAT_ROWS
-// when split-K: the combine launch computes them; such launches never use the in-launch combine
-// or kept slabs)
+// when split-K: the combine launch computes them)
 int cs_conv_ered_rows(int K, int bm, int bk, int splits);
-
-// pre-split ("XP") conv GEMMs (conv_xp.hip): operands as three bf16 planes (x = h + m + l),
-// fp32-accurate six-product split-bf16 MFMA maths, LDS-DMA ring staging. bm, bn in {64, 128},
-// bk in {32, 64}, kg K-groups of 4 waves in {1, 2}, nb LDS ring stages (0 = as many as fit one
-// block per CU; 2-3 on some bk-32 tiles so two blocks share a CU) — cs_conv_xp_ok; layers with
-// Cin, Cout >= 64.
-bool cs_conv_xp_ok(int bm, int bn, int bk, int kg, int nb = 0);
-hipError_t cs_conv_xp(CsConvArgs a, int mode, int bm, int bn, int bk, int splits, int kg, int nb, hipStream_t stream);
-// fp32 x[n] (n % 8 == 0) -> P3 bf16 chunks out[n/8][3][8] (h, m, l)
-hipError_t cs_split3(const float* x, uint16_t* out, int64_t n, hipStream_t stream);
 
 // ---------------------------------------------------------------- BatchNorm + ReLU (+ 2x2 max-pool), NHWC
 hipError_t cs_bn_finalize(const float* part, int T, int R, int M, int C, const float* gamma, const float* beta,
@@ -204,35 +180,6 @@ hipError_t cs_bn_bwd_tail(const float* y, const float* G, int B, int H, int W, i
                           const float* part, int P, float* coef, float* dgamma, float* dbeta, float* dbias, float* dz,
                           hipStream_t stream, int gslabs = 1, int64_t gstride = 0,
                           unsigned long long* signal = nullptr);
-// One-launch BN (bn_grid.hip): P <= 256 blocks (all resident) whose phases meet at in-kernel grid
-// barriers — backward: partials | per-channel finalize | dZ apply (replaces cs_bn_bwd's three
-// launches, same partials bit for bit); forward: finalize from the conv epilogue's tile partials |
-// normalize/ReLU/pool (replaces cs_bn_finalize + cs_bn_apply). bar: kCsBnGridBarInts zeroed device
-// ints the kernels leave zeroed (one set per stream and direction); err: device word set
-// on a barrier timeout; signal: optional stream-link counter bumped when the launch starts.
-struct CsBnGridBwd {
-  const float *y, *G, *scale, *shift, *mean, *invstd, *gamma;
-  float *part, *coef, *dgamma, *dbeta, *dbias, *dz;
-  int64_t gstride;
-  int B, H, W, C, pool, gslabs;
-  unsigned* bar;
-  int* err;
-  unsigned long long* signal;
-};
-struct CsBnGridFwd {
-  const float *part, *gamma, *beta, *y;
-  float *running_mean, *running_var, *bnv, *out;  // bnv [4][C]: scale, shift, mean, invstd
-  int64_t* nbt;
-  float momentum, eps;
-  int T, R, M, B, H, W, C, pool;
-  unsigned* bar;
-  int* err;
-  unsigned long long* signal;
-};
-constexpr int kCsBnGridBarInts = 640;  // 2 barriers x (8 group lines + top line) + exit counter
-hipError_t cs_bn_grid_bwd(const CsBnGridBwd& a, hipStream_t stream);
-hipError_t cs_bn_grid_fwd(const CsBnGridFwd& a, hipStream_t stream);
-int cs_bn_grid_fwd_blocks(int B, int H, int W, int C, int pool);
 // G may be split-K slabs of the data-gradient GEMM: G = sum_{z < gslabs} G[z * gstride + i]
 // (summed in z order, bit-equal to the split-K combine launch it replaces)
 hipError_t cs_bn_bwd(const float* y, const float* G, int B, int H, int W, int C, int pool, const float* scale,
@@ -250,12 +197,11 @@ hipError_t cs_bn_fused_bwd(const float* y, const float* G, int B, int H, int W, 
                            const float* gamma, float* coef, float* dgamma, float* dbeta, float* dbias, float* dz,
                            hipStream_t stream, int gslabs = 1, int64_t gstride = 0,
                            unsigned long long* signal = nullptr);
-// two-launch backward for larger layers (C % 16 == 0): channel-sliced chunk partials, then
-// finalize folded into the apply; part: [cs_bn_bwd_chunks][C][3] scratch
-int cs_bn_bwd_chunks(int B, int H, int W, int C, int pool);
-hipError_t cs_bn_bwd2(const float* y, const float* G, int B, int H, int W, int C, int pool, const float* bnv,
-                      const float* gamma, float* part, float* dgamma, float* dbeta, float* dbias, float* dz,
-                      hipStream_t stream);
+// the BN backward's apply pass alone (dZ from G, y and the finalized coef [C][3]): the finalize
+// ran as the last-arriver tail of the data-gradient launch that produced G (CsConvArgs::fin)
+hipError_t cs_bn_bwd_apply(const float* y, const float* G, int B, int H, int W, int C, int pool, const float* scale,
+                           const float* shift, const float* mean, const float* invstd, const float* coef, float* dz,
+                           hipStream_t stream);
 
 // ---------------------------------------------------------------- ordering-probe communicator (comm_probe.hip)
 enum { CS_SCRAMBLE_F32 = 0, CS_SCRAMBLE_I64 = 1, CS_SCRAMBLE_I32 = 2 };

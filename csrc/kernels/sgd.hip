@@ -51,62 +51,6 @@ __global__ __launch_bounds__(256) void sgd_flat_kernel(float* __restrict__ p, co
   }
 }
 
-// The flat pass with the split-K combine of some weight gradients folded in (CsSgdSlabs): a
-// float4 of such a range sums its slabs in z order (the combine launch's order: bit-equal),
-// stores the gradient (the grads buffer stays the step's gradient) and updates. Saves each
-// kept wgrad a combine launch and one write + read of its gradient.
-__global__ __launch_bounds__(256) void sgd_slabs_kernel(float* __restrict__ p, float* __restrict__ g,
-                                                        float* __restrict__ m, int64_t n, SgdArgs a,
-                                                        int64_t* __restrict__ counter, CsSgdSlabs sl) {
-  if (counter != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *counter += 1;
-  const int64_t n4 = n >> 2;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  float4* p4 = reinterpret_cast<float4*>(p);
-  float4* g4 = reinterpret_cast<float4*>(g);
-  float4* m4 = reinterpret_cast<float4*>(m);
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
-    const int64_t e = i << 2;
-    int k = -1;
-    for (int q = 0; q < sl.n; ++q)
-      if (e >= sl.off[q] && e < sl.off[q] + sl.len[q]) k = q;
-    float4 gv;
-    if (k < 0) {
-      gv = g4[i];
-    } else {
-      const float* s0 = sl.slab[k] + (e - sl.off[k]);
-      const int64_t st = sl.stride[k];
-      const int nz = sl.ns[k];
-      gv = make_float4(0.f, 0.f, 0.f, 0.f);
-      for (int z0 = 0; z0 < nz; z0 += 8) {  // 8 slab loads in flight, added in z order
-        float4 t[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          t[j] = z0 + j < nz ? *reinterpret_cast<const float4*>(s0 + (int64_t)(z0 + j) * st) : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if (z0 + j < nz) {
-            gv.x += t[j].x; gv.y += t[j].y; gv.z += t[j].z; gv.w += t[j].w;
-          }
-      }
-      g4[i] = gv;
-    }
-    float4 pv = p4[i];
-    float4 mv = a.first ? make_float4(0.f, 0.f, 0.f, 0.f) : m4[i];
-    sgd1(pv.x, gv.x, mv.x, a);
-    sgd1(pv.y, gv.y, mv.y, a);
-    sgd1(pv.z, gv.z, mv.z, a);
-    sgd1(pv.w, gv.w, mv.w, a);
-    p4[i] = pv;
-    if (a.mom != 0.f) m4[i] = mv;
-  }
-  for (int64_t i = (n4 << 2) + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    float pv = p[i], mv = a.first ? 0.f : m[i];  // (slab ranges are float4-aligned: never here)
-    sgd1(pv, g[i], mv, a);
-    p[i] = pv;
-    if (a.mom != 0.f) m[i] = mv;
-  }
-}
-
 // Multi-tensor form: table of {p, g, m, n}; each block walks chunks of 4096 elements.
 __global__ __launch_bounds__(256) void sgd_multi_kernel(const CsTensorEntry* __restrict__ tab, int ntens,
                                                         const int64_t* __restrict__ chunk_start, int nchunks,
@@ -144,22 +88,6 @@ hipError_t cs_sgd_flat(float* p, const float* g, float* m, int64_t n, float lr, 
   int blocks = (int)((work + 255) / 256);
   if (blocks > 2048) blocks = 2048;
   hipLaunchKernelGGL(sgd_flat_kernel, dim3(blocks), dim3(256), 0, stream, p, g, m, n, a, counter);
-  return hipGetLastError();
-}
-
-hipError_t cs_sgd_flat_slabs(float* p, float* g, float* m, int64_t n, float lr, float mom, float wd, float damp,
-                             float scale, int first, hipStream_t stream, int64_t* counter, const CsSgdSlabs& slabs) {
-  if (n <= 0) return hipSuccess;
-  if (slabs.n < 0 || slabs.n > kCsSgdSlabsMax) return hipErrorInvalidValue;
-  for (int k = 0; k < slabs.n; ++k)
-    if (slabs.off[k] % 4 || slabs.len[k] % 4 || slabs.stride[k] % 4 || slabs.off[k] < 0 ||
-        slabs.off[k] + slabs.len[k] > n || slabs.ns[k] < 1 || slabs.slab[k] == nullptr)
-      return hipErrorInvalidValue;
-  SgdArgs a{lr, mom, wd, damp, scale, first};
-  const int64_t work = (n + 3) / 4;
-  int blocks = (int)((work + 255) / 256);
-  if (blocks > 2048) blocks = 2048;
-  hipLaunchKernelGGL(sgd_slabs_kernel, dim3(blocks), dim3(256), 0, stream, p, g, m, n, a, counter, slabs);
   return hipGetLastError();
 }
 

@@ -52,16 +52,12 @@ class DeviceComm {
 // whether `s` is being captured into a graph (links fall back to events there)
 bool stream_capturing(hipStream_t s);
 
-// The engine's side stream (weight gradients + their SGD), created once per process and bound to
-// a hardware queue on creation (one tiny fill runs on it). Measured on MI355X: when the side
-// stream is created after other streams have already taken the process's hardware queues
-// (GPU_MAX_HW_QUEUES), it shares a queue and every side/main link handoff stalls — the VGG-11
-// step went from 0.72 to 2.8 ms with 8-40 busy streams created first (at 8, 16 or 32 queues), and
-// stayed at 0.72 ms when those streams came after it. reserve_streams() creates it now: call it
-// before anything else creates streams (NativeTrainer and bench.py do).
-// reserved_comm_stream(): the same for RcclComm's (high-priority) stream, whose fork/join links
-// stall the same way when it shares a queue.
-hipStream_t reserved_side_stream();
+// RcclComm's (high-priority) comm stream, created once per process and bound to a hardware
+// queue on creation (one tiny fill runs on it). Measured on MI355X (round 2): a stream created
+// after other streams have taken the process's hardware queues (GPU_MAX_HW_QUEUES) shares a
+// queue, and every fork/join link handoff with it stalls (a 0.72 ms VGG-11 step went to 2.8 ms
+// with 8-40 busy streams created first). reserve_streams() creates it now: call it before
+// anything else creates streams (NativeTrainer and bench.py do).
 hipStream_t reserved_comm_stream();
 void reserve_streams();
 
@@ -85,11 +81,6 @@ class StreamLink {
   StreamLink(const StreamLink&) = delete;
   StreamLink& operator=(const StreamLink&) = delete;
   void signal(hipStream_t producer);
-  // signal folded into the NEXT kernel launched on the producer stream: returns the counter that
-  // kernel must bump (once, at its start: it starts only after everything before it on that
-  // stream completed and released — the same edge as a signal launch, without the launch).
-  // nullptr when the link runs on events (CS_LINK_EVENTS): then call signal() instead.
-  unsigned long long* defer();
   void wait(hipStream_t consumer);
   std::string error() const;
 
@@ -97,7 +88,6 @@ class StreamLink {
   unsigned long long* dev_ = nullptr;  // [count, expect]
   int* err_ = nullptr;                 // host-mapped error word: 1 timeout, 2 aborted
   unsigned long long pending_ = 0;     // signals issued since the last wait
-  hipEvent_t ev_ = nullptr;            // CS_LINK_EVENTS=1 (diagnostic): the same link through an event
 };
 
 // The fork / join machinery every communicator shares (CS_COMM_FORK selects it):

@@ -24,17 +24,9 @@ std::string RcclComm::unique_id() {
 }
 
 namespace {
-// fork/join events only order two streams of this device: no system-scope fence needed
-// (CS_COMM_EVENT_FLAGS: 0 timing-free default events, 1 + hipEventDisableSystemFence,
-// 2 + hipEventReleaseToDevice)
-unsigned comm_event_flags() {
-  unsigned flags = hipEventDisableTiming;
-  int mode = 1;
-  if (const char* e = getenv("CS_COMM_EVENT_FLAGS")) mode = atoi(e);
-  if (mode == 1) flags |= hipEventDisableSystemFence;
-  if (mode == 2) flags |= hipEventReleaseToDevice;
-  return flags;
-}
+// fork/join events only order two streams of this device: no system-scope fence needed (round 1
+// measured the three flag variants within 2 %: 72.3k / 73.7k / 72.4k img/s)
+unsigned comm_event_flags() { return hipEventDisableTiming | hipEventDisableSystemFence; }
 }  // namespace
 
 RcclComm::RcclComm(const std::string& uid, int rank, int world, int device, bool high_priority, int max_ctas)

@@ -128,7 +128,10 @@ void StagedComm::abort() {
 
 // ------------------------------------------------------------------------------ ProbeComm
 
-ProbeComm::ProbeComm(int device, double spin_us) : spin_us_(spin_us) { make_stream(device, &stream_); }
+ProbeComm::ProbeComm(int device, double spin_us, double gbps, int world)
+    : spin_us_(spin_us), gbps_(gbps), model_world_(world < 2 ? 2 : world) {
+  make_stream(device, &stream_);
+}
 
 ProbeComm::~ProbeComm() {
   if (stream_) hipStreamSynchronize(stream_);
@@ -157,6 +160,12 @@ void ProbeComm::all_reduce(void* buf, size_t count, ncclDataType_t dt, ncclRedOp
   ++calls_;
   fault_point("all_reduce", 0);
   if (do_fork) bridge_.fork(compute, stream_);
+  if (gbps_ > 0.0) {  // xGMI ring model: 1e3 B/us per GB/s
+    const double bytes = (double)count * (dt == ncclInt64 || dt == ncclFloat64 ? 8 : 4);
+    const double w = (double)model_world_;
+    hip_ok(cs_comm_spin(spin_us_ + 2.0 * (w - 1.0) / w * bytes / (gbps_ * 1e3), stream_), "model spin");
+    return;
+  }
   scramble(buf, count, dt);
 }
 
@@ -164,6 +173,11 @@ void ProbeComm::broadcast(void* buf, size_t count, ncclDataType_t dt, int, hipSt
   ++calls_;
   fault_point("broadcast", 0);
   if (do_fork) bridge_.fork(compute, stream_);
+  if (gbps_ > 0.0) {
+    const double bytes = (double)count * (dt == ncclInt64 || dt == ncclFloat64 ? 8 : 4);
+    hip_ok(cs_comm_spin(spin_us_ + bytes / (gbps_ * 1e3), stream_), "model spin");
+    return;
+  }
   scramble(buf, count, dt);
 }
 

@@ -67,7 +67,10 @@ class StagedComm final : public DeviceComm {
 // read a scrambled or stale buffer — either shows up as a mismatch.
 class ProbeComm final : public DeviceComm {
  public:
-  ProbeComm(int device, double spin_us);
+  // gbps > 0: the xGMI model — no scramble; every all-reduce is a spin of spin_us + the ring time
+  // 2 (W-1)/W * bytes / gbps of a W-GPU ring, every broadcast spin_us + bytes / gbps, so the step
+  // runs its fork / collective / comm-stream SGD / join schedule with modelled collective durations
+  ProbeComm(int device, double spin_us, double gbps = 0.0, int world = 8);
   ~ProbeComm() override;
   ProbeComm(const ProbeComm&) = delete;
   ProbeComm& operator=(const ProbeComm&) = delete;
@@ -86,7 +89,8 @@ class ProbeComm final : public DeviceComm {
   void scramble(void* buf, size_t count, ncclDataType_t dt);
   hipStream_t stream_ = nullptr;
   StreamBridge bridge_;
-  double spin_us_ = 0.0;
+  double spin_us_ = 0.0, gbps_ = 0.0;
+  int model_world_ = 8;
   int64_t calls_ = 0;
 };
 

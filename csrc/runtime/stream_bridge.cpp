@@ -48,39 +48,22 @@ StreamLink::StreamLink() {
   hip_ok(hipHostMalloc(&h, sizeof(int), hipHostMallocMapped), "hipHostMalloc(link error word)");
   err_ = static_cast<int*>(h);
   *err_ = 0;
-  if (const char* e = getenv("CS_LINK_EVENTS"))
-    if (atoi(e) != 0) hip_ok(hipEventCreateWithFlags(&ev_, hipEventDisableTiming), "event");
   hip_ok(hipDeviceSynchronize(), "sync");
 }
 
 StreamLink::~StreamLink() {
   if (dev_) hipFree(dev_);
   if (err_) hipHostFree(err_);
-  if (ev_) hipEventDestroy(ev_);
 }
 
 void StreamLink::signal(hipStream_t producer) {
-  if (ev_) {
-    hip_ok(hipEventRecord(ev_, producer), "link event record");
-  } else {
-    hip_ok(cs_link_signal(dev_, producer), "link signal");
-  }
+  hip_ok(cs_link_signal(dev_, producer), "link signal");
   ++pending_;
-}
-
-unsigned long long* StreamLink::defer() {
-  if (ev_) return nullptr;
-  ++pending_;
-  return dev_;
 }
 
 void StreamLink::wait(hipStream_t consumer) {
   if (pending_ == 0) return;  // nothing signalled since the last wait
-  if (ev_) {
-    hip_ok(hipStreamWaitEvent(consumer, ev_, 0), "link event wait");
-  } else {
-    hip_ok(cs_link_wait(dev_, dev_ + 1, err_, abort_word(), g_link_timeout, consumer, pending_), "link wait");
-  }
+  hip_ok(cs_link_wait(dev_, dev_ + 1, err_, abort_word(), g_link_timeout, consumer, pending_), "link wait");
   pending_ = 0;
 }
 
@@ -94,40 +77,13 @@ std::string StreamLink::error() const {
 }
 
 namespace {
-// CS_SIDE_CU_SHARE = m (opt-in, default 0): the side stream may only use (m-1)/m of the CUs — one
-// block of 8 consecutive CU-mask bits in every 8*m is left out, which is the same share of
-// every XCD whether the driver numbers CUs XCD by XCD or interleaved (m = 4: 64 of 256 CUs).
-// Why: a side-stream weight-gradient GEMM fills every CU it lands on (1024 threads x 128
-// VGPRs, or 512 x 256: the whole register file), so a main-stream kernel of the critical chain
-// (the BN backward, the next data gradient) waits for side blocks to drain before it can
-// start at all. Reserved CUs keep the critical chain moving. 0 or 1: no mask.
-int side_cu_share() {
-  static const int m = [] {
-    const char* e = getenv("CS_SIDE_CU_SHARE");
-    return e ? atoi(e) : 0;
-  }();
-  return m;
-}
-
 // a non-blocking stream at the lowest (or highest) priority, bound to a hardware queue by one
-// tiny fill (queues are taken when a stream first runs work); masked: on a CU subset
-// (side_cu_share) at the default priority (a CU-masked stream takes no priority)
-hipStream_t bound_stream(bool high, bool masked = false) {
+// tiny fill (queues are taken when a stream first runs work)
+hipStream_t bound_stream(bool high) {
   int least = 0, greatest = 0;
   hip_ok(hipDeviceGetStreamPriorityRange(&least, &greatest), "stream priorities");
   hipStream_t s = nullptr;
-  const int m = masked ? side_cu_share() : 0;
-  if (m > 1) {
-    int dev = 0, cus = 0;
-    hip_ok(hipGetDevice(&dev), "device");
-    hip_ok(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev), "CU count");
-    std::vector<uint32_t> mask((cus + 31) / 32, 0u);
-    for (int i = 0; i < cus; ++i)
-      if ((i / 8) % m != m - 1) mask[i / 32] |= 1u << (i % 32);
-    hip_ok(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()), "CU-masked side stream");
-  } else {
-    hip_ok(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, high ? greatest : least), "reserved stream");
-  }
+  hip_ok(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, high ? greatest : least), "reserved stream");
   void* scratch = nullptr;
   hip_ok(hipMalloc(&scratch, 256), "reserved stream scratch");
   hip_ok(hipMemsetAsync(scratch, 0, 256, s), "bind reserved stream");
@@ -137,20 +93,12 @@ hipStream_t bound_stream(bool high, bool masked = false) {
 }
 }  // namespace
 
-hipStream_t reserved_side_stream() {
-  static hipStream_t side = bound_stream(false, true);
-  return side;
-}
-
 hipStream_t reserved_comm_stream() {
   static hipStream_t comm = bound_stream(true);
   return comm;
 }
 
-void reserve_streams() {
-  (void)reserved_side_stream();
-  (void)reserved_comm_stream();
-}
+void reserve_streams() { (void)reserved_comm_stream(); }
 
 bool stream_capturing(hipStream_t s) {
   hipStreamCaptureStatus st = hipStreamCaptureStatusNone;

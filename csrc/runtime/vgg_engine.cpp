@@ -97,7 +97,7 @@ VggEngine::VggEngine(int64_t Bmax, std::vector<int64_t> desc, std::vector<int64_
   TORCH_CHECK(nbt_.is_cuda() && nbt_.scalar_type() == at::kLong && nbt_.numel() == L, "VggEngine: nbt int64 [L]");
   const auto fo = params_.options();
   const int64_t P = params_.numel();
-  int64_t gmax = 0, dzmax = 0, partmax = 0, cmax = 0;
+  int64_t gmax = 0, dzmax = 0, partmax = 0, cmax = 0, fin_ints = 0, grpmax = 4;
   blocks_.resize(L);
   for (int64_t l = 0; l < L; ++l) {
     VggBlock& b = blocks_[l];
@@ -135,9 +135,19 @@ VggEngine::VggEngine(int64_t Bmax, std::vector<int64_t> desc, std::vector<int64_
     gmax = std::max(gmax, Bmax * ho * ho * b.cout);
     dzmax = std::max(dzmax, pix * b.cout);
     partmax = std::max<int64_t>(partmax, (int64_t)cs_bn_bwd_blocks(Bmax, b.H, b.H, b.cout, b.pool) * b.cout * 3);
-    partmax = std::max<int64_t>(partmax, (int64_t)cs_bn_bwd_chunks(Bmax, b.H, b.H, b.cout, b.pool) * b.cout * 3);
-    // row-tile partials of block l-1 out of block l's data gradient (>= CS_SPLITK_STAT_ROWS rows each)
-    if (l > 0) partmax = std::max<int64_t>(partmax, cdiv(pix, CS_SPLITK_STAT_ROWS) * b.cin * 3);
+    // in-launch finalize state, sized for the finest partials (16-row tiles, 64-wide column tiles):
+    // forward over this block's statistics, backward over block l-1's (carried by this dgrad)
+    const int64_t tf = cdiv(pix, CS_SPLITK_STAT_ROWS);
+    b.fin_fwd = fin_ints;
+    fin_ints += cs_bn_fin_ints((int)tf, b.cout, 64);
+    grpmax = std::max<int64_t>(grpmax, cs_bn_fin_grp_floats((int)tf, b.cout, 64));
+    if (l > 0) {
+      // block l-1's BN-backward partials out of block l's data gradient: [row tiles][cin][4]
+      partmax = std::max<int64_t>(partmax, tf * b.cin * 4);
+      b.fin_bwd = fin_ints;
+      fin_ints += cs_bn_fin_ints((int)tf, b.cin, 64);
+      grpmax = std::max<int64_t>(grpmax, cs_bn_fin_grp_floats((int)tf, b.cin, 64));
+    }
     cmax = std::max<int64_t>(cmax, b.cout);
     for (int m = 0; m < 3; ++m) b.tile[m] = default_tile(b, m, Bmax);
   }
@@ -160,25 +170,11 @@ VggEngine::VggEngine(int64_t Bmax, std::vector<int64_t> desc, std::vector<int64_
   dz_[1] = torch::zeros({dzmax}, fo);
   ws_elems_ = kWsElems;
   ws_ = torch::zeros({ws_elems_}, fo);
-  ws_side_ = torch::zeros({ws_elems_}, fo);
-  side_ = reserved_side_stream();  // process-wide, created early (device_comm.h)
-  dz_link_ = std::make_unique<StreamLink>();
-  wg_link_ = std::make_unique<StreamLink>();
-  ok(hipStreamCreateWithFlags(&opt_, hipStreamNonBlocking), "optimizer stream");
-  ev_opt_.resize(64);
-  for (auto& e : ev_opt_) ok(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event");
-  if (const char* e = getenv("CS_SGD_OVERLAP")) sgd_overlap_ = atoi(e) != 0;
-  if (const char* e = getenv("CS_OVERLAP_WGRAD")) set_overlap_wgrad(atoi(e) != 0);
-  if (const char* e = getenv("CS_WGRAD_AFTER_DGRAD")) wgrad_after_dgrad_ = atoi(e) != 0;
-  // split-K tile tickets for the in-launch combine: one zeroed region per (block, mode) call site
-  tiles_max_ = 1;
-  for (int64_t l = 0; l < L; ++l)
-    for (int m = 0; m < 3; ++m) {
-      const Dims d = dims(blocks_[l], m, Bmax);
-      tiles_max_ = std::max(tiles_max_, cdiv(d.M, 64) * cdiv(d.N, 64));
-    }
-  counters_ = torch::zeros({3 * L * tiles_max_}, fo.dtype(at::kInt));
-  // per-block parameter ranges for the side-stream SGD: the backward-ready layout puts fc first,
+  ws_w_ = torch::zeros({ws_elems_}, fo);
+  // zeroed once; every in-launch finalize leaves its tickets zeroed (bn_fin.h)
+  fin_cnt_ = torch::zeros({std::max<int64_t>(fin_ints, 1)}, fo.dtype(at::kInt));
+  fin_grp_ = torch::zeros({grpmax}, fo);
+  // per-block parameter ranges for the per-block SGD: the backward-ready layout puts fc first,
   // then blocks L-1..0, each {w, bias, gamma, beta} inside [w_off, next block's w_off)
   {
     bool contiguous = fc_w_ + ncls * feat <= blocks_[L - 1].w_off && fc_b_ + ncls <= blocks_[L - 1].w_off;
@@ -194,78 +190,14 @@ VggEngine::VggEngine(int64_t Bmax, std::vector<int64_t> desc, std::vector<int64_
     }
     if (!contiguous) blk_range_.clear();
   }
-  if (const char* e = getenv("CS_SGD_SIDE")) sgd_side_ = atoi(e) != 0;
-  if (const char* e = getenv("CS_CONV_FIXUP")) fixup_ = atoi(e) != 0;
   if (const char* e = getenv("CS_CONV_DUAL")) dual_ = atoi(e) != 0;
   if (const char* e = getenv("CS_BN_FUSED_ROWS")) bn_fused_rows_ = atoll(e);
   if (const char* e = getenv("CS_CONV_MATH")) math_ = atoi(e);
-  if (const char* e = getenv("CS_BN_PATH")) bn_path_ = atoi(e);
-  if (const char* e = getenv("CS_DEFER_SIGNALS")) defer_signals_ = atoi(e) != 0;
-  if (const char* e = getenv("CS_KEEP_SLABS")) keep_slabs_ = atoi(e) != 0;
-  if (const char* e = getenv("CS_FUSE_BN_RED")) fuse_red_ = atoi(e) != 0;
-  if (const char* e = getenv("CS_BN_EPI_RED")) epi_red_ = atoi(e) != 0;
-  if (const char* e = getenv("CS_SGD_SLABS")) sgd_slabs_on_ = atoi(e) != 0;
-  if (const char* e = getenv("CS_SGD_TAIL")) sgd_tail_on_ = atoi(e) != 0;
-  if (const char* e = getenv("CS_KTAIL")) ktail_on_ = atoi(e) != 0;
-  grid_bar_ = torch::zeros({2 * kCsBnGridBarInts}, fo.dtype(at::kInt));  // backward set, forward set
-  {
-    void* h = nullptr;
-    ok(hipHostMalloc(&h, sizeof(int), hipHostMallocMapped), "hipHostMalloc(grid error word)");
-    grid_err_ = static_cast<int*>(h);
-    *grid_err_ = 0;
-  }
   bn_part_ = torch::zeros({partmax}, fo);
   bn_coef_ = torch::zeros({cmax * 3}, fo);
   bn_eval_ = torch::zeros({2, cmax}, fo);
   TORCH_CHECK(feat % 4 == 0, "VggEngine: feature size must be a multiple of 4");
   head_ws_ = torch::zeros({cs_linear_xent_ws((int)Bmax, (int)ncls)}, fo);
-}
-
-bool VggEngine::side_wgrad(hipStream_t s) const { return overlap_wgrad_ && !stream_capturing(s); }
-
-// The link wait orders `s` after the side stream's weight gradients for kernels on this device:
-// each side-stream kernel ends with the device-scope release the next kernel's acquire pairs
-// with. A host-side reader is not covered: gloo copies a CUDA tensor to the host on its own
-// stream, ordered after `s` only, and without a system-scope release on the producing stream a
-// weight gradient can still sit in an L2 the copy does not see (measured round 2: a stale
-// layers.25.weight gradient at world 2, with a link or a plain event join alike; only a host
-// sync of the side stream avoided it). sys_join_ adds an event recorded with
-// hipEventReleaseToSystem on the side stream, which `s` (and so the copy behind it) waits on.
-void VggEngine::join_side(hipStream_t s) {
-  flush_signal(s);  // the side stream may be waiting for it: never wait on side before it is out
-  wg_link_->wait(s);
-  if (sys_join_) {
-    ok(hipEventRecord(sys_ev_, side_), "sys-join event record");
-    ok(hipStreamWaitEvent(s, sys_ev_, 0), "sys-join event wait");
-  }
-}
-
-void VggEngine::set_sys_join(bool on) {
-  if (on && sys_ev_ == nullptr)
-    ok(hipEventCreateWithFlags(&sys_ev_, hipEventDisableTiming | hipEventReleaseToSystem), "sys-join event");
-  sys_join_ = on;
-}
-
-std::string VggEngine::link_error() const {
-  std::string e = dz_link_->error();
-  if (e.empty()) e = wg_link_->error();
-  if (e.empty() && grid_err_ != nullptr && __atomic_load_n(grid_err_, __ATOMIC_ACQUIRE) != 0)
-    e = "BN grid barrier timed out (a block of the one-launch BN kernel never arrived)";
-  return e;
-}
-
-void VggEngine::flush_signal(hipStream_t s) {
-  if (pending_sig_ == nullptr) return;
-  ok(cs_link_signal(pending_sig_, s), "link signal");
-  pending_sig_ = nullptr;
-}
-
-void VggEngine::set_overlap_wgrad(bool on) {
-  overlap_wgrad_ = on;
-  if (on && dz_blk_.empty()) {
-    const auto fo = params_.options();
-    for (const VggBlock& b : blocks_) dz_blk_.push_back(torch::zeros({Bmax_ * b.H * b.H * b.cout}, fo));
-  }
 }
 
 torch::Tensor VggEngine::tensor(int64_t block, const std::string& name) const {
@@ -308,7 +240,6 @@ CsConvArgs VggEngine::conv_args(int l, int mode, int B, bool with_stats, float* 
   a.Cout = b.cout;
   a.w_oihw = (l == 0 && b.cin == 4) ? 1 : 0;
   a.ws = ws != nullptr ? ws : ws_.data_ptr<float>();
-  a.counters = fixup_ ? counters_.data_ptr<int>() + (3 * l + mode) * tiles_max_ : nullptr;
   if (dz == nullptr) dz = dz_[0].data_ptr<float>();
   if (mode == CS_CONV_FWD) {
     a.x = b.x.data_ptr<float>();
@@ -329,34 +260,16 @@ CsConvArgs VggEngine::conv_args(int l, int mode, int B, bool with_stats, float* 
   return a;
 }
 
-void VggEngine::set_perm(torch::Tensor perm) {
-  TORCH_CHECK(data_[0].defined(), "set_perm: set_data(0, ...) first");
-  TORCH_CHECK(perm.scalar_type() == at::kLong && perm.dim() == 1 && perm.numel() > 0, "set_perm: int64 [n] indices");
-  const int64_t n = perm.numel();
-  TORCH_CHECK(n <= data_[0].size(0) + Bmax_, "set_perm: permutation longer than the dataset");
-  if (!perm_.defined()) {
-    // fixed capacity (graph-captured kernels keep the pointer): dataset size + one batch of slack
-    perm_ = torch::zeros({data_[0].size(0) + Bmax_}, params_.options().dtype(at::kLong));
-    cursor_ = torch::zeros({1}, params_.options().dtype(at::kLong));
-  }
-  perm_.narrow(0, 0, n).copy_(perm.to(perm_.device()), /*non_blocking=*/false);
-  cursor_.zero_();
-  perm_len_ = n;
-}
-
 void VggEngine::conv(int l, int mode, int B, const ConvTile& t, hipStream_t s, bool with_stats, float* ws,
-                     float* dz, bool keep_slabs, const CsBnRed* red, const CsBnRed* ered, const CsSgdTail* sgd,
-                     const CsSplitkTail* ktail) {
+                     float* dz, const CsBnRed* ered, const CsSgdTail* sgd, const CsBnFin* fin) {
   VggBlock& b = blocks_[l];
   CsConvArgs a = conv_args(l, mode, B, with_stats, ws, dz);
-  a.keep_slabs = keep_slabs ? 1 : 0;
-  if (red != nullptr) a.red = *red;
   if (ered != nullptr) {
-    TORCH_CHECK(mode == CS_CONV_DGRAD && !keep_slabs, "VggEngine: BN partials ride a data gradient without kept slabs");
+    TORCH_CHECK(mode == CS_CONV_DGRAD, "VggEngine: BN partials ride a data gradient");
     a.ered = *ered;
   }
   if (sgd != nullptr) a.sgd = *sgd;
-  if (ktail != nullptr) a.ktail = *ktail;
+  if (fin != nullptr) a.fin = *fin;
   const Dims d = dims(b, mode, B);
   const int sp = eff_splits(d.K, t.splits, t.bk);
   TORCH_CHECK(sp == 1 || (int64_t)sp * d.M * d.N <= ws_elems_, "VggEngine: split-K workspace too small");
@@ -375,19 +288,20 @@ bool VggEngine::dual_ok(int l) const {
   return w.bm == 64 && w.bn == 64 && d.bm == 64 && d.bn == 64 && cs_conv_dual_ok(w.stage, w.bk, d.stage, d.bk);
 }
 
-void VggEngine::conv_dual(int l, int B, hipStream_t s, float* dz, const CsBnRed* ered) {
+void VggEngine::conv_dual(int l, int B, hipStream_t s, float* dz, const CsBnRed* ered, const CsBnFin* fin) {
   const ConvTile& w = blocks_[l].tile[CS_CONV_WGRAD];
   const ConvTile& d = blocks_[l].tile[CS_CONV_DGRAD];
-  CsConvArgs wa = conv_args(l, CS_CONV_WGRAD, B, false, ws_side_.data_ptr<float>(), dz);
+  CsConvArgs wa = conv_args(l, CS_CONV_WGRAD, B, false, ws_w_.data_ptr<float>(), dz);
   CsConvArgs da = conv_args(l, CS_CONV_DGRAD, B, false, nullptr, dz);
   if (ered != nullptr) da.ered = *ered;
+  if (fin != nullptr) da.fin = *fin;
   ok(cs_conv_gemm_dual(wa, w.bk, w.splits, da, d.bk, d.splits, s, w.stage), "conv_gemm_dual");
 }
 
 CsSgdTail VggEngine::sgd_tail_args(int64_t block) {
   CsSgdTail t{};
   const int64_t off = blk_range_[block].first, n = blk_range_[block].second;
-  if (n <= 0 || off % 4 != 0) return t;  // float4 rows (otherwise the final pass takes it)
+  if (n <= 0 || off % 4 != 0) return t;  // float4 rows (otherwise a launch of its own takes it)
   t.p = P(off);
   t.g = G(off);
   t.m = mom_.data_ptr<float>() + off;
@@ -400,11 +314,7 @@ CsSgdTail VggEngine::sgd_tail_args(int64_t block) {
   return t;
 }
 
-bool VggEngine::epi_red_ok(int l, int64_t B) const {
-  return epi_red_ && bn_path_ == 0 && !fixup_ && !keep_slabs_ && l > 0 && !bn_fused(l - 1, B);
-}
-
-CsBnRed VggEngine::epi_red_args(int l, int B) {
+CsBnRed VggEngine::ered_args(int l, int B) {
   VggBlock& c = blocks_[l - 1];
   float* cb = c.bn.data_ptr<float>();
   CsBnRed r{};
@@ -423,8 +333,51 @@ CsBnRed VggEngine::epi_red_args(int l, int B) {
   const ConvTile& t = blocks_[l].tile[CS_CONV_DGRAD];
   const Dims d = dims(blocks_[l], CS_CONV_DGRAD, B);
   r.P = (int)cdiv(d.M, cs_conv_ered_rows((int)d.K, t.bm, t.bk, t.splits));
-  TORCH_CHECK((int64_t)r.P * c.cout * 3 <= bn_part_.numel(), "VggEngine: BN partial buffer");
+  TORCH_CHECK((int64_t)r.P * c.cout * 4 <= bn_part_.numel(), "VggEngine: BN partial buffer");
   return r;
+}
+
+CsBnFin VggEngine::fin_fwd_args(int l, int B) {
+  VggBlock& b = blocks_[l];
+  const ConvTile& t = b.tile[CS_CONV_FWD];
+  const Dims d = dims(b, CS_CONV_FWD, B);
+  const int R = cs_conv_stat_rows((int)d.K, t.bm, t.bk, t.splits);
+  CsBnFin f{};
+  f.cnt = fin_cnt_.data_ptr<int>() + b.fin_fwd;
+  f.grp = fin_grp_.data_ptr<float>();
+  f.R = R;
+  f.M = (int)d.M;
+  f.T = (int)cdiv(d.M, R);
+  f.gamma = P(b.g_off);
+  f.beta = P(b.be_off);
+  f.rmean = bufs_.data_ptr<float>() + b.rm_off;
+  f.rvar = bufs_.data_ptr<float>() + b.rv_off;
+  f.nbt = nbt_.data_ptr<int64_t>() + l;
+  f.momentum = kBnMomentum;
+  f.eps = kBnEps;
+  f.bnv = b.bn.data_ptr<float>();
+  return f;
+}
+
+CsBnFin VggEngine::fin_bwd_args(int l, int B) {
+  VggBlock& c = blocks_[l - 1];
+  const ConvTile& t = blocks_[l].tile[CS_CONV_DGRAD];
+  const Dims d = dims(blocks_[l], CS_CONV_DGRAD, B);
+  const int R = cs_conv_ered_rows((int)d.K, t.bm, t.bk, t.splits);
+  CsBnFin f{};
+  f.cnt = fin_cnt_.data_ptr<int>() + blocks_[l].fin_bwd;
+  f.grp = fin_grp_.data_ptr<float>();
+  f.R = R;
+  f.M = (int)d.M;
+  f.T = (int)cdiv(d.M, R);
+  f.count = B * c.H * c.H;
+  f.gamma = P(c.g_off);
+  f.invstd = c.bn.data_ptr<float>() + 3 * c.cout;
+  f.coef = bn_coef_.data_ptr<float>();
+  f.dgamma = G(c.g_off);
+  f.dbeta = G(c.be_off);
+  f.dbias = G(c.b_off);
+  return f;
 }
 
 void VggEngine::forward_train(int64_t B) {
@@ -432,9 +385,7 @@ void VggEngine::forward_train(int64_t B) {
   TORCH_CHECK(data_[0].defined(), "forward_train: set_data(0, ...) first");
   hipStream_t s = cur_stream();
   const int L = (int)blocks_.size();
-  g_slabs_ = 1;  // the head writes the top block's gradient to gbuf_
   red_pending_ = -1;
-  flush_signal(s);
   // one launch: sampler index (device cursor into the epoch permutation, or idx_ when no
   // permutation is set), label gather, crop/flip/normalize into block 0's NHWC input
   const bool use_perm = perm_len_ > 0;
@@ -444,61 +395,25 @@ void VggEngine::forward_train(int64_t B) {
                    blocks_[0].x.data_ptr<float>(), idx_.data_ptr<int64_t>(), ylab_.data_ptr<int64_t>(), (int)B, kMean,
                    kStd, s),
      "make_batch");
-  // CS_PROBE_EXTRA_LAUNCHES=k (measurement only): k redundant tiny launches per step, to price
-  // one kernel boundary inside the replayed graph (measured: ~1.5 us each on MI355X)
-  static const int extra = [] {
-    const char* e = getenv("CS_PROBE_EXTRA_LAUNCHES");
-    return e ? atoi(e) : 0;
-  }();
-  for (int i = 0; i < extra; ++i)
-    ok(cs_gather_labels(labels_[0].data_ptr<int64_t>(), idx_.data_ptr<int64_t>(), ylab_.data_ptr<int64_t>(), (int)B,
-                        s),
-       "probe");
+  float* bufs = bufs_.data_ptr<float>();
   for (int l = 0; l < L; ++l) {
     VggBlock& b = blocks_[l];
     const ConvTile& t = b.tile[CS_CONV_FWD];
-    conv(l, CS_CONV_FWD, (int)B, t, s, true);
-    const int64_t M = B * b.H * b.H;
-    const int rows = cs_conv_stat_rows(9 * b.cin, t.bm, t.bn, t.bk, t.splits, fixup_);
     float* bn = b.bn.data_ptr<float>();
-    float* bufs = bufs_.data_ptr<float>();
     float* out = (l + 1 < L) ? blocks_[l + 1].x.data_ptr<float>() : gbuf_[1].data_ptr<float>();
-    if (bn_fused(l, B) || bn_path_ == 1) {  // finalize + normalize/ReLU/pool in one launch
-      ok(cs_bn_fused_fwd(b.stats.data_ptr<float>(), (int)cdiv(M, rows), rows, (int)M, b.cout, P(b.g_off),
-                         P(b.be_off), bufs + b.rm_off, bufs + b.rv_off, nbt_.data_ptr<int64_t>() + l, kBnMomentum,
-                         kBnEps, bn, b.y.data_ptr<float>(), out, (int)B, b.H, b.H, b.pool, s),
-         "bn_fused_fwd");
-      continue;
+    if (fin_on_) {
+      // conv [+ split-K combine]: its last-arriving block finalizes the batch statistics
+      const CsBnFin f = fin_fwd_args(l, (int)B);
+      conv(l, CS_CONV_FWD, (int)B, t, s, true, nullptr, nullptr, nullptr, nullptr, &f);
+    } else {
+      conv(l, CS_CONV_FWD, (int)B, t, s, true);
+      const int64_t M = B * b.H * b.H;
+      const int rows = cs_conv_stat_rows(9 * b.cin, t.bm, t.bk, t.splits);
+      ok(cs_bn_finalize(b.stats.data_ptr<float>(), (int)cdiv(M, rows), rows, (int)M, b.cout, P(b.g_off),
+                        P(b.be_off), bufs + b.rm_off, bufs + b.rv_off, nbt_.data_ptr<int64_t>() + l, kBnMomentum,
+                        kBnEps, bn, bn + b.cout, bn + 2 * b.cout, bn + 3 * b.cout, s),
+         "bn_finalize");
     }
-    if (bn_path_ == 2) {  // finalize + normalize/ReLU/pool in one grid-barrier launch
-      CsBnGridFwd g{};
-      g.part = b.stats.data_ptr<float>();
-      g.gamma = P(b.g_off);
-      g.beta = P(b.be_off);
-      g.y = b.y.data_ptr<float>();
-      g.running_mean = bufs + b.rm_off;
-      g.running_var = bufs + b.rv_off;
-      g.bnv = bn;
-      g.out = out;
-      g.nbt = nbt_.data_ptr<int64_t>() + l;
-      g.momentum = kBnMomentum;
-      g.eps = kBnEps;
-      g.T = (int)cdiv(M, rows);
-      g.R = rows;
-      g.M = (int)M;
-      g.B = (int)B;
-      g.H = g.W = b.H;
-      g.C = b.cout;
-      g.pool = b.pool;
-      g.bar = reinterpret_cast<unsigned*>(grid_bar_.data_ptr<int>()) + kCsBnGridBarInts;
-      g.err = grid_err_;
-      ok(cs_bn_grid_fwd(g, s), "bn_grid_fwd");
-      continue;
-    }
-    ok(cs_bn_finalize(b.stats.data_ptr<float>(), (int)cdiv(M, rows), rows, (int)M, b.cout, P(b.g_off), P(b.be_off),
-                      bufs + b.rm_off, bufs + b.rv_off, nbt_.data_ptr<int64_t>() + l, kBnMomentum, kBnEps, bn,
-                      bn + b.cout, bn + 2 * b.cout, bn + 3 * b.cout, s),
-       "bn_finalize");
     ok(cs_bn_apply(b.y.data_ptr<float>(), bn, bn + b.cout, out, (int)B, b.H, b.H, b.cout, b.pool, s), "bn_apply");
   }
   // features of the last block were staged in gbuf_[1] (free until the first dgrad); dfeat -> gbuf_[0]
@@ -508,225 +423,71 @@ void VggEngine::forward_train(int64_t B) {
      "linear_xent");
 }
 
-void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
+void VggEngine::backward(int64_t hi, int64_t lo, int64_t B) {
   const int L = (int)blocks_.size();
   TORCH_CHECK(0 <= lo && lo <= hi && hi < L, "backward: need 0 <= lo <= hi < num_blocks");
   TORCH_CHECK(B > 0 && B <= Bmax_, "backward: 0 < B <= Bmax");
   hipStream_t s = cur_stream();
-  // side-stream weight gradients, except while a graph is captured (the side stream would not
-  // join the capture; the serial order computes the same bits)
-  const bool ovl = side_wgrad(s);
   for (int l = (int)hi; l >= (int)lo; --l) {
     VggBlock& b = blocks_[l];
     float* bn = b.bn.data_ptr<float>();
-    // with the side-stream weight gradients every block has its own dz buffer (no WAR wait
-    // on a wgrad that may still be reading it)
-    float* dz = ovl ? dz_blk_[l].data_ptr<float>() : dz_[l & 1].data_ptr<float>();
-    // this block's output gradient: gbuf_, or the split-K slabs the dgrad above left in ws_
-    const int gs = g_slabs_;
-    const float* Gin = gs > 1 ? ws_.data_ptr<float>() : gbuf_[(L - 1 - l) % 2].data_ptr<float>();
-    TORCH_CHECK(gs == 1 || bn_path_ != 1, "VggEngine: kept split-K slabs need the grid or three-launch BN path");
-    if (red_pending_ != l && !bn_fused(l, B) && bn_path_ == 2) {  // reduce + finalize + apply: one launch
-      CsBnGridBwd g{};
-      g.y = b.y.data_ptr<float>();
-      g.G = Gin;
-      g.scale = bn;
-      g.shift = bn + b.cout;
-      g.mean = bn + 2 * b.cout;
-      g.invstd = bn + 3 * b.cout;
-      g.gamma = P(b.g_off);
-      g.part = bn_part_.data_ptr<float>();
-      g.coef = bn_coef_.data_ptr<float>();
-      g.dgamma = G(b.g_off);
-      g.dbeta = G(b.be_off);
-      g.dbias = G(b.b_off);
-      g.dz = dz;
-      g.gstride = g_stride_;
-      g.B = (int)B;
-      g.H = g.W = b.H;
-      g.C = b.cout;
-      g.pool = b.pool;
-      g.gslabs = gs;
-      g.bar = reinterpret_cast<unsigned*>(grid_bar_.data_ptr<int>());
-      g.err = grid_err_;
-      g.signal = pending_sig_;  // the previous block's dz-link signal rides this launch
-      pending_sig_ = nullptr;
-      ok(cs_bn_grid_bwd(g, s), "bn_grid_bwd");
-    } else if (red_pending_ == l) {
-      // the partial sums already ran: in block l+1's data-gradient GEMM (epilogue / split-K
-      // combine) or inside the weight-gradient launch above; the pending signal rides the finalize
-      ok(cs_bn_bwd_tail(b.y.data_ptr<float>(), Gin, (int)B, b.H, b.H, b.cout, b.pool, bn, bn + b.cout,
-                        bn + 2 * b.cout, bn + 3 * b.cout, P(b.g_off), bn_part_.data_ptr<float>(), red_P_,
-                        bn_coef_.data_ptr<float>(), G(b.g_off), G(b.be_off), G(b.b_off), dz, s, gs, g_stride_,
-                        pending_sig_),
-         "bn_bwd_tail");
-      pending_sig_ = nullptr;
-    } else if (bn_fused(l, B)) {  // reduce + finalize + apply in one launch
+    float* dz = dz_[l & 1].data_ptr<float>();
+    const float* Gin = gbuf_[(L - 1 - l) % 2].data_ptr<float>();
+    // ---- BN (+ReLU, +pool) backward of block l -> dz
+    if (red_pending_ == l) {
+      // the partial sums (and, with fin, the finalize) ran inside block l+1's data-gradient launch
+      if (fin_on_)
+        ok(cs_bn_bwd_apply(b.y.data_ptr<float>(), Gin, (int)B, b.H, b.H, b.cout, b.pool, bn, bn + b.cout,
+                           bn + 2 * b.cout, bn + 3 * b.cout, bn_coef_.data_ptr<float>(), dz, s),
+           "bn_bwd_apply");
+      else
+        ok(cs_bn_bwd_tail(b.y.data_ptr<float>(), Gin, (int)B, b.H, b.H, b.cout, b.pool, bn, bn + b.cout,
+                          bn + 2 * b.cout, bn + 3 * b.cout, P(b.g_off), bn_part_.data_ptr<float>(), red_P_,
+                          bn_coef_.data_ptr<float>(), G(b.g_off), G(b.be_off), G(b.b_off), dz, s),
+           "bn_bwd_tail");
+    } else if (bn_fused(l, B)) {  // reduce + finalize + apply in one launch (the top block)
       ok(cs_bn_fused_bwd(b.y.data_ptr<float>(), Gin, (int)B, b.H, b.H, b.cout, b.pool, bn, P(b.g_off),
-                         bn_coef_.data_ptr<float>(), G(b.g_off), G(b.be_off), G(b.b_off), dz, s, gs, g_stride_,
-                         pending_sig_),
+                         bn_coef_.data_ptr<float>(), G(b.g_off), G(b.be_off), G(b.b_off), dz, s),
          "bn_fused_bwd");
-      pending_sig_ = nullptr;
-    } else if (bn_path_ == 1) {  // chunk partials, then finalize folded into the apply: two launches
-      flush_signal(s);
-      ok(cs_bn_bwd2(b.y.data_ptr<float>(), gbuf_[(L - 1 - l) % 2].data_ptr<float>(), (int)B, b.H, b.H, b.cout, b.pool,
-                    bn, P(b.g_off), bn_part_.data_ptr<float>(), G(b.g_off), G(b.be_off), G(b.b_off), dz, s),
-         "bn_bwd2");
     } else {
-      flush_signal(s);
       ok(cs_bn_bwd(b.y.data_ptr<float>(), Gin, (int)B, b.H, b.H, b.cout, b.pool, bn, bn + b.cout,
                    bn + 2 * b.cout, bn + 3 * b.cout, P(b.g_off), bn_part_.data_ptr<float>(),
-                   bn_coef_.data_ptr<float>(), G(b.g_off), G(b.be_off), G(b.b_off), dz, s, gs, g_stride_),
+                   bn_coef_.data_ptr<float>(), G(b.g_off), G(b.be_off), G(b.b_off), dz, s),
          "bn_bwd");
     }
-    g_slabs_ = 1;
     red_pending_ = -1;
-    // block l-1's BN partials out of this block's data gradient (no reduce launch of their own)
-    const bool er = epi_red_ok(l, B);
+    // ---- weight and data gradients of block l; block l-1's BN-backward partials (and their
+    // finalize) ride the data gradient
+    const bool er = l > 0;
     CsBnRed erv{};
-    if (er) erv = epi_red_args(l, (int)B);
-    if (!ovl && dual_ok(l)) {  // wgrad + dgrad in one launch
-      if (sgd_tail_ && l + 1 < (int)blocks_.size()) sgd_on(s, blk_range_[l + 1].first, blk_range_[l + 1].second, false);
-      conv_dual(l, (int)B, s, dz, er ? &erv : nullptr);
-      if (er) {
-        red_pending_ = l - 1;
-        red_P_ = erv.P;
-      }
-      continue;
+    CsBnFin fin{};
+    if (er) {
+      erv = ered_args(l, (int)B);
+      if (fin_on_) fin = fin_bwd_args(l, (int)B);
     }
-    if (!er && fuse_red_ && !ovl && bn_path_ == 0 && l > 0 && !bn_fused(l - 1, B)) {
-      // dgrad(l) first, then wgrad(l) carrying block l-1's BN partial-sum pass
-      const ConvTile& t = b.tile[CS_CONV_DGRAD];
-      const Dims d = dims(b, CS_CONV_DGRAD, B);
-      const int sp = eff_splits(d.K, t.splits, t.bk);
-      const bool keep = keep_slabs_ && sp > 1 && sp <= 32;
-      conv(l, CS_CONV_DGRAD, (int)B, t, s, false, nullptr, dz, keep);
-      if (keep) {
-        g_slabs_ = sp;
-        g_stride_ = d.M * d.N;
-      }
-      VggBlock& c = blocks_[l - 1];
-      float* cb = c.bn.data_ptr<float>();
-      CsBnRed r{};
-      r.y = c.y.data_ptr<float>();
-      r.G = g_slabs_ > 1 ? ws_.data_ptr<float>() : gbuf_[(L - l) % 2].data_ptr<float>();
-      r.scale = cb;
-      r.shift = cb + c.cout;
-      r.mean = cb + 2 * c.cout;
-      r.invstd = cb + 3 * c.cout;
-      r.part = bn_part_.data_ptr<float>();
-      r.gstride = g_stride_;
-      r.B = (int)B;
-      r.H = r.W = (int)c.H;
-      r.C = (int)c.cout;
-      r.pool = c.pool;
-      r.P = cs_bn_bwd_blocks((int)B, (int)c.H, (int)c.H, (int)c.cout, c.pool);
-      r.gslabs = g_slabs_;
-      if (sgd_tail_ && l + 1 < (int)blocks_.size()) sgd_on(s, blk_range_[l + 1].first, blk_range_[l + 1].second, false);
-      conv(l, CS_CONV_WGRAD, (int)B, b.tile[CS_CONV_WGRAD], s, false, ws_side_.data_ptr<float>(), dz, false, &r);
-      red_pending_ = l - 1;
-      red_P_ = r.P;
-      continue;
-    }
-    if (ovl && !wgrad_after_dgrad_) {
-      // the weight gradient leaves the critical chain: it runs on the (low-priority) side
-      // stream once dz(l) exists, beside this block's dgrad and the BN backward below
-      dz_link_->signal(s);
-      dz_link_->wait(side_);
-      conv(l, CS_CONV_WGRAD, (int)B, b.tile[CS_CONV_WGRAD], side_, false, ws_side_.data_ptr<float>(), dz);
-      wg_link_->signal(side_);
-    } else if (!ovl) {
-      // block l+1's SGD rides this launch (its BN backward and data gradient ran before it)
+    const CsBnFin* fp = er && fin_on_ ? &fin : nullptr;
+    if (dual_ok(l)) {  // wgrad + dgrad in one launch (no appended SGD blocks: the update runs first)
+      if (sgd_tail_ && l + 1 < L) sgd_on(s, blk_range_[l + 1].first, blk_range_[l + 1].second, false);
+      conv_dual(l, (int)B, s, dz, &erv, fp);
+    } else {
+      // block l+1's SGD rides this weight-gradient launch (its BN backward and data gradient ran)
       CsSgdTail tail{};
-      if (sgd_tail_ && l + 1 < (int)blocks_.size()) {
+      if (sgd_tail_ && l + 1 < L) {
         tail = sgd_tail_args(l + 1);
         if (tail.n == 0) sgd_on(s, blk_range_[l + 1].first, blk_range_[l + 1].second, false);
       }
-      const CsSgdTail* tp = tail.n > 0 ? &tail : nullptr;
-      const ConvTile& tw = b.tile[CS_CONV_WGRAD];
-      const Dims dw = dims(b, CS_CONV_WGRAD, B);
-      const int spw = eff_splits(dw.K, tw.splits, tw.bk);
-      const int64_t slab = dw.M * dw.N;
-      if (keep_wg_ && l > 0 && spw > 1 && spw <= 32 && sgd_slabs_.n < kCsSgdSlabsMax &&
-          keep_used_ + spw * slab <= keep_ws_.numel()) {
-        // slabs stay for the step's SGD launch to sum (no combine launch)
-        float* w = keep_ws_.data_ptr<float>() + keep_used_;
-        conv(l, CS_CONV_WGRAD, (int)B, tw, s, false, w, dz, /*keep_slabs=*/true, nullptr, nullptr, tp);
-        const int k = sgd_slabs_.n++;
-        sgd_slabs_.off[k] = b.w_off;
-        sgd_slabs_.len[k] = slab;
-        sgd_slabs_.stride[k] = slab;
-        sgd_slabs_.slab[k] = w;
-        sgd_slabs_.ns[k] = spw;
-        keep_used_ += spw * slab;
-      } else {
-        // with a split K (no fold, not conv0's OIHW scatter) the combine rides this block's
-        // data-gradient launch below (independent of it) instead of a launch of its own
-        const bool kt = ktail_on_ && in_step_ && l > 0 && spw > 1 && spw <= 32 && !dual_ok(l);
-        conv(l, CS_CONV_WGRAD, (int)B, tw, s, false, ws_side_.data_ptr<float>(), dz, kt, nullptr, nullptr, tp);
-        if (kt) {
-          pend_ktail_ = CsSplitkTail{ws_side_.data_ptr<float>(), G(b.w_off), (int)dw.M, (int)dw.N, spw, 0};
-        }
-      }
+      conv(l, CS_CONV_WGRAD, (int)B, b.tile[CS_CONV_WGRAD], s, false, ws_w_.data_ptr<float>(), dz, nullptr,
+           tail.n > 0 ? &tail : nullptr);
+      if (er) conv(l, CS_CONV_DGRAD, (int)B, b.tile[CS_CONV_DGRAD], s, false, nullptr, dz, &erv, nullptr, fp);
     }
-    if (l > 0) {
-      const ConvTile& t = b.tile[CS_CONV_DGRAD];
-      const Dims d = dims(b, CS_CONV_DGRAD, B);
-      const int sp = eff_splits(d.K, t.splits, t.bk);
-      const bool keep = !er && keep_slabs_ && bn_path_ != 1 && sp > 1 && sp <= 32;
-      const CsSplitkTail kt = pend_ktail_;
-      pend_ktail_ = CsSplitkTail{};
-      conv(l, CS_CONV_DGRAD, (int)B, t, s, false, nullptr, dz, keep, nullptr, er ? &erv : nullptr, nullptr,
-           kt.M > 0 ? &kt : nullptr);
-      if (keep) {
-        g_slabs_ = sp;
-        g_stride_ = d.M * d.N;
-      }
-      if (er) {
-        red_pending_ = l - 1;
-        red_P_ = erv.P;
-      }
-    }
-    if (ovl && wgrad_after_dgrad_ && l == 0) {
-      // block 0's weight gradient is the step's last GEMM: nothing is left to overlap it with,
-      // so it runs on this stream (main's split-K workspace is free once the BN backward above
-      // has read the dgrad result) without a fork/join round trip
-      conv(l, CS_CONV_WGRAD, (int)B, b.tile[CS_CONV_WGRAD], s, false, ws_.data_ptr<float>(), dz);
-      if (bwd_sgd_) sgd_on(s, blk_range_[0].first, blk_range_[0].second, true);
-    } else if (ovl && wgrad_after_dgrad_) {
-      // (default) fork the weight gradient only after this block's data gradient: the
-      // critical dgrad keeps the whole chip, and the wgrad fills it while the main stream
-      // runs the latency-bound split-K combine / BN backward kernels of the block below.
-      // The signal rides the next main-stream launch (the BN backward of block l-1) instead of
-      // a launch of its own on the critical path (measured ~5.5 us each)
-      pending_sig_ = defer_signals_ ? dz_link_->defer() : nullptr;
-      if (pending_sig_ == nullptr) dz_link_->signal(s);
-      dz_link_->wait(side_);
-      conv(l, CS_CONV_WGRAD, (int)B, b.tile[CS_CONV_WGRAD], side_, false, ws_side_.data_ptr<float>(), dz);
-      // block l's dgrad (the last reader of its weights) and BN backward ran before the fork
-      if (bwd_sgd_) sgd_on(side_, blk_range_[l].first, blk_range_[l].second, false);
-      wg_link_->signal(side_);
+    if (er) {
+      red_pending_ = l - 1;
+      red_P_ = erv.P;
     }
   }
-  if (!in_step_ || join) flush_signal(s);  // nothing left on this stream to carry it
-  if (join && ovl) join_side(s);
 }
 
 VggEngine::~VggEngine() {
-  if (sys_ev_ != nullptr) {
-    hipEventSynchronize(sys_ev_);
-    hipEventDestroy(sys_ev_);
-  }
-  if (grid_err_ != nullptr) {
-    hipDeviceSynchronize();
-    hipHostFree(grid_err_);
-  }
-  if (side_ != nullptr) hipStreamSynchronize(side_);  // shared process-wide stream: not destroyed
-  if (opt_ != nullptr) {
-    hipStreamSynchronize(opt_);
-    hipStreamDestroy(opt_);
-  }
-  for (auto e : ev_opt_) hipEventDestroy(e);
   for (auto e : tev_) hipEventDestroy(e);
 }
 
@@ -735,7 +496,7 @@ void VggEngine::sgd_on(hipStream_t st, int64_t off, int64_t n, bool cursor) {
   ok(cs_sgd_flat(P(off), G(off), mom_.data_ptr<float>() + off, n, (float)hp_[0], (float)hp_[1], (float)hp_[2],
                  (float)hp_[3], 1.0f, sgd_first_ ? 1 : 0, st,
                  cursor && perm_len_ > 0 ? cursor_.data_ptr<int64_t>() : nullptr),
-     "sgd_flat(side)");
+     "sgd_flat(block)");
 }
 
 void VggEngine::sgd(double lr, double momentum, double wd, double dampening, int64_t off, int64_t n) {
@@ -751,7 +512,20 @@ void VggEngine::sgd(double lr, double momentum, double wd, double dampening, int
   sgd_first_ = false;
 }
 
-hipEvent_t VggEngine::opt_event() { return ev_opt_[next_opt_ev_++ % ev_opt_.size()]; }
+void VggEngine::set_perm(torch::Tensor perm) {
+  TORCH_CHECK(data_[0].defined(), "set_perm: set_data(0, ...) first");
+  TORCH_CHECK(perm.scalar_type() == at::kLong && perm.dim() == 1 && perm.numel() > 0, "set_perm: int64 [n] indices");
+  const int64_t n = perm.numel();
+  TORCH_CHECK(n <= data_[0].size(0) + Bmax_, "set_perm: permutation longer than the dataset");
+  if (!perm_.defined()) {
+    // fixed capacity (graph-captured kernels keep the pointer): dataset size + one batch of slack
+    perm_ = torch::zeros({data_[0].size(0) + Bmax_}, params_.options().dtype(at::kLong));
+    cursor_ = torch::zeros({1}, params_.options().dtype(at::kLong));
+  }
+  perm_.narrow(0, 0, n).copy_(perm.to(perm_.device()), /*non_blocking=*/false);
+  cursor_.zero_();
+  perm_len_ = n;
+}
 
 void VggEngine::set_timing(bool on) {
   timing_ = on;
@@ -784,34 +558,6 @@ std::vector<std::pair<std::string, double>> VggEngine::phase_times() {
   }
   out.emplace_back("step", total);
   return out;
-}
-
-void VggEngine::sgd_bucket(DeviceComm* comm, int64_t lo_block, int64_t off, int64_t n, double lr, double momentum,
-                           double wd, double dampening, bool advance_cursor) {
-  TORCH_CHECK(off >= 0 && n >= 0 && off + n <= params_.numel(), "sgd_bucket: range");
-  TORCH_CHECK(lo_block >= 0 && lo_block < (int64_t)blocks_.size(), "sgd_bucket: block");
-  hipStream_t s = cur_stream();
-  hipEvent_t e = opt_event();
-  ok(hipEventRecord(e, s), "record main");
-  ok(hipStreamWaitEvent(opt_, e, 0), "opt wait main");
-  TORCH_CHECK(!overlap_wgrad_, "sgd_bucket: per-bucket SGD and side-stream weight gradients are exclusive");
-  if (comm != nullptr) {
-    hipEvent_t c = opt_event();
-    ok(hipEventRecord(c, comm->stream()), "record comm");
-    ok(hipStreamWaitEvent(opt_, c, 0), "opt wait comm");
-  }
-  if (n == 0) return;
-  ok(cs_sgd_flat(P(off), G(off), mom_.data_ptr<float>() + off, n, (float)lr, (float)momentum, (float)wd,
-                 (float)dampening, 1.0f, sgd_first_ ? 1 : 0, opt_,
-                 advance_cursor && perm_len_ > 0 ? cursor_.data_ptr<int64_t>() : nullptr),
-     "sgd_flat(bucket)");
-  if (advance_cursor) sgd_first_ = false;  // the step's last bucket
-}
-
-void VggEngine::join_opt() {
-  hipEvent_t e = opt_event();
-  ok(hipEventRecord(e, opt_), "record opt");
-  ok(hipStreamWaitEvent(cur_stream(), e, 0), "join opt");
 }
 
 void VggEngine::forward_eval(int64_t B) {
@@ -851,7 +597,6 @@ void VggEngine::step(int64_t B, DeviceComm* comm, const std::vector<int64_t>& bu
   // the caller passes a communicator only when the step is data-parallel (a one-rank
   // communicator too: the CS_COMM_PROBE measurement and the ProbeComm ordering test)
   const bool dp = comm != nullptr;
-  const bool ovl = side_wgrad(s);
   tn_ = 0;
   Range step_range("cs.step");
   mark("start");
@@ -860,46 +605,21 @@ void VggEngine::step(int64_t B, DeviceComm* comm, const std::vector<int64_t>& bu
     forward_train(B);
   }
   mark("forward");
-  // per-bucket SGD needs the buckets to tile the flat buffer exactly
-  bool tiled = sgd_overlap_ && !ovl;
-  for (size_t k = 0, at = 0; k < nb && tiled; ++k) {
-    tiled = bucket_ranges[2 * k] == (int64_t)at;
-    at += bucket_ranges[2 * k + 1];
-    if (k + 1 == nb) tiled = tiled && (int64_t)at == params_.numel();
-  }
-  // SGD behind the weight gradients (sgd_side_): per block on the side stream (world 1), or per
-  // bucket on the comm stream behind its all-reduce; the buckets must tile the flat buffer
-  bool side_sgd = ovl && sgd_side_ && wgrad_after_dgrad_ && !blk_range_.empty();
-  for (size_t k = 0, at = 0; k < nb && side_sgd; ++k) {
-    side_sgd = bucket_ranges[2 * k] == (int64_t)at;
-    at += bucket_ranges[2 * k + 1];
-    if (k + 1 == nb) side_sgd = side_sgd && (int64_t)at == params_.numel();
-  }
   hp_[0] = lr;
   hp_[1] = momentum;
   hp_[2] = wd;
   hp_[3] = dampening;
-  bwd_sgd_ = side_sgd && !dp;
-  in_step_ = true;
-  // kept weight-gradient slabs for the final SGD (world 1, serial backward, one flat SGD launch)
-  sgd_slabs_.n = 0;
-  keep_used_ = 0;
-  keep_wg_ = sgd_slabs_on_ && !dp && !ovl && !tiled && !side_sgd;
-  // per-block SGD in the weight-gradient launches' tails (not with the kept-slab SGD, which needs
-  // the whole pass at the end)
-  sgd_tail_ = sgd_tail_on_ && !keep_wg_ && !dp && !ovl && !tiled && !side_sgd && !blk_range_.empty();
-  if (keep_wg_) {
-    int64_t need = 0;
-    for (int64_t l = 1; l < L; ++l) {
-      const ConvTile& tw = blocks_[l].tile[CS_CONV_WGRAD];
-      const Dims dw = dims(blocks_[l], CS_CONV_WGRAD, B);
-      const int spw = eff_splits(dw.K, tw.splits, tw.bk);
-      if (spw > 1 && spw <= 32) need += spw * dw.M * dw.N;
-    }
-    if ((!keep_ws_.defined() || keep_ws_.numel() < need) && !stream_capturing(s))
-      keep_ws_ = torch::zeros({std::max<int64_t>(need, 4)}, params_.options());
-    keep_wg_ = keep_ws_.defined() && keep_ws_.numel() >= need;
+  // data-parallel: each bucket's SGD runs on the comm stream right behind its all-reduce (every
+  // reader of the bucket's weights — its blocks' data gradients — was enqueued before the fork);
+  // the buckets must tile the flat buffer
+  bool comm_sgd = dp;
+  for (size_t k = 0, at = 0; k < nb && comm_sgd; ++k) {
+    comm_sgd = bucket_ranges[2 * k] == (int64_t)at;
+    at += bucket_ranges[2 * k + 1];
+    if (k + 1 == nb) comm_sgd = comm_sgd && (int64_t)at == params_.numel();
   }
+  // world 1: block l+1's SGD rides block l's weight-gradient launch
+  sgd_tail_ = sgd_tail_on_ && !dp && !blk_range_.empty();
   int64_t hi = L - 1;
   for (size_t k = 0; k < nb; ++k) {
     const int64_t lo = bucket_blocks[k];
@@ -908,75 +628,44 @@ void VggEngine::step(int64_t B, DeviceComm* comm, const std::vector<int64_t>& bu
                                   "cs.backward.bucket3", "cs.backward.bucket4", "cs.backward.bucket5",
                                   "cs.backward.bucket6", "cs.backward.bucket7"};
     Range bwd_range(k < 8 ? kBwdR[k] : "cs.backward.bucket8+");
-    backward(hi, lo, B, /*join=*/false);
+    backward(hi, lo, B);
     bwd_range.end();
     static const char* kBwd[] = {"backward_bucket0", "backward_bucket1", "backward_bucket2", "backward_bucket3",
                                  "backward_bucket4", "backward_bucket5", "backward_bucket6", "backward_bucket7"};
     mark(k < 8 ? kBwd[k] : "backward_bucket8+");
     hi = lo - 1;
-    // a bucket is complete once its last weight-gradient GEMM (side stream) is: fork the
-    // all-reduce from there, so it overlaps the rest of the backward on the main stream. The
-    // last bucket also holds block 0, whose weight gradient ran on the main stream: join the
-    // side stream into main and fork from main
-    hipStream_t src = ovl ? side_ : s;
-    if (ovl && lo == 0 && wgrad_after_dgrad_) {
-      join_side(s);
-      src = s;
-    }
-    if (dp) {
+    if (!dp) continue;
+    {
+      // the bucket is complete: its all-reduce forks from here and overlaps the rest of the backward
       Range r("cs.allreduce.enqueue");
-      if (comm->host_blocking()) flush_signal(s);
-      comm->all_reduce(G(bucket_ranges[2 * k]), bucket_ranges[2 * k + 1], ncclFloat32, ncclAvg, src,
+      comm->all_reduce(G(bucket_ranges[2 * k]), bucket_ranges[2 * k + 1], ncclFloat32, ncclAvg, s,
                        /*fork=*/!(debug_skip_ & 2));
     }
-    if (dp && broadcast_buffers && k == 0) {
+    if (broadcast_buffers && k == 0) {
       // DDP broadcast_buffers (rank 0's BN running stats before every training forward), issued
       // for the NEXT forward right behind the first bucket: this forward has produced the
       // buffers, nothing touches them until the next forward, and the step's closing join
-      // orders them before it — no fork/join of its own at the head of the step (step 0 is
-      // covered by the construction-time broadcast)
-      // (no fork: the all-reduce just enqueued already waited for the forward)
+      // orders them before it (step 0 is covered by the construction-time broadcast)
       comm->broadcast(bufs_.data_ptr<float>(), bufs_.numel(), ncclFloat32, 0, s, /*fork=*/false);
       comm->broadcast(nbt_.data_ptr<int64_t>(), nbt_.numel(), ncclInt64, 0, s, /*fork=*/false);
     }
-    // ... and its SGD can run as soon as the averaged gradient is in and block lo's data
-    // gradient (the last reader of these weights) is done, beside the backward below
-    if (tiled)
-      sgd_bucket(comm, lo, bucket_ranges[2 * k], bucket_ranges[2 * k + 1], lr, momentum, wd, dampening, k + 1 == nb);
-    // the comm stream runs this bucket's SGD right behind its all-reduce (every reader of the
-    // bucket's weights — its blocks' data gradients — was enqueued before the fork)
-    if (side_sgd && dp) sgd_on(comm->stream(), bucket_ranges[2 * k], bucket_ranges[2 * k + 1], k + 1 == nb);
+    if (comm_sgd) sgd_on(comm->stream(), bucket_ranges[2 * k], bucket_ranges[2 * k + 1], k + 1 == nb);
   }
-  bwd_sgd_ = false;
-  in_step_ = false;
-  flush_signal(s);
   {
     Range r("cs.comm.join");
-    if (ovl) join_side(s);
     if (dp && !(debug_skip_ & 1)) comm->join(s);
   }
   mark("allreduce_wait");
   {
     Range r("cs.sgd");
-    if (tiled) {
-      join_opt();
-    } else if (!side_sgd && sgd_slabs_.n > 0) {
-      ok(cs_sgd_flat_slabs(P(0), G(0), mom_.data_ptr<float>(), params_.numel(), (float)lr, (float)momentum, (float)wd,
-                           (float)dampening, 1.0f, sgd_first_ ? 1 : 0, s,
-                           perm_len_ > 0 ? cursor_.data_ptr<int64_t>() : nullptr, sgd_slabs_),
-         "sgd_flat_slabs");
-      sgd_first_ = false;
-    } else if (sgd_tail_) {
+    if (sgd_tail_) {
       // blocks 1.. rode the weight-gradient launches; block 0 (+ the cursor) here
       sgd_on(s, blk_range_[0].first, blk_range_[0].second, true);
-      sgd_first_ = false;
-    } else if (!side_sgd) {
+    } else if (!comm_sgd) {
       sgd(lr, momentum, wd, dampening, 0, params_.numel());
     }
-    sgd_slabs_.n = 0;
-    keep_wg_ = false;
+    sgd_first_ = false;
     sgd_tail_ = false;
-    if (side_sgd) sgd_first_ = false;
   }
   mark("sgd");
 }
@@ -1122,9 +811,6 @@ std::vector<double> VggEngine::autotune(int64_t B, int64_t iters) {
         float ms = 0.f;
         ok(hipEventElapsedTime(&ms, e0, e1), "elapsed");
         const float dual_us = 1000.f * ms / (float)iters;
-        if (getenv("CS_TUNE_VERBOSE"))
-          fprintf(stderr, "[tune] block %d: dual (stage %d) %.1f us vs separate %.1f us\n", l, c.first.stage,
-                  dual_us, keep_w.us + keep_d.us);
         if (dual_us < best_t) {
           best_t = dual_us;
           win_w = c.first;

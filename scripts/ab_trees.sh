@@ -1,27 +1,30 @@
 #!/bin/bash
-# Same-box A/B of two source trees (each with its own built _C.so), interleaved:
-#   bash scripts/ab_trees.sh TREE_A TREE_B [rounds] [bench.py args]
-# e.g. TREE_A = .ab/r2 (a `git worktree add .ab/r2 <commit>` built in place), TREE_B = . (HEAD).
-# One bench.py process per run, A and B alternating `rounds` times (default 3), so clock and
-# thermal drift on the box hit both trees alike. Prints one line per run and a median per tree.
+# Same-box A/B of source trees (each with its own built _C.so), interleaved:
+#   bash scripts/ab_trees.sh ROUNDS TREE... [-- bench.py args]
+# e.g. TREE = .ab/r2 (a `git worktree add .ab/r2 <commit>` built in place) and . (the working tree).
+# One bench.py process per run, the trees alternating ROUNDS times, so clock and thermal drift on
+# the box hit every tree alike. Prints one line per run and a median per tree.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}" || exit 1
 mkdir -p gpurun_out
-A=$1; B=$2; N=${3:-3}; shift 3 || shift $#
+N=$1; shift
+TREES=()
+while [ $# -gt 0 ] && [ "$1" != "--" ]; do TREES+=("$1"); shift; done
+[ "$1" = "--" ] && shift
 [ $# -eq 0 ] && set -- --steps 20 --warmup 5
 R=$PWD
 : > gpurun_out/ab_trees.tmp
 for i in $(seq 1 "$N"); do
-  for t in "$A" "$B"; do
+  for t in "${TREES[@]}"; do
     out=$(cd "$t" && timeout -k 10 300 python -u bench.py "$@" 2>>"$R/gpurun_out/ab_trees.err" | tail -1) || exit $?
-    v=$(python3 -c "import json,sys; d=json.loads(sys.argv[1]); print(d['value'], d['ms_per_step'])" "$out") || exit $?
+    v=$(python3 -c "import json,sys; d=json.loads(sys.argv[1]); print(d['value'], d['ms_per_step'], (d.get('calibration') or {}).get('mfma_bf16_gemm_tflops'))" "$out") || exit $?
     echo "$t $v" | tee -a gpurun_out/ab_trees.tmp
   done
 done
-python3 - "$A" "$B" "$*" <<'EOF'
+python3 - "$*" "${TREES[@]}" <<'PY'
 import statistics, sys
 rows = [l.split() for l in open("gpurun_out/ab_trees.tmp") if l.strip()]
-for t in sys.argv[1:3]:
+for t in sys.argv[2:]:
     v = [float(r[1]) for r in rows if r[0] == t]
-    print(f"# {t}: median {statistics.median(v):.0f} img/s over {len(v)} runs ({sys.argv[3]}); all {v}")
-EOF
+    print(f"# {t}: median {statistics.median(v):.0f} img/s over {len(v)} runs ({sys.argv[1]}); all {v}")
+PY

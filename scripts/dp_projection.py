@@ -1,0 +1,68 @@
+"""N>1 projection of the VGG-11 data-parallel step on ONE MI355X (a model, not a measurement of N GPUs).
+
+The native engine runs its real data-parallel schedule — bucket all-reduces forked from the compute
+stream as soon as each bucket's gradients exist, each bucket's SGD behind its all-reduce on the
+comm stream, the BN-buffer broadcast, the closing join — against a probe communicator
+(ProbeComm "xgmi:G:W:us") whose every all-reduce is a spin as long as a W-GPU ring all-reduce of its
+bytes at G GB/s bus bandwidth plus a per-call latency: t = us + 2 (W-1)/W * bytes / G. Compute per
+GPU is what weak scaling keeps fixed (B = 64 per GPU), so the projected W-GPU throughput is
+W * B / t_step. Not modelled: RCCL's CTAs (CS_COMM_CTAS, default 16 of 256 CUs) competing with the
+backward GEMMs while a collective runs (bounded below by the CU share: <= 16/256 = 6 % of the
+overlapped GEMM time), and rank skew.
+
+Usage (GPU box): python scripts/dp_projection.py [--steps 50] [--gbps 100,150,300] [--worlds 2,4,8]
+"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import cs744_pytorch_distributed_tutorial_amd  # noqa: F401,E402
+import torch  # noqa: E402
+
+
+def run(probe, steps, warmup, B=64):
+    from cs744_pytorch_distributed_tutorial_amd.runtime.engine import NativeTrainer
+    dev = torch.device("cuda", 0)
+    tr = NativeTrainer(batch_size=B, device=dev, probe=probe, graph="none")
+    for _ in range(warmup):
+        tr.step()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(steps):
+        tr.step()
+    e1.record()
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / steps
+    ph = tr.phase_breakdown(5)
+    buckets = [n * 4 / 2 ** 20 for _, n in tr.bucket_ranges]
+    tr.close()
+    return ms, ph, buckets
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--gbps", type=str, default="100,150,300")
+    p.add_argument("--worlds", type=str, default="2,4,8")
+    p.add_argument("--latency-us", type=float, default=25.0)
+    a = p.parse_args()
+    torch.cuda.set_device(0)
+    base, ph0, buckets = run("0", a.steps, a.warmup)
+    print(json.dumps({"config": "world 1 (no communicator)", "ms_per_step": round(base, 4),
+                      "img_s": round(64 / base * 1e3), "bucket_mib": [round(b, 2) for b in buckets],
+                      "phases_ms": {k: round(v, 4) for k, v in ph0.items()}}), flush=True)
+    for g in [float(x) for x in a.gbps.split(",")]:
+        for w in [int(x) for x in a.worlds.split(",")]:
+            ms, ph, _ = run(f"xgmi:{g}:{w}:{a.latency_us}", a.steps, a.warmup)
+            print(json.dumps({"config": f"projected N={w}, ring busBW {g:g} GB/s, {a.latency_us:g} us/collective",
+                              "ms_per_step": round(ms, 4), "projected_img_s": round(w * 64 / ms * 1e3),
+                              "per_gpu_img_s": round(64 / ms * 1e3), "efficiency_vs_world1": round(base / ms, 4),
+                              "allreduce_wait_ms": round(ph.get("allreduce_wait", 0.0), 4)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -14,8 +14,6 @@
 #                              per-queue timeline (scripts/prof_summary.py, scripts/step_timeline.py)
 #   pmc TAG "COUNTERS" [args]  one rocprofv3 counter pass over a short bench (kernel trace only,
 #                              never combined with other trace domains) -> scripts/pmc_summary.py
-#   xp                         pre-split conv GEMM tests + graph-timed sweep (scripts/xp_bench.py)
-#   probe                      XP K-loop ablation (scripts/xp_probe.py)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}" || exit 1
 mkdir -p gpurun_out
@@ -67,8 +65,6 @@ case "$what" in
     TAG=${1:-pmc}; P=$2; shift 2 || true
     [ $# -eq 0 ] && set -- --steps 3 --warmup 2
     page_in
-    # counter collection serialises dispatches: the side-stream link waits cannot overlap
-    export CS_OVERLAP_WGRAD=0
     (cd /tmp && timeout -s KILL 150 rocprofv3 --pmc $P --output-format csv -d $R/gpurun_out/$TAG -o run -- \
       python3 $R/bench.py "$@" > $R/gpurun_out/$TAG.log 2>&1)
     rc=$?; echo "pmc pass exit $rc"; tail -2 gpurun_out/$TAG.log
@@ -76,19 +72,7 @@ case "$what" in
     python3 scripts/pmc_summary.py gpurun_out/$TAG > gpurun_out/${TAG}_summary.txt 2>&1
     head -40 gpurun_out/${TAG}_summary.txt
     ;;
-  xp)
-    timeout -k 10 700 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_conv_xp_gpu.py \
-      > gpurun_out/xp_tests.log 2>&1
-    rc=$?; tail -5 gpurun_out/xp_tests.log; echo "pytest rc=$rc"
-    [ $rc -eq 0 ] || exit $rc
-    timeout -k 10 600 python -u scripts/xp_bench.py 64 10 > gpurun_out/xp_bench.log 2>&1
-    rc=$?; grep -v amdgpu.ids gpurun_out/xp_bench.log; exit $rc
-    ;;
-  probe)
-    timeout -k 10 400 python -u scripts/xp_probe.py > gpurun_out/xp_probe.log 2>&1
-    rc=$?; cat gpurun_out/xp_probe.log; exit $rc
-    ;;
   *)
-    echo "usage: bash scripts/gpu.sh suite|tests|bench|trace|pmc|xp|probe ..."; exit 2
+    echo "usage: bash scripts/gpu.sh suite|tests|bench|trace|pmc ..."; exit 2
     ;;
 esac

@@ -28,18 +28,13 @@ def _close(a, b, rel=2e-5):
 SHAPES = [(2, 32, 3, 64), (2, 16, 64, 128), (2, 8, 128, 256), (3, 4, 256, 512), (4, 2, 512, 512)]
 TILES = [(64, 64, 1, 16), (128, 64, 1, 16), (64, 128, 3, 16), (128, 128, 2, 16), (64, 64, 1, 32), (128, 128, 3, 32),
          (64, 128, 4, 32), (128, 64, 2, 32), (64, 64, 2, 64), (128, 64, 1, 64)]
-# (in-launch split-K combine, operand staging): 0 = registers + ds_write, 1/2 = LDS-DMA ring of
-# depth 3/5 (bk 32 only)
+# operand staging: 0 = registers + ds_write, 1/2 = LDS-DMA ring of depth 3/5 (bk 32 only)
 # 3/4 = register staging with 2/4 K-groups of waves per block
 # +8 = the same staging with the fp32-accurate split-bf16 (X6) math, +16 = X6 split once at the LDS
 # store (bf16 planes, transposed LDS reads for K-major operands): held to the same f64 tolerance
-VARIANTS = [(False, 0), (True, 0), (False, 1), (True, 1), (False, 2), (False, 3), (False, 4),
-            (False, 8), (True, 8), (False, 9), (False, 10), (False, 11), (False, 12),
-            (False, 16), (True, 16), (False, 19), (False, 20)]
-# the in-launch combine in K-group kernels (KG * 256 threads; the combine runs on the first 256)
-VARIANTS += [(True, 3), (True, 4), (True, 11), (True, 12), (True, 19), (True, 20)]
+VARIANTS = [0, 1, 2, 3, 4, 8, 9, 10, 11, 12, 16, 19, 20]
 # +32 = bf16 operands, f32 accumulation (the engine's opt-in bf16 mode): bf16-level tolerance
-VARIANTS += [(False, 32), (False, 35), (False, 36)]
+VARIANTS += [32, 35, 36]
 
 
 def _tol(stage, f32=2e-5):
@@ -82,8 +77,8 @@ def _stage_ok(stage, bm, bn, bk, conv0_fwd=False):
 
 
 def _matrix(shapes, tiles, conv0_fwd_shapes=()):
-    return [pytest.param(sh, t, fx, st, id=f"{sh}-{t}-{int(fx)}-{st}") for sh in shapes for t in tiles
-            for fx, st in VARIANTS if _stage_ok(st, t[0], t[1], t[3], sh in conv0_fwd_shapes)]
+    return [pytest.param(sh, t, st, id=f"{sh}-{t}-{st}") for sh in shapes for t in tiles
+            for st in VARIANTS if _stage_ok(st, t[0], t[1], t[3], sh in conv0_fwd_shapes)]
 
 
 def _skip_stage(stage, bk, bm, bn, conv0_fwd=False):
@@ -118,8 +113,8 @@ def _nhwc(x, pad4=False):
     return t.contiguous()
 
 
-@pytest.mark.parametrize("shape,tile,fixup,stage", _matrix(SHAPES, TILES, conv0_fwd_shapes=(SHAPES[0],)))
-def test_conv_fwd_and_stats(dev, shape, tile, fixup, stage):
+@pytest.mark.parametrize("shape,tile,stage", _matrix(SHAPES, TILES, conv0_fwd_shapes=(SHAPES[0],)))
+def test_conv_fwd_and_stats(dev, shape, tile, stage):
     from cs744_pytorch_distributed_tutorial_amd.ops import functional as Fn
     B, H, cin, cout = shape
     bm, bn, sp, bk = tile
@@ -130,7 +125,7 @@ def test_conv_fwd_and_stats(dev, shape, tile, fixup, stage):
     xd = _nhwc(x, pad4=conv0).float().to(dev)
     wd = (w if conv0 else w.permute(0, 2, 3, 1)).contiguous().float().to(dev)
     y, st, rows = Fn.conv_fwd(xd, wd, b.float().to(dev), w_oihw=conv0, bm=bm, bn=bn, splits=sp, stats=True, bk=bk,
-                            fixup=fixup, stage=stage)
+                            stage=stage)
     _close(y, ref, _tol(stage))
     M = ref.shape[0]
     for t in range(st.shape[0]):
@@ -140,8 +135,8 @@ def test_conv_fwd_and_stats(dev, shape, tile, fixup, stage):
         _close(st[t, :, 1], ((seg - mu) ** 2).sum(0), _tol(stage, 1e-4))
 
 
-@pytest.mark.parametrize("shape,tile,fixup,stage", _matrix(SHAPES[1:], TILES))
-def test_conv_dgrad(dev, shape, tile, fixup, stage):
+@pytest.mark.parametrize("shape,tile,stage", _matrix(SHAPES[1:], TILES))
+def test_conv_dgrad(dev, shape, tile, stage):
     from cs744_pytorch_distributed_tutorial_amd.ops import functional as Fn
     B, H, cin, cout = shape
     bm, bn, sp, bk = tile
@@ -150,7 +145,7 @@ def test_conv_dgrad(dev, shape, tile, fixup, stage):
     gy = torch.randn(B, cout, H, H, dtype=torch.float64)
     ref = torch.nn.grad.conv2d_input(x.shape, w, gy, padding=1).permute(0, 2, 3, 1).reshape(-1, cin)
     dx = Fn.conv_dgrad(_nhwc(gy).float().to(dev).view(-1, cout), w.permute(0, 2, 3, 1).contiguous().float().to(dev),
-                       B, H, H, bm=bm, bn=bn, splits=sp, bk=bk, fixup=fixup, stage=stage)
+                       B, H, H, bm=bm, bn=bn, splits=sp, bk=bk, stage=stage)
     _close(dx, ref, _tol(stage))
 
 
@@ -158,8 +153,8 @@ WGRAD_TILES = [(64, 64, 1, 16), (64, 64, 8, 16), (128, 128, 4, 16), (128, 64, 2,
                (64, 128, 4, 32), (128, 128, 1, 32), (64, 64, 4, 64)]
 
 
-@pytest.mark.parametrize("shape,tile,fixup,stage", _matrix(SHAPES, WGRAD_TILES))
-def test_conv_wgrad(dev, shape, tile, fixup, stage):
+@pytest.mark.parametrize("shape,tile,stage", _matrix(SHAPES, WGRAD_TILES))
+def test_conv_wgrad(dev, shape, tile, stage):
     from cs744_pytorch_distributed_tutorial_amd.ops import functional as Fn
     B, H, cin, cout = shape
     bm, bn, sp, bk = tile
@@ -169,7 +164,7 @@ def test_conv_wgrad(dev, shape, tile, fixup, stage):
     ref = torch.nn.grad.conv2d_weight(x, w.shape, gy, padding=1)
     conv0 = cin == 3
     dw = Fn.conv_wgrad(_nhwc(gy).float().to(dev).view(-1, cout), _nhwc(x, pad4=conv0).float().to(dev), cout,
-                       w_oihw=conv0, bm=bm, bn=bn, splits=sp, bk=bk, fixup=fixup, stage=stage)
+                       w_oihw=conv0, bm=bm, bn=bn, splits=sp, bk=bk, stage=stage)
     _close(dw, ref if conv0 else ref.permute(0, 2, 3, 1), _tol(stage))
 
 
@@ -177,11 +172,10 @@ def test_conv_wgrad(dev, shape, tile, fixup, stage):
                                         (64, 2, 512, True), (5, 16, 128, True), (8, 8, 256, False),
                                         (16, 8, 256, False), (8, 4, 512, False), (64, 8, 256, False),
                                         (64, 32, 64, True)])
-@pytest.mark.parametrize("fused", [False, True, "two", "grid"])
+@pytest.mark.parametrize("fused", [False, True])
 def test_bn_relu_pool_fwd_bwd(dev, B, H, C, pool, fused):
     # False: finalize / apply / reduce / finalize / apply launches; True: the single-launch kernels
-    # (forward row-chunked over blocks); "two": row-chunked forward + the two-launch backward;
-    # "grid": the one-launch grid-barrier kernels (bn_grid.hip, the engine's default)
+    # (forward row-chunked over blocks)
     from cs744_pytorch_distributed_tutorial_amd.ops import functional as Fn
     torch.manual_seed(B * C)
     y = (torch.randn(B, C, H, H, dtype=torch.float64) * 2 + 0.5).requires_grad_()
@@ -205,8 +199,7 @@ def test_bn_relu_pool_fwd_bwd(dev, B, H, C, pool, fused):
         seg = yd.double().view(-1, R, C)
         mu_t = seg.mean(1)
         st = torch.stack([mu_t, ((seg - mu_t[:, None]) ** 2).sum(1)], 2).float().contiguous()
-        out, bst = Fn.bn_relu_pool_fwd(yd, st, R, B, H, H, gd, bd, rmd, rvd, nbt, pool=pool,
-                                       fused="grid" if fused == "grid" else True)
+        out, bst = Fn.bn_relu_pool_fwd(yd, st, R, B, H, H, gd, bd, rmd, rvd, nbt, pool=pool, fused=True)
         # every row chunk of the forward computed the same coefficients: bnv matches a fresh finalize
         _close(bst.mean, yd.double().mean(0), 1e-5)
     else:
@@ -267,3 +260,48 @@ def test_bn_finalize_many_partials(dev, B, H, C, R):
     _close(rmd, rm, 1e-5)
     _close(rvd, rv, 1e-5)
     assert int(nbt) == 1
+
+
+# (B, H, cin, cout, tile): conv0 (1024 / 4096 row tiles: two-level combine), a 64x128 tile
+# (128-channel column tiles), split-K (statistics from the combine's 16-row tiles), X6S K-groups
+FIN_CASES = [((16, 32, 3, 64), (64, 64, 1, 16, 0)), ((64, 32, 3, 64), (64, 64, 1, 32, 0)),
+             ((8, 16, 64, 128), (64, 128, 1, 32, 0)), ((8, 16, 64, 128), (128, 64, 1, 32, 3)),
+             ((16, 8, 128, 256), (64, 64, 1, 64, 16 | 4)), ((16, 4, 256, 512), (64, 64, 3, 32, 0)),
+             ((64, 2, 512, 512), (64, 64, 4, 64, 16 | 4)), ((5, 8, 128, 256), (64, 64, 2, 16, 0))]
+
+
+@pytest.mark.parametrize("shape,tile", FIN_CASES)
+def test_conv_fwd_in_launch_bn_finalize(dev, shape, tile):
+    """The BN finalize done by the conv launch's last-arriving block (bn_fin.h: sc1 partials, two-level
+    ticket combine) vs fp64 batch statistics of the same conv output: scale / shift / mean /
+    invstd and the running-stat update; repeated launches leave the tickets zeroed and give the
+    same bits (the combine order does not depend on which block arrives last)."""
+    from cs744_pytorch_distributed_tutorial_amd.ops import functional as Fn
+    B, H, cin, cout = shape
+    bm, bn, sp, bk, stage = tile
+    conv0 = cin == 3
+    x, w, b = _inputs(dev, B, H, cin, cout, 3)
+    x = x * 2.0 + 0.75  # a mean offset: the Chan combine must not lose the variance
+    ref = F.conv2d(x, w, b, padding=1).permute(0, 2, 3, 1).reshape(-1, cout)
+    xd = _nhwc(x, pad4=conv0).float().to(dev)
+    wd = (w if conv0 else w.permute(0, 2, 3, 1)).contiguous().float().to(dev)
+    g = torch.Generator().manual_seed(7)
+    gamma = (torch.rand(cout, generator=g, dtype=torch.float64) + 0.5)
+    beta = torch.randn(cout, generator=g, dtype=torch.float64)
+    outs = []
+    for _ in range(3):
+        rm, rv = torch.full((cout,), 0.25, device=dev), torch.full((cout,), 2.0, device=dev)
+        fin = dict(gamma=gamma.float().to(dev), beta=beta.float().to(dev), running_mean=rm, running_var=rv)
+        y, st, rows, bs = Fn.conv_fwd(xd, wd, b.float().to(dev), w_oihw=conv0, bm=bm, bn=bn, splits=sp, stats=True,
+                                      bk=bk, stage=stage, fin=fin)
+        torch.cuda.synchronize()
+        outs.append(torch.cat([bs.scale, bs.shift, bs.mean, bs.invstd, rm, rv]).cpu())
+    mu, var = ref.mean(0), ref.var(0, unbiased=False)
+    inv = 1.0 / torch.sqrt(var + 1e-5)
+    _close(bs.mean, mu, 1e-5)
+    _close(bs.invstd, inv, 1e-5)
+    _close(bs.scale, gamma * inv, 1e-5)
+    _close(bs.shift, beta - mu * gamma * inv, 1e-5)
+    _close(rm, 0.9 * 0.25 + 0.1 * mu, 1e-5)
+    _close(rv, 0.9 * 2.0 + 0.1 * ref.var(0, unbiased=True), 1e-5)
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])

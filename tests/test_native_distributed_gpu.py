@@ -47,8 +47,7 @@ def _train(rank, world, sync, graph, steps, comm="torch", B=16, autotune=False, 
            "tiles": tr.tile_source, "maths": maths,
            "loss": tr.last_loss(), "buckets": len(tr.bucket_lows), "graph": tr.graph_mode,
            "calls": tr.native_comm.calls() if tr.native_comm is not None else -1,
-           "kind": tr.native_comm.kind if tr.native_comm is not None else "none", "eval": ev,
-           "wgrad_side": tr.overlap_wgrad, "sys_join": tr.sys_join}
+           "kind": tr.native_comm.kind if tr.native_comm is not None else "none", "eval": ev}
     tr.close()
     return out
 
@@ -74,47 +73,25 @@ def test_ddp_segments_replicas_identical_and_match_eager(gpu):
 
 
 @pytest.mark.slow
-def test_python_gloo_collectives_with_side_stream_wgrad(gpu):
-    """Round-2 advisor finding: side-stream weight gradients + an all-reduce issued from Python
-    over gloo intermittently read a stale gradient (layers.25.weight at step 3 of 4). gloo moves a
-    CUDA tensor to the host with a copy ordered after the main stream only; the side stream's
-    last kernels had released at device scope, which does not cover that copy. The join of the
-    side stream into the main stream now also waits on a HIP event recorded with a system-scope
-    release (VggEngine::join_side, sys_join on for Python collectives). Eager steps (no graph:
-    the side stream runs every step), several repetitions, bitwise against the serial backward."""
-    ser = run_world(_train, 2, "ddp", "none", 6, "torch", 16, False, {"CS_OVERLAP_WGRAD": "0"})
-    assert not ser[0]["wgrad_side"]
-    for _ in range(3):
-        ovl = run_world(_train, 2, "ddp", "none", 6, "torch", 16, False, {"CS_OVERLAP_WGRAD": "1"})
-        assert ovl[0]["wgrad_side"] and ovl[0]["sys_join"]
-        for r in range(2):
-            for k in ("params", "mom", "bufs"):
-                assert torch.equal(ovl[r][k], ser[r][k]), (r, k, (ovl[r][k] - ser[r][k]).abs().max())
-
-
-@pytest.mark.slow
 @pytest.mark.parametrize("world", [2, 4])
 def test_cpp_ddp_step_multi_rank_staged(gpu, world):
     """The N>1 benchmark's C++ step (not _step_eager) with `world` ranks on one GPU."""
     steps = 8
     ref = run_world(_train, world, "ddp", "segments", steps, "torch")
-    # the serial backward (default) and the opt-in side-stream weight gradients
-    for side in (False, True):
-        nat = run_world(_train, world, "ddp", "none", steps, "staged", 16, False,
-                        {"CS_OVERLAP_WGRAD": "1" if side else "0"})
-        nb = nat[0]["buckets"]
-        assert nb > 1 and nat[0]["kind"] == "staged"
-        # construction: 4 broadcasts; per step: one all-reduce per bucket + 2 buffer broadcasts
-        assert nat[0]["calls"] == steps * (nb + 2), nat[0]["calls"]
-        for r in range(world):
-            for k in ("params", "mom", "bufs", "nbt"):
-                assert torch.equal(nat[r][k], nat[0][k]), (r, k)
-            assert nat[r]["eval"]["global_correct"] == world * nat[r]["eval"]["correct"]
-            assert nat[r]["wgrad_side"] == side
-        # same gradients, same averaging bytes, same SGD: the C++ step equals the Python-orchestrated one
-        assert torch.equal(nat[0]["params"], ref[0]["params"])
-        assert torch.equal(nat[0]["mom"], ref[0]["mom"])
-        assert nat[0]["loss"] == ref[0]["loss"]
+    # (each bucket's SGD runs on the comm stream right behind its all-reduce)
+    nat = run_world(_train, world, "ddp", "none", steps, "staged", 16, False)
+    nb = nat[0]["buckets"]
+    assert nb > 1 and nat[0]["kind"] == "staged"
+    # construction: 4 broadcasts; per step: one all-reduce per bucket + 2 buffer broadcasts
+    assert nat[0]["calls"] == steps * (nb + 2), nat[0]["calls"]
+    for r in range(world):
+        for k in ("params", "mom", "bufs", "nbt"):
+            assert torch.equal(nat[r][k], nat[0][k]), (r, k)
+        assert nat[r]["eval"]["global_correct"] == world * nat[r]["eval"]["correct"]
+    # same gradients, same averaging bytes, same SGD: the C++ step equals the Python-orchestrated one
+    assert torch.equal(nat[0]["params"], ref[0]["params"])
+    assert torch.equal(nat[0]["mom"], ref[0]["mom"])
+    assert nat[0]["loss"] == ref[0]["loss"]
 
 
 @pytest.mark.slow
@@ -125,7 +102,7 @@ def test_cpp_ddp_step_multi_rank_staged_bench_config(gpu):
     nat = run_world(_train, 2, "ddp", "none", steps, "staged", 64, True)
     ref = run_world(_train, 2, "ddp", "segments", steps, "torch", 64, True)
     assert nat[0]["tiles"] == "shipped" and "x6s" in nat[0]["maths"], (nat[0]["tiles"], nat[0]["maths"])
-    assert not nat[0]["wgrad_side"] and nat[0]["kind"] == "staged"  # the bench default: serial backward
+    assert nat[0]["kind"] == "staged"
     for k in ("params", "mom", "bufs", "nbt"):
         assert torch.equal(nat[1][k], nat[0][k]), k
     assert torch.equal(nat[0]["params"], ref[0]["params"])
@@ -165,17 +142,13 @@ def test_sync_modes_agree(gpu):
         torch.testing.assert_close(out[0]["params"], ref, rtol=1e-5, atol=1e-6, msg=mode)
 
 
-def _probe_run(probe, steps=6, skip=0, sgd_overlap=False, sgd_side=True):
+def _probe_run(probe, steps=6, skip=0):
     from cs744_pytorch_distributed_tutorial_amd.runtime.engine import NativeTrainer
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     tr = NativeTrainer(batch_size=32, device=dev, bucket_mb=1.0, graph="none", train_size=512, test_size=32,
                        autotune=False, probe=probe, probe_spin_us=40.0)
     tr.engine.set_debug_skip(skip)
-    if sgd_overlap:  # per-bucket SGD and side-stream weight gradients are exclusive
-        tr.engine.set_overlap_wgrad(False)
-    tr.engine.set_sgd_overlap(sgd_overlap)
-    tr.engine.set_sgd_side(sgd_side)
     for _ in range(steps):
         tr.step()
     torch.cuda.synchronize()
@@ -186,27 +159,23 @@ def _probe_run(probe, steps=6, skip=0, sgd_overlap=False, sgd_side=True):
 
 
 def test_probe_comm_ordering_bitwise(gpu):
+    """One-rank probe communicator (each collective = a spin + an exact scramble / unscramble on the
+    comm stream): the data-parallel step — bucket all-reduces forked from the compute stream, each
+    bucket's SGD behind its all-reduce on the comm stream, the closing join — equals the world-1
+    step (SGD in the weight-gradient tails) bit for bit."""
     base, _ = _probe_run("0")
     probed, calls = _probe_run("order")
     assert calls > 6
     for k in base:
         assert torch.equal(base[k], probed[k]), k
-    # per-bucket SGD on the optimizer stream must wait for each bucket's collective too
-    ovl, _ = _probe_run("order", sgd_overlap=True)
-    for k in base:
-        assert torch.equal(base[k], ovl[k]), ("sgd_overlap", k)
-    # one SGD after the join instead of per-bucket SGD behind each collective on the comm stream
-    end, _ = _probe_run("order", sgd_side=False)
-    for k in base:
-        assert torch.equal(base[k], end[k]), ("sgd at the end", k)
 
 
 def test_probe_comm_detects_missing_join(gpu):
-    """Negative controls: without the join before the step's SGD, or without the fork before
-    the collectives (which the per-bucket SGD then follows on the comm stream), the scrambled
-    gradients are consumed."""
+    """Negative controls: without the closing join (the next forward reads parameters the comm
+    stream's SGD has not written yet), or without the fork before the collectives (which the
+    per-bucket SGD then follows on the comm stream), the results differ."""
     base, _ = _probe_run("0")
-    bad, _ = _probe_run("order", skip=1, sgd_side=False)
+    bad, _ = _probe_run("order", skip=1)
     assert not torch.equal(base["params"], bad["params"])
     bad, _ = _probe_run("order", skip=2)
     assert not torch.equal(base["params"], bad["params"])

@@ -251,63 +251,6 @@ def test_single_launch_bn_matches_multi_kernel_bn(dev):
     torch.testing.assert_close(b.nbt, a.nbt)
 
 
-def test_grid_bn_matches_multi_launch_bn(dev, monkeypatch):
-    """The one-launch grid-barrier BN kernels (default, CS_BN_PATH=2) vs the 2/3-launch path
-    (CS_BN_PATH=0): same partials, different (fixed) finalize order -> a norm bound after two
-    steps, identical num_batches_tracked; and the grid path is deterministic run to run."""
-    out = []
-    for path in ("0", "2", "2"):
-        monkeypatch.setenv("CS_BN_PATH", path)
-        t = _trainer(dev, batch_size=32, train_size=256)
-        for _ in range(2):
-            t.step()
-        torch.cuda.synchronize()
-        assert not t.engine.link_error()
-        out.append((t.params.clone(), t.nbt.clone(), t.last_loss()))
-    a, b, c = out
-    assert abs(a[2] - b[2]) < 1e-3 * max(1.0, abs(a[2]))
-    d = (b[0].double() - a[0].double()).norm() / a[0].double().norm()
-    assert d.item() < 2e-3, d.item()
-    torch.testing.assert_close(a[1], b[1])
-    assert torch.equal(b[0], c[0])
-
-
-def test_deferred_link_signals_bitwise_equal(dev, monkeypatch):
-    """Side-stream weight gradients forked by a signal folded into the next main-stream BN launch
-    (CS_DEFER_SIGNALS=1, default) == a separate signal launch per block, bit for bit."""
-    out = []
-    monkeypatch.setenv("CS_OVERLAP_WGRAD", "1")
-    for defer in ("0", "1"):
-        monkeypatch.setenv("CS_DEFER_SIGNALS", defer)
-        t = _trainer(dev, batch_size=32, train_size=256)
-        assert t.overlap_wgrad
-        for _ in range(4):
-            t.step()
-        torch.cuda.synchronize()
-        t.check_comm()
-        out.append((t.params.clone(), t.mom.clone(), t.bufs.clone()))
-    for a, b in zip(out[0], out[1]):
-        assert torch.equal(a, b)
-
-
-@pytest.mark.parametrize("stage", [0, 16 | 4])
-def test_kept_dgrad_slabs_bitwise_equal(dev, stage, monkeypatch):
-    # CS_KEEP_SLABS=1 (opt-in): split-K data gradients left as slabs and summed (z order) by the
-    # next BN backward while it reads G == the separate split-K combine launch, bit for bit
-    out = []
-    monkeypatch.setenv("CS_BN_EPI_RED", "0")  # kept slabs leave the BN partials to the reduce pass
-    for keep in ("0", "1"):
-        monkeypatch.setenv("CS_KEEP_SLABS", keep)
-        t = _trainer(dev, batch_size=32, train_size=256)
-        for l in range(1, t.layout.L):
-            t.engine.set_tile(l, 1, 64, 64, 4 if l % 2 else 3, 64 if stage else 16, stage)
-        for _ in range(3):
-            t.step()
-        torch.cuda.synchronize()
-        out.append((t.params.clone(), t.mom.clone()))
-    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
-
-
 def test_phase_breakdown(dev):
     # opt-in device-side phase timing of the C++ step (SURVEY.md §5.1)
     t = _trainer(dev, batch_size=16, train_size=128)
@@ -337,123 +280,71 @@ def test_bf16_mode_tracks_fp32(dev):
     assert (ga @ gb / (ga.norm() * gb.norm())).item() > 0.95
 
 
+def _set_tiles(t, tiles):
+    """Tile tables exercising every in-launch finalize / apply site: split-K fwd / dgrad (statistics,
+    partials and apply in the combine), epilogue partials with 64x64 / 128x64 / 64x128 tiles at 256 /
+    1024 threads, and one wgrad + dgrad launch."""
+    if tiles in ("shipped", "default"):
+        return
+    for l in range(t.layout.L):
+        if tiles == "split":
+            t.engine.set_tile(l, 0, 64, 64, 2 + (l % 2), 16 if l == 0 else 64, 0 if l % 2 == 0 else (16 | 4))
+            if l > 0:
+                t.engine.set_tile(l, 1, 64, 64, 4 if l % 2 else 3, 64 if l % 2 else 16, (16 | 4) if l % 2 else 0)
+        elif tiles == "nosplit":
+            t.engine.set_tile(l, 0, 64, 128 if l % 2 else 64, 1, 32, 0)
+            if l > 0:
+                t.engine.set_tile(l, 1, 64 if l % 2 else 128, 64, 1, 64 if l % 2 else 32, (16 | 4) if l % 2 else 0)
+        elif l > 0:  # one wgrad + dgrad launch, split-K on every other dgrad
+            t.engine.set_tile(l, 1, 64, 64, 1 + (l % 2), 16, 0)
+            t.engine.set_tile(l, 2, 64, 64, 2, 16, 0)
+            t.engine.set_block_dual(l, True)
+
+
 @pytest.mark.parametrize("tiles", ["shipped", "split", "nosplit", "dual"])
-def test_bn_partials_from_dgrad_match_reduce_pass(dev, tiles, monkeypatch):
-    """Block l-1's BN-backward partial sums taken from block l's data gradient — in the dgrad
-    GEMM epilogue (no split-K) or in its split-K combine (CS_BN_EPI_RED=1, default) — vs the
-    separate reduce launch (=0): same per-element terms, a different fixed summation order ->
-    a norm bound after two steps at B=64; run to run bitwise."""
-    monkeypatch.setenv("CS_BN_PATH", "0")
-    if tiles == "dual":
-        monkeypatch.setenv("CS_OVERLAP_WGRAD", "0")
+def test_in_launch_bn_finalize_matches_finalize_launches(dev, tiles):
+    """Every BatchNorm finalize as the last-arriving block of the launch that produced its partial
+    sums (bn_fin.h: forward in the conv epilogue / split-K combine, backward in the data
+    gradient's epilogue / combine; set_fin(True), the default) vs the separate bn_finalize /
+    bn_bwd_finalize launches: same partials, a different fixed combine order -> a norm bound after
+    two steps at B=64 and identical num_batches_tracked; run to run bitwise (the combine order
+    does not depend on which block arrives last)."""
     out = []
-    for er in ("0", "1", "1"):
-        monkeypatch.setenv("CS_BN_EPI_RED", er)
+    for fin in (False, True, True):
         t = _trainer(dev, batch_size=64, train_size=256, autotune=tiles == "shipped")
-        if tiles != "shipped":
-            for l in range(1, t.layout.L):
-                if tiles == "split":  # split-K 3/4 dgrads, f32 and X6S kernels (partials in the combine)
-                    t.engine.set_tile(l, 1, 64, 64, 4 if l % 2 else 3, 64 if l % 2 else 16, (16 | 4) if l % 2 else 0)
-                elif tiles == "nosplit":  # epilogue partials: 64x64 / 128x64 tiles, 256 / 1024 threads
-                    t.engine.set_tile(l, 1, 64 if l % 2 else 128, 64, 1, 64 if l % 2 else 32,
-                                      (16 | 4) if l % 2 else 0)
-                else:  # one wgrad + dgrad launch
-                    t.engine.set_tile(l, 1, 64, 64, 1 + (l % 2), 16, 0)
-                    t.engine.set_tile(l, 2, 64, 64, 2, 16, 0)
-                    t.engine.set_block_dual(l, True)
+        t.engine.set_fin(fin)
+        _set_tiles(t, tiles)
         for _ in range(2):
             t.step()
         torch.cuda.synchronize()
-        assert not t.engine.link_error()
-        out.append((t.params.clone(), t.mom.clone(), t.bufs.clone(), t.last_loss()))
+        out.append((t.params.clone(), t.mom.clone(), t.bufs.clone(), t.nbt.clone(), t.last_loss()))
     a, b, c = out
-    assert abs(a[3] - b[3]) < 1e-4 * max(1.0, abs(a[3]))
-    for x, y in zip(a[:2], b[:2]):
+    assert abs(a[4] - b[4]) < 1e-4 * max(1.0, abs(a[4]))
+    # (a reordered fp32 combine: after two SGD steps the BN backward has amplified it to 1e-3 -
+    # 8.5e-3 of the momentum (measured: the dual-launch tiles are the most sensitive); the absolute
+    # accuracy of both orders is checked against fp64 in test_bench_config_b64_matches_fp64)
+    for name, x, y in zip(("params", "mom", "bufs"), a[:3], b[:3]):
         d = (y.double() - x.double()).norm() / x.double().norm()
-        assert d.item() < 1e-3, d.item()
-    for x, y in zip(b[:3], c[:3]):
+        assert d.item() < 1e-2, (name, d.item())
+    assert torch.equal(a[3], b[3])
+    for x, y in zip(b[:4], c[:4]):
         assert torch.equal(x, y)
 
 
-@pytest.mark.parametrize("tiles", ["shipped", "split"])
-def test_wgrad_combine_in_dgrad_launch_bitwise_equal(dev, tiles, monkeypatch):
-    """Serial step: block l's split-K weight-gradient combine as blocks appended to block l's
-    data-gradient launch (CS_KTAIL=1, opt-in) == its own combine launch, bit for bit."""
-    out = []
-    for on in ("0", "1"):
-        monkeypatch.setenv("CS_KTAIL", on)
-        t = _trainer(dev, batch_size=64, train_size=512, autotune=tiles == "shipped")
-        if tiles == "split":  # f32 and X6S weight gradients with 2..32 slabs, 256- and 1024-thread dgrads
-            for l in range(1, t.layout.L):
-                t.engine.set_tile(l, 2, 64, 64, [2, 32, 16, 8, 5, 3, 4][l - 1], 32 if l % 2 else 64,
-                                  0 if l % 2 else (16 | 4))
-                t.engine.set_tile(l, 1, 64, 64, 1, 64 if l % 2 else 16, (16 | 4) if l % 2 else 0)
-        for _ in range(3):
-            t.step()
-        torch.cuda.synchronize()
-        out.append((t.params.clone(), t.mom.clone(), t.grads.clone(), t.bufs.clone()))
-    for a, b in zip(*out):
-        assert torch.equal(a, b)
-
-
 @pytest.mark.parametrize("tiles", ["shipped", "default"])
-def test_sgd_in_wgrad_tails_bitwise_equal(dev, tiles, monkeypatch):
+def test_sgd_in_wgrad_tails_bitwise_equal(dev, tiles):
     """World-1 serial step: block l+1's SGD as blocks appended to block l's weight-gradient
-    launch (CS_SGD_TAIL=1, default) == one flat SGD pass at the end, bit for bit (parameters,
-    momentum incl. the first step's buf = d, BN buffers, the device cursor)."""
+    launch (set_sgd_tail(True), the default) == one flat SGD pass at the end, bit for bit
+    (parameters, momentum incl. the first step's buf = d, BN buffers, the device cursor)."""
     out = []
-    for on in ("0", "1"):
-        monkeypatch.setenv("CS_SGD_TAIL", on)
+    for on in (False, True):
         t = _trainer(dev, batch_size=64, train_size=512, autotune=tiles == "shipped")
+        t.engine.set_sgd_tail(on)
         for _ in range(4):
             t.step()
         torch.cuda.synchronize()
         out.append((t.params.clone(), t.mom.clone(), t.bufs.clone(), t.engine.cursor().clone()))
     for a, b in zip(*out):
-        assert torch.equal(a, b)
-
-
-@pytest.mark.parametrize("tiles", ["shipped", "split"])
-def test_wgrad_slabs_summed_by_sgd_bitwise_equal(dev, tiles, monkeypatch):
-    """World-1 serial step: split-K weight gradients left as slabs and summed (z order) by the
-    step's SGD launch (CS_SGD_SLABS=1, opt-in) == the combine launch + plain SGD, bit for bit —
-    parameters, momentum and the gradient buffer itself."""
-    out = []
-    for on in ("0", "1"):
-        monkeypatch.setenv("CS_SGD_SLABS", on)
-        t = _trainer(dev, batch_size=64, train_size=512, autotune=tiles == "shipped")
-        if tiles == "split":  # f32 and X6S weight gradients, 2..32 slabs
-            for l in range(1, t.layout.L):
-                t.engine.set_tile(l, 2, 64, 64, [2, 32, 16, 8, 5, 3, 4][l - 1], 32 if l % 2 else 64,
-                                  0 if l % 2 else (16 | 4))
-        for _ in range(3):
-            t.step()
-        torch.cuda.synchronize()
-        out.append((t.params.clone(), t.mom.clone(), t.grads.clone(), t.bufs.clone()))
-    for a, b in zip(*out):
-        assert torch.equal(a, b)
-
-
-@pytest.mark.parametrize("keep", ["0", "1"])
-def test_bn_reduce_in_wgrad_launch_bitwise_equal(dev, keep, monkeypatch):
-    # block l-1's BN partial-sum pass appended to block l's weight-gradient launch (extra blocks
-    # after the GEMM tiles) == the standalone reduce launch, bit for bit (also with kept slabs)
-    monkeypatch.setenv("CS_KEEP_SLABS", keep)
-    monkeypatch.setenv("CS_BN_PATH", "0")  # the appended reduce belongs to the three-launch BN path
-    monkeypatch.setenv("CS_BN_EPI_RED", "0")  # (partials out of the dgrad would take precedence)
-    out = []
-    for fuse in ("0", "1"):
-        monkeypatch.setenv("CS_FUSE_BN_RED", fuse)
-        t = _trainer(dev, batch_size=32, train_size=256)
-        for l in range(1, t.layout.L):  # wgrad launches of both block sizes: 1024-thread X6S, 256-thread f32
-            if l % 2:
-                t.engine.set_tile(l, 2, 64, 64, 2, 64, 16 | 4)
-            t.engine.set_tile(l, 1, 64, 64, 2, 16, 0)
-        for _ in range(3):
-            t.step()
-        torch.cuda.synchronize()
-        out.append((t.params.clone(), t.mom.clone(), t.bufs.clone()))
-    for a, b in zip(out[0], out[1]):
         assert torch.equal(a, b)
 
 
@@ -548,12 +439,18 @@ def _force_x6s(tr):
     return n
 
 
-@pytest.mark.parametrize("variant", ["autotuned", "x6s_everywhere", "f32_only"])
+@pytest.mark.parametrize("variant", ["autotuned", "x6s_everywhere", "f32_only", "split", "nosplit", "dual", "separate"])
 def test_bench_config_b64_matches_fp64(dev, variant):
     """The benchmarked configuration (B=64; tuned tiles = 22 of 23 GEMMs on X6S split-bf16
-    maths), every X6S GEMM, and f32-MFMA-only tiles vs the decision-aligned fp64 model: every
-    gradient tensor within 1e-4 relative (max-abs normalised)."""
-    tr = _trainer(dev, batch_size=64, train_size=1024, autotune=variant == "autotuned")
+    maths), every X6S GEMM, f32-MFMA-only tiles, and the tile tables that put the in-launch BN
+    finalize / apply at every site (split-K combines, 64x128 / 128x64 epilogues, dual launches;
+    "separate" = the finalize and apply as launches of their own) vs the decision-aligned fp64
+    model: every gradient tensor within 1e-4 relative (max-abs normalised)."""
+    tr = _trainer(dev, batch_size=64, train_size=1024, autotune=variant in ("autotuned", "separate"))
+    if variant in ("split", "nosplit", "dual"):
+        _set_tiles(tr, variant)
+    if variant == "separate":
+        tr.engine.set_fin(False)
     if variant == "x6s_everywhere":
         assert _force_x6s(tr) == 22
         assert sum(t["math"] == "x6s" for t in tr.tile_table()) == 22
@@ -576,30 +473,13 @@ def test_ragged_batches_match_fp64(dev, B, Bmax):
     assert rel < 1e-5, rel
 
 
-def test_wgrad_side_stream_bitwise_and_graph(dev):
-    """Weight gradients on the side stream (kernel stream links, CS_OVERLAP_WGRAD=1) compute exactly
-    what the serial backward does; a full-step graph of the two-stream step replays it exactly."""
-    runs = []
-    for ovl, graph in ((False, "none"), (True, "none"), (True, "full")):
-        t = _trainer(dev, batch_size=32, train_size=256, graph=graph)
-        t.engine.set_overlap_wgrad(ovl)
-        for _ in range(5):
-            t.step()
-        torch.cuda.synchronize()
-        runs.append((t.params.clone(), t.mom.clone(), t.bufs.clone()))
-        t.close()
-    for r in runs[1:]:
-        for a, b in zip(runs[0], r):
-            assert torch.equal(a, b)
-
-
-def test_wgrad_side_stream_long_run_no_syncs(dev):
-    """30 back-to-back steps (the host far ahead of the GPU, epoch boundary crossed) with the
-    side-stream weight gradients == the serial backward, bit for bit."""
+def test_long_run_no_syncs_deterministic(dev):
+    """30 back-to-back steps (the host far ahead of the GPU, an epoch boundary crossed): two runs
+    bitwise equal (the in-launch finalizes' arrival order changes run to run, their combine order
+    does not), and the in-launch ticket counters are left zeroed."""
     out = []
-    for ovl in (False, True):
+    for _ in range(2):
         t = _trainer(dev, batch_size=32, train_size=640)
-        t.engine.set_overlap_wgrad(ovl)
         for _ in range(30):
             t.step()
         torch.cuda.synchronize()
