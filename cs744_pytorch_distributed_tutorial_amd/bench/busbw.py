@@ -38,6 +38,11 @@ FACTORS = {
     "broadcast": lambda n: 1.0,
 }
 
+def _sig(x: float) -> float:
+    """4 significant digits (a fixed 3-decimal round turns a slow gloo 4 KiB op into 0)."""
+    return float(f"{x:.4g}")
+
+
 VGG11_GRAD_FLOATS = 9_231_114  # SURVEY.md §2.6
 
 
@@ -176,7 +181,7 @@ def main(argv=None) -> int:
         alg = tot / dt / 1e9
         rows.append({"bench": "vgg11_ddp_buckets", "comm": a.comm, "device": device.type, "n": world,
                      "bucket_mb": a.vgg_buckets, "buckets": len(sizes), "bytes": tot, "time_us": round(dt * 1e6, 2),
-                     "algbw_GBps": round(alg, 3), "busbw_GBps": round(alg * FACTORS["all_reduce"](world), 3)})
+                     "algbw_GBps": _sig(alg), "busbw_GBps": _sig(alg * FACTORS["all_reduce"](world))})
     else:
         sizes = [parse_size(s) for s in a.sizes.split(",")] if a.sizes else default_sizes(device.type)
         for s in sizes:
@@ -185,8 +190,8 @@ def main(argv=None) -> int:
             nbytes = run.nbytes
             alg = nbytes / dt / 1e9
             rows.append({"bench": "busbw", "op": a.op, "comm": a.comm, "device": device.type, "n": world,
-                         "bytes": nbytes, "time_us": round(dt * 1e6, 2), "algbw_GBps": round(alg, 3),
-                         "busbw_GBps": round(alg * FACTORS[a.op](world), 3)})
+                         "bytes": nbytes, "time_us": round(dt * 1e6, 2), "algbw_GBps": _sig(alg),
+                         "busbw_GBps": _sig(alg * FACTORS[a.op](world))})
             del run
     if rank == 0:
         for r in rows:

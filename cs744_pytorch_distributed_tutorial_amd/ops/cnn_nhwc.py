@@ -274,9 +274,13 @@ def conv_nhwc(x: torch.Tensor, conv: nn.Conv2d, grad_box: Optional[dict] = None)
         return y.permute(0, 2, 3, 1).contiguous()
     Co, Ci, R, S = conv.weight.shape
     st, pad = int(conv.stride[0]), int(conv.padding[0])
-    if _implicit_ok(act_dtype(x), x.shape[3], Ci, Co, R, S, st, pad):
+    # the implicit kernels address every operand with 32-bit buffer offsets (cs_conv_nhwc rejects
+    # a tensor of 2 GiB or more): larger convs take the batch-chunked im2col path
+    Ho, Wo = (x.shape[1] + 2 * pad - R) // st + 1, (x.shape[2] + 2 * pad - S) // st + 1
+    fits = 2 * max(x.numel(), x.shape[0] * Ho * Wo * Co, Co * R * S * max(Ci, 4)) < 0x7ffffff0
+    if fits and _implicit_ok(act_dtype(x), x.shape[3], Ci, Co, R, S, st, pad):
         return _ConvImplicitNHWC.apply(x.to(torch.bfloat16).contiguous(), conv.weight, st, pad)
-    if _stem_ok(x, Ci, Co, S):
+    if fits and _stem_ok(x, Ci, Co, S):
         return _ConvStemNHWC.apply(x.to(torch.bfloat16).contiguous(), conv.weight, st, pad)
     return _ConvNHWC.apply(x, conv.weight, st, pad, grad_box)
 

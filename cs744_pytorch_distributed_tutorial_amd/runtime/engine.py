@@ -283,6 +283,20 @@ class NativeTrainer:
         self._probe = getattr(self, "_probe", None)
         self.engine = C.VggEngine(self.B, lay.desc(), lay.offs(), lay.buf_offs(), lay.feat, lay.ncls,
                                   self.params, self.grads, self.mom, self.bufs, self.nbt)
+        # weight gradients on the side stream, overlapping the data-gradient / BatchNorm chain (bit-
+        # identical to the serial backward). Off when collectives are issued from Python (gloo copies
+        # each bucket to the host ordered after the main stream only: round 2 measured a stale
+        # gradient without a system-scope release of the side stream), under rocprofv3 counter
+        # collection (it serialises every dispatch: a stream-link wait would spin to its timeout),
+        # and with a communicator but fewer than 8 HIP hardware queues (side, comm and main stream
+        # links stall on a shared queue). CS_OVERLAP_WGRAD=0 forces the serial backward.
+        from .. import hw_queues
+        python_collectives = world > 1 and self.native_comm is None
+        self.overlap_wgrad = (os.environ.get("CS_OVERLAP_WGRAD", "1") != "0" and not python_collectives
+                              and not self._counters and (self.native_comm is None or hw_queues() >= 8))
+        self.engine.set_overlap(self.overlap_wgrad)
+        # in-launch BN finalize (bn_fin.h; CS_BN_FIN=0: the separate finalize launches)
+        self.engine.set_fin(os.environ.get("CS_BN_FIN", "1") != "0")
         self.engine.set_data(0, self.train_data, self.train_labels, self.aug_train)
         self.engine.set_data(1, self.test_data, self.test_labels, self.aug_test)
         self.idx_buf = self.engine.idx()

@@ -96,9 +96,13 @@ class TorchTrainer:
         if self.channels_last:
             self.module = self.module.to(memory_format=torch.channels_last)
         self.dtype = dtype
+        self.grad_comm_dtype = "fp32"
         if world > 1 and sync == "ddp":
-            # decoder LMs all-reduce bf16 gradients by default (CS744_GRAD_COMM_DTYPE=fp32 | bf16)
-            gdt = os.environ.get("CS744_GRAD_COMM_DTYPE", "bf16" if self.is_lm else "fp32")
+            # gradients travel in fp32 like the reference's DDP; CS744_GRAD_COMM_DTYPE=bf16 halves the
+            # all-reduce bytes for the decoder LMs (opt-in: RCCL then sums in bf16 over N ranks, a
+            # rounding per hop that no reference fixture pins)
+            gdt = os.environ.get("CS744_GRAD_COMM_DTYPE", "fp32")
+            self.grad_comm_dtype = gdt
             self.net = DistributedDataParallel(self.module, comm=make_comm(comm), bucket_cap_mb=bucket_mb,
                                                bucket_policy=bucket_policy,
                                                grad_comm_dtype=torch.bfloat16 if gdt == "bf16" else None)

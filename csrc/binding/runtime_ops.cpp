@@ -43,8 +43,8 @@ void check_gpu(const torch::Tensor& t, const char* name) {
 
 void register_runtime(pybind11::module& m) {
   m.def("reserve_streams", &cs::reserve_streams,
-        "create (once per process) the native communicator's stream and bind it to a hardware queue; call "
-        "it before other code creates streams");
+        "create (once per process) the native engine's side stream and the communicator's stream and bind "
+        "each to a hardware queue; call it before other code creates streams");
   namespace py = pybind11;
   m.def("rccl_unique_id", []() { return py::bytes(cs::RcclComm::unique_id()); });
   m.def("rccl_version", []() {
@@ -174,7 +174,8 @@ void register_runtime(pybind11::module& m) {
       .def("num_blocks", &cs::VggEngine::num_blocks)
       .def("tensor", &cs::VggEngine::tensor)
       .def("forward_train", &cs::VggEngine::forward_train)
-      .def("backward", &cs::VggEngine::backward, py::arg("hi"), py::arg("lo"), py::arg("B"))
+      .def("backward", &cs::VggEngine::backward, py::arg("hi"), py::arg("lo"), py::arg("B"), py::arg("join") = true)
+      .def("set_overlap", &cs::VggEngine::set_overlap)
       .def("sgd", &cs::VggEngine::sgd)
       .def("forward_eval", &cs::VggEngine::forward_eval)
       .def("step", &cs::VggEngine::step, py::arg("B"), py::arg("comm").none(true), py::arg("bucket_blocks"),

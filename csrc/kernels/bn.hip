@@ -206,8 +206,12 @@ __global__ __launch_bounds__(256) void bn_bwd_kernel(const float* __restrict__ y
                                                      const float* __restrict__ shift, const float* __restrict__ mean,
                                                      const float* __restrict__ invstd, const float* __restrict__ coef,
                                                      float* __restrict__ dz, float* __restrict__ part, int gslabs,
-                                                     int64_t gstride) {
+                                                     int64_t gstride, unsigned long long* __restrict__ signal) {
   extern __shared__ __attribute__((aligned(16))) float red[];  // [rows][C][3] (reduce only)
+  // a deferred stream-link signal (device_comm.h StreamLink::defer): this launch started, so the
+  // kernels before it on the stream completed
+  if (signal != nullptr && blockIdx.x == 0 && threadIdx.x == 0)
+    __hip_atomic_fetch_add(signal, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if constexpr (!APPLY) {  // the shared body (also run inside weight-gradient GEMM launches)
     const CsBnRed r{y, G, scale, shift, mean, invstd, part, gstride, B, H, W, C, POOL ? 1 : 0, (int)gridDim.x, gslabs};
     cs_bn::bn_red_body<POOL>(r, blockIdx.x, gridDim.x, red);
@@ -571,10 +575,10 @@ hipError_t cs_bn_bwd(const float* y, const float* G, int B, int H, int W, int C,
   const size_t lds = (size_t)rows * C * 3 * sizeof(float);
   if (pool) {
     hipLaunchKernelGGL((bn_bwd_kernel<false, true>), dim3(P), dim3(256), lds, stream, y, G, B, H, W, C, scale, shift,
-                       mean, invstd, nullptr, nullptr, part, gslabs, gstride);
+                       mean, invstd, nullptr, nullptr, part, gslabs, gstride, nullptr);
   } else {
     hipLaunchKernelGGL((bn_bwd_kernel<false, false>), dim3(P), dim3(256), lds, stream, y, G, B, H, W, C, scale, shift,
-                       mean, invstd, nullptr, nullptr, part, gslabs, gstride);
+                       mean, invstd, nullptr, nullptr, part, gslabs, gstride, nullptr);
   }
   if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
   return cs_bn_bwd_tail(y, G, B, H, W, C, pool, scale, shift, mean, invstd, gamma, part, P, coef, dgamma, dbeta,
@@ -596,17 +600,17 @@ hipError_t cs_bn_bwd_tail(const float* y, const float* G, int B, int H, int W, i
   if (blocks > 2048) blocks = 2048;
   if (pool) {
     hipLaunchKernelGGL((bn_bwd_kernel<true, true>), dim3(blocks), dim3(256), 0, stream, y, G, B, H, W, C, scale, shift,
-                       mean, invstd, coef, dz, nullptr, gslabs, gstride);
+                       mean, invstd, coef, dz, nullptr, gslabs, gstride, nullptr);
   } else {
     hipLaunchKernelGGL((bn_bwd_kernel<true, false>), dim3(blocks), dim3(256), 0, stream, y, G, B, H, W, C, scale,
-                       shift, mean, invstd, coef, dz, nullptr, gslabs, gstride);
+                       shift, mean, invstd, coef, dz, nullptr, gslabs, gstride, nullptr);
   }
   return hipGetLastError();
 }
 
 hipError_t cs_bn_bwd_apply(const float* y, const float* G, int B, int H, int W, int C, int pool, const float* scale,
                            const float* shift, const float* mean, const float* invstd, const float* coef, float* dz,
-                           hipStream_t stream) {
+                           hipStream_t stream, unsigned long long* signal) {
   if (C % 4 != 0 || C > 1024 || (pool && ((H | W) & 1))) return hipErrorInvalidValue;
   const int rows = 256 / (C / 4);
   const int units = pool ? B * (H / 2) * (W / 2) : B * H * W;
@@ -614,10 +618,10 @@ hipError_t cs_bn_bwd_apply(const float* y, const float* G, int B, int H, int W, 
   if (blocks > 2048) blocks = 2048;
   if (pool)
     hipLaunchKernelGGL((bn_bwd_kernel<true, true>), dim3(blocks), dim3(256), 0, stream, y, G, B, H, W, C, scale, shift,
-                       mean, invstd, coef, dz, nullptr, 1, (int64_t)0);
+                       mean, invstd, coef, dz, nullptr, 1, (int64_t)0, signal);
   else
     hipLaunchKernelGGL((bn_bwd_kernel<true, false>), dim3(blocks), dim3(256), 0, stream, y, G, B, H, W, C, scale,
-                       shift, mean, invstd, coef, dz, nullptr, 1, (int64_t)0);
+                       shift, mean, invstd, coef, dz, nullptr, 1, (int64_t)0, signal);
   return hipGetLastError();
 }
 

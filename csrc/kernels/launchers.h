@@ -37,7 +37,9 @@ hipError_t cs_sgd_multi(const CsTensorEntry* tab_dev, int ntens, const int64_t* 
 // classifier head
 hipError_t cs_linear_xent(const float* feat, const float* W, const float* bias, const int64_t* labels, int B, int K,
                           int C, float gscale, float* loss_out, int* correct_out, float* logits_out, float* dW,
-                          float* db, float* dfeat, int64_t* pred_out, float* ws, hipStream_t stream);
+                          float* db, float* dfeat, int64_t* pred_out, float* ws, hipStream_t stream, int part = 0);
+// part: 0 both launches; 1 the per-row pass (logits, prediction, dlogits -> ws, dfeat); 2 the
+// per-column pass (dW, db, loss, correct count from ws and feat) — run after part 1 (ws)
 inline int64_t cs_linear_xent_ws(int B, int C) { return (int64_t)B * (C + 2); }
 hipError_t cs_softmax_xent(const float* logits, const int64_t* labels, int B, int C, float gscale, float* loss_out,
                            float* dlogits, int* correct_out, hipStream_t stream);
@@ -201,7 +203,7 @@ hipError_t cs_bn_fused_bwd(const float* y, const float* G, int B, int H, int W, 
 // ran as the last-arriver tail of the data-gradient launch that produced G (CsConvArgs::fin)
 hipError_t cs_bn_bwd_apply(const float* y, const float* G, int B, int H, int W, int C, int pool, const float* scale,
                            const float* shift, const float* mean, const float* invstd, const float* coef, float* dz,
-                           hipStream_t stream);
+                           hipStream_t stream, unsigned long long* signal = nullptr);
 
 // ---------------------------------------------------------------- ordering-probe communicator (comm_probe.hip)
 enum { CS_SCRAMBLE_F32 = 0, CS_SCRAMBLE_I64 = 1, CS_SCRAMBLE_I32 = 2 };

@@ -261,15 +261,18 @@ __global__ __launch_bounds__(kThreads) void softmax_xent_kernel(const float* __r
 
 hipError_t cs_linear_xent(const float* feat, const float* W, const float* bias, const int64_t* labels, int B, int K,
                           int C, float gscale, float* loss_out, int* correct_out, float* logits_out, float* dW,
-                          float* db, float* dfeat, int64_t* pred_out, float* ws, hipStream_t stream) {
-  if (C > kMaxC || C < 1 || B <= 0 || (K & 3) != 0 || ws == nullptr) return hipErrorInvalidValue;
+                          float* db, float* dfeat, int64_t* pred_out, float* ws, hipStream_t stream, int part) {
+  if (C > kMaxC || C < 1 || B <= 0 || (K & 3) != 0 || ws == nullptr || part < 0 || part > 2) return hipErrorInvalidValue;
+  if (part == 2) goto cols;
   if (C == 10)
     hipLaunchKernelGGL(head_rows_kernel<10>, dim3((B + 3) / 4), dim3(256), 0, stream, feat, W, bias, labels, B, K, C,
                        gscale, ws, logits_out, pred_out, dfeat);
   else
     hipLaunchKernelGGL(head_rows_kernel<0>, dim3((B + 3) / 4), dim3(256), 0, stream, feat, W, bias, labels, B, K, C,
                        gscale, ws, logits_out, pred_out, dfeat);
-  const bool bwd = dW != nullptr && db != nullptr && dfeat != nullptr;
+  if (part == 1) return hipGetLastError();
+cols:
+  const bool bwd = dW != nullptr && db != nullptr && (dfeat != nullptr || part == 2);
   hipLaunchKernelGGL(head_cols_kernel, dim3(bwd ? C * ((K + 63) / 64) + 1 : 1), dim3(64), 0, stream, feat, B, K, C, ws,
                      bwd ? dW : nullptr, bwd ? db : nullptr, loss_out, correct_out);
   return hipGetLastError();

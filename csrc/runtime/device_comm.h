@@ -59,6 +59,9 @@ bool stream_capturing(hipStream_t s);
 // with 8-40 busy streams created first). reserve_streams() creates it now: call it before
 // anything else creates streams (NativeTrainer and bench.py do).
 hipStream_t reserved_comm_stream();
+// the engine's side stream (weight gradients + their SGD, VggEngine overlap), lowest priority,
+// reserved the same way
+hipStream_t reserved_side_stream();
 void reserve_streams();
 
 // One-direction kernel stream link (stream_link.hip): signal(producer) enqueues a one-lane
@@ -81,6 +84,10 @@ class StreamLink {
   StreamLink(const StreamLink&) = delete;
   StreamLink& operator=(const StreamLink&) = delete;
   void signal(hipStream_t producer);
+  // signal folded into the NEXT kernel launched on the producer stream: returns the counter that
+  // kernel must bump (once, at its start: it starts only after everything before it on that
+  // stream completed — the same edge as a signal launch, without a launch of its own)
+  unsigned long long* defer();
   void wait(hipStream_t consumer);
   std::string error() const;
 

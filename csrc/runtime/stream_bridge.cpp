@@ -61,6 +61,11 @@ void StreamLink::signal(hipStream_t producer) {
   ++pending_;
 }
 
+unsigned long long* StreamLink::defer() {
+  ++pending_;
+  return dev_;
+}
+
 void StreamLink::wait(hipStream_t consumer) {
   if (pending_ == 0) return;  // nothing signalled since the last wait
   hip_ok(cs_link_wait(dev_, dev_ + 1, err_, abort_word(), g_link_timeout, consumer, pending_), "link wait");
@@ -98,7 +103,15 @@ hipStream_t reserved_comm_stream() {
   return comm;
 }
 
-void reserve_streams() { (void)reserved_comm_stream(); }
+hipStream_t reserved_side_stream() {
+  static hipStream_t side = bound_stream(false);
+  return side;
+}
+
+void reserve_streams() {
+  (void)reserved_side_stream();
+  (void)reserved_comm_stream();
+}
 
 bool stream_capturing(hipStream_t s) {
   hipStreamCaptureStatus st = hipStreamCaptureStatusNone;

@@ -166,6 +166,7 @@ VggEngine::VggEngine(int64_t Bmax, std::vector<int64_t> desc, std::vector<int64_
   logits_ = torch::zeros({Bmax, ncls}, fo);
   gbuf_[0] = torch::zeros({gmax}, fo);
   gbuf_[1] = torch::zeros({gmax}, fo);
+  feats_ = torch::zeros({Bmax * feat}, fo);
   dz_[0] = torch::zeros({dzmax}, fo);
   dz_[1] = torch::zeros({dzmax}, fo);
   ws_elems_ = kWsElems;
@@ -174,6 +175,11 @@ VggEngine::VggEngine(int64_t Bmax, std::vector<int64_t> desc, std::vector<int64_
   // zeroed once; every in-launch finalize leaves its tickets zeroed (bn_fin.h)
   fin_cnt_ = torch::zeros({std::max<int64_t>(fin_ints, 1)}, fo.dtype(at::kInt));
   fin_grp_ = torch::zeros({grpmax}, fo);
+  side_ = reserved_side_stream();  // process-wide, created early (device_comm.h)
+  dz_link_ = std::make_unique<StreamLink>();
+  wg_link_ = std::make_unique<StreamLink>();
+  for (const VggBlock& b : blocks_) dz_blk_.push_back(torch::zeros({Bmax * b.H * b.H * b.cout}, fo));
+  if (const char* e = getenv("CS_OVERLAP_WGRAD")) overlap_ = atoi(e) != 0;
   // per-block parameter ranges for the per-block SGD: the backward-ready layout puts fc first,
   // then blocks L-1..0, each {w, bias, gamma, beta} inside [w_off, next block's w_off)
   {
@@ -380,12 +386,26 @@ CsBnFin VggEngine::fin_bwd_args(int l, int B) {
   return f;
 }
 
+bool VggEngine::side_ok(hipStream_t s) const { return overlap_ && side_ != nullptr && !stream_capturing(s); }
+
+void VggEngine::flush_signal(hipStream_t s) {
+  if (pending_sig_ == nullptr) return;
+  ok(cs_link_signal(pending_sig_, s), "link signal");
+  pending_sig_ = nullptr;
+}
+
+void VggEngine::join_side(hipStream_t s) {
+  flush_signal(s);  // the side stream may be waiting for it: never wait on side before it is out
+  wg_link_->wait(s);
+}
+
 void VggEngine::forward_train(int64_t B) {
   TORCH_CHECK(B > 0 && B <= Bmax_, "forward_train: 0 < B <= Bmax");
   TORCH_CHECK(data_[0].defined(), "forward_train: set_data(0, ...) first");
   hipStream_t s = cur_stream();
   const int L = (int)blocks_.size();
   red_pending_ = -1;
+  flush_signal(s);
   // one launch: sampler index (device cursor into the epoch permutation, or idx_ when no
   // permutation is set), label gather, crop/flip/normalize into block 0's NHWC input
   const bool use_perm = perm_len_ > 0;
@@ -400,7 +420,7 @@ void VggEngine::forward_train(int64_t B) {
     VggBlock& b = blocks_[l];
     const ConvTile& t = b.tile[CS_CONV_FWD];
     float* bn = b.bn.data_ptr<float>();
-    float* out = (l + 1 < L) ? blocks_[l + 1].x.data_ptr<float>() : gbuf_[1].data_ptr<float>();
+    float* out = (l + 1 < L) ? blocks_[l + 1].x.data_ptr<float>() : feats_.data_ptr<float>();
     if (fin_on_) {
       // conv [+ split-K combine]: its last-arriving block finalizes the batch statistics
       const CsBnFin f = fin_fwd_args(l, (int)B);
@@ -416,40 +436,59 @@ void VggEngine::forward_train(int64_t B) {
     }
     ok(cs_bn_apply(b.y.data_ptr<float>(), bn, bn + b.cout, out, (int)B, b.H, b.H, b.cout, b.pool, s), "bn_apply");
   }
-  // features of the last block were staged in gbuf_[1] (free until the first dgrad); dfeat -> gbuf_[0]
-  ok(cs_linear_xent(gbuf_[1].data_ptr<float>(), P(fc_w_), P(fc_b_), ylab_.data_ptr<int64_t>(), (int)B, (int)feat_,
+  // classifier + loss: dfeat -> gbuf_[0]. Inside the overlapped step the per-column pass (dW, db,
+  // loss, accuracy: only the SGD and the host read them) forks to the side stream, off the
+  // critical chain that continues with dfeat (the top block's BN backward)
+  const bool fork = in_step_ && side_ok(s);
+  ok(cs_linear_xent(feats_.data_ptr<float>(), P(fc_w_), P(fc_b_), ylab_.data_ptr<int64_t>(), (int)B, (int)feat_,
                     (int)ncls_, 1.0f, loss_.data_ptr<float>(), correct_.data_ptr<int>(), logits_.data_ptr<float>(),
-                    G(fc_w_), G(fc_b_), gbuf_[0].data_ptr<float>(), pred_.data_ptr<int64_t>(), head_ws_.data_ptr<float>(), s),
+                    G(fc_w_), G(fc_b_), gbuf_[0].data_ptr<float>(), pred_.data_ptr<int64_t>(), head_ws_.data_ptr<float>(), s,
+                    fork ? 1 : 0),
      "linear_xent");
+  if (fork) {
+    pending_sig_ = dz_link_->defer();  // rides the top block's BN backward launch
+    dz_link_->wait(side_);
+    ok(cs_linear_xent(feats_.data_ptr<float>(), P(fc_w_), P(fc_b_), ylab_.data_ptr<int64_t>(), (int)B, (int)feat_,
+                      (int)ncls_, 1.0f, loss_.data_ptr<float>(), correct_.data_ptr<int>(), logits_.data_ptr<float>(),
+                      G(fc_w_), G(fc_b_), nullptr, pred_.data_ptr<int64_t>(), head_ws_.data_ptr<float>(), side_, 2),
+       "linear_xent(cols)");
+    wg_link_->signal(side_);
+  }
 }
 
-void VggEngine::backward(int64_t hi, int64_t lo, int64_t B) {
+void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
   const int L = (int)blocks_.size();
   TORCH_CHECK(0 <= lo && lo <= hi && hi < L, "backward: need 0 <= lo <= hi < num_blocks");
   TORCH_CHECK(B > 0 && B <= Bmax_, "backward: 0 < B <= Bmax");
   hipStream_t s = cur_stream();
+  const bool ovl = side_ok(s);
   for (int l = (int)hi; l >= (int)lo; --l) {
     VggBlock& b = blocks_[l];
     float* bn = b.bn.data_ptr<float>();
-    float* dz = dz_[l & 1].data_ptr<float>();
+    // overlapped: every block has its own dz buffer (no WAR wait on a side wgrad still reading it)
+    float* dz = ovl ? dz_blk_[l].data_ptr<float>() : dz_[l & 1].data_ptr<float>();
     const float* Gin = gbuf_[(L - 1 - l) % 2].data_ptr<float>();
-    // ---- BN (+ReLU, +pool) backward of block l -> dz
+    // ---- BN (+ReLU, +pool) backward of block l -> dz (the deferred side-stream signal of block
+    // l+1's fork rides its first launch)
     if (red_pending_ == l) {
       // the partial sums (and, with fin, the finalize) ran inside block l+1's data-gradient launch
       if (fin_on_)
         ok(cs_bn_bwd_apply(b.y.data_ptr<float>(), Gin, (int)B, b.H, b.H, b.cout, b.pool, bn, bn + b.cout,
-                           bn + 2 * b.cout, bn + 3 * b.cout, bn_coef_.data_ptr<float>(), dz, s),
+                           bn + 2 * b.cout, bn + 3 * b.cout, bn_coef_.data_ptr<float>(), dz, s, pending_sig_),
            "bn_bwd_apply");
       else
         ok(cs_bn_bwd_tail(b.y.data_ptr<float>(), Gin, (int)B, b.H, b.H, b.cout, b.pool, bn, bn + b.cout,
                           bn + 2 * b.cout, bn + 3 * b.cout, P(b.g_off), bn_part_.data_ptr<float>(), red_P_,
-                          bn_coef_.data_ptr<float>(), G(b.g_off), G(b.be_off), G(b.b_off), dz, s),
+                          bn_coef_.data_ptr<float>(), G(b.g_off), G(b.be_off), G(b.b_off), dz, s, 1, 0, pending_sig_),
            "bn_bwd_tail");
+      pending_sig_ = nullptr;
     } else if (bn_fused(l, B)) {  // reduce + finalize + apply in one launch (the top block)
       ok(cs_bn_fused_bwd(b.y.data_ptr<float>(), Gin, (int)B, b.H, b.H, b.cout, b.pool, bn, P(b.g_off),
-                         bn_coef_.data_ptr<float>(), G(b.g_off), G(b.be_off), G(b.b_off), dz, s),
+                         bn_coef_.data_ptr<float>(), G(b.g_off), G(b.be_off), G(b.b_off), dz, s, 1, 0, pending_sig_),
          "bn_fused_bwd");
+      pending_sig_ = nullptr;
     } else {
+      flush_signal(s);
       ok(cs_bn_bwd(b.y.data_ptr<float>(), Gin, (int)B, b.H, b.H, b.cout, b.pool, bn, bn + b.cout,
                    bn + 2 * b.cout, bn + 3 * b.cout, P(b.g_off), bn_part_.data_ptr<float>(),
                    bn_coef_.data_ptr<float>(), G(b.g_off), G(b.be_off), G(b.b_off), dz, s),
@@ -466,7 +505,25 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B) {
       if (fin_on_) fin = fin_bwd_args(l, (int)B);
     }
     const CsBnFin* fp = er && fin_on_ ? &fin : nullptr;
-    if (dual_ok(l)) {  // wgrad + dgrad in one launch (no appended SGD blocks: the update runs first)
+    if (ovl) {
+      if (l > 0) {
+        // the data gradient keeps the whole chip on the critical chain; the weight gradient forks
+        // to the side stream after it and fills the chip while the main stream runs the
+        // latency-bound BN kernels (and the split-K combine) of the block below
+        conv(l, CS_CONV_DGRAD, (int)B, b.tile[CS_CONV_DGRAD], s, false, nullptr, dz, &erv, nullptr, fp);
+        pending_sig_ = dz_link_->defer();
+        dz_link_->wait(side_);
+        conv(l, CS_CONV_WGRAD, (int)B, b.tile[CS_CONV_WGRAD], side_, false, ws_w_.data_ptr<float>(), dz);
+        // block l's dgrad (the last reader of its weights) and BN backward ran before the fork
+        if (bwd_sgd_) sgd_on(side_, blk_range_[l].first, blk_range_[l].second, false);
+        wg_link_->signal(side_);
+      } else {
+        // block 0's weight gradient is the step's last GEMM: nothing left to overlap it with, so it
+        // runs here (the main split-K workspace is free: no data gradient for block 0)
+        conv(l, CS_CONV_WGRAD, (int)B, b.tile[CS_CONV_WGRAD], s, false, ws_.data_ptr<float>(), dz);
+        if (bwd_sgd_) sgd_on(s, blk_range_[0].first, blk_range_[0].second, true);
+      }
+    } else if (dual_ok(l)) {  // wgrad + dgrad in one launch (no appended SGD blocks: the update runs first)
       if (sgd_tail_ && l + 1 < L) sgd_on(s, blk_range_[l + 1].first, blk_range_[l + 1].second, false);
       conv_dual(l, (int)B, s, dz, &erv, fp);
     } else {
@@ -484,6 +541,10 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B) {
       red_pending_ = l - 1;
       red_P_ = erv.P;
     }
+  }
+  if (join) {
+    flush_signal(s);
+    if (ovl) join_side(s);
   }
 }
 
@@ -578,10 +639,10 @@ void VggEngine::forward_eval(int64_t B) {
     conv(l, CS_CONV_FWD, (int)B, b.tile[CS_CONV_FWD], s, false);
     ok(cs_bn_eval_coeffs(P(b.g_off), P(b.be_off), bufs + b.rm_off, bufs + b.rv_off, b.cout, kBnEps, sc, sh, s),
        "bn_eval_coeffs");
-    float* out = (l + 1 < L) ? blocks_[l + 1].x.data_ptr<float>() : gbuf_[1].data_ptr<float>();
+    float* out = (l + 1 < L) ? blocks_[l + 1].x.data_ptr<float>() : feats_.data_ptr<float>();
     ok(cs_bn_apply(b.y.data_ptr<float>(), sc, sh, out, (int)B, b.H, b.H, b.cout, b.pool, s), "bn_apply");
   }
-  ok(cs_linear_xent(gbuf_[1].data_ptr<float>(), P(fc_w_), P(fc_b_), ylab_.data_ptr<int64_t>(), (int)B, (int)feat_,
+  ok(cs_linear_xent(feats_.data_ptr<float>(), P(fc_w_), P(fc_b_), ylab_.data_ptr<int64_t>(), (int)B, (int)feat_,
                     (int)ncls_, 1.0f, loss_.data_ptr<float>(), correct_.data_ptr<int>(), logits_.data_ptr<float>(),
                     nullptr, nullptr, nullptr, pred_.data_ptr<int64_t>(), head_ws_.data_ptr<float>(), s),
      "linear_xent");
@@ -590,6 +651,23 @@ void VggEngine::forward_eval(int64_t B) {
 void VggEngine::step(int64_t B, DeviceComm* comm, const std::vector<int64_t>& bucket_blocks,
                      const std::vector<int64_t>& bucket_ranges, bool broadcast_buffers, double lr, double momentum,
                      double wd, double dampening) {
+  try {
+    step_impl(B, comm, bucket_blocks, bucket_ranges, broadcast_buffers, lr, momentum, wd, dampening);
+  } catch (...) {
+    // a launch failed with a deferred link signal pending: bump it now, so the side stream's wait
+    // does not spin to the link timeout behind a kernel that will never run
+    if (pending_sig_ != nullptr) {
+      (void)cs_link_signal(pending_sig_, cur_stream());
+      pending_sig_ = nullptr;
+    }
+    in_step_ = false;
+    throw;
+  }
+}
+
+void VggEngine::step_impl(int64_t B, DeviceComm* comm, const std::vector<int64_t>& bucket_blocks,
+                          const std::vector<int64_t>& bucket_ranges, bool broadcast_buffers, double lr,
+                          double momentum, double wd, double dampening) {
   const int64_t L = (int64_t)blocks_.size();
   const size_t nb = bucket_blocks.size();
   TORCH_CHECK(nb >= 1 && bucket_ranges.size() == 2 * nb && bucket_blocks.back() == 0, "step: bucket plan");
@@ -600,6 +678,7 @@ void VggEngine::step(int64_t B, DeviceComm* comm, const std::vector<int64_t>& bu
   tn_ = 0;
   Range step_range("cs.step");
   mark("start");
+  in_step_ = true;
   {
     Range r("cs.forward");
     forward_train(B);
@@ -618,8 +697,12 @@ void VggEngine::step(int64_t B, DeviceComm* comm, const std::vector<int64_t>& bu
     at += bucket_ranges[2 * k + 1];
     if (k + 1 == nb) comm_sgd = comm_sgd && (int64_t)at == params_.numel();
   }
-  // world 1: block l+1's SGD rides block l's weight-gradient launch
-  sgd_tail_ = sgd_tail_on_ && !dp && !blk_range_.empty();
+  // world 1: overlapped — block l's SGD right behind its weight gradient on the side stream (block
+  // 0's, with the batch cursor, on this stream); serial — block l+1's SGD rides block l's
+  // weight-gradient launch
+  const bool ovl = side_ok(s);
+  bwd_sgd_ = ovl && !dp && !blk_range_.empty();
+  sgd_tail_ = !ovl && sgd_tail_on_ && !dp && !blk_range_.empty();
   int64_t hi = L - 1;
   for (size_t k = 0; k < nb; ++k) {
     const int64_t lo = bucket_blocks[k];
@@ -628,7 +711,7 @@ void VggEngine::step(int64_t B, DeviceComm* comm, const std::vector<int64_t>& bu
                                   "cs.backward.bucket3", "cs.backward.bucket4", "cs.backward.bucket5",
                                   "cs.backward.bucket6", "cs.backward.bucket7"};
     Range bwd_range(k < 8 ? kBwdR[k] : "cs.backward.bucket8+");
-    backward(hi, lo, B);
+    backward(hi, lo, B, /*join=*/false);
     bwd_range.end();
     static const char* kBwd[] = {"backward_bucket0", "backward_bucket1", "backward_bucket2", "backward_bucket3",
                                  "backward_bucket4", "backward_bucket5", "backward_bucket6", "backward_bucket7"};
@@ -636,9 +719,20 @@ void VggEngine::step(int64_t B, DeviceComm* comm, const std::vector<int64_t>& bu
     hi = lo - 1;
     if (!dp) continue;
     {
-      // the bucket is complete: its all-reduce forks from here and overlaps the rest of the backward
+      // the bucket is complete once its last weight gradient is: the all-reduce forks from there
+      // (the side stream when overlapped; the bucket holding block 0, whose weight gradient ran on
+      // this stream, joins the side stream first) and overlaps the rest of the backward
       Range r("cs.allreduce.enqueue");
-      comm->all_reduce(G(bucket_ranges[2 * k]), bucket_ranges[2 * k + 1], ncclFloat32, ncclAvg, s,
+      hipStream_t src = s;
+      if (ovl && lo == 0) {
+        join_side(s);
+      } else if (ovl) {
+        src = side_;
+        // a host-blocking communicator (staged) runs the collective inside this call: the deferred
+        // signal its fork waits behind must be out first
+        if (comm->host_blocking()) flush_signal(s);
+      }
+      comm->all_reduce(G(bucket_ranges[2 * k]), bucket_ranges[2 * k + 1], ncclFloat32, ncclAvg, src,
                        /*fork=*/!(debug_skip_ & 2));
     }
     if (broadcast_buffers && k == 0) {
@@ -653,6 +747,8 @@ void VggEngine::step(int64_t B, DeviceComm* comm, const std::vector<int64_t>& bu
   }
   {
     Range r("cs.comm.join");
+    flush_signal(s);
+    if (ovl) join_side(s);
     if (dp && !(debug_skip_ & 1)) comm->join(s);
   }
   mark("allreduce_wait");
@@ -661,11 +757,13 @@ void VggEngine::step(int64_t B, DeviceComm* comm, const std::vector<int64_t>& bu
     if (sgd_tail_) {
       // blocks 1.. rode the weight-gradient launches; block 0 (+ the cursor) here
       sgd_on(s, blk_range_[0].first, blk_range_[0].second, true);
-    } else if (!comm_sgd) {
+    } else if (!comm_sgd && !bwd_sgd_) {
       sgd(lr, momentum, wd, dampening, 0, params_.numel());
     }
     sgd_first_ = false;
     sgd_tail_ = false;
+    bwd_sgd_ = false;
+    in_step_ = false;
   }
   mark("sgd");
 }

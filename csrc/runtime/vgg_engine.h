@@ -77,8 +77,14 @@ class VggEngine {
 
   // augment + conv/BN/ReLU/pool chain + fused linear/xent fwd+bwd (train) for B <= Bmax samples
   void forward_train(int64_t B);
-  // backward of blocks hi..lo (inclusive, hi >= lo), writing their gradients into `grads`
-  void backward(int64_t hi, int64_t lo, int64_t B);
+  // backward of blocks hi..lo (inclusive, hi >= lo), writing their gradients into `grads`.
+  // Overlapped (default, not while a graph is captured): block l's weight gradient runs on the
+  // side stream once block l's data gradient is done, beside the BN backward and data gradient
+  // of the blocks below on the caller's stream; join = true makes the caller's stream wait for
+  // the side stream before returning.
+  void backward(int64_t hi, int64_t lo, int64_t B, bool join = true);
+  // weight gradients on the side stream (default on); off = the serial backward
+  void set_overlap(bool on) { overlap_ = on; }
   // SGD (momentum, weight decay, dampening) on [off, off+n) of the flat buffers
   void sgd(double lr, double momentum, double wd, double dampening, int64_t off, int64_t n);
   void set_dual(bool on) { dual_ = on; }
@@ -113,6 +119,10 @@ class VggEngine {
   void step(int64_t B, DeviceComm* comm, const std::vector<int64_t>& bucket_blocks,
             const std::vector<int64_t>& bucket_ranges, bool broadcast_buffers, double lr, double momentum,
             double wd, double dampening);
+
+  void step_impl(int64_t B, DeviceComm* comm, const std::vector<int64_t>& bucket_blocks,
+                 const std::vector<int64_t>& bucket_ranges, bool broadcast_buffers, double lr, double momentum,
+                 double wd, double dampening);
 
   // Phase timing (opt-in): timing events on the compute stream at the step's phase
   // boundaries (forward, each gradient bucket's backward, waiting for the all-reduces, SGD);
@@ -151,6 +161,21 @@ class VggEngine {
   CsBnFin fin_bwd_args(int l, int B);  // block l-1's finalize, carried by block l's data gradient
   int red_pending_ = -1;  // block whose BN-backward partials (fin: coefficients) are already in place
   int red_P_ = 0;         // ... as red_P_ row-tile partials (bn_part_; the separate finalize reads them)
+  // ---- side-stream weight gradients (overlap_): kernel stream links (device_comm.h) main -> side
+  // "dz(l) ready" and side -> main "weight gradients done", one dz buffer per block (the side
+  // stream may still read dz(l) while the main stream writes dz(l-2)); the main -> side signal
+  // rides the next main-stream launch (StreamLink::defer) instead of a launch of its own
+  bool overlap_ = true;
+  hipStream_t side_ = nullptr;
+  std::unique_ptr<StreamLink> dz_link_, wg_link_;
+  std::vector<torch::Tensor> dz_blk_;
+  unsigned long long* pending_sig_ = nullptr;
+  bool bwd_sgd_ = false;  // set by step() (world 1, overlapped): block l's SGD behind its wgrad on the side stream
+  bool in_step_ = false;  // inside step(): the head's per-column pass forks to the side stream
+  torch::Tensor feats_;   // [Bmax, feat]: the last block's output, the classifier's input
+  bool side_ok(hipStream_t s) const;  // overlap on and `s` not capturing a graph
+  void flush_signal(hipStream_t s);   // launch a pending deferred signal as its own kernel
+  void join_side(hipStream_t s);      // `s` waits for every side-stream kernel enqueued so far
   float* P(int64_t off) { return params_.data_ptr<float>() + off; }
   float* G(int64_t off) { return grads_.data_ptr<float>() + off; }
   int64_t Bmax_, feat_, ncls_;

@@ -473,17 +473,38 @@ def test_ragged_batches_match_fp64(dev, B, Bmax):
     assert rel < 1e-5, rel
 
 
+def test_side_stream_wgrad_bitwise_and_graph(dev):
+    """Weight gradients on the side stream (the default: kernel stream links, per-block SGD behind
+    each weight gradient) compute exactly what the serial backward does (SGD in the weight-gradient
+    tails); a full-step graph (captured: serial) replays the same bits."""
+    runs = []
+    for ovl, graph in ((False, "none"), (True, "none"), (True, "full")):
+        t = _trainer(dev, batch_size=32, train_size=256, graph=graph)
+        t.engine.set_overlap(ovl)
+        for _ in range(5):
+            t.step()
+        torch.cuda.synchronize()
+        t.check_comm()
+        runs.append((t.params.clone(), t.mom.clone(), t.bufs.clone(), t.engine.cursor().clone()))
+        t.close()
+    for r in runs[1:]:
+        for a, b in zip(runs[0], r):
+            assert torch.equal(a, b)
+
+
 def test_long_run_no_syncs_deterministic(dev):
-    """30 back-to-back steps (the host far ahead of the GPU, an epoch boundary crossed): two runs
-    bitwise equal (the in-launch finalizes' arrival order changes run to run, their combine order
-    does not), and the in-launch ticket counters are left zeroed."""
+    """30 back-to-back steps (the host far ahead of the GPU, an epoch boundary crossed): side-stream
+    weight gradients == the serial backward, bit for bit, run to run (the in-launch finalizes'
+    arrival order changes, their combine order does not; the tickets stay zeroed)."""
     out = []
-    for _ in range(2):
+    for ovl in (False, True, True):
         t = _trainer(dev, batch_size=32, train_size=640)
+        t.engine.set_overlap(ovl)
         for _ in range(30):
             t.step()
         torch.cuda.synchronize()
         out.append((t.params.clone(), t.mom.clone(), t.bufs.clone()))
         t.close()
-    for a, b in zip(*out):
-        assert torch.equal(a, b)
+    for r in out[1:]:
+        for a, b in zip(out[0], r):
+            assert torch.equal(a, b)
