@@ -7,6 +7,8 @@ multi-process gloo tests).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import native
@@ -107,6 +109,23 @@ def rope(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
 
 
 # ------------------------------------------------------------------ bf16 projections with fp32 masters
+# "native": the gfx950 matrix-core GEMM of csrc/kernels/gemm_bf16.hip runs all three products of a
+# projection (y = x W^T, dx = dy W, dW = dy^T x, the last two reading the operands transposed in
+# LDS, no copies); "blas": torch.mm (hipBLASLt). scripts/gemm_bench.py compares them per shape.
+_GEMM = os.environ.get("CS_LM_GEMM", "blas")
+if _GEMM not in ("native", "blas"):
+    raise ValueError(f"CS_LM_GEMM must be 'native' or 'blas', got {_GEMM!r}")
+
+
+def _mm(a: torch.Tensor, b: torch.Tensor, out_f32: bool = False) -> torch.Tensor:
+    """a @ b for bf16 2-D operands (views allowed), bf16 or fp32 out"""
+    if _GEMM == "native":
+        return native.C().mm_bf16(a, b, out_f32)
+    if out_f32:
+        return torch.mm(a, b, out_dtype=torch.float32)
+    return torch.mm(a, b)
+
+
 class _LinearShadow(torch.autograd.Function):
     """y = x @ W^T on the bf16 shadow of the fp32 master W; dW straight out of the GEMM in fp32"""
 
@@ -114,7 +133,7 @@ class _LinearShadow(torch.autograd.Function):
     def forward(ctx, x, weight, shadow):
         x2 = x.reshape(-1, x.shape[-1])
         with torch.autocast("cuda", enabled=False):
-            y = torch.mm(x2, shadow.t())
+            y = _mm(x2, shadow.t())
         ctx.save_for_backward(x2, shadow)
         ctx.xshape = x.shape
         return y.view(*x.shape[:-1], shadow.shape[0])
@@ -128,9 +147,9 @@ class _LinearShadow(torch.autograd.Function):
         dx = dw = None
         with torch.autocast("cuda", enabled=False):
             if ctx.needs_input_grad[0]:
-                dx = torch.mm(g2, shadow).view(ctx.xshape)
+                dx = _mm(g2, shadow).view(ctx.xshape)
             if ctx.needs_input_grad[1]:
-                dw = torch.mm(g2.t(), x2, out_dtype=torch.float32)
+                dw = _mm(g2.t(), x2, out_f32=True)
         return dx, dw, None
 
 

@@ -149,6 +149,40 @@ std::vector<torch::Tensor> attn_bwd(torch::Tensor q, torch::Tensor k, torch::Ten
   return {dq, dk, dv};
 }
 
+// C = a @ b on the bf16 matrix cores (gemm_bf16.hip). a: [M, K], b: [K, N], bf16, each with unit
+// stride along one of its two dimensions (so x @ w.t(), dy @ w and dy.t() @ x all run without a
+// copy); out: a new bf16 (out_f32 false) or fp32 [M, N] tensor, or fp32 `acc` [M, N] += a @ b.
+torch::Tensor mm_bf16(torch::Tensor a, torch::Tensor b, bool out_f32, c10::optional<torch::Tensor> acc) {
+  TORCH_CHECK(a.is_cuda() && b.is_cuda() && a.dim() == 2 && b.dim() == 2, "mm_bf16: 2-D GPU tensors");
+  TORCH_CHECK(a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16, "mm_bf16: bf16 operands");
+  TORCH_CHECK(a.size(1) == b.size(0), "mm_bf16: inner dimensions differ");
+  const int64_t M = a.size(0), K = a.size(1), N = b.size(1);
+  TORCH_CHECK(M < (1LL << 31) && N < (1LL << 31) && K < (1LL << 31), "mm_bf16: dimension too large");
+  int ak, bk;
+  int64_t lda, ldb;
+  if (a.stride(1) == 1) { ak = 1; lda = a.stride(0); }
+  else if (a.stride(0) == 1) { ak = 0; lda = a.stride(1); }
+  else TORCH_CHECK(false, "mm_bf16: a needs a unit stride");
+  if (b.stride(0) == 1) { bk = 1; ldb = b.stride(1); }
+  else if (b.stride(1) == 1) { bk = 0; ldb = b.stride(0); }
+  else TORCH_CHECK(false, "mm_bf16: b needs a unit stride");
+  DevGuard g(a.device());
+  torch::Tensor c;
+  int mode;
+  if (acc.has_value()) {
+    c = *acc;
+    TORCH_CHECK(c.is_cuda() && c.scalar_type() == at::kFloat && c.dim() == 2 && c.size(0) == M && c.size(1) == N &&
+                    c.stride(1) == 1, "mm_bf16: acc must be fp32 [M, N] with unit column stride");
+    mode = 2;
+  } else {
+    c = torch::empty({M, N}, a.options().dtype(out_f32 ? at::kFloat : at::kBFloat16));
+    mode = out_f32 ? 1 : 0;
+  }
+  CS_LAUNCH(cs_gemm_bf16(ak, a.data_ptr(), lda, bk, b.data_ptr(), ldb, c.data_ptr(), c.stride(0), (int)M, (int)N,
+                         (int)K, mode, cur_stream()));
+  return c;
+}
+
 }  // namespace
 
 void register_lm_ops(pybind11::module& m) {
@@ -161,4 +195,6 @@ void register_lm_ops(pybind11::module& m) {
   m.def("rope", &rope);
   m.def("attn_fwd", &attn_fwd, "flash attention forward (bf16 [B,S,H,D], GQA, causal)");
   m.def("attn_bwd", &attn_bwd, "flash attention backward -> dq, dk, dv");
+  m.def("mm_bf16", &mm_bf16, "C = a @ b on the bf16 matrix cores", pybind11::arg("a"), pybind11::arg("b"),
+        pybind11::arg("out_f32") = false, pybind11::arg("acc") = c10::nullopt);
 }

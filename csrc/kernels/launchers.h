@@ -264,6 +264,12 @@ hipError_t cs_maxpool3s2_fwd(int dt, const void* x, void* y, unsigned char* pos,
                              int Wo, hipStream_t stream);
 hipError_t cs_maxpool3s2_bwd(int dt, const void* dy, const unsigned char* pos, void* dx, int64_t planes, int H, int W,
                              int Ho, int Wo, hipStream_t stream);
+// bf16 GEMM on the matrix cores (gemm_bf16.hip): C[M, N] (=, +=) sum_k A(m, k) B(n, k), fp32
+// accumulate. A is stored K-major ([M][K], row stride lda) or M-major ([K][M]); B K-major ([N][K])
+// or N-major ([K][N]). out_mode 0: C bf16, 1: C fp32, 2: C fp32 +=. Needs 16-byte aligned
+// operands, lda / ldb % 8 == 0, K % 8 == 0 for a K-major operand, N, ldc % 4 == 0.
+hipError_t cs_gemm_bf16(int a_kmajor, const void* A, int64_t lda, int b_kmajor, const void* B, int64_t ldb, void* C,
+                        int64_t ldc, int M, int N, int K, int out_mode, hipStream_t stream);
 hipError_t cs_rope(int dt, const void* x, const float* cosv, const float* sinv, void* out, int B, int S, int H, int hd,
                    int inverse, hipStream_t s);
 // channels-last (NHWC) CNN kernels (cnn_nhwc.hip), fp32 / bf16 activations, M = B*H*W rows of C.

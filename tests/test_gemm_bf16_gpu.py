@@ -1,0 +1,126 @@
+"""bf16 matrix-core GEMM (csrc/kernels/gemm_bf16.hip via C.mm_bf16(a, b) = a @ b) vs a plain
+PyTorch reference of the same bf16 operands in fp64 (MI355X only). bf16 x bf16 products are exact
+in fp32, so the fp32 output differs from the reference only by summation order; the bf16 output
+by one rounding on top. All four operand layouts: a K-major ([M][K]) or M-major (a view of a
+[K][M] tensor), b K-major (a view of [N][K], the nn.Linear weight) or N-major ([K][N])."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def C():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from cs744_pytorch_distributed_tutorial_amd.ops import native
+    return native.C()
+
+
+def _ref(a, b):
+    return a.double() @ b.double()
+
+
+def _operands(M, N, K, layout, g, scale=1.0, uniform=True):
+    """a [M, K], b [K, N] as views with the requested storage: layout = (a K-major, b K-major)"""
+    def rnd(*shape):
+        x = torch.rand(*shape, device="cuda", generator=g) * 2 - 1 if uniform else \
+            torch.randn(*shape, device="cuda", generator=g)
+        return (x * scale).bfloat16()
+    ak, bk = layout
+    p8 = lambda n: (n + 7) // 8 * 8  # noqa: E731  (row strides stay 16-byte multiples)
+    a = rnd(M, K) if ak else rnd(K, p8(M))[:, :M].t()
+    b = rnd(N, K).t() if bk else rnd(K, p8(N))[:, :N]
+    return a, b
+
+
+LAYOUTS = [(True, True), (True, False), (False, True), (False, False)]
+LID = ["nt", "nn", "tt", "tn"]
+
+
+SHAPES = [
+    (256, 256, 64),      # one tile, one K-tile
+    (512, 768, 4096),    # full tiles, long K
+    (300, 260, 72),      # partial row / column tiles, partial last K-tile
+    (1000, 1028, 136),   # N % 256 = 4, K % 64 = 8
+    (64, 2048, 512),     # fewer rows than a tile
+    (2304, 1024, 1024),  # grid not a multiple of 8 tiles (9 x 4 = 36 workgroups)
+]
+
+
+@pytest.mark.parametrize("layout", LAYOUTS, ids=LID)
+@pytest.mark.parametrize("M,N,K", SHAPES)
+def test_gemm_fp32_out(C, M, N, K, layout):
+    g = torch.Generator(device="cuda").manual_seed(M * 7 + N + K)
+    a, b = _operands(M, N, K, layout, g)
+    c = C.mm_bf16(a, b, True)
+    ref = _ref(a, b)
+    assert c.dtype == torch.float32 and c.shape == (M, N)
+    err = (c.double() - ref).abs().max().item()
+    # fp32 accumulation error bound ~ K * eps32 * sum|a b| (|a b| <= 1)
+    assert err <= 1e-6 * K + 1e-5, err
+
+
+@pytest.mark.parametrize("layout", LAYOUTS, ids=LID)
+@pytest.mark.parametrize("M,N,K", SHAPES[:4])
+def test_gemm_bf16_out(C, M, N, K, layout):
+    g = torch.Generator(device="cuda").manual_seed(3 + M + N * 5 + K)
+    a, b = _operands(M, N, K, layout, g, uniform=False)
+    c = C.mm_bf16(a, b)
+    assert c.dtype == torch.bfloat16
+    ref = _ref(a, b)
+    # one bf16 rounding of the fp32 result: relative 2^-8 of |C| plus the fp32 summation slack
+    bound = ref.abs() * 2.0 ** -8 + 1e-5 * K
+    assert bool(((c.double() - ref).abs() <= bound).all())
+
+
+@pytest.mark.parametrize("layout", LAYOUTS, ids=LID)
+def test_gemm_identity_asymmetric(C, layout):
+    """A = I with an asymmetric B: C must be B exactly (catches a row/column-swapped store or a
+    k-order slip in the transposed reads)."""
+    K = 256
+    ak, bk = layout
+    eye = torch.eye(K, device="cuda").bfloat16()
+    a = eye if ak else eye.t().contiguous().t()
+    bm = (torch.arange(K * 384, device="cuda").reshape(K, 384) % 251 - 125).bfloat16()  # [K, N]
+    b = bm.t().contiguous().t() if bk else bm
+    c = C.mm_bf16(a, b, True)
+    assert torch.equal(c, bm.float())
+
+
+def test_gemm_accumulate_and_strided(C):
+    torch.manual_seed(1)
+    big = torch.randn(512, 640, device="cuda").bfloat16()
+    a = big[:, 64:640]  # row stride 640, K = 576
+    b = torch.randn(384, 576, device="cuda").bfloat16().t()
+    acc = torch.randn(512, 384, device="cuda")
+    acc0 = acc.clone()
+    out = C.mm_bf16(a, b, acc=acc)
+    assert out.data_ptr() == acc.data_ptr()
+    ref = acc0.double() + _ref(a, b)
+    assert (acc.double() - ref).abs().max().item() < 1e-3
+
+
+def test_gemm_linear_layer_products(C):
+    """the three GEMMs of a linear layer on one weight, as ops/lm.py issues them"""
+    torch.manual_seed(2)
+    x = torch.randn(1024, 768, device="cuda").bfloat16()
+    w = (torch.randn(1280, 768, device="cuda") * 0.05).bfloat16()
+    dy = torch.randn(1024, 1280, device="cuda").bfloat16()
+    y = C.mm_bf16(x, w.t(), True)
+    dx = C.mm_bf16(dy, w, True)
+    dw = C.mm_bf16(dy.t(), x, True)
+    for got, ref in ((y, x.double() @ w.double().t()), (dx, dy.double() @ w.double()),
+                     (dw, dy.double().t() @ x.double())):
+        assert (got.double() - ref).abs().max().item() < 1e-6 * ref.abs().max().item() * 64
+
+
+def test_gemm_rejects_unsupported(C):
+    a = torch.randn(64, 12, device="cuda").bfloat16()  # K-major with K % 8 != 0
+    b = torch.randn(12, 64, device="cuda").bfloat16()
+    with pytest.raises(RuntimeError):
+        C.mm_bf16(a, b.t().contiguous().t())
+    with pytest.raises(RuntimeError):
+        C.mm_bf16(a.float(), b.float())
+    with pytest.raises(RuntimeError):
+        C.mm_bf16(torch.randn(64, 64, 2, device="cuda").bfloat16()[:, :, 0], b[:, :64].contiguous())
