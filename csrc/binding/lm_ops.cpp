@@ -152,7 +152,9 @@ std::vector<torch::Tensor> attn_bwd(torch::Tensor q, torch::Tensor k, torch::Ten
 // C = a @ b on the bf16 matrix cores (gemm_bf16.hip). a: [M, K], b: [K, N], bf16, each with unit
 // stride along one of its two dimensions (so x @ w.t(), dy @ w and dy.t() @ x all run without a
 // copy); out: a new bf16 (out_f32 false) or fp32 [M, N] tensor, or fp32 `acc` [M, N] += a @ b.
-torch::Tensor mm_bf16(torch::Tensor a, torch::Tensor b, bool out_f32, c10::optional<torch::Tensor> acc) {
+// splits: reduction splits of an fp32 result (-1: cs_gemm_bf16_splits), summed in fixed order.
+torch::Tensor mm_bf16(torch::Tensor a, torch::Tensor b, bool out_f32, c10::optional<torch::Tensor> acc,
+                      int64_t splits) {
   TORCH_CHECK(a.is_cuda() && b.is_cuda() && a.dim() == 2 && b.dim() == 2, "mm_bf16: 2-D GPU tensors");
   TORCH_CHECK(a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16, "mm_bf16: bf16 operands");
   TORCH_CHECK(a.size(1) == b.size(0), "mm_bf16: inner dimensions differ");
@@ -169,6 +171,10 @@ torch::Tensor mm_bf16(torch::Tensor a, torch::Tensor b, bool out_f32, c10::optio
   DevGuard g(a.device());
   torch::Tensor c;
   int mode;
+  // fp32 results of a reduction too long for the output's tile count are split over K into slabs
+  int S = splits >= 0 ? (int)splits : cs_gemm_bf16_splits((int)M, (int)N, (int)K);
+  if (!out_f32 && !acc.has_value()) S = 1;
+  TORCH_CHECK(S >= 1 && S <= 64, "mm_bf16: splits out of range");
   if (acc.has_value()) {
     c = *acc;
     TORCH_CHECK(c.is_cuda() && c.scalar_type() == at::kFloat && c.dim() == 2 && c.size(0) == M && c.size(1) == N &&
@@ -178,8 +184,22 @@ torch::Tensor mm_bf16(torch::Tensor a, torch::Tensor b, bool out_f32, c10::optio
     c = torch::empty({M, N}, a.options().dtype(out_f32 ? at::kFloat : at::kBFloat16));
     mode = out_f32 ? 1 : 0;
   }
+  if (S > 1) {
+    auto part = torch::empty({S + (mode == 2 ? 1 : 0), M, N}, a.options().dtype(at::kFloat));
+    CS_LAUNCH(cs_gemm_bf16(ak, a.data_ptr(), lda, bk, b.data_ptr(), ldb, part.data_ptr(), N, (int)M, (int)N, (int)K, 1,
+                           S, M * N, cur_stream()));
+    if (mode == 2) part[S].copy_(c);  // the accumulator joins the fixed-order sum as the last slab
+    if (c.is_contiguous()) {
+      CS_LAUNCH(cs_slab_sum(part.data_ptr<float>(), (int)part.size(0), M * N, c.data_ptr<float>(), cur_stream()));
+    } else {
+      auto sum = torch::empty({M, N}, part.options());
+      CS_LAUNCH(cs_slab_sum(part.data_ptr<float>(), (int)part.size(0), M * N, sum.data_ptr<float>(), cur_stream()));
+      c.copy_(sum);
+    }
+    return c;
+  }
   CS_LAUNCH(cs_gemm_bf16(ak, a.data_ptr(), lda, bk, b.data_ptr(), ldb, c.data_ptr(), c.stride(0), (int)M, (int)N,
-                         (int)K, mode, cur_stream()));
+                         (int)K, mode, 1, 0, cur_stream()));
   return c;
 }
 
@@ -196,5 +216,5 @@ void register_lm_ops(pybind11::module& m) {
   m.def("attn_fwd", &attn_fwd, "flash attention forward (bf16 [B,S,H,D], GQA, causal)");
   m.def("attn_bwd", &attn_bwd, "flash attention backward -> dq, dk, dv");
   m.def("mm_bf16", &mm_bf16, "C = a @ b on the bf16 matrix cores", pybind11::arg("a"), pybind11::arg("b"),
-        pybind11::arg("out_f32") = false, pybind11::arg("acc") = c10::nullopt);
+        pybind11::arg("out_f32") = false, pybind11::arg("acc") = c10::nullopt, pybind11::arg("splits") = -1);
 }

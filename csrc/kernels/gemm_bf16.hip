@@ -260,10 +260,12 @@ struct Op<false, HS> {
 };
 
 // OUT: 0 = bf16 C, 1 = fp32 C, 2 = fp32 C += product; AK / BK: operand K-major
+// split-K: workgroup row blockIdx.y = split s takes k in [s * kper, (s + 1) * kper) and writes its
+// own C slab C + s * slab (fp32 partials, summed by cs_slab_sum)
 template <int OUT, bool AK, bool BK>
 __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B,
                                                         void* __restrict__ C, int M, int N, int K, int64_t lda,
-                                                        int64_t ldb, int64_t ldc) {
+                                                        int64_t ldb, int64_t ldc, int kper, int64_t slab) {
   __shared__ __attribute__((aligned(1024))) char smem[2 * kBuf];
   const int nM = (M + kTile - 1) / kTile, nN = (N + kTile - 1) / kTile, nwg = nM * nN;
   // XCD remap (bijective for any nwg), then GROUP_M tile order
@@ -275,6 +277,12 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(const __bf16* __restr
   const int m0 = tm * kTile, n0 = tn * kTile;
 
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, wr = wv >> 2, wc = wv & 3;
+  const int kb = blockIdx.y * kper;
+  K = K - kb < kper ? K - kb : kper;
+  A += AK ? (int64_t)kb : (int64_t)kb * lda;
+  B += BK ? (int64_t)kb : (int64_t)kb * ldb;
+  if constexpr (OUT == 0) C = static_cast<__bf16*>(C) + blockIdx.y * slab;
+  else C = static_cast<float*>(C) + blockIdx.y * slab;
   const auto sa = Op<AK, 6>::make(A, lda, m0, M, K);
   const auto sb = Op<BK, 5>::make(B, ldb, n0, N, K);
 
@@ -328,27 +336,43 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(const __bf16* __restr
   }
 }
 
+struct Geo {
+  int M, N, K;
+  int64_t lda, ldb, ldc;
+  int kper;
+  int64_t slab;
+};
+
 template <int OUT, bool AK, bool BK>
-void launch(const __bf16* a, const __bf16* b, void* c, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc,
-            dim3 grid, hipStream_t stream) {
-  hipLaunchKernelGGL((gemm_kernel<OUT, AK, BK>), grid, dim3(kThreads), 0, stream, a, b, c, M, N, K, lda, ldb, ldc);
+void launch(const __bf16* a, const __bf16* b, void* c, const Geo& g, dim3 grid, hipStream_t stream) {
+  hipLaunchKernelGGL((gemm_kernel<OUT, AK, BK>), grid, dim3(kThreads), 0, stream, a, b, c, g.M, g.N, g.K, g.lda, g.ldb,
+                     g.ldc, g.kper, g.slab);
 }
 
 template <int OUT>
-void launch_layout(int ak, int bk, const __bf16* a, const __bf16* b, void* c, int M, int N, int K, int64_t lda,
-                   int64_t ldb, int64_t ldc, dim3 grid, hipStream_t stream) {
-  if (ak && bk) launch<OUT, true, true>(a, b, c, M, N, K, lda, ldb, ldc, grid, stream);
-  else if (ak) launch<OUT, true, false>(a, b, c, M, N, K, lda, ldb, ldc, grid, stream);
-  else if (bk) launch<OUT, false, true>(a, b, c, M, N, K, lda, ldb, ldc, grid, stream);
-  else launch<OUT, false, false>(a, b, c, M, N, K, lda, ldb, ldc, grid, stream);
+void launch_layout(int ak, int bk, const __bf16* a, const __bf16* b, void* c, const Geo& g, dim3 grid,
+                   hipStream_t stream) {
+  if (ak && bk) launch<OUT, true, true>(a, b, c, g, grid, stream);
+  else if (ak) launch<OUT, true, false>(a, b, c, g, grid, stream);
+  else if (bk) launch<OUT, false, true>(a, b, c, g, grid, stream);
+  else launch<OUT, false, false>(a, b, c, g, grid, stream);
 }
 
 }  // namespace
 
+int cs_gemm_bf16_splits(int M, int N, int K) {
+  // split the reduction only when the output alone leaves most CUs idle: about one wave of
+  // workgroups over the 256 CUs, >= 1024 k per split, <= 8 splits
+  const int64_t tiles = (int64_t)((M + kTile - 1) / kTile) * ((N + kTile - 1) / kTile);
+  int s = 1;
+  while (s < 8 && tiles * s * 2 <= 256 && K / (2 * s) >= 1024) s *= 2;
+  return s;
+}
+
 hipError_t cs_gemm_bf16(int a_kmajor, const void* A, int64_t lda, int b_kmajor, const void* B, int64_t ldb, void* C,
-                        int64_t ldc, int M, int N, int K, int out_mode, hipStream_t stream) {
+                        int64_t ldc, int M, int N, int K, int out_mode, int splits, int64_t slab, hipStream_t stream) {
   if (M <= 0 || N <= 0 || K <= 0) return hipSuccess;
-  if (out_mode < 0 || out_mode > 2) return hipErrorInvalidValue;
+  if (out_mode < 0 || out_mode > 2 || splits < 1 || (splits > 1 && out_mode != 1)) return hipErrorInvalidValue;
   // 16-byte source chunks (rows 16-byte aligned), 8/16-byte output quads
   if (lda % 8 || ldb % 8 || N % 4 || ldc % 4 || ldc < N) return hipErrorInvalidValue;
   if ((a_kmajor && K % 8) || (b_kmajor && K % 8)) return hipErrorInvalidValue;
@@ -361,11 +385,15 @@ hipError_t cs_gemm_bf16(int a_kmajor, const void* A, int64_t lda, int b_kmajor, 
   if ((int64_t)(b_kmajor ? kTile : kBK) * ldb * 2 >= 0x7fffffff) return hipErrorInvalidValue;
   const int64_t tiles = (int64_t)((M + kTile - 1) / kTile) * ((N + kTile - 1) / kTile);
   if (tiles > 0x7fffffff) return hipErrorInvalidValue;
-  const dim3 grid((unsigned)tiles);
+  // K per split: a multiple of the K-tile (and of 8), every split non-empty
+  const int kper = splits == 1 ? K : (int)(((K + splits - 1) / splits + kBK - 1) / kBK * kBK);
+  if (splits > 1 && ((int64_t)kper * (splits - 1) >= K || slab < (int64_t)(M - 1) * ldc + N)) return hipErrorInvalidValue;
+  const Geo g{M, N, K, lda, ldb, ldc, kper, slab};
+  const dim3 grid((unsigned)tiles, (unsigned)splits);
   const auto* a = static_cast<const __bf16*>(A);
   const auto* b = static_cast<const __bf16*>(B);
-  if (out_mode == 0) launch_layout<0>(a_kmajor, b_kmajor, a, b, C, M, N, K, lda, ldb, ldc, grid, stream);
-  else if (out_mode == 1) launch_layout<1>(a_kmajor, b_kmajor, a, b, C, M, N, K, lda, ldb, ldc, grid, stream);
-  else launch_layout<2>(a_kmajor, b_kmajor, a, b, C, M, N, K, lda, ldb, ldc, grid, stream);
+  if (out_mode == 0) launch_layout<0>(a_kmajor, b_kmajor, a, b, C, g, grid, stream);
+  else if (out_mode == 1) launch_layout<1>(a_kmajor, b_kmajor, a, b, C, g, grid, stream);
+  else launch_layout<2>(a_kmajor, b_kmajor, a, b, C, g, grid, stream);
   return hipGetLastError();
 }

@@ -268,8 +268,11 @@ hipError_t cs_maxpool3s2_bwd(int dt, const void* dy, const unsigned char* pos, v
 // accumulate. A is stored K-major ([M][K], row stride lda) or M-major ([K][M]); B K-major ([N][K])
 // or N-major ([K][N]). out_mode 0: C bf16, 1: C fp32, 2: C fp32 +=. Needs 16-byte aligned
 // operands, lda / ldb % 8 == 0, K % 8 == 0 for a K-major operand, N, ldc % 4 == 0.
+// splits > 1 (out_mode 1 only): split s of the reduction writes the fp32 slab C + s * slab
+// (elements), to be summed by cs_slab_sum; cs_gemm_bf16_splits gives the default count.
+int cs_gemm_bf16_splits(int M, int N, int K);
 hipError_t cs_gemm_bf16(int a_kmajor, const void* A, int64_t lda, int b_kmajor, const void* B, int64_t ldb, void* C,
-                        int64_t ldc, int M, int N, int K, int out_mode, hipStream_t stream);
+                        int64_t ldc, int M, int N, int K, int out_mode, int splits, int64_t slab, hipStream_t stream);
 hipError_t cs_rope(int dt, const void* x, const float* cosv, const float* sinv, void* out, int B, int S, int H, int hd,
                    int inverse, hipStream_t s);
 // channels-last (NHWC) CNN kernels (cnn_nhwc.hip), fp32 / bf16 activations, M = B*H*W rows of C.

@@ -11,4 +11,7 @@ rc=$?; grep -E "PASSED|FAILED|ERROR|passed|failed" gpurun_out/gemm_tests.log | t
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -u scripts/gemm_bench.py --rounds 3 --reps 5 > gpurun_out/gemm_bench.log 2>&1 || exit $?
 cat gpurun_out/gemm_bench.log
+bash scripts/ab_trees.sh 2 .:CS_LM_GEMM=blas .:CS_LM_GEMM=native -- --model llama3-8b --steps 6 --warmup 3 \
+  > gpurun_out/ab_llama_gemm.log 2>&1 || exit $?
+tail -2 gpurun_out/ab_llama_gemm.log
 if [ "${1:-}" = "next" ]; then bash scripts/r4_next.sh; fi

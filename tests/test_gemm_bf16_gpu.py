@@ -124,3 +124,22 @@ def test_gemm_rejects_unsupported(C):
         C.mm_bf16(a.float(), b.float())
     with pytest.raises(RuntimeError):
         C.mm_bf16(torch.randn(64, 64, 2, device="cuda").bfloat16()[:, :, 0], b[:, :64].contiguous())
+
+
+@pytest.mark.parametrize("layout", [(True, True), (False, False)], ids=["nt", "tn"])
+def test_gemm_split_k(C, layout):
+    """reduction split over slabs (the weight-gradient shape: small output, long K), summed in
+    fixed order; also into an accumulator"""
+    g = torch.Generator(device="cuda").manual_seed(11)
+    M, N, K = 256, 512, 8200
+    a, b = _operands(M, N, K, layout, g)
+    ref = _ref(a, b)
+    one = C.mm_bf16(a, b, True, splits=1)
+    auto = C.mm_bf16(a, b, True)
+    three = C.mm_bf16(a, b, True, splits=3)
+    for c in (one, auto, three):
+        assert (c.double() - ref).abs().max().item() <= 1e-6 * K + 1e-5
+    assert torch.equal(auto, C.mm_bf16(a, b, True))  # deterministic
+    acc = torch.ones(M, N, device="cuda")
+    C.mm_bf16(a, b, acc=acc, splits=4)
+    assert (acc.double() - (ref + 1)).abs().max().item() <= 1e-6 * K + 1e-5
