@@ -64,10 +64,25 @@ def _wgrad_splits(M: int, Co: int, Kp: int) -> int:
     return s
 
 
+# GEMMs of the im2col / 1x1 convolutions: "blas" = torch.mm (hipBLASLt), "native" = the gfx950
+# bf16 GEMM of csrc/kernels/gemm_bf16.hip for every bf16 one (operands read in place, transposed in
+# LDS where needed, split-K weight gradient), "auto" = native where the output has >= 256 columns
+# (its 256 x 256 tile would be mostly idle on narrower ones)
+_CONV_GEMM = os.environ.get("CS_CONV_GEMM", "blas")
+if _CONV_GEMM not in ("blas", "native", "auto"):
+    raise ValueError(f"CS_CONV_GEMM must be 'blas', 'native' or 'auto', got {_CONV_GEMM!r}")
+
+
+def _native_gemm(a: torch.Tensor, n: int) -> bool:
+    return a.dtype == torch.bfloat16 and (_CONV_GEMM == "native" or (_CONV_GEMM == "auto" and n >= 256))
+
+
 def _wgrad(dy2: torch.Tensor, col: torch.Tensor) -> torch.Tensor:
     """fp32 dY^T @ col, split over row chunks when the output alone cannot fill the chip"""
     M, Co = dy2.shape
     Kp = col.shape[1]
+    if _native_gemm(col, Kp):
+        return native.C().mm_bf16(dy2.t(), col, True)  # split-K slabs + fixed-order sum inside
     S = _wgrad_splits(M, Co, Kp)
     if S == 1:
         return torch.mm(dy2.t(), col, out_dtype=torch.float32) if col.dtype != torch.float32 else torch.mm(dy2.t(), col)
@@ -219,7 +234,7 @@ class _ConvNHWC(torch.autograd.Function):
                 wf = F.pad(wf, (0, Kp - K))
         wf = wf.contiguous()
         with torch.autocast("cuda", enabled=False):
-            y = torch.mm(col, wf.t())
+            y = native.C().mm_bf16(col, wf.t()) if _native_gemm(col, Co) else torch.mm(col, wf.t())
         ctx.save_for_backward(col, wf)
         ctx.geo = (B, H, W, C, Ci, Co, R, S, stride, pad, K, direct)
         ctx.wdtype = weight.dtype
@@ -251,12 +266,13 @@ class _ConvNHWC(torch.autograd.Function):
                 if box is not None:
                     box["done"] = True  # a ResidualGradSink running after this returns its gradient
                     box["fused"] = gres is not None
+                nat = _native_gemm(dy2, wf.shape[1])
                 if gres is not None and gres.dtype == dy2.dtype and gres.is_contiguous():
                     # dx + the residual's gradient in one GEMM (beta = 1), written over the residual
                     # gradient itself (an out-of-place addmm would first copy it into a new buffer)
-                    dcol = gres.view(-1, C).addmm_(dy2, wf)
+                    dcol = native.C().mm_bf16(dy2, wf, acc=gres.view(-1, C)) if nat else gres.view(-1, C).addmm_(dy2, wf)
                 else:
-                    dcol = torch.mm(dy2, wf)  # [M, Kp]
+                    dcol = native.C().mm_bf16(dy2, wf) if nat else torch.mm(dy2, wf)  # [M, Kp]
                     if gres is not None:
                         dcol = dcol + gres.reshape(dcol.shape)
                 dx = dcol.view(B, H, W, C) if direct else native.C().col2im_nhwc(dcol, B, H, W, C, R, S, stride, pad)

@@ -151,8 +151,13 @@ std::vector<torch::Tensor> attn_bwd(torch::Tensor q, torch::Tensor k, torch::Ten
 
 // C = a @ b on the bf16 matrix cores (gemm_bf16.hip). a: [M, K], b: [K, N], bf16, each with unit
 // stride along one of its two dimensions (so x @ w.t(), dy @ w and dy.t() @ x all run without a
-// copy); out: a new bf16 (out_f32 false) or fp32 [M, N] tensor, or fp32 `acc` [M, N] += a @ b.
+// copy); out: a new bf16 (out_f32 false) or fp32 [M, N] tensor, or `acc` [M, N] += a @ b (fp32, or
+// bf16: summed in fp32 with one rounding).
 // splits: reduction splits of an fp32 result (-1: cs_gemm_bf16_splits), summed in fixed order.
+bool mode_bf16_acc(const c10::optional<torch::Tensor>& acc) {
+  return acc.has_value() && acc->scalar_type() == at::kBFloat16;
+}
+
 torch::Tensor mm_bf16(torch::Tensor a, torch::Tensor b, bool out_f32, c10::optional<torch::Tensor> acc,
                       int64_t splits) {
   TORCH_CHECK(a.is_cuda() && b.is_cuda() && a.dim() == 2 && b.dim() == 2, "mm_bf16: 2-D GPU tensors");
@@ -173,13 +178,14 @@ torch::Tensor mm_bf16(torch::Tensor a, torch::Tensor b, bool out_f32, c10::optio
   int mode;
   // fp32 results of a reduction too long for the output's tile count are split over K into slabs
   int S = splits >= 0 ? (int)splits : cs_gemm_bf16_splits((int)M, (int)N, (int)K);
-  if (!out_f32 && !acc.has_value()) S = 1;
+  if ((!out_f32 && !acc.has_value()) || mode_bf16_acc(acc)) S = 1;
   TORCH_CHECK(S >= 1 && S <= 64, "mm_bf16: splits out of range");
   if (acc.has_value()) {
     c = *acc;
-    TORCH_CHECK(c.is_cuda() && c.scalar_type() == at::kFloat && c.dim() == 2 && c.size(0) == M && c.size(1) == N &&
-                    c.stride(1) == 1, "mm_bf16: acc must be fp32 [M, N] with unit column stride");
-    mode = 2;
+    TORCH_CHECK(c.is_cuda() && (c.scalar_type() == at::kFloat || c.scalar_type() == at::kBFloat16) && c.dim() == 2 &&
+                    c.size(0) == M && c.size(1) == N && c.stride(1) == 1,
+                "mm_bf16: acc must be fp32 or bf16 [M, N] with unit column stride");
+    mode = c.scalar_type() == at::kFloat ? 2 : 3;
   } else {
     c = torch::empty({M, N}, a.options().dtype(out_f32 ? at::kFloat : at::kBFloat16));
     mode = out_f32 ? 1 : 0;

@@ -259,7 +259,8 @@ struct Op<false, HS> {
   }
 };
 
-// OUT: 0 = bf16 C, 1 = fp32 C, 2 = fp32 C += product; AK / BK: operand K-major
+// OUT: 0 = bf16 C, 1 = fp32 C, 2 = fp32 C += product, 3 = bf16 C += product (summed in fp32, one
+// rounding); AK / BK: operand K-major
 // split-K: workgroup row blockIdx.y = split s takes k in [s * kper, (s + 1) * kper) and writes its
 // own C slab C + s * slab (fp32 partials, summed by cs_slab_sum)
 template <int OUT, bool AK, bool BK>
@@ -281,7 +282,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(const __bf16* __restr
   K = K - kb < kper ? K - kb : kper;
   A += AK ? (int64_t)kb : (int64_t)kb * lda;
   B += BK ? (int64_t)kb : (int64_t)kb * ldb;
-  if constexpr (OUT == 0) C = static_cast<__bf16*>(C) + blockIdx.y * slab;
+  if constexpr (OUT == 0 || OUT == 3) C = static_cast<__bf16*>(C) + blockIdx.y * slab;
   else C = static_cast<float*>(C) + blockIdx.y * slab;
   const auto sa = Op<AK, 6>::make(A, lda, m0, M, K);
   const auto sb = Op<BK, 5>::make(B, ldb, n0, N, K);
@@ -322,11 +323,18 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(const __bf16* __restr
       const int n = n0 + wc * 64 + j * 16 + (lane >> 4) * 4;
       if (n >= N) continue;
       const f32x4 v = t.acc[i][j];
-      if constexpr (OUT == 0) {
+      if constexpr (OUT == 0 || OUT == 3) {
+        bf16x4* p = reinterpret_cast<bf16x4*>(static_cast<__bf16*>(C) + (int64_t)m * ldc + n);
+        f32x4 w = v;
+        if constexpr (OUT == 3) {
+          const bf16x4 old = *p;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) w[e] += (float)old[e];
+        }
         bf16x4 o;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = (__bf16)v[e];
-        *reinterpret_cast<bf16x4*>(static_cast<__bf16*>(C) + (int64_t)m * ldc + n) = o;
+        for (int e = 0; e < 4; ++e) o[e] = (__bf16)w[e];
+        *p = o;
       } else {
         f32x4* p = reinterpret_cast<f32x4*>(static_cast<float*>(C) + (int64_t)m * ldc + n);
         if constexpr (OUT == 2) *p = *p + v;
@@ -372,14 +380,14 @@ int cs_gemm_bf16_splits(int M, int N, int K) {
 hipError_t cs_gemm_bf16(int a_kmajor, const void* A, int64_t lda, int b_kmajor, const void* B, int64_t ldb, void* C,
                         int64_t ldc, int M, int N, int K, int out_mode, int splits, int64_t slab, hipStream_t stream) {
   if (M <= 0 || N <= 0 || K <= 0) return hipSuccess;
-  if (out_mode < 0 || out_mode > 2 || splits < 1 || (splits > 1 && out_mode != 1)) return hipErrorInvalidValue;
+  if (out_mode < 0 || out_mode > 3 || splits < 1 || (splits > 1 && out_mode != 1)) return hipErrorInvalidValue;
   // 16-byte source chunks (rows 16-byte aligned), 8/16-byte output quads
   if (lda % 8 || ldb % 8 || N % 4 || ldc % 4 || ldc < N) return hipErrorInvalidValue;
   if ((a_kmajor && K % 8) || (b_kmajor && K % 8)) return hipErrorInvalidValue;
   if (a_kmajor ? lda < K : lda < M) return hipErrorInvalidValue;
   if (b_kmajor ? ldb < K : ldb < N) return hipErrorInvalidValue;
   if ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B)) & 15) return hipErrorInvalidValue;
-  if (reinterpret_cast<uintptr_t>(C) & (out_mode == 0 ? 7 : 15)) return hipErrorInvalidValue;
+  if (reinterpret_cast<uintptr_t>(C) & (out_mode == 0 || out_mode == 3 ? 7 : 15)) return hipErrorInvalidValue;
   // 32-bit buffer offsets: a K-major operand addresses 256 rows, an M-major one 64 k rows
   if ((int64_t)(a_kmajor ? kTile : kBK) * lda * 2 >= 0x7fffffff) return hipErrorInvalidValue;
   if ((int64_t)(b_kmajor ? kTile : kBK) * ldb * 2 >= 0x7fffffff) return hipErrorInvalidValue;
@@ -394,6 +402,7 @@ hipError_t cs_gemm_bf16(int a_kmajor, const void* A, int64_t lda, int b_kmajor, 
   const auto* b = static_cast<const __bf16*>(B);
   if (out_mode == 0) launch_layout<0>(a_kmajor, b_kmajor, a, b, C, g, grid, stream);
   else if (out_mode == 1) launch_layout<1>(a_kmajor, b_kmajor, a, b, C, g, grid, stream);
-  else launch_layout<2>(a_kmajor, b_kmajor, a, b, C, g, grid, stream);
+  else if (out_mode == 2) launch_layout<2>(a_kmajor, b_kmajor, a, b, C, g, grid, stream);
+  else launch_layout<3>(a_kmajor, b_kmajor, a, b, C, g, grid, stream);
   return hipGetLastError();
 }

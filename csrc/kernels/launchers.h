@@ -266,7 +266,7 @@ hipError_t cs_maxpool3s2_bwd(int dt, const void* dy, const unsigned char* pos, v
                              int Ho, int Wo, hipStream_t stream);
 // bf16 GEMM on the matrix cores (gemm_bf16.hip): C[M, N] (=, +=) sum_k A(m, k) B(n, k), fp32
 // accumulate. A is stored K-major ([M][K], row stride lda) or M-major ([K][M]); B K-major ([N][K])
-// or N-major ([K][N]). out_mode 0: C bf16, 1: C fp32, 2: C fp32 +=. Needs 16-byte aligned
+// or N-major ([K][N]). out_mode 0: C bf16, 1: C fp32, 2: C fp32 +=, 3: C bf16 +=. Needs 16-byte aligned
 // operands, lda / ldb % 8 == 0, K % 8 == 0 for a K-major operand, N, ldc % 4 == 0.
 // splits > 1 (out_mode 1 only): split s of the reduction writes the fp32 slab C + s * slab
 // (elements), to be summed by cs_slab_sum; cs_gemm_bf16_splits gives the default count.

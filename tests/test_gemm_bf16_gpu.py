@@ -143,3 +143,30 @@ def test_gemm_split_k(C, layout):
     acc = torch.ones(M, N, device="cuda")
     C.mm_bf16(a, b, acc=acc, splits=4)
     assert (acc.double() - (ref + 1)).abs().max().item() <= 1e-6 * K + 1e-5
+
+
+# (B, Cin, H, W, Cout, k, stride, pad): ResNet-50 bf16 GEMM convolutions (1x1, strided 1x1 through
+# im2col, a deep 3x3 through im2col) on the native GEMM (CS_CONV_GEMM=native) vs fp64
+@pytest.mark.parametrize("geo", [(2, 64, 14, 14, 256, 1, 1, 0), (2, 256, 14, 14, 64, 1, 1, 0),
+                                 (2, 256, 14, 14, 512, 1, 2, 0), (2, 256, 7, 7, 256, 3, 1, 1)])
+def test_conv_nhwc_on_native_gemm(C, geo, monkeypatch):
+    import torch.nn as nn
+    import torch.nn.functional as F
+    from cs744_pytorch_distributed_tutorial_amd.ops import cnn_nhwc
+    monkeypatch.setattr(cnn_nhwc, "_CONV_GEMM", "native")
+    B, Ci, H, W, Co, k, st, pad = geo
+    torch.manual_seed(sum(geo))
+    conv = nn.Conv2d(Ci, Co, k, stride=st, padding=pad, bias=False).cuda()
+    x = torch.randn(B, Ci, H, W, device="cuda").bfloat16()
+    xh = x.permute(0, 2, 3, 1).contiguous().requires_grad_()
+    y = cnn_nhwc.conv_nhwc(xh, conv)
+    xr = x.double().requires_grad_()
+    wr = conv.weight.detach().bfloat16().double().requires_grad_()
+    yr = F.conv2d(xr, wr, None, st, pad)
+    torch.testing.assert_close(y.permute(0, 3, 1, 2).double(), yr, rtol=1e-2, atol=1e-2)
+    g = torch.randn(yr.shape, device="cuda").bfloat16()
+    y.backward(g.permute(0, 2, 3, 1).contiguous())
+    yr.backward(g.double())
+    torch.testing.assert_close(xh.grad.permute(0, 3, 1, 2).double(), xr.grad, rtol=1e-2, atol=1e-2)
+    # the weight gradient leaves the GEMM in fp32 (bf16 operands): only summation order differs
+    torch.testing.assert_close(conv.weight.grad.double(), wr.grad, rtol=1e-4, atol=1e-3)
