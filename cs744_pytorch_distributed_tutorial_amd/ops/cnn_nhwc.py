@@ -77,6 +77,12 @@ def _native_gemm(a: torch.Tensor, n: int) -> bool:
     return a.dtype == torch.bfloat16 and (_CONV_GEMM == "native" or (_CONV_GEMM == "auto" and n >= 256))
 
 
+# a native-GEMM forward convolution also returns its output's BatchNorm statistics per 256-row
+# tile (the GEMM epilogue, gemm_bf16.hip tile_stats); the BatchNorm reading that output then skips
+# its statistics pass (cs_bn_nhwc_fwd_tiles). CS_CONV_BN_STATS=0: the separate pass.
+_BN_STATS = os.environ.get("CS_CONV_BN_STATS", "1") != "0"
+
+
 def _wgrad(dy2: torch.Tensor, col: torch.Tensor) -> torch.Tensor:
     """fp32 dY^T @ col, split over row chunks when the output alone cannot fill the chip"""
     M, Co = dy2.shape
@@ -233,17 +239,26 @@ class _ConvNHWC(torch.autograd.Function):
             if Kp != K:
                 wf = F.pad(wf, (0, Kp - K))
         wf = wf.contiguous()
+        tiles = None
         with torch.autocast("cuda", enabled=False):
-            y = native.C().mm_bf16(col, wf.t()) if _native_gemm(col, Co) else torch.mm(col, wf.t())
+            if _native_gemm(col, Co) and _BN_STATS:
+                y, tiles = native.C().mm_bf16_bn_stats(col, wf.t())
+                ctx.mark_non_differentiable(tiles)
+            elif _native_gemm(col, Co):
+                y = native.C().mm_bf16(col, wf.t())
+            else:
+                y = torch.mm(col, wf.t())
         ctx.save_for_backward(col, wf)
         ctx.geo = (B, H, W, C, Ci, Co, R, S, stride, pad, K, direct)
         ctx.wdtype = weight.dtype
         ctx.wstride = weight.stride()
         ctx.box = box
+        if tiles is not None:
+            return y.view(B, Ho, Wo, Co), tiles
         return y.view(B, Ho, Wo, Co)
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx, dy, *_tiles):
         col, wf = ctx.saved_tensors
         B, H, W, C, Ci, Co, R, S, stride, pad, K, direct = ctx.geo
         dy2 = dy.reshape(-1, Co)
@@ -298,7 +313,12 @@ def conv_nhwc(x: torch.Tensor, conv: nn.Conv2d, grad_box: Optional[dict] = None)
         return _ConvImplicitNHWC.apply(x.to(torch.bfloat16).contiguous(), conv.weight, st, pad)
     if fits and _stem_ok(x, Ci, Co, S):
         return _ConvStemNHWC.apply(x.to(torch.bfloat16).contiguous(), conv.weight, st, pad)
-    return _ConvNHWC.apply(x, conv.weight, st, pad, grad_box)
+    out = _ConvNHWC.apply(x, conv.weight, st, pad, grad_box)
+    if isinstance(out, tuple):
+        y, tiles = out
+        y._cs_bn_tiles = tiles  # read by the bn_act_nhwc on this output
+        return y
+    return out
 
 
 def residual_sink_ok(x: torch.Tensor, conv: nn.Conv2d) -> bool:
@@ -313,10 +333,10 @@ class _BnActNHWC(torch.autograd.Function):
     mask (CS_BN_MASK=0: recompute from x and the residual)"""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, residual, running_mean, running_var, nbt, momentum, eps, relu):
+    def forward(ctx, x, weight, bias, residual, running_mean, running_var, nbt, momentum, eps, relu, tiles=None):
         use_mask = relu and residual is not None and os.environ.get("CS_BN_MASK", "1") != "0"
         y, stat, mask = native.C().bn_nhwc_fwd(x, residual, weight, bias, running_mean, running_var, nbt, momentum,
-                                               eps, relu, use_mask)
+                                               eps, relu, use_mask, tiles)
         ctx.save_for_backward(x, None if use_mask else residual, weight, stat, mask if use_mask else None)
         ctx.relu = relu
         ctx.has_res = residual is not None
@@ -327,7 +347,7 @@ class _BnActNHWC(torch.autograd.Function):
         x, residual, weight, stat, mask = ctx.saved_tensors
         dx, dres, dw, db = native.C().bn_nhwc_bwd(dy.contiguous(), x, residual, weight, stat, ctx.relu, ctx.has_res,
                                                   mask)
-        return (dx, dw, db, dres if ctx.has_res else None, None, None, None, None, None, None)
+        return (dx, dw, db, dres if ctx.has_res else None, None, None, None, None, None, None, None)
 
 
 def bn_act_nhwc(bn: nn.BatchNorm2d, x: torch.Tensor, relu: bool = True,
@@ -337,8 +357,9 @@ def bn_act_nhwc(bn: nn.BatchNorm2d, x: torch.Tensor, relu: bool = True,
             and x.dtype in (torch.float32, torch.bfloat16) and x.shape[0] * x.shape[1] * x.shape[2] > 1):
         if residual is not None:
             residual = residual.contiguous()
+        tiles = getattr(x, "_cs_bn_tiles", None)  # statistics from the producing GEMM, if any
         return _BnActNHWC.apply(x.contiguous(), bn.weight, bn.bias, residual, bn.running_mean, bn.running_var,
-                                bn.num_batches_tracked, float(bn.momentum), float(bn.eps), relu)
+                                bn.num_batches_tracked, float(bn.momentum), float(bn.eps), relu, tiles)
     if bn.training:  # CPU training: the module itself on an NCHW view
         y = bn(x.permute(0, 3, 1, 2)).permute(0, 2, 3, 1)
     else:

@@ -209,6 +209,23 @@ torch::Tensor mm_bf16(torch::Tensor a, torch::Tensor b, bool out_f32, c10::optio
   return c;
 }
 
+// y = a @ b (bf16, a [M, K] K-major, b [K, N] with unit stride along K) plus the BatchNorm
+// statistics of y per 256-row tile: {y, tiles [ceil(M / 256), N, 2] = (mean, M2)}
+std::vector<torch::Tensor> mm_bf16_bn_stats(torch::Tensor a, torch::Tensor b) {
+  TORCH_CHECK(a.is_cuda() && b.is_cuda() && a.dim() == 2 && b.dim() == 2 && a.scalar_type() == at::kBFloat16 &&
+                  b.scalar_type() == at::kBFloat16, "mm_bf16_bn_stats: 2-D bf16 GPU tensors");
+  TORCH_CHECK(a.size(1) == b.size(0) && a.stride(1) == 1 && b.stride(0) == 1,
+              "mm_bf16_bn_stats: a [M, K] and b [K, N], both with unit stride along K");
+  const int64_t M = a.size(0), K = a.size(1), N = b.size(1);
+  TORCH_CHECK(M < (1LL << 31) && N < (1LL << 31) && K < (1LL << 31), "mm_bf16_bn_stats: dimension too large");
+  DevGuard g(a.device());
+  auto y = torch::empty({M, N}, a.options());
+  auto tiles = torch::empty({(M + 255) / 256, N, 2}, a.options().dtype(at::kFloat));
+  CS_LAUNCH(cs_gemm_bf16_bn_stats(a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(1), y.data_ptr(), N, (int)M,
+                                  (int)N, (int)K, tiles.data_ptr<float>(), cur_stream()));
+  return {y, tiles};
+}
+
 }  // namespace
 
 void register_lm_ops(pybind11::module& m) {
@@ -223,4 +240,5 @@ void register_lm_ops(pybind11::module& m) {
   m.def("attn_bwd", &attn_bwd, "flash attention backward -> dq, dk, dv");
   m.def("mm_bf16", &mm_bf16, "C = a @ b on the bf16 matrix cores", pybind11::arg("a"), pybind11::arg("b"),
         pybind11::arg("out_f32") = false, pybind11::arg("acc") = c10::nullopt, pybind11::arg("splits") = -1);
+  m.def("mm_bf16_bn_stats", &mm_bf16_bn_stats, "a @ b (bf16) plus per-256-row-tile BatchNorm (mean, M2) of the result");
 }

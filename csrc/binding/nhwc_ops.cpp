@@ -109,7 +109,7 @@ std::vector<torch::Tensor> bn_nhwc_fwd(torch::Tensor x, c10::optional<torch::Ten
                                        c10::optional<torch::Tensor> w, c10::optional<torch::Tensor> b,
                                        c10::optional<torch::Tensor> rm, c10::optional<torch::Tensor> rv,
                                        c10::optional<torch::Tensor> nbt, double momentum, double eps, bool relu,
-                                       bool with_mask) {
+                                       bool with_mask, c10::optional<torch::Tensor> tiles, int64_t tile_rows) {
   check_nhwc(x, "bn_nhwc_fwd");
   const int dt = act_dt(x, "bn_nhwc_fwd");
   const int64_t C = x.size(3), M = x.numel() / C;
@@ -127,9 +127,22 @@ std::vector<torch::Tensor> bn_nhwc_fwd(torch::Tensor x, c10::optional<torch::Ten
   auto fo = x.options().dtype(at::kFloat);
   auto y = torch::empty_like(x);
   auto stat = torch::empty({4, C}, fo);
-  auto part = torch::empty({cs_bn_nhwc_partials(M, (int)C, dt)}, fo);
   torch::Tensor mask;
   if (with_mask) mask = torch::empty({M * C / cs_bn_nhwc_vec((int)C, dt)}, x.options().dtype(at::kByte));
+  if (tiles.has_value() && tiles->defined()) {
+    // statistics already computed per row tile by the producing GEMM (mm_bf16_bn_stats)
+    TORCH_CHECK(tiles->is_cuda() && tiles->scalar_type() == at::kFloat && tiles->is_contiguous() && tiles->dim() == 3 &&
+                    tiles->size(1) == C && tiles->size(2) == 2 && tile_rows > 0 &&
+                    tiles->size(0) == (M + tile_rows - 1) / tile_rows,
+                "bn_nhwc_fwd: tiles must be fp32 [ceil(M / tile_rows), C, 2] (mean, M2) partials of x");
+    CS_LAUNCH(cs_bn_nhwc_fwd_tiles(dt, x.data_ptr(), has_res ? res->data_ptr() : nullptr, opt_ptr<float>(w),
+                                   opt_ptr<float>(b), opt_ptr<float>(rm), opt_ptr<float>(rv), opt_ptr<int64_t>(nbt),
+                                   (float)momentum, (float)eps, relu ? 1 : 0, y.data_ptr(), stat.data_ptr<float>(),
+                                   tiles->data_ptr<float>(), (int)tiles->size(0), (int)tile_rows, M, (int)C,
+                                   cur_stream(), with_mask ? mask.data_ptr<uint8_t>() : nullptr));
+    return {y, stat, mask};
+  }
+  auto part = torch::empty({cs_bn_nhwc_partials(M, (int)C, dt)}, fo);
   CS_LAUNCH(cs_bn_nhwc_fwd(dt, x.data_ptr(), has_res ? res->data_ptr() : nullptr, opt_ptr<float>(w), opt_ptr<float>(b),
                            opt_ptr<float>(rm), opt_ptr<float>(rv), opt_ptr<int64_t>(nbt), (float)momentum, (float)eps,
                            relu ? 1 : 0, y.data_ptr(), stat.data_ptr<float>(), part.data_ptr<float>(), M, (int)C,
@@ -275,7 +288,8 @@ void register_nhwc_ops(pybind11::module& m) {
   m.def("slab_sum", &slab_sum, "sum of fp32 partial slabs over dim 0, deterministic");
   m.def("bn_nhwc_fwd", &bn_nhwc_fwd, "training BatchNorm2d (+residual) (+ReLU), NHWC fp32/bf16 -> (y, stat, mask)",
         pybind11::arg("x"), pybind11::arg("res"), pybind11::arg("w"), pybind11::arg("b"), pybind11::arg("rm"), pybind11::arg("rv"), pybind11::arg("nbt"),
-        pybind11::arg("momentum"), pybind11::arg("eps"), pybind11::arg("relu"), pybind11::arg("with_mask") = false);
+        pybind11::arg("momentum"), pybind11::arg("eps"), pybind11::arg("relu"), pybind11::arg("with_mask") = false,
+        pybind11::arg("tiles") = c10::nullopt, pybind11::arg("tile_rows") = 256);
   m.def("bn_nhwc_bwd", &bn_nhwc_bwd, "its backward -> (dx, dres, dweight, dbias); mask: the forward's ReLU mask",
         pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("res"), pybind11::arg("w"), pybind11::arg("stat"), pybind11::arg("relu"),
         pybind11::arg("need_dres"), pybind11::arg("mask") = pybind11::none());

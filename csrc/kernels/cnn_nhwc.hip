@@ -186,6 +186,68 @@ __global__ __launch_bounds__(256) void finalize_fwd_kernel(const T* __restrict__
   }
 }
 
+// The same outputs from per-tile (mean, M2) partials of R-row tiles (the bf16 GEMM's statistics
+// epilogue, gemm_bf16.hip tile_stats): tiles [T][C][2]. Lane pl Chan-combines tiles pl, pl + 32,
+// ... in order (f64), then the 32 lane states combine in a fixed tree: deterministic.
+__device__ __forceinline__ void chan64(double& n, double& m, double& M2, double nb, double mb, double M2b) {
+  if (nb == 0.0) return;
+  if (n == 0.0) {
+    n = nb; m = mb; M2 = M2b;
+    return;
+  }
+  const double nn = n + nb, d = mb - m;
+  m += d * (nb / nn);
+  M2 += M2b + d * d * (n * nb / nn);
+  n = nn;
+}
+
+__global__ __launch_bounds__(256) void finalize_tiles_kernel(const float* __restrict__ tiles, int T, int R, int64_t M,
+                                                             int C, const float* __restrict__ w,
+                                                             const float* __restrict__ b, float* __restrict__ rm,
+                                                             float* __restrict__ rv, float momentum, float eps,
+                                                             float* __restrict__ stat, int64_t* __restrict__ nbt) {
+  __shared__ double sh[32][8][3];
+  const int cl = threadIdx.x & 7, pl = threadIdx.x >> 3, c = blockIdx.x * 8 + cl;
+  double n = 0.0, m = 0.0, M2 = 0.0;
+  if (c < C)
+    for (int p = pl; p < T; p += 32) {
+      const int64_t left = M - (int64_t)p * R;
+      const float2 v = *reinterpret_cast<const float2*>(tiles + ((size_t)p * C + c) * 2);
+      chan64(n, m, M2, (double)(left < R ? left : R), (double)v.x, (double)v.y);
+    }
+  sh[pl][cl][0] = n;
+  sh[pl][cl][1] = m;
+  sh[pl][cl][2] = M2;
+  __syncthreads();
+#pragma unroll
+  for (int h = 16; h > 0; h >>= 1) {
+    if (pl < h) {
+      double a = sh[pl][cl][0], am = sh[pl][cl][1], a2 = sh[pl][cl][2];
+      chan64(a, am, a2, sh[pl + h][cl][0], sh[pl + h][cl][1], sh[pl + h][cl][2]);
+      sh[pl][cl][0] = a;
+      sh[pl][cl][1] = am;
+      sh[pl][cl][2] = a2;
+    }
+    __syncthreads();
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0 && nbt != nullptr) *nbt += 1;  // num_batches_tracked
+  if (pl != 0 || c >= C) return;
+  const double mean = sh[0][cl][1];
+  double var = sh[0][cl][2] / (double)M;
+  if (var < 0.0) var = 0.0;
+  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+  const float scale = (w != nullptr ? w[c] : 1.f) * invstd;
+  stat[c] = scale;
+  stat[C + c] = (b != nullptr ? b[c] : 0.f) - (float)mean * scale;
+  stat[2 * C + c] = (float)mean;
+  stat[3 * C + c] = invstd;
+  if (rm != nullptr) {
+    const double unbiased = M > 1 ? var * (double)M / (double)(M - 1) : var;
+    rm[c] = (1.f - momentum) * rm[c] + momentum * (float)mean;
+    rv[c] = (1.f - momentum) * rv[c] + momentum * (float)unbiased;
+  }
+}
+
 // Block (p, g): rows [p*rpb, ...) x this block's channel vectors (the stats kernel's split): each
 // thread keeps its V channels' scale / shift in registers and walks rows.
 template <typename T, int V>
@@ -656,6 +718,22 @@ hipError_t cs_bn_nhwc_fwd(int dt, const void* x, const void* res, const float* w
                           int64_t M, int C, hipStream_t stream, unsigned char* mask) {
   if (M * C == 0) return hipSuccess;
   CS_NHWC_DISPATCH(dt, C, bn_fwd_t<T, V>(x, res, w, b, rm, rv, nbt, momentum, eps, relu, y, stat, part, M, C, mask, stream));
+  return hipGetLastError();
+}
+
+hipError_t cs_bn_nhwc_fwd_tiles(int dt, const void* x, const void* res, const float* w, const float* b, float* rm,
+                                float* rv, int64_t* nbt, float momentum, float eps, int relu, void* y, float* stat,
+                                const float* tiles, int ntiles, int R, int64_t M, int C, hipStream_t stream,
+                                unsigned char* mask) {
+  if (M * C == 0) return hipSuccess;
+  if (ntiles < 1 || R < 1 || (int64_t)(ntiles - 1) * R >= M || (int64_t)ntiles * R < M) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(finalize_tiles_kernel, dim3((C + 7) / 8), dim3(256), 0, stream, tiles, ntiles, R, M, C, w, b, rm, rv,
+                     momentum, eps, stat, nbt);
+  CS_NHWC_DISPATCH(dt, C, {
+    const BnGrid a = apply_grid(M, C, V);
+    hipLaunchKernelGGL((apply_fwd_kernel<T, V>), dim3(a.P, a.CG), dim3(256), 0, stream, (const T*)x, (const T*)res,
+                       stat, (T*)y, M, C, a.rpb, relu, mask);
+  });
   return hipGetLastError();
 }
 

@@ -261,12 +261,79 @@ struct Op<false, HS> {
 
 // OUT: 0 = bf16 C, 1 = fp32 C, 2 = fp32 C += product, 3 = bf16 C += product (summed in fp32, one
 // rounding); AK / BK: operand K-major
+// BatchNorm statistics of the bf16-rounded outputs of one 256-row tile (the values the BN pass
+// reads back), per column: the mean over the tile's valid rows, then M2 = sum (y - mean)^2 around
+// that mean (two passes over the accumulators, no cancellation), combined across the 16 lanes of
+// a column group by xor-shuffles and across the two wave rows through LDS (`red`: 512 floats).
+// The finalize Chan-combines the tiles in a fixed order (cs_bn_nhwc_fwd_tiles).
+__device__ __forceinline__ void tile_stats(const Tile& t, int M, int N, int m0, int n0, int tm, int wr, int wc,
+                                           int lane, float* red, float* __restrict__ stats) {
+  const int rows = M - m0 < kTile ? M - m0 : kTile;
+  float v[4][4];  // [j][e]: column n0 + wc*64 + j*16 + (lane >> 4)*4 + e
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    float mean[4][4];
+    if (pass == 1) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int c = wc * 64 + j * 16 + (lane >> 4) * 4 + e;
+          mean[j][e] = (red[c] + red[256 + c]) / (float)rows;
+        }
+      __syncthreads();  // every wave has its means before red is overwritten
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[j][e] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const bool ok = m0 + wr * 128 + i * 16 + (lane & 15) < M;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float y = (float)(__bf16)t.acc[i][j][e];
+          const float d = pass == 0 ? y : y - mean[j][e];
+          v[j][e] += ok ? (pass == 0 ? d : d * d) : 0.f;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float x = v[j][e];
+        x += __shfl_xor(x, 1);
+        x += __shfl_xor(x, 2);
+        x += __shfl_xor(x, 4);
+        x += __shfl_xor(x, 8);
+        if ((lane & 15) == 0) red[wr * 256 + wc * 64 + j * 16 + (lane >> 4) * 4 + e] = x;
+      }
+    __syncthreads();
+    if (pass == 1 && wr == 0 && (lane & 15) == 0) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int c = wc * 64 + j * 16 + (lane >> 4) * 4 + e;
+          if (n0 + c < N)
+            *reinterpret_cast<float2*>(stats + ((int64_t)tm * N + n0 + c) * 2) =
+                make_float2(mean[j][e], red[c] + red[256 + c]);
+        }
+    }
+  }
+}
+
 // split-K: workgroup row blockIdx.y = split s takes k in [s * kper, (s + 1) * kper) and writes its
 // own C slab C + s * slab (fp32 partials, summed by cs_slab_sum)
-template <int OUT, bool AK, bool BK>
+// STATS (bf16 C, no split): per-channel BatchNorm statistics of this tile's bf16 outputs, tile
+// mean and M2 = sum (y - mean)^2 per column, into stats[tile row][N][2] (see tile_stats below)
+template <int OUT, bool AK, bool BK, bool STATS = false>
 __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B,
                                                         void* __restrict__ C, int M, int N, int K, int64_t lda,
-                                                        int64_t ldb, int64_t ldc, int kper, int64_t slab) {
+                                                        int64_t ldb, int64_t ldc, int kper, int64_t slab,
+                                                        float* __restrict__ stats) {
   __shared__ __attribute__((aligned(1024))) char smem[2 * kBuf];
   const int nM = (M + kTile - 1) / kTile, nN = (N + kTile - 1) / kTile, nwg = nM * nN;
   // XCD remap (bijective for any nwg), then GROUP_M tile order
@@ -342,6 +409,10 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(const __bf16* __restr
       }
     }
   }
+  if constexpr (STATS) {
+    __syncthreads();  // every wave is past its last reads of the operand images: reuse the LDS
+    tile_stats(t, M, N, m0, n0, tm, wr, wc, lane, reinterpret_cast<float*>(smem), stats);
+  }
 }
 
 struct Geo {
@@ -354,7 +425,7 @@ struct Geo {
 template <int OUT, bool AK, bool BK>
 void launch(const __bf16* a, const __bf16* b, void* c, const Geo& g, dim3 grid, hipStream_t stream) {
   hipLaunchKernelGGL((gemm_kernel<OUT, AK, BK>), grid, dim3(kThreads), 0, stream, a, b, c, g.M, g.N, g.K, g.lda, g.ldb,
-                     g.ldc, g.kper, g.slab);
+                     g.ldc, g.kper, g.slab, nullptr);
 }
 
 template <int OUT>
@@ -404,5 +475,21 @@ hipError_t cs_gemm_bf16(int a_kmajor, const void* A, int64_t lda, int b_kmajor, 
   else if (out_mode == 1) launch_layout<1>(a_kmajor, b_kmajor, a, b, C, g, grid, stream);
   else if (out_mode == 2) launch_layout<2>(a_kmajor, b_kmajor, a, b, C, g, grid, stream);
   else launch_layout<3>(a_kmajor, b_kmajor, a, b, C, g, grid, stream);
+  return hipGetLastError();
+}
+
+hipError_t cs_gemm_bf16_bn_stats(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int M,
+                                 int N, int K, float* stats, hipStream_t stream) {
+  if (M <= 0 || N <= 0 || K <= 0) return hipSuccess;
+  if (K % 8 || lda % 8 || ldb % 8 || N % 4 || ldc % 4 || ldc < N || lda < K || ldb < K) return hipErrorInvalidValue;
+  if ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B)) & 15 || reinterpret_cast<uintptr_t>(C) & 7 ||
+      reinterpret_cast<uintptr_t>(stats) & 7)
+    return hipErrorInvalidValue;
+  if ((int64_t)kTile * lda * 2 >= 0x7fffffff || (int64_t)kTile * ldb * 2 >= 0x7fffffff) return hipErrorInvalidValue;
+  const int64_t tiles = (int64_t)((M + kTile - 1) / kTile) * ((N + kTile - 1) / kTile);
+  if (tiles > 0x7fffffff) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((gemm_kernel<0, true, true, true>), dim3((unsigned)tiles), dim3(kThreads), 0, stream,
+                     static_cast<const __bf16*>(A), static_cast<const __bf16*>(B), C, M, N, K, lda, ldb, ldc, K,
+                     (int64_t)0, stats);
   return hipGetLastError();
 }

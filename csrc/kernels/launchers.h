@@ -270,6 +270,10 @@ hipError_t cs_maxpool3s2_bwd(int dt, const void* dy, const unsigned char* pos, v
 // operands, lda / ldb % 8 == 0, K % 8 == 0 for a K-major operand, N, ldc % 4 == 0.
 // splits > 1 (out_mode 1 only): split s of the reduction writes the fp32 slab C + s * slab
 // (elements), to be summed by cs_slab_sum; cs_gemm_bf16_splits gives the default count.
+// forward product with BatchNorm statistics of its bf16 output C[M, N] (A, B K-major, out bf16):
+// stats[tile row t][N][2] = (mean, M2) of the bf16 values of rows [256 t, 256 t + 256)
+hipError_t cs_gemm_bf16_bn_stats(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int M,
+                                 int N, int K, float* stats, hipStream_t stream);
 int cs_gemm_bf16_splits(int M, int N, int K);
 hipError_t cs_gemm_bf16(int a_kmajor, const void* A, int64_t lda, int b_kmajor, const void* B, int64_t ldb, void* C,
                         int64_t ldc, int M, int N, int K, int out_mode, int splits, int64_t slab, hipStream_t stream);
@@ -285,6 +289,12 @@ int cs_bn_nhwc_vec(int C, int dt);
 hipError_t cs_bn_nhwc_fwd(int dt, const void* x, const void* res, const float* w, const float* b, float* rm, float* rv,
                           int64_t* nbt, float momentum, float eps, int relu, void* y, float* stat, float* part,
                           int64_t M, int C, hipStream_t stream, unsigned char* mask = nullptr);
+// the same from per-tile (mean, M2) partials of R-row tiles ([T][C][2], cs_gemm_bf16_bn_stats)
+// instead of a statistics pass over x: finalize (Chan, f64, fixed order) + apply
+hipError_t cs_bn_nhwc_fwd_tiles(int dt, const void* x, const void* res, const float* w, const float* b, float* rm,
+                                float* rv, int64_t* nbt, float momentum, float eps, int relu, void* y, float* stat,
+                                const float* tiles, int T, int R, int64_t M, int C, hipStream_t stream,
+                                unsigned char* mask);
 hipError_t cs_bn_nhwc_bwd(int dt, const void* dy, const void* x, const void* res, const float* w, const float* stat,
                           int relu, void* dx, void* dres, float* dw, float* db, float* coef, float* part, int64_t M,
                           int C, hipStream_t stream, const unsigned char* mask = nullptr,

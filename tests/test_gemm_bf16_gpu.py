@@ -170,3 +170,70 @@ def test_conv_nhwc_on_native_gemm(C, geo, monkeypatch):
     torch.testing.assert_close(xh.grad.permute(0, 3, 1, 2).double(), xr.grad, rtol=1e-2, atol=1e-2)
     # the weight gradient leaves the GEMM in fp32 (bf16 operands): only summation order differs
     torch.testing.assert_close(conv.weight.grad.double(), wr.grad, rtol=1e-4, atol=1e-3)
+
+
+def test_gemm_bn_stats_epilogue(C):
+    """per-256-row-tile (mean, M2) of the bf16 output, from the GEMM epilogue, vs fp64 of y itself"""
+    g = torch.Generator(device="cuda").manual_seed(5)
+    M, N, K = 700, 384, 320  # a partial last row tile
+    a = (torch.randn(M, K, device="cuda", generator=g) + 0.3).bfloat16()
+    b = torch.randn(N, K, device="cuda", generator=g).bfloat16().t()
+    y, tiles = C.mm_bf16_bn_stats(a, b)
+    assert torch.equal(y, C.mm_bf16(a, b))
+    assert tiles.shape == (3, N, 2)
+    yd = y.double()
+    for t in range(3):
+        blk = yd[256 * t:256 * (t + 1)]
+        mean = blk.mean(0)
+        m2 = ((blk - mean) ** 2).sum(0)
+        torch.testing.assert_close(tiles[t, :, 0].double(), mean, rtol=1e-5, atol=1e-5)
+        torch.testing.assert_close(tiles[t, :, 1].double(), m2, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("relu,residual", [(True, False), (True, True), (False, False)])
+def test_bn_nhwc_from_gemm_tiles_matches_stats_pass(C, relu, residual):
+    g = torch.Generator(device="cuda").manual_seed(6)
+    B, H, W, K, Co = 4, 15, 13, 256, 256
+    M = B * H * W
+    a = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(Co, K, device="cuda", generator=g) * 0.1).bfloat16()
+    y, tiles = C.mm_bf16_bn_stats(a, w.t())
+    x = y.view(B, H, W, Co)
+    res = torch.randn(B, H, W, Co, device="cuda", generator=g).bfloat16() if residual else None
+    gam = torch.rand(Co, device="cuda", generator=g) + 0.5
+    bet = torch.randn(Co, device="cuda", generator=g)
+    outs = []
+    for t in (None, tiles):
+        rm, rv = torch.zeros(Co, device="cuda"), torch.ones(Co, device="cuda")
+        nbt = torch.zeros((), dtype=torch.long, device="cuda")
+        yo, stat, _ = C.bn_nhwc_fwd(x, res, gam, bet, rm, rv, nbt, 0.1, 1e-5, relu, False, t)
+        outs.append((yo, stat, rm, rv, nbt))
+    (y0, s0, rm0, rv0, n0), (y1, s1, rm1, rv1, n1) = outs
+    torch.testing.assert_close(s1, s0, rtol=2e-5, atol=2e-5)
+    torch.testing.assert_close(rm1, rm0, rtol=2e-5, atol=2e-6)
+    torch.testing.assert_close(rv1, rv0, rtol=2e-5, atol=2e-6)
+    assert int(n0) == int(n1) == 1
+    # same scale/shift up to float rounding -> outputs within a bf16 ulp
+    torch.testing.assert_close(y1.float(), y0.float(), rtol=1e-2, atol=1e-2)
+
+
+def test_resnet_bottleneck_native_gemm_close_to_blas(C, monkeypatch):
+    """a ResNet-50 bottleneck step (bf16 autocast, channels-last) with its GEMM convolutions and
+    the BatchNorm statistics on the native GEMM vs hipBLASLt + the statistics pass"""
+    from cs744_pytorch_distributed_tutorial_amd.models import resnet as rn
+    from cs744_pytorch_distributed_tutorial_amd.ops import cnn_nhwc
+    torch.manual_seed(8)
+    blk0 = rn.Bottleneck(256, 64).cuda()
+    x0 = torch.randn(8, 14, 14, 256, device="cuda").bfloat16()
+    res = {}
+    for mode in ("blas", "native"):
+        monkeypatch.setattr(cnn_nhwc, "_CONV_GEMM", mode)
+        blk = rn.Bottleneck(256, 64).cuda()
+        blk.load_state_dict(blk0.state_dict())
+        x = x0.clone().requires_grad_()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = blk.forward_nhwc(x)
+        y.float().square().mean().backward()
+        res[mode] = (y.float(), x.grad.float(), blk.conv1.weight.grad, blk.bn3.running_var.clone())
+    for a, b in zip(res["native"], res["blas"]):
+        torch.testing.assert_close(a, b, rtol=3e-2, atol=3e-2)
