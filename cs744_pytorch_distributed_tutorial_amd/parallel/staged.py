@@ -54,11 +54,13 @@ class ProbeComm(Comm):
     """World-1 ordering probe (no Python-level collectives: world 1)."""
     kind = "probe"
 
-    def __init__(self, device: Optional[int] = None, spin_us: float = 20.0, gbps: float = 0.0, world: int = 8):
+    def __init__(self, device: Optional[int] = None, spin_us: float = 20.0, gbps: float = 0.0, world: int = 8,
+                 ctas: int = 0):
         """gbps > 0: the xGMI model (no scramble): every all-reduce spins spin_us plus the ring time
-        of a ``world``-GPU ring at ``gbps`` bus bandwidth, every broadcast spin_us + bytes / gbps."""
+        of a ``world``-GPU ring at ``gbps`` bus bandwidth, every broadcast spin_us + bytes / gbps;
+        ctas > 0: the spin is that many busy workgroups (an RCCL collective's CU footprint)."""
         dev = torch.cuda.current_device() if device is None else device
-        self.native = native.C().ProbeComm(dev, spin_us, gbps, world)
+        self.native = native.C().ProbeComm(dev, spin_us, gbps, world, ctas)
         self.rank, self.world_size = 0, 1
 
     def broadcast(self, buf: torch.Tensor, src: int = 0) -> None:

@@ -243,12 +243,14 @@ class NativeTrainer:
                 self._probe = ProbeComm(self.device.index or 0, spin)
             elif probe.startswith("xgmi"):
                 # N > 1 projection on one GPU: every collective = a spin as long as a ring all-reduce
-                # of its bytes over W GPUs at G GB/s bus bandwidth plus a latency term ("xgmi:G:W:us",
-                # defaults 150 GB/s, 8 GPUs, 25 us): the real step schedule with modelled collectives
+                # of its bytes over W GPUs at G GB/s bus bandwidth plus a latency term
+                # ("xgmi:G:W:us[:ctas]", defaults 150 GB/s, 8 GPUs, 25 us; ctas > 0: the spin runs as
+                # that many busy workgroups, the CU footprint of RCCL's CTAs): the real step schedule
+                # with modelled collectives
                 from ..parallel.staged import ProbeComm
-                f = (probe.split(":") + ["", "", ""])[1:4]
+                f = (probe.split(":") + ["", "", "", ""])[1:5]
                 self._probe = ProbeComm(self.device.index or 0, float(f[2] or 25.0), float(f[0] or 150.0),
-                                        int(f[1] or 8))
+                                        int(f[1] or 8), int(f[3] or 0))
             else:
                 # measurement only: a one-rank RCCL communicator so the engine's bucketed all-reduce,
                 # buffer broadcast and stream fork/join run (and cost what they cost) on one GPU

@@ -90,8 +90,8 @@ void register_runtime(pybind11::module& m) {
   py::class_<cs::StagedComm, cs::DeviceComm>(m, "StagedComm")
       .def(py::init<const std::string&, int>(), py::arg("group_name"), py::arg("device"));
   py::class_<cs::ProbeComm, cs::DeviceComm>(m, "ProbeComm")
-      .def(py::init<int, double, double, int>(), py::arg("device"), py::arg("spin_us") = 20.0, py::arg("gbps") = 0.0,
-           py::arg("world") = 8);
+      .def(py::init<int, double, double, int, int>(), py::arg("device"), py::arg("spin_us") = 20.0,
+           py::arg("gbps") = 0.0, py::arg("world") = 8, py::arg("ctas") = 0);
   py::class_<cs::RcclComm, cs::DeviceComm>(m, "RcclComm")
       .def(py::init([](py::bytes uid, int rank, int world, int device, bool high_priority, int max_ctas) {
              return new cs::RcclComm(std::string(uid), rank, world, device, high_priority, max_ctas);

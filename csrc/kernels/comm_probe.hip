@@ -13,6 +13,22 @@ __global__ __launch_bounds__(64) void spin_kernel(uint64_t ticks) {
   while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(2);
 }
 
+// stand-in for an RCCL collective's CTAs: `gridDim.x` workgroups of 256 threads that keep their
+// CUs' vector pipes busy (dependent FMA chains, no sleep) for the collective's modelled duration,
+// so compute overlapping it loses those CUs' issue slots the way a copy-reduce CTA takes them
+__global__ __launch_bounds__(256) void busy_kernel(uint64_t ticks, float* __restrict__ sink) {
+  const uint64_t t0 = wall_clock64();
+  float a = (float)threadIdx.x, b = 1.0f;
+  while (wall_clock64() - t0 < ticks) {
+#pragma unroll
+    for (int i = 0; i < 64; ++i) {
+      a = fmaf(a, 0.999f, b);
+      b = fmaf(b, 1.001f, a);
+    }
+  }
+  if (a == 1234.5f && b == 0.f) sink[threadIdx.x] = a;  // keeps the chains live; never true
+}
+
 __global__ __launch_bounds__(256) void scramble_f32_kernel(float* __restrict__ x, int64_t n, float s) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) x[i] = x[i] * s;
@@ -31,10 +47,15 @@ int grid_for(int64_t n) {
 
 }  // namespace
 
-hipError_t cs_comm_spin(double us, hipStream_t stream) {
+hipError_t cs_comm_spin(double us, hipStream_t stream, int ctas, float* sink) {
   if (us <= 0.0) return hipSuccess;
   const double capped = us > 1e5 ? 1e5 : us;  // never more than 0.1 s per call
-  hipLaunchKernelGGL(spin_kernel, dim3(1), dim3(64), 0, stream, (uint64_t)(capped * 100.0));
+  if (ctas > 0) {
+    if (ctas > 256 || sink == nullptr) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(busy_kernel, dim3(ctas), dim3(256), 0, stream, (uint64_t)(capped * 100.0), sink);
+  } else {
+    hipLaunchKernelGGL(spin_kernel, dim3(1), dim3(64), 0, stream, (uint64_t)(capped * 100.0));
+  }
   return hipGetLastError();
 }
 

@@ -26,9 +26,10 @@
 //    per quadrant of the wave tile (64 rows x 32 cols, 16 MFMAs). Phase p of tile t first waits
 //    (counted vmcnt) for the half-tiles it reads, passes a raw s_barrier, then stages one
 //    half-tile of tile t + 1 (2 DMA instructions per wave) and runs its quadrant. Quadrant order
-//    (A0 B0) (A1 B0) (A1 B1) (A0 B1) against staging order A0 B0 A1 B1 (A_h = the 128 A rows
+//    (A0 B0) (A0 B1) (A1 B1) (A1 B0) against staging order A0 B0 B1 A1 (A_h = the 128 A rows
 //    with (r >> 6) & 1 == h, the rows every wave's quadrant h reads; B_h likewise by (r >> 5) & 1)
-//    means every phase needs at most the half-tile staged 2 phases before it: vmcnt(4) = 2
+//    keeps one operand half in registers from phase to phase (28 fragment reads per K-tile, not
+//    48), and every phase needs at most the half-tile staged 2 phases before it: vmcnt(4) = 2
 //    half-tiles stay in flight across each barrier and every DMA has >= 3 phases (~1500 clocks)
 //    to land. Nothing drains the load queue inside the K loop (guide T3+T4).
 //    WAR: phase p stages into the buffer tile t - 1 read; its last read of that half-tile was in
@@ -187,21 +188,27 @@ struct Tile {
   f32x4 acc[8][4];
 };
 
-// quadrant (MH, NH) of the wave tile over one K-tile held in `buf`
-template <int MH, int NH, class SA, class SB>
-__device__ __forceinline__ void quadrant(Tile& t, const char* buf, const SA& sa, const SB& sb, int wr, int wc,
-                                         int lane) {
-  const char* ia = buf;
-  const char* ib = buf + kImg;
-  bf16x8 fa[4][2], fb[2][2];
+// fragments of the wave tile's A rows of half MH (4 subtiles) / B rows of half NH (2 subtiles)
+// for both 32-deep k-steps of the K-tile in `buf`
+template <int MH, class SA>
+__device__ __forceinline__ void load_a(bf16x8 (&fa)[4][2], const char* buf, const SA& sa, int wr, int lane) {
 #pragma unroll
-  for (int s = 0; s < 2; ++s) {
+  for (int s = 0; s < 2; ++s)
 #pragma unroll
-    for (int q = 0; q < 2; ++q) fb[q][s] = sb.frag(ib, wc * 64 + NH * 32 + q * 16, s, lane);
+    for (int i = 0; i < 4; ++i) fa[i][s] = sa.frag(buf, wr * 128 + MH * 64 + i * 16, s, lane);
+}
+template <int NH, class SB>
+__device__ __forceinline__ void load_b(bf16x8 (&fb)[2][2], const char* buf, const SB& sb, int wc, int lane) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) fa[i][s] = sa.frag(ia, wr * 128 + MH * 64 + i * 16, s, lane);
-  }
-  if constexpr (!SA::kRowRead || !SB::kRowRead) {
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) fb[q][s] = sb.frag(buf + kImg, wc * 64 + NH * 32 + q * 16, s, lane);
+}
+
+// quadrant (MH, NH) of the wave tile: 16 MFMAs on fragments already in registers
+template <int MH, int NH, bool ASM_READS>
+__device__ __forceinline__ void mma(Tile& t, const bf16x8 (&fa)[4][2], const bf16x8 (&fb)[2][2]) {
+  if constexpr (ASM_READS) {
     // inline-asm transposed reads are invisible to hipcc's waitcnt insertion (and an asm wait
     // does not order the register-only MFMAs after it without the sched_barrier: guide §5.4 rule 18)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -219,25 +226,35 @@ __device__ __forceinline__ void quadrant(Tile& t, const char* buf, const SA& sa,
   __builtin_amdgcn_s_setprio(0);
 }
 
-// one K-tile: 4 phases; STAGE: tile k0n is staged into `nxt` meanwhile; W: vmcnt before phases 1-3
+// one K-tile: 4 phases, quadrant order (A0 B0) (A0 B1) (A1 B1) (A1 B0), so consecutive phases share
+// one operand half in registers: 28 fragment reads per K-tile instead of 48 (LDS read bandwidth,
+// not the MFMA, bounds the 16x16x32 wave tile otherwise). STAGE: tile k0n is staged into `nxt`
+// meanwhile, in the order its phases need it (A0 B0 B1 A1); W: vmcnt before phases 1-3.
 template <bool STAGE, bool KTAIL, int W, class SA, class SB>
 __device__ __forceinline__ void ktile(Tile& t, const char* cur, char* nxt, const SA& sa, const SB& sb, int k0n, int wr,
                                       int wc, int lane) {
+  constexpr bool ASM = !SA::kRowRead || !SB::kRowRead;
+  bf16x8 fa[4][2], fb[2][2];
   wait_vm<W>();
   barrier();
   if constexpr (STAGE) sa.template stage<KTAIL>(nxt, 0, k0n);
-  quadrant<0, 0>(t, cur, sa, sb, wr, wc, lane);
+  load_a<0>(fa, cur, sa, wr, lane);
+  load_b<0>(fb, cur, sb, wc, lane);
+  mma<0, 0, ASM>(t, fa, fb);
   wait_vm<W>();
   barrier();
   if constexpr (STAGE) sb.template stage<KTAIL>(nxt + kImg, 0, k0n);
-  quadrant<1, 0>(t, cur, sa, sb, wr, wc, lane);
+  load_b<1>(fb, cur, sb, wc, lane);
+  mma<0, 1, ASM>(t, fa, fb);
   wait_vm<W>();
   barrier();
-  if constexpr (STAGE) sa.template stage<KTAIL>(nxt, 1, k0n);
-  quadrant<1, 1>(t, cur, sa, sb, wr, wc, lane);
-  barrier();
   if constexpr (STAGE) sb.template stage<KTAIL>(nxt + kImg, 1, k0n);
-  quadrant<0, 1>(t, cur, sa, sb, wr, wc, lane);
+  load_a<1>(fa, cur, sa, wr, lane);
+  mma<1, 1, ASM>(t, fa, fb);
+  barrier();
+  if constexpr (STAGE) sa.template stage<KTAIL>(nxt, 1, k0n);
+  load_b<0>(fb, cur, sb, wc, lane);
+  mma<1, 0, ASM>(t, fa, fb);
 }
 
 template <bool KM, int HS>
@@ -361,11 +378,11 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(const __bf16* __restr
     for (int j = 0; j < 4; ++j) t.acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = (K + kBK - 1) / kBK;
-  // prologue: all of K-tile 0 (A0 B0 A1 B1, the order the loop's phases stage in)
+  // prologue: all of K-tile 0 (A0 B0 B1 A1, the order the loop's phases stage in)
   sa.template stage<true>(smem, 0, 0);
   sb.template stage<true>(smem + kImg, 0, 0);
-  sa.template stage<true>(smem, 1, 0);
   sb.template stage<true>(smem + kImg, 1, 0);
+  sa.template stage<true>(smem, 1, 0);
   int kt = 0;
   // the last K-tile may be partial (K % 64 != 0): only its staging checks k against K
   for (; kt + 2 < nk; ++kt) {

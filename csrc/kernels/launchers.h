@@ -208,7 +208,9 @@ hipError_t cs_bn_bwd_apply(const float* y, const float* G, int B, int H, int W, 
 // ---------------------------------------------------------------- ordering-probe communicator (comm_probe.hip)
 enum { CS_SCRAMBLE_F32 = 0, CS_SCRAMBLE_I64 = 1, CS_SCRAMBLE_I32 = 2 };
 // a bounded (<= 0.1 s) busy wait of `us` microseconds on `stream`
-hipError_t cs_comm_spin(double us, hipStream_t stream);
+// ctas > 0: that many busy 256-thread workgroups (an RCCL collective's CTA footprint) instead
+// of one sleeping wave; sink: 256 floats never written in practice
+hipError_t cs_comm_spin(double us, hipStream_t stream, int ctas = 0, float* sink = nullptr);
 // exact invertible scramble: floats x2 (inverse x0.5), integers +1 (inverse -1)
 hipError_t cs_comm_scramble(void* buf, int64_t n, int kind, int inverse, hipStream_t stream);
 

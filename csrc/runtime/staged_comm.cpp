@@ -128,14 +128,21 @@ void StagedComm::abort() {
 
 // ------------------------------------------------------------------------------ ProbeComm
 
-ProbeComm::ProbeComm(int device, double spin_us, double gbps, int world)
-    : spin_us_(spin_us), gbps_(gbps), model_world_(world < 2 ? 2 : world) {
+ProbeComm::ProbeComm(int device, double spin_us, double gbps, int world, int ctas)
+    : spin_us_(spin_us), gbps_(gbps), model_world_(world < 2 ? 2 : world), ctas_(ctas) {
+  if (ctas_ < 0 || ctas_ > 256) throw std::runtime_error("ProbeComm: ctas must be in [0, 256]");
   make_stream(device, &stream_);
+  if (ctas_ > 0) {
+    void* p = nullptr;
+    hip_ok(hipMalloc(&p, 256 * sizeof(float)), "probe sink");
+    sink_ = static_cast<float*>(p);
+  }
 }
 
 ProbeComm::~ProbeComm() {
   if (stream_) hipStreamSynchronize(stream_);
   if (stream_) hipStreamDestroy(stream_);
+  if (sink_) hipFree(sink_);
 }
 
 void ProbeComm::scramble(void* buf, size_t count, ncclDataType_t dt) {
@@ -163,7 +170,7 @@ void ProbeComm::all_reduce(void* buf, size_t count, ncclDataType_t dt, ncclRedOp
   if (gbps_ > 0.0) {  // xGMI ring model: 1e3 B/us per GB/s
     const double bytes = (double)count * (dt == ncclInt64 || dt == ncclFloat64 ? 8 : 4);
     const double w = (double)model_world_;
-    hip_ok(cs_comm_spin(spin_us_ + 2.0 * (w - 1.0) / w * bytes / (gbps_ * 1e3), stream_), "model spin");
+    hip_ok(cs_comm_spin(spin_us_ + 2.0 * (w - 1.0) / w * bytes / (gbps_ * 1e3), stream_, ctas_, sink_), "model spin");
     return;
   }
   scramble(buf, count, dt);
@@ -175,7 +182,7 @@ void ProbeComm::broadcast(void* buf, size_t count, ncclDataType_t dt, int, hipSt
   if (do_fork) bridge_.fork(compute, stream_);
   if (gbps_ > 0.0) {
     const double bytes = (double)count * (dt == ncclInt64 || dt == ncclFloat64 ? 8 : 4);
-    hip_ok(cs_comm_spin(spin_us_ + bytes / (gbps_ * 1e3), stream_), "model spin");
+    hip_ok(cs_comm_spin(spin_us_ + bytes / (gbps_ * 1e3), stream_, ctas_, sink_), "model spin");
     return;
   }
   scramble(buf, count, dt);

@@ -70,7 +70,8 @@ class ProbeComm final : public DeviceComm {
   // gbps > 0: the xGMI model — no scramble; every all-reduce is a spin of spin_us + the ring time
   // 2 (W-1)/W * bytes / gbps of a W-GPU ring, every broadcast spin_us + bytes / gbps, so the step
   // runs its fork / collective / comm-stream SGD / join schedule with modelled collective durations
-  ProbeComm(int device, double spin_us, double gbps = 0.0, int world = 8);
+  // ctas > 0: each modelled collective also occupies that many CUs with busy workgroups
+  ProbeComm(int device, double spin_us, double gbps = 0.0, int world = 8, int ctas = 0);
   ~ProbeComm() override;
   ProbeComm(const ProbeComm&) = delete;
   ProbeComm& operator=(const ProbeComm&) = delete;
@@ -91,6 +92,8 @@ class ProbeComm final : public DeviceComm {
   StreamBridge bridge_;
   double spin_us_ = 0.0, gbps_ = 0.0;
   int model_world_ = 8;
+  int ctas_ = 0;
+  float* sink_ = nullptr;
   int64_t calls_ = 0;
 };
 

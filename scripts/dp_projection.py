@@ -6,9 +6,10 @@ comm stream, the BN-buffer broadcast, the closing join — against a probe commu
 (ProbeComm "xgmi:G:W:us") whose every all-reduce is a spin as long as a W-GPU ring all-reduce of its
 bytes at G GB/s bus bandwidth plus a per-call latency: t = us + 2 (W-1)/W * bytes / G. Compute per
 GPU is what weak scaling keeps fixed (B = 64 per GPU), so the projected W-GPU throughput is
-W * B / t_step. Not modelled: RCCL's CTAs (CS_COMM_CTAS, default 16 of 256 CUs) competing with the
-backward GEMMs while a collective runs (bounded below by the CU share: <= 16/256 = 6 % of the
-overlapped GEMM time), and rank skew.
+W * B / t_step. RCCL's CTAs (CS_COMM_CTAS, default 16 of 256 CUs) competing with the backward GEMMs
+while a collective runs are priced with --ctas: the modelled collective then runs as that many busy
+workgroups (dependent FMA chains) instead of one sleeping wave. Not modelled: rank skew, and the
+memory traffic of the real copy-reduce.
 
 Usage (GPU box): python scripts/dp_projection.py [--steps 50] [--gbps 100,150,300] [--worlds 2,4,8]
 """
@@ -49,6 +50,8 @@ def main():
     p.add_argument("--gbps", type=str, default="100,150,300")
     p.add_argument("--worlds", type=str, default="2,4,8")
     p.add_argument("--latency-us", type=float, default=25.0)
+    p.add_argument("--ctas", type=str, default="0,8,16,32",
+                   help="busy workgroups standing in for RCCL's CTAs during each collective (0: one sleeping wave)")
     a = p.parse_args()
     torch.cuda.set_device(0)
     base, ph0, buckets = run("0", a.steps, a.warmup)
@@ -57,11 +60,13 @@ def main():
                       "phases_ms": {k: round(v, 4) for k, v in ph0.items()}}), flush=True)
     for g in [float(x) for x in a.gbps.split(",")]:
         for w in [int(x) for x in a.worlds.split(",")]:
-            ms, ph, _ = run(f"xgmi:{g}:{w}:{a.latency_us}", a.steps, a.warmup)
-            print(json.dumps({"config": f"projected N={w}, ring busBW {g:g} GB/s, {a.latency_us:g} us/collective",
-                              "ms_per_step": round(ms, 4), "projected_img_s": round(w * 64 / ms * 1e3),
-                              "per_gpu_img_s": round(64 / ms * 1e3), "efficiency_vs_world1": round(base / ms, 4),
-                              "allreduce_wait_ms": round(ph.get("allreduce_wait", 0.0), 4)}), flush=True)
+            for c in [int(x) for x in a.ctas.split(",")]:
+                ms, ph, _ = run(f"xgmi:{g}:{w}:{a.latency_us}:{c}", a.steps, a.warmup)
+                print(json.dumps({"config": f"projected N={w}, ring busBW {g:g} GB/s, {a.latency_us:g} us/collective, "
+                                            f"{c} busy CTAs per collective",
+                                  "ms_per_step": round(ms, 4), "projected_img_s": round(w * 64 / ms * 1e3),
+                                  "per_gpu_img_s": round(64 / ms * 1e3), "efficiency_vs_world1": round(base / ms, 4),
+                                  "allreduce_wait_ms": round(ph.get("allreduce_wait", 0.0), 4)}), flush=True)
 
 
 if __name__ == "__main__":
