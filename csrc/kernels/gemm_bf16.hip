@@ -43,6 +43,7 @@
 //    that XCD's L2.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "launchers.h"
 
@@ -257,6 +258,35 @@ __device__ __forceinline__ void ktile(Tile& t, const char* cur, char* nxt, const
   mma<1, 0, ASM>(t, fa, fb);
 }
 
+// SCHED 1: one barrier per K-tile. The wave waits for all of this K-tile's DMAs (issued one tile
+// earlier), passes the barrier, issues all of the next K-tile's DMAs and then runs the 4 quadrant
+// phases without any barrier, so the two waves of a SIMD drift apart and one's fragment reads
+// overlap the other's MFMAs (the per-phase barriers of SCHED 0 keep them in lockstep: both read,
+// then both multiply). Each DMA has one whole K-tile (~2000 clocks) to land.
+template <bool STAGE, bool KTAIL, class SA, class SB>
+__device__ __forceinline__ void ktile_free(Tile& t, const char* cur, char* nxt, const SA& sa, const SB& sb, int k0n,
+                                           int wr, int wc, int lane) {
+  constexpr bool ASM = !SA::kRowRead || !SB::kRowRead;
+  bf16x8 fa[4][2], fb[2][2];
+  wait_vm<0>();
+  barrier();
+  if constexpr (STAGE) {
+    sa.template stage<KTAIL>(nxt, 0, k0n);
+    sb.template stage<KTAIL>(nxt + kImg, 0, k0n);
+    sb.template stage<KTAIL>(nxt + kImg, 1, k0n);
+    sa.template stage<KTAIL>(nxt, 1, k0n);
+  }
+  load_a<0>(fa, cur, sa, wr, lane);
+  load_b<0>(fb, cur, sb, wc, lane);
+  mma<0, 0, ASM>(t, fa, fb);
+  load_b<1>(fb, cur, sb, wc, lane);
+  mma<0, 1, ASM>(t, fa, fb);
+  load_a<1>(fa, cur, sa, wr, lane);
+  mma<1, 1, ASM>(t, fa, fb);
+  load_b<0>(fb, cur, sb, wc, lane);
+  mma<1, 0, ASM>(t, fa, fb);
+}
+
 template <bool KM, int HS>
 struct Op;
 template <int HS>
@@ -346,7 +376,7 @@ __device__ __forceinline__ void tile_stats(const Tile& t, int M, int N, int m0, 
 // own C slab C + s * slab (fp32 partials, summed by cs_slab_sum)
 // STATS (bf16 C, no split): per-channel BatchNorm statistics of this tile's bf16 outputs, tile
 // mean and M2 = sum (y - mean)^2 per column, into stats[tile row][N][2] (see tile_stats below)
-template <int OUT, bool AK, bool BK, bool STATS = false>
+template <int OUT, bool AK, bool BK, bool STATS = false, int SCHED = 0>
 __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B,
                                                         void* __restrict__ C, int M, int N, int K, int64_t lda,
                                                         int64_t ldb, int64_t ldc, int kper, int64_t slab,
@@ -385,17 +415,29 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(const __bf16* __restr
   sa.template stage<true>(smem, 1, 0);
   int kt = 0;
   // the last K-tile may be partial (K % 64 != 0): only its staging checks k against K
-  for (; kt + 2 < nk; ++kt) {
-    char* cur = smem + (kt & 1) * kBuf;
-    char* nxt = smem + ((kt + 1) & 1) * kBuf;
-    ktile<true, false, 4>(t, cur, nxt, sa, sb, (kt + 1) * kBK, wr, wc, lane);
+  if constexpr (SCHED == 1) {
+    for (; kt + 2 < nk; ++kt)
+      ktile_free<true, false>(t, smem + (kt & 1) * kBuf, smem + ((kt + 1) & 1) * kBuf, sa, sb, (kt + 1) * kBK, wr, wc,
+                              lane);
+    if (kt + 1 < nk) {
+      ktile_free<true, true>(t, smem + (kt & 1) * kBuf, smem + ((kt + 1) & 1) * kBuf, sa, sb, (kt + 1) * kBK, wr, wc,
+                             lane);
+      ++kt;
+    }
+    ktile_free<false, false>(t, smem + (kt & 1) * kBuf, nullptr, sa, sb, 0, wr, wc, lane);
+  } else {
+    for (; kt + 2 < nk; ++kt) {
+      char* cur = smem + (kt & 1) * kBuf;
+      char* nxt = smem + ((kt + 1) & 1) * kBuf;
+      ktile<true, false, 4>(t, cur, nxt, sa, sb, (kt + 1) * kBK, wr, wc, lane);
+    }
+    if (kt + 1 < nk) {
+      ktile<true, true, 4>(t, smem + (kt & 1) * kBuf, smem + ((kt + 1) & 1) * kBuf, sa, sb, (kt + 1) * kBK, wr, wc,
+                           lane);
+      ++kt;
+    }
+    ktile<false, false, 0>(t, smem + (kt & 1) * kBuf, nullptr, sa, sb, 0, wr, wc, lane);
   }
-  if (kt + 1 < nk) {
-    ktile<true, true, 4>(t, smem + (kt & 1) * kBuf, smem + ((kt + 1) & 1) * kBuf, sa, sb, (kt + 1) * kBK, wr, wc,
-                         lane);
-    ++kt;
-  }
-  ktile<false, false, 0>(t, smem + (kt & 1) * kBuf, nullptr, sa, sb, 0, wr, wc, lane);
 
   // epilogue: acc[i][j] register e = C[row m0 + wr*128 + i*16 + (lane & 15)][col n0 + wc*64 + j*16 + (lane >> 4)*4 + e]
 #pragma unroll
@@ -439,10 +481,21 @@ struct Geo {
   int64_t slab;
 };
 
+// K-loop schedule (measurement toggle while the two are compared): CS_GEMM_SCHED=1 one barrier
+// per K-tile, else the 4-phase counted-vmcnt pipeline
+int g_sched = [] {
+  const char* e = getenv("CS_GEMM_SCHED");
+  return e != nullptr && atoi(e) == 1 ? 1 : 0;
+}();
+
 template <int OUT, bool AK, bool BK>
 void launch(const __bf16* a, const __bf16* b, void* c, const Geo& g, dim3 grid, hipStream_t stream) {
-  hipLaunchKernelGGL((gemm_kernel<OUT, AK, BK>), grid, dim3(kThreads), 0, stream, a, b, c, g.M, g.N, g.K, g.lda, g.ldb,
-                     g.ldc, g.kper, g.slab, nullptr);
+  if (g_sched == 1)
+    hipLaunchKernelGGL((gemm_kernel<OUT, AK, BK, false, 1>), grid, dim3(kThreads), 0, stream, a, b, c, g.M, g.N, g.K,
+                       g.lda, g.ldb, g.ldc, g.kper, g.slab, nullptr);
+  else
+    hipLaunchKernelGGL((gemm_kernel<OUT, AK, BK>), grid, dim3(kThreads), 0, stream, a, b, c, g.M, g.N, g.K, g.lda,
+                       g.ldb, g.ldc, g.kper, g.slab, nullptr);
 }
 
 template <int OUT>
@@ -509,4 +562,9 @@ hipError_t cs_gemm_bf16_bn_stats(const void* A, int64_t lda, const void* B, int6
                      static_cast<const __bf16*>(A), static_cast<const __bf16*>(B), C, M, N, K, lda, ldb, ldc, K,
                      (int64_t)0, stats);
   return hipGetLastError();
+}
+
+int cs_gemm_bf16_sched(int sched) {
+  if (sched == 0 || sched == 1) g_sched = sched;
+  return g_sched;
 }
