@@ -111,15 +111,17 @@ def rope(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
 # ------------------------------------------------------------------ bf16 projections with fp32 masters
 # "native": the gfx950 matrix-core GEMM of csrc/kernels/gemm_bf16.hip runs all three products of a
 # projection (y = x W^T, dx = dy W, dW = dy^T x, the last two reading the operands transposed in
-# LDS, no copies); "blas": torch.mm (hipBLASLt). scripts/gemm_bench.py compares them per shape.
+# LDS, no copies); "wgrad": it runs the fp32 weight gradient dW only (where it measured faster
+# than hipBLASLt at every Llama-3-8B shape, profiles/r4_gemm_bench_v2.jsonl); "blas": torch.mm
+# (hipBLASLt) for all three. scripts/gemm_bench.py compares them per shape.
 _GEMM = os.environ.get("CS_LM_GEMM", "blas")
-if _GEMM not in ("native", "blas"):
-    raise ValueError(f"CS_LM_GEMM must be 'native' or 'blas', got {_GEMM!r}")
+if _GEMM not in ("native", "wgrad", "blas"):
+    raise ValueError(f"CS_LM_GEMM must be 'native', 'wgrad' or 'blas', got {_GEMM!r}")
 
 
 def _mm(a: torch.Tensor, b: torch.Tensor, out_f32: bool = False) -> torch.Tensor:
-    """a @ b for bf16 2-D operands (views allowed), bf16 or fp32 out"""
-    if _GEMM == "native":
+    """a @ b for bf16 2-D operands (views allowed), bf16 or fp32 out (fp32: the weight gradient)"""
+    if _GEMM == "native" or (_GEMM == "wgrad" and out_f32):
         return native.C().mm_bf16(a, b, out_f32)
     if out_f32:
         return torch.mm(a, b, out_dtype=torch.float32)

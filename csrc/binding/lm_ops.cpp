@@ -179,7 +179,7 @@ torch::Tensor mm_bf16(torch::Tensor a, torch::Tensor b, bool out_f32, c10::optio
   // fp32 results of a reduction too long for the output's tile count are split over K into slabs
   int S = splits >= 0 ? (int)splits : cs_gemm_bf16_splits((int)M, (int)N, (int)K);
   if ((!out_f32 && !acc.has_value()) || mode_bf16_acc(acc)) S = 1;
-  TORCH_CHECK(S >= 1 && S <= 64, "mm_bf16: splits out of range");
+  TORCH_CHECK(S >= 1 && S <= 256, "mm_bf16: splits out of range");
   if (acc.has_value()) {
     c = *acc;
     TORCH_CHECK(c.is_cuda() && (c.scalar_type() == at::kFloat || c.scalar_type() == at::kBFloat16) && c.dim() == 2 &&

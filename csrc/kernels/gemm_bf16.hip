@@ -510,11 +510,11 @@ void launch_layout(int ak, int bk, const __bf16* a, const __bf16* b, void* c, co
 }  // namespace
 
 int cs_gemm_bf16_splits(int M, int N, int K) {
-  // split the reduction only when the output alone leaves most CUs idle: about one wave of
-  // workgroups over the 256 CUs, >= 1024 k per split, <= 8 splits
+  // split the reduction only when the output alone leaves CUs idle: up to about two waves of
+  // workgroups over the 256 CUs, >= 1024 k per split, fp32 slabs within 1 GiB
   const int64_t tiles = (int64_t)((M + kTile - 1) / kTile) * ((N + kTile - 1) / kTile);
   int s = 1;
-  while (s < 8 && tiles * s * 2 <= 256 && K / (2 * s) >= 1024) s *= 2;
+  while (s < 256 && tiles * s * 2 <= 512 && K / (2 * s) >= 1024 && (int64_t)2 * s * M * N * 4 <= (1LL << 30)) s *= 2;
   return s;
 }
 

@@ -8,7 +8,9 @@ import sys
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-import cs744_pytorch_distributed_tutorial_amd  # noqa: F401,E402  (sets the HIP queue count first)
+import cs744_pytorch_distributed_tutorial_amd as _pkg  # noqa: E402
+
+_pkg.ensure_hw_queues()  # before HIP starts, as bench.py does
 import torch  # noqa: E402
 
 

@@ -19,7 +19,11 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-import cs744_pytorch_distributed_tutorial_amd  # noqa: F401,E402
+import cs744_pytorch_distributed_tutorial_amd as _pkg  # noqa: E402
+
+# the engine overlaps weight gradients on a side stream next to a communicator only with >= 8 HIP
+# hardware queues (bench.py does the same before HIP starts)
+_pkg.ensure_hw_queues()
 import torch  # noqa: E402
 
 
@@ -54,6 +58,8 @@ def main():
                    help="busy workgroups standing in for RCCL's CTAs during each collective (0: one sleeping wave)")
     a = p.parse_args()
     torch.cuda.set_device(0)
+    from cs744_pytorch_distributed_tutorial_amd.ops import native
+    native.C().reserve_streams()  # the side stream owns a hardware queue (as in bench.py)
     base, ph0, buckets = run("0", a.steps, a.warmup)
     print(json.dumps({"config": "world 1 (no communicator)", "ms_per_step": round(base, 4),
                       "img_s": round(64 / base * 1e3), "bucket_mib": [round(b, 2) for b in buckets],
