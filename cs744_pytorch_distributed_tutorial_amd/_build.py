@@ -86,9 +86,9 @@ def _compile_cmd(src: str, obj: str):
             "-o", obj]
 
 
-def _link_cmd(objs):
+def _link_cmd(objs, out=OUT):
     _, _, tlib = _torch_paths()
-    return [HIPCC, "-shared", f"--offload-arch={ARCH}", "-fgpu-rdc" if False else "-fPIC", "-o", OUT, *objs,
+    return [HIPCC, "-shared", f"--offload-arch={ARCH}", "-fgpu-rdc" if False else "-fPIC", "-o", out, *objs,
             f"-L{tlib}", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-lc10", "-lc10_hip", "-ltorch_python",
             "-l:libamdhip64.so", "-l:librccl.so", f"-Wl,-rpath,{tlib}", "-Wl,--no-as-needed"]
 
@@ -119,13 +119,19 @@ def build(jobs: int = 0, force: bool = False, verbose: bool = False) -> str:
             for s in ex.map(run, todo):
                 print(f"[build] compiled {os.path.relpath(s, ROOT)}", flush=True)
     if todo or not os.path.exists(OUT) or any(os.path.getmtime(o) > os.path.getmtime(OUT) for o in objs):
-        cmd = _link_cmd(objs)
+        # link to a temporary name and rename: a reader (an import, a tree snapshot) never sees a
+        # half-written library
+        tmp = OUT + f".tmp{os.getpid()}"
+        cmd = _link_cmd(objs, tmp)
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
+            if os.path.exists(tmp):
+                os.remove(tmp)
             raise RuntimeError(f"link failed\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+        _check_stubs(tmp)
+        os.replace(tmp, OUT)
         print(f"[build] linked {os.path.relpath(OUT, ROOT)} ({len(objs)} objects, {time.time() - t0:.1f}s)",
               flush=True)
-        _check_stubs(OUT)
     return OUT
 
 
