@@ -79,8 +79,8 @@ def _native_gemm(a: torch.Tensor, n: int) -> bool:
 
 # a native-GEMM forward convolution also returns its output's BatchNorm statistics per 256-row
 # tile (the GEMM epilogue, gemm_bf16.hip tile_stats); the BatchNorm reading that output then skips
-# its statistics pass (cs_bn_nhwc_fwd_tiles). CS_CONV_BN_STATS=0: the separate pass.
-_BN_STATS = os.environ.get("CS_CONV_BN_STATS", "1") != "0"
+# its statistics pass (cs_bn_nhwc_fwd_tiles)
+_BN_STATS = True
 
 
 def _wgrad(dy2: torch.Tensor, col: torch.Tensor) -> torch.Tensor:
@@ -95,7 +95,7 @@ def _wgrad(dy2: torch.Tensor, col: torch.Tensor) -> torch.Tensor:
     a = dy2.view(S, M // S, Co).transpose(1, 2)
     b = col.view(S, M // S, Kp)
     part = torch.bmm(a, b, out_dtype=torch.float32) if col.dtype != torch.float32 else torch.bmm(a, b)
-    if Co * Kp % 4 == 0 and os.environ.get("CS_SLAB_SUM", "1") != "0":
+    if Co * Kp % 4 == 0:
         return native.C().slab_sum(part)  # split-lane slab sum (csrc/kernels/conv_nhwc.hip)
     return part.sum(0)
 
@@ -163,8 +163,8 @@ class _ConvImplicitNHWC(torch.autograd.Function):
 def _stem_ok(x: torch.Tensor, Ci: int, Co: int, S: int) -> bool:
     """the 4-channel stem (image + a zero channel) as the implicit-GEMM kernel's C4 mode: forward and
     weight gradient without the [B*Ho*Wo, R*S*4] patch matrix (1.3 GB for ResNet-50 at B=256, written
-    by im2col and read twice). The image needs no gradient. CS_CONV_IMPLICIT=0 or CS_CONV_STEM=0 disables."""
-    return (os.environ.get("CS_CONV_IMPLICIT", "1") != "0" and os.environ.get("CS_CONV_STEM", "1") != "0"
+    by im2col and read twice). The image needs no gradient. CS_CONV_IMPLICIT=0 disables."""
+    return (os.environ.get("CS_CONV_IMPLICIT", "1") != "0"
             and act_dtype(x) == torch.bfloat16 and x.shape[3] == 4
             and Ci <= 4 and S <= 8 and Co % 32 == 0 and not x.requires_grad)
 

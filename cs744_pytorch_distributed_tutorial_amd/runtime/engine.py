@@ -457,7 +457,7 @@ class NativeTrainer:
         ranges = [v for r in self.bucket_ranges for v in r]
         probe = self.world == 1 and self.native_comm is not None
         self.engine.step(B, self.native_comm, self.bucket_lows, ranges,
-                         self.broadcast_buffers and (self.world > 1 or probe) and not os.environ.get("CS_NO_BCAST"),
+                         self.broadcast_buffers and (self.world > 1 or probe),
                          self.lr, self.momentum, self.wd, self.damp)
 
     def _pre_forward_sync(self) -> None:

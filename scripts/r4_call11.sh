@@ -17,3 +17,13 @@ import json,sys
 for l in sys.stdin:
     d=json.loads(l) if l.startswith('{') else None
     d and print(d['shape'], d['product'], d['ours_tflops_med'], d['hipblaslt_tflops_med'], d['ours_vs_hipblaslt'], d.get('sched1_vs_hipblaslt'), d.get('sched2_vs_hipblaslt'))"
+# same-box kernel traces of the round-2 tree and the working tree (where is round 2's remaining lead?)
+R=$PWD
+trace_tree() {
+  (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --marker-trace --stats -d $R/gpurun_out/$2 -o run -- \
+    python3 $R/$1/bench.py --steps 10 --warmup 5 > $R/gpurun_out/$2.log 2>&1) || return $?
+  python3 scripts/prof_summary.py gpurun_out/$2 --steps 15 --top 45 > gpurun_out/${2}_kernels.txt 2>&1
+  python3 scripts/step_timeline.py gpurun_out/$2 > gpurun_out/${2}_timeline.txt 2>&1
+  tail -3 gpurun_out/${2}_timeline.txt
+}
+trace_tree .ab/r2 r2_trace && trace_tree . r4_trace

@@ -1,5 +1,5 @@
 """ResNet-50 stem (3 -> 64, 7x7/2, B x 224 x 224 image padded to 4 channels, bf16): forward and
-forward + weight-gradient time of ops/cnn_nhwc.conv_nhwc, C4 implicit kernel (CS_CONV_STEM=1) vs
+forward + weight-gradient time of ops/cnn_nhwc.conv_nhwc, C4 implicit kernel (CS_CONV_IMPLICIT=1) vs
 im2col + hipBLASLt (=0), CUDA-event timed. One JSON line per mode."""
 import json
 import os
@@ -32,7 +32,7 @@ def timed(fn):
 
 
 for mode in ("0", "1"):
-    os.environ["CS_CONV_STEM"] = mode
+    os.environ["CS_CONV_IMPLICIT"] = mode
 
     def fwd():
         with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
