@@ -812,6 +812,8 @@ int cs_gemm_bf16_splits(int M, int N, int K) {
   const int64_t tiles = (int64_t)((M + kTile - 1) / kTile) * ((N + kTile - 1) / kTile);
   int s = 1;
   while (s < 256 && tiles * s * 2 <= 512 && K / (2 * s) >= 1024 && (int64_t)2 * s * M * N * 4 <= (1LL << 30)) s *= 2;
+  // K per split is rounded up to whole K-tiles: keep every split non-empty
+  while (s > 1 && (int64_t)(((K + s - 1) / s + kBK - 1) / kBK * kBK) * (s - 1) >= K) --s;
   return s;
 }
 

@@ -27,3 +27,6 @@ trace_tree() {
   tail -3 gpurun_out/${2}_timeline.txt
 }
 trace_tree .ab/r2 r2_trace && trace_tree . r4_trace
+bash scripts/ab_trees.sh 2 .:CS_CONV_GEMM=blas .:CS_CONV_GEMM=auto -- --model resnet50 --dtype bf16 --steps 10 \
+  --warmup 4 > gpurun_out/ab_resnet_gemm.log 2>&1 || exit $?
+tail -2 gpurun_out/ab_resnet_gemm.log
