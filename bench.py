@@ -218,6 +218,14 @@ def main(argv=None) -> int:
     wd = Watchdog(args.watchdog_s, "bench step", on_timeout=getattr(trainer, "abort", None)).start() \
         if args.watchdog_s > 0 else None
 
+    # no Python garbage-collector pass inside the timed steps: a full collection of the
+    # interpreter's heap takes milliseconds, as long as a short window's whole budget (one
+    # 20-step run measured a one-off 0.98 ms/step against 0.72-0.74 in five repeats). Collect
+    # before the warmup steps, not between them and the timed ones, so the timed window does not
+    # start behind a millisecond of idle GPU (profiles/r4_bench_windows.jsonl)
+    import gc
+    gc.collect()
+    gc.disable()
     for _ in range(args.warmup):
         trainer.step()
         if wd is not None:
@@ -225,12 +233,6 @@ def main(argv=None) -> int:
     torch.cuda.synchronize()
     D.barrier()
     torch.cuda.synchronize()
-    # no Python garbage-collector pass inside the timed steps: a full collection of the
-    # interpreter's heap takes milliseconds, as long as a short window's whole budget (one
-    # 20-step run measured a one-off 0.98 ms/step against 0.72-0.74 in five repeats)
-    import gc
-    gc.collect()
-    gc.disable()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         trainer.step()
