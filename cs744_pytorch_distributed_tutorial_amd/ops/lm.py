@@ -114,7 +114,7 @@ def rope(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
 # LDS, no copies); "wgrad": it runs the fp32 weight gradient dW only (where it measured faster
 # than hipBLASLt at every Llama-3-8B shape, profiles/r4_gemm_bench_v2.jsonl); "blas": torch.mm
 # (hipBLASLt) for all three. scripts/gemm_bench.py compares them per shape.
-_GEMM = os.environ.get("CS_LM_GEMM", "blas")
+_GEMM = os.environ.get("CS_LM_GEMM", "wgrad")
 if _GEMM not in ("native", "wgrad", "blas"):
     raise ValueError(f"CS_LM_GEMM must be 'native', 'wgrad' or 'blas', got {_GEMM!r}")
 

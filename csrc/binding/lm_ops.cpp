@@ -240,6 +240,5 @@ void register_lm_ops(pybind11::module& m) {
   m.def("attn_bwd", &attn_bwd, "flash attention backward -> dq, dk, dv");
   m.def("mm_bf16", &mm_bf16, "C = a @ b on the bf16 matrix cores", pybind11::arg("a"), pybind11::arg("b"),
         pybind11::arg("out_f32") = false, pybind11::arg("acc") = c10::nullopt, pybind11::arg("splits") = -1);
-  m.def("gemm_bf16_sched", &cs_gemm_bf16_sched, "set (0 / 1) or query (-1) the bf16 GEMM K-loop schedule");
   m.def("mm_bf16_bn_stats", &mm_bf16_bn_stats, "a @ b (bf16) plus per-256-row-tile BatchNorm (mean, M2) of the result");
 }

@@ -43,7 +43,6 @@
 //    that XCD's L2.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
-#include <stdlib.h>
 
 #include "launchers.h"
 
@@ -258,35 +257,6 @@ __device__ __forceinline__ void ktile(Tile& t, const char* cur, char* nxt, const
   mma<1, 0, ASM>(t, fa, fb);
 }
 
-// SCHED 1: one barrier per K-tile. The wave waits for all of this K-tile's DMAs (issued one tile
-// earlier), passes the barrier, issues all of the next K-tile's DMAs and then runs the 4 quadrant
-// phases without any barrier, so the two waves of a SIMD drift apart and one's fragment reads
-// overlap the other's MFMAs (the per-phase barriers of SCHED 0 keep them in lockstep: both read,
-// then both multiply). Each DMA has one whole K-tile (~2000 clocks) to land.
-template <bool STAGE, bool KTAIL, class SA, class SB>
-__device__ __forceinline__ void ktile_free(Tile& t, const char* cur, char* nxt, const SA& sa, const SB& sb, int k0n,
-                                           int wr, int wc, int lane) {
-  constexpr bool ASM = !SA::kRowRead || !SB::kRowRead;
-  bf16x8 fa[4][2], fb[2][2];
-  wait_vm<0>();
-  barrier();
-  if constexpr (STAGE) {
-    sa.template stage<KTAIL>(nxt, 0, k0n);
-    sb.template stage<KTAIL>(nxt + kImg, 0, k0n);
-    sb.template stage<KTAIL>(nxt + kImg, 1, k0n);
-    sa.template stage<KTAIL>(nxt, 1, k0n);
-  }
-  load_a<0>(fa, cur, sa, wr, lane);
-  load_b<0>(fb, cur, sb, wc, lane);
-  mma<0, 0, ASM>(t, fa, fb);
-  load_b<1>(fb, cur, sb, wc, lane);
-  mma<0, 1, ASM>(t, fa, fb);
-  load_a<1>(fa, cur, sa, wr, lane);
-  mma<1, 1, ASM>(t, fa, fb);
-  load_b<0>(fb, cur, sb, wc, lane);
-  mma<1, 0, ASM>(t, fa, fb);
-}
-
 template <bool KM, int HS>
 struct Op;
 template <int HS>
@@ -376,7 +346,7 @@ __device__ __forceinline__ void tile_stats(const Tile& t, int M, int N, int m0, 
 // own C slab C + s * slab (fp32 partials, summed by cs_slab_sum)
 // STATS (bf16 C, no split): per-channel BatchNorm statistics of this tile's bf16 outputs, tile
 // mean and M2 = sum (y - mean)^2 per column, into stats[tile row][N][2] (see tile_stats below)
-template <int OUT, bool AK, bool BK, bool STATS = false, int SCHED = 0>
+template <int OUT, bool AK, bool BK, bool STATS = false>
 __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B,
                                                         void* __restrict__ C, int M, int N, int K, int64_t lda,
                                                         int64_t ldb, int64_t ldc, int kper, int64_t slab,
@@ -415,29 +385,17 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(const __bf16* __restr
   sa.template stage<true>(smem, 1, 0);
   int kt = 0;
   // the last K-tile may be partial (K % 64 != 0): only its staging checks k against K
-  if constexpr (SCHED == 1) {
-    for (; kt + 2 < nk; ++kt)
-      ktile_free<true, false>(t, smem + (kt & 1) * kBuf, smem + ((kt + 1) & 1) * kBuf, sa, sb, (kt + 1) * kBK, wr, wc,
-                              lane);
-    if (kt + 1 < nk) {
-      ktile_free<true, true>(t, smem + (kt & 1) * kBuf, smem + ((kt + 1) & 1) * kBuf, sa, sb, (kt + 1) * kBK, wr, wc,
-                             lane);
-      ++kt;
-    }
-    ktile_free<false, false>(t, smem + (kt & 1) * kBuf, nullptr, sa, sb, 0, wr, wc, lane);
-  } else {
-    for (; kt + 2 < nk; ++kt) {
-      char* cur = smem + (kt & 1) * kBuf;
-      char* nxt = smem + ((kt + 1) & 1) * kBuf;
-      ktile<true, false, 4>(t, cur, nxt, sa, sb, (kt + 1) * kBK, wr, wc, lane);
-    }
-    if (kt + 1 < nk) {
-      ktile<true, true, 4>(t, smem + (kt & 1) * kBuf, smem + ((kt + 1) & 1) * kBuf, sa, sb, (kt + 1) * kBK, wr, wc,
-                           lane);
-      ++kt;
-    }
-    ktile<false, false, 0>(t, smem + (kt & 1) * kBuf, nullptr, sa, sb, 0, wr, wc, lane);
+  for (; kt + 2 < nk; ++kt) {
+    char* cur = smem + (kt & 1) * kBuf;
+    char* nxt = smem + ((kt + 1) & 1) * kBuf;
+    ktile<true, false, 4>(t, cur, nxt, sa, sb, (kt + 1) * kBK, wr, wc, lane);
   }
+  if (kt + 1 < nk) {
+    ktile<true, true, 4>(t, smem + (kt & 1) * kBuf, smem + ((kt + 1) & 1) * kBuf, sa, sb, (kt + 1) * kBK, wr, wc,
+                         lane);
+    ++kt;
+  }
+  ktile<false, false, 0>(t, smem + (kt & 1) * kBuf, nullptr, sa, sb, 0, wr, wc, lane);
 
   // epilogue: acc[i][j] register e = C[row m0 + wr*128 + i*16 + (lane & 15)][col n0 + wc*64 + j*16 + (lane >> 4)*4 + e]
 #pragma unroll
@@ -474,299 +432,6 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_kernel(const __bf16* __restr
   }
 }
 
-// ------------------------------------------------------------------------------------------
-// 4-wave variant (SCHED 2): the same 256 x 256 tile on 4 waves of 128 x 128 (8 x 8 MFMA tiles, 256
-// accumulator registers: one wave per SIMD with the whole register file), BK = 32 K-tiles in 4 LDS
-// buffers (4 x 32 KiB). A wave reads the next K-tile's 16 fragments while its 64 MFMAs run on the
-// current ones (two register sets): with one wave per SIMD nothing else would hide the LDS reads,
-// and a 128 x 128 wave tile needs 16 fragment reads per 64 MFMAs (the 8-wave 128 x 64 tile: 28 per
-// 64). One barrier per K-tile: every wave has its reads of K-tile t done (lgkmcnt 0) and K-tile
-// t + 1 landed (counted vmcnt: K-tile t + 2 stays in flight) before any wave restages the buffer
-// of K-tile t - 1 with K-tile t + 3, so each DMA has two K-tiles (~2000 clocks) to land.
-constexpr int kBK4 = 32, kThreads4 = 256;
-constexpr int kImg4 = kTile * kBK4 * 2;  // 16 KiB per operand image
-constexpr int kBuf4 = 2 * kImg4;         // A + B
-
-__device__ __forceinline__ int sw4(int r) { return (r >> 2) & 3; }
-
-// K-major operand, [256 rows][32 k] image of 64-byte rows, 16-byte chunk c at c ^ ((r >> 2) & 3)
-// (the 16 lanes of a ds_read_b128 group, 16 consecutive rows at one chunk, hit 16 distinct
-// 16-byte slots); wave w fills rows 64 w .. 64 w + 63 (4 DMA instructions of 16 rows)
-struct OpK4 {
-  static constexpr bool kRowRead = true;
-  __amdgpu_buffer_rsrc_t rs;
-  int off[4], kch[4], K;
-  __device__ OpK4(const __bf16* base, int64_t ld, int nrows, int K_) : K(K_) {
-    const int64_t bytes = nrows > 0 ? (int64_t)(nrows - 1) * ld * 2 + (int64_t)K_ * 2 : 0;
-    rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<__bf16*>(base), (short)0,
-                                           (int)(bytes < 0x7fffffff ? bytes : 0x7fffffff), 0x00020000);
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r = 64 * wv + 16 * i + (lane >> 2), kc = ((lane & 3) ^ sw4(r)) << 3;
-      kch[i] = kc;
-      off[i] = r < nrows ? r * (int)(ld * 2) + kc * 2 : kOOB;
-    }
-  }
-  template <bool KTAIL>
-  __device__ __forceinline__ void stage(char* img, int k0) const {
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      int o = off[i] == kOOB ? kOOB : off[i] + 2 * k0;
-      if constexpr (KTAIL) o = k0 + kch[i] < K ? o : kOOB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rs, (__attribute__((address_space(3))) void*)(img + (64 * wv + 16 * i) * 64), 16, o, 0, 0, 0);
-    }
-  }
-  // 16-row subtile at tile row r0: lane l gets row r0 + (l & 15), k = 8 (l >> 4) + j
-  __device__ __forceinline__ bf16x8 frag(const char* img, int r0, int lane) const {
-    const int r = r0 + (lane & 15), ch = lane >> 4;
-    return *reinterpret_cast<const bf16x8*>(img + r * 64 + ((ch ^ sw4(r)) << 4));
-  }
-};
-
-// M-major operand, memory [K][cols]: [32 k][256 columns] image of 512-byte k rows, chunk c of k
-// row kr at c ^ xs(kr) (the 8 k rows a 32-lane half of a transposed read takes land on 8 distinct
-// 32-byte bank slots); wave w fills k rows 8 w .. 8 w + 7 (4 DMA instructions of 2 k rows). The
-// buffer resource is re-based at every K-tile, so k rows past K fall outside it (zeros).
-struct OpM4 {
-  static constexpr bool kRowRead = false;
-  const __bf16* base;
-  int64_t ld;
-  int ncols, K;
-  int off[4];
-  __device__ OpM4(const __bf16* base_, int64_t ld_, int ncols_, int K_) : base(base_), ld(ld_), ncols(ncols_), K(K_) {
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int kr = 8 * wv + 2 * i + (lane >> 5), c = ((lane & 31) ^ xs(kr)) << 3;
-      off[i] = c < ncols ? kr * (int)(ld * 2) + c * 2 : kOOB;
-    }
-  }
-  template <bool KTAIL>
-  __device__ __forceinline__ void stage(char* img, int k0) const {
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int rows = K - k0 < kBK4 ? K - k0 : kBK4;
-    const int bytes = (int)((int64_t)(rows - 1) * ld * 2 + (int64_t)ncols * 2);
-    const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<__bf16*>(base + (int64_t)k0 * ld), (short)0, bytes, 0x00020000);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rs, (__attribute__((address_space(3))) void*)(img + (8 * wv + 2 * i) * 512), 16, off[i], 0, 0, 0);
-  }
-  // the OpK4::frag fragment of columns c0 .. c0 + 15 by two transposed reads (k rows 8g + q, then + 4)
-  __device__ __forceinline__ bf16x8 frag(const char* img, int c0, int lane) const {
-    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-    const int kr = 8 * g + q, ch = (c0 >> 3) + (p >> 1);
-    const char* a0 = img + kr * 512 + ((ch ^ xs(kr)) << 4) + 8 * (p & 1);
-    const unsigned ad = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)a0;
-    i32x2 lo, hi;
-    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(ad) : "memory");
-    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:2048" : "=v"(hi) : "v"(ad) : "memory");
-    const bf16x4 blo = __builtin_bit_cast(bf16x4, lo), bhi = __builtin_bit_cast(bf16x4, hi);
-    return __builtin_shufflevector(blo, bhi, 0, 1, 2, 3, 4, 5, 6, 7);
-  }
-};
-
-template <bool KM>
-struct Op4;
-template <>
-struct Op4<true> {
-  __device__ static OpK4 make(const __bf16* p, int64_t ld, int r0, int rows, int K) {
-    return OpK4(p + (int64_t)r0 * ld, ld, rows - r0 < kTile ? rows - r0 : kTile, K);
-  }
-};
-template <>
-struct Op4<false> {
-  __device__ static OpM4 make(const __bf16* p, int64_t ld, int r0, int rows, int K) {
-    return OpM4(p + r0, ld, rows - r0 < kTile ? rows - r0 : kTile, K);
-  }
-};
-
-struct Frags4 {
-  bf16x8 a[8], b[8];
-};
-
-template <class SA, class SB>
-__device__ __forceinline__ void read4(Frags4& f, const char* buf, const SA& sa, const SB& sb, int wr, int wc,
-                                      int lane) {
-#pragma unroll
-  for (int j = 0; j < 8; ++j) f.b[j] = sb.frag(buf + kImg4, wc * 128 + j * 16, lane);
-#pragma unroll
-  for (int i = 0; i < 8; ++i) f.a[i] = sa.frag(buf, wr * 128 + i * 16, lane);
-}
-
-// In-place accumulation through inline asm ("+a": srcC = vDst, an AGPR quad): with the builtin,
-// hipcc's register allocator does not keep the 256 accumulators of a 128 x 128 wave tile in place
-// (it rotates them through a scratch quad: ~1.9 v_accvgpr_mov / read per MFMA in the K loop).
-// Hazards the compiler then cannot see are covered explicitly: each accumulator is written by
-// one MFMA per 64 (no back-to-back srcC dependence), the fragments are read a whole K-tile before
-// use (lgkmcnt), acc_fence() pads the VALU / XDL <-> accumulator transitions (init, epilogue).
-__device__ __forceinline__ void mma4(f32x4 (&acc)[8][8], const Frags4& f) {
-  __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-      asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(f.b[j]), "v"(f.a[i]));
-  __builtin_amdgcn_s_setprio(0);
-}
-
-// wait states between the accumulators' last writer (VALU init / an asm MFMA, 8 passes) and their
-// next reader of the other kind (>= 11 needed after an 8-pass XDL write; 24 given). The empty asm
-// statements on every accumulator pin the order: all writers before the nops, all readers after.
-__device__ __forceinline__ void acc_touch(f32x4 (&acc)[8][8]) {
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; j += 4)
-      asm volatile("" : "+a"(acc[i][j]), "+a"(acc[i][j + 1]), "+a"(acc[i][j + 2]), "+a"(acc[i][j + 3]));
-}
-__device__ __forceinline__ void acc_fence(f32x4 (&acc)[8][8]) {
-  acc_touch(acc);
-  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
-  acc_touch(acc);
-}
-
-template <class SA, class SB>
-__device__ __forceinline__ void stage4(char* smem, int kt, int nk, const SA& sa, const SB& sb, int K) {
-  char* buf = smem + (kt & 3) * kBuf4;
-  const int k0 = kt * kBK4;
-  if (k0 + kBK4 > K) {
-    sa.template stage<true>(buf, k0);
-    sb.template stage<true>(buf + kImg4, k0);
-  } else {
-    sa.template stage<false>(buf, k0);
-    sb.template stage<false>(buf + kImg4, k0);
-  }
-}
-
-// the steady-state K-tile step (K-tiles kt + 1 .. kt + 3 exist): wait for K-tile kt + 1, restage
-// the buffer of kt - 1 with kt + 3, read kt + 1 into `nxt`, multiply `cur`. Branch-free, so the two
-// fragment sets stay in fixed registers across the unrolled pair.
-template <bool ASM, class SA, class SB>
-__device__ __forceinline__ void step4_full(f32x4 (&acc)[8][8], const Frags4& cur, Frags4& nxt, char* smem, int kt,
-                                           const SA& sa, const SB& sb, int wr, int wc, int lane) {
-  wait_vm<8>();
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  barrier();
-  char* buf = smem + ((kt + 3) & 3) * kBuf4;
-  sa.template stage<false>(buf, (kt + 3) * kBK4);
-  sb.template stage<false>(buf + kImg4, (kt + 3) * kBK4);
-  read4(nxt, smem + ((kt + 1) & 3) * kBuf4, sa, sb, wr, wc, lane);
-  if constexpr (ASM) __builtin_amdgcn_sched_barrier(0);
-  mma4(acc, cur);
-}
-
-// any K-tile step (the last few: fewer K-tiles left to wait for / stage / read)
-template <bool ASM, class SA, class SB>
-__device__ __forceinline__ void step4(f32x4 (&acc)[8][8], Frags4& cur, Frags4& nxt, char* smem, int kt, int nk,
-                                      const SA& sa, const SB& sb, int K, int wr, int wc, int lane) {
-  if (kt + 1 < nk) {
-    if (kt + 2 < nk) wait_vm<8>();
-    else wait_vm<0>();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    barrier();
-    if (kt + 3 < nk) stage4(smem, kt + 3, nk, sa, sb, K);
-    read4(nxt, smem + ((kt + 1) & 3) * kBuf4, sa, sb, wr, wc, lane);
-  }
-  if constexpr (ASM) {
-    // the transposed reads of `cur` are inline asm (invisible to hipcc's waitcnt insertion); the
-    // lgkmcnt(0) before the barrier above retired them, except on the last K-tile (rule 18)
-    if (kt + 1 >= nk) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  mma4(acc, cur);
-}
-
-template <int OUT, bool AK, bool BK>
-__global__ __launch_bounds__(kThreads4, 1) void gemm4_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B,
-                                                          void* __restrict__ C, int M, int N, int K, int64_t lda,
-                                                          int64_t ldb, int64_t ldc, int kper, int64_t slab) {
-  __shared__ __attribute__((aligned(1024))) char smem[4 * kBuf4];
-  const int nM = (M + kTile - 1) / kTile, nN = (N + kTile - 1) / kTile, nwg = nM * nN;
-  const int orig = blockIdx.x, xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
-  constexpr int G = 8;
-  const int per = G * nN, grp = wg / per, first = grp * G, gm = nM - first < G ? nM - first : G;
-  const int tm = first + (wg % per) % gm, tn = (wg % per) / gm;
-  const int m0 = tm * kTile, n0 = tn * kTile;
-
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, wr = wv >> 1, wc = wv & 1;
-  const int kb = blockIdx.y * kper;
-  K = K - kb < kper ? K - kb : kper;
-  A += AK ? (int64_t)kb : (int64_t)kb * lda;
-  B += BK ? (int64_t)kb : (int64_t)kb * ldb;
-  if constexpr (OUT == 0 || OUT == 3) C = static_cast<__bf16*>(C) + blockIdx.y * slab;
-  else C = static_cast<float*>(C) + blockIdx.y * slab;
-  const auto sa = Op4<AK>::make(A, lda, m0, M, K);
-  const auto sb = Op4<BK>::make(B, ldb, n0, N, K);
-  constexpr bool ASM = !AK || !BK;
-
-  f32x4 acc[8][8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  acc_fence(acc);
-
-  const int nk = (K + kBK4 - 1) / kBK4;
-  // prologue: K-tiles 0, 1, 2 in flight, wait for 0
-  for (int j = 0; j < 3 && j < nk; ++j) stage4(smem, j, nk, sa, sb, K);
-  if (nk >= 3) wait_vm<16>();
-  else if (nk == 2) wait_vm<8>();
-  else wait_vm<0>();
-  barrier();
-  Frags4 f0, f1;
-  read4(f0, smem, sa, sb, wr, wc, lane);
-  // two steps per iteration so the fragment sets keep fixed registers (no runtime-indexed arrays);
-  // the steady state holds while K-tile kt + 3 (the one restaged) exists and is not the last
-  // (partial) one. Staging K-tile j needs the K check only when (j + 1) * 32 > K.
-  int kt = 0;
-  for (; (kt + 5) * kBK4 <= K; kt += 2) {
-    step4_full<ASM>(acc, f0, f1, smem, kt, sa, sb, wr, wc, lane);
-    step4_full<ASM>(acc, f1, f0, smem, kt + 1, sa, sb, wr, wc, lane);
-  }
-  for (; kt + 1 < nk; kt += 2) {
-    step4<ASM>(acc, f0, f1, smem, kt, nk, sa, sb, K, wr, wc, lane);
-    step4<ASM>(acc, f1, f0, smem, kt + 1, nk, sa, sb, K, wr, wc, lane);
-  }
-  if (kt < nk) step4<ASM>(acc, f0, f1, smem, kt, nk, sa, sb, K, wr, wc, lane);
-  acc_fence(acc);
-
-  // epilogue: acc[i][j] register e = C[m0 + wr*128 + i*16 + (lane & 15)][n0 + wc*128 + j*16 + (lane >> 4)*4 + e]
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int m = m0 + wr * 128 + i * 16 + (lane & 15);
-    if (m >= M) continue;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int n = n0 + wc * 128 + j * 16 + (lane >> 4) * 4;
-      if (n >= N) continue;
-      const f32x4 v = acc[i][j];
-      if constexpr (OUT == 0 || OUT == 3) {
-        bf16x4* p = reinterpret_cast<bf16x4*>(static_cast<__bf16*>(C) + (int64_t)m * ldc + n);
-        f32x4 w = v;
-        if constexpr (OUT == 3) {
-          const bf16x4 old = *p;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) w[e] += (float)old[e];
-        }
-        bf16x4 o;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = (__bf16)w[e];
-        *p = o;
-      } else {
-        f32x4* p = reinterpret_cast<f32x4*>(static_cast<float*>(C) + (int64_t)m * ldc + n);
-        if constexpr (OUT == 2) *p = *p + v;
-        else *p = v;
-      }
-    }
-  }
-}
-
 struct Geo {
   int M, N, K;
   int64_t lda, ldb, ldc;
@@ -774,25 +439,10 @@ struct Geo {
   int64_t slab;
 };
 
-// K-loop schedule (measurement toggle while the two are compared): CS_GEMM_SCHED=1 one barrier
-// per K-tile, else the 4-phase counted-vmcnt pipeline
-int g_sched = [] {
-  const char* e = getenv("CS_GEMM_SCHED");
-  const int v = e != nullptr ? atoi(e) : 0;
-  return v == 1 || v == 2 ? v : 0;
-}();
-
 template <int OUT, bool AK, bool BK>
 void launch(const __bf16* a, const __bf16* b, void* c, const Geo& g, dim3 grid, hipStream_t stream) {
-  if (g_sched == 2)
-    hipLaunchKernelGGL((gemm4_kernel<OUT, AK, BK>), grid, dim3(kThreads4), 0, stream, a, b, c, g.M, g.N, g.K, g.lda,
-                       g.ldb, g.ldc, g.kper, g.slab);
-  else if (g_sched == 1)
-    hipLaunchKernelGGL((gemm_kernel<OUT, AK, BK, false, 1>), grid, dim3(kThreads), 0, stream, a, b, c, g.M, g.N, g.K,
-                       g.lda, g.ldb, g.ldc, g.kper, g.slab, nullptr);
-  else
-    hipLaunchKernelGGL((gemm_kernel<OUT, AK, BK>), grid, dim3(kThreads), 0, stream, a, b, c, g.M, g.N, g.K, g.lda,
-                       g.ldb, g.ldc, g.kper, g.slab, nullptr);
+  hipLaunchKernelGGL((gemm_kernel<OUT, AK, BK>), grid, dim3(kThreads), 0, stream, a, b, c, g.M, g.N, g.K, g.lda, g.ldb,
+                     g.ldc, g.kper, g.slab, nullptr);
 }
 
 template <int OUT>
@@ -861,9 +511,4 @@ hipError_t cs_gemm_bf16_bn_stats(const void* A, int64_t lda, const void* B, int6
                      static_cast<const __bf16*>(A), static_cast<const __bf16*>(B), C, M, N, K, lda, ldb, ldc, K,
                      (int64_t)0, stats);
   return hipGetLastError();
-}
-
-int cs_gemm_bf16_sched(int sched) {
-  if (sched >= 0 && sched <= 2) g_sched = sched;
-  return g_sched;
 }

@@ -277,9 +277,6 @@ hipError_t cs_maxpool3s2_bwd(int dt, const void* dy, const unsigned char* pos, v
 hipError_t cs_gemm_bf16_bn_stats(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int M,
                                  int N, int K, float* stats, hipStream_t stream);
 int cs_gemm_bf16_splits(int M, int N, int K);
-// K-loop schedule of the next launches (0: 4-phase counted vmcnt, 1: one barrier per K-tile; other
-// values only query); returns the current one
-int cs_gemm_bf16_sched(int sched);
 hipError_t cs_gemm_bf16(int a_kmajor, const void* A, int64_t lda, int b_kmajor, const void* B, int64_t ldb, void* C,
                         int64_t ldc, int M, int N, int K, int out_mode, int splits, int64_t slab, hipStream_t stream);
 hipError_t cs_rope(int dt, const void* x, const float* cosv, const float* sinv, void* out, int B, int S, int H, int hd,

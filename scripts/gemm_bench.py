@@ -41,14 +41,9 @@ def main():
     p.add_argument("--reps", type=int, default=10)
     p.add_argument("--shapes", type=str, default="")
     p.add_argument("--products", type=str, default="")
-    p.add_argument("--sched-ab", type=str, default="",
-                   help="also time these GEMM K-loop schedules (comma list, e.g. 1,2; see gemm_bf16_sched)")
     a = p.parse_args()
     from cs744_pytorch_distributed_tutorial_amd.ops import native
     C = native.C()
-    if a.sched_ab and not hasattr(C, "gemm_bf16_sched"):
-        print("# --sched-ab: this build has one GEMM schedule only", flush=True)
-        a.sched_ab = ""
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(0)
     for name, N, K in SHAPES:
@@ -72,28 +67,16 @@ def main():
             err = ((y0.float() - y1.float()).abs().max() / y1.float().abs().max()).item()
             del y0, y1
             t = {"ours": [], "hipblaslt": []}
-            others = [int(x) for x in a.sched_ab.split(",")] if a.sched_ab else []
-            base = C.gemm_bf16_sched(-1) if others else 0
-            for sc in others:
-                t[f"ours_sched{sc}"] = []
             for _ in range(a.rounds):
                 for k, fn in (("ours", ours), ("hipblaslt", blas)):
                     fn()
                     t[k].append(timed(fn, a.reps))
-                for sc in others:
-                    C.gemm_bf16_sched(sc)
-                    ours()
-                    t[f"ours_sched{sc}"].append(timed(ours, a.reps))
-                    C.gemm_bf16_sched(base)
             row = {"shape": name, "product": label, "M": M, "N": N, "K": K, "max_rel_diff": round(err, 5)}
             for k, v in t.items():
                 row[f"{k}_ms_med"] = round(statistics.median(v), 4)
                 row[f"{k}_tflops_med"] = round(flop / statistics.median(v) / 1e9, 1)
                 row[f"{k}_tflops_best"] = round(flop / min(v) / 1e9, 1)
             row["ours_vs_hipblaslt"] = round(statistics.median(t["hipblaslt"]) / statistics.median(t["ours"]), 3)
-            for sc in others:
-                row[f"sched{sc}_vs_hipblaslt"] = round(statistics.median(t["hipblaslt"]) /
-                                                      statistics.median(t[f"ours_sched{sc}"]), 3)
             print(json.dumps(row), flush=True)
         del x, w, dy
         torch.cuda.empty_cache()
