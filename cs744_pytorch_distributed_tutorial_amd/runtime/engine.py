@@ -297,8 +297,11 @@ class NativeTrainer:
         self.overlap_wgrad = (os.environ.get("CS_OVERLAP_WGRAD", "1") != "0" and not python_collectives
                               and not self._counters and (self.native_comm is None or hw_queues() >= 8))
         self.engine.set_overlap(self.overlap_wgrad)
-        # in-launch BN finalize (bn_fin.h; CS_BN_FIN=0: the separate finalize launches)
-        self.engine.set_fin(os.environ.get("CS_BN_FIN", "1") != "0")
+        # BatchNorm finalize: separate launches by default. The in-launch last-arriver finalize
+        # (bn_fin.h, CS_BN_FIN=1) removes one launch per block but measured 6-8 % slower with the
+        # side-stream weight gradients on one box (88.6 k vs 83.3 k img/s at 20/5, 90.3 k vs 83.7 k at
+        # 100/10; profiles/r4_ab_bn_fin.txt) and neutral on the serial step
+        self.engine.set_fin(os.environ.get("CS_BN_FIN", "0") == "1")
         self.engine.set_data(0, self.train_data, self.train_labels, self.aug_train)
         self.engine.set_data(1, self.test_data, self.test_labels, self.aug_test)
         self.idx_buf = self.engine.idx()

@@ -305,7 +305,7 @@ def _set_tiles(t, tiles):
 def test_in_launch_bn_finalize_matches_finalize_launches(dev, tiles):
     """Every BatchNorm finalize as the last-arriving block of the launch that produced its partial
     sums (bn_fin.h: forward in the conv epilogue / split-K combine, backward in the data
-    gradient's epilogue / combine; set_fin(True), the default) vs the separate bn_finalize /
+    gradient's epilogue / combine; set_fin(True), opt-in) vs the separate bn_finalize (default) /
     bn_bwd_finalize launches: same partials, a different fixed combine order -> a norm bound after
     two steps at B=64 and identical num_batches_tracked; run to run bitwise (the combine order
     does not depend on which block arrives last)."""
@@ -439,18 +439,18 @@ def _force_x6s(tr):
     return n
 
 
-@pytest.mark.parametrize("variant", ["autotuned", "x6s_everywhere", "f32_only", "split", "nosplit", "dual", "separate"])
+@pytest.mark.parametrize("variant", ["autotuned", "x6s_everywhere", "f32_only", "split", "nosplit", "dual", "in_launch"])
 def test_bench_config_b64_matches_fp64(dev, variant):
     """The benchmarked configuration (B=64; tuned tiles = 22 of 23 GEMMs on X6S split-bf16
-    maths), every X6S GEMM, f32-MFMA-only tiles, and the tile tables that put the in-launch BN
-    finalize / apply at every site (split-K combines, 64x128 / 128x64 epilogues, dual launches;
-    "separate" = the finalize and apply as launches of their own) vs the decision-aligned fp64
-    model: every gradient tensor within 1e-4 relative (max-abs normalised)."""
-    tr = _trainer(dev, batch_size=64, train_size=1024, autotune=variant in ("autotuned", "separate"))
+    maths), every X6S GEMM, f32-MFMA-only tiles, the tile tables that put split-K combines,
+    64x128 / 128x64 epilogues and dual launches at every site, and the opt-in in-launch BN finalize
+    (CS_BN_FIN=1, bn_fin.h) vs the decision-aligned fp64 model: every gradient tensor within 1e-4
+    relative (max-abs normalised)."""
+    tr = _trainer(dev, batch_size=64, train_size=1024, autotune=variant in ("autotuned", "in_launch"))
     if variant in ("split", "nosplit", "dual"):
         _set_tiles(tr, variant)
-    if variant == "separate":
-        tr.engine.set_fin(False)
+    if variant == "in_launch":
+        tr.engine.set_fin(True)
     if variant == "x6s_everywhere":
         assert _force_x6s(tr) == 22
         assert sum(t["math"] == "x6s" for t in tr.tile_table()) == 22
