@@ -198,6 +198,7 @@ VggEngine::VggEngine(int64_t Bmax, std::vector<int64_t> desc, std::vector<int64_
   }
   if (const char* e = getenv("CS_CONV_DUAL")) dual_ = atoi(e) != 0;
   if (const char* e = getenv("CS_BN_FUSED_ROWS")) bn_fused_rows_ = atoll(e);
+  if (const char* e = getenv("CS_BN_EPI_RED")) ered_on_ = atoi(e) != 0;
   if (const char* e = getenv("CS_CONV_MATH")) math_ = atoi(e);
   bn_part_ = torch::zeros({partmax}, fo);
   bn_coef_ = torch::zeros({cmax * 3}, fo);
@@ -497,7 +498,7 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
     red_pending_ = -1;
     // ---- weight and data gradients of block l; block l-1's BN-backward partials (and their
     // finalize) ride the data gradient
-    const bool er = l > 0;
+    const bool er = l > 0 && ered_on_;
     CsBnRed erv{};
     CsBnFin fin{};
     if (er) {
@@ -535,7 +536,7 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
       }
       conv(l, CS_CONV_WGRAD, (int)B, b.tile[CS_CONV_WGRAD], s, false, ws_w_.data_ptr<float>(), dz, nullptr,
            tail.n > 0 ? &tail : nullptr);
-      if (er) conv(l, CS_CONV_DGRAD, (int)B, b.tile[CS_CONV_DGRAD], s, false, nullptr, dz, &erv, nullptr, fp);
+      if (l > 0) conv(l, CS_CONV_DGRAD, (int)B, b.tile[CS_CONV_DGRAD], s, false, nullptr, dz, &erv, nullptr, fp);
     }
     if (er) {
       red_pending_ = l - 1;

@@ -191,6 +191,9 @@ class VggEngine {
   torch::Tensor gbuf_[2], dz_[2], ws_, ws_w_, bn_part_, bn_coef_, bn_eval_, head_ws_, fin_cnt_, fin_grp_;
   int64_t ws_elems_ = 0;
   bool fin_on_ = true;
+  // block l-1's BatchNorm-backward partial sums in block l's data-gradient epilogue (else the
+  // BN backward's own reduce pass); CS_BN_EPI_RED=0 (measurement)
+  bool ered_on_ = true;
   bool dual_ = true;
   int math_ = 2;  // conv autotune candidates: 0 f32 MFMA, 1 split-bf16 X6, 2 both (CS_CONV_MATH)
   // CS_BN_FUSED_ROWS; 0 disables. Measured on MI355X at B=64 (img/s): 0 -> 71.46k, 256 (blocks 6-7)
