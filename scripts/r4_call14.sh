@@ -16,3 +16,6 @@ bash scripts/ab_trees.sh 3 $V -- --steps 20 --warmup 5 > gpurun_out/ab6_20_5.log
 tail -2 gpurun_out/ab6_20_5.log
 bash scripts/ab_trees.sh 2 $V -- --steps 100 --warmup 10 > gpurun_out/ab6_100_10.log 2>&1 || exit $?
 tail -2 gpurun_out/ab6_100_10.log
+bash scripts/ab_trees.sh 1 .ab/r2 .ab/r3 .:CS_LM_GEMM=blas . -- --model llama3-8b --steps 6 --warmup 3 \
+  > gpurun_out/ab_llama_r2r3r4.log 2>&1 || exit $?
+tail -4 gpurun_out/ab_llama_r2r3r4.log
