@@ -199,6 +199,7 @@ VggEngine::VggEngine(int64_t Bmax, std::vector<int64_t> desc, std::vector<int64_
   if (const char* e = getenv("CS_CONV_DUAL")) dual_ = atoi(e) != 0;
   if (const char* e = getenv("CS_BN_FUSED_ROWS")) bn_fused_rows_ = atoll(e);
   if (const char* e = getenv("CS_BN_EPI_RED")) ered_on_ = atoi(e) != 0;
+  if (const char* e = getenv("CS_BN_SPLITK_TAIL")) bn_tail_on_ = atoi(e) != 0;
   if (const char* e = getenv("CS_CONV_MATH")) math_ = atoi(e);
   bn_part_ = torch::zeros({partmax}, fo);
   bn_coef_ = torch::zeros({cmax * 3}, fo);
@@ -268,7 +269,8 @@ CsConvArgs VggEngine::conv_args(int l, int mode, int B, bool with_stats, float* 
 }
 
 void VggEngine::conv(int l, int mode, int B, const ConvTile& t, hipStream_t s, bool with_stats, float* ws,
-                     float* dz, const CsBnRed* ered, const CsSgdTail* sgd, const CsBnFin* fin) {
+                     float* dz, const CsBnRed* ered, const CsSgdTail* sgd, const CsBnFin* fin,
+                     const CsBnFwdTail* bnt) {
   VggBlock& b = blocks_[l];
   CsConvArgs a = conv_args(l, mode, B, with_stats, ws, dz);
   if (ered != nullptr) {
@@ -277,10 +279,17 @@ void VggEngine::conv(int l, int mode, int B, const ConvTile& t, hipStream_t s, b
   }
   if (sgd != nullptr) a.sgd = *sgd;
   if (fin != nullptr) a.fin = *fin;
+  if (bnt != nullptr) a.bnt = *bnt;
   const Dims d = dims(b, mode, B);
   const int sp = eff_splits(d.K, t.splits, t.bk);
   TORCH_CHECK(sp == 1 || (int64_t)sp * d.M * d.N <= ws_elems_, "VggEngine: split-K workspace too small");
   ok(cs_conv_gemm(a, mode, t.bm, t.bn, t.bk, t.splits, s, t.stage), "conv_gemm");
+}
+
+bool VggEngine::bn_tail_ok(int l, int64_t B) const {
+  const VggBlock& b = blocks_[l];
+  const ConvTile& t = b.tile[CS_CONV_FWD];
+  return bn_tail_on_ && B * b.H * b.H <= 1024 && b.cout % 8 == 0 && eff_splits(9 * b.cin, t.splits, t.bk) > 1;
 }
 
 bool VggEngine::bn_fused(int l, int64_t B) const {
@@ -422,6 +431,14 @@ void VggEngine::forward_train(int64_t B) {
     const ConvTile& t = b.tile[CS_CONV_FWD];
     float* bn = b.bn.data_ptr<float>();
     float* out = (l + 1 < L) ? blocks_[l + 1].x.data_ptr<float>() : feats_.data_ptr<float>();
+    if (!fin_on_ && bn_tail_ok(l, B)) {
+      // small layer: the split-K combine also computes the BN statistics, finalizes them and
+      // writes relu(BN(y)) (pooled) into the next block's input
+      const CsBnFwdTail bt{P(b.g_off), P(b.be_off), bufs + b.rm_off, bufs + b.rv_off, nbt_.data_ptr<int64_t>() + l,
+                           kBnMomentum, kBnEps, bn, out, b.H, b.H, b.pool ? 1 : 0};
+      conv(l, CS_CONV_FWD, (int)B, t, s, true, nullptr, nullptr, nullptr, nullptr, nullptr, &bt);
+      continue;
+    }
     if (fin_on_) {
       // conv [+ split-K combine]: its last-arriving block finalizes the batch statistics
       const CsBnFin f = fin_fwd_args(l, (int)B);

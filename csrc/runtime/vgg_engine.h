@@ -145,7 +145,9 @@ class VggEngine {
  private:
   void conv(int l, int mode, int B, const ConvTile& t, hipStream_t s, bool with_stats, float* ws = nullptr,
             float* dz = nullptr, const CsBnRed* ered = nullptr, const CsSgdTail* sgd = nullptr,
-            const CsBnFin* fin = nullptr);
+            const CsBnFin* fin = nullptr, const CsBnFwdTail* bnt = nullptr);
+  // block l's forward BN runs inside its split-K combine (small layers: M <= 1024 rows)
+  bool bn_tail_ok(int l, int64_t B) const;
   CsConvArgs conv_args(int l, int mode, int B, bool with_stats, float* ws, float* dz);
   // block l's wgrad + dgrad as one launch (both 64x64 register-staged tiles)
   bool dual_ok(int l) const;
@@ -194,6 +196,8 @@ class VggEngine {
   // block l-1's BatchNorm-backward partial sums in block l's data-gradient epilogue (else the
   // BN backward's own reduce pass); CS_BN_EPI_RED=0 (measurement)
   bool ered_on_ = true;
+  // small-layer forward tail fused into the split-K combine (CS_BN_SPLITK_TAIL=0: measurement)
+  bool bn_tail_on_ = true;
   bool dual_ = true;
   int math_ = 2;  // conv autotune candidates: 0 f32 MFMA, 1 split-bf16 X6, 2 both (CS_CONV_MATH)
   // CS_BN_FUSED_ROWS; 0 disables. Measured on MI355X at B=64 (img/s): 0 -> 71.46k, 256 (blocks 6-7)
