@@ -198,7 +198,6 @@ VggEngine::VggEngine(int64_t Bmax, std::vector<int64_t> desc, std::vector<int64_
   }
   if (const char* e = getenv("CS_CONV_DUAL")) dual_ = atoi(e) != 0;
   if (const char* e = getenv("CS_BN_FUSED_ROWS")) bn_fused_rows_ = atoll(e);
-  if (const char* e = getenv("CS_BN_EPI_RED")) ered_on_ = atoi(e) != 0;
   if (const char* e = getenv("CS_BN_SPLITK_TAIL")) bn_tail_on_ = atoi(e) != 0;
   if (const char* e = getenv("CS_CONV_MATH")) math_ = atoi(e);
   bn_part_ = torch::zeros({partmax}, fo);
@@ -515,7 +514,9 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
     red_pending_ = -1;
     // ---- weight and data gradients of block l; block l-1's BN-backward partials (and their
     // finalize) ride the data gradient
-    const bool er = l > 0 && ered_on_;
+    // (measured against the BN backward's own reduce pass next to the side stream: +0.2-0.7 %,
+    // profiles/r4_ab_bn_epi_red.txt)
+    const bool er = l > 0;
     CsBnRed erv{};
     CsBnFin fin{};
     if (er) {

@@ -193,9 +193,6 @@ class VggEngine {
   torch::Tensor gbuf_[2], dz_[2], ws_, ws_w_, bn_part_, bn_coef_, bn_eval_, head_ws_, fin_cnt_, fin_grp_;
   int64_t ws_elems_ = 0;
   bool fin_on_ = true;
-  // block l-1's BatchNorm-backward partial sums in block l's data-gradient epilogue (else the
-  // BN backward's own reduce pass); CS_BN_EPI_RED=0 (measurement)
-  bool ered_on_ = true;
   // small-layer forward tail fused into the split-K combine (CS_BN_SPLITK_TAIL=0: measurement)
   bool bn_tail_on_ = true;
   bool dual_ = true;
