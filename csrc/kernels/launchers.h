@@ -129,6 +129,9 @@ struct CsConvArgs {
   // FWD with split-K on a small layer (M <= 1024): the combine also runs the BatchNorm over all
   // rows and applies it; bnt.next == null: off (cs_conv_gemm)
   CsBnFwdTail bnt;
+  // DGRAD with split-K (<= 32 splits): no combine launch; the [splits][M][N] slabs in ws are the
+  // consumer's input (cs_bn_fused_bwd sums them as it reads, gslabs / gstride)
+  int no_reduce;
   // filled by the launcher:
   int lgH, lgW, lgCin, lgCout, M, N, K, ksteps_per_split, total_ksteps;
 };

@@ -145,7 +145,9 @@ class VggEngine {
  private:
   void conv(int l, int mode, int B, const ConvTile& t, hipStream_t s, bool with_stats, float* ws = nullptr,
             float* dz = nullptr, const CsBnRed* ered = nullptr, const CsSgdTail* sgd = nullptr,
-            const CsBnFin* fin = nullptr, const CsBnFwdTail* bnt = nullptr);
+            const CsBnFin* fin = nullptr, const CsBnFwdTail* bnt = nullptr, bool no_reduce = false);
+  // block l's data gradient leaves its split-K slabs for block l-1's one-launch BN backward
+  bool bwd_slab_ok(int l, int64_t B) const;
   // block l's forward BN runs inside its split-K combine (small layers: M <= 1024 rows)
   bool bn_tail_ok(int l, int64_t B) const;
   CsConvArgs conv_args(int l, int mode, int B, bool with_stats, float* ws, float* dz);
@@ -195,6 +197,12 @@ class VggEngine {
   bool fin_on_ = true;
   // small-layer forward tail fused into the split-K combine (CS_BN_SPLITK_TAIL=0: measurement)
   bool bn_tail_on_ = true;
+  // small-layer BN backward straight from the data gradient's split-K slabs: one launch (reduce +
+  // finalize + apply, cs_bn_fused_bwd) instead of the combine, finalize and apply launches
+  // (CS_BN_BWD_SLABS=0: measurement)
+  bool bwd_slab_on_ = true;
+  int slab_pending_ = -1, slab_S_ = 0;
+  int64_t slab_stride_ = 0;
   bool dual_ = true;
   int math_ = 2;  // conv autotune candidates: 0 f32 MFMA, 1 split-bf16 X6, 2 both (CS_CONV_MATH)
   // CS_BN_FUSED_ROWS; 0 disables. Measured on MI355X at B=64 (img/s): 0 -> 71.46k, 256 (blocks 6-7)
