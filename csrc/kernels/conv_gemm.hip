@@ -925,142 +925,6 @@ __global__ __launch_bounds__(256) void splitk_reduce_dual_kernel(CsConvArgs a1, 
   else splitk_reduce_body(a2, mode2, nslab2, zstep2, blockIdx.x - nb1, smem);
 }
 
-// Small-layer forward tail (M <= 1024 rows; VGG-11 blocks 4-7 at B = 64): the split-K combine
-// (+ bias) -> y, the BatchNorm batch statistics over all M rows (two passes over the values held in
-// registers: the column mean, then M2 around it), the finalize, and relu(BN(y)) (+ 2x2 max-pool)
-// into the next block's input: one launch instead of combine, finalize and apply (two kernel
-// boundaries and two latency-bound passes of ~5 us each). Block = 8 channels x every row; row m
-// of the block is thread m % 256, register set m / 256. Fixed summation orders: deterministic.
-constexpr int kTailRows = 1024;
-__global__ __launch_bounds__(256) void splitk_bn_fwd_kernel(CsConvArgs a, int nslab, int zstep) {
-  __shared__ float img[kTailRows * 8];  // post-ReLU values for the pool, [M][8]
-  __shared__ float red[256][9];
-  __shared__ float colv[3][8];  // mean, scale, shift
-  const CsBnFwdTail& f = a.bnt;
-  const int tid = threadIdx.x, c0 = blockIdx.x * 8, M = a.M, N = a.N;
-  const size_t slab = (size_t)M * N;
-  float v[4][8];
-  float acc[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
-  float bias[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) bias[j] = a.bias != nullptr ? a.bias[c0 + j] : 0.f;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int m = tid + 256 * i;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[i][j] = 0.f;
-    if (m < M) {
-      const float* p = a.ws + (size_t)m * N + c0;
-      float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0;
-      for (int z = 0; z < nslab; ++z) {  // z ascending, as the plain combine
-        const float4 t0 = *reinterpret_cast<const float4*>(p + (size_t)z * zstep * slab);
-        const float4 t1 = *reinterpret_cast<const float4*>(p + (size_t)z * zstep * slab + 4);
-        s0.x += t0.x; s0.y += t0.y; s0.z += t0.z; s0.w += t0.w;
-        s1.x += t1.x; s1.y += t1.y; s1.z += t1.z; s1.w += t1.w;
-      }
-      v[i][0] = s0.x + bias[0]; v[i][1] = s0.y + bias[1]; v[i][2] = s0.z + bias[2]; v[i][3] = s0.w + bias[3];
-      v[i][4] = s1.x + bias[4]; v[i][5] = s1.y + bias[5]; v[i][6] = s1.z + bias[6]; v[i][7] = s1.w + bias[7];
-      float* y = a.out + (size_t)m * N + c0;
-      *reinterpret_cast<float4*>(y) = make_float4(v[i][0], v[i][1], v[i][2], v[i][3]);
-      *reinterpret_cast<float4*>(y + 4) = make_float4(v[i][4], v[i][5], v[i][6], v[i][7]);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc[j] += v[i][j];
-    }
-  }
-  // column means (thread partials summed in thread order)
-#pragma unroll
-  for (int j = 0; j < 8; ++j) red[tid][j] = acc[j];
-  __syncthreads();
-  if (tid < 8) {
-    float t = 0.f;
-    for (int r = 0; r < 256; ++r) t += red[r][tid];
-    colv[0][tid] = t / (float)M;
-  }
-  __syncthreads();
-  float mean[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    mean[j] = colv[0][j];
-    acc[j] = 0.f;
-  }
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-    if (tid + 256 * i < M)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float d = v[i][j] - mean[j];
-        acc[j] = fmaf(d, d, acc[j]);
-      }
-  __syncthreads();  // every thread has read colv[0] / is done with red
-#pragma unroll
-  for (int j = 0; j < 8; ++j) red[tid][j] = acc[j];
-  __syncthreads();
-  if (tid < 8) {
-    float M2 = 0.f;
-    for (int r = 0; r < 256; ++r) M2 += red[r][tid];
-    const int c = c0 + tid;
-    const float n = (float)M, m = colv[0][tid];
-    const float var = M2 / n, inv = 1.0f / sqrtf(var + f.eps);
-    const float g = f.gamma[c], b = f.beta[c];
-    const float sc = g * inv, sh = b - m * g * inv;
-    f.bn[c] = sc;
-    f.bn[N + c] = sh;
-    f.bn[2 * N + c] = m;
-    f.bn[3 * N + c] = inv;
-    if (f.rmean != nullptr) {
-      const float unb = n > 1.f ? M2 / (n - 1.f) : var;
-      f.rmean[c] = (1.f - f.momentum) * f.rmean[c] + f.momentum * m;
-      f.rvar[c] = (1.f - f.momentum) * f.rvar[c] + f.momentum * unb;
-    }
-    colv[1][tid] = sc;
-    colv[2][tid] = sh;
-  }
-  if (f.nbt != nullptr && blockIdx.x == 0 && tid == 0) *f.nbt += 1;
-  __syncthreads();
-  float sc[8], sh[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    sc[j] = colv[1][j];
-    sh[j] = colv[2][j];
-  }
-  if (!f.pool) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int m = tid + 256 * i;
-      if (m >= M) continue;
-      float o[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = fmaxf(fmaf(v[i][j], sc[j], sh[j]), 0.f);
-      float* q = f.next + (size_t)m * N + c0;
-      *reinterpret_cast<float4*>(q) = make_float4(o[0], o[1], o[2], o[3]);
-      *reinterpret_cast<float4*>(q + 4) = make_float4(o[4], o[5], o[6], o[7]);
-    }
-    return;
-  }
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int m = tid + 256 * i;
-    if (m < M)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) img[m * 8 + j] = fmaxf(fmaf(v[i][j], sc[j], sh[j]), 0.f);
-  }
-  __syncthreads();
-  const int H = f.H, W = f.W, Ho = H >> 1, Wo = W >> 1, Mo = M >> 2;
-  for (int mo = tid; mo < Mo; mo += 256) {
-    const int wo = mo % Wo, ho = (mo / Wo) % Ho, bb = mo / (Wo * Ho);
-    const int r0 = (bb * H + 2 * ho) * W + 2 * wo;
-    float o[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-      o[j] = fmaxf(fmaxf(img[r0 * 8 + j], img[(r0 + 1) * 8 + j]), fmaxf(img[(r0 + W) * 8 + j], img[(r0 + W + 1) * 8 + j]));
-    float* q = f.next + (size_t)mo * N + c0;
-    *reinterpret_cast<float4*>(q) = make_float4(o[0], o[1], o[2], o[3]);
-    *reinterpret_cast<float4*>(q + 4) = make_float4(o[4], o[5], o[6], o[7]);
-  }
-}
-
 int reduce_blocks(const CsConvArgs& a) { return ((a.M + kRedRows - 1) / kRedRows) * ((a.N + 63) / 64); }
 
 // fold pre-pass for large split counts; returns (nslab, zstep) for the combine
@@ -1081,10 +945,6 @@ void fold_if_needed(const CsConvArgs& a, int splits, hipStream_t stream, int& ns
 hipError_t launch_reduce(const CsConvArgs& a, int mode, int splits, hipStream_t stream) {
   int nslab, zstep;
   fold_if_needed(a, splits, stream, nslab, zstep);
-  if (mode == CS_CONV_FWD && a.bnt.next != nullptr) {
-    hipLaunchKernelGGL(splitk_bn_fwd_kernel, dim3(a.N / 8), dim3(256), 0, stream, a, nslab, zstep);
-    return hipGetLastError();
-  }
   hipLaunchKernelGGL(splitk_reduce_kernel, dim3(reduce_blocks(a)), dim3(256), 0, stream, a, mode, nslab, zstep);
   return hipGetLastError();
 }
@@ -1403,13 +1263,6 @@ hipError_t cs_conv_gemm(CsConvArgs a, int mode, int bm, int bn, int bk, int spli
   if (a.no_reduce && (mode != CS_CONV_DGRAD || splits < 2 || splits > 2 * kFold || a.ered.part != nullptr ||
                       a.fin.cnt != nullptr))
     return hipErrorInvalidValue;  // slabs left for the consumer: plain DGRAD split-K only
-  if (a.bnt.next != nullptr) {  // fused small-layer forward tail: rides the split-K combine
-    const CsBnFwdTail& t = a.bnt;
-    if (mode != CS_CONV_FWD || splits < 2 || a.M > kTailRows || a.N % 8 || a.fin.cnt != nullptr ||
-        t.gamma == nullptr || t.beta == nullptr || t.bn == nullptr || t.H <= 0 || t.W <= 0 ||
-        a.M % (t.H * t.W) != 0 || (t.pool && (t.H % 2 || t.W % 2)))
-      return hipErrorInvalidValue;
-  }
   if (a.fin.cnt != nullptr) {  // last-arriver BN finalize: its statistics must exist in this launch pair
     if (mode == CS_CONV_WGRAD || (mode == CS_CONV_FWD && a.stats == nullptr) ||
         (mode == CS_CONV_DGRAD && a.ered.part == nullptr))

@@ -72,20 +72,6 @@ struct CsSgdTail {
 // partials (bn_fin.h): FWD with CsConvArgs::stats (scale / shift / mean / invstd -> bnv [4][C],
 // running stats, num_batches_tracked), BWD with CsConvArgs::ered (coef [C][3], dgamma, dbeta,
 // dbias; ered.part is then [T][C][4]). cnt == null: off (the separate finalize launch runs).
-// Small-layer forward tail fused into the split-K combine (conv_gemm.hip splitk_bn_fwd_kernel):
-// y = combine + bias (written to CsConvArgs::out), batch statistics of y over all M rows, the
-// finalize (bn = [scale | shift | mean | invstd][C], running stats, num_batches_tracked += 1) and
-// relu(y * scale + shift) (2x2 max-pooled when pool) into `next`; H, W: spatial size of y
-struct CsBnFwdTail {
-  const float *gamma, *beta;
-  float *rmean, *rvar;
-  int64_t* nbt;
-  float momentum, eps;
-  float* bn;
-  float* next;
-  int H, W, pool;
-};
-
 struct CsBnFin {
   int* cnt;    // zeroed ticket counters, >= cs_bn_fin_ints(...) ints (left zeroed by the launch)
   float* grp;  // level-1 group partials, >= cs_bn_fin_grp_floats(...) floats
@@ -126,9 +112,6 @@ struct CsConvArgs {
   // FWD (with stats) / DGRAD (with ered): the BN finalize by the launch's last-arriving block
   // (or the split-K combine's); fin.cnt == null: off
   CsBnFin fin;
-  // FWD with split-K on a small layer (M <= 1024): the combine also runs the BatchNorm over all
-  // rows and applies it; bnt.next == null: off (cs_conv_gemm)
-  CsBnFwdTail bnt;
   // DGRAD with split-K (<= 32 splits): no combine launch; the [splits][M][N] slabs in ws are the
   // consumer's input (cs_bn_fused_bwd sums them as it reads, gslabs / gstride)
   int no_reduce;

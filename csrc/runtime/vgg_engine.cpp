@@ -198,7 +198,6 @@ VggEngine::VggEngine(int64_t Bmax, std::vector<int64_t> desc, std::vector<int64_
   }
   if (const char* e = getenv("CS_CONV_DUAL")) dual_ = atoi(e) != 0;
   if (const char* e = getenv("CS_BN_FUSED_ROWS")) bn_fused_rows_ = atoll(e);
-  if (const char* e = getenv("CS_BN_SPLITK_TAIL")) bn_tail_on_ = atoi(e) != 0;
   if (const char* e = getenv("CS_BN_BWD_SLABS")) bwd_slab_on_ = atoi(e) != 0;
   if (const char* e = getenv("CS_CONV_MATH")) math_ = atoi(e);
   bn_part_ = torch::zeros({partmax}, fo);
@@ -270,7 +269,7 @@ CsConvArgs VggEngine::conv_args(int l, int mode, int B, bool with_stats, float* 
 
 void VggEngine::conv(int l, int mode, int B, const ConvTile& t, hipStream_t s, bool with_stats, float* ws,
                      float* dz, const CsBnRed* ered, const CsSgdTail* sgd, const CsBnFin* fin,
-                     const CsBnFwdTail* bnt, bool no_reduce) {
+                     bool no_reduce) {
   VggBlock& b = blocks_[l];
   CsConvArgs a = conv_args(l, mode, B, with_stats, ws, dz);
   if (ered != nullptr) {
@@ -279,18 +278,11 @@ void VggEngine::conv(int l, int mode, int B, const ConvTile& t, hipStream_t s, b
   }
   if (sgd != nullptr) a.sgd = *sgd;
   if (fin != nullptr) a.fin = *fin;
-  if (bnt != nullptr) a.bnt = *bnt;
   a.no_reduce = no_reduce ? 1 : 0;
   const Dims d = dims(b, mode, B);
   const int sp = eff_splits(d.K, t.splits, t.bk);
   TORCH_CHECK(sp == 1 || (int64_t)sp * d.M * d.N <= ws_elems_, "VggEngine: split-K workspace too small");
   ok(cs_conv_gemm(a, mode, t.bm, t.bn, t.bk, t.splits, s, t.stage), "conv_gemm");
-}
-
-bool VggEngine::bn_tail_ok(int l, int64_t B) const {
-  const VggBlock& b = blocks_[l];
-  const ConvTile& t = b.tile[CS_CONV_FWD];
-  return bn_tail_on_ && B * b.H * b.H <= 1024 && b.cout % 8 == 0 && eff_splits(9 * b.cin, t.splits, t.bk) > 1;
 }
 
 bool VggEngine::bwd_slab_ok(int l, int64_t B) const {
@@ -442,14 +434,6 @@ void VggEngine::forward_train(int64_t B) {
     const ConvTile& t = b.tile[CS_CONV_FWD];
     float* bn = b.bn.data_ptr<float>();
     float* out = (l + 1 < L) ? blocks_[l + 1].x.data_ptr<float>() : feats_.data_ptr<float>();
-    if (!fin_on_ && bn_tail_ok(l, B)) {
-      // small layer: the split-K combine also computes the BN statistics, finalizes them and
-      // writes relu(BN(y)) (pooled) into the next block's input
-      const CsBnFwdTail bt{P(b.g_off), P(b.be_off), bufs + b.rm_off, bufs + b.rv_off, nbt_.data_ptr<int64_t>() + l,
-                           kBnMomentum, kBnEps, bn, out, b.H, b.H, b.pool ? 1 : 0};
-      conv(l, CS_CONV_FWD, (int)B, t, s, true, nullptr, nullptr, nullptr, nullptr, nullptr, &bt);
-      continue;
-    }
     if (fin_on_) {
       // conv [+ split-K combine]: its last-arriving block finalizes the batch statistics
       const CsBnFin f = fin_fwd_args(l, (int)B);
@@ -553,7 +537,7 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
         // to the side stream after it and fills the chip while the main stream runs the
         // latency-bound BN kernels (and the split-K combine) of the block below
         conv(l, CS_CONV_DGRAD, (int)B, b.tile[CS_CONV_DGRAD], s, false, nullptr, dz, slabs ? nullptr : &erv, nullptr,
-             fp, nullptr, slabs);
+             fp, slabs);
         pending_sig_ = dz_link_->defer();
         dz_link_->wait(side_);
         conv(l, CS_CONV_WGRAD, (int)B, b.tile[CS_CONV_WGRAD], side_, false, ws_w_.data_ptr<float>(), dz);
@@ -580,7 +564,7 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
            tail.n > 0 ? &tail : nullptr);
       if (l > 0)
         conv(l, CS_CONV_DGRAD, (int)B, b.tile[CS_CONV_DGRAD], s, false, nullptr, dz, slabs ? nullptr : &erv, nullptr,
-             fp, nullptr, slabs);
+             fp, slabs);
     }
     if (er) {
       red_pending_ = l - 1;

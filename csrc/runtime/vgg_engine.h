@@ -145,11 +145,9 @@ class VggEngine {
  private:
   void conv(int l, int mode, int B, const ConvTile& t, hipStream_t s, bool with_stats, float* ws = nullptr,
             float* dz = nullptr, const CsBnRed* ered = nullptr, const CsSgdTail* sgd = nullptr,
-            const CsBnFin* fin = nullptr, const CsBnFwdTail* bnt = nullptr, bool no_reduce = false);
+            const CsBnFin* fin = nullptr, bool no_reduce = false);
   // block l's data gradient leaves its split-K slabs for block l-1's one-launch BN backward
   bool bwd_slab_ok(int l, int64_t B) const;
-  // block l's forward BN runs inside its split-K combine (small layers: M <= 1024 rows)
-  bool bn_tail_ok(int l, int64_t B) const;
   CsConvArgs conv_args(int l, int mode, int B, bool with_stats, float* ws, float* dz);
   // block l's wgrad + dgrad as one launch (both 64x64 register-staged tiles)
   bool dual_ok(int l) const;
@@ -195,8 +193,6 @@ class VggEngine {
   torch::Tensor gbuf_[2], dz_[2], ws_, ws_w_, bn_part_, bn_coef_, bn_eval_, head_ws_, fin_cnt_, fin_grp_;
   int64_t ws_elems_ = 0;
   bool fin_on_ = true;
-  // small-layer forward tail fused into the split-K combine (CS_BN_SPLITK_TAIL=0: measurement)
-  bool bn_tail_on_ = true;
   // small-layer BN backward straight from the data gradient's split-K slabs: one launch (reduce +
   // finalize + apply, cs_bn_fused_bwd) instead of the combine, finalize and apply launches
   // (CS_BN_BWD_SLABS=0: measurement)

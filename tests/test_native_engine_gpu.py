@@ -510,31 +510,6 @@ def test_long_run_no_syncs_deterministic(dev):
             assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("B", [64, 48])
-def test_bn_splitk_tail_matches_separate_launches(dev, monkeypatch, B):
-    """Small layers' forward BatchNorm inside the split-K combine (splitk_bn_fwd_kernel: batch
-    statistics over all rows, finalize, BN + ReLU (+ pool); the default) vs the combine +
-    bn_finalize + bn_apply launches (CS_BN_SPLITK_TAIL=0): same forward values up to the order
-    of the statistics sums, a norm bound after two SGD steps, identical num_batches_tracked and
-    running statistics to float rounding; run to run bitwise."""
-    out = []
-    for tail in ("0", "1", "1"):
-        monkeypatch.setenv("CS_BN_SPLITK_TAIL", tail)
-        t = _trainer(dev, batch_size=B, train_size=256, autotune=True)
-        for _ in range(2):
-            t.step()
-        torch.cuda.synchronize()
-        out.append((t.params.clone(), t.mom.clone(), t.bufs.clone(), t.nbt.clone(), t.last_loss()))
-    a, b, c = out
-    assert abs(a[4] - b[4]) < 1e-4 * max(1.0, abs(a[4]))
-    for name, x, y in zip(("params", "mom", "bufs"), a[:3], b[:3]):
-        d = (y.double() - x.double()).norm() / x.double().norm()
-        assert d.item() < 1e-2, (name, d.item())
-    assert torch.equal(a[3], b[3])
-    for x, y in zip(b[:4], c[:4]):
-        assert torch.equal(x, y)
-
-
 @pytest.mark.parametrize("B", [64, 40])
 def test_bn_bwd_from_slabs_matches_combine(dev, monkeypatch, B):
     """Small layers' BN backward read straight from the producing data gradient's split-K slabs
