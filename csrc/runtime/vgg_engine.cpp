@@ -522,7 +522,8 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
     // one-launch BN backward
     // (measured against the BN backward's own reduce pass next to the side stream: +0.2-0.7 %,
     // profiles/r4_ab_bn_epi_red.txt)
-    const bool slabs = bwd_slab_ok(l, B) && (ovl || !dual_ok(l));
+    // (the same choice in both schedules: the overlapped and the serial step stay bitwise equal)
+    const bool slabs = bwd_slab_ok(l, B);
     const bool er = l > 0 && !slabs;
     CsBnRed erv{};
     CsBnFin fin{};
@@ -550,7 +551,7 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
         conv(l, CS_CONV_WGRAD, (int)B, b.tile[CS_CONV_WGRAD], s, false, ws_.data_ptr<float>(), dz);
         if (bwd_sgd_) sgd_on(s, blk_range_[0].first, blk_range_[0].second, true);
       }
-    } else if (dual_ok(l)) {  // wgrad + dgrad in one launch (no appended SGD blocks: the update runs first)
+    } else if (dual_ok(l) && !slabs) {  // wgrad + dgrad in one launch (no appended SGD blocks: the update runs first)
       if (sgd_tail_ && l + 1 < L) sgd_on(s, blk_range_[l + 1].first, blk_range_[l + 1].second, false);
       conv_dual(l, (int)B, s, dz, &erv, fp);
     } else {
