@@ -198,7 +198,7 @@ VggEngine::VggEngine(int64_t Bmax, std::vector<int64_t> desc, std::vector<int64_
   }
   if (const char* e = getenv("CS_CONV_DUAL")) dual_ = atoi(e) != 0;
   if (const char* e = getenv("CS_BN_FUSED_ROWS")) bn_fused_rows_ = atoll(e);
-  if (const char* e = getenv("CS_BN_BWD_SLABS")) bwd_slab_on_ = atoi(e) != 0;
+  if (const char* e = getenv("CS_BN_BWD_SLABS")) bwd_slab_rows_ = atoll(e);
   if (const char* e = getenv("CS_CONV_MATH")) math_ = atoi(e);
   bn_part_ = torch::zeros({partmax}, fo);
   bn_coef_ = torch::zeros({cmax * 3}, fo);
@@ -286,12 +286,12 @@ void VggEngine::conv(int l, int mode, int B, const ConvTile& t, hipStream_t s, b
 }
 
 bool VggEngine::bwd_slab_ok(int l, int64_t B) const {
-  if (!bwd_slab_on_ || l < 1) return false;
+  if (bwd_slab_rows_ <= 0 || l < 1) return false;
   const VggBlock& b = blocks_[l];
   const VggBlock& p = blocks_[l - 1];
   const ConvTile& t = b.tile[CS_CONV_DGRAD];
   const int sp = eff_splits(dims(b, CS_CONV_DGRAD, B).K, t.splits, t.bk);
-  return B * p.H * p.H <= 1024 && p.cout % 16 == 0 && sp >= 2 && sp <= 32;
+  return B * p.H * p.H <= bwd_slab_rows_ && p.cout % 16 == 0 && sp >= 2 && sp <= 32;
 }
 
 bool VggEngine::bn_fused(int l, int64_t B) const {

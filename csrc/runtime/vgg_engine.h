@@ -195,8 +195,8 @@ class VggEngine {
   bool fin_on_ = true;
   // small-layer BN backward straight from the data gradient's split-K slabs: one launch (reduce +
   // finalize + apply, cs_bn_fused_bwd) instead of the combine, finalize and apply launches
-  // (CS_BN_BWD_SLABS=0: measurement)
-  bool bwd_slab_on_ = true;
+  // for layers of at most bwd_slab_rows_ rows (CS_BN_BWD_SLABS=<rows>, 0: off)
+  int64_t bwd_slab_rows_ = 0;  // off: at <= 1024 rows it measured 7 % slower (profiles/r4_ab_bn_bwd_slabs.txt)
   int slab_pending_ = -1, slab_S_ = 0;
   int64_t slab_stride_ = 0;
   bool dual_ = true;

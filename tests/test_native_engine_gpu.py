@@ -513,12 +513,12 @@ def test_long_run_no_syncs_deterministic(dev):
 @pytest.mark.parametrize("B", [64, 40])
 def test_bn_bwd_from_slabs_matches_combine(dev, monkeypatch, B):
     """Small layers' BN backward read straight from the producing data gradient's split-K slabs
-    (one launch: reduce + finalize + apply summing the slabs as it reads; the default) vs the
-    combine (with the BN partials in its epilogue) + finalize + apply launches (CS_BN_BWD_SLABS=0):
+    (one launch: reduce + finalize + apply summing the slabs as it reads; CS_BN_BWD_SLABS=1024,
+    opt-in) vs the combine (with the BN partials in its epilogue) + finalize + apply launches (the default):
     a norm bound after two SGD steps (different summation orders), identical num_batches_tracked,
     run to run bitwise."""
     out = []
-    for slabs in ("0", "1", "1"):
+    for slabs in ("0", "1024", "1024"):
         monkeypatch.setenv("CS_BN_BWD_SLABS", slabs)
         t = _trainer(dev, batch_size=B, train_size=256, autotune=True)
         for _ in range(2):
