@@ -1260,9 +1260,6 @@ hipError_t cs_conv_gemm(CsConvArgs a, int mode, int bm, int bn, int bk, int spli
   splits = prep_gemm(a, mode, bk, splits);
   if (splits < 0) return hipErrorInvalidValue;
   a.sgd.P = a.sgd.n > 0 ? (int)std::min<int64_t>(256, (a.sgd.n / 4 + 255) / 256) : 0;
-  if (a.no_reduce && (mode != CS_CONV_DGRAD || splits < 2 || splits > 2 * kFold || a.ered.part != nullptr ||
-                      a.fin.cnt != nullptr))
-    return hipErrorInvalidValue;  // slabs left for the consumer: plain DGRAD split-K only
   if (a.fin.cnt != nullptr) {  // last-arriver BN finalize: its statistics must exist in this launch pair
     if (mode == CS_CONV_WGRAD || (mode == CS_CONV_FWD && a.stats == nullptr) ||
         (mode == CS_CONV_DGRAD && a.ered.part == nullptr))
@@ -1277,7 +1274,7 @@ hipError_t cs_conv_gemm(CsConvArgs a, int mode, int bm, int bn, int bk, int spli
     if (mode == CS_CONV_FWD) e = launch_gemm<BM_, BN_, CS_CONV_FWD, BK_>(a, splits, stage, stream);     \
     else if (mode == CS_CONV_DGRAD) e = launch_gemm<BM_, BN_, CS_CONV_DGRAD, BK_>(a, splits, stage, stream); \
     else e = launch_gemm<BM_, BN_, CS_CONV_WGRAD, BK_>(a, splits, stage, stream);                       \
-    if (e != hipSuccess || splits == 1 || a.no_reduce) return e;                                         \
+    if (e != hipSuccess || splits == 1) return e;                                                        \
     return launch_reduce(a, mode, splits, stream);                                                       \
   }
   CS_DISPATCH(64, 64, 16)

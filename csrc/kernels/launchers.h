@@ -112,9 +112,6 @@ struct CsConvArgs {
   // FWD (with stats) / DGRAD (with ered): the BN finalize by the launch's last-arriving block
   // (or the split-K combine's); fin.cnt == null: off
   CsBnFin fin;
-  // DGRAD with split-K (<= 32 splits): no combine launch; the [splits][M][N] slabs in ws are the
-  // consumer's input (cs_bn_fused_bwd sums them as it reads, gslabs / gstride)
-  int no_reduce;
   // filled by the launcher:
   int lgH, lgW, lgCin, lgCout, M, N, K, ksteps_per_split, total_ksteps;
 };

@@ -198,7 +198,6 @@ VggEngine::VggEngine(int64_t Bmax, std::vector<int64_t> desc, std::vector<int64_
   }
   if (const char* e = getenv("CS_CONV_DUAL")) dual_ = atoi(e) != 0;
   if (const char* e = getenv("CS_BN_FUSED_ROWS")) bn_fused_rows_ = atoll(e);
-  if (const char* e = getenv("CS_BN_BWD_SLABS")) bwd_slab_rows_ = atoll(e);
   if (const char* e = getenv("CS_CONV_MATH")) math_ = atoi(e);
   bn_part_ = torch::zeros({partmax}, fo);
   bn_coef_ = torch::zeros({cmax * 3}, fo);
@@ -268,8 +267,7 @@ CsConvArgs VggEngine::conv_args(int l, int mode, int B, bool with_stats, float* 
 }
 
 void VggEngine::conv(int l, int mode, int B, const ConvTile& t, hipStream_t s, bool with_stats, float* ws,
-                     float* dz, const CsBnRed* ered, const CsSgdTail* sgd, const CsBnFin* fin,
-                     bool no_reduce) {
+                     float* dz, const CsBnRed* ered, const CsSgdTail* sgd, const CsBnFin* fin) {
   VggBlock& b = blocks_[l];
   CsConvArgs a = conv_args(l, mode, B, with_stats, ws, dz);
   if (ered != nullptr) {
@@ -278,20 +276,10 @@ void VggEngine::conv(int l, int mode, int B, const ConvTile& t, hipStream_t s, b
   }
   if (sgd != nullptr) a.sgd = *sgd;
   if (fin != nullptr) a.fin = *fin;
-  a.no_reduce = no_reduce ? 1 : 0;
   const Dims d = dims(b, mode, B);
   const int sp = eff_splits(d.K, t.splits, t.bk);
   TORCH_CHECK(sp == 1 || (int64_t)sp * d.M * d.N <= ws_elems_, "VggEngine: split-K workspace too small");
   ok(cs_conv_gemm(a, mode, t.bm, t.bn, t.bk, t.splits, s, t.stage), "conv_gemm");
-}
-
-bool VggEngine::bwd_slab_ok(int l, int64_t B) const {
-  if (bwd_slab_rows_ <= 0 || l < 1) return false;
-  const VggBlock& b = blocks_[l];
-  const VggBlock& p = blocks_[l - 1];
-  const ConvTile& t = b.tile[CS_CONV_DGRAD];
-  const int sp = eff_splits(dims(b, CS_CONV_DGRAD, B).K, t.splits, t.bk);
-  return B * p.H * p.H <= bwd_slab_rows_ && p.cout % 16 == 0 && sp >= 2 && sp <= 32;
 }
 
 bool VggEngine::bn_fused(int l, int64_t B) const {
@@ -420,7 +408,6 @@ void VggEngine::forward_train(int64_t B) {
   flush_signal(s);
   // one launch: sampler index (device cursor into the epoch permutation, or idx_ when no
   // permutation is set), label gather, crop/flip/normalize into block 0's NHWC input
-  slab_pending_ = -1;
   const bool use_perm = perm_len_ > 0;
   ok(cs_make_batch(data_[0].data_ptr<uint8_t>(), labels_[0].data_ptr<int64_t>(),
                    use_perm ? perm_.data_ptr<int64_t>() : nullptr, use_perm ? cursor_.data_ptr<int64_t>() : nullptr,
@@ -483,15 +470,7 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
     const float* Gin = gbuf_[(L - 1 - l) % 2].data_ptr<float>();
     // ---- BN (+ReLU, +pool) backward of block l -> dz (the deferred side-stream signal of block
     // l+1's fork rides its first launch)
-    if (slab_pending_ == l) {
-      // block l+1's data gradient left its split-K slabs: reduce + finalize + apply in one launch,
-      // summing the slabs as it reads them
-      ok(cs_bn_fused_bwd(b.y.data_ptr<float>(), ws_.data_ptr<float>(), (int)B, b.H, b.H, b.cout, b.pool, bn, P(b.g_off),
-                         bn_coef_.data_ptr<float>(), G(b.g_off), G(b.be_off), G(b.b_off), dz, s, slab_S_, slab_stride_,
-                         pending_sig_),
-         "bn_fused_bwd(slabs)");
-      pending_sig_ = nullptr;
-    } else if (red_pending_ == l) {
+    if (red_pending_ == l) {
       // the partial sums (and, with fin, the finalize) ran inside block l+1's data-gradient launch
       if (fin_on_)
         ok(cs_bn_bwd_apply(b.y.data_ptr<float>(), Gin, (int)B, b.H, b.H, b.cout, b.pool, bn, bn + b.cout,
@@ -516,15 +495,11 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
          "bn_bwd");
     }
     red_pending_ = -1;
-    slab_pending_ = -1;
     // ---- weight and data gradients of block l; block l-1's BN-backward partials (and their
-    // finalize) ride the data gradient, or (small layers) its split-K slabs go to block l-1's
-    // one-launch BN backward
+    // finalize) ride the data gradient
     // (measured against the BN backward's own reduce pass next to the side stream: +0.2-0.7 %,
     // profiles/r4_ab_bn_epi_red.txt)
-    // (the same choice in both schedules: the overlapped and the serial step stay bitwise equal)
-    const bool slabs = bwd_slab_ok(l, B);
-    const bool er = l > 0 && !slabs;
+    const bool er = l > 0;
     CsBnRed erv{};
     CsBnFin fin{};
     if (er) {
@@ -537,8 +512,7 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
         // the data gradient keeps the whole chip on the critical chain; the weight gradient forks
         // to the side stream after it and fills the chip while the main stream runs the
         // latency-bound BN kernels (and the split-K combine) of the block below
-        conv(l, CS_CONV_DGRAD, (int)B, b.tile[CS_CONV_DGRAD], s, false, nullptr, dz, slabs ? nullptr : &erv, nullptr,
-             fp, slabs);
+        conv(l, CS_CONV_DGRAD, (int)B, b.tile[CS_CONV_DGRAD], s, false, nullptr, dz, &erv, nullptr, fp);
         pending_sig_ = dz_link_->defer();
         dz_link_->wait(side_);
         conv(l, CS_CONV_WGRAD, (int)B, b.tile[CS_CONV_WGRAD], side_, false, ws_w_.data_ptr<float>(), dz);
@@ -551,7 +525,7 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
         conv(l, CS_CONV_WGRAD, (int)B, b.tile[CS_CONV_WGRAD], s, false, ws_.data_ptr<float>(), dz);
         if (bwd_sgd_) sgd_on(s, blk_range_[0].first, blk_range_[0].second, true);
       }
-    } else if (dual_ok(l) && !slabs) {  // wgrad + dgrad in one launch (no appended SGD blocks: the update runs first)
+    } else if (dual_ok(l)) {  // wgrad + dgrad in one launch (no appended SGD blocks: the update runs first)
       if (sgd_tail_ && l + 1 < L) sgd_on(s, blk_range_[l + 1].first, blk_range_[l + 1].second, false);
       conv_dual(l, (int)B, s, dz, &erv, fp);
     } else {
@@ -564,20 +538,11 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
       conv(l, CS_CONV_WGRAD, (int)B, b.tile[CS_CONV_WGRAD], s, false, ws_w_.data_ptr<float>(), dz, nullptr,
            tail.n > 0 ? &tail : nullptr);
       if (l > 0)
-        conv(l, CS_CONV_DGRAD, (int)B, b.tile[CS_CONV_DGRAD], s, false, nullptr, dz, slabs ? nullptr : &erv, nullptr,
-             fp, slabs);
+        conv(l, CS_CONV_DGRAD, (int)B, b.tile[CS_CONV_DGRAD], s, false, nullptr, dz, &erv, nullptr, fp);
     }
     if (er) {
       red_pending_ = l - 1;
       red_P_ = erv.P;
-    }
-    if (slabs) {
-      const VggBlock& bp = blocks_[l - 1];
-      slab_pending_ = l - 1;
-      const Dims d = dims(b, CS_CONV_DGRAD, B);
-      slab_S_ = eff_splits(d.K, b.tile[CS_CONV_DGRAD].splits, b.tile[CS_CONV_DGRAD].bk);
-      slab_stride_ = d.M * d.N;  // one [M][N] slab of the data gradient (= block l-1's pooled output)
-      TORCH_CHECK(d.N == bp.cout && d.M * 4 == B * bp.H * bp.H * (bp.pool ? 1 : 4), "VggEngine: slab geometry");
     }
   }
   if (join) {

@@ -145,9 +145,7 @@ class VggEngine {
  private:
   void conv(int l, int mode, int B, const ConvTile& t, hipStream_t s, bool with_stats, float* ws = nullptr,
             float* dz = nullptr, const CsBnRed* ered = nullptr, const CsSgdTail* sgd = nullptr,
-            const CsBnFin* fin = nullptr, bool no_reduce = false);
-  // block l's data gradient leaves its split-K slabs for block l-1's one-launch BN backward
-  bool bwd_slab_ok(int l, int64_t B) const;
+            const CsBnFin* fin = nullptr);
   CsConvArgs conv_args(int l, int mode, int B, bool with_stats, float* ws, float* dz);
   // block l's wgrad + dgrad as one launch (both 64x64 register-staged tiles)
   bool dual_ok(int l) const;
@@ -193,12 +191,6 @@ class VggEngine {
   torch::Tensor gbuf_[2], dz_[2], ws_, ws_w_, bn_part_, bn_coef_, bn_eval_, head_ws_, fin_cnt_, fin_grp_;
   int64_t ws_elems_ = 0;
   bool fin_on_ = true;
-  // small-layer BN backward straight from the data gradient's split-K slabs: one launch (reduce +
-  // finalize + apply, cs_bn_fused_bwd) instead of the combine, finalize and apply launches
-  // for layers of at most bwd_slab_rows_ rows (CS_BN_BWD_SLABS=<rows>, 0: off)
-  int64_t bwd_slab_rows_ = 0;  // off: at <= 1024 rows it measured 7 % slower (profiles/r4_ab_bn_bwd_slabs.txt)
-  int slab_pending_ = -1, slab_S_ = 0;
-  int64_t slab_stride_ = 0;
   bool dual_ = true;
   int math_ = 2;  // conv autotune candidates: 0 f32 MFMA, 1 split-bf16 X6, 2 both (CS_CONV_MATH)
   // CS_BN_FUSED_ROWS; 0 disables. Measured on MI355X at B=64 (img/s): 0 -> 71.46k, 256 (blocks 6-7)

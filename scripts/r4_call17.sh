@@ -1,15 +1,9 @@
 #!/bin/bash
-# Round-4 measurement 17 (end of round): every GPU test, smoke(), the default bench; a same-box
-# A/B of the slab-fed BN backward on the smallest layer only; the default step's kernel trace;
-# the probe projection on the final engine.
+# Round-4 measurement 17 (end of round): every GPU test, smoke(), the default bench; the default
+# step's kernel trace; the probe projection on the final engine.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}" || exit 1
 bash scripts/gpu.sh suite || exit $?
-V=". .:CS_BN_BWD_SLABS=256"
-bash scripts/ab_trees.sh 3 $V -- --steps 20 --warmup 5 > gpurun_out/ab9_20_5.log 2>&1 || exit $?
-tail -2 gpurun_out/ab9_20_5.log
-bash scripts/ab_trees.sh 2 $V -- --steps 100 --warmup 10 > gpurun_out/ab9_100_10.log 2>&1 || exit $?
-tail -2 gpurun_out/ab9_100_10.log
 bash scripts/gpu.sh trace r4_end --steps 10 --warmup 5 || exit $?
 timeout -k 10 500 python -u scripts/dp_projection.py --steps 40 --warmup 10 --gbps 150,300 --ctas 0,16 \
   > gpurun_out/dp_projection_end.log 2>&1 || exit $?

@@ -508,28 +508,3 @@ def test_long_run_no_syncs_deterministic(dev):
     for r in out[1:]:
         for a, b in zip(out[0], r):
             assert torch.equal(a, b)
-
-
-@pytest.mark.parametrize("B", [64, 40])
-def test_bn_bwd_from_slabs_matches_combine(dev, monkeypatch, B):
-    """Small layers' BN backward read straight from the producing data gradient's split-K slabs
-    (one launch: reduce + finalize + apply summing the slabs as it reads; CS_BN_BWD_SLABS=1024,
-    opt-in) vs the combine (with the BN partials in its epilogue) + finalize + apply launches (the default):
-    a norm bound after two SGD steps (different summation orders), identical num_batches_tracked,
-    run to run bitwise."""
-    out = []
-    for slabs in ("0", "1024", "1024"):
-        monkeypatch.setenv("CS_BN_BWD_SLABS", slabs)
-        t = _trainer(dev, batch_size=B, train_size=256, autotune=True)
-        for _ in range(2):
-            t.step()
-        torch.cuda.synchronize()
-        out.append((t.params.clone(), t.mom.clone(), t.bufs.clone(), t.nbt.clone(), t.last_loss()))
-    a, b, c = out
-    assert abs(a[4] - b[4]) < 1e-4 * max(1.0, abs(a[4]))
-    for name, x, y in zip(("params", "mom", "bufs"), a[:3], b[:3]):
-        d = (y.double() - x.double()).norm() / x.double().norm()
-        assert d.item() < 1e-2, (name, d.item())
-    assert torch.equal(a[3], b[3])
-    for x, y in zip(b[:4], c[:4]):
-        assert torch.equal(x, y)
