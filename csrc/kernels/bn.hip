@@ -205,15 +205,15 @@ __global__ __launch_bounds__(256) void bn_bwd_kernel(const float* __restrict__ y
                                                      int H, int W, int C, const float* __restrict__ scale,
                                                      const float* __restrict__ shift, const float* __restrict__ mean,
                                                      const float* __restrict__ invstd, const float* __restrict__ coef,
-                                                     float* __restrict__ dz, float* __restrict__ part, int gslabs,
-                                                     int64_t gstride, unsigned long long* __restrict__ signal) {
+                                                     float* __restrict__ dz, float* __restrict__ part,
+                                                     unsigned long long* __restrict__ signal) {
   extern __shared__ __attribute__((aligned(16))) float red[];  // [rows][C][3] (reduce only)
   // a deferred stream-link signal (device_comm.h StreamLink::defer): this launch started, so the
   // kernels before it on the stream completed
   if (signal != nullptr && blockIdx.x == 0 && threadIdx.x == 0)
     __hip_atomic_fetch_add(signal, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if constexpr (!APPLY) {  // the shared body (also run inside weight-gradient GEMM launches)
-    const CsBnRed r{y, G, scale, shift, mean, invstd, part, gstride, B, H, W, C, POOL ? 1 : 0, (int)gridDim.x, gslabs};
+    const CsBnRed r{y, G, scale, shift, mean, invstd, part, B, H, W, C, POOL ? 1 : 0, (int)gridDim.x};
     cs_bn::bn_red_body<POOL>(r, blockIdx.x, gridDim.x, red);
     return;
   }
@@ -224,7 +224,7 @@ __global__ __launch_bounds__(256) void bn_bwd_kernel(const float* __restrict__ y
   float acc[3][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
   if (rl < rows) {
     for (int u = blockIdx.x * rows + rl; u < units; u += gridDim.x * rows)
-      bwd_visit<APPLY, POOL>(y, G, B, H, W, C, cq, u, scale, shift, mean, invstd, coef, dz, acc, gslabs, gstride);
+      bwd_visit<APPLY, POOL>(y, G, B, H, W, C, cq, u, scale, shift, mean, invstd, coef, dz, acc);
   }
   if (APPLY) return;
   if (rl < rows) {
@@ -475,7 +475,6 @@ __global__ __launch_bounds__(256) void bn_fused_bwd_kernel(const float* __restri
                                                            const float* __restrict__ gamma, float* __restrict__ coef,
                                                            float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                            float* __restrict__ dbias, float* __restrict__ dz,
-                                                           int gslabs, int64_t gstride,
                                                            unsigned long long* __restrict__ signal) {
   __shared__ float lds[4 * 4 * 3 * 4];
   __shared__ float coef_sh[3 * kFusedCh];  // this block's 16 channels' dZ coefficients
@@ -497,7 +496,7 @@ __global__ __launch_bounds__(256) void bn_fused_bwd_kernel(const float* __restri
     for (int q = 0; q < 4; ++q) k1q[q] = gamma[4 * cqg + q] * invstd[4 * cqg + q];
   float acc[3][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
   for (int u = rl; u < units; u += 64)
-    bwd_visit<false, POOL>(y, G, B, H, W, C, cqg, u, scale, shift, mean, invstd, coef, dz, acc, gslabs, gstride);
+    bwd_visit<false, POOL>(y, G, B, H, W, C, cqg, u, scale, shift, mean, invstd, coef, dz, acc);
   sum_reduce_block(acc, lds);
   const int c0 = blockIdx.x * kFusedCh;
   if (threadIdx.x < 4) {
@@ -520,8 +519,7 @@ __global__ __launch_bounds__(256) void bn_fused_bwd_kernel(const float* __restri
   __syncthreads();  // the apply pass reads the coefficients from LDS (no global round trip)
   float dummy[3][4];
   for (int u = rl; u < units; u += 64)
-    bwd_visit<true, POOL>(y, G, B, H, W, C, cqg, u, scale, shift, mean, invstd, coef_sh, dz, dummy, gslabs, gstride,
-                          c0);
+    bwd_visit<true, POOL>(y, G, B, H, W, C, cqg, u, scale, shift, mean, invstd, coef_sh, dz, dummy, c0);
 }
 
 }  // namespace
@@ -567,29 +565,28 @@ hipError_t cs_bn_apply(const float* y, const float* scale, const float* shift, f
 
 hipError_t cs_bn_bwd(const float* y, const float* G, int B, int H, int W, int C, int pool, const float* scale,
                      const float* shift, const float* mean, const float* invstd, const float* gamma, float* part,
-                     float* coef, float* dgamma, float* dbeta, float* dbias, float* dz, hipStream_t stream,
-                     int gslabs, int64_t gstride) {
-  if (C % 4 != 0 || C > 1024 || (pool && ((H | W) & 1)) || gslabs < 1) return hipErrorInvalidValue;
+                     float* coef, float* dgamma, float* dbeta, float* dbias, float* dz, hipStream_t stream) {
+  if (C % 4 != 0 || C > 1024 || (pool && ((H | W) & 1))) return hipErrorInvalidValue;
   const int P = cs_bn_bwd_blocks(B, H, W, C, pool);
   const int rows = 256 / (C / 4);
   const size_t lds = (size_t)rows * C * 3 * sizeof(float);
   if (pool) {
     hipLaunchKernelGGL((bn_bwd_kernel<false, true>), dim3(P), dim3(256), lds, stream, y, G, B, H, W, C, scale, shift,
-                       mean, invstd, nullptr, nullptr, part, gslabs, gstride, nullptr);
+                       mean, invstd, nullptr, nullptr, part, nullptr);
   } else {
     hipLaunchKernelGGL((bn_bwd_kernel<false, false>), dim3(P), dim3(256), lds, stream, y, G, B, H, W, C, scale, shift,
-                       mean, invstd, nullptr, nullptr, part, gslabs, gstride, nullptr);
+                       mean, invstd, nullptr, nullptr, part, nullptr);
   }
   if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
   return cs_bn_bwd_tail(y, G, B, H, W, C, pool, scale, shift, mean, invstd, gamma, part, P, coef, dgamma, dbeta,
-                        dbias, dz, stream, gslabs, gstride);
+                        dbias, dz, stream);
 }
 
 hipError_t cs_bn_bwd_tail(const float* y, const float* G, int B, int H, int W, int C, int pool, const float* scale,
                           const float* shift, const float* mean, const float* invstd, const float* gamma,
                           const float* part, int P, float* coef, float* dgamma, float* dbeta, float* dbias, float* dz,
-                          hipStream_t stream, int gslabs, int64_t gstride, unsigned long long* signal) {
-  if (C % 4 != 0 || C > 1024 || (pool && ((H | W) & 1)) || gslabs < 1 || P < 1) return hipErrorInvalidValue;
+                          hipStream_t stream, unsigned long long* signal) {
+  if (C % 4 != 0 || C > 1024 || (pool && ((H | W) & 1)) || P < 1) return hipErrorInvalidValue;
   const int M = B * H * W;
   const int rows = 256 / (C / 4);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 3) / 4), dim3(256), 0, stream, part, P, C, M, gamma, invstd,
@@ -600,10 +597,10 @@ hipError_t cs_bn_bwd_tail(const float* y, const float* G, int B, int H, int W, i
   if (blocks > 2048) blocks = 2048;
   if (pool) {
     hipLaunchKernelGGL((bn_bwd_kernel<true, true>), dim3(blocks), dim3(256), 0, stream, y, G, B, H, W, C, scale, shift,
-                       mean, invstd, coef, dz, nullptr, gslabs, gstride, nullptr);
+                       mean, invstd, coef, dz, nullptr, nullptr);
   } else {
     hipLaunchKernelGGL((bn_bwd_kernel<true, false>), dim3(blocks), dim3(256), 0, stream, y, G, B, H, W, C, scale,
-                       shift, mean, invstd, coef, dz, nullptr, gslabs, gstride, nullptr);
+                       shift, mean, invstd, coef, dz, nullptr, nullptr);
   }
   return hipGetLastError();
 }
@@ -618,10 +615,10 @@ hipError_t cs_bn_bwd_apply(const float* y, const float* G, int B, int H, int W, 
   if (blocks > 2048) blocks = 2048;
   if (pool)
     hipLaunchKernelGGL((bn_bwd_kernel<true, true>), dim3(blocks), dim3(256), 0, stream, y, G, B, H, W, C, scale, shift,
-                       mean, invstd, coef, dz, nullptr, 1, (int64_t)0, signal);
+                       mean, invstd, coef, dz, nullptr, signal);
   else
     hipLaunchKernelGGL((bn_bwd_kernel<true, false>), dim3(blocks), dim3(256), 0, stream, y, G, B, H, W, C, scale,
-                       shift, mean, invstd, coef, dz, nullptr, 1, (int64_t)0, signal);
+                       shift, mean, invstd, coef, dz, nullptr, signal);
   return hipGetLastError();
 }
 
@@ -642,13 +639,13 @@ hipError_t cs_bn_fused_fwd(const float* part, int T, int R, int M, int C, const 
 
 hipError_t cs_bn_fused_bwd(const float* y, const float* G, int B, int H, int W, int C, int pool, const float* bnv,
                            const float* gamma, float* coef, float* dgamma, float* dbeta, float* dbias, float* dz,
-                           hipStream_t stream, int gslabs, int64_t gstride, unsigned long long* signal) {
-  if (C % kFusedCh != 0 || (pool && ((H | W) & 1)) || gslabs < 1) return hipErrorInvalidValue;
+                           hipStream_t stream, unsigned long long* signal) {
+  if (C % kFusedCh != 0 || (pool && ((H | W) & 1))) return hipErrorInvalidValue;
   if (pool)
     hipLaunchKernelGGL((bn_fused_bwd_kernel<true>), dim3(C / kFusedCh), dim3(256), 0, stream, y, G, B, H, W, C, bnv,
-                       gamma, coef, dgamma, dbeta, dbias, dz, gslabs, gstride, signal);
+                       gamma, coef, dgamma, dbeta, dbias, dz, signal);
   else
     hipLaunchKernelGGL((bn_fused_bwd_kernel<false>), dim3(C / kFusedCh), dim3(256), 0, stream, y, G, B, H, W, C, bnv,
-                       gamma, coef, dgamma, dbeta, dbias, dz, gslabs, gstride, signal);
+                       gamma, coef, dgamma, dbeta, dbias, dz, signal);
   return hipGetLastError();
 }

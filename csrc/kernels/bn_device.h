@@ -19,8 +19,7 @@ template <bool APPLY, bool POOL>
 __device__ __forceinline__ void bwd_visit(const float* __restrict__ y, const float* __restrict__ G, int B, int H,
                                           int W, int C, int cq, int unit, const float* scale, const float* shift,
                                           const float* mean, const float* invstd, const float* coef, float* dz,
-                                          float (&acc)[3][4], int gslabs = 1, int64_t gstride = 0,
-                                          int coef_c0 = 0) {
+                                          float (&acc)[3][4], int coef_c0 = 0) {
   const int C4 = C >> 2;
   float sc[4], sh[4], mu[4], is[4], k1[4], k2[4], k3[4];
 #pragma unroll
@@ -31,11 +30,7 @@ __device__ __forceinline__ void bwd_visit(const float* __restrict__ y, const flo
       k1[q] = coef[3 * (c - coef_c0)]; k2[q] = coef[3 * (c - coef_c0) + 1]; k3[q] = coef[3 * (c - coef_c0) + 2];
     }
   }
-  float4 g4 = reinterpret_cast<const float4*>(G)[(size_t)unit * C4 + cq];
-  for (int z = 1; z < gslabs; ++z) {  // split-K slabs of the producing GEMM, summed in z order
-    const float4 t = reinterpret_cast<const float4*>(G + (size_t)z * gstride)[(size_t)unit * C4 + cq];
-    g4.x += t.x; g4.y += t.y; g4.z += t.z; g4.w += t.w;
-  }
+  const float4 g4 = reinterpret_cast<const float4*>(G)[(size_t)unit * C4 + cq];
   const float gin[4] = {g4.x, g4.y, g4.z, g4.w};
   constexpr int NP = POOL ? 4 : 1;
   size_t off[NP];
@@ -183,7 +178,7 @@ __device__ __forceinline__ void bn_red_body(const CsBnRed& r, int blk, int nblk,
   if (rl < rows && threadIdx.x < 256) {
     for (int u = blk * rows + rl; u < units; u += nblk * rows)
       bwd_visit<false, POOL>(r.y, r.G, r.B, r.H, r.W, C, cq, u, r.scale, r.shift, r.mean, r.invstd, nullptr, nullptr,
-                             acc, r.gslabs, r.gstride);
+                             acc);
     for (int k = 0; k < 3; ++k)
       for (int q = 0; q < 4; ++q) red[((size_t)rl * C + 4 * cq + q) * 3 + k] = acc[k][q];
   }

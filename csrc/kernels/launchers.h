@@ -47,14 +47,12 @@ hipError_t cs_softmax_xent(const float* logits, const int64_t* labels, int B, in
 // ---------------------------------------------------------------- conv (implicit GEMM, fp32 MFMA)
 enum { CS_CONV_FWD = 0, CS_CONV_DGRAD = 1, CS_CONV_WGRAD = 2 };
 
-// One BN-backward partial-sum pass (bn.hip "reduce"): y, incoming gradient G (optionally as
-// gslabs split-K slabs gstride apart), the forward's scale/shift/mean/invstd, partials out
-// part [P][C][3]. P == 0: none.
+// One BN-backward partial-sum pass (bn.hip "reduce"): y, incoming gradient G, the forward's
+// scale/shift/mean/invstd, partials out part [P][C][3]. P == 0: none.
 struct CsBnRed {
   const float *y, *G, *scale, *shift, *mean, *invstd;
   float* part;
-  int64_t gstride;
-  int B, H, W, C, pool, P, gslabs;
+  int B, H, W, C, pool, P;
 };
 
 // An SGD update of one parameter range carried by extra blocks appended to a GEMM launch (after
@@ -180,14 +178,10 @@ inline size_t cs_bn_red_lds(int C) { return (size_t)(256 / (C / 4)) * C * 3 * si
 hipError_t cs_bn_bwd_tail(const float* y, const float* G, int B, int H, int W, int C, int pool, const float* scale,
                           const float* shift, const float* mean, const float* invstd, const float* gamma,
                           const float* part, int P, float* coef, float* dgamma, float* dbeta, float* dbias, float* dz,
-                          hipStream_t stream, int gslabs = 1, int64_t gstride = 0,
-                          unsigned long long* signal = nullptr);
-// G may be split-K slabs of the data-gradient GEMM: G = sum_{z < gslabs} G[z * gstride + i]
-// (summed in z order, bit-equal to the split-K combine launch it replaces)
+                          hipStream_t stream, unsigned long long* signal = nullptr);
 hipError_t cs_bn_bwd(const float* y, const float* G, int B, int H, int W, int C, int pool, const float* scale,
                      const float* shift, const float* mean, const float* invstd, const float* gamma, float* part,
-                     float* coef, float* dgamma, float* dbeta, float* dbias, float* dz, hipStream_t stream,
-                     int gslabs = 1, int64_t gstride = 0);
+                     float* coef, float* dgamma, float* dbeta, float* dbias, float* dz, hipStream_t stream);
 
 // single-launch BN for small layers (one block per 16 channels owns all their rows):
 // forward = finalize (tile partials -> bnv [4][C] = scale, shift, mean, invstd + running stats)
@@ -197,8 +191,7 @@ hipError_t cs_bn_fused_fwd(const float* part, int T, int R, int M, int C, const 
                            float* bnv, const float* y, float* out, int B, int H, int W, int pool, hipStream_t stream);
 hipError_t cs_bn_fused_bwd(const float* y, const float* G, int B, int H, int W, int C, int pool, const float* bnv,
                            const float* gamma, float* coef, float* dgamma, float* dbeta, float* dbias, float* dz,
-                           hipStream_t stream, int gslabs = 1, int64_t gstride = 0,
-                           unsigned long long* signal = nullptr);
+                           hipStream_t stream, unsigned long long* signal = nullptr);
 // the BN backward's apply pass alone (dZ from G, y and the finalized coef [C][3]): the finalize
 // ran as the last-arriver tail of the data-gradient launch that produced G (CsConvArgs::fin)
 hipError_t cs_bn_bwd_apply(const float* y, const float* G, int B, int H, int W, int C, int pool, const float* scale,

@@ -334,7 +334,6 @@ CsBnRed VggEngine::ered_args(int l, int B) {
   r.H = r.W = (int)c.H;
   r.C = (int)c.cout;
   r.pool = c.pool;
-  r.gslabs = 1;
   // P = row tiles of block l's data gradient (M = B * H_l * W_l rows)
   const ConvTile& t = blocks_[l].tile[CS_CONV_DGRAD];
   const Dims d = dims(blocks_[l], CS_CONV_DGRAD, B);
@@ -479,12 +478,12 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
       else
         ok(cs_bn_bwd_tail(b.y.data_ptr<float>(), Gin, (int)B, b.H, b.H, b.cout, b.pool, bn, bn + b.cout,
                           bn + 2 * b.cout, bn + 3 * b.cout, P(b.g_off), bn_part_.data_ptr<float>(), red_P_,
-                          bn_coef_.data_ptr<float>(), G(b.g_off), G(b.be_off), G(b.b_off), dz, s, 1, 0, pending_sig_),
+                          bn_coef_.data_ptr<float>(), G(b.g_off), G(b.be_off), G(b.b_off), dz, s, pending_sig_),
            "bn_bwd_tail");
       pending_sig_ = nullptr;
     } else if (bn_fused(l, B)) {  // reduce + finalize + apply in one launch (the top block)
       ok(cs_bn_fused_bwd(b.y.data_ptr<float>(), Gin, (int)B, b.H, b.H, b.cout, b.pool, bn, P(b.g_off),
-                         bn_coef_.data_ptr<float>(), G(b.g_off), G(b.be_off), G(b.b_off), dz, s, 1, 0, pending_sig_),
+                         bn_coef_.data_ptr<float>(), G(b.g_off), G(b.be_off), G(b.b_off), dz, s, pending_sig_),
          "bn_fused_bwd");
       pending_sig_ = nullptr;
     } else {
