@@ -68,18 +68,18 @@ def _wgrad_splits(M: int, Co: int, Kp: int) -> int:
 # bf16 GEMM of csrc/kernels/gemm_bf16.hip for every bf16 one (operands read in place, transposed in
 # LDS where needed, split-K weight gradient), "auto" = native where the output has >= 256 columns
 # (its 256 x 256 tile would be mostly idle on narrower ones), "wgrad" = native for the weight
-# gradients with >= 256 columns only (dY^T col, both operands M-major: the product where the
-# native GEMM beats hipBLASLt, profiles/r4_gemm_bench_v2.jsonl; ops/lm.py's CS_LM_GEMM=wgrad)
+# gradients with >= 256 rows and columns only (dY^T col, both operands M-major: the product where
+# the native GEMM beats hipBLASLt, profiles/r4_gemm_bench_v2.jsonl; ops/lm.py's CS_LM_GEMM=wgrad)
 _CONV_GEMM = os.environ.get("CS_CONV_GEMM", "blas")
 if _CONV_GEMM not in ("blas", "native", "auto", "wgrad"):
     raise ValueError(f"CS_CONV_GEMM must be 'blas', 'native', 'auto' or 'wgrad', got {_CONV_GEMM!r}")
 
 
-def _native_gemm(a: torch.Tensor, n: int, wgrad: bool = False) -> bool:
+def _native_gemm(a: torch.Tensor, n: int, wgrad: bool = False, m: int = 0) -> bool:
     if a.dtype != torch.bfloat16:
         return False
     return (_CONV_GEMM == "native" or (_CONV_GEMM == "auto" and n >= 256)
-            or (_CONV_GEMM == "wgrad" and wgrad and n >= 256))
+            or (_CONV_GEMM == "wgrad" and wgrad and n >= 256 and m >= 256))
 
 
 # a native-GEMM forward convolution also returns its output's BatchNorm statistics per 256-row
@@ -92,7 +92,7 @@ def _wgrad(dy2: torch.Tensor, col: torch.Tensor) -> torch.Tensor:
     """fp32 dY^T @ col, split over row chunks when the output alone cannot fill the chip"""
     M, Co = dy2.shape
     Kp = col.shape[1]
-    if _native_gemm(col, Kp, wgrad=True):
+    if _native_gemm(col, Kp, wgrad=True, m=Co):
         return native.C().mm_bf16(dy2.t(), col, True)  # split-K slabs + fixed-order sum inside
     S = _wgrad_splits(M, Co, Kp)
     if S == 1:

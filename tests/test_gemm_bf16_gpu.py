@@ -223,12 +223,13 @@ def test_resnet_bottleneck_native_gemm_close_to_blas(C, monkeypatch):
     from cs744_pytorch_distributed_tutorial_amd.models import resnet as rn
     from cs744_pytorch_distributed_tutorial_amd.ops import cnn_nhwc
     torch.manual_seed(8)
-    blk0 = rn.Bottleneck(256, 64).cuda()
-    x0 = torch.randn(8, 14, 14, 256, device="cuda").bfloat16()
+    # 1024 -> 256 -> 1024 channels: every GEMM of the block is >= 256 wide (the "wgrad" mode's bar)
+    blk0 = rn.Bottleneck(1024, 256).cuda()
+    x0 = torch.randn(8, 14, 14, 1024, device="cuda").bfloat16()
     res = {}
     for mode in ("blas", "native", "wgrad"):
         monkeypatch.setattr(cnn_nhwc, "_CONV_GEMM", mode)
-        blk = rn.Bottleneck(256, 64).cuda()
+        blk = rn.Bottleneck(1024, 256).cuda()
         blk.load_state_dict(blk0.state_dict())
         x = x0.clone().requires_grad_()
         with torch.autocast("cuda", dtype=torch.bfloat16):
