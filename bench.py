@@ -57,7 +57,12 @@ def parse(argv=None):
                    choices=["torch", "native"])
     p.add_argument("--sync", type=str, default="ddp",
                    choices=["ddp", "allreduce", "gather_scatter", "p2p", "flat"])
-    p.add_argument("--comm", type=str, default="rccl", choices=["torch", "rccl"])
+    p.add_argument("--comm", type=str, default="rccl", choices=["torch", "rccl", "staged"],
+                   help="gradient transport at N > 1: rccl = the native RCCL communicator over xGMI (one GPU per "
+                        "rank); torch = torch.distributed; staged = the native C++ step over a gloo process group "
+                        "with host staging (several ranks may share one GPU: the N > 1 code path on a 1-GPU box)")
+    p.add_argument("--busbw-iters", type=int, default=10,
+                   help="N > 1: all-reduce timings per bucket size after the timed steps (0 = skip)")
     p.add_argument("--bucket-mb", type=float, default=4.0,
                    help="DDP bucket cap; buckets close at layer boundaries (VGG-11: 9|9|9|4.5|3.7 MiB)")
     p.add_argument("--bucket-policy", type=str, default="layer", choices=["size", "layer", "single"])
@@ -184,6 +189,49 @@ def calibration(device) -> dict:
     return out
 
 
+def _bench_comm(trainer):
+    """The native DeviceComm the steps used (VGG engine, or the framework DDP's), or None."""
+    native = getattr(trainer, "native_comm", None)
+    if native is None:
+        native = getattr(getattr(getattr(trainer, "net", None), "comm", None), "native", None)
+    return native
+
+
+def measure_busbw(trainer, world: int, device, iters: int = 10, warm: int = 3) -> dict:
+    """All-reduce(AVG) bus bandwidth (GB/s, nccl-tests factor 2(N-1)/N) per distinct gradient-bucket
+    size of the trainer's plan (VGG-11 at the 4 MiB cap: 9.0 / 4.5 / 3.4 / 0.3 MiB ...; 1/4/16/64 MiB
+    for the autograd trainers), on the communicator the timed steps used; time = max over ranks.
+    Reference: the gloo all_reduce of `master/part2b/part2b.py:43-45`, BASELINE.md busBW rows."""
+    native = _bench_comm(trainer)
+    ranges = getattr(trainer, "bucket_ranges", None)
+    sizes = sorted({int(n) for _, n in ranges}, reverse=True) if ranges else [(k << 20) // 4 for k in (1, 4, 16, 64)]
+    out = {}
+    for n in sizes:
+        buf = torch.ones(n, dtype=torch.float32, device=device)
+
+        def run():
+            if native is not None:
+                native.all_reduce(buf, "avg")
+            else:
+                D.all_reduce(buf, op=D.ReduceOp.AVG)
+        for _ in range(warm):
+            run()
+        if native is not None:
+            native.join()
+        torch.cuda.synchronize()
+        D.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            run()
+        if native is not None:
+            native.join()
+        torch.cuda.synchronize()
+        t = D.all_reduce_scalar((time.perf_counter() - t0) / iters, op=D.ReduceOp.MAX)
+        out[f"{4 * n / 2 ** 20:.2f}MiB"] = round(4 * n / t / 1e9 * 2 * (world - 1) / world, 3)
+    return out
+
+
 def main(argv=None) -> int:
     args = parse(argv)
     if args.batch_size is None:
@@ -198,18 +246,23 @@ def main(argv=None) -> int:
     if args.seq_len == 0 and "8b" in args.model.lower():
         args.seq_len = 2048  # the round-1 measurements' context (the model's max_seq is 8192)
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    # one GPU per rank; the staged transport lets ranks share GPUs (local rank modulo the count:
+    # device_count() does not initialise HIP on this stack)
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev_index = local % max(torch.cuda.device_count(), 1) if args.comm == "staged" else local
     if args.engine == "native" and is_vgg(args.model):
         # before the process group or anything else creates streams: the native engine's side
         # stream must own a hardware queue (measured 4x slower steps when it shares one)
         from cs744_pytorch_distributed_tutorial_amd.ops import native
-        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+        torch.cuda.set_device(dev_index)
         native.C().reserve_streams()
     if world_env > 1:
-        D.init_process_group(backend="nccl")
+        D.init_process_group(backend="gloo" if args.comm == "staged" else "nccl")
     rank, world = D.get_rank(), D.get_world_size()
     if world != args.gpus and rank == 0:
         print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
-    device = D.device() if world > 1 else torch.device("cuda", 0)
+    device = torch.device("cuda", dev_index) if args.comm == "staged" else (D.device() if world > 1
+                                                                             else torch.device("cuda", 0))
     torch.cuda.set_device(device)
     trainer = make_trainer(args, device, rank, world)
     # a dead peer leaves RCCL kernels spinning forever: the watchdog turns that into ncclCommAbort
@@ -248,6 +301,9 @@ def main(argv=None) -> int:
     if hasattr(trainer, "check_comm"):
         trainer.check_comm()  # async RCCL errors surface here instead of as a silent bad number
     elapsed = D.all_reduce_scalar(elapsed, op=D.ReduceOp.MAX) if world > 1 else elapsed
+    # after the timed window (it never changes `value`): all-reduce bus bandwidth per gradient-bucket
+    # size on the communicator the steps used — BASELINE.json's metric also names it
+    busbw = measure_busbw(trainer, world, device, args.busbw_iters) if world > 1 and args.busbw_iters > 0 else None
     comm_used = comm_kind(trainer, world)
     loss = trainer.last_loss()
     metric, unit, gbatch, seq, baseline, data = describe(args, trainer, world)
@@ -274,6 +330,10 @@ def main(argv=None) -> int:
                    "optimizer": "SGD(lr=0.1, momentum=0.9, wd=1e-4)", "final_loss": round(loss, 4),
                    "baseline_img_s": baseline},
     }
+    if busbw is not None:
+        out["busbw_GBps"] = busbw
+    if getattr(trainer, "queue_shared", None) is not None:
+        out["config"]["hw_queue_shared"] = trainer.queue_shared
     if hasattr(trainer, "tile_table"):
         # which MFMA math the autotuner picked per conv GEMM: f32-input MFMA, or the fp32-accurate
         # split-bf16 x6 kernels (3 bf16 pieces per operand, 6 MFMAs; f64-checked like the f32 path)

@@ -119,9 +119,42 @@ if _GEMM not in ("native", "wgrad", "blas"):
     raise ValueError(f"CS_LM_GEMM must be 'native', 'wgrad' or 'blas', got {_GEMM!r}")
 
 
+def gemm_operands_ok(a: torch.Tensor, b: torch.Tensor) -> bool:
+    """Whether ``native.C().mm_bf16(a, b)`` can run ``a @ b`` in place: the host-side preconditions
+    of ``cs_gemm_bf16`` (csrc/kernels/gemm_bf16.hip), checked here so an operand the kernel cannot
+    read (no unit stride — e.g. an expanded stride-0 gradient —, a leading dimension or an N that is
+    not a multiple of 8 / 4 — an odd vocabulary —, a base pointer off 16 bytes) goes to torch.mm
+    instead of raising inside backward."""
+    if a.dim() != 2 or b.dim() != 2 or a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16 or not a.is_cuda:
+        return False
+    M, K = a.shape
+    N = b.shape[1]
+    if M == 0 or N == 0 or K == 0:
+        return True  # mm_bf16 returns zeros without a launch
+    if a.stride(1) == 1:
+        a_kmajor, lda = True, a.stride(0)
+    elif a.stride(0) == 1:
+        a_kmajor, lda = False, a.stride(1)
+    else:
+        return False
+    if b.stride(0) == 1:
+        b_kmajor, ldb = True, b.stride(1)
+    elif b.stride(1) == 1:
+        b_kmajor, ldb = False, b.stride(0)
+    else:
+        return False
+    if lda % 8 or ldb % 8 or N % 4:
+        return False
+    if (a_kmajor or b_kmajor) and K % 8:
+        return False
+    if (lda < K if a_kmajor else lda < M) or (ldb < K if b_kmajor else ldb < N):
+        return False
+    return (a.data_ptr() | b.data_ptr()) % 16 == 0
+
+
 def _mm(a: torch.Tensor, b: torch.Tensor, out_f32: bool = False) -> torch.Tensor:
     """a @ b for bf16 2-D operands (views allowed), bf16 or fp32 out (fp32: the weight gradient)"""
-    if _GEMM == "native" or (_GEMM == "wgrad" and out_f32):
+    if (_GEMM == "native" or (_GEMM == "wgrad" and out_f32)) and gemm_operands_ok(a, b):
         return native.C().mm_bf16(a, b, out_f32)
     if out_f32:
         return torch.mm(a, b, out_dtype=torch.float32)

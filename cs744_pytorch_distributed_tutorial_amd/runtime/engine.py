@@ -296,6 +296,22 @@ class NativeTrainer:
         python_collectives = world > 1 and self.native_comm is None
         self.overlap_wgrad = (os.environ.get("CS_OVERLAP_WGRAD", "1") != "0" and not python_collectives
                               and not self._counters and (self.native_comm is None or hw_queues() >= 8))
+        # start-up self-check of what the overlap relies on: the main, side and communicator streams
+        # each own a hardware queue (a link wait ahead of its signal on a SHARED in-order queue only
+        # ends by its timeout: round 2 measured 4x slower steps). At N > 1, torch's process group and
+        # RCCL add streams of their own; if any of ours ended up sharing, the weight gradients stay
+        # on the main stream (serial backward, bit-identical) and stderr says so.
+        self.queue_shared: List[str] = []
+        if self.overlap_wgrad and os.environ.get("CS_QUEUE_CHECK", "1") != "0":
+            comm_stream = self.native_comm.stream_ptr() if self.native_comm is not None else 0
+            with torch.cuda.device(self.device):
+                self.queue_shared = list(C.queue_probe(comm_stream, 0.25))
+            if self.queue_shared:
+                import sys
+                print(f"[engine] rank {rank}: streams share a hardware queue ({', '.join(self.queue_shared)}; "
+                      f"GPU_MAX_HW_QUEUES={hw_queues()}): weight gradients run serially on the main stream",
+                      file=sys.stderr, flush=True)
+                self.overlap_wgrad = False
         self.engine.set_overlap(self.overlap_wgrad)
         # BatchNorm finalize: separate launches by default. The in-launch last-arriver finalize
         # (bn_fin.h, CS_BN_FIN=1) removes one launch per block but measured 6-8 % slower with the
@@ -535,7 +551,12 @@ class NativeTrainer:
         """Async-error poll of the native communicator (ncclCommGetAsyncError for RCCL): on an
         error the communicator is aborted (ncclCommAbort) and the step raises, so a dead peer
         becomes a prompt failure instead of a hang. Also raises when one of the
-        communicator's fork/join stream links timed out (its ordering can no longer be trusted)."""
+        communicator's fork/join stream links timed out (its ordering can no longer be trusted),
+        and — at every world size, with or without a communicator — when one of the engine's own
+        side-stream weight-gradient links timed out or was released by ``abort()``."""
+        link = self.engine.link_error() if self.engine is not None else ""
+        if link:
+            raise RuntimeError(f"rank {self.rank}: side-stream weight-gradient link failed: {link}")
         if self.native_comm is None:
             return
         err = self.native_comm.async_error()

@@ -174,6 +174,12 @@ torch::Tensor mm_bf16(torch::Tensor a, torch::Tensor b, bool out_f32, c10::optio
   else if (b.stride(1) == 1) { bk = 0; ldb = b.stride(0); }
   else TORCH_CHECK(false, "mm_bf16: b needs a unit stride");
   DevGuard g(a.device());
+  if (M == 0 || N == 0 || K == 0) {
+    // empty reduction: torch.mm semantics (zeros; an accumulator is returned unchanged) without a
+    // launch — the kernel would return hipSuccess and leave a fresh output uninitialised
+    if (acc.has_value()) return *acc;
+    return torch::zeros({M, N}, a.options().dtype(out_f32 ? at::kFloat : at::kBFloat16));
+  }
   torch::Tensor c;
   int mode;
   // fp32 results of a reduction too long for the output's tile count are split over K into slabs

@@ -46,6 +46,22 @@ void register_runtime(pybind11::module& m) {
         "create (once per process) the native engine's side stream and the communicator's stream and bind "
         "each to a hardware queue; call it before other code creates streams");
   namespace py = pybind11;
+  m.def(
+      "queue_probe",
+      [](intptr_t comm_stream, double timeout_s) {
+        // pairs of {main = the current stream, side = the engine's side stream, comm} that share one
+        // hardware queue (device_comm.h streams_share_queue); comm_stream 0 = the reserved comm stream
+        hipStream_t main_s = cur_stream(), side = cs::reserved_side_stream();
+        hipStream_t comm = comm_stream ? reinterpret_cast<hipStream_t>(comm_stream) : cs::reserved_comm_stream();
+        std::vector<std::string> out;
+        const std::pair<const char*, std::pair<hipStream_t, hipStream_t>> pairs[] = {
+            {"main/side", {main_s, side}}, {"main/comm", {main_s, comm}}, {"side/comm", {side, comm}}};
+        for (const auto& pr : pairs)
+          if (cs::streams_share_queue(pr.second.first, pr.second.second, timeout_s)) out.emplace_back(pr.first);
+        return out;
+      },
+      py::arg("comm_stream") = 0, py::arg("timeout_s") = 0.25,
+      "start-up check: which of the main / side / comm streams share a hardware queue");
   m.def("rccl_unique_id", []() { return py::bytes(cs::RcclComm::unique_id()); });
   m.def("rccl_version", []() {
     int v = 0;
@@ -188,6 +204,7 @@ void register_runtime(pybind11::module& m) {
       .def("set_timing", &cs::VggEngine::set_timing)
       .def("set_math", &cs::VggEngine::set_math)
       .def("phase_times", &cs::VggEngine::phase_times)
+      .def("link_error", &cs::VggEngine::link_error)
       .def("set_dual", &cs::VggEngine::set_dual)
       .def("set_bn_fused_rows", &cs::VggEngine::set_bn_fused_rows)
       .def("block_dual", &cs::VggEngine::block_dual)

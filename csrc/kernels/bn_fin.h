@@ -171,6 +171,16 @@ constexpr int group_tiles() { return 8 * (256 / NC); }
 
 // Called by EVERY thread of the block (barriers inside) after its partials of row tile `mt`
 // for channels [c0, c0 + NC) (column tile nt) were stored with put_stats / put_sums.
+// Memory ordering (why relaxed atomics are enough on gfx950): this is the write-through hand-off
+// of MI355X_MICROARCH.md "Valid forms" (first table row) rather than a C++ release/acquire pair:
+// (1) every partial is stored by an 8-byte agent-scope atomic store (put_stats / put_sums -> st2:
+// `global_store_dwordx2 ... sc1`, write-through), (2) EVERY storing wave drains its stores with an inline-asm
+// `s_waitcnt vmcnt(0)` (invisible to the compiler, so it cannot be dropped) before (3) the
+// workgroup barrier, after which ONE lane does the agent-scope ticket add, and (4) the last
+// arriver reads every partial back with 8-byte agent-scope atomic loads only (combine -> ld2: `sc1`
+// loads, which bypass the reading CU's L1) — the guide's "{8-B agent atomics both sides}" form. The C++ memory model does not describe `sc1`, hence no ACQ_REL on the ticket;
+// an ISA change that altered these cache semantics would need the agent release/acquire fences
+// (cdna_hip_programming.md §6 Guideline 16). Opt-in path (CS_BN_FIN=1), fp64-parity tested.
 // part: the partial array ([T][C][2] FWD, [T][C][4] BWD); C: channels; lds >= 1024 + 16 floats
 // that no wave still reads.
 template <bool BWD, int NC>

@@ -63,6 +63,11 @@ hipStream_t reserved_comm_stream();
 // reserved the same way
 hipStream_t reserved_side_stream();
 void reserve_streams();
+// Start-up self-check of the queue assumption the stream links rely on: true when `a` and `b`
+// run on ONE hardware queue. A link wait with a short timeout is enqueued on `b` ahead of its
+// signal on `a`: on separate queues the signal releases the wait at once; on a shared (in-order)
+// queue the signal sits behind the wait, which then ends by its timeout (bounded: never a hang).
+bool streams_share_queue(hipStream_t a, hipStream_t b, double timeout_s = 0.25);
 
 // One-direction kernel stream link (stream_link.hip): signal(producer) enqueues a one-lane
 // counter bump; wait(consumer) makes the consumer wait for EVERY signal issued so far (the

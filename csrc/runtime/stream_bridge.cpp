@@ -113,6 +113,27 @@ void reserve_streams() {
   (void)reserved_comm_stream();
 }
 
+bool streams_share_queue(hipStream_t a, hipStream_t b, double timeout_s) {
+  if (a == b) return true;
+  void* p = nullptr;
+  hip_ok(hipMalloc(&p, 2 * sizeof(unsigned long long)), "hipMalloc(queue probe)");
+  void* h = nullptr;
+  hip_ok(hipHostMalloc(&h, sizeof(int), hipHostMallocMapped), "hipHostMalloc(queue probe error word)");
+  int* err = static_cast<int*>(h);
+  *err = 0;
+  auto* cnt = static_cast<unsigned long long*>(p);
+  hip_ok(hipMemset(cnt, 0, 2 * sizeof(unsigned long long)), "hipMemset(queue probe)");
+  hip_ok(hipDeviceSynchronize(), "sync");
+  hip_ok(cs_link_wait(cnt, cnt + 1, err, abort_word(), timeout_s, b, 1), "queue probe wait");
+  hip_ok(cs_link_signal(cnt, a), "queue probe signal");
+  hip_ok(hipStreamSynchronize(b), "queue probe sync");
+  hip_ok(hipStreamSynchronize(a), "queue probe sync");
+  const bool shared = __atomic_load_n(err, __ATOMIC_ACQUIRE) != 0;
+  hipFree(p);
+  hipHostFree(h);
+  return shared;
+}
+
 bool stream_capturing(hipStream_t s) {
   hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
   return hipStreamIsCapturing(s, &st) == hipSuccess && st != hipStreamCaptureStatusNone;

@@ -199,6 +199,7 @@ VggEngine::VggEngine(int64_t Bmax, std::vector<int64_t> desc, std::vector<int64_
   if (const char* e = getenv("CS_CONV_DUAL")) dual_ = atoi(e) != 0;
   if (const char* e = getenv("CS_BN_FUSED_ROWS")) bn_fused_rows_ = atoll(e);
   if (const char* e = getenv("CS_CONV_MATH")) math_ = atoi(e);
+  if (const char* e = getenv("CS_DEBUG_SKIP")) debug_skip_ = atoi(e);
   bn_part_ = torch::zeros({partmax}, fo);
   bn_coef_ = torch::zeros({cmax * 3}, fo);
   bn_eval_ = torch::zeros({2, cmax}, fo);
@@ -424,7 +425,7 @@ void VggEngine::forward_train(int64_t B) {
       // conv [+ split-K combine]: its last-arriving block finalizes the batch statistics
       const CsBnFin f = fin_fwd_args(l, (int)B);
       conv(l, CS_CONV_FWD, (int)B, t, s, true, nullptr, nullptr, nullptr, nullptr, &f);
-    } else {
+    } else if (!(debug_skip_ & 8)) {
       conv(l, CS_CONV_FWD, (int)B, t, s, true);
       const int64_t M = B * b.H * b.H;
       const int rows = cs_conv_stat_rows(9 * b.cin, t.bm, t.bk, t.splits);
@@ -432,7 +433,10 @@ void VggEngine::forward_train(int64_t B) {
                         P(b.be_off), bufs + b.rm_off, bufs + b.rv_off, nbt_.data_ptr<int64_t>() + l, kBnMomentum,
                         kBnEps, bn, bn + b.cout, bn + 2 * b.cout, bn + 3 * b.cout, s),
          "bn_finalize");
+    } else {
+      conv(l, CS_CONV_FWD, (int)B, t, s, true);
     }
+    if (!(debug_skip_ & 4))
     ok(cs_bn_apply(b.y.data_ptr<float>(), bn, bn + b.cout, out, (int)B, b.H, b.H, b.cout, b.pool, s), "bn_apply");
   }
   // classifier + loss: dfeat -> gbuf_[0]. Inside the overlapped step the per-column pass (dW, db,
@@ -469,7 +473,9 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
     const float* Gin = gbuf_[(L - 1 - l) % 2].data_ptr<float>();
     // ---- BN (+ReLU, +pool) backward of block l -> dz (the deferred side-stream signal of block
     // l+1's fork rides its first launch)
-    if (red_pending_ == l) {
+    if (debug_skip_ & 16) {
+      flush_signal(s);
+    } else if (red_pending_ == l) {
       // the partial sums (and, with fin, the finalize) ran inside block l+1's data-gradient launch
       if (fin_on_)
         ok(cs_bn_bwd_apply(b.y.data_ptr<float>(), Gin, (int)B, b.H, b.H, b.cout, b.pool, bn, bn + b.cout,
@@ -514,7 +520,8 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
         conv(l, CS_CONV_DGRAD, (int)B, b.tile[CS_CONV_DGRAD], s, false, nullptr, dz, &erv, nullptr, fp);
         pending_sig_ = dz_link_->defer();
         dz_link_->wait(side_);
-        conv(l, CS_CONV_WGRAD, (int)B, b.tile[CS_CONV_WGRAD], side_, false, ws_w_.data_ptr<float>(), dz);
+        if (!(debug_skip_ & 32))
+          conv(l, CS_CONV_WGRAD, (int)B, b.tile[CS_CONV_WGRAD], side_, false, ws_w_.data_ptr<float>(), dz);
         // block l's dgrad (the last reader of its weights) and BN backward ran before the fork
         if (bwd_sgd_) sgd_on(side_, blk_range_[l].first, blk_range_[l].second, false);
         wg_link_->signal(side_);
@@ -548,6 +555,12 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
     flush_signal(s);
     if (ovl) join_side(s);
   }
+}
+
+std::string VggEngine::link_error() const {
+  std::string e = dz_link_ ? dz_link_->error() : std::string();
+  if (e.empty() && wg_link_) e = wg_link_->error();
+  return e;
 }
 
 VggEngine::~VggEngine() {

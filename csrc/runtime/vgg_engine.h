@@ -100,6 +100,11 @@ class VggEngine {
   void set_sgd_tail(bool on) { sgd_tail_on_ = on; }
   // test-only ordering faults for the ProbeComm test's negative control (tests must see a
   // mismatch): bit 0 = step() skips the closing join, bit 1 = its all-reduces skip the fork
+  // measurement / negative-control switches (WRONG numbers when set; never in a product run):
+  // 1 skip the comm join, 2 no comm fork (ordering-test controls); ablation upper bounds of a
+  // fusion (what the step would save if a launch class were free): 4 forward bn_apply,
+  // 8 forward bn_finalize, 16 backward BN (finalize + apply), 32 side-stream weight-gradient GEMMs.
+  // CS_DEBUG_SKIP sets the mask at construction.
   void set_debug_skip(int64_t mask) { debug_skip_ = (int)mask; }
   // conv autotune candidates (CS_CONV_MATH): 0 f32, 1 x6, 2 f32 + x6 (default), 3 bf16 operands
   void set_math(int64_t m) {
@@ -130,6 +135,11 @@ class VggEngine {
   // record on the compute stream costs a few us of launch gap on this stack.
   void set_timing(bool on);
   std::vector<std::pair<std::string, double>> phase_times();
+
+  // error of the side-stream weight-gradient links (dz_link_ main -> side, wg_link_ side -> main):
+  // a wait that timed out or was released by abort_links() ran its consumer unordered, so the
+  // wgrad / SGD ordering of the steps since can no longer be trusted ("" when healthy)
+  std::string link_error() const;
 
   // conv tile control: mode 0 fwd / 1 dgrad / 2 wgrad
   void set_tile(int64_t block, int64_t mode, int64_t bm, int64_t bn, int64_t splits, int64_t bk = 16,

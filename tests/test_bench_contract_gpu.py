@@ -33,3 +33,36 @@ def test_bench_json_line():
     assert c["model"] == "VGG11" and c["global_batch"] == 64 and c["parallelism"] == "dp1" and c["seq_len"] is None
     assert d["value"] > 0 and abs(d["value"] - 64 * 1e3 / d["ms_per_step"]) / d["value"] < 1e-3
     assert d["vs_baseline"] == pytest.approx(d["value"] / 554.0, rel=1e-2)
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_bench_two_ranks_staged_json_line():
+    """The N > 1 branch of bench.py, exactly as the driver launches it (torch.distributed.run, one
+    process per rank), with the staged transport so both ranks fit on the 1-GPU box: process-group
+    init, the C++ data-parallel step (bucket all-reduces forked from the backward), the barrier +
+    sync bracket, max-over-ranks time, the busBW report after the window, and ONE JSON line."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
+           "--comm", "staged", "--steps", "5", "--warmup", "2", "--busbw-iters", "3"]
+    env = dict(os.environ, CS744_BENCH_CALIBRATE="0")
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["steps"] == 5 and d["warmup"] == 2
+    c = d["config"]
+    assert c["comm"] == "staged" and c["parallelism"] == "dp2" and c["global_batch"] == 128
+    assert c["sync"] == "ddp" and c["engine"] == "native"
+    assert d["value"] > 0 and abs(d["value"] - 128 * 1e3 / d["ms_per_step"]) / d["value"] < 1e-3
+    bw = d["busbw_GBps"]
+    assert bw and all(v > 0 for v in bw.values()), bw
+    assert "9.00MiB" in bw or any(k.endswith("MiB") for k in bw)

@@ -164,3 +164,35 @@ def test_cross_entropy_matches_torch(dev, dtype, R, V):
     (2.5 * ref).backward()
     tol = dict(rtol=1e-4, atol=1e-6) if dtype == torch.float32 else dict(rtol=1e-2, atol=1e-4)
     torch.testing.assert_close(x.grad.double(), xr.grad, **tol)
+
+
+@pytest.mark.parametrize("out_features", [32001, 50257, 390])
+def test_shadow_linear_odd_shapes_fall_back(dev, out_features):
+    """Shapes the native GEMM cannot read in place (an odd vocabulary: N % 4 != 0 / ld % 8 != 0;
+    an expanded stride-0 upstream gradient from y.sum().backward()) run through torch.mm instead
+    of raising in backward; the fp32 weight gradient matches the fp64 product."""
+    from cs744_pytorch_distributed_tutorial_amd.ops.lm import ShadowLinear, gemm_operands_ok
+    torch.manual_seed(0)
+    lin = ShadowLinear(264, out_features, bias=False).to(dev)
+    x = torch.randn(24, 264, device=dev)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = lin(x)
+    y.float().sum().backward()  # expanded (stride-0) upstream gradient
+    ref = torch.ones(24, out_features, dtype=torch.float64, device=dev).t() @ x.to(torch.bfloat16).double()
+    assert lin.weight.grad.dtype == torch.float32
+    torch.testing.assert_close(lin.weight.grad.double(), ref, rtol=2e-2, atol=2e-1)
+    g = torch.ones(1, 1, device=dev, dtype=torch.bfloat16).expand(24, out_features)
+    assert not gemm_operands_ok(g.t(), x.to(torch.bfloat16))
+
+
+def test_mm_bf16_empty_reduction_is_zero(dev):
+    """K = 0 (an empty token batch's weight gradient) returns zeros like torch.mm, not uninitialised
+    memory; an accumulator comes back unchanged."""
+    from cs744_pytorch_distributed_tutorial_amd.ops import native
+    a = torch.empty(64, 0, device=dev, dtype=torch.bfloat16)
+    b = torch.empty(0, 128, device=dev, dtype=torch.bfloat16)
+    for out_f32 in (False, True):
+        c = native.C().mm_bf16(a, b, out_f32)
+        assert c.shape == (64, 128) and bool((c == 0).all())
+    acc = torch.full((64, 128), 3.0, device=dev)
+    assert torch.equal(native.C().mm_bf16(a, b, True, acc), torch.full_like(acc, 3.0))

@@ -508,3 +508,30 @@ def test_long_run_no_syncs_deterministic(dev):
     for r in out[1:]:
         for a, b in zip(out[0], r):
             assert torch.equal(a, b)
+
+
+def test_side_stream_link_error_surfaces(dev):
+    """The side-stream weight-gradient links report a failed wait: healthy after overlapped steps;
+    after abort_links() the next step's waits release early (error 2) and check_comm() raises,
+    at world 1 with no communicator (the default bench configuration)."""
+    from cs744_pytorch_distributed_tutorial_amd.ops import native
+    t = _trainer(dev, batch_size=32, train_size=256)
+    t.engine.set_overlap(True)
+    for _ in range(3):
+        t.step()
+    torch.cuda.synchronize()
+    assert t.engine.link_error() == ""
+    t.check_comm()
+    try:
+        native.C().abort_links()
+        # a wait only checks the abort word while it is still waiting (every 256 polls): hold the
+        # main stream for ~tens of ms so the side stream's first wait of the step is still spinning
+        torch.cuda._sleep(100_000_000)
+        t.step()
+        torch.cuda.synchronize()
+        assert "aborted" in t.engine.link_error()
+        with pytest.raises(RuntimeError, match="side-stream weight-gradient link"):
+            t.check_comm()
+    finally:
+        native.C().reset_link_abort()
+        t.close()
