@@ -522,6 +522,86 @@ __global__ __launch_bounds__(256) void bn_fused_bwd_kernel(const float* __restri
     bwd_visit<true, POOL>(y, G, B, H, W, C, cqg, u, scale, shift, mean, invstd, coef_sh, dz, dummy, c0);
 }
 
+// grid (C/16, row chunks): finalize the BN backward of this block's 16 channels from the P
+// partials [P][C][3] (sum g, sum g*xhat, sum xhat) — thread (rl, cq) sums partials rl, rl + 64, ...
+// of its channel quad, then the fixed-order block reduce: identical in every block — block row 0
+// publishes the coefficients and the parameter gradients, and every block writes dZ for its chunk
+// of `upb` units. The first statistics-independent loads (the chunk's first unit of G and y) are
+// issued before the partial gather so their latency overlaps it.
+template <bool POOL>
+__global__ __launch_bounds__(256) void bn_bwd_tail_fused_kernel(const float* __restrict__ y, const float* __restrict__ G,
+                                                                int B, int H, int W, int C,
+                                                                const float* __restrict__ bnv,
+                                                                const float* __restrict__ gamma,
+                                                                const float* __restrict__ part, int P,
+                                                                float* __restrict__ coef, float* __restrict__ dgamma,
+                                                                float* __restrict__ dbeta, float* __restrict__ dbias,
+                                                                float* __restrict__ dz, int upb,
+                                                                unsigned long long* __restrict__ signal) {
+  __shared__ float lds[4 * 4 * 3 * 4];
+  __shared__ float coef_sh[3 * kFusedCh];
+  if (signal != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
+    __hip_atomic_fetch_add(signal, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int cq = threadIdx.x & 3, rl = threadIdx.x >> 2;
+  const int cqg = blockIdx.x * 4 + cq;
+  const bool lead = blockIdx.y == 0;
+  const float* invstd = bnv + 3 * C;
+  float k1q[4] = {0.f, 0.f, 0.f, 0.f};
+  if (threadIdx.x < 4)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) k1q[q] = gamma[4 * cqg + q] * invstd[4 * cqg + q];
+  float acc[3][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  // 4 partials in flight per lane before their adds (same ascending order per lane)
+  for (int p0 = rl; p0 < P; p0 += 4 * 64) {
+    float4 v[4][3];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int p = p0 + 64 * j;
+      const float* q = part + ((size_t)p * C + 4 * cqg) * 3;
+      v[j][0] = p < P ? *reinterpret_cast<const float4*>(q) : make_float4(0.f, 0.f, 0.f, 0.f);
+      v[j][1] = p < P ? *reinterpret_cast<const float4*>(q + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+      v[j][2] = p < P ? *reinterpret_cast<const float4*>(q + 8) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      // 12 floats = channels 4cqg..4cqg+3 x (g, g*xhat, xhat), channel-major
+      const float f[12] = {v[j][0].x, v[j][0].y, v[j][0].z, v[j][0].w, v[j][1].x, v[j][1].y,
+                           v[j][1].z, v[j][1].w, v[j][2].x, v[j][2].y, v[j][2].z, v[j][2].w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) acc[k][q] += f[3 * q + k];
+    }
+  }
+  sum_reduce_block(acc, lds);
+  const int c0 = blockIdx.x * kFusedCh;
+  if (threadIdx.x < 4) {
+    const float Mf = (float)(B * H * W);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int c = 4 * cqg + q;
+      const float k1 = k1q[q], k2 = acc[0][q] / Mf, k3 = acc[1][q] / Mf;
+      if (lead) {
+        if (dgamma) dgamma[c] = acc[1][q];
+        if (dbeta) dbeta[c] = acc[0][q];
+        if (dbias) dbias[c] = -k1 * k3 * acc[2][q];
+        coef[3 * c] = k1;
+        coef[3 * c + 1] = k2;
+        coef[3 * c + 2] = k3;
+      }
+      coef_sh[3 * (c - c0)] = k1;
+      coef_sh[3 * (c - c0) + 1] = k2;
+      coef_sh[3 * (c - c0) + 2] = k3;
+    }
+  }
+  __syncthreads();
+  const int units = POOL ? B * (H >> 1) * (W >> 1) : B * H * W;
+  const int u_end = min(units, (int)(blockIdx.y + 1) * upb);
+  float dummy[3][4];
+  for (int u = blockIdx.y * upb + rl; u < u_end; u += 64)
+    bwd_visit<true, POOL>(y, G, B, H, W, C, cqg, u, bnv, bnv + C, bnv + 2 * C, invstd, coef_sh, dz, dummy, c0);
+}
+
 }  // namespace
 
 int cs_bn_bwd_blocks(int B, int H, int W, int C, int pool) {
@@ -634,6 +714,25 @@ hipError_t cs_bn_fused_fwd(const float* part, int T, int R, int M, int C, const 
   chunks = (units + upb - 1) / upb;
   hipLaunchKernelGGL(bn_fused_fwd_kernel, dim3(cg, chunks), dim3(256), 0, stream, part, T, R, M, C, gamma, beta,
                      running_mean, running_var, nbt, momentum, eps, bnv, y, out, B, H, W, pool, upb);
+  return hipGetLastError();
+}
+
+hipError_t cs_bn_bwd_tail_fused(const float* y, const float* G, int B, int H, int W, int C, int pool, const float* bnv,
+                                const float* gamma, const float* part, int P, float* coef, float* dgamma, float* dbeta,
+                                float* dbias, float* dz, hipStream_t stream, unsigned long long* signal) {
+  if (C % kFusedCh != 0 || C > 1024 || (pool && ((H | W) & 1)) || P < 1) return hipErrorInvalidValue;
+  // row chunks of >= 64 units (one per row lane), ~512 blocks at most (as cs_bn_fused_fwd)
+  const int units = B * (pool ? H / 2 : H) * (pool ? W / 2 : W);
+  const int cg = C / kFusedCh;
+  int chunks = std::max(1, std::min((units + 63) / 64, std::max(1, 512 / cg)));
+  const int upb = (units + chunks - 1) / chunks;
+  chunks = (units + upb - 1) / upb;
+  if (pool)
+    hipLaunchKernelGGL((bn_bwd_tail_fused_kernel<true>), dim3(cg, chunks), dim3(256), 0, stream, y, G, B, H, W, C, bnv,
+                       gamma, part, P, coef, dgamma, dbeta, dbias, dz, upb, signal);
+  else
+    hipLaunchKernelGGL((bn_bwd_tail_fused_kernel<false>), dim3(cg, chunks), dim3(256), 0, stream, y, G, B, H, W, C,
+                       bnv, gamma, part, P, coef, dgamma, dbeta, dbias, dz, upb, signal);
   return hipGetLastError();
 }
 

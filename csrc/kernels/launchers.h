@@ -192,6 +192,14 @@ hipError_t cs_bn_fused_fwd(const float* part, int T, int R, int M, int C, const 
 hipError_t cs_bn_fused_bwd(const float* y, const float* G, int B, int H, int W, int C, int pool, const float* bnv,
                            const float* gamma, float* coef, float* dgamma, float* dbeta, float* dbias, float* dz,
                            hipStream_t stream, unsigned long long* signal = nullptr);
+// finalize + apply of the BN backward in ONE launch when the reduce already ran (the data-gradient
+// epilogue's P row-tile partials [P][C][3], CsConvArgs::ered): grid (C/16, row chunks), every block
+// finalizes its 16 channels from the P partials (the same fixed-order sum in every block), block row
+// 0 publishes coef / dgamma / dbeta / dbias, each block applies dZ to its chunk of rows — the
+// backward twin of cs_bn_fused_fwd (one launch boundary fewer than cs_bn_bwd_tail)
+hipError_t cs_bn_bwd_tail_fused(const float* y, const float* G, int B, int H, int W, int C, int pool, const float* bnv,
+                                const float* gamma, const float* part, int P, float* coef, float* dgamma, float* dbeta,
+                                float* dbias, float* dz, hipStream_t stream, unsigned long long* signal = nullptr);
 // the BN backward's apply pass alone (dZ from G, y and the finalized coef [C][3]): the finalize
 // ran as the last-arriver tail of the data-gradient launch that produced G (CsConvArgs::fin)
 hipError_t cs_bn_bwd_apply(const float* y, const float* G, int B, int H, int W, int C, int pool, const float* scale,

@@ -200,6 +200,8 @@ VggEngine::VggEngine(int64_t Bmax, std::vector<int64_t> desc, std::vector<int64_
   if (const char* e = getenv("CS_BN_FUSED_ROWS")) bn_fused_rows_ = atoll(e);
   if (const char* e = getenv("CS_CONV_MATH")) math_ = atoi(e);
   if (const char* e = getenv("CS_DEBUG_SKIP")) debug_skip_ = atoi(e);
+  if (const char* e = getenv("CS_BN_FWD_FUSED_T")) fwd_fused_t_ = atoi(e);
+  if (const char* e = getenv("CS_BN_BWD_FUSED_P")) bwd_fused_p_ = atoi(e);
   bn_part_ = torch::zeros({partmax}, fo);
   bn_coef_ = torch::zeros({cmax * 3}, fo);
   bn_eval_ = torch::zeros({2, cmax}, fo);
@@ -429,7 +431,17 @@ void VggEngine::forward_train(int64_t B) {
       conv(l, CS_CONV_FWD, (int)B, t, s, true);
       const int64_t M = B * b.H * b.H;
       const int rows = cs_conv_stat_rows(9 * b.cin, t.bm, t.bk, t.splits);
-      ok(cs_bn_finalize(b.stats.data_ptr<float>(), (int)cdiv(M, rows), rows, (int)M, b.cout, P(b.g_off),
+      const int T = (int)cdiv(M, rows);
+      if (T <= fwd_fused_t_ && b.cout % 16 == 0) {
+        // finalize + normalize/ReLU(/pool) in one launch: each block re-combines its 16 channels'
+        // T tile partials (the same fixed order in every block) instead of waiting on a finalize
+        ok(cs_bn_fused_fwd(b.stats.data_ptr<float>(), T, rows, (int)M, b.cout, P(b.g_off), P(b.be_off),
+                           bufs + b.rm_off, bufs + b.rv_off, nbt_.data_ptr<int64_t>() + l, kBnMomentum, kBnEps, bn,
+                           b.y.data_ptr<float>(), out, (int)B, b.H, b.H, b.pool, s),
+           "bn_fused_fwd");
+        continue;
+      }
+      ok(cs_bn_finalize(b.stats.data_ptr<float>(), T, rows, (int)M, b.cout, P(b.g_off),
                         P(b.be_off), bufs + b.rm_off, bufs + b.rv_off, nbt_.data_ptr<int64_t>() + l, kBnMomentum,
                         kBnEps, bn, bn + b.cout, bn + 2 * b.cout, bn + 3 * b.cout, s),
          "bn_finalize");
@@ -481,6 +493,12 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
         ok(cs_bn_bwd_apply(b.y.data_ptr<float>(), Gin, (int)B, b.H, b.H, b.cout, b.pool, bn, bn + b.cout,
                            bn + 2 * b.cout, bn + 3 * b.cout, bn_coef_.data_ptr<float>(), dz, s, pending_sig_),
            "bn_bwd_apply");
+      else if (red_P_ <= bwd_fused_p_ && b.cout % 16 == 0)
+        // finalize + apply in one launch (cs_bn_fused_fwd's backward twin)
+        ok(cs_bn_bwd_tail_fused(b.y.data_ptr<float>(), Gin, (int)B, b.H, b.H, b.cout, b.pool, bn, P(b.g_off),
+                                bn_part_.data_ptr<float>(), red_P_, bn_coef_.data_ptr<float>(), G(b.g_off),
+                                G(b.be_off), G(b.b_off), dz, s, pending_sig_),
+           "bn_bwd_tail_fused");
       else
         ok(cs_bn_bwd_tail(b.y.data_ptr<float>(), Gin, (int)B, b.H, b.H, b.cout, b.pool, bn, bn + b.cout,
                           bn + 2 * b.cout, bn + 3 * b.cout, P(b.g_off), bn_part_.data_ptr<float>(), red_P_,

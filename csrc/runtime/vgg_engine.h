@@ -106,6 +106,13 @@ class VggEngine {
   // 8 forward bn_finalize, 16 backward BN (finalize + apply), 32 side-stream weight-gradient GEMMs.
   // CS_DEBUG_SKIP sets the mask at construction.
   void set_debug_skip(int64_t mask) { debug_skip_ = (int)mask; }
+  // single-launch BatchNorm (finalize folded into the apply pass, every block re-combining its 16
+  // channels' partials): forward for layers with <= fwd_t statistics partials, backward for <= bwd_p
+  // (0 = the separate finalize launch). CS_BN_FWD_FUSED_T / CS_BN_BWD_FUSED_P override.
+  void set_bn_fused_limits(int64_t fwd_t, int64_t bwd_p) {
+    fwd_fused_t_ = (int)fwd_t;
+    bwd_fused_p_ = (int)bwd_p;
+  }
   // conv autotune candidates (CS_CONV_MATH): 0 f32, 1 x6, 2 f32 + x6 (default), 3 bf16 operands
   void set_math(int64_t m) {
     TORCH_CHECK(m >= 0 && m <= 3, "set_math: 0..3");
@@ -210,6 +217,7 @@ class VggEngine {
   bool sgd_tail_ = false;  // set by step() for the step in flight (world 1)
   bool sgd_first_ = false;
   int debug_skip_ = 0;
+  int fwd_fused_t_ = 0, bwd_fused_p_ = 0;
   double hp_[4] = {0, 0, 0, 0};  // lr, momentum, wd, dampening of the step in flight
   std::vector<std::pair<int64_t, int64_t>> blk_range_;  // block l's [off, off + n) (block L-1 from 0: fc)
   CsSgdTail sgd_tail_args(int64_t block);

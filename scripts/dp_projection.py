@@ -11,6 +11,12 @@ while a collective runs are priced with --ctas: the modelled collective then run
 workgroups (dependent FMA chains) instead of one sleeping wave. Not modelled: rank skew, and the
 memory traffic of the real copy-reduce.
 
+CTA budget (--cta-gbps B > 0): RCCL runs a ring collective as one CTA per channel, and a channel's
+throughput is bounded by its CTA's copy-reduce rate as well as by the link, so the bus bandwidth a
+collective gets with c CTAs is modelled as min(G, c * B) — the CTA count prices both sides: fewer
+CTAs leave more CUs to the backward GEMMs but slow the all-reduce. B is an ASSUMPTION (default
+10 GB/s per CTA, i.e. 16 CTAs ~ 160 GB/s), not a measurement on an 8-GPU node.
+
 Usage (GPU box): python scripts/dp_projection.py [--steps 50] [--gbps 100,150,300] [--worlds 2,4,8]
 """
 import argparse
@@ -56,6 +62,8 @@ def main():
     p.add_argument("--latency-us", type=float, default=25.0)
     p.add_argument("--ctas", type=str, default="0,8,16,32",
                    help="busy workgroups standing in for RCCL's CTAs during each collective (0: one sleeping wave)")
+    p.add_argument("--cta-gbps", type=float, default=0.0,
+                   help="> 0: per-CTA channel bandwidth (GB/s); busBW = min(G, ctas * this) (a model)")
     a = p.parse_args()
     torch.cuda.set_device(0)
     from cs744_pytorch_distributed_tutorial_amd.ops import native
@@ -67,9 +75,11 @@ def main():
     for g in [float(x) for x in a.gbps.split(",")]:
         for w in [int(x) for x in a.worlds.split(",")]:
             for c in [int(x) for x in a.ctas.split(",")]:
-                ms, ph, _ = run(f"xgmi:{g}:{w}:{a.latency_us}:{c}", a.steps, a.warmup)
-                print(json.dumps({"config": f"projected N={w}, ring busBW {g:g} GB/s, {a.latency_us:g} us/collective, "
-                                            f"{c} busy CTAs per collective",
+                ge = min(g, c * a.cta_gbps) if a.cta_gbps > 0 and c > 0 else g
+                ms, ph, _ = run(f"xgmi:{ge}:{w}:{a.latency_us}:{c}", a.steps, a.warmup)
+                print(json.dumps({"config": f"projected N={w}, ring busBW {ge:g} GB/s (link {g:g}), "
+                                            f"{a.latency_us:g} us/collective, {c} busy CTAs per collective",
+                                  "model": "busBW=min(link, ctas*cta_gbps)" if a.cta_gbps > 0 else "busBW=link",
                                   "ms_per_step": round(ms, 4), "projected_img_s": round(w * 64 / ms * 1e3),
                                   "per_gpu_img_s": round(64 / ms * 1e3), "efficiency_vs_world1": round(base / ms, 4),
                                   "allreduce_wait_ms": round(ph.get("allreduce_wait", 0.0), 4)}), flush=True)

@@ -439,18 +439,21 @@ def _force_x6s(tr):
     return n
 
 
-@pytest.mark.parametrize("variant", ["autotuned", "x6s_everywhere", "f32_only", "split", "nosplit", "dual", "in_launch"])
+@pytest.mark.parametrize("variant", ["autotuned", "x6s_everywhere", "f32_only", "split", "nosplit", "dual", "in_launch",
+                                     "bn_fused"])
 def test_bench_config_b64_matches_fp64(dev, variant):
     """The benchmarked configuration (B=64; tuned tiles = 22 of 23 GEMMs on X6S split-bf16
     maths), every X6S GEMM, f32-MFMA-only tiles, the tile tables that put split-K combines,
     64x128 / 128x64 epilogues and dual launches at every site, and the opt-in in-launch BN finalize
     (CS_BN_FIN=1, bn_fin.h) vs the decision-aligned fp64 model: every gradient tensor within 1e-4
     relative (max-abs normalised)."""
-    tr = _trainer(dev, batch_size=64, train_size=1024, autotune=variant in ("autotuned", "in_launch"))
+    tr = _trainer(dev, batch_size=64, train_size=1024, autotune=variant in ("autotuned", "in_launch", "bn_fused"))
     if variant in ("split", "nosplit", "dual"):
         _set_tiles(tr, variant)
     if variant == "in_launch":
         tr.engine.set_fin(True)
+    if variant == "bn_fused":  # single-launch BN at every layer, forward and backward
+        tr.engine.set_bn_fused_limits(1 << 30, 1 << 30)
     if variant == "x6s_everywhere":
         assert _force_x6s(tr) == 22
         assert sum(t["math"] == "x6s" for t in tr.tile_table()) == 22
