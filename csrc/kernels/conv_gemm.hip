@@ -741,6 +741,8 @@ __global__ __launch_bounds__(256 * KG) void conv_gemm_kernel(CsConvArgs a) {
   // dispatched them), then sgd.P blocks of an independent SGD update that run in the GEMM's tail
   const int nsplit = (a.total_ksteps + a.ksteps_per_split - 1) / a.ksteps_per_split;
   const int ng = ntiles * nsplit, lin = blockIdx.x;
+  if (a.start_sig != nullptr && lin == 0 && threadIdx.x == 0)
+    __hip_atomic_fetch_add(a.start_sig, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (lin >= ng) {
     cs_sgd::tail_body(a.sgd, lin - ng, a.sgd.P);
     return;

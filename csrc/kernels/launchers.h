@@ -110,6 +110,10 @@ struct CsConvArgs {
   // FWD (with stats) / DGRAD (with ered): the BN finalize by the launch's last-arriving block
   // (or the split-K combine's); fin.cnt == null: off
   CsBnFin fin;
+  // a deferred stream-link signal (device_comm.h StreamLink::defer) the launch's block 0 bumps when
+  // it starts — every kernel before it on its stream has completed (the engine's staggered fork:
+  // block l+1's side-stream weight gradient waits for block l's data gradient to be resident)
+  unsigned long long* start_sig;
   // filled by the launcher:
   int lgH, lgW, lgCin, lgCout, M, N, K, ksteps_per_split, total_ksteps;
 };

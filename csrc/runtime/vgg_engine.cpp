@@ -201,6 +201,7 @@ VggEngine::VggEngine(int64_t Bmax, std::vector<int64_t> desc, std::vector<int64_
   if (const char* e = getenv("CS_CONV_MATH")) math_ = atoi(e);
   if (const char* e = getenv("CS_DEBUG_SKIP")) debug_skip_ = atoi(e);
   if (const char* e = getenv("CS_BN_FWD_FUSED_T")) fwd_fused_t_ = atoi(e);
+  if (const char* e = getenv("CS_WGRAD_STAGGER")) stagger_ = atoi(e) != 0;
   if (const char* e = getenv("CS_BN_BWD_FUSED_P")) bwd_fused_p_ = atoi(e);
   bn_part_ = torch::zeros({partmax}, fo);
   bn_coef_ = torch::zeros({cmax * 3}, fo);
@@ -279,6 +280,8 @@ void VggEngine::conv(int l, int mode, int B, const ConvTile& t, hipStream_t s, b
   }
   if (sgd != nullptr) a.sgd = *sgd;
   if (fin != nullptr) a.fin = *fin;
+  a.start_sig = start_sig_;  // the staggered fork's deferred signal rides this launch (once)
+  start_sig_ = nullptr;
   const Dims d = dims(b, mode, B);
   const int sp = eff_splits(d.K, t.splits, t.bk);
   TORCH_CHECK(sp == 1 || (int64_t)sp * d.M * d.N <= ws_elems_, "VggEngine: split-K workspace too small");
@@ -534,19 +537,26 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
       if (l > 0) {
         // the data gradient keeps the whole chip on the critical chain; the weight gradient forks
         // to the side stream after it and fills the chip while the main stream runs the
-        // latency-bound BN kernels (and the split-K combine) of the block below
+        // latency-bound BN kernels (and the split-K combine) of the block below.
+        // Staggered (stagger_): block l+1's weight gradient, held back one block, forks when THIS
+        // data gradient starts (its launch carries the signal), so the data gradient's blocks take
+        // the CUs first and the side GEMM fills its tail and the BN gaps after it, instead of
+        // holding LDS that keeps data-gradient blocks off their CUs
+        if (side_pending_ >= 0) start_sig_ = dz_link_->defer();
         conv(l, CS_CONV_DGRAD, (int)B, b.tile[CS_CONV_DGRAD], s, false, nullptr, dz, &erv, nullptr, fp);
-        pending_sig_ = dz_link_->defer();
-        dz_link_->wait(side_);
-        if (!(debug_skip_ & 32))
-          conv(l, CS_CONV_WGRAD, (int)B, b.tile[CS_CONV_WGRAD], side_, false, ws_w_.data_ptr<float>(), dz);
-        // block l's dgrad (the last reader of its weights) and BN backward ran before the fork
-        if (bwd_sgd_) sgd_on(side_, blk_range_[l].first, blk_range_[l].second, false);
-        wg_link_->signal(side_);
+        if (side_pending_ >= 0) fork_wgrad(side_pending_, B, false);
+        if (stagger_) {
+          side_pending_ = l;
+        } else {
+          pending_sig_ = dz_link_->defer();
+          fork_wgrad(l, B, true);
+        }
       } else {
         // block 0's weight gradient is the step's last GEMM: nothing left to overlap it with, so it
         // runs here (the main split-K workspace is free: no data gradient for block 0)
+        if (side_pending_ >= 0) start_sig_ = dz_link_->defer();
         conv(l, CS_CONV_WGRAD, (int)B, b.tile[CS_CONV_WGRAD], s, false, ws_.data_ptr<float>(), dz);
+        if (side_pending_ >= 0) fork_wgrad(side_pending_, B, false);
         if (bwd_sgd_) sgd_on(s, blk_range_[0].first, blk_range_[0].second, true);
       }
     } else if (dual_ok(l)) {  // wgrad + dgrad in one launch (no appended SGD blocks: the update runs first)
@@ -569,10 +579,32 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
       red_P_ = erv.P;
     }
   }
+  // a weight gradient still held back at the end of this range (a bucket boundary): fork it now,
+  // behind the next main-stream launch as the unstaggered fork does, so the bucket's all-reduce
+  // (forked from the side stream next) covers it
+  if (side_pending_ >= 0) {
+    flush_signal(s);
+    pending_sig_ = dz_link_->defer();
+    fork_wgrad(side_pending_, B, false);
+  }
   if (join) {
     flush_signal(s);
     if (ovl) join_side(s);
   }
+}
+
+void VggEngine::fork_wgrad(int l, int64_t B, bool current) {
+  // the side stream waits for the deferred signal just issued (it rides a main-stream launch), then
+  // block l's weight gradient into its own dz buffer's consumer, its SGD, and the join signal
+  VggBlock& b = blocks_[l];
+  float* dz = dz_blk_[l].data_ptr<float>();
+  dz_link_->wait(side_);
+  if (!(debug_skip_ & 32))
+    conv(l, CS_CONV_WGRAD, (int)B, b.tile[CS_CONV_WGRAD], side_, false, ws_w_.data_ptr<float>(), dz);
+  // block l's dgrad (the last reader of its weights) ran before the fork
+  if (bwd_sgd_) sgd_on(side_, blk_range_[l].first, blk_range_[l].second, false);
+  wg_link_->signal(side_);
+  if (!current) side_pending_ = -1;
 }
 
 std::string VggEngine::link_error() const {

@@ -106,6 +106,7 @@ class VggEngine {
   // 8 forward bn_finalize, 16 backward BN (finalize + apply), 32 side-stream weight-gradient GEMMs.
   // CS_DEBUG_SKIP sets the mask at construction.
   void set_debug_skip(int64_t mask) { debug_skip_ = (int)mask; }
+  void set_stagger(bool on) { stagger_ = on; }
   // single-launch BatchNorm (finalize folded into the apply pass, every block re-combining its 16
   // channels' partials): forward for layers with <= fwd_t statistics partials, backward for <= bwd_p
   // (0 = the separate finalize launch). CS_BN_FWD_FUSED_T / CS_BN_BWD_FUSED_P override.
@@ -217,6 +218,12 @@ class VggEngine {
   bool sgd_tail_ = false;  // set by step() for the step in flight (world 1)
   bool sgd_first_ = false;
   int debug_skip_ = 0;
+  // staggered side-stream fork (backward): block l's weight gradient forks when block l-1's data
+  // gradient starts instead of right after its own data gradient (CS_WGRAD_STAGGER)
+  bool stagger_ = false;
+  int side_pending_ = -1;                      // block whose weight-gradient fork is held back
+  unsigned long long* start_sig_ = nullptr;    // deferred signal the next conv launch carries
+  void fork_wgrad(int l, int64_t B, bool current);
   int fwd_fused_t_ = 0, bwd_fused_p_ = 0;
   double hp_[4] = {0, 0, 0, 0};  // lr, momentum, wd, dampening of the step in flight
   std::vector<std::pair<int64_t, int64_t>> blk_range_;  // block l's [off, off + n) (block L-1 from 0: fc)

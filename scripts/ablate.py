@@ -90,14 +90,19 @@ def main() -> int:
     def apply_tiles(name):
         for t in shipped:  # [block, mode, bm, bn, splits, bk, stage] -> set_tile(block, mode, bm, bn, splits, bk, stage)
             tr.engine.set_tile(t[0], t[1], t[2], t[3], t[4], t[5], t[6])
-        if name:
+        if name.startswith("file="):  # a step_tune.py output (tiles [[block, mode, bm, bn, splits, bk, stage]])
+            with open(name[5:]) as f:
+                for t in json.load(f)["tiles"]:
+                    tr.engine.set_tile(*t[:7])
+        elif name:
             TILESETS[name](tr)
     variants = []
     for v in args.variants:
-        # name:mask:serial:tiles:FWD_T/BWD_P:fin
-        f = v.split(":") + ["", "", "", "", ""]
+        # name:mask:serial:tiles:FWD_T/BWD_P:fin:stagger
+        f = v.split(":") + ["", "", "", "", "", ""]
         fl = tuple(int(x) for x in f[4].split("/")) if f[4] else (0, 0)
-        variants.append((f[0], int(f[1]) if f[1] else 0, f[2] == "serial", f[3], fl, f[5] == "fin"))
+        variants.append((f[0], int(f[1]) if f[1] else 0, f[2] == "serial", f[3], fl, f[5] == "fin",
+                         f[6] == "stagger"))
     import gc
     gc.collect()
     gc.disable()
@@ -112,13 +117,14 @@ def main() -> int:
     times = {v[0]: [] for v in variants}
     losses = {v[0]: [] for v in variants}
     for _ in range(args.rounds):
-        for name, mask, serial, tiles, fl, fin in variants:
+        for name, mask, serial, tiles, fl, fin, stag in variants:
             for dst, src in zip((tr.params, tr.mom, tr.bufs, tr.nbt), snap):
                 dst.copy_(src)
             tr.engine.cursor().copy_(cursor)
             apply_tiles(tiles)
             tr.engine.set_bn_fused_limits(*fl)
             tr.engine.set_fin(fin)
+            tr.engine.set_stagger(stag)
             tr.engine.set_debug_skip(mask)
             tr.engine.set_overlap(base_overlap and not serial)
             for _ in range(args.warmup):
@@ -133,10 +139,10 @@ def main() -> int:
     tr.engine.set_debug_skip(0)
     tr.engine.set_overlap(base_overlap)
     base = statistics.median(times[variants[0][0]])
-    for name, mask, serial, tiles, fl, fin in variants:
+    for name, mask, serial, tiles, fl, fin, stag in variants:
         med = statistics.median(times[name])
         print(json.dumps({"variant": name, "mask": mask, "serial": serial, "tiles": tiles or "shipped",
-                          "bn_fused_limits": list(fl), "fin": fin, "ms_median": round(med, 4),
+                          "bn_fused_limits": list(fl), "fin": fin, "stagger": stag, "ms_median": round(med, 4),
                           "ms_min": round(min(times[name]), 4), "img_s_median": round(args.batch_size * 1e3 / med, 1),
                           "delta_vs_first_pct": round(100.0 * (med - base) / base, 2),
                           "ms_all": [round(t, 4) for t in times[name]],

@@ -89,6 +89,12 @@ def main() -> int:
     p.add_argument("--passes", type=int, default=1)
     p.add_argument("--budget-s", type=float, default=900.0)
     p.add_argument("--out", default=None)
+    p.add_argument("--start", default="shipped",
+                   help="shipped | coresident (every GEMM at its fastest-alone tile within --co-lds-main / "
+                        "--co-lds-side KiB, so a main-stream and a side-stream block fit one CU together) | "
+                        "file:PATH (a previous step_tune.py output)")
+    p.add_argument("--co-lds-main", type=float, default=80.0)
+    p.add_argument("--co-lds-side", type=float, default=75.0)
     args = p.parse_args()
     t_start = time.time()
     from cs744_pytorch_distributed_tutorial_amd.ops import native
@@ -132,6 +138,10 @@ def main() -> int:
     for _ in range(20):
         tr.step()
     torch.cuda.synchronize()
+    if args.start.startswith("file:"):
+        with open(args.start[5:]) as f:
+            for t in json.load(f)["tiles"]:
+                cur[(t[0], t[1])] = list(t[2:7])
     # ---- phase 1: isolated timings
     short = {}
     iso_cur = {}
@@ -142,10 +152,15 @@ def main() -> int:
                 res.append((alone(g, t), t))
             except RuntimeError:
                 continue
+        res.sort(key=lambda x: x[0])
+        if args.start == "coresident":
+            cap = args.co_lds_side if g[1] == 2 else args.co_lds_main
+            fit = [t for _, t in res if _lds_kib(t[0], t[1], t[3], t[4], g[1]) <= cap]
+            if fit and not (g[0] == 0 and g[1] == 0):
+                cur[g] = list(fit[0])
         set_t(g, cur[g])
         iso_cur[g] = alone(g, cur[g])
         set_t(g, cur[g])
-        res.sort(key=lambda x: x[0])
         keep = [t for _, t in res[:args.keep]]
         small = [t for us, t in res if _lds_kib(t[0], t[1], t[3], t[4], g[1]) <= args.small_lds][:args.keep_small]
         short[g] = [list(t) for t in dict.fromkeys(tuple(t) for t in keep + small) if list(t) != cur[g]]

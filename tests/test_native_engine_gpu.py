@@ -481,9 +481,11 @@ def test_side_stream_wgrad_bitwise_and_graph(dev):
     each weight gradient) compute exactly what the serial backward does (SGD in the weight-gradient
     tails); a full-step graph (captured: serial) replays the same bits."""
     runs = []
-    for ovl, graph in ((False, "none"), (True, "none"), (True, "full")):
+    for ovl, graph, stagger in ((False, "none", False), (True, "none", False), (True, "full", False),
+                                (True, "none", True)):
         t = _trainer(dev, batch_size=32, train_size=256, graph=graph)
         t.engine.set_overlap(ovl)
+        t.engine.set_stagger(stagger)  # block l's weight gradient forks at block l-1's data gradient
         for _ in range(5):
             t.step()
         torch.cuda.synchronize()
@@ -500,9 +502,10 @@ def test_long_run_no_syncs_deterministic(dev):
     weight gradients == the serial backward, bit for bit, run to run (the in-launch finalizes'
     arrival order changes, their combine order does not; the tickets stay zeroed)."""
     out = []
-    for ovl in (False, True, True):
+    for ovl, stagger in ((False, False), (True, False), (True, False), (True, True)):
         t = _trainer(dev, batch_size=32, train_size=640)
         t.engine.set_overlap(ovl)
+        t.engine.set_stagger(stagger)
         for _ in range(30):
             t.step()
         torch.cuda.synchronize()
