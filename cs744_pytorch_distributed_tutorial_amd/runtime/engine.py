@@ -648,14 +648,23 @@ class NativeTrainer:
             out.update(reduce_eval(self.comm, float(loss_sum.item()), out["correct"], total, nb, self.device))
         return out
 
+    def _join_lag(self) -> None:
+        """The current stream waits for weight gradients / SGD the engine deferred into the next
+        step (CS_WGRAD_LAG): every host read of the parameters goes through here."""
+        if self.engine is not None:
+            self.engine.join_lag()
+
     def state_dict(self) -> Dict[str, torch.Tensor]:
+        self._join_lag()
         return self.layout.unpack(self.params, self.bufs, self.nbt)
 
     def load_state_dict(self, sd: Dict[str, torch.Tensor]) -> None:
+        self._join_lag()
         self.layout.pack(sd, self.params, self.bufs, self.nbt)
 
     def optimizer_state_dict(self) -> dict:
         """torch.optim.SGD ``state_dict`` format (momentum_buffer per parameter index)."""
+        self._join_lag()
         state = {i: {"momentum_buffer": self.layout.view(self.mom, n).detach().cpu().contiguous()}
                  for i, n in enumerate(self.layout.param_names)} if self._mom_valid else {}
         group = {"lr": self.lr, "momentum": self.momentum, "dampening": self.damp, "weight_decay": self.wd,
@@ -664,6 +673,7 @@ class NativeTrainer:
         return {"state": state, "param_groups": [group]}
 
     def load_optimizer_state_dict(self, sd: dict) -> None:
+        self._join_lag()
         with torch.no_grad():
             self.mom.zero_()
             for i, n in enumerate(self.layout.param_names):
@@ -677,6 +687,7 @@ class NativeTrainer:
     def close(self) -> None:
         """Release graphs, the engine and the native communicator deterministically (before the
         process group is torn down), instead of leaving ncclCommDestroy to interpreter exit."""
+        self._join_lag()
         torch.cuda.synchronize()
         self._graphs = None
         self.engine = None
@@ -693,6 +704,7 @@ class NativeTrainer:
         gc.collect()
 
     def grads_state(self) -> Dict[str, torch.Tensor]:
+        self._join_lag()
         return self.layout.unpack_grads(self.grads)
 
     @classmethod

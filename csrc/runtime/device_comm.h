@@ -62,6 +62,10 @@ hipStream_t reserved_comm_stream();
 // the engine's side stream (weight gradients + their SGD, VggEngine overlap), lowest priority,
 // reserved the same way
 hipStream_t reserved_side_stream();
+// the engine's lag stream (world 1: the top blocks' weight gradients deferred into the next
+// step's forward), lowest priority, bound on first use — NOT by reserve_streams(), so a run that
+// never defers (every world > 1 run) does not spend a hardware queue on it
+hipStream_t reserved_lag_stream();
 void reserve_streams();
 // Start-up self-check of the queue assumption the stream links rely on: true when `a` and `b`
 // run on ONE hardware queue. A link wait with a short timeout is enqueued on `b` ahead of its

@@ -108,6 +108,11 @@ hipStream_t reserved_side_stream() {
   return side;
 }
 
+hipStream_t reserved_lag_stream() {
+  static hipStream_t lag = bound_stream(false);
+  return lag;
+}
+
 void reserve_streams() {
   (void)reserved_side_stream();
   (void)reserved_comm_stream();

@@ -202,6 +202,7 @@ VggEngine::VggEngine(int64_t Bmax, std::vector<int64_t> desc, std::vector<int64_
   if (const char* e = getenv("CS_DEBUG_SKIP")) debug_skip_ = atoi(e);
   if (const char* e = getenv("CS_BN_FWD_FUSED_T")) fwd_fused_t_ = atoi(e);
   if (const char* e = getenv("CS_WGRAD_STAGGER")) stagger_ = atoi(e) != 0;
+  if (const char* e = getenv("CS_WGRAD_LAG")) lag_blocks_ = atoi(e);
   if (const char* e = getenv("CS_BN_BWD_FUSED_P")) bwd_fused_p_ = atoi(e);
   bn_part_ = torch::zeros({partmax}, fo);
   bn_coef_ = torch::zeros({cmax * 3}, fo);
@@ -436,6 +437,10 @@ void VggEngine::forward_train(int64_t B) {
       const int rows = cs_conv_stat_rows(9 * b.cin, t.bm, t.bk, t.splits);
       const int T = (int)cdiv(M, rows);
       if (T <= fwd_fused_t_ && b.cout % 16 == 0) {
+        if (lag_pending_ && l + 1 >= L - lag_blocks_) {
+          lag_out_->wait(s);
+          lag_pending_ = false;
+        }
         // finalize + normalize/ReLU(/pool) in one launch: each block re-combines its 16 channels'
         // T tile partials (the same fixed order in every block) instead of waiting on a finalize
         ok(cs_bn_fused_fwd(b.stats.data_ptr<float>(), T, rows, (int)M, b.cout, P(b.g_off), P(b.be_off),
@@ -450,6 +455,12 @@ void VggEngine::forward_train(int64_t B) {
          "bn_finalize");
     } else {
       conv(l, CS_CONV_FWD, (int)B, t, s, true);
+    }
+    if (lag_pending_ && l + 1 >= L - lag_blocks_) {
+      // the deferred weight gradients read this block's output activation (the next block's input)
+      // and the lagged blocks' parameters: wait for them before overwriting / reading either
+      lag_out_->wait(s);
+      lag_pending_ = false;
     }
     if (!(debug_skip_ & 4))
     ok(cs_bn_apply(b.y.data_ptr<float>(), bn, bn + b.cout, out, (int)B, b.H, b.H, b.cout, b.pool, s), "bn_apply");
@@ -545,7 +556,9 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
         if (side_pending_ >= 0) start_sig_ = dz_link_->defer();
         conv(l, CS_CONV_DGRAD, (int)B, b.tile[CS_CONV_DGRAD], s, false, nullptr, dz, &erv, nullptr, fp);
         if (side_pending_ >= 0) fork_wgrad(side_pending_, B, false);
-        if (stagger_) {
+        if (lag_on(s) && l >= L - lag_blocks_) {
+          lag_list_.push_back(l);  // weight gradient + SGD deferred to the lag stream (step end)
+        } else if (stagger_) {
           side_pending_ = l;
         } else {
           pending_sig_ = dz_link_->defer();
@@ -591,6 +604,17 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
     flush_signal(s);
     if (ovl) join_side(s);
   }
+}
+
+bool VggEngine::lag_on(hipStream_t s) const {
+  const int L = (int)blocks_.size();
+  return lag_blocks_ > 0 && lag_blocks_ <= L - 2 && in_step_ && bwd_sgd_ && side_ok(s) && lag_ != nullptr;
+}
+
+void VggEngine::join_lag() {
+  if (!lag_pending_) return;
+  lag_out_->wait(cur_stream());
+  lag_pending_ = false;
 }
 
 void VggEngine::fork_wgrad(int l, int64_t B, bool current) {
@@ -689,6 +713,7 @@ std::vector<std::pair<std::string, double>> VggEngine::phase_times() {
 void VggEngine::forward_eval(int64_t B) {
   TORCH_CHECK(B > 0 && B <= Bmax_, "forward_eval: 0 < B <= Bmax");
   TORCH_CHECK(data_[1].defined(), "forward_eval: set_data(1, ...) first");
+  join_lag();
   hipStream_t s = cur_stream();
   const int L = (int)blocks_.size();
   ok(cs_gather_labels(labels_[1].data_ptr<int64_t>(), idx_.data_ptr<int64_t>(), ylab_.data_ptr<int64_t>(), (int)B, s),
@@ -767,6 +792,11 @@ void VggEngine::step_impl(int64_t B, DeviceComm* comm, const std::vector<int64_t
   // weight-gradient launch
   const bool ovl = side_ok(s);
   bwd_sgd_ = ovl && !dp && !blk_range_.empty();
+  if (bwd_sgd_ && lag_blocks_ > 0 && lag_ == nullptr) {
+    lag_ = reserved_lag_stream();
+    lag_in_ = std::make_unique<StreamLink>();
+    lag_out_ = std::make_unique<StreamLink>();
+  }
   sgd_tail_ = !ovl && sgd_tail_on_ && !dp && !blk_range_.empty();
   int64_t hi = L - 1;
   for (size_t k = 0; k < nb; ++k) {
@@ -815,6 +845,24 @@ void VggEngine::step_impl(int64_t B, DeviceComm* comm, const std::vector<int64_t
     flush_signal(s);
     if (ovl) join_side(s);
     if (dp && !(debug_skip_ & 1)) comm->join(s);
+  }
+  if (!lag_list_.empty()) {
+    // deferred weight gradients: the lag stream starts once the step's main stream (joined with
+    // the side stream: the head's column pass wrote the fc gradient the top block's SGD reads) is
+    // done — an explicit signal kernel, so nothing waits on a launch that may never come
+    Range r("cs.lag.fork");
+    flush_signal(s);
+    lag_in_->signal(s);
+    lag_in_->wait(lag_);
+    for (int l : lag_list_) {
+      if (!(debug_skip_ & 32))
+        conv(l, CS_CONV_WGRAD, (int)B, blocks_[l].tile[CS_CONV_WGRAD], lag_, false, ws_w_.data_ptr<float>(),
+             dz_blk_[l].data_ptr<float>());
+      sgd_on(lag_, blk_range_[l].first, blk_range_[l].second, false);
+    }
+    lag_out_->signal(lag_);
+    lag_pending_ = true;
+    lag_list_.clear();
   }
   mark("allreduce_wait");
   {

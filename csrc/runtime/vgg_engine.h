@@ -107,6 +107,17 @@ class VggEngine {
   // CS_DEBUG_SKIP sets the mask at construction.
   void set_debug_skip(int64_t mask) { debug_skip_ = (int)mask; }
   void set_stagger(bool on) { stagger_ = on; }
+  // Deferred weight gradients (world 1, overlapped step): the top `n` blocks' weight gradients and
+  // SGD run on a lag stream that starts at the end of the step and overlaps the NEXT step's forward
+  // (whose BatchNorm gaps leave CUs idle) instead of the backward's data-gradient GEMMs; the forward
+  // waits for them before it overwrites their input activation (the apply of block L-n-1). Exact:
+  // every parameter is updated before its next use, so the numbers are bit-identical. 0 = off
+  // (CS_WGRAD_LAG). join_lag(): the current stream waits for deferred work (before reading params).
+  void set_lag(int64_t n) {
+    join_lag();  // work deferred under the old setting is waited for where the new one expects none
+    lag_blocks_ = (int)n;
+  }
+  void join_lag();
   // single-launch BatchNorm (finalize folded into the apply pass, every block re-combining its 16
   // channels' partials): forward for layers with <= fwd_t statistics partials, backward for <= bwd_p
   // (0 = the separate finalize launch). CS_BN_FWD_FUSED_T / CS_BN_BWD_FUSED_P override.
@@ -224,6 +235,12 @@ class VggEngine {
   int side_pending_ = -1;                      // block whose weight-gradient fork is held back
   unsigned long long* start_sig_ = nullptr;    // deferred signal the next conv launch carries
   void fork_wgrad(int l, int64_t B, bool current);
+  int lag_blocks_ = 0;
+  hipStream_t lag_ = nullptr;
+  std::unique_ptr<StreamLink> lag_in_, lag_out_;  // main -> lag (step end), lag -> main (deferred work done)
+  std::vector<int> lag_list_;                      // blocks whose weight gradient this step defers
+  bool lag_pending_ = false;                       // deferred work enqueued, not yet waited for
+  bool lag_on(hipStream_t s) const;
   int fwd_fused_t_ = 0, bwd_fused_p_ = 0;
   double hp_[4] = {0, 0, 0, 0};  // lr, momentum, wd, dampening of the step in flight
   std::vector<std::pair<int64_t, int64_t>> blk_range_;  // block l's [off, off + n) (block L-1 from 0: fc)

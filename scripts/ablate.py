@@ -4,8 +4,8 @@ property). A variant is an engine debug-skip mask (VggEngine::set_debug_skip: th
 what fusing away a launch class could save — WRONG numbers while set) and/or the serial backward
 and/or a conv tile override (TILESETS below; exact numerics, only the kernels change).
 
-    python scripts/ablate.py --variants "base:0" "no_fwd_apply:4" "no_fwd_fin:8" "serial:0:serial" \
-        "side_small:0::wg16" --rounds 5 --steps 50
+    python scripts/ablate.py --variants base no_fwd_apply:mask=4 serial:serial side_small:tiles=wg16 \
+        lag3:lag=3,file=scripts/tables/st_co.json --rounds 5 --steps 50
 Prints one JSON line per variant: median / min ms per step over the rounds."""
 from __future__ import annotations
 
@@ -98,11 +98,26 @@ def main() -> int:
             TILESETS[name](tr)
     variants = []
     for v in args.variants:
-        # name:mask:serial:tiles:FWD_T/BWD_P:fin:stagger
-        f = v.split(":") + ["", "", "", "", "", ""]
-        fl = tuple(int(x) for x in f[4].split("/")) if f[4] else (0, 0)
-        variants.append((f[0], int(f[1]) if f[1] else 0, f[2] == "serial", f[3], fl, f[5] == "fin",
-                         f[6] == "stagger"))
+        # NAME[:opt,opt,...]  opts: mask=M serial tiles=NAME|file=PATH fused=FWD_T/BWD_P fin stagger lag=N
+        name, _, rest = v.partition(":")
+        o = {"mask": 0, "serial": False, "tiles": "", "fused": (0, 0), "fin": False, "stagger": False, "lag": 0}
+        for tok in filter(None, rest.split(",")):
+            k, _, val = tok.partition("=")
+            if k == "mask":
+                o["mask"] = int(val)
+            elif k == "tiles":
+                o["tiles"] = val
+            elif k == "file":
+                o["tiles"] = "file=" + val
+            elif k == "fused":
+                o["fused"] = tuple(int(x) for x in val.split("/"))
+            elif k == "lag":
+                o["lag"] = int(val)
+            elif k in ("serial", "fin", "stagger"):
+                o[k] = True
+            else:
+                raise SystemExit(f"unknown variant option {tok!r}")
+        variants.append((name, o))
     import gc
     gc.collect()
     gc.disable()
@@ -117,16 +132,18 @@ def main() -> int:
     times = {v[0]: [] for v in variants}
     losses = {v[0]: [] for v in variants}
     for _ in range(args.rounds):
-        for name, mask, serial, tiles, fl, fin, stag in variants:
+        for name, o in variants:
+            tr.engine.set_lag(0)  # joins deferred work before the state is restored
             for dst, src in zip((tr.params, tr.mom, tr.bufs, tr.nbt), snap):
                 dst.copy_(src)
             tr.engine.cursor().copy_(cursor)
-            apply_tiles(tiles)
-            tr.engine.set_bn_fused_limits(*fl)
-            tr.engine.set_fin(fin)
-            tr.engine.set_stagger(stag)
-            tr.engine.set_debug_skip(mask)
-            tr.engine.set_overlap(base_overlap and not serial)
+            apply_tiles(o["tiles"])
+            tr.engine.set_bn_fused_limits(*o["fused"])
+            tr.engine.set_fin(o["fin"])
+            tr.engine.set_stagger(o["stagger"])
+            tr.engine.set_lag(o["lag"])
+            tr.engine.set_debug_skip(o["mask"])
+            tr.engine.set_overlap(base_overlap and not o["serial"])
             for _ in range(args.warmup):
                 tr.step()
             torch.cuda.synchronize()
@@ -137,13 +154,14 @@ def main() -> int:
             times[name].append(1e3 * (time.perf_counter() - t0) / args.steps)
             losses[name].append(tr.last_loss())
     tr.engine.set_debug_skip(0)
+    tr.engine.set_lag(0)
     tr.engine.set_overlap(base_overlap)
     base = statistics.median(times[variants[0][0]])
-    for name, mask, serial, tiles, fl, fin, stag in variants:
+    for name, o in variants:
         med = statistics.median(times[name])
-        print(json.dumps({"variant": name, "mask": mask, "serial": serial, "tiles": tiles or "shipped",
-                          "bn_fused_limits": list(fl), "fin": fin, "stagger": stag, "ms_median": round(med, 4),
-                          "ms_min": round(min(times[name]), 4), "img_s_median": round(args.batch_size * 1e3 / med, 1),
+        print(json.dumps({"variant": name, "opts": {k: (list(v) if isinstance(v, tuple) else v) for k, v in o.items()},
+                          "ms_median": round(med, 4), "ms_min": round(min(times[name]), 4),
+                          "img_s_median": round(args.batch_size * 1e3 / med, 1),
                           "delta_vs_first_pct": round(100.0 * (med - base) / base, 2),
                           "ms_all": [round(t, 4) for t in times[name]],
                           "loss_last": [round(x, 4) for x in losses[name]]}), flush=True)

@@ -481,11 +481,12 @@ def test_side_stream_wgrad_bitwise_and_graph(dev):
     each weight gradient) compute exactly what the serial backward does (SGD in the weight-gradient
     tails); a full-step graph (captured: serial) replays the same bits."""
     runs = []
-    for ovl, graph, stagger in ((False, "none", False), (True, "none", False), (True, "full", False),
-                                (True, "none", True)):
+    for ovl, graph, stagger, lag in ((False, "none", False, 0), (True, "none", False, 0), (True, "full", False, 0),
+                                     (True, "none", True, 0), (True, "none", False, 3), (True, "none", True, 2)):
         t = _trainer(dev, batch_size=32, train_size=256, graph=graph)
         t.engine.set_overlap(ovl)
         t.engine.set_stagger(stagger)  # block l's weight gradient forks at block l-1's data gradient
+        t.engine.set_lag(lag)  # the top `lag` blocks' weight gradients + SGD run into the next forward
         for _ in range(5):
             t.step()
         torch.cuda.synchronize()
@@ -502,10 +503,11 @@ def test_long_run_no_syncs_deterministic(dev):
     weight gradients == the serial backward, bit for bit, run to run (the in-launch finalizes'
     arrival order changes, their combine order does not; the tickets stay zeroed)."""
     out = []
-    for ovl, stagger in ((False, False), (True, False), (True, False), (True, True)):
+    for ovl, stagger, lag in ((False, False, 0), (True, False, 0), (True, False, 0), (True, True, 0), (True, False, 3)):
         t = _trainer(dev, batch_size=32, train_size=640)
         t.engine.set_overlap(ovl)
         t.engine.set_stagger(stagger)
+        t.engine.set_lag(lag)
         for _ in range(30):
             t.step()
         torch.cuda.synchronize()
