@@ -202,7 +202,7 @@ VggEngine::VggEngine(int64_t Bmax, std::vector<int64_t> desc, std::vector<int64_
   if (const char* e = getenv("CS_DEBUG_SKIP")) debug_skip_ = atoi(e);
   if (const char* e = getenv("CS_BN_FWD_FUSED_T")) fwd_fused_t_ = atoi(e);
   if (const char* e = getenv("CS_WGRAD_STAGGER")) stagger_ = atoi(e) != 0;
-  if (const char* e = getenv("CS_WGRAD_LAG")) lag_blocks_ = atoi(e);
+  if (const char* e = getenv("CS_WGRAD_LAG")) set_lag(atoi(e));
   if (const char* e = getenv("CS_BN_BWD_FUSED_P")) bwd_fused_p_ = atoi(e);
   bn_part_ = torch::zeros({partmax}, fo);
   bn_coef_ = torch::zeros({cmax * 3}, fo);
@@ -606,6 +606,18 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
   }
 }
 
+void VggEngine::set_lag(int64_t n) {
+  join_lag();  // work deferred under the old setting is waited for where the new one expects none
+  lag_blocks_ = (int)n;
+  // the stream and its links are made here, never inside a step: creating either synchronises the
+  // device, which would wait on a side-stream link whose signal rides a launch not yet enqueued
+  if (lag_blocks_ > 0 && lag_ == nullptr) {
+    lag_ = reserved_lag_stream();
+    lag_in_ = std::make_unique<StreamLink>();
+    lag_out_ = std::make_unique<StreamLink>();
+  }
+}
+
 bool VggEngine::lag_on(hipStream_t s) const {
   const int L = (int)blocks_.size();
   return lag_blocks_ > 0 && lag_blocks_ <= L - 2 && in_step_ && bwd_sgd_ && side_ok(s) && lag_ != nullptr;
@@ -792,11 +804,7 @@ void VggEngine::step_impl(int64_t B, DeviceComm* comm, const std::vector<int64_t
   // weight-gradient launch
   const bool ovl = side_ok(s);
   bwd_sgd_ = ovl && !dp && !blk_range_.empty();
-  if (bwd_sgd_ && lag_blocks_ > 0 && lag_ == nullptr) {
-    lag_ = reserved_lag_stream();
-    lag_in_ = std::make_unique<StreamLink>();
-    lag_out_ = std::make_unique<StreamLink>();
-  }
+
   sgd_tail_ = !ovl && sgd_tail_on_ && !dp && !blk_range_.empty();
   int64_t hi = L - 1;
   for (size_t k = 0; k < nb; ++k) {

@@ -113,10 +113,7 @@ class VggEngine {
   // waits for them before it overwrites their input activation (the apply of block L-n-1). Exact:
   // every parameter is updated before its next use, so the numbers are bit-identical. 0 = off
   // (CS_WGRAD_LAG). join_lag(): the current stream waits for deferred work (before reading params).
-  void set_lag(int64_t n) {
-    join_lag();  // work deferred under the old setting is waited for where the new one expects none
-    lag_blocks_ = (int)n;
-  }
+  void set_lag(int64_t n);
   void join_lag();
   // single-launch BatchNorm (finalize folded into the apply pass, every block re-combining its 16
   // channels' partials): forward for layers with <= fwd_t statistics partials, backward for <= bwd_p

@@ -14,6 +14,8 @@
 #                              per-queue timeline (scripts/prof_summary.py, scripts/step_timeline.py)
 #   pmc TAG "COUNTERS" [args]  one rocprofv3 counter pass over a short bench (kernel trace only,
 #                              never combined with other trace domains) -> scripts/pmc_summary.py
+#   extras                     part1 batch (B=256), stock PyTorch-ROCm baseline, ResNet-50, Llama-3-8B
+#   projection                 N>1 projection with the RCCL CTA budget priced (a model)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}" || exit 1
 mkdir -p gpurun_out
@@ -72,7 +74,25 @@ case "$what" in
     python3 scripts/pmc_summary.py gpurun_out/$TAG > gpurun_out/${TAG}_summary.txt 2>&1
     head -40 gpurun_out/${TAG}_summary.txt
     ;;
+  extras)
+    # end-of-round side measurements (each its own bench.py process, JSON lines appended to
+    # gpurun_out/extras.jsonl): the tutorial's part1 batch (B=256, master/part1/part1.py:17), the
+    # stock PyTorch-ROCm (MIOpen) VGG-11 baseline on this chip, the BASELINE.json extension configs
+    : > gpurun_out/extras.jsonl
+    for args in "--batch-size 256 --steps 20 --warmup 5" "--engine torch --steps 20 --warmup 5" \
+                "--model resnet50 --dtype bf16 --steps 10 --warmup 4" "--model llama3-8b --steps 6 --warmup 3"; do
+      timeout -k 10 500 python -u bench.py $args 2>>gpurun_out/extras.err | tail -1 >> gpurun_out/extras.jsonl || exit $?
+      tail -1 gpurun_out/extras.jsonl | cut -c1-200
+    done
+    ;;
+  projection)
+    # N > 1 projection with the RCCL CTA budget priced (scripts/dp_projection.py --cta-gbps; a model)
+    timeout -k 10 600 python -u scripts/dp_projection.py --steps 40 --warmup 10 --gbps ${PJ_GBPS:-150,300} \
+      --worlds ${PJ_WORLDS:-8} --ctas ${PJ_CTAS:-8,16,32} --cta-gbps ${PJ_CTA_GBPS:-10} > gpurun_out/projection.jsonl \
+      2> gpurun_out/projection.err || exit $?
+    cut -c1-220 gpurun_out/projection.jsonl
+    ;;
   *)
-    echo "usage: bash scripts/gpu.sh suite|tests|bench|trace|pmc ..."; exit 2
+    echo "usage: bash scripts/gpu.sh suite|tests|bench|trace|pmc|extras|projection ..."; exit 2
     ;;
 esac

@@ -93,6 +93,7 @@ def main() -> int:
                    help="shipped | coresident (every GEMM at its fastest-alone tile within --co-lds-main / "
                         "--co-lds-side KiB, so a main-stream and a side-stream block fit one CU together) | "
                         "file:PATH (a previous step_tune.py output)")
+    p.add_argument("--lag", type=int, default=None, help="engine set_lag(N) during the tuning (default: engine default)")
     p.add_argument("--co-lds-main", type=float, default=80.0)
     p.add_argument("--co-lds-side", type=float, default=75.0)
     args = p.parse_args()
@@ -104,6 +105,8 @@ def main() -> int:
     tr = NativeTrainer(model=args.model, batch_size=args.batch_size, device=torch.device("cuda", 0), graph="none")
     tr._dims = [(4 if l == 0 else s.cin, s.cout, s.hw) for l, s in enumerate(tr.layout.specs)]
     eng = tr.engine
+    if args.lag is not None:
+        eng.set_lag(args.lag)
     gemms = [(l, m) for l in range(tr.layout.L) for m in range(3) if not (l == 0 and m == 1)]
     cur = {g: list(eng.get_tile(*g)) for g in gemms}  # [bm, bn, splits, bk, stage]
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -142,6 +145,8 @@ def main() -> int:
         with open(args.start[5:]) as f:
             for t in json.load(f)["tiles"]:
                 cur[(t[0], t[1])] = list(t[2:7])
+    eng.join_lag()  # isolated timings write gradients the deferred SGD would read
+    torch.cuda.synchronize()
     # ---- phase 1: isolated timings
     short = {}
     iso_cur = {}
@@ -212,7 +217,7 @@ def main() -> int:
                 set_t((l, m), cur[(l, m)])
     ent = {"tiles": [[g[0], g[1]] + cur[g] for g in gemms], "us": us,
            "dual": [0] * tr.layout.L, "step_ms": {"start": round(base, 4), "end": round(final, 4)},
-           "history": history, "tuner": "scripts/step_tune.py"}
+           "history": history, "tuner": "scripts/step_tune.py", "lag": args.lag}
     print(json.dumps(ent), flush=True)
     if args.out:
         with open(args.out, "w") as f:

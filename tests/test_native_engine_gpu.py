@@ -19,7 +19,9 @@ def dev():
 
 def _trainer(dev, **kw):
     from cs744_pytorch_distributed_tutorial_amd.runtime.engine import NativeTrainer
-    args = dict(batch_size=8, device=dev, train_size=256, test_size=40, autotune=False, graph="none")
+    # a stream-link wait that never gets its signal ends after 60 s with an error the test reports,
+    # instead of spinning to the 30 min production timeout
+    args = dict(batch_size=8, device=dev, train_size=256, test_size=40, autotune=False, graph="none", timeout_s=60.0)
     args.update(kw)
     return NativeTrainer(**args)
 
