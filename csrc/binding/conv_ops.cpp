@@ -216,6 +216,38 @@ void register_conv_ops(pybind11::module& m) {
   m.def("conv_stat_rows", [](int64_t K, int64_t bm, int64_t bk, int64_t splits) {
     return cs_conv_stat_rows((int)K, (int)bm, (int)bk, (int)splits);
   }, "FWD BN-statistics tile height of a conv_gemm launch");
+  m.def(
+      "conv0_fwd",
+      [](torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> bias, bool with_stats) {
+        // x [B, 32, 32, 4] NHWC (channel 3 unused), w OIHW [64, 3, 3, 3] -> y [B*32*32, 64] (+ stats)
+        TORCH_CHECK(x.dim() == 4 && x.size(1) == 32 && x.size(2) == 32 && x.size(3) == 4, "conv0_fwd: x [B,32,32,4]");
+        check_t(x, x.numel(), "x");
+        check_t(w, 64 * 27, "w");
+        check_t(bias, 64, "bias");
+        DevGuard g(x.device());
+        const int64_t B = x.size(0), pix = B * 1024;
+        auto y = torch::empty({pix, 64}, x.options());
+        torch::Tensor st = with_stats ? torch::empty({pix / cs_conv0_tile_rows(), 64, 2}, x.options()) : torch::Tensor();
+        CS_LAUNCH(cs_conv0_fwd(x.data_ptr<float>(), w.data_ptr<float>(), cptr(bias), y.data_ptr<float>(),
+                               with_stats ? st.data_ptr<float>() : nullptr, (int)B, 32, 32, 64, cur_stream()));
+        return std::vector<torch::Tensor>{y, st};
+      },
+      "VGG block 0's 3x3 conv (3 -> 64) as the direct f32 kernel (+ BN tile statistics)");
+  m.def(
+      "conv0_wgrad",
+      [](torch::Tensor x, torch::Tensor dz) {
+        TORCH_CHECK(x.dim() == 4 && x.size(1) == 32 && x.size(2) == 32 && x.size(3) == 4, "conv0_wgrad: x [B,32,32,4]");
+        const int64_t B = x.size(0), pix = B * 1024;
+        check_t(x, x.numel(), "x");
+        check_t(dz, pix * 64, "dz");
+        DevGuard g(x.device());
+        auto part = torch::empty({(int64_t)cs_conv0_wgrad_part_floats((int)B, 32, 32)}, x.options());
+        auto dw = torch::empty({64, 3, 3, 3}, x.options());
+        CS_LAUNCH(cs_conv0_wgrad(x.data_ptr<float>(), dz.data_ptr<float>(), part.data_ptr<float>(), dw.data_ptr<float>(),
+                                 (int)B, 32, 32, 64, cur_stream()));
+        return dw;
+      },
+      "VGG block 0's weight gradient (OIHW) as the direct f32 kernels (fixed-order sum)");
   m.def("bn_finalize", &bn_finalize);
   m.def("bn_eval_coeffs", &bn_eval_coeffs);
   m.def("bn_apply", &bn_apply);

@@ -119,6 +119,17 @@ struct CsConvArgs {
 };
 
 void cs_conv_fill_dims(CsConvArgs* a, int mode);
+
+// VGG block 0 (3 -> 64 channels, 32 x 32, input padded to 4 channels NHWC, OIHW weights) as direct
+// f32 kernels (conv0.hip). fwd: y [pix][64] (+bias) and, when stats != null, the BatchNorm tile
+// statistics [pix / cs_conv0_tile_rows()][64][2] = (mean, M2); wgrad: dW (OIHW [64][27]) through
+// `part` scratch of cs_conv0_wgrad_part_floats() floats (fixed-order sum: deterministic)
+int cs_conv0_tile_rows();
+size_t cs_conv0_wgrad_part_floats(int B, int H, int W);
+hipError_t cs_conv0_fwd(const float* x, const float* w, const float* bias, float* y, float* stats, int B, int H,
+                        int W, int Cout, hipStream_t stream);
+hipError_t cs_conv0_wgrad(const float* x, const float* dz, float* part, float* dw, int B, int H, int W, int Cout,
+                          hipStream_t stream);
 // bm, bn in {64, 128}; bk in {16, 32}; splits >= 1 (split-K over blockIdx.z + deterministic reduce).
 // FWD stats tiles have `bm` rows when splits == 1 and CS_SPLITK_STAT_ROWS rows otherwise.
 #define CS_SPLITK_STAT_ROWS 16

@@ -203,6 +203,7 @@ VggEngine::VggEngine(int64_t Bmax, std::vector<int64_t> desc, std::vector<int64_
   if (const char* e = getenv("CS_BN_FWD_FUSED_T")) fwd_fused_t_ = atoi(e);
   if (const char* e = getenv("CS_WGRAD_STAGGER")) stagger_ = atoi(e) != 0;
   if (const char* e = getenv("CS_WGRAD_LAG")) set_lag(atoi(e));
+  if (const char* e = getenv("CS_CONV0_DIRECT")) conv0_direct_ = atoi(e) != 0;
   if (const char* e = getenv("CS_BN_BWD_FUSED_P")) bwd_fused_p_ = atoi(e);
   bn_part_ = torch::zeros({partmax}, fo);
   bn_coef_ = torch::zeros({cmax * 3}, fo);
@@ -432,9 +433,17 @@ void VggEngine::forward_train(int64_t B) {
       const CsBnFin f = fin_fwd_args(l, (int)B);
       conv(l, CS_CONV_FWD, (int)B, t, s, true, nullptr, nullptr, nullptr, nullptr, &f);
     } else if (!(debug_skip_ & 8)) {
-      conv(l, CS_CONV_FWD, (int)B, t, s, true);
       const int64_t M = B * b.H * b.H;
-      const int rows = cs_conv_stat_rows(9 * b.cin, t.bm, t.bk, t.splits);
+      int rows;
+      if (l == 0 && conv0_direct_ok(B)) {
+        ok(cs_conv0_fwd(b.x.data_ptr<float>(), P(b.w_off), P(b.b_off), b.y.data_ptr<float>(), b.stats.data_ptr<float>(),
+                        (int)B, b.H, b.H, b.cout, s),
+           "conv0_fwd");
+        rows = cs_conv0_tile_rows();
+      } else {
+        conv(l, CS_CONV_FWD, (int)B, t, s, true);
+        rows = cs_conv_stat_rows(9 * b.cin, t.bm, t.bk, t.splits);
+      }
       const int T = (int)cdiv(M, rows);
       if (T <= fwd_fused_t_ && b.cout % 16 == 0) {
         if (lag_pending_ && l + 1 >= L - lag_blocks_) {
@@ -568,7 +577,7 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
         // block 0's weight gradient is the step's last GEMM: nothing left to overlap it with, so it
         // runs here (the main split-K workspace is free: no data gradient for block 0)
         if (side_pending_ >= 0) start_sig_ = dz_link_->defer();
-        conv(l, CS_CONV_WGRAD, (int)B, b.tile[CS_CONV_WGRAD], s, false, ws_.data_ptr<float>(), dz);
+        conv0_wgrad(B, s, dz);
         if (side_pending_ >= 0) fork_wgrad(side_pending_, B, false);
         if (bwd_sgd_) sgd_on(s, blk_range_[0].first, blk_range_[0].second, true);
       }
@@ -582,8 +591,13 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
         tail = sgd_tail_args(l + 1);
         if (tail.n == 0) sgd_on(s, blk_range_[l + 1].first, blk_range_[l + 1].second, false);
       }
-      conv(l, CS_CONV_WGRAD, (int)B, b.tile[CS_CONV_WGRAD], s, false, ws_w_.data_ptr<float>(), dz, nullptr,
-           tail.n > 0 ? &tail : nullptr);
+      if (l == 0 && conv0_direct_ok(B)) {
+        if (tail.n > 0) sgd_on(s, blk_range_[l + 1].first, blk_range_[l + 1].second, false);
+        conv0_wgrad(B, s, dz);
+      } else {
+        conv(l, CS_CONV_WGRAD, (int)B, b.tile[CS_CONV_WGRAD], s, false, ws_w_.data_ptr<float>(), dz, nullptr,
+             tail.n > 0 ? &tail : nullptr);
+      }
       if (l > 0)
         conv(l, CS_CONV_DGRAD, (int)B, b.tile[CS_CONV_DGRAD], s, false, nullptr, dz, &erv, nullptr, fp);
     }
@@ -616,6 +630,26 @@ void VggEngine::set_lag(int64_t n) {
     lag_in_ = std::make_unique<StreamLink>();
     lag_out_ = std::make_unique<StreamLink>();
   }
+}
+
+bool VggEngine::conv0_direct_ok(int64_t B) const {
+  const VggBlock& b = blocks_[0];
+  return conv0_direct_ && b.cin == 4 && b.cout == 64 && b.H == 32 &&
+         cs_conv0_wgrad_part_floats((int)B, b.H, b.H) <= (size_t)ws_elems_;
+}
+
+void VggEngine::conv0_wgrad(int64_t B, hipStream_t s, float* dz) {
+  VggBlock& b = blocks_[0];
+  if (!conv0_direct_ok(B)) {
+    conv(0, CS_CONV_WGRAD, (int)B, b.tile[CS_CONV_WGRAD], s, false, ws_.data_ptr<float>(), dz);
+    return;
+  }
+  if (start_sig_ != nullptr) {  // the deferred fork signal this launch would have carried
+    ok(cs_link_signal(start_sig_, s), "link signal");
+    start_sig_ = nullptr;
+  }
+  ok(cs_conv0_wgrad(b.x.data_ptr<float>(), dz, ws_.data_ptr<float>(), G(b.w_off), (int)B, b.H, b.H, b.cout, s),
+     "conv0_wgrad");
 }
 
 bool VggEngine::lag_on(hipStream_t s) const {
@@ -738,7 +772,12 @@ void VggEngine::forward_eval(int64_t B) {
   float* bufs = bufs_.data_ptr<float>();
   for (int l = 0; l < L; ++l) {
     VggBlock& b = blocks_[l];
-    conv(l, CS_CONV_FWD, (int)B, b.tile[CS_CONV_FWD], s, false);
+    if (l == 0 && conv0_direct_ok(B))
+      ok(cs_conv0_fwd(b.x.data_ptr<float>(), P(b.w_off), P(b.b_off), b.y.data_ptr<float>(), nullptr, (int)B, b.H, b.H,
+                      b.cout, s),
+         "conv0_fwd");
+    else
+      conv(l, CS_CONV_FWD, (int)B, b.tile[CS_CONV_FWD], s, false);
     ok(cs_bn_eval_coeffs(P(b.g_off), P(b.be_off), bufs + b.rm_off, bufs + b.rv_off, b.cout, kBnEps, sc, sh, s),
        "bn_eval_coeffs");
     float* out = (l + 1 < L) ? blocks_[l + 1].x.data_ptr<float>() : feats_.data_ptr<float>();

@@ -107,6 +107,9 @@ class VggEngine {
   // CS_DEBUG_SKIP sets the mask at construction.
   void set_debug_skip(int64_t mask) { debug_skip_ = (int)mask; }
   void set_stagger(bool on) { stagger_ = on; }
+  // block 0's convolution (3 -> 64) as the direct conv0.hip kernels instead of the implicit GEMM
+  // (forward + BN tile statistics, weight gradient); CS_CONV0_DIRECT=0 restores the GEMM
+  void set_conv0_direct(bool on) { conv0_direct_ = on; }
   // Deferred weight gradients (world 1, overlapped step): the top `n` blocks' weight gradients and
   // SGD run on a lag stream that starts at the end of the step and overlaps the NEXT step's forward
   // (whose BatchNorm gaps leave CUs idle) instead of the backward's data-gradient GEMMs; the forward
@@ -233,6 +236,9 @@ class VggEngine {
   unsigned long long* start_sig_ = nullptr;    // deferred signal the next conv launch carries
   void fork_wgrad(int l, int64_t B, bool current);
   int lag_blocks_ = 0;
+  bool conv0_direct_ = true;
+  bool conv0_direct_ok(int64_t B) const;
+  void conv0_wgrad(int64_t B, hipStream_t s, float* dz);
   hipStream_t lag_ = nullptr;
   std::unique_ptr<StreamLink> lag_in_, lag_out_;  // main -> lag (step end), lag -> main (deferred work done)
   std::vector<int> lag_list_;                      // blocks whose weight gradient this step defers

@@ -98,9 +98,10 @@ def main() -> int:
             TILESETS[name](tr)
     variants = []
     for v in args.variants:
-        # NAME[:opt,opt,...]  opts: mask=M serial tiles=NAME|file=PATH fused=FWD_T/BWD_P fin stagger lag=N
+        # NAME[:opt,opt,...]  opts: mask=M serial tiles=NAME|file=PATH fused=FWD_T/BWD_P fin stagger lag=N conv0=0|1
         name, _, rest = v.partition(":")
-        o = {"mask": 0, "serial": False, "tiles": "", "fused": (0, 0), "fin": False, "stagger": False, "lag": 0}
+        o = {"mask": 0, "serial": False, "tiles": "", "fused": (0, 0), "fin": False, "stagger": False, "lag": 0,
+             "conv0": 1}
         for tok in filter(None, rest.split(",")):
             k, _, val = tok.partition("=")
             if k == "mask":
@@ -111,8 +112,8 @@ def main() -> int:
                 o["tiles"] = "file=" + val
             elif k == "fused":
                 o["fused"] = tuple(int(x) for x in val.split("/"))
-            elif k == "lag":
-                o["lag"] = int(val)
+            elif k in ("lag", "conv0"):
+                o[k] = int(val)
             elif k in ("serial", "fin", "stagger"):
                 o[k] = True
             else:
@@ -142,6 +143,7 @@ def main() -> int:
             tr.engine.set_fin(o["fin"])
             tr.engine.set_stagger(o["stagger"])
             tr.engine.set_lag(o["lag"])
+            tr.engine.set_conv0_direct(bool(o["conv0"]))
             tr.engine.set_debug_skip(o["mask"])
             tr.engine.set_overlap(base_overlap and not o["serial"])
             for _ in range(args.warmup):

@@ -305,3 +305,35 @@ def test_conv_fwd_in_launch_bn_finalize(dev, shape, tile):
     _close(rm, 0.9 * 0.25 + 0.1 * mu, 1e-5)
     _close(rv, 0.9 * 2.0 + 0.1 * ref.var(0, unbiased=True), 1e-5)
     assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+
+
+@pytest.mark.parametrize("B", [1, 4, 64])
+def test_conv0_direct_kernels_match_fp64(dev, B):
+    """VGG block 0 (3 -> 64, 3x3, pad 1) as the direct conv0.hip kernels: y (+bias), the BatchNorm
+    tile statistics (per 256-row tile mean and M2) and the OIHW weight gradient against float64
+    PyTorch on the same inputs (channel 3 of the padded NHWC input is ignored)."""
+    from cs744_pytorch_distributed_tutorial_amd.ops import native
+    C = native.C()
+    g = torch.Generator().manual_seed(B)
+    x = torch.randn(B, 32, 32, 4, generator=g)
+    x[..., 3] = 7.0  # must not leak into the result
+    w = torch.randn(64, 3, 3, 3, generator=g) * 0.2
+    b = torch.randn(64, generator=g)
+    y, st = C.conv0_fwd(x.to(dev), w.to(dev), b.to(dev), True)
+    xr = x[..., :3].permute(0, 3, 1, 2).double()
+    yr = F.conv2d(xr, w.double(), b.double(), padding=1).permute(0, 2, 3, 1).reshape(-1, 64)
+    rel = (y.double().cpu() - yr).abs().max() / yr.abs().max()
+    assert rel < 2e-6, rel
+    t = yr.view(-1, 256, 64)
+    mean = t.mean(1)
+    m2 = ((t - mean[:, None, :]) ** 2).sum(1)
+    st = st.double().cpu()
+    assert ((st[..., 0] - mean).abs().max() / yr.abs().max()) < 2e-6
+    assert ((st[..., 1] - m2).abs().max() / m2.abs().max()) < 2e-5
+    dz = torch.randn(B * 1024, 64, generator=g)
+    dw = C.conv0_wgrad(x.to(dev), dz.to(dev)).double().cpu()
+    dzr = dz.double().view(B, 32, 32, 64).permute(0, 3, 1, 2)
+    dwr = torch.nn.grad.conv2d_weight(xr, (64, 3, 3, 3), dzr, padding=1)
+    assert ((dw - dwr).abs().max() / dwr.abs().max()) < 2e-5
+    # deterministic: the fixed-order sum gives the same bits run to run
+    assert torch.equal(C.conv0_wgrad(x.to(dev), dz.to(dev)).cpu(), dw.float())
