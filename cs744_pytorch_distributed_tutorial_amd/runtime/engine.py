@@ -410,12 +410,16 @@ class NativeTrainer:
         """Chosen (bm, bn, split-K) and measured time per conv GEMM of the step."""
         out = []
         names = ("fwd", "dgrad", "wgrad")
+        direct0 = self.engine.conv0_direct(self.B)
         for l in range(self.layout.L):
             for m in range(3):
                 if l == 0 and m == 1:
                     continue
                 bm, bn, sp, bk, st = self.engine.get_tile(l, m)
                 us = self.tune_us[3 * l + m] if self.tune_us else None
+                if l == 0 and direct0:  # block 0 runs the direct conv0.hip kernels, not this GEMM tile
+                    out.append({"block": 0, "op": names[m], "kernel": "conv0_direct", "math": "f32-direct"})
+                    continue
                 out.append({"block": l, "op": names[m], "bm": bm, "bn": bn, "bk": bk, "splits": sp,
                             "stage": _STAGE_NAMES.get(st & 7, str(st & 7)),
                             "math": "bf16" if st & 32 else ("x6s" if st & 16 else ("x6" if st & 8 else "f32")),

@@ -428,7 +428,7 @@ void VggEngine::forward_train(int64_t B) {
     const ConvTile& t = b.tile[CS_CONV_FWD];
     float* bn = b.bn.data_ptr<float>();
     float* out = (l + 1 < L) ? blocks_[l + 1].x.data_ptr<float>() : feats_.data_ptr<float>();
-    if (fin_on_) {
+    if (fin_on_ && !(l == 0 && conv0_direct_ok(B))) {
       // conv [+ split-K combine]: its last-arriving block finalizes the batch statistics
       const CsBnFin f = fin_fwd_args(l, (int)B);
       conv(l, CS_CONV_FWD, (int)B, t, s, true, nullptr, nullptr, nullptr, nullptr, &f);

@@ -110,6 +110,7 @@ class VggEngine {
   // block 0's convolution (3 -> 64) as the direct conv0.hip kernels instead of the implicit GEMM
   // (forward + BN tile statistics, weight gradient); CS_CONV0_DIRECT=0 restores the GEMM
   void set_conv0_direct(bool on) { conv0_direct_ = on; }
+  bool conv0_direct(int64_t B) const { return conv0_direct_ok(B); }
   // Deferred weight gradients (world 1, overlapped step): the top `n` blocks' weight gradients and
   // SGD run on a lag stream that starts at the end of the step and overlaps the NEXT step's forward
   // (whose BatchNorm gaps leave CUs idle) instead of the backward's data-gradient GEMMs; the forward

@@ -269,7 +269,7 @@ def test_bf16_mode_tracks_fp32(dev):
     # bf16 kernel except the padded conv0 forward, and a step stays close to the f32 engine
     a = _trainer(dev, batch_size=16, train_size=128)
     b = _trainer(dev, batch_size=16, train_size=128, dtype="bf16", autotune=True)
-    assert all(t["math"] == "bf16" for t in b.tile_table() if not (t["block"] == 0 and t["op"] == "fwd"))
+    assert all(t["math"] == "bf16" for t in b.tile_table() if t["block"] != 0)  # block 0: f32 (direct or GEMM)
     a.step()
     b.step()
     torch.cuda.synchronize()
@@ -457,6 +457,7 @@ def test_bench_config_b64_matches_fp64(dev, variant):
     if variant == "bn_fused":  # single-launch BN at every layer, forward and backward
         tr.engine.set_bn_fused_limits(1 << 30, 1 << 30)
     if variant == "x6s_everywhere":
+        tr.engine.set_conv0_direct(False)  # block 0's weight gradient on its X6S GEMM tile too
         assert _force_x6s(tr) == 22
         assert sum(t["math"] == "x6s" for t in tr.tile_table()) == 22
     if variant == "autotuned":
