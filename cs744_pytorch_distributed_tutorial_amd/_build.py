@@ -150,7 +150,7 @@ def _check_stubs(so: str) -> None:
 
 ASAN_OUT = os.path.join(PKG_DIR, "bin", "asan_runtime_test")
 # host code only: device code is never sanitized (each -fsanitize right after -Xarch_host)
-ASAN_FLAGS = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fno-omit-frame-pointer", "-O1", "-g"]
+ASAN_FLAGS = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fno-omit-frame-pointer", "-O1", "-gline-tables-only"]
 
 
 def build_asan(jobs: int = 0, verbose: bool = False) -> str:
