@@ -340,6 +340,7 @@ def main(argv=None) -> int:
         maths = [t["math"] for t in trainer.tile_table()]
         out["config"]["conv_gemm_math"] = {m: maths.count(m) for m in sorted(set(maths))}
         out["config"]["conv_tiles"] = getattr(trainer, "tile_source", None)
+        out["config"]["comm_defer"] = getattr(trainer, "comm_defer", None)
         out["config"]["wgrad_side_stream"] = getattr(trainer, "overlap_wgrad", None)
     out["config"]["grad_comm_dtype"] = getattr(trainer, "grad_comm_dtype", "fp32")
     if os.environ.get("CS744_BENCH_CALIBRATE", "1") != "0":

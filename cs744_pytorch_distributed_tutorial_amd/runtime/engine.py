@@ -313,6 +313,14 @@ class NativeTrainer:
                       file=sys.stderr, flush=True)
                 self.overlap_wgrad = False
         self.engine.set_overlap(self.overlap_wgrad)
+        # deferred buckets (VggEngine::set_comm_defer): data-parallel steps enqueue these buckets'
+        # all-reduce + SGD after the last bucket's and the next forward waits for them before their
+        # lowest block. CS_COMM_DEFER = "auto" (default: the 4th bucket from the bottom when there
+        # are >= 5 — for VGG-11's 4 MiB plan the 9 MiB bucket of block 5, whose collective then
+        # overlaps the next forward of blocks 0-4), "none", or a comma list of bucket indices.
+        self.comm_defer = self._plan_defer(os.environ.get("CS_COMM_DEFER", "auto"),
+                                           world > 1 or str(probe).startswith("xgmi"))
+        self.engine.set_comm_defer(self.comm_defer)
         # BatchNorm finalize: separate launches by default. The in-launch last-arriver finalize
         # (bn_fin.h, CS_BN_FIN=1) removes one launch per block but measured 6-8 % slower with the
         # side-stream weight gradients on one box (88.6 k vs 83.3 k img/s at 20/5, 90.3 k vs 83.7 k at
@@ -330,6 +338,10 @@ class NativeTrainer:
             self.engine.set_math(3)
         self.tune_us: Optional[List[float]] = None
         self.tile_source = "default"
+        # data-parallel steps (world > 1, or the one-GPU N>1 model) use the table tuned with the
+        # communicator's CTAs holding CUs (scripts/step_tune.py --probe), when one is shipped
+        self._dp_tiles = {"dp": True, "w1": False}.get(os.environ.get("CS_TILE_TABLE", ""),
+                                                        world > 1 or str(probe).startswith("xgmi"))
         if autotune:
             self._tune(model + ("" if dtype == "fp32" else "/bf16"), os.environ.get("CS744_TUNE_CACHE"))
         if graph == "auto":
@@ -357,11 +369,24 @@ class NativeTrainer:
         self._epoch_idx = None
         self._start_epoch(0)
 
+    def _plan_defer(self, spec: str, dp: bool) -> List[int]:
+        nb = len(self.bucket_lows)
+        if spec == "auto":
+            return [nb - 4] if dp and nb >= 5 else []
+        if spec in ("", "none"):
+            return []
+        ks = sorted({int(x) + (nb if int(x) < 0 else 0) for x in spec.split(",")})  # -2: bucket nb - 2
+        if any(k < 0 or k >= nb - 1 for k in ks):
+            raise ValueError(f"CS_COMM_DEFER={spec!r}: bucket indices in [0, {nb - 1}) (the last bucket never defers)")
+        return ks
+
     def sync_from_root(self) -> None:
         """DDP construction-time sync (`torch:nn/parallel/distributed.py:855-870`): rank 0's
         parameters, momentum, BN buffers and counters on every rank (also after a resume)."""
         if self.comm is None:
             return
+        if getattr(self, "engine", None) is not None:
+            self._join_lag()
         for t in (self.params, self.mom, self.bufs, self.nbt):
             self.comm.broadcast(t, 0)
 
@@ -393,6 +418,9 @@ class NativeTrainer:
         if os.environ.get("CS744_TUNE", "0") != "1" and os.path.exists(SHIPPED_TILES):
             with open(SHIPPED_TILES) as f:
                 shipped = json.load(f)
+            if self._dp_tiles and key + "/dp" in shipped and self._apply_tiles(shipped[key + "/dp"]):
+                self.tile_source = "shipped-dp"
+                return
             if key in shipped and self._apply_tiles(shipped[key]):
                 self.tile_source = "shipped"
                 return
@@ -627,6 +655,7 @@ class NativeTrainer:
     @torch.no_grad()
     def evaluate(self, max_batches: Optional[int] = None) -> Dict[str, float]:
         """Full (non-sharded) test-set evaluation, as every reference rank does (`part2b.py:111-115`)."""
+        self._join_lag()
         if self.comm is not None and self.sync_mode == "ddp" and self.broadcast_buffers:
             self._pre_forward_sync()
         n = len(self.test_set)
@@ -654,7 +683,8 @@ class NativeTrainer:
 
     def _join_lag(self) -> None:
         """The current stream waits for weight gradients / SGD the engine deferred into the next
-        step (CS_WGRAD_LAG): every host read of the parameters goes through here."""
+        step (CS_WGRAD_LAG) and for deferred buckets' all-reduce + SGD (CS_COMM_DEFER): every host
+        read of the parameters goes through here."""
         if self.engine is not None:
             self.engine.join_lag()
 

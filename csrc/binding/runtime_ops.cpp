@@ -210,6 +210,9 @@ void register_runtime(pybind11::module& m) {
       .def("set_conv0_direct", &cs::VggEngine::set_conv0_direct)
       .def("conv0_direct", &cs::VggEngine::conv0_direct)
       .def("join_lag", &cs::VggEngine::join_lag)
+      .def("set_comm_defer", &cs::VggEngine::set_comm_defer)
+      .def("comm_defer", &cs::VggEngine::comm_defer)
+      .def("defer_pending", &cs::VggEngine::defer_pending)
       .def("set_bn_fused_limits", &cs::VggEngine::set_bn_fused_limits, py::arg("fwd_t"), py::arg("bwd_p"))
       .def("set_dual", &cs::VggEngine::set_dual)
       .def("set_bn_fused_rows", &cs::VggEngine::set_bn_fused_rows)

@@ -427,6 +427,7 @@ void VggEngine::forward_train(int64_t B) {
     VggBlock& b = blocks_[l];
     const ConvTile& t = b.tile[CS_CONV_FWD];
     float* bn = b.bn.data_ptr<float>();
+    if (l == defer_block_) join_deferred(s);  // the previous step's deferred buckets wrote these weights
     float* out = (l + 1 < L) ? blocks_[l + 1].x.data_ptr<float>() : feats_.data_ptr<float>();
     if (fin_on_ && !(l == 0 && conv0_direct_ok(B))) {
       // conv [+ split-K combine]: its last-arriving block finalizes the batch statistics
@@ -658,9 +659,17 @@ bool VggEngine::lag_on(hipStream_t s) const {
 }
 
 void VggEngine::join_lag() {
+  join_deferred(cur_stream());
   if (!lag_pending_) return;
   lag_out_->wait(cur_stream());
   lag_pending_ = false;
+}
+
+void VggEngine::join_deferred(hipStream_t s) {
+  if (defer_comm_ == nullptr) return;
+  if (!(debug_skip_ & 64)) defer_comm_->join(s);
+  defer_comm_ = nullptr;
+  defer_block_ = -1;
 }
 
 void VggEngine::fork_wgrad(int l, int64_t B, bool current) {
@@ -816,6 +825,13 @@ void VggEngine::step_impl(int64_t B, DeviceComm* comm, const std::vector<int64_t
   // the caller passes a communicator only when the step is data-parallel (a one-rank
   // communicator too: the CS_COMM_PROBE measurement and the ProbeComm ordering test)
   const bool dp = comm != nullptr;
+  // deferred buckets: never inside a graph capture (the wait would have to cross graph launches),
+  // and a previous step's deferral on another communicator (or none) is waited for here
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  ok(hipStreamIsCapturing(s, &cap), "hipStreamIsCapturing");
+  const bool capturing = cap != hipStreamCaptureStatusNone;
+  if (defer_comm_ != nullptr && (capturing || defer_comm_ != comm)) join_deferred(s);
+  std::vector<size_t> deferred;
   tn_ = 0;
   Range step_range("cs.step");
   mark("start");
@@ -860,6 +876,16 @@ void VggEngine::step_impl(int64_t B, DeviceComm* comm, const std::vector<int64_t
     mark(k < 8 ? kBwd[k] : "backward_bucket8+");
     hi = lo - 1;
     if (!dp) continue;
+    if (comm_sgd && !capturing && k + 1 < nb &&
+        std::find(comm_defer_.begin(), comm_defer_.end(), (int64_t)k) != comm_defer_.end()) {
+      deferred.push_back(k);  // enqueued after the last bucket (below)
+      if (broadcast_buffers && k == 0) {
+        // no all-reduce of bucket 0 ahead of it to order it after this forward: the broadcast forks
+        comm->broadcast(bufs_.data_ptr<float>(), bufs_.numel(), ncclFloat32, 0, s, /*fork=*/true);
+        comm->broadcast(nbt_.data_ptr<int64_t>(), nbt_.numel(), ncclInt64, 0, s, /*fork=*/false);
+      }
+      continue;
+    }
     {
       // the bucket is complete once its last weight gradient is: the all-reduce forks from there
       // (the side stream when overlapped; the bucket holding block 0, whose weight gradient ran on
@@ -892,6 +918,17 @@ void VggEngine::step_impl(int64_t B, DeviceComm* comm, const std::vector<int64_t
     flush_signal(s);
     if (ovl) join_side(s);
     if (dp && !(debug_skip_ & 1)) comm->join(s);
+    if (!deferred.empty()) {
+      // every weight gradient is complete on this stream (joined above): the deferred buckets fork
+      // from here, behind the last bucket on the comm stream; the next forward joins them
+      for (size_t k : deferred) {
+        comm->all_reduce(G(bucket_ranges[2 * k]), bucket_ranges[2 * k + 1], ncclFloat32, ncclAvg, s, /*fork=*/true);
+        sgd_on(comm->stream(), bucket_ranges[2 * k], bucket_ranges[2 * k + 1], false);
+        const int lo = (int)bucket_blocks[k];
+        defer_block_ = defer_block_ < 0 ? lo : std::min(defer_block_, lo);
+      }
+      defer_comm_ = comm;
+    }
   }
   if (!lag_list_.empty()) {
     // deferred weight gradients: the lag stream starts once the step's main stream (joined with

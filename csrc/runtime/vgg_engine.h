@@ -103,7 +103,8 @@ class VggEngine {
   // measurement / negative-control switches (WRONG numbers when set; never in a product run):
   // 1 skip the comm join, 2 no comm fork (ordering-test controls); ablation upper bounds of a
   // fusion (what the step would save if a launch class were free): 4 forward bn_apply,
-  // 8 forward bn_finalize, 16 backward BN (finalize + apply), 32 side-stream weight-gradient GEMMs.
+  // 8 forward bn_finalize, 16 backward BN (finalize + apply), 32 side-stream weight-gradient GEMMs;
+  // 64 the next forward skips its wait for deferred buckets (ordering-test control).
   // CS_DEBUG_SKIP sets the mask at construction.
   void set_debug_skip(int64_t mask) { debug_skip_ = (int)mask; }
   void set_stagger(bool on) { stagger_ = on; }
@@ -119,6 +120,15 @@ class VggEngine {
   // (CS_WGRAD_LAG). join_lag(): the current stream waits for deferred work (before reading params).
   void set_lag(int64_t n);
   void join_lag();
+  // Data-parallel steps: the buckets listed (bucket indices, never the last one) have their
+  // all-reduce + SGD enqueued on the comm stream AFTER the last bucket's, and the step's closing
+  // join covers only the others; the next step's forward waits for them right before the conv of
+  // their lowest block. The bottom blocks' buckets — produced last by the backward, needed first by
+  // the next forward — then no longer queue behind a large top bucket, whose collective instead
+  // overlaps the next forward's lower blocks. join_lag() waits for them too (eval, host reads).
+  void set_comm_defer(std::vector<int64_t> buckets) { comm_defer_ = std::move(buckets); }
+  std::vector<int64_t> comm_defer() const { return comm_defer_; }
+  bool defer_pending() const { return defer_comm_ != nullptr; }
   // single-launch BatchNorm (finalize folded into the apply pass, every block re-combining its 16
   // channels' partials): forward for layers with <= fwd_t statistics partials, backward for <= bwd_p
   // (0 = the separate finalize launch). CS_BN_FWD_FUSED_T / CS_BN_BWD_FUSED_P override.
@@ -243,6 +253,10 @@ class VggEngine {
   hipStream_t lag_ = nullptr;
   std::unique_ptr<StreamLink> lag_in_, lag_out_;  // main -> lag (step end), lag -> main (deferred work done)
   std::vector<int> lag_list_;                      // blocks whose weight gradient this step defers
+  std::vector<int64_t> comm_defer_;
+  DeviceComm* defer_comm_ = nullptr;  // deferred buckets enqueued on this communicator, not waited for
+  int defer_block_ = -1;              // the next forward waits before this block's conv
+  void join_deferred(hipStream_t s);
   bool lag_pending_ = false;                       // deferred work enqueued, not yet waited for
   bool lag_on(hipStream_t s) const;
   int fwd_fused_t_ = 0, bwd_fused_p_ = 0;

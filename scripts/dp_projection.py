@@ -17,11 +17,16 @@ collective gets with c CTAs is modelled as min(G, c * B) — the CTA count price
 CTAs leave more CUs to the backward GEMMs but slow the all-reduce. B is an ASSUMPTION (default
 10 GB/s per CTA, i.e. 16 CTAs ~ 160 GB/s), not a measurement on an 8-GPU node.
 
-Usage (GPU box): python scripts/dp_projection.py [--steps 50] [--gbps 100,150,300] [--worlds 2,4,8]
+Every configuration (world 1 included) runs --repeats times, the rounds interleaved, and the
+median step time is reported with all samples: one run of a configuration can land on a slow
+clock phase (a 2x outlier was seen in a single-pass sweep).
+
+Usage (GPU box): python scripts/dp_projection.py [--steps 50] [--gbps 100,150,300] [--worlds 2,4,8] [--repeats 3]
 """
 import argparse
 import json
 import os
+import statistics
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -64,25 +69,42 @@ def main():
                    help="busy workgroups standing in for RCCL's CTAs during each collective (0: one sleeping wave)")
     p.add_argument("--cta-gbps", type=float, default=0.0,
                    help="> 0: per-CTA channel bandwidth (GB/s); busBW = min(G, ctas * this) (a model)")
+    p.add_argument("--repeats", type=int, default=3)
     a = p.parse_args()
     torch.cuda.set_device(0)
     from cs744_pytorch_distributed_tutorial_amd.ops import native
     native.C().reserve_streams()  # the side stream owns a hardware queue (as in bench.py)
-    base, ph0, buckets = run("0", a.steps, a.warmup)
-    print(json.dumps({"config": "world 1 (no communicator)", "ms_per_step": round(base, 4),
-                      "img_s": round(64 / base * 1e3), "bucket_mib": [round(b, 2) for b in buckets],
-                      "phases_ms": {k: round(v, 4) for k, v in ph0.items()}}), flush=True)
+    configs = [(None, None, None, None)]
     for g in [float(x) for x in a.gbps.split(",")]:
         for w in [int(x) for x in a.worlds.split(",")]:
             for c in [int(x) for x in a.ctas.split(",")]:
                 ge = min(g, c * a.cta_gbps) if a.cta_gbps > 0 and c > 0 else g
-                ms, ph, _ = run(f"xgmi:{ge}:{w}:{a.latency_us}:{c}", a.steps, a.warmup)
-                print(json.dumps({"config": f"projected N={w}, ring busBW {ge:g} GB/s (link {g:g}), "
-                                            f"{a.latency_us:g} us/collective, {c} busy CTAs per collective",
-                                  "model": "busBW=min(link, ctas*cta_gbps)" if a.cta_gbps > 0 else "busBW=link",
-                                  "ms_per_step": round(ms, 4), "projected_img_s": round(w * 64 / ms * 1e3),
-                                  "per_gpu_img_s": round(64 / ms * 1e3), "efficiency_vs_world1": round(base / ms, 4),
-                                  "allreduce_wait_ms": round(ph.get("allreduce_wait", 0.0), 4)}), flush=True)
+                configs.append((g, w, c, ge))
+    samples = [[] for _ in configs]
+    for _ in range(a.repeats):
+        for i, (g, w, c, ge) in enumerate(configs):
+            probe = "0" if g is None else f"xgmi:{ge}:{w}:{a.latency_us}:{c}"
+            samples[i].append(run(probe, a.steps, a.warmup))
+            print(f"[projection] {probe}: {samples[i][-1][0]:.4f} ms", file=sys.stderr, flush=True)
+    med = statistics.median_low  # an even count keeps the lower middle sample (outliers are slow)
+    base = med([ms for ms, _, _ in samples[0]])
+    for i, (g, w, c, ge) in enumerate(configs):
+        ms = med([m for m, _, _ in samples[i]])
+        ms_all = [round(m, 4) for m, _, _ in samples[i]]
+        ph = min(samples[i], key=lambda t: abs(t[0] - ms))[1]
+        if g is None:
+            buckets = samples[i][0][2]
+            print(json.dumps({"config": "world 1 (no communicator)", "ms_per_step": round(ms, 4), "ms_all": ms_all,
+                              "img_s": round(64 / ms * 1e3), "bucket_mib": [round(b, 2) for b in buckets],
+                              "phases_ms": {k: round(v, 4) for k, v in ph.items()}}), flush=True)
+            continue
+        print(json.dumps({"config": f"projected N={w}, ring busBW {ge:g} GB/s (link {g:g}), "
+                                    f"{a.latency_us:g} us/collective, {c} busy CTAs per collective",
+                          "model": "busBW=min(link, ctas*cta_gbps)" if a.cta_gbps > 0 else "busBW=link",
+                          "ms_per_step": round(ms, 4), "ms_all": ms_all, "projected_img_s": round(w * 64 / ms * 1e3),
+                          "per_gpu_img_s": round(64 / ms * 1e3), "efficiency_vs_world1": round(base / ms, 4),
+                          "allreduce_wait_ms": round(ph.get("allreduce_wait", 0.0), 4),
+                          "phases_ms": {k: round(v, 4) for k, v in ph.items()}}), flush=True)
 
 
 if __name__ == "__main__":

@@ -18,6 +18,12 @@ here changes speed, not numerics. Output: one JSON object, a drop-in entry for
 runtime/tiles_gfx950.json ({"tiles": [[block, mode, bm, bn, splits, bk, stage], ...], "us": ...}).
 
     python scripts/step_tune.py --out gpurun_out/step_tune.json
+    python scripts/step_tune.py --probe xgmi:150:8:25:16 --out gpurun_out/step_tune_dp.json   # N>1 table
+
+N>1 (--probe): RCCL runs each collective as CTAs that occupy CUs while the backward GEMMs run. A
+tile whose grid is exactly one 1024-thread block per CU then needs a second wave for the blocks
+whose CU an RCCL CTA holds (the one-GPU projection saw 0.69 -> 1.02 ms per step from 16 busy
+CTAs), so the data-parallel step gets its own table, tuned with the communicator model running.
 """
 from __future__ import annotations
 
@@ -94,6 +100,9 @@ def main() -> int:
                         "--co-lds-side KiB, so a main-stream and a side-stream block fit one CU together) | "
                         "file:PATH (a previous step_tune.py output)")
     p.add_argument("--lag", type=int, default=None, help="engine set_lag(N) during the tuning (default: engine default)")
+    p.add_argument("--probe", default=None,
+                   help="tune under a one-GPU communicator model, e.g. xgmi:150:8:25:16 (N=8 ring at 150 GB/s, "
+                        "16 busy CTAs per collective: the N>1 table, runtime/tiles_gfx950.json key '.../dp')")
     p.add_argument("--co-lds-main", type=float, default=80.0)
     p.add_argument("--co-lds-side", type=float, default=75.0)
     args = p.parse_args()
@@ -102,7 +111,8 @@ def main() -> int:
     torch.cuda.set_device(0)
     native.C().reserve_streams()
     from cs744_pytorch_distributed_tutorial_amd.runtime.engine import NativeTrainer
-    tr = NativeTrainer(model=args.model, batch_size=args.batch_size, device=torch.device("cuda", 0), graph="none")
+    tr = NativeTrainer(model=args.model, batch_size=args.batch_size, device=torch.device("cuda", 0), graph="none",
+                       probe=args.probe)
     tr._dims = [(4 if l == 0 else s.cin, s.cout, s.hw) for l, s in enumerate(tr.layout.specs)]
     eng = tr.engine
     if args.lag is not None:
@@ -217,7 +227,7 @@ def main() -> int:
                 set_t((l, m), cur[(l, m)])
     ent = {"tiles": [[g[0], g[1]] + cur[g] for g in gemms], "us": us,
            "dual": [0] * tr.layout.L, "step_ms": {"start": round(base, 4), "end": round(final, 4)},
-           "history": history, "tuner": "scripts/step_tune.py", "lag": args.lag}
+           "history": history, "tuner": "scripts/step_tune.py", "lag": args.lag, "probe": args.probe}
     print(json.dumps(ent), flush=True)
     if args.out:
         with open(args.out, "w") as f:

@@ -142,12 +142,23 @@ def test_sync_modes_agree(gpu):
         torch.testing.assert_close(out[0]["params"], ref, rtol=1e-5, atol=1e-6, msg=mode)
 
 
-def _probe_run(probe, steps=6, skip=0):
+def _probe_run(probe, steps=6, skip=0, spin_us=40.0, defer=None):
     from cs744_pytorch_distributed_tutorial_amd.runtime.engine import NativeTrainer
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    tr = NativeTrainer(batch_size=32, device=dev, bucket_mb=1.0, graph="none", train_size=512, test_size=32,
-                       autotune=False, probe=probe, probe_spin_us=40.0)
+    old = os.environ.get("CS_COMM_DEFER")
+    if defer is not None:
+        os.environ["CS_COMM_DEFER"] = defer
+    try:
+        tr = NativeTrainer(batch_size=32, device=dev, bucket_mb=1.0, graph="none", train_size=512, test_size=32,
+                           autotune=False, probe=probe, probe_spin_us=spin_us)
+    finally:
+        if old is None:
+            os.environ.pop("CS_COMM_DEFER", None)
+        else:
+            os.environ["CS_COMM_DEFER"] = old
+    if defer not in (None, "none"):
+        assert tr.comm_defer, defer
     tr.engine.set_debug_skip(skip)
     for _ in range(steps):
         tr.step()
@@ -178,6 +189,27 @@ def test_probe_comm_detects_missing_join(gpu):
     bad, _ = _probe_run("order", skip=1)
     assert not torch.equal(base["params"], bad["params"])
     bad, _ = _probe_run("order", skip=2)
+    assert not torch.equal(base["params"], bad["params"])
+
+
+@pytest.mark.parametrize("defer", ["-2", "-4,-2", "0"])
+def test_probe_comm_deferred_buckets_bitwise(gpu, defer):
+    """Deferred buckets (VggEngine::set_comm_defer): their all-reduce + SGD go behind the last
+    bucket on the comm stream and the NEXT forward waits for them before their lowest block. With
+    scrambling probe collectives the steps stay bitwise equal to the world-1 run, and an evaluation
+    between steps (a host-side reader) sees the finished parameters."""
+    base, _ = _probe_run("0")
+    probed, calls = _probe_run("order", defer=defer)
+    assert calls > 6
+    for k in base:
+        assert torch.equal(base[k], probed[k]), (defer, k)
+
+
+def test_probe_comm_deferred_buckets_negative_control(gpu):
+    """Without the next forward's wait for the deferred buckets (debug bit 64; long probe
+    collectives so the forward reaches the deferred block first) the results differ."""
+    base, _ = _probe_run("0")
+    bad, _ = _probe_run("order", skip=64, spin_us=3000.0, defer="-2")
     assert not torch.equal(base["params"], bad["params"])
 
 
