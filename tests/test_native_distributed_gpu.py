@@ -97,11 +97,11 @@ def test_cpp_ddp_step_multi_rank_staged(gpu, world):
 @pytest.mark.slow
 def test_cpp_ddp_step_multi_rank_staged_bench_config(gpu):
     """The same multi-rank C++ step at the benchmark's configuration: B = 64 per rank and the
-    shipped gfx950 tile table (split-bf16 X6S conv kernels, split-K), not the small default tiles."""
+    shipped gfx950 N>1 tile table (split-bf16 X6S conv kernels, split-K), not the small default tiles."""
     steps = 4
     nat = run_world(_train, 2, "ddp", "none", steps, "staged", 64, True)
     ref = run_world(_train, 2, "ddp", "segments", steps, "torch", 64, True)
-    assert nat[0]["tiles"] == "shipped" and "x6s" in nat[0]["maths"], (nat[0]["tiles"], nat[0]["maths"])
+    assert nat[0]["tiles"] == "shipped-dp" and "x6s" in nat[0]["maths"], (nat[0]["tiles"], nat[0]["maths"])
     assert nat[0]["kind"] == "staged"
     for k in ("params", "mom", "bufs", "nbt"):
         assert torch.equal(nat[1][k], nat[0][k]), k
