@@ -192,17 +192,17 @@ def test_probe_comm_detects_missing_join(gpu):
     assert not torch.equal(base["params"], bad["params"])
 
 
-@pytest.mark.parametrize("defer", ["-2", "-4,-2", "0"])
-def test_probe_comm_deferred_buckets_bitwise(gpu, defer):
+@pytest.mark.parametrize("probe,defer", [("order", "-2"), ("order", "-4,-2"), ("order", "0"), ("1", "-2")])
+def test_probe_comm_deferred_buckets_bitwise(gpu, probe, defer):
     """Deferred buckets (VggEngine::set_comm_defer): their all-reduce + SGD go behind the last
     bucket on the comm stream and the NEXT forward waits for them before their lowest block. With
-    scrambling probe collectives the steps stay bitwise equal to the world-1 run, and an evaluation
-    between steps (a host-side reader) sees the finished parameters."""
+    scrambling probe collectives (and over a one-rank RCCL communicator) the steps stay bitwise
+    equal to the world-1 run."""
     base, _ = _probe_run("0")
-    probed, calls = _probe_run("order", defer=defer)
+    probed, calls = _probe_run(probe, defer=defer)  # "1": a one-rank RCCL communicator
     assert calls > 6
     for k in base:
-        assert torch.equal(base[k], probed[k]), (defer, k)
+        assert torch.equal(base[k], probed[k]), (probe, defer, k)
 
 
 def test_probe_comm_deferred_buckets_negative_control(gpu):
