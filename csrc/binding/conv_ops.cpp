@@ -248,6 +248,27 @@ void register_conv_ops(pybind11::module& m) {
         return dw;
       },
       "VGG block 0's weight gradient (OIHW) as the direct f32 kernels (fixed-order sum)");
+  m.def(
+      "conv0_wgrad_bn",
+      [](torch::Tensor x, torch::Tensor y, torch::Tensor G, torch::Tensor scale, torch::Tensor shift,
+         torch::Tensor mean, torch::Tensor invstd, torch::Tensor coef) {
+        TORCH_CHECK(x.dim() == 4 && x.size(1) == 32 && x.size(2) == 32 && x.size(3) == 4, "conv0_wgrad_bn: x [B,32,32,4]");
+        const int64_t B = x.size(0), pix = B * 1024;
+        check_t(x, x.numel(), "x");
+        check_t(y, pix * 64, "y");
+        check_t(G, pix / 4 * 64, "G");
+        for (auto* t : {&scale, &shift, &mean, &invstd}) check_t(*t, 64, "bn vec");
+        check_t(coef, 64 * 3, "coef");
+        DevGuard g(x.device());
+        auto part = torch::empty({(int64_t)cs_conv0_wgrad_part_floats((int)B, 32, 32)}, x.options());
+        auto dw = torch::empty({64, 3, 3, 3}, x.options());
+        CS_LAUNCH(cs_conv0_wgrad_bn(x.data_ptr<float>(), y.data_ptr<float>(), G.data_ptr<float>(),
+                                    scale.data_ptr<float>(), shift.data_ptr<float>(), mean.data_ptr<float>(),
+                                    invstd.data_ptr<float>(), coef.data_ptr<float>(), part.data_ptr<float>(),
+                                    dw.data_ptr<float>(), (int)B, 32, 32, 64, cur_stream()));
+        return dw;
+      },
+      "VGG block 0's weight gradient with its BN (+ReLU, 2x2 max-pool) backward apply folded in");
   m.def("bn_finalize", &bn_finalize);
   m.def("bn_eval_coeffs", &bn_eval_coeffs);
   m.def("bn_apply", &bn_apply);

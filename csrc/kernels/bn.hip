@@ -662,6 +662,15 @@ hipError_t cs_bn_bwd(const float* y, const float* G, int B, int H, int W, int C,
                         dbias, dz, stream);
 }
 
+hipError_t cs_bn_bwd_finalize(const float* part, int P, int C, int M, const float* gamma, const float* invstd,
+                              float* coef, float* dgamma, float* dbeta, float* dbias, hipStream_t stream,
+                              unsigned long long* signal) {
+  if (C % 4 != 0 || P < 1) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 3) / 4), dim3(256), 0, stream, part, P, C, M, gamma, invstd,
+                     dgamma, dbeta, dbias, coef, signal);
+  return hipGetLastError();
+}
+
 hipError_t cs_bn_bwd_tail(const float* y, const float* G, int B, int H, int W, int C, int pool, const float* scale,
                           const float* shift, const float* mean, const float* invstd, const float* gamma,
                           const float* part, int P, float* coef, float* dgamma, float* dbeta, float* dbias, float* dz,

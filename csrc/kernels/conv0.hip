@@ -176,6 +176,102 @@ __global__ __launch_bounds__(256) void conv0_wgrad_part_kernel(const float* __re
     part[(size_t)blockIdx.x * kCols + e] = ((red[0][e] + red[1][e]) + red[2][e]) + red[3][e];
 }
 
+// The same partial dW with block 0's BatchNorm backward folded in (dZ is never written to memory):
+// the block first turns its 128 pixels' incoming gradient into dZ in LDS — G is the gradient of
+// the 2x2-pooled output, so each unit is one pooling window x 4 channels: recompute relu(bn(y)),
+// route G to the window's first maximum (if positive), dZ = k1 (g - k2 - x_hat k3) — the very
+// expression and decisions of bn_device.h bwd_visit, so dZ has the same bits — then runs the MFMA
+// loop with the A operand read from that tile. The tile's 4 image rows are 2 pooling rows.
+constexpr int kDZP = kCo + 4;  // dZ tile pitch: lanes j read consecutive channels, k-halves 68 apart
+__global__ __launch_bounds__(256) void conv0_wgrad_bn_part_kernel(
+    const float* __restrict__ x, const float* __restrict__ y, const float* __restrict__ G,
+    const float* __restrict__ scale, const float* __restrict__ shift, const float* __restrict__ mean,
+    const float* __restrict__ invstd, const float* __restrict__ coef, float* __restrict__ part, int H) {
+  __shared__ float xs[3 * kPlane];
+  __shared__ float dzs[kPix * kDZP];  // reused as the waves' [4][64 * 27] partial tiles at the end
+  static_assert(4 * kCols <= kPix * kDZP, "partial tiles alias the dZ tile");
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int m0 = blockIdx.x * kPix;
+  const int b = m0 / (H * kW), h0 = (m0 / kW) % H;
+  const int j = lane & 31, kh = lane >> 5;
+  load_halo_planar(x, b, h0, H, xs);
+  // ---- dZ tile: 2 pooling rows x 16 windows x 16 channel quads = 512 units, 2 per thread
+  constexpr int C4 = kCo / 4, Wo = kW / 2;
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int u = tid + 256 * it;
+    const int cq = u % C4, win = u / C4, pr = win / Wo, pc = win % Wo;
+    const int ug = (b * (H / 2) + h0 / 2 + pr) * Wo + pc;  // pooled position
+    const float4 g4 = reinterpret_cast<const float4*>(G)[(size_t)ug * C4 + cq];
+    const float4 s4 = reinterpret_cast<const float4*>(scale)[cq], t4 = reinterpret_cast<const float4*>(shift)[cq];
+    const float4 mu4 = reinterpret_cast<const float4*>(mean)[cq], is4 = reinterpret_cast<const float4*>(invstd)[cq];
+    const float4 c0 = reinterpret_cast<const float4*>(coef)[3 * cq], c1 = reinterpret_cast<const float4*>(coef)[3 * cq + 1],
+                 c2 = reinterpret_cast<const float4*>(coef)[3 * cq + 2];
+    const float gin[4] = {g4.x, g4.y, g4.z, g4.w}, sc[4] = {s4.x, s4.y, s4.z, s4.w}, sh[4] = {t4.x, t4.y, t4.z, t4.w};
+    const float mu[4] = {mu4.x, mu4.y, mu4.z, mu4.w}, is[4] = {is4.x, is4.y, is4.z, is4.w};
+    const float cf[12] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w, c2.x, c2.y, c2.z, c2.w};
+    int px[4];  // tile pixels of the window in bwd_visit's order: (0,0) (0,1) (1,0) (1,1)
+#pragma unroll
+    for (int p = 0; p < 4; ++p) px[p] = (2 * pr + (p >> 1)) * kW + 2 * pc + (p & 1);
+    float yv[4][4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const float4 v = reinterpret_cast<const float4*>(y)[(size_t)(m0 + px[p]) * C4 + cq];
+      yv[p][0] = v.x; yv[p][1] = v.y; yv[p][2] = v.z; yv[p][3] = v.w;
+    }
+    float out[4][4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float z[4];
+      int am = 0;
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        z[p] = fmaxf(yv[p][q] * sc[q] + sh[q], 0.f);
+        if (p > 0 && z[p] > z[am]) am = p;
+      }
+      const float k1 = cf[3 * q], k2 = cf[3 * q + 1], k3 = cf[3 * q + 2];
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const float g = (p == am && z[p] > 0.f) ? gin[q] : 0.f;
+        const float xh = (yv[p][q] - mu[q]) * is[q];
+        out[p][q] = k1 * (g - k2 - xh * k3);
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+      *reinterpret_cast<float4*>(dzs + px[p] * kDZP + 4 * cq) = make_float4(out[p][0], out[p][1], out[p][2], out[p][3]);
+  }
+  __syncthreads();
+  // ---- A = dZ^T [channel mt * 32 + j][pixel 2s + kh of the wave's row], from the LDS tile
+  const float* dzp = dzs + (wv * kW + kh) * kDZP + j;
+  const bool col_ok = j < 27;
+  const float* xw = xs + wv * kWP + kh + (col_ok ? (j / 9) * kPlane + ((j % 9) / 3) * kWP + (j % 9) % 3 : 0);
+  f32x16 acc[2];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int g = 0; g < 16; ++g) acc[mt][g] = 0.f;
+#pragma unroll
+  for (int st = 0; st < 16; ++st) {
+    const float bv = col_ok ? xw[2 * st] : 0.f;
+    const float a0 = dzp[2 * st * kDZP], a1 = dzp[2 * st * kDZP + 32];
+    acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, bv, acc[0], 0, 0, 0);
+    acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, bv, acc[1], 0, 0, 0);
+  }
+  __syncthreads();  // every wave's dZ reads are done: the tile becomes the partial buffer
+  float* red = dzs;
+  if (col_ok) {
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int g = 0; g < 16; ++g) red[wv * kCols + (mt * 32 + (g & 3) + 8 * (g >> 2) + 4 * kh) * 27 + j] = acc[mt][g];
+  }
+  __syncthreads();
+  for (int e = tid; e < kCols; e += 256)
+    part[(size_t)blockIdx.x * kCols + e] = ((red[e] + red[kCols + e]) + red[2 * kCols + e]) + red[3 * kCols + e];
+}
+
 // dW[i] = sum over the nb partials in a fixed order: workgroup = 16 columns x 16 row slices, slice s
 // sums rows s, s + 16, ... (16 loads in flight), then the 16 slices in order
 __global__ __launch_bounds__(256) void conv0_wgrad_sum_kernel(const float* __restrict__ part, int nb,
@@ -226,6 +322,18 @@ hipError_t cs_conv0_wgrad(const float* x, const float* dz, float* part, float* d
   if (W != 32 || Cout != kCo || (H * W) % kPix != 0) return hipErrorInvalidValue;
   const int nb = (B * H * W) / kPix;
   hipLaunchKernelGGL(conv0_wgrad_part_kernel, dim3(nb), dim3(256), 0, stream, x, dz, part, H);
+  if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+  hipLaunchKernelGGL(conv0_wgrad_sum_kernel, dim3((kCols + 15) / 16), dim3(256), 0, stream, part, nb, dw);
+  return hipGetLastError();
+}
+
+hipError_t cs_conv0_wgrad_bn(const float* x, const float* y, const float* G, const float* scale, const float* shift,
+                             const float* mean, const float* invstd, const float* coef, float* part, float* dw, int B,
+                             int H, int W, int Cout, hipStream_t stream) {
+  if (W != 32 || Cout != kCo || (H * W) % kPix != 0 || H % 4 != 0) return hipErrorInvalidValue;
+  const int nb = (B * H * W) / kPix;
+  hipLaunchKernelGGL(conv0_wgrad_bn_part_kernel, dim3(nb), dim3(256), 0, stream, x, y, G, scale, shift, mean, invstd,
+                     coef, part, H);
   if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
   hipLaunchKernelGGL(conv0_wgrad_sum_kernel, dim3((kCols + 15) / 16), dim3(256), 0, stream, part, nb, dw);
   return hipGetLastError();

@@ -130,6 +130,13 @@ hipError_t cs_conv0_fwd(const float* x, const float* w, const float* bias, float
                         int W, int Cout, hipStream_t stream);
 hipError_t cs_conv0_wgrad(const float* x, const float* dz, float* part, float* dw, int B, int H, int W, int Cout,
                           hipStream_t stream);
+// the same weight gradient with block 0's BN (+ReLU, 2x2 max-pool) backward apply folded in: dZ is
+// computed in LDS from y (pre-BN conv output), G (gradient of the pooled output), the forward's
+// scale/shift/mean/invstd and the backward finalize's coef [C][3] (cs_bn_bwd_finalize) — the
+// same bits as cs_bn_bwd_tail's dZ, never written to memory
+hipError_t cs_conv0_wgrad_bn(const float* x, const float* y, const float* G, const float* scale, const float* shift,
+                             const float* mean, const float* invstd, const float* coef, float* part, float* dw, int B,
+                             int H, int W, int Cout, hipStream_t stream);
 // bm, bn in {64, 128}; bk in {16, 32}; splits >= 1 (split-K over blockIdx.z + deterministic reduce).
 // FWD stats tiles have `bm` rows when splits == 1 and CS_SPLITK_STAT_ROWS rows otherwise.
 #define CS_SPLITK_STAT_ROWS 16
@@ -194,6 +201,11 @@ hipError_t cs_bn_bwd_tail(const float* y, const float* G, int B, int H, int W, i
                           const float* shift, const float* mean, const float* invstd, const float* gamma,
                           const float* part, int P, float* coef, float* dgamma, float* dbeta, float* dbias, float* dz,
                           hipStream_t stream, unsigned long long* signal = nullptr);
+// the finalize half of cs_bn_bwd_tail alone (coef, dgamma / dbeta / dbias), for a consumer that
+// applies the backward itself (cs_conv0_wgrad_bn)
+hipError_t cs_bn_bwd_finalize(const float* part, int P, int C, int M, const float* gamma, const float* invstd,
+                              float* coef, float* dgamma, float* dbeta, float* dbias, hipStream_t stream,
+                              unsigned long long* signal = nullptr);
 hipError_t cs_bn_bwd(const float* y, const float* G, int B, int H, int W, int C, int pool, const float* scale,
                      const float* shift, const float* mean, const float* invstd, const float* gamma, float* part,
                      float* coef, float* dgamma, float* dbeta, float* dbias, float* dz, hipStream_t stream);

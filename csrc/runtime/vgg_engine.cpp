@@ -204,6 +204,7 @@ VggEngine::VggEngine(int64_t Bmax, std::vector<int64_t> desc, std::vector<int64_
   if (const char* e = getenv("CS_WGRAD_STAGGER")) stagger_ = atoi(e) != 0;
   if (const char* e = getenv("CS_WGRAD_LAG")) set_lag(atoi(e));
   if (const char* e = getenv("CS_CONV0_DIRECT")) conv0_direct_ = atoi(e) != 0;
+  if (const char* e = getenv("CS_CONV0_BN_FOLD")) conv0_bn_fold_ = atoi(e) != 0;
   if (const char* e = getenv("CS_BN_BWD_FUSED_P")) bwd_fused_p_ = atoi(e);
   bn_part_ = torch::zeros({partmax}, fo);
   bn_coef_ = torch::zeros({cmax * 3}, fo);
@@ -511,6 +512,15 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
     // l+1's fork rides its first launch)
     if (debug_skip_ & 16) {
       flush_signal(s);
+    } else if (red_pending_ == l && l == 0 && !fin_on_ && conv0_bn_fold_ && b.pool && conv0_direct_ok(B) &&
+               !(red_P_ <= bwd_fused_p_ && b.cout % 16 == 0)) {
+      // block 0: only the finalize here; the apply runs inside the weight gradient (conv0_wgrad)
+      ok(cs_bn_bwd_finalize(bn_part_.data_ptr<float>(), red_P_, b.cout, (int)(B * b.H * b.H), P(b.g_off),
+                            bn + 3 * b.cout, bn_coef_.data_ptr<float>(), G(b.g_off), G(b.be_off), G(b.b_off), s,
+                            pending_sig_),
+         "bn_bwd_finalize");
+      pending_sig_ = nullptr;
+      conv0_bn_G_ = Gin;
     } else if (red_pending_ == l) {
       // the partial sums (and, with fin, the finalize) ran inside block l+1's data-gradient launch
       if (fin_on_)
@@ -648,6 +658,16 @@ void VggEngine::conv0_wgrad(int64_t B, hipStream_t s, float* dz) {
   if (start_sig_ != nullptr) {  // the deferred fork signal this launch would have carried
     ok(cs_link_signal(start_sig_, s), "link signal");
     start_sig_ = nullptr;
+  }
+  if (conv0_bn_G_ != nullptr) {  // block 0's BN-backward apply folded in (dz is not written)
+    const float* bn = b.bn.data_ptr<float>();
+    const float* Gin = conv0_bn_G_;
+    conv0_bn_G_ = nullptr;
+    ok(cs_conv0_wgrad_bn(b.x.data_ptr<float>(), b.y.data_ptr<float>(), Gin, bn, bn + b.cout, bn + 2 * b.cout,
+                         bn + 3 * b.cout, bn_coef_.data_ptr<float>(), ws_.data_ptr<float>(), G(b.w_off), (int)B, b.H,
+                         b.H, b.cout, s),
+       "conv0_wgrad_bn");
+    return;
   }
   ok(cs_conv0_wgrad(b.x.data_ptr<float>(), dz, ws_.data_ptr<float>(), G(b.w_off), (int)B, b.H, b.H, b.cout, s),
      "conv0_wgrad");

@@ -111,6 +111,9 @@ class VggEngine {
   // block 0's convolution (3 -> 64) as the direct conv0.hip kernels instead of the implicit GEMM
   // (forward + BN tile statistics, weight gradient); CS_CONV0_DIRECT=0 restores the GEMM
   void set_conv0_direct(bool on) { conv0_direct_ = on; }
+  // with the direct kernels, block 0's BN-backward apply folded into its weight gradient (dZ of
+  // block 0 never written; CS_CONV0_BN_FOLD=0 keeps the separate apply launch)
+  void set_conv0_bn_fold(bool on) { conv0_bn_fold_ = on; }
   bool conv0_direct(int64_t B) const { return conv0_direct_ok(B); }
   // Deferred weight gradients (world 1, overlapped step): the top `n` blocks' weight gradients and
   // SGD run on a lag stream that starts at the end of the step and overlaps the NEXT step's forward
@@ -250,6 +253,10 @@ class VggEngine {
   bool conv0_direct_ = true;
   bool conv0_direct_ok(int64_t B) const;
   void conv0_wgrad(int64_t B, hipStream_t s, float* dz);
+  // block 0's BN-backward apply runs inside its weight gradient (cs_conv0_wgrad_bn): set by the BN
+  // step of block 0 (only its finalize launched), consumed by conv0_wgrad
+  const float* conv0_bn_G_ = nullptr;
+  bool conv0_bn_fold_ = true;
   hipStream_t lag_ = nullptr;
   std::unique_ptr<StreamLink> lag_in_, lag_out_;  // main -> lag (step end), lag -> main (deferred work done)
   std::vector<int> lag_list_;                      // blocks whose weight gradient this step defers

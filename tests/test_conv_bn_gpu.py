@@ -339,3 +339,29 @@ def test_conv0_direct_kernels_match_fp64(dev, B):
     assert ((dw - dwr).abs().max() / dwr.abs().max()) < 2e-5
     # deterministic: the fixed-order sum gives the same bits run to run
     assert torch.equal(C.conv0_wgrad(x.to(dev), dz.to(dev)).cpu(), dw.float())
+
+
+@pytest.mark.parametrize("B", [1, 64])
+def test_conv0_wgrad_bn_fold_bitwise(dev, B):
+    """Block 0's weight gradient with its BN (+ReLU, 2x2 max-pool) backward apply folded in
+    (`conv0_wgrad_bn`: dZ computed in LDS, never written) equals the separate BN backward
+    (`bn_bwd`: reduce + finalize + apply -> dZ) followed by `conv0_wgrad`, bit for bit."""
+    from cs744_pytorch_distributed_tutorial_amd.ops import native
+    C = native.C()
+    g = torch.Generator().manual_seed(100 + B)
+    x = torch.randn(B, 32, 32, 4, generator=g).to(dev)
+    y = torch.randn(B * 1024, 64, generator=g).to(dev)
+    G = torch.randn(B * 256, 64, generator=g).to(dev)
+    gamma = (torch.rand(64, generator=g) + 0.5).to(dev)
+    mean = (0.1 * torch.randn(64, generator=g)).to(dev)
+    invstd = (torch.rand(64, generator=g) + 0.5).to(dev)
+    scale = gamma * invstd
+    shift = (0.2 * torch.randn(64, generator=g)).to(dev) - mean * scale
+    part = torch.empty(C.bn_bwd_blocks(B, 32, 32, 64, True) * 64 * 3, device=dev)
+    coef = torch.empty(64 * 3, device=dev)
+    dz = torch.empty(B * 1024, 64, device=dev)
+    C.bn_bwd(y, G, B, 32, 32, 64, True, scale, shift, mean, invstd, gamma, part, coef, None, None, None, dz)
+    ref = C.conv0_wgrad(x, dz)
+    fold = C.conv0_wgrad_bn(x, y, G, scale, shift, mean, invstd, coef)
+    assert torch.equal(fold, ref), (fold - ref).abs().max()
+    assert float(ref.abs().max()) > 0
