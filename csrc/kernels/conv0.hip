@@ -21,6 +21,7 @@
 //    partials summed in a fixed order -> dW.
 #include "common.h"
 #include "launchers.h"
+#include "sgd_device.h"
 
 namespace {
 
@@ -273,9 +274,26 @@ __global__ __launch_bounds__(256) void conv0_wgrad_bn_part_kernel(
 }
 
 // dW[i] = sum over the nb partials in a fixed order: workgroup = 16 columns x 16 row slices, slice s
-// sums rows s, s + 16, ... (16 loads in flight), then the 16 slices in order
+// sums rows s, s + 16, ... (16 loads in flight), then the 16 slices in order. With an SGD range
+// (sgd.n > 0: block 0's parameters, dW at w_rel within it) each finished column also takes its
+// SGD step here, and one extra workgroup updates the range's other parameters (their gradients
+// are final) and bumps the batch cursor: the step's last separate optimizer launch disappears
+// (the same cs_sgd::step1 on the same values as the flat pass: bit-equal)
 __global__ __launch_bounds__(256) void conv0_wgrad_sum_kernel(const float* __restrict__ part, int nb,
-                                                             float* __restrict__ dw) {
+                                                             float* __restrict__ dw, CsSgdTail sgd, int w_rel,
+                                                             int64_t* __restrict__ counter) {
+  constexpr int NCB = (kCols + 15) / 16;  // column workgroups
+  if ((int)blockIdx.x == NCB) {           // the range's other parameters + the cursor
+    if (counter != nullptr && threadIdx.x == 0) *counter += 1;
+    for (int64_t i = threadIdx.x; i < sgd.n; i += 256) {
+      if (i >= w_rel && i < w_rel + kCols) continue;
+      float pv = sgd.p[i], mv = sgd.first ? 0.f : sgd.m[i];
+      cs_sgd::step1(pv, sgd.g[i], mv, sgd.lr, sgd.mom, sgd.wd, sgd.damp, 1.0f, sgd.first);
+      sgd.p[i] = pv;
+      if (sgd.mom != 0.f) sgd.m[i] = mv;
+    }
+    return;
+  }
   __shared__ float red[16][16];
   const int cl = threadIdx.x & 15, sl = threadIdx.x >> 4;
   const int col = blockIdx.x * 16 + cl;
@@ -299,6 +317,13 @@ __global__ __launch_bounds__(256) void conv0_wgrad_sum_kernel(const float* __res
 #pragma unroll
     for (int j = 0; j < 16; ++j) t += red[j][cl];
     dw[col] = t;
+    if (sgd.n > 0) {
+      const int64_t i = w_rel + col;
+      float pv = sgd.p[i], mv = sgd.first ? 0.f : sgd.m[i];
+      cs_sgd::step1(pv, t, mv, sgd.lr, sgd.mom, sgd.wd, sgd.damp, 1.0f, sgd.first);
+      sgd.p[i] = pv;
+      if (sgd.mom != 0.f) sgd.m[i] = mv;
+    }
   }
 }
 
@@ -317,24 +342,36 @@ hipError_t cs_conv0_fwd(const float* x, const float* w, const float* bias, float
   return hipGetLastError();
 }
 
+static hipError_t conv0_sum(const float* part, int nb, float* dw, const CsSgdTail* sgd, int w_rel,
+                            int64_t* counter, hipStream_t stream) {
+  CsSgdTail t{};
+  if (sgd != nullptr) {
+    if (sgd->n < w_rel + kCols || w_rel < 0) return hipErrorInvalidValue;
+    t = *sgd;
+  }
+  const int ncb = (kCols + 15) / 16;
+  hipLaunchKernelGGL(conv0_wgrad_sum_kernel, dim3(ncb + (t.n > 0 ? 1 : 0)), dim3(256), 0, stream, part, nb, dw, t,
+                     w_rel, t.n > 0 ? counter : nullptr);
+  return hipGetLastError();
+}
+
 hipError_t cs_conv0_wgrad(const float* x, const float* dz, float* part, float* dw, int B, int H, int W, int Cout,
-                          hipStream_t stream) {
+                          hipStream_t stream, const CsSgdTail* sgd, int w_rel, int64_t* counter) {
   if (W != 32 || Cout != kCo || (H * W) % kPix != 0) return hipErrorInvalidValue;
   const int nb = (B * H * W) / kPix;
   hipLaunchKernelGGL(conv0_wgrad_part_kernel, dim3(nb), dim3(256), 0, stream, x, dz, part, H);
   if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
-  hipLaunchKernelGGL(conv0_wgrad_sum_kernel, dim3((kCols + 15) / 16), dim3(256), 0, stream, part, nb, dw);
-  return hipGetLastError();
+  return conv0_sum(part, nb, dw, sgd, w_rel, counter, stream);
 }
 
 hipError_t cs_conv0_wgrad_bn(const float* x, const float* y, const float* G, const float* scale, const float* shift,
                              const float* mean, const float* invstd, const float* coef, float* part, float* dw, int B,
-                             int H, int W, int Cout, hipStream_t stream) {
+                             int H, int W, int Cout, hipStream_t stream, const CsSgdTail* sgd, int w_rel,
+                             int64_t* counter) {
   if (W != 32 || Cout != kCo || (H * W) % kPix != 0 || H % 4 != 0) return hipErrorInvalidValue;
   const int nb = (B * H * W) / kPix;
   hipLaunchKernelGGL(conv0_wgrad_bn_part_kernel, dim3(nb), dim3(256), 0, stream, x, y, G, scale, shift, mean, invstd,
                      coef, part, H);
   if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
-  hipLaunchKernelGGL(conv0_wgrad_sum_kernel, dim3((kCols + 15) / 16), dim3(256), 0, stream, part, nb, dw);
-  return hipGetLastError();
+  return conv0_sum(part, nb, dw, sgd, w_rel, counter, stream);
 }

@@ -128,15 +128,19 @@ int cs_conv0_tile_rows();
 size_t cs_conv0_wgrad_part_floats(int B, int H, int W);
 hipError_t cs_conv0_fwd(const float* x, const float* w, const float* bias, float* y, float* stats, int B, int H,
                         int W, int Cout, hipStream_t stream);
+// sgd (optional): block 0's parameter range, whose SGD step then rides the fixed-order sum (dW at
+// w_rel within the range; the range's other gradients must be final; counter: the batch cursor)
 hipError_t cs_conv0_wgrad(const float* x, const float* dz, float* part, float* dw, int B, int H, int W, int Cout,
-                          hipStream_t stream);
+                          hipStream_t stream, const CsSgdTail* sgd = nullptr, int w_rel = 0,
+                          int64_t* counter = nullptr);
 // the same weight gradient with block 0's BN (+ReLU, 2x2 max-pool) backward apply folded in: dZ is
 // computed in LDS from y (pre-BN conv output), G (gradient of the pooled output), the forward's
 // scale/shift/mean/invstd and the backward finalize's coef [C][3] (cs_bn_bwd_finalize) — the
 // same bits as cs_bn_bwd_tail's dZ, never written to memory
 hipError_t cs_conv0_wgrad_bn(const float* x, const float* y, const float* G, const float* scale, const float* shift,
                              const float* mean, const float* invstd, const float* coef, float* part, float* dw, int B,
-                             int H, int W, int Cout, hipStream_t stream);
+                             int H, int W, int Cout, hipStream_t stream, const CsSgdTail* sgd = nullptr,
+                             int w_rel = 0, int64_t* counter = nullptr);
 // bm, bn in {64, 128}; bk in {16, 32}; splits >= 1 (split-K over blockIdx.z + deterministic reduce).
 // FWD stats tiles have `bm` rows when splits == 1 and CS_SPLITK_STAT_ROWS rows otherwise.
 #define CS_SPLITK_STAT_ROWS 16

@@ -205,6 +205,7 @@ VggEngine::VggEngine(int64_t Bmax, std::vector<int64_t> desc, std::vector<int64_
   if (const char* e = getenv("CS_WGRAD_LAG")) set_lag(atoi(e));
   if (const char* e = getenv("CS_CONV0_DIRECT")) conv0_direct_ = atoi(e) != 0;
   if (const char* e = getenv("CS_CONV0_BN_FOLD")) conv0_bn_fold_ = atoi(e) != 0;
+  if (const char* e = getenv("CS_CONV0_SGD_FOLD")) conv0_sgd_fold_ = atoi(e) != 0;
   if (const char* e = getenv("CS_BN_BWD_FUSED_P")) bwd_fused_p_ = atoi(e);
   bn_part_ = torch::zeros({partmax}, fo);
   bn_coef_ = torch::zeros({cmax * 3}, fo);
@@ -588,9 +589,9 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
         // block 0's weight gradient is the step's last GEMM: nothing left to overlap it with, so it
         // runs here (the main split-K workspace is free: no data gradient for block 0)
         if (side_pending_ >= 0) start_sig_ = dz_link_->defer();
-        conv0_wgrad(B, s, dz);
+        const bool sgd_done = conv0_wgrad(B, s, dz, bwd_sgd_);
         if (side_pending_ >= 0) fork_wgrad(side_pending_, B, false);
-        if (bwd_sgd_) sgd_on(s, blk_range_[0].first, blk_range_[0].second, true);
+        if (bwd_sgd_ && !sgd_done) sgd_on(s, blk_range_[0].first, blk_range_[0].second, true);
       }
     } else if (dual_ok(l)) {  // wgrad + dgrad in one launch (no appended SGD blocks: the update runs first)
       if (sgd_tail_ && l + 1 < L) sgd_on(s, blk_range_[l + 1].first, blk_range_[l + 1].second, false);
@@ -649,12 +650,22 @@ bool VggEngine::conv0_direct_ok(int64_t B) const {
          cs_conv0_wgrad_part_floats((int)B, b.H, b.H) <= (size_t)ws_elems_;
 }
 
-void VggEngine::conv0_wgrad(int64_t B, hipStream_t s, float* dz) {
+bool VggEngine::conv0_wgrad(int64_t B, hipStream_t s, float* dz, bool with_sgd) {
   VggBlock& b = blocks_[0];
   if (!conv0_direct_ok(B)) {
     conv(0, CS_CONV_WGRAD, (int)B, b.tile[CS_CONV_WGRAD], s, false, ws_.data_ptr<float>(), dz);
-    return;
+    return false;
   }
+  CsSgdTail sgd{};
+  int w_rel = 0;
+  int64_t* counter = nullptr;
+  if (with_sgd && conv0_sgd_fold_ && !blk_range_.empty()) {
+    sgd = sgd_tail_args(0);
+    w_rel = (int)(b.w_off - blk_range_[0].first);
+    if (w_rel < 0 || w_rel + 27 * b.cout > sgd.n) sgd.n = 0;
+    counter = perm_len_ > 0 ? cursor_.data_ptr<int64_t>() : nullptr;
+  }
+  const CsSgdTail* sp = sgd.n > 0 ? &sgd : nullptr;
   if (start_sig_ != nullptr) {  // the deferred fork signal this launch would have carried
     ok(cs_link_signal(start_sig_, s), "link signal");
     start_sig_ = nullptr;
@@ -665,12 +676,14 @@ void VggEngine::conv0_wgrad(int64_t B, hipStream_t s, float* dz) {
     conv0_bn_G_ = nullptr;
     ok(cs_conv0_wgrad_bn(b.x.data_ptr<float>(), b.y.data_ptr<float>(), Gin, bn, bn + b.cout, bn + 2 * b.cout,
                          bn + 3 * b.cout, bn_coef_.data_ptr<float>(), ws_.data_ptr<float>(), G(b.w_off), (int)B, b.H,
-                         b.H, b.cout, s),
+                         b.H, b.cout, s, sp, w_rel, counter),
        "conv0_wgrad_bn");
-    return;
+    return sp != nullptr;
   }
-  ok(cs_conv0_wgrad(b.x.data_ptr<float>(), dz, ws_.data_ptr<float>(), G(b.w_off), (int)B, b.H, b.H, b.cout, s),
+  ok(cs_conv0_wgrad(b.x.data_ptr<float>(), dz, ws_.data_ptr<float>(), G(b.w_off), (int)B, b.H, b.H, b.cout, s, sp,
+                    w_rel, counter),
      "conv0_wgrad");
+  return sp != nullptr;
 }
 
 bool VggEngine::lag_on(hipStream_t s) const {

@@ -114,6 +114,9 @@ class VggEngine {
   // with the direct kernels, block 0's BN-backward apply folded into its weight gradient (dZ of
   // block 0 never written; CS_CONV0_BN_FOLD=0 keeps the separate apply launch)
   void set_conv0_bn_fold(bool on) { conv0_bn_fold_ = on; }
+  // ... and block 0's SGD step (+ batch cursor) into the weight gradient's final sum (world 1,
+  // overlapped backward; CS_CONV0_SGD_FOLD=0 keeps the separate optimizer launch)
+  void set_conv0_sgd_fold(bool on) { conv0_sgd_fold_ = on; }
   bool conv0_direct(int64_t B) const { return conv0_direct_ok(B); }
   // Deferred weight gradients (world 1, overlapped step): the top `n` blocks' weight gradients and
   // SGD run on a lag stream that starts at the end of the step and overlaps the NEXT step's forward
@@ -252,11 +255,14 @@ class VggEngine {
   int lag_blocks_ = 0;
   bool conv0_direct_ = true;
   bool conv0_direct_ok(int64_t B) const;
-  void conv0_wgrad(int64_t B, hipStream_t s, float* dz);
+  // with_sgd: block 0's SGD step (+ the batch cursor) rides the weight gradient's final sum when the
+  // direct kernels run; returns whether it did (else the caller launches the SGD)
+  bool conv0_wgrad(int64_t B, hipStream_t s, float* dz, bool with_sgd = false);
   // block 0's BN-backward apply runs inside its weight gradient (cs_conv0_wgrad_bn): set by the BN
   // step of block 0 (only its finalize launched), consumed by conv0_wgrad
   const float* conv0_bn_G_ = nullptr;
   bool conv0_bn_fold_ = true;
+  bool conv0_sgd_fold_ = true;
   hipStream_t lag_ = nullptr;
   std::unique_ptr<StreamLink> lag_in_, lag_out_;  // main -> lag (step end), lag -> main (deferred work done)
   std::vector<int> lag_list_;                      // blocks whose weight gradient this step defers
