@@ -47,12 +47,47 @@ __device__ __forceinline__ void load_halo_planar(const float* __restrict__ x, in
   }
 }
 
+// the same halo computed from the uint8 training images (make_batch's arithmetic: crop offsets and
+// flip of the sample, (v / 255 - mean) / std), writing the tile's own rows to the block-0 input
+__device__ __forceinline__ void load_halo_batch(const CsBatchSrc& src, int b, int h0, int H, int m0, float* xs) {
+  const int64_t smp = src.perm != nullptr ? src.perm[*src.cursor * src.stride + b] : src.idx_in[b];
+  if (m0 % (H * kW) == 0 && threadIdx.x == 0) {
+    src.idx_out[b] = smp;
+    src.ylab[b] = src.labels[smp];
+  }
+  const int dy = src.params[smp * 3 + 0], dx = src.params[smp * 3 + 1], fl = src.params[smp * 3 + 2];
+  for (int i = threadIdx.x; i < kPlane; i += blockDim.x) {
+    const int r = i / kWP, c = i - r * kWP;
+    const int h = h0 - 1 + r, w = c - 1;
+    float v[3] = {0.f, 0.f, 0.f};
+    if ((unsigned)h < (unsigned)H && (unsigned)w < (unsigned)kW) {
+      const int sx = fl ? (31 - w) : w;
+      const int py = h + dy - 4, px = sx + dx - 4;
+      float u[3] = {0.f, 0.f, 0.f};
+      if (py >= 0 && py < 32 && px >= 0 && px < 32) {
+        const uint8_t* p = src.data + ((smp * 32 + py) * 32 + px) * 3;
+        u[0] = p[0];
+        u[1] = p[1];
+        u[2] = p[2];
+      }
+#pragma unroll
+      for (int ci = 0; ci < 3; ++ci) v[ci] = (u[ci] / 255.0f - src.m[ci]) * src.inv[ci];
+      if (r >= 1 && r <= kRows)
+        *reinterpret_cast<float4*>(src.x_out + (((size_t)b * H + h) * kW + w) * 4) = make_float4(v[0], v[1], v[2], 0.f);
+    }
+    xs[i] = v[0];
+    xs[kPlane + i] = v[1];
+    xs[2 * kPlane + i] = v[2];
+  }
+}
+
 // halo offset of column k = ci * 9 + tap of the (row 0, column 0) pixel's window
 __host__ __device__ constexpr int win_off(int k) { return (k / 9) * kPlane + ((k % 9) / 3) * kWP + (k % 9) % 3; }
 
+template <bool BATCH>
 __global__ __launch_bounds__(256) void conv0_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                         const float* __restrict__ bias, float* __restrict__ y,
-                                                        float* __restrict__ stats, int H) {
+                                                        float* __restrict__ stats, int H, CsBatchSrc src) {
   __shared__ float xs[3 * kPlane];
   __shared__ float red[4][kCo];
   __shared__ float mean_sh[kCo];
@@ -77,7 +112,10 @@ __global__ __launch_bounds__(256) void conv0_fwd_kernel(const float* __restrict_
 #pragma unroll
     for (int g = 0; g < 16; ++g) acc[nt][g] = bv;
   }
-  load_halo_planar(x, b, h0, H, xs);
+  if constexpr (BATCH)
+    load_halo_batch(src, b, h0, H, m0, xs);
+  else
+    load_halo_planar(x, b, h0, H, xs);
   __syncthreads();
   // A = windows [pixel j of image row wv][k]
   const float* xw = xs + wv * kWP + j;
@@ -336,9 +374,18 @@ size_t cs_conv0_wgrad_part_floats(int B, int H, int W) {
 }
 
 hipError_t cs_conv0_fwd(const float* x, const float* w, const float* bias, float* y, float* stats, int B, int H,
-                        int W, int Cout, hipStream_t stream) {
+                        int W, int Cout, hipStream_t stream, const CsBatchSrc* batch) {
   if (W != 32 || Cout != kCo || (H * W) % kPix != 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(conv0_fwd_kernel, dim3((B * H * W) / kPix), dim3(256), 0, stream, x, w, bias, y, stats, H);
+  if (batch != nullptr) {
+    if (H != 32 || (batch->perm == nullptr) == (batch->idx_in == nullptr) ||
+        (batch->perm != nullptr && batch->cursor == nullptr))
+      return hipErrorInvalidValue;
+    hipLaunchKernelGGL(conv0_fwd_kernel<true>, dim3((B * H * W) / kPix), dim3(256), 0, stream, nullptr, w, bias, y,
+                       stats, H, *batch);
+  } else {
+    hipLaunchKernelGGL(conv0_fwd_kernel<false>, dim3((B * H * W) / kPix), dim3(256), 0, stream, x, w, bias, y, stats,
+                       H, CsBatchSrc{});
+  }
   return hipGetLastError();
 }
 

@@ -124,10 +124,27 @@ void cs_conv_fill_dims(CsConvArgs* a, int mode);
 // f32 kernels (conv0.hip). fwd: y [pix][64] (+bias) and, when stats != null, the BatchNorm tile
 // statistics [pix / cs_conv0_tile_rows()][64][2] = (mean, M2); wgrad: dW (OIHW [64][27]) through
 // `part` scratch of cs_conv0_wgrad_part_floats() floats (fixed-order sum: deterministic)
+// the training batch itself (augment.hip make_batch's job) as conv0's input source: sample index
+// (device cursor into the permutation, or idx_in), label gather, RandomCrop(32, 4) + HFlip +
+// Normalize of the uint8 images straight into the conv's LDS halo; the block-0 input x_out
+// (for the weight gradient) is written as make_batch writes it
+struct CsBatchSrc {
+  const uint8_t* data;
+  const int64_t* labels;
+  const int64_t* perm;
+  const int64_t* cursor;
+  int stride;
+  const int64_t* idx_in;
+  const int32_t* params;
+  float* x_out;
+  int64_t* idx_out;
+  int64_t* ylab;
+  float m[3], inv[3];
+};
 int cs_conv0_tile_rows();
 size_t cs_conv0_wgrad_part_floats(int B, int H, int W);
 hipError_t cs_conv0_fwd(const float* x, const float* w, const float* bias, float* y, float* stats, int B, int H,
-                        int W, int Cout, hipStream_t stream);
+                        int W, int Cout, hipStream_t stream, const CsBatchSrc* batch = nullptr);
 // sgd (optional): block 0's parameter range, whose SGD step then rides the fixed-order sum (dW at
 // w_rel within the range; the range's other gradients must be final; counter: the batch cursor)
 hipError_t cs_conv0_wgrad(const float* x, const float* dz, float* part, float* dw, int B, int H, int W, int Cout,

@@ -206,6 +206,7 @@ VggEngine::VggEngine(int64_t Bmax, std::vector<int64_t> desc, std::vector<int64_
   if (const char* e = getenv("CS_CONV0_DIRECT")) conv0_direct_ = atoi(e) != 0;
   if (const char* e = getenv("CS_CONV0_BN_FOLD")) conv0_bn_fold_ = atoi(e) != 0;
   if (const char* e = getenv("CS_CONV0_SGD_FOLD")) conv0_sgd_fold_ = atoi(e) != 0;
+  if (const char* e = getenv("CS_CONV0_BATCH_FOLD")) conv0_batch_fold_ = atoi(e) != 0;
   if (const char* e = getenv("CS_BN_BWD_FUSED_P")) bwd_fused_p_ = atoi(e);
   bn_part_ = torch::zeros({partmax}, fo);
   bn_coef_ = torch::zeros({cmax * 3}, fo);
@@ -418,12 +419,21 @@ void VggEngine::forward_train(int64_t B) {
   // one launch: sampler index (device cursor into the epoch permutation, or idx_ when no
   // permutation is set), label gather, crop/flip/normalize into block 0's NHWC input
   const bool use_perm = perm_len_ > 0;
-  ok(cs_make_batch(data_[0].data_ptr<uint8_t>(), labels_[0].data_ptr<int64_t>(),
-                   use_perm ? perm_.data_ptr<int64_t>() : nullptr, use_perm ? cursor_.data_ptr<int64_t>() : nullptr,
-                   (int)Bmax_, use_perm ? nullptr : idx_.data_ptr<int64_t>(), aug_[0].data_ptr<int32_t>(),
-                   blocks_[0].x.data_ptr<float>(), idx_.data_ptr<int64_t>(), ylab_.data_ptr<int64_t>(), (int)B, kMean,
-                   kStd, s),
-     "make_batch");
+  // with the direct block-0 kernels the batch is built inside conv0's forward (one launch fewer at
+  // the head of the chain; CS_CONV0_BATCH_FOLD=0 keeps make_batch)
+  const bool batch_fold = conv0_batch_fold_ && conv0_direct_ok(B) && !(debug_skip_ & 8);
+  CsBatchSrc bsrc{data_[0].data_ptr<uint8_t>(), labels_[0].data_ptr<int64_t>(),
+                  use_perm ? perm_.data_ptr<int64_t>() : nullptr, use_perm ? cursor_.data_ptr<int64_t>() : nullptr,
+                  (int)Bmax_, use_perm ? nullptr : idx_.data_ptr<int64_t>(), aug_[0].data_ptr<int32_t>(),
+                  blocks_[0].x.data_ptr<float>(), idx_.data_ptr<int64_t>(), ylab_.data_ptr<int64_t>(),
+                  {kMean[0], kMean[1], kMean[2]}, {1.0f / kStd[0], 1.0f / kStd[1], 1.0f / kStd[2]}};
+  if (!batch_fold)
+    ok(cs_make_batch(data_[0].data_ptr<uint8_t>(), labels_[0].data_ptr<int64_t>(),
+                     use_perm ? perm_.data_ptr<int64_t>() : nullptr, use_perm ? cursor_.data_ptr<int64_t>() : nullptr,
+                     (int)Bmax_, use_perm ? nullptr : idx_.data_ptr<int64_t>(), aug_[0].data_ptr<int32_t>(),
+                     blocks_[0].x.data_ptr<float>(), idx_.data_ptr<int64_t>(), ylab_.data_ptr<int64_t>(), (int)B,
+                     kMean, kStd, s),
+       "make_batch");
   float* bufs = bufs_.data_ptr<float>();
   for (int l = 0; l < L; ++l) {
     VggBlock& b = blocks_[l];
@@ -440,7 +450,7 @@ void VggEngine::forward_train(int64_t B) {
       int rows;
       if (l == 0 && conv0_direct_ok(B)) {
         ok(cs_conv0_fwd(b.x.data_ptr<float>(), P(b.w_off), P(b.b_off), b.y.data_ptr<float>(), b.stats.data_ptr<float>(),
-                        (int)B, b.H, b.H, b.cout, s),
+                        (int)B, b.H, b.H, b.cout, s, batch_fold ? &bsrc : nullptr),
            "conv0_fwd");
         rows = cs_conv0_tile_rows();
       } else {

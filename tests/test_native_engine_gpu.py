@@ -546,3 +546,28 @@ def test_side_stream_link_error_surfaces(dev):
     finally:
         native.C().reset_link_abort()
         t.close()
+
+
+def test_conv0_folds_bitwise(dev):
+    """Block 0's folds — the training batch built inside conv0's forward (no make_batch launch),
+    its BN-backward apply inside the weight gradient, its SGD step + batch cursor inside the
+    weight gradient's final sum — each change launches, not bits: every on/off combination trains
+    to the same parameters, momentum, buffers, cursor, labels and loss as all of them off."""
+    combos = [(0, 0, 0), (1, 1, 1), (1, 0, 0), (0, 1, 0), (0, 0, 1)]
+    runs = []
+    for batch, bn, sgd in combos:
+        t = _trainer(dev, batch_size=64, train_size=512)
+        assert t.engine.conv0_direct(64)
+        t.engine.set_conv0_batch_fold(bool(batch))
+        t.engine.set_conv0_bn_fold(bool(bn))
+        t.engine.set_conv0_sgd_fold(bool(sgd))
+        for _ in range(4):
+            t.step()
+        torch.cuda.synchronize()
+        t.check_comm()
+        runs.append((t.params.clone(), t.mom.clone(), t.bufs.clone(), t.engine.cursor().clone(),
+                     torch.tensor([t.last_loss()])))
+        t.close()
+    for combo, r in zip(combos[1:], runs[1:]):
+        for k, (a, b) in enumerate(zip(runs[0], r)):
+            assert torch.equal(a.cpu(), b.cpu()), (combo, k)
