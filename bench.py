@@ -44,6 +44,10 @@ from cs744_pytorch_distributed_tutorial_amd import distributed as D  # noqa: E40
 
 # best reference configuration (part3 DDP, N=4, local CPU repro) = 554 img/s.
 BASELINE_IMG_S = 554.0
+# The same-chip comparator: stock PyTorch-ROCm (MIOpen convolutions, ATen BN/ReLU/pool, torch.optim
+# SGD) on one MI355X, VGG-11 fp32, 64 images per GPU — `bench.py --engine torch`, measured in round 5
+# (profiles/r5_extras.jsonl: 29,893 img/s, 2.141 ms/step). Reported as vs_stock_torch_per_gpu.
+STOCK_TORCH_IMG_S_PER_GPU = 29893.0
 
 
 def parse(argv=None):
@@ -332,6 +336,8 @@ def main(argv=None) -> int:
     }
     if busbw is not None:
         out["busbw_GBps"] = busbw
+    if is_vgg(args.model) and args.model.upper() == "VGG11" and args.batch_size == 64 and args.dtype == "fp32":
+        out["vs_stock_torch_per_gpu"] = round(value / world / STOCK_TORCH_IMG_S_PER_GPU, 3)
     if getattr(trainer, "queue_shared", None) is not None:
         out["config"]["hw_queue_shared"] = trainer.queue_shared
     if hasattr(trainer, "tile_table"):
