@@ -38,10 +38,10 @@ _pkg.ensure_hw_queues()
 import torch  # noqa: E402
 
 
-def run(probe, steps, warmup, B=64):
+def run(probe, steps, warmup, B=64, bucket_mb=4.0):
     from cs744_pytorch_distributed_tutorial_amd.runtime.engine import NativeTrainer
     dev = torch.device("cuda", 0)
-    tr = NativeTrainer(batch_size=B, device=dev, probe=probe, graph="none")
+    tr = NativeTrainer(batch_size=B, device=dev, probe=probe, graph="none", bucket_mb=bucket_mb)
     for _ in range(warmup):
         tr.step()
     torch.cuda.synchronize()
@@ -70,6 +70,7 @@ def main():
     p.add_argument("--cta-gbps", type=float, default=0.0,
                    help="> 0: per-CTA channel bandwidth (GB/s); busBW = min(G, ctas * this) (a model)")
     p.add_argument("--repeats", type=int, default=3)
+    p.add_argument("--bucket-mb", type=float, default=4.0, help="DDP bucket cap (MiB; layer-aligned buckets)")
     a = p.parse_args()
     torch.cuda.set_device(0)
     from cs744_pytorch_distributed_tutorial_amd.ops import native
@@ -84,7 +85,7 @@ def main():
     for _ in range(a.repeats):
         for i, (g, w, c, ge) in enumerate(configs):
             probe = "0" if g is None else f"xgmi:{ge}:{w}:{a.latency_us}:{c}"
-            samples[i].append(run(probe, a.steps, a.warmup))
+            samples[i].append(run(probe, a.steps, a.warmup, bucket_mb=a.bucket_mb))
             print(f"[projection] {probe}: {samples[i][-1][0]:.4f} ms", file=sys.stderr, flush=True)
     med = statistics.median_low  # an even count keeps the lower middle sample (outliers are slow)
     base = med([ms for ms, _, _ in samples[0]])
