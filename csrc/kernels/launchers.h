@@ -35,9 +35,18 @@ hipError_t cs_sgd_multi(const CsTensorEntry* tab_dev, int ntens, const int64_t* 
                         float lr, float mom, float wd, float damp, float scale, int first, hipStream_t stream);
 
 // classifier head
+// bn (optional, part 0 / 1): the features are the last VGG block's BatchNorm + ReLU + 2x2 max-pool of
+// its pre-BN output y [B][2][2][K] (scale / shift per channel), computed in the row pass (bn_apply's
+// arithmetic and max order: the same bits) and written to feat for the column pass
+struct CsHeadBn {
+  const float* y;
+  const float* scale;
+  const float* shift;
+};
 hipError_t cs_linear_xent(const float* feat, const float* W, const float* bias, const int64_t* labels, int B, int K,
                           int C, float gscale, float* loss_out, int* correct_out, float* logits_out, float* dW,
-                          float* db, float* dfeat, int64_t* pred_out, float* ws, hipStream_t stream, int part = 0);
+                          float* db, float* dfeat, int64_t* pred_out, float* ws, hipStream_t stream, int part = 0,
+                          const CsHeadBn* bn = nullptr);
 // part: 0 both launches; 1 the per-row pass (logits, prediction, dlogits -> ws, dfeat); 2 the
 // per-column pass (dW, db, loss, correct count from ws and feat) — run after part 1 (ws)
 inline int64_t cs_linear_xent_ws(int B, int C) { return (int64_t)B * (C + 2); }

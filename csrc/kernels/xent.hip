@@ -58,20 +58,38 @@ __device__ void head_loss(const float* lg, const int64_t* __restrict__ labels, i
 // registers; dl is staged in `ws` for the column pass. CT = compile-time class count
 // (10 for CIFAR-10: every class loop and cross-lane sum is unrolled and interleaved),
 // 0 = runtime C <= kMaxC.
+// feature float4 k of a row: read, or (bn.y != null) the last block's BN + ReLU + 2x2 max-pool of
+// its pre-BN output [2][2][K] (bn.hip bn_apply's arithmetic and max order), written back to feat
+__device__ __forceinline__ float4 bnrelu4h(float4 y, float4 s, float4 t) {
+  return make_float4(fmaxf(y.x * s.x + t.x, 0.f), fmaxf(y.y * s.y + t.y, 0.f), fmaxf(y.z * s.z + t.z, 0.f),
+                     fmaxf(y.w * s.w + t.w, 0.f));
+}
+__device__ __forceinline__ float4 head_feat(float4* f4, const CsHeadBn& bn, int row, int K4, int k) {
+  if (bn.y == nullptr) return f4[k];
+  const float4* y4 = reinterpret_cast<const float4*>(bn.y) + (size_t)row * 4 * K4 + k;
+  const float4 s = reinterpret_cast<const float4*>(bn.scale)[k], t = reinterpret_cast<const float4*>(bn.shift)[k];
+  const float4 a0 = bnrelu4h(y4[0], s, t), a1 = bnrelu4h(y4[K4], s, t);
+  const float4 a2 = bnrelu4h(y4[2 * K4], s, t), a3 = bnrelu4h(y4[3 * K4], s, t);
+  const float4 r = make_float4(fmaxf(fmaxf(a0.x, a1.x), fmaxf(a2.x, a3.x)), fmaxf(fmaxf(a0.y, a1.y), fmaxf(a2.y, a3.y)),
+                               fmaxf(fmaxf(a0.z, a1.z), fmaxf(a2.z, a3.z)), fmaxf(fmaxf(a0.w, a1.w), fmaxf(a2.w, a3.w)));
+  f4[k] = r;
+  return r;
+}
+
 template <int CT>
-__global__ __launch_bounds__(256) void head_rows_kernel(const float* __restrict__ feat, const float* __restrict__ W,
+__global__ __launch_bounds__(256) void head_rows_kernel(float* __restrict__ feat, const float* __restrict__ W,
                                                         const float* __restrict__ bias,
                                                         const int64_t* __restrict__ labels, int B, int K, int C,
                                                         float gscale, float* __restrict__ ws,
                                                         float* __restrict__ logits_out, int64_t* __restrict__ pred_out,
-                                                        float* __restrict__ dfeat) {
+                                                        float* __restrict__ dfeat, CsHeadBn bn) {
   constexpr int NC = CT ? CT : kMaxC;
   if (CT) C = CT;
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= B) return;
   const int K4 = K >> 2;
-  const float4* f4 = reinterpret_cast<const float4*>(feat) + (size_t)row * K4;
+  float4* f4 = reinterpret_cast<float4*>(feat) + (size_t)row * K4;
   const float4* w4 = reinterpret_cast<const float4*>(W);
   // label and bias loaded up front: their latency overlaps the dot products
   const int y = (int)labels[row];
@@ -92,7 +110,7 @@ __global__ __launch_bounds__(256) void head_rows_kernel(const float* __restrict_
       for (int it = 0; it < KIT; ++it) {
         const int k = lane + 64 * it;
         if (k < K4) {
-          const float4 f = f4[k];
+          const float4 f = head_feat(f4, bn, row, K4, k);
 #pragma unroll
           for (int j = 0; j < NC; ++j) {
             wc[it][j] = w4[(size_t)j * K4 + k];
@@ -104,7 +122,7 @@ __global__ __launch_bounds__(256) void head_rows_kernel(const float* __restrict_
   }
   if (!cached) {
     for (int k = lane; k < K4; k += 64) {
-      const float4 f = f4[k];
+      const float4 f = head_feat(f4, bn, row, K4, k);
 #pragma unroll
       for (int j = 0; j < NC; ++j) {
         if (j < C) {
@@ -261,15 +279,18 @@ __global__ __launch_bounds__(kThreads) void softmax_xent_kernel(const float* __r
 
 hipError_t cs_linear_xent(const float* feat, const float* W, const float* bias, const int64_t* labels, int B, int K,
                           int C, float gscale, float* loss_out, int* correct_out, float* logits_out, float* dW,
-                          float* db, float* dfeat, int64_t* pred_out, float* ws, hipStream_t stream, int part) {
+                          float* db, float* dfeat, int64_t* pred_out, float* ws, hipStream_t stream, int part,
+                          const CsHeadBn* bn) {
   if (C > kMaxC || C < 1 || B <= 0 || (K & 3) != 0 || ws == nullptr || part < 0 || part > 2) return hipErrorInvalidValue;
+  const CsHeadBn hb = bn != nullptr ? *bn : CsHeadBn{nullptr, nullptr, nullptr};
+  float* fw = const_cast<float*>(feat);  // written only when the row pass builds the features (bn)
   if (part == 2) goto cols;
   if (C == 10)
-    hipLaunchKernelGGL(head_rows_kernel<10>, dim3((B + 3) / 4), dim3(256), 0, stream, feat, W, bias, labels, B, K, C,
-                       gscale, ws, logits_out, pred_out, dfeat);
+    hipLaunchKernelGGL(head_rows_kernel<10>, dim3((B + 3) / 4), dim3(256), 0, stream, fw, W, bias, labels, B, K, C,
+                       gscale, ws, logits_out, pred_out, dfeat, hb);
   else
-    hipLaunchKernelGGL(head_rows_kernel<0>, dim3((B + 3) / 4), dim3(256), 0, stream, feat, W, bias, labels, B, K, C,
-                       gscale, ws, logits_out, pred_out, dfeat);
+    hipLaunchKernelGGL(head_rows_kernel<0>, dim3((B + 3) / 4), dim3(256), 0, stream, fw, W, bias, labels, B, K, C,
+                       gscale, ws, logits_out, pred_out, dfeat, hb);
   if (part == 1) return hipGetLastError();
 cols:
   const bool bwd = dW != nullptr && db != nullptr && (dfeat != nullptr || part == 2);

@@ -207,6 +207,7 @@ VggEngine::VggEngine(int64_t Bmax, std::vector<int64_t> desc, std::vector<int64_
   if (const char* e = getenv("CS_CONV0_BN_FOLD")) conv0_bn_fold_ = atoi(e) != 0;
   if (const char* e = getenv("CS_CONV0_SGD_FOLD")) conv0_sgd_fold_ = atoi(e) != 0;
   if (const char* e = getenv("CS_CONV0_BATCH_FOLD")) conv0_batch_fold_ = atoi(e) != 0;
+  if (const char* e = getenv("CS_HEAD_BN_FOLD")) head_bn_fold_ = atoi(e) != 0;
   if (const char* e = getenv("CS_BN_BWD_FUSED_P")) bwd_fused_p_ = atoi(e);
   bn_part_ = torch::zeros({partmax}, fo);
   bn_coef_ = torch::zeros({cmax * 3}, fo);
@@ -435,6 +436,7 @@ void VggEngine::forward_train(int64_t B) {
                      kMean, kStd, s),
        "make_batch");
   float* bufs = bufs_.data_ptr<float>();
+  CsHeadBn head_bn{nullptr, nullptr, nullptr};
   for (int l = 0; l < L; ++l) {
     VggBlock& b = blocks_[l];
     const ConvTile& t = b.tile[CS_CONV_FWD];
@@ -484,6 +486,11 @@ void VggEngine::forward_train(int64_t B) {
       lag_out_->wait(s);
       lag_pending_ = false;
     }
+    if (l + 1 == L && head_bn_fold_ && b.pool && b.H == 2 && b.cout == feat_ && !(debug_skip_ & 4)) {
+      // the last block's normalize/ReLU/pool runs inside the classifier's row pass (below)
+      head_bn = CsHeadBn{b.y.data_ptr<float>(), bn, bn + b.cout};
+      continue;
+    }
     if (!(debug_skip_ & 4))
     ok(cs_bn_apply(b.y.data_ptr<float>(), bn, bn + b.cout, out, (int)B, b.H, b.H, b.cout, b.pool, s), "bn_apply");
   }
@@ -494,7 +501,7 @@ void VggEngine::forward_train(int64_t B) {
   ok(cs_linear_xent(feats_.data_ptr<float>(), P(fc_w_), P(fc_b_), ylab_.data_ptr<int64_t>(), (int)B, (int)feat_,
                     (int)ncls_, 1.0f, loss_.data_ptr<float>(), correct_.data_ptr<int>(), logits_.data_ptr<float>(),
                     G(fc_w_), G(fc_b_), gbuf_[0].data_ptr<float>(), pred_.data_ptr<int64_t>(), head_ws_.data_ptr<float>(), s,
-                    fork ? 1 : 0),
+                    fork ? 1 : 0, head_bn.y != nullptr ? &head_bn : nullptr),
      "linear_xent");
   if (fork) {
     pending_sig_ = dz_link_->defer();  // rides the top block's BN backward launch

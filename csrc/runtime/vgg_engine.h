@@ -119,6 +119,9 @@ class VggEngine {
   void set_conv0_sgd_fold(bool on) { conv0_sgd_fold_ = on; }
   // ... and the training batch (make_batch) into the conv0 forward's input halo
   void set_conv0_batch_fold(bool on) { conv0_batch_fold_ = on; }
+  // the last block's BN + ReLU + max-pool inside the classifier's row pass (no bn_apply launch at the
+  // forward's end; CS_HEAD_BN_FOLD=0 keeps it)
+  void set_head_bn_fold(bool on) { head_bn_fold_ = on; }
   bool conv0_direct(int64_t B) const { return conv0_direct_ok(B); }
   // Deferred weight gradients (world 1, overlapped step): the top `n` blocks' weight gradients and
   // SGD run on a lag stream that starts at the end of the step and overlaps the NEXT step's forward
@@ -266,6 +269,7 @@ class VggEngine {
   bool conv0_bn_fold_ = true;
   bool conv0_sgd_fold_ = true;
   bool conv0_batch_fold_ = true;
+  bool head_bn_fold_ = true;
   hipStream_t lag_ = nullptr;
   std::unique_ptr<StreamLink> lag_in_, lag_out_;  // main -> lag (step end), lag -> main (deferred work done)
   std::vector<int> lag_list_;                      // blocks whose weight gradient this step defers

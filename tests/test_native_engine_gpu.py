@@ -549,18 +549,20 @@ def test_side_stream_link_error_surfaces(dev):
 
 
 def test_conv0_folds_bitwise(dev):
-    """Block 0's folds — the training batch built inside conv0's forward (no make_batch launch),
-    its BN-backward apply inside the weight gradient, its SGD step + batch cursor inside the
-    weight gradient's final sum — each change launches, not bits: every on/off combination trains
-    to the same parameters, momentum, buffers, cursor, labels and loss as all of them off."""
-    combos = [(0, 0, 0), (1, 1, 1), (1, 0, 0), (0, 1, 0), (0, 0, 1)]
+    """The chain-end folds — the training batch built inside conv0's forward (no make_batch launch),
+    block 0's BN-backward apply inside its weight gradient, its SGD step + batch cursor inside the
+    weight gradient's final sum, the last block's BN/ReLU/pool inside the classifier's row pass —
+    each change launches, not bits: every on/off combination trains to the same parameters,
+    momentum, buffers, cursor and loss as all of them off."""
+    combos = [(0, 0, 0, 0), (1, 1, 1, 1), (1, 0, 0, 0), (0, 1, 0, 0), (0, 0, 1, 0), (0, 0, 0, 1)]
     runs = []
-    for batch, bn, sgd in combos:
+    for batch, bn, sgd, head in combos:
         t = _trainer(dev, batch_size=64, train_size=512)
         assert t.engine.conv0_direct(64)
         t.engine.set_conv0_batch_fold(bool(batch))
         t.engine.set_conv0_bn_fold(bool(bn))
         t.engine.set_conv0_sgd_fold(bool(sgd))
+        t.engine.set_head_bn_fold(bool(head))
         for _ in range(4):
             t.step()
         torch.cuda.synchronize()
