@@ -208,6 +208,7 @@ VggEngine::VggEngine(int64_t Bmax, std::vector<int64_t> desc, std::vector<int64_
   if (const char* e = getenv("CS_CONV0_SGD_FOLD")) conv0_sgd_fold_ = atoi(e) != 0;
   if (const char* e = getenv("CS_CONV0_BATCH_FOLD")) conv0_batch_fold_ = atoi(e) != 0;
   if (const char* e = getenv("CS_HEAD_BN_FOLD")) head_bn_fold_ = atoi(e) != 0;
+  if (const char* e = getenv("CS_SIDE_SGD_TAIL")) side_sgd_tail_ = atoi(e) != 0;
   if (const char* e = getenv("CS_BN_BWD_FUSED_P")) bwd_fused_p_ = atoi(e);
   bn_part_ = torch::zeros({partmax}, fo);
   bn_coef_ = torch::zeros({cmax * 3}, fo);
@@ -405,7 +406,16 @@ void VggEngine::flush_signal(hipStream_t s) {
   pending_sig_ = nullptr;
 }
 
+void VggEngine::flush_side_sgd() {
+  // the SGD of the last block whose weight gradient forked, not yet carried by a later one
+  if (side_sgd_pending_ < 0) return;
+  sgd_on(side_, blk_range_[side_sgd_pending_].first, blk_range_[side_sgd_pending_].second, false);
+  wg_link_->signal(side_);
+  side_sgd_pending_ = -1;
+}
+
 void VggEngine::join_side(hipStream_t s) {
+  flush_side_sgd();
   flush_signal(s);  // the side stream may be waiting for it: never wait on side before it is out
   wg_link_->wait(s);
 }
@@ -728,10 +738,22 @@ void VggEngine::fork_wgrad(int l, int64_t B, bool current) {
   VggBlock& b = blocks_[l];
   float* dz = dz_blk_[l].data_ptr<float>();
   dz_link_->wait(side_);
-  if (!(debug_skip_ & 32))
-    conv(l, CS_CONV_WGRAD, (int)B, b.tile[CS_CONV_WGRAD], side_, false, ws_w_.data_ptr<float>(), dz);
-  // block l's dgrad (the last reader of its weights) ran before the fork
-  if (bwd_sgd_) sgd_on(side_, blk_range_[l].first, blk_range_[l].second, false);
+  // the previous fork's SGD (its gradient is final: its weight gradient ran before on this stream)
+  // rides this weight gradient's launch as extra workgroups; block l's own SGD waits for the next
+  // fork or the join (block l's dgrad — the last reader of its weights — ran before the fork)
+  CsSgdTail tail{};
+  if (side_sgd_pending_ >= 0) {
+    tail = side_sgd_tail_ ? sgd_tail_args(side_sgd_pending_) : CsSgdTail{};
+    if (tail.n == 0) sgd_on(side_, blk_range_[side_sgd_pending_].first, blk_range_[side_sgd_pending_].second, false);
+    side_sgd_pending_ = -1;
+  }
+  if (!(debug_skip_ & 32)) {
+    conv(l, CS_CONV_WGRAD, (int)B, b.tile[CS_CONV_WGRAD], side_, false, ws_w_.data_ptr<float>(), dz, nullptr,
+         tail.n > 0 ? &tail : nullptr);
+  } else if (tail.n > 0) {
+    sgd_on(side_, tail.p - P(0), tail.n, false);
+  }
+  if (bwd_sgd_) side_sgd_pending_ = l;
   wg_link_->signal(side_);
   if (!current) side_pending_ = -1;
 }

@@ -122,6 +122,9 @@ class VggEngine {
   // the last block's BN + ReLU + max-pool inside the classifier's row pass (no bn_apply launch at the
   // forward's end; CS_HEAD_BN_FOLD=0 keeps it)
   void set_head_bn_fold(bool on) { head_bn_fold_ = on; }
+  // side stream: block l+1's SGD as extra workgroups of block l's weight-gradient launch (one SGD
+  // launch per block fewer; CS_SIDE_SGD_TAIL=0 launches each block's SGD behind its weight gradient)
+  void set_side_sgd_tail(bool on) { side_sgd_tail_ = on; }
   bool conv0_direct(int64_t B) const { return conv0_direct_ok(B); }
   // Deferred weight gradients (world 1, overlapped step): the top `n` blocks' weight gradients and
   // SGD run on a lag stream that starts at the end of the step and overlaps the NEXT step's forward
@@ -270,6 +273,9 @@ class VggEngine {
   bool conv0_sgd_fold_ = true;
   bool conv0_batch_fold_ = true;
   bool head_bn_fold_ = true;
+  bool side_sgd_tail_ = true;
+  int side_sgd_pending_ = -1;  // block whose side-stream SGD has not been enqueued yet
+  void flush_side_sgd();
   hipStream_t lag_ = nullptr;
   std::unique_ptr<StreamLink> lag_in_, lag_out_;  // main -> lag (step end), lag -> main (deferred work done)
   std::vector<int> lag_list_;                      // blocks whose weight gradient this step defers
