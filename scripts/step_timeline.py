@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """One training step of a rocprofv3 kernel trace (.db), per HIP queue: every dispatch with its
 start / end offset from the step's first kernel, plus per-queue busy time and the critical
-(main-queue) idle gaps. A step = [the second-to-last make_batch dispatch, the last one).
+(main-queue) idle gaps. A step = [the second-to-last step-head dispatch, the last one): make_batch, or
+the conv0 forward when the batch is built inside it (round 5's fold).
 Usage: python scripts/step_timeline.py <rocprofv3 out dir> [--names 48]"""
 import argparse
 import collections
@@ -36,6 +37,8 @@ def main():
     a = p.parse_args()
     rows = load(a.path)
     mb = [i for i, r in enumerate(rows) if "make_batch" in r["name"]]
+    if len(mb) < 2:  # the batch is built inside conv0's forward: that kernel heads the step
+        mb = [i for i, r in enumerate(rows) if "conv0_fwd_kernel<true>" in r["name"]]
     if len(mb) < 2:
         print("need two make_batch dispatches")
         return
@@ -46,7 +49,7 @@ def main():
     for r in step:
         byq[r["q"]].append(r)
     main_q = step[0]["q"]
-    print(f"# one step: {len(step)} dispatches, span {span:.1f} us (make_batch to make_batch), queues {len(byq)}")
+    print(f"# one step: {len(step)} dispatches, span {span:.1f} us (step head to step head), queues {len(byq)}")
     for qid, rs in sorted(byq.items(), key=lambda kv: (kv[0] != main_q, kv[0])):
         busy = sum(r["end"] - r["start"] for r in rs) / 1e3
         print(f"\n## queue {qid}{' (main)' if qid == main_q else ''}: {len(rs)} dispatches, busy {busy:.1f} us")
@@ -61,7 +64,7 @@ def main():
         print(f"# queue {qid}: idle between its dispatches {gaps:.1f} us")
     # kernel-name classes on the main queue
     cls = collections.OrderedDict((k, 0.0) for k in ("conv_gemm", "conv_xp", "splitk", "bn_", "link_", "sgd",
-                                                       "head_", "make_batch", "other"))
+                                                       "head_", "make_batch", "conv0", "other"))
     for r in byq[main_q]:
         d = (r["end"] - r["start"]) / 1e3
         k = next((k for k in cls if k != "other" and k in r["name"]), "other")
