@@ -29,6 +29,8 @@ def main():
                         "buffers / cursor (a ramp that comes back is a property of the training state)")
     p.add_argument("--prewarm-ms", type=float, default=0.0,
                    help="> 0: that long of bf16 GEMMs before the warmup steps (is the ramp the clock?)")
+    p.add_argument("--prewarm-copy-ms", type=float, default=0.0,
+                   help="> 0: that long of 256 MiB device copies before the warmup steps (is it the memory clock?)")
     a = p.parse_args()
     from cs744_pytorch_distributed_tutorial_amd.ops import native
     torch.cuda.set_device(0)
@@ -58,6 +60,15 @@ def main():
         tr.engine.cursor().copy_(cur)
         tr._mom_valid, tr.global_step = mom_valid, gstep
         torch.cuda.synchronize()
+    if a.prewarm_copy_ms > 0:
+        src = torch.empty(64 << 20, device="cuda")
+        dst = torch.empty_like(src)
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < a.prewarm_copy_ms / 1e3:
+            for _ in range(4):
+                dst.copy_(src)
+            torch.cuda.synchronize()
+        del src, dst
     import gc
     gc.collect()
     gc.disable()
