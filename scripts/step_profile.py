@@ -29,6 +29,11 @@ def main():
                         "buffers / cursor (a ramp that comes back is a property of the training state)")
     p.add_argument("--prewarm-ms", type=float, default=0.0,
                    help="> 0: that long of bf16 GEMMs before the warmup steps (is the ramp the clock?)")
+    p.add_argument("--host-sleep-us", type=float, default=0.0,
+                   help="> 0: busy-wait this long on the host after each timed step's enqueue (does the "
+                        "host's lead over the GPU change the device step time?)")
+    p.add_argument("--second-trainer", type=int, default=0,
+                   help="> 0: first run a throw-away trainer for this many steps (is the ramp per process or per trainer?)")
     p.add_argument("--prewarm-copy-ms", type=float, default=0.0,
                    help="> 0: that long of 256 MiB device copies before the warmup steps (is it the memory clock?)")
     a = p.parse_args()
@@ -36,6 +41,13 @@ def main():
     torch.cuda.set_device(0)
     native.C().reserve_streams()
     from cs744_pytorch_distributed_tutorial_amd.runtime.engine import NativeTrainer
+    if a.second_trainer > 0:
+        t0_ = NativeTrainer(batch_size=64, device=torch.device("cuda", 0))
+        for _ in range(a.second_trainer):
+            t0_.step()
+        torch.cuda.synchronize()
+        t0_.close()
+        del t0_
     tr = NativeTrainer(batch_size=64, device=torch.device("cuda", 0))
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     from bench import _sysfs_card, _dpm_current
@@ -81,6 +93,10 @@ def main():
         for i in range(a.steps):
             ev[i].record()
             tr.step()
+            if a.host_sleep_us > 0:
+                t1 = time.perf_counter()
+                while time.perf_counter() - t1 < a.host_sleep_us / 1e6:
+                    pass
         ev[-1].record()
         t_enq = time.perf_counter() - t0
         torch.cuda.synchronize()
