@@ -213,6 +213,7 @@ void register_runtime(pybind11::module& m) {
       .def("set_conv0_batch_fold", &cs::VggEngine::set_conv0_batch_fold)
       .def("set_head_bn_fold", &cs::VggEngine::set_head_bn_fold)
       .def("set_side_sgd_tail", &cs::VggEngine::set_side_sgd_tail)
+      .def("set_head_tail", &cs::VggEngine::set_head_tail)
       .def("conv0_direct", &cs::VggEngine::conv0_direct)
       .def("join_lag", &cs::VggEngine::join_lag)
       .def("set_comm_defer", &cs::VggEngine::set_comm_defer)

@@ -36,6 +36,7 @@
 
 #include "conv_common.h"
 #include "sgd_device.h"
+#include "xent_device.h"
 
 namespace {
 
@@ -743,6 +744,11 @@ __global__ __launch_bounds__(256 * KG) void conv_gemm_kernel(CsConvArgs a) {
   const int ng = ntiles * nsplit, lin = blockIdx.x;
   if (a.start_sig != nullptr && lin == 0 && threadIdx.x == 0)
     __hip_atomic_fetch_add(a.start_sig, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (lin >= ng + a.sgd.P) {  // the classifier's column pass: one piece per wave
+    const int hb = (lin - ng - a.sgd.P) * KG * 4 + (int)(threadIdx.x >> 6);
+    if (hb < a.head.P) cs_head::cols_wave(a.head, hb, threadIdx.x & 63);
+    return;
+  }
   if (lin >= ng) {
     cs_sgd::tail_body(a.sgd, lin - ng, a.sgd.P);
     return;
@@ -955,6 +961,7 @@ template <int BM, int BN, int MODE, int BK, int SCHED, bool C4, int GL, int KG =
 hipError_t launch_k(dim3 grid, size_t lds, hipStream_t stream, const CsConvArgs& a) {
   size_t l = std::max(lds, (size_t)(1024 + 16) * sizeof(float));  // bn_fin.h's combine space
   if (MODE == CS_CONV_DGRAD && a.ered.part != nullptr) l = std::max(l, (size_t)BM * (BN + 4) * sizeof(float));
+  if (a.head.P > 0) grid.x += (a.head.P + 4 * KG - 1) / (4 * KG);  // the column pass: a piece per wave
   hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, MODE, BK, SCHED, C4, GL, KG>), grid, dim3(256 * KG), l, stream, a);
   return hipGetLastError();
 }
@@ -1205,7 +1212,8 @@ int prep_gemm(CsConvArgs& a, int mode, int bk, int splits) {
 
 hipError_t cs_conv_gemm_dual(CsConvArgs wg, int wbk, int wsplits, CsConvArgs dg, int dbk, int dsplits,
                              hipStream_t stream, int stage) {
-  if (wg.sgd.n != 0 || dg.sgd.n != 0) return hipErrorInvalidValue;  // no appended work in dual launches
+  if (wg.sgd.n != 0 || dg.sgd.n != 0 || wg.head.P != 0 || dg.head.P != 0)
+    return hipErrorInvalidValue;  // no appended work in dual launches
   if (wg.w_oihw) return hipErrorInvalidValue;  // conv0 has no data gradient
   if (wg.fin.cnt != nullptr) return hipErrorInvalidValue;  // (the weight gradient has no BN statistics)
   const int s1 = prep_gemm(wg, CS_CONV_WGRAD, wbk, wsplits), s2 = prep_gemm(dg, CS_CONV_DGRAD, dbk, dsplits);

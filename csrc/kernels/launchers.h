@@ -38,6 +38,20 @@ hipError_t cs_sgd_multi(const CsTensorEntry* tab_dev, int ntens, const int64_t* 
 // bn (optional, part 0 / 1): the features are the last VGG block's BatchNorm + ReLU + 2x2 max-pool of
 // its pre-BN output y [B][2][2][K] (scale / shift per channel), computed in the row pass (bn_apply's
 // arithmetic and max order: the same bits) and written to feat for the column pass
+// the classifier's per-column pass (dW, db, loss, correct count) as data: run by its own launch or
+// carried as extra workgroups of a weight-gradient launch (CsConvArgs::head; P = C*ceil(K/64)+1
+// wave-sized pieces, 0 = none)
+struct CsHeadCols {
+  const float* feat;
+  int B, K, C;
+  const float* ws;
+  float* dW;
+  float* db;
+  float* loss_out;
+  int* correct_out;
+  int P;
+};
+inline int cs_head_cols_pieces(int K, int C) { return C * ((K + 63) / 64) + 1; }
 struct CsHeadBn {
   const float* y;
   const float* scale;
@@ -123,6 +137,8 @@ struct CsConvArgs {
   // it starts — every kernel before it on its stream has completed (the engine's staggered fork:
   // block l+1's side-stream weight gradient waits for block l's data gradient to be resident)
   unsigned long long* start_sig;
+  // the classifier's per-column pass carried as extra workgroups (head.P == 0: none)
+  CsHeadCols head;
   // filled by the launcher:
   int lgH, lgW, lgCin, lgCout, M, N, K, ksteps_per_split, total_ksteps;
 };

@@ -9,6 +9,7 @@
 // never syncs the host (the loss is read only every 20 iterations).
 #include "common.h"
 #include "launchers.h"
+#include "xent_device.h"
 
 namespace {
 
@@ -204,67 +205,8 @@ __global__ __launch_bounds__(256) void head_rows_kernel(float* __restrict__ feat
   }
 }
 
-// Column pass: blocks [0, C*ceil(K/64)) compute dW[j][k] = sum_b dl[b][j] feat[b][k] for one j and
-// 64 consecutive k (one wave, lane = k, b-loop unrolled so the loads pipeline); the last block
-// computes db and the batch loss / correct count (fixed summation order: deterministic).
-__global__ __launch_bounds__(64) void head_cols_kernel(const float* __restrict__ feat, int B, int K, int C,
-                                                       const float* __restrict__ ws, float* __restrict__ dW,
-                                                       float* __restrict__ db, float* __restrict__ loss_out,
-                                                       int* __restrict__ correct_out) {
-  __shared__ float red[16];
-  const float* dl = ws;
-  const float* rowloss = ws + (size_t)B * C;
-  const float* rowcorr = rowloss + B;
-  const int nkc = (K + 63) / 64;
-  const int bid = blockIdx.x;
-  if (dW != nullptr && bid < C * nkc) {
-    const int j = bid / nkc, k = (bid - j * nkc) * 64 + threadIdx.x;
-    if (k >= K) return;
-    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-    int b = 0;
-    // 16 rows of loads in flight, then the adds in the 4-accumulator order of the loop below
-    for (; b + 16 <= B; b += 16) {
-      float d[16], f[16];
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        d[i] = dl[(size_t)(b + i) * C + j];
-        f[i] = feat[(size_t)(b + i) * K + k];
-      }
-#pragma unroll
-      for (int i = 0; i < 16; i += 4) {
-        s0 += d[i] * f[i];
-        s1 += d[i + 1] * f[i + 1];
-        s2 += d[i + 2] * f[i + 2];
-        s3 += d[i + 3] * f[i + 3];
-      }
-    }
-    for (; b + 4 <= B; b += 4) {
-      s0 += dl[(size_t)b * C + j] * feat[(size_t)b * K + k];
-      s1 += dl[(size_t)(b + 1) * C + j] * feat[(size_t)(b + 1) * K + k];
-      s2 += dl[(size_t)(b + 2) * C + j] * feat[(size_t)(b + 2) * K + k];
-      s3 += dl[(size_t)(b + 3) * C + j] * feat[(size_t)(b + 3) * K + k];
-    }
-    for (; b < B; ++b) s0 += dl[(size_t)b * C + j] * feat[(size_t)b * K + k];
-    dW[(size_t)j * K + k] = (s0 + s1) + (s2 + s3);
-    return;
-  }
-  float l = 0.f, c = 0.f;
-  for (int r = threadIdx.x; r < B; r += blockDim.x) {
-    l += rowloss[r];
-    c += rowcorr[r];
-  }
-  l = cs::block_sum(l, red);
-  c = cs::block_sum(c, red);
-  if (threadIdx.x == 0) {
-    if (loss_out) *loss_out = l / (float)B;
-    if (correct_out) *correct_out = (int)(c + 0.5f);
-  }
-  if (db != nullptr && threadIdx.x < (unsigned)C) {
-    float acc = 0.f;
-    for (int r = 0; r < B; ++r) acc += dl[(size_t)r * C + threadIdx.x];
-    db[threadIdx.x] = acc;
-  }
-}
+// Column pass: one 64-thread block per piece of cs_head::cols_wave (xent_device.h)
+__global__ __launch_bounds__(64) void head_cols_kernel(CsHeadCols h) { cs_head::cols_wave(h, blockIdx.x, threadIdx.x); }
 
 __global__ __launch_bounds__(kThreads) void softmax_xent_kernel(const float* __restrict__ logits,
                                                                 const int64_t* __restrict__ labels, int B, int C,
@@ -294,8 +236,9 @@ hipError_t cs_linear_xent(const float* feat, const float* W, const float* bias, 
   if (part == 1) return hipGetLastError();
 cols:
   const bool bwd = dW != nullptr && db != nullptr && (dfeat != nullptr || part == 2);
-  hipLaunchKernelGGL(head_cols_kernel, dim3(bwd ? C * ((K + 63) / 64) + 1 : 1), dim3(64), 0, stream, feat, B, K, C, ws,
-                     bwd ? dW : nullptr, bwd ? db : nullptr, loss_out, correct_out);
+  const CsHeadCols h{feat, B, K, C, ws, bwd ? dW : nullptr, bwd ? db : nullptr, loss_out, correct_out,
+                     bwd ? cs_head_cols_pieces(K, C) : 1};
+  hipLaunchKernelGGL(head_cols_kernel, dim3(h.P), dim3(64), 0, stream, h);
   return hipGetLastError();
 }
 

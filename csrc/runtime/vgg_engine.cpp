@@ -209,6 +209,7 @@ VggEngine::VggEngine(int64_t Bmax, std::vector<int64_t> desc, std::vector<int64_
   if (const char* e = getenv("CS_CONV0_BATCH_FOLD")) conv0_batch_fold_ = atoi(e) != 0;
   if (const char* e = getenv("CS_HEAD_BN_FOLD")) head_bn_fold_ = atoi(e) != 0;
   if (const char* e = getenv("CS_SIDE_SGD_TAIL")) side_sgd_tail_ = atoi(e) != 0;
+  if (const char* e = getenv("CS_HEAD_TAIL")) head_tail_ = atoi(e) != 0;
   if (const char* e = getenv("CS_BN_BWD_FUSED_P")) bwd_fused_p_ = atoi(e);
   bn_part_ = torch::zeros({partmax}, fo);
   bn_coef_ = torch::zeros({cmax * 3}, fo);
@@ -287,6 +288,10 @@ void VggEngine::conv(int l, int mode, int B, const ConvTile& t, hipStream_t s, b
   }
   if (sgd != nullptr) a.sgd = *sgd;
   if (fin != nullptr) a.fin = *fin;
+  if (head_next_.P > 0 && mode == CS_CONV_WGRAD && s == side_ && l + 1 == (int)blocks_.size()) {
+    a.head = head_next_;  // the classifier's column pass (forward_train) rides this launch
+    head_next_.P = 0;
+  }
   a.start_sig = start_sig_;  // the staggered fork's deferred signal rides this launch (once)
   start_sig_ = nullptr;
   const Dims d = dims(b, mode, B);
@@ -415,6 +420,7 @@ void VggEngine::flush_side_sgd() {
 }
 
 void VggEngine::join_side(hipStream_t s) {
+  TORCH_CHECK(head_next_.P == 0, "VggEngine: the classifier column pass was never launched");
   flush_side_sgd();
   flush_signal(s);  // the side stream may be waiting for it: never wait on side before it is out
   wg_link_->wait(s);
@@ -513,7 +519,13 @@ void VggEngine::forward_train(int64_t B) {
                     G(fc_w_), G(fc_b_), gbuf_[0].data_ptr<float>(), pred_.data_ptr<int64_t>(), head_ws_.data_ptr<float>(), s,
                     fork ? 1 : 0, head_bn.y != nullptr ? &head_bn : nullptr),
      "linear_xent");
-  if (fork) {
+  if (fork && head_tail_ && !stagger_ && lag_blocks_ == 0 && !(debug_skip_ & 32)) {
+    // the column pass rides the top block's weight-gradient launch on the side stream (extra
+    // workgroups; that launch forks after the top block's data gradient, long after this row pass)
+    head_next_ = CsHeadCols{feats_.data_ptr<float>(), (int)B, (int)feat_, (int)ncls_, head_ws_.data_ptr<float>(),
+                            G(fc_w_), G(fc_b_), loss_.data_ptr<float>(), correct_.data_ptr<int>(),
+                            cs_head_cols_pieces((int)feat_, (int)ncls_)};
+  } else if (fork) {
     pending_sig_ = dz_link_->defer();  // rides the top block's BN backward launch
     dz_link_->wait(side_);
     ok(cs_linear_xent(feats_.data_ptr<float>(), P(fc_w_), P(fc_b_), ylab_.data_ptr<int64_t>(), (int)B, (int)feat_,

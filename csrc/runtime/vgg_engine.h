@@ -125,6 +125,9 @@ class VggEngine {
   // side stream: block l+1's SGD as extra workgroups of block l's weight-gradient launch (one SGD
   // launch per block fewer; CS_SIDE_SGD_TAIL=0 launches each block's SGD behind its weight gradient)
   void set_side_sgd_tail(bool on) { side_sgd_tail_ = on; }
+  // the classifier's column pass as extra workgroups of the top block's side-stream weight-gradient
+  // launch instead of its own fork (CS_HEAD_TAIL=1; default: own launch behind a link wait)
+  void set_head_tail(bool on) { head_tail_ = on; }
   bool conv0_direct(int64_t B) const { return conv0_direct_ok(B); }
   // Deferred weight gradients (world 1, overlapped step): the top `n` blocks' weight gradients and
   // SGD run on a lag stream that starts at the end of the step and overlaps the NEXT step's forward
@@ -274,6 +277,8 @@ class VggEngine {
   bool conv0_batch_fold_ = true;
   bool head_bn_fold_ = true;
   bool side_sgd_tail_ = true;
+  bool head_tail_ = false;  // measured neutral (profiles/r5_ab_head_tail.txt): opt-in
+  CsHeadCols head_next_{};  // P > 0: the column pass waiting for the top block's weight-gradient launch
   int side_sgd_pending_ = -1;  // block whose side-stream SGD has not been enqueued yet
   void flush_side_sgd();
   hipStream_t lag_ = nullptr;

@@ -98,10 +98,10 @@ def main() -> int:
             TILESETS[name](tr)
     variants = []
     for v in args.variants:
-        # NAME[:opt,opt,...]  opts: mask=M serial tiles=NAME|file=PATH fused=FWD_T/BWD_P fin stagger lag=N conv0=0|1 fold=0|1 sgdfold=0|1 batchfold=0|1 headfold=0|1 sidetail=0|1
+        # NAME[:opt,opt,...]  opts: mask=M serial tiles=NAME|file=PATH fused=FWD_T/BWD_P fin stagger lag=N conv0=0|1 fold=0|1 sgdfold=0|1 batchfold=0|1 headfold=0|1 sidetail=0|1 headtail=0|1
         name, _, rest = v.partition(":")
         o = {"mask": 0, "serial": False, "tiles": "", "fused": (0, 0), "fin": False, "stagger": False, "lag": 0,
-             "conv0": 1, "fold": 1, "sgdfold": 1, "batchfold": 1, "headfold": 1, "sidetail": 1}
+             "conv0": 1, "fold": 1, "sgdfold": 1, "batchfold": 1, "headfold": 1, "sidetail": 1, "headtail": 0}
         for tok in filter(None, rest.split(",")):
             k, _, val = tok.partition("=")
             if k == "mask":
@@ -112,7 +112,7 @@ def main() -> int:
                 o["tiles"] = "file=" + val
             elif k == "fused":
                 o["fused"] = tuple(int(x) for x in val.split("/"))
-            elif k in ("lag", "conv0", "fold", "sgdfold", "batchfold", "headfold", "sidetail"):
+            elif k in ("lag", "conv0", "fold", "sgdfold", "batchfold", "headfold", "sidetail", "headtail"):
                 o[k] = int(val)
             elif k in ("serial", "fin", "stagger"):
                 o[k] = True
@@ -149,6 +149,7 @@ def main() -> int:
             tr.engine.set_conv0_batch_fold(bool(o["batchfold"]))
             tr.engine.set_head_bn_fold(bool(o["headfold"]))
             tr.engine.set_side_sgd_tail(bool(o["sidetail"]))
+            tr.engine.set_head_tail(bool(o["headtail"]))
             tr.engine.set_debug_skip(o["mask"])
             tr.engine.set_overlap(base_overlap and not o["serial"])
             for _ in range(args.warmup):
