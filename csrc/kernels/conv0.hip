@@ -19,6 +19,10 @@
 //    B = the input windows (N = the 27 (ci, tap) columns) from the LDS halo. The 4 waves' tiles
 //    are summed in order into one [64][27] partial per workgroup (OIHW order); conv0_wgrad_sum: the
 //    partials summed in a fixed order -> dW.
+//  Folds (each bit-equal to the separate launch it replaces; vgg_engine.cpp chooses them):
+//    conv0_fwd<BATCH> builds the training batch in its halo load (make_batch's sampler index, label
+//    gather and crop/flip/normalize of the uint8 images); conv0_wgrad_bn_part computes block 0's
+//    BN-backward dZ in LDS instead of reading it; conv0_wgrad_sum can apply block 0's SGD step.
 #include "common.h"
 #include "launchers.h"
 #include "sgd_device.h"
