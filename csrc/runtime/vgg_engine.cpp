@@ -210,6 +210,7 @@ VggEngine::VggEngine(int64_t Bmax, std::vector<int64_t> desc, std::vector<int64_
   if (const char* e = getenv("CS_HEAD_BN_FOLD")) head_bn_fold_ = atoi(e) != 0;
   if (const char* e = getenv("CS_SIDE_SGD_TAIL")) side_sgd_tail_ = atoi(e) != 0;
   if (const char* e = getenv("CS_HEAD_TAIL")) head_tail_ = atoi(e) != 0;
+  if (const char* e = getenv("CS_SIDE_JOIN_ONCE")) side_join_once_ = atoi(e) != 0;
   if (const char* e = getenv("CS_BN_BWD_FUSED_P")) bwd_fused_p_ = atoi(e);
   bn_part_ = torch::zeros({partmax}, fo);
   bn_coef_ = torch::zeros({cmax * 3}, fo);
@@ -415,13 +416,20 @@ void VggEngine::flush_side_sgd() {
   // the SGD of the last block whose weight gradient forked, not yet carried by a later one
   if (side_sgd_pending_ < 0) return;
   sgd_on(side_, blk_range_[side_sgd_pending_].first, blk_range_[side_sgd_pending_].second, false);
-  wg_link_->signal(side_);
+  if (side_join_once_)
+    side_dirty_ = true;
+  else
+    wg_link_->signal(side_);
   side_sgd_pending_ = -1;
 }
 
 void VggEngine::join_side(hipStream_t s) {
   TORCH_CHECK(head_next_.P == 0, "VggEngine: the classifier column pass was never launched");
   flush_side_sgd();
+  if (side_dirty_) {  // one join signal for everything forked since the last join (side_join_once_)
+    wg_link_->signal(side_);
+    side_dirty_ = false;
+  }
   flush_signal(s);  // the side stream may be waiting for it: never wait on side before it is out
   wg_link_->wait(s);
 }
@@ -532,7 +540,10 @@ void VggEngine::forward_train(int64_t B) {
                       (int)ncls_, 1.0f, loss_.data_ptr<float>(), correct_.data_ptr<int>(), logits_.data_ptr<float>(),
                       G(fc_w_), G(fc_b_), nullptr, pred_.data_ptr<int64_t>(), head_ws_.data_ptr<float>(), side_, 2),
        "linear_xent(cols)");
-    wg_link_->signal(side_);
+    if (side_join_once_)
+      side_dirty_ = true;
+    else
+      wg_link_->signal(side_);
   }
 }
 
@@ -766,7 +777,10 @@ void VggEngine::fork_wgrad(int l, int64_t B, bool current) {
     sgd_on(side_, tail.p - P(0), tail.n, false);
   }
   if (bwd_sgd_) side_sgd_pending_ = l;
-  wg_link_->signal(side_);
+  if (side_join_once_)
+    side_dirty_ = true;
+  else
+    wg_link_->signal(side_);
   if (!current) side_pending_ = -1;
 }
 

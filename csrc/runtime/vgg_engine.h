@@ -128,6 +128,9 @@ class VggEngine {
   // the classifier's column pass as extra workgroups of the top block's side-stream weight-gradient
   // launch instead of its own fork (CS_HEAD_TAIL=1; default: own launch behind a link wait)
   void set_head_tail(bool on) { head_tail_ = on; }
+  // one side-stream join signal per join instead of one per fork (CS_SIDE_JOIN_ONCE=1; measured
+  // 2.4 % slower in-process: profiles/r5_ab_side_join_once.txt)
+  void set_side_join_once(bool on) { side_join_once_ = on; }
   bool conv0_direct(int64_t B) const { return conv0_direct_ok(B); }
   // Deferred weight gradients (world 1, overlapped step): the top `n` blocks' weight gradients and
   // SGD run on a lag stream that starts at the end of the step and overlaps the NEXT step's forward
@@ -277,6 +280,8 @@ class VggEngine {
   bool conv0_batch_fold_ = true;
   bool head_bn_fold_ = true;
   bool side_sgd_tail_ = true;
+  bool side_join_once_ = false;
+  bool side_dirty_ = false;  // side-stream work since the last join signal (side_join_once_)
   bool head_tail_ = false;  // measured neutral (profiles/r5_ab_head_tail.txt): opt-in
   CsHeadCols head_next_{};  // P > 0: the column pass waiting for the top block's weight-gradient launch
   int side_sgd_pending_ = -1;  // block whose side-stream SGD has not been enqueued yet
