@@ -1,5 +1,4 @@
 import os
-import socket
 import sys
 
 import pytest
@@ -18,14 +17,39 @@ def pytest_configure(config):
     pkg.ensure_hw_queues()
 
 
-def free_port() -> int:
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
+class HostedStore:
+    """A rendezvous store the TEST process owns for the whole life of a spawned world.
+
+    The server binds port 0 and keeps the socket, so no other socket can take the port between
+    "pick a port" and "rank 0 listens on it" (the round-5 EADDRINUSE race of bind(0)-then-close).
+    Ranks connect as clients: ``TORCHELASTIC_USE_AGENT_STORE=True`` makes torch's env://
+    rendezvous create a client on every rank, rank 0 included — exactly what torchrun's agent
+    does with its own store. One store per world: process-group keys restart in every process.
+    """
+
+    def __init__(self, world: int):
+        from torch.distributed import TCPStore
+        self.store = TCPStore("127.0.0.1", 0, world, is_master=True, wait_for_workers=False)
+        self.port = self.store.port
+
+    def env(self, base=None) -> dict:
+        e = dict(os.environ if base is None else base)
+        e.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(self.port), TORCHELASTIC_USE_AGENT_STORE="True")
+        return e
+
+
+def torchrun_cmd(nproc: int) -> list:
+    """torchrun with a standalone rendezvous: the launcher's agent binds port 0 and hands its store
+    to the workers, so there is no port to race for."""
+    return [sys.executable, "-m", "torch.distributed.run", "--standalone", "--local-addr", "127.0.0.1",
+            "--nnodes=1", f"--nproc-per-node={nproc}"]
 
 
 @pytest.fixture
-def port():
-    return free_port()
+def hosted_store(monkeypatch):
+    """A one-rank HostedStore whose port/env the test's child processes inherit."""
+    hs = HostedStore(1)
+    for k, v in hs.env({}).items():
+        monkeypatch.setenv(k, v)
+    yield hs
+    del hs.store

@@ -1,17 +1,10 @@
 """Spawn a gloo world on 127.0.0.1 and collect per-rank results."""
 import os
-import socket
 import traceback
 
 import torch.multiprocessing as mp
 
-
-def _free_port() -> int:
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+from conftest import HostedStore
 
 
 def _to_host(obj):
@@ -29,6 +22,8 @@ def _to_host(obj):
 def _entry(rank, world, port, fn, args, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
+    # the parent hosts the store (HostedStore): every rank, rank 0 included, is a client
+    os.environ["TORCHELASTIC_USE_AGENT_STORE"] = "True"
     os.environ.setdefault("OMP_NUM_THREADS", "1")
     import torch
     torch.set_num_threads(1)
@@ -51,8 +46,8 @@ def _entry(rank, world, port, fn, args, q):
 def run_world(fn, world: int, *args, timeout: float = 240.0):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_entry, args=(r, world, port, fn, args, q)) for r in range(world)]
+    hosted = HostedStore(world)
+    procs = [ctx.Process(target=_entry, args=(r, world, hosted.port, fn, args, q)) for r in range(world)]
     for p in procs:
         p.start()
     results = {}
@@ -69,6 +64,7 @@ def run_world(fn, world: int, *args, timeout: float = 240.0):
             p.join(timeout=30)
             if p.is_alive():
                 p.kill()
+        del hosted
     def back(o):
         if isinstance(o, np.ndarray):
             return torch.from_numpy(o)

@@ -35,13 +35,6 @@ def test_bench_json_line():
     assert d["vs_baseline"] == pytest.approx(d["value"] / 554.0, rel=1e-2)
 
 
-def _free_port() -> int:
-    import socket
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
-
-
 def test_bench_two_ranks_staged_json_line():
     """The N > 1 branch of bench.py, exactly as the driver launches it (torch.distributed.run, one
     process per rank), with the staged transport so both ranks fit on the 1-GPU box: process-group
@@ -49,8 +42,8 @@ def test_bench_two_ranks_staged_json_line():
     sync bracket, max-over-ranks time, the busBW report after the window, and ONE JSON line."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
+    from conftest import torchrun_cmd
+    cmd = torchrun_cmd(2) + ["bench.py", "--gpus", "2",
            "--comm", "staged", "--steps", "5", "--warmup", "2", "--busbw-iters", "3"]
     env = dict(os.environ, CS744_BENCH_CALIBRATE="0")
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)

@@ -8,15 +8,14 @@ import sys
 
 import pytest
 
-from conftest import free_port
+from conftest import torchrun_cmd
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _torchrun(module, args, nproc=2, timeout=240):
     env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
-           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "-m", module] + args
+    cmd = torchrun_cmd(nproc) + ["-m", module] + args
     p = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=timeout)
     assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
     return [json.loads(l) for l in p.stdout.splitlines() if l.startswith("{")]

@@ -58,9 +58,10 @@ def test_distributed_parts_agree_with_each_other():
 
 @pytest.mark.slow
 def test_pingpong_entrypoint_cli(tmp_path):
-    from conftest import free_port
-    port = str(free_port())
-    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
+    from conftest import HostedStore
+    hosted = HostedStore(2)
+    port = str(hosted.port)
+    env = hosted.env(dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1"))
     cmd = [sys.executable, "-m", "cs744_pytorch_distributed_tutorial_amd.entrypoints.part1_pingpong",
            "--master-ip", "127.0.0.1", "--num-nodes", "2"]
     procs = [subprocess.Popen(cmd + ["--rank", str(r), "--port", port], env=env, cwd=ROOT, stdout=subprocess.PIPE,

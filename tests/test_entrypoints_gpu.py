@@ -62,10 +62,9 @@ def test_part1_resume_mid_epoch_is_bitwise(gpu, tune_cache, tmp_path):
 
 @pytest.mark.slow
 def test_part3_torchrun_world1_native(gpu, tune_cache):
-    from conftest import free_port
+    from conftest import torchrun_cmd
     env = dict(os.environ, PYTHONPATH=ROOT)
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "1", "--master-addr",
-           "127.0.0.1", "--master-port", str(free_port()), "-m",
+    cmd = torchrun_cmd(1) + ["-m",
            "cs744_pytorch_distributed_tutorial_amd.entrypoints.part3", "--steps", "30"] + SMALL[:-1] + ["1"]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-1500:]

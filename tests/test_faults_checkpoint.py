@@ -51,8 +51,8 @@ def _kill_child(port, spec):
     return subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
 
 
-def test_fault_kill_exits_rank_with_code_17(port):
-    r = _kill_child(port, "all_reduce@2:0:kill")
+def test_fault_kill_exits_rank_with_code_17(hosted_store):
+    r = _kill_child(hosted_store.port, "all_reduce@2:0:kill")
     assert r.returncode == 17, (r.returncode, r.stderr[-500:])
     assert "survived" not in r.stdout and "[fault]" in r.stderr
 

@@ -15,7 +15,6 @@ box), so N processes share cuda:0 and talk over gloo:
   (negative control) must not.
 """
 import os
-import socket
 import subprocess
 import sys
 import textwrap
@@ -289,19 +288,13 @@ def test_rccl_one_rank_abort_path(gpu):
     tr.close()
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
-
-
 @pytest.mark.slow
 def test_killed_rank_fails_peer_promptly(gpu):
     """CS744_FAULT kills rank 1 inside the native all-reduce of step 3: rank 0 must exit
     non-zero within seconds (gloo sees the closed connection), not hang."""
-    port = _free_port()
+    from conftest import HostedStore
+    hosted = HostedStore(2)
+    port = hosted.port
     code = textwrap.dedent(f"""
         import os, sys
         sys.path.insert(0, {ROOT!r})
@@ -322,7 +315,7 @@ def test_killed_rank_fails_peer_promptly(gpu):
         print("finished", flush=True)
     """)
     procs = [subprocess.Popen([sys.executable, "-c", code, str(r)], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
-                              text=True) for r in range(2)]
+                              text=True, env=hosted.env()) for r in range(2)]
     try:
         outs = [p.communicate(timeout=100) for p in procs]
     finally:
