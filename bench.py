@@ -79,6 +79,10 @@ def parse(argv=None):
     p.add_argument("--json-out", type=str, default=None)
     p.add_argument("--watchdog-s", type=float, default=600.0,
                    help="abort the communicator and exit(18) if one step stalls this long (0 = off)")
+    p.add_argument("--comm-probe", type=str, default=None,
+                   help="native engine, world 1, measurement only: run the data-parallel step (bucket "
+                        "all-reduces, buffer broadcast, fork/join) against a one-rank communicator: "
+                        "'1' = RCCL, 'order' = scrambling probe, 'xgmi:G:W:us[:ctas]' = modelled ring")
     p.add_argument("--phases", type=int, default=0,
                    help="native engine: after the timed steps, N more steps with per-phase device timing "
                         "(forward / bucket backward / all-reduce wait / SGD), printed to stderr as JSON")
@@ -92,7 +96,7 @@ def is_vgg(name: str) -> bool:
 def make_trainer(args, device, rank, world):
     if args.engine == "native" and is_vgg(args.model):
         from cs744_pytorch_distributed_tutorial_amd.runtime.engine import NativeTrainer
-        return NativeTrainer.from_bench_args(args, device, rank, world)
+        return NativeTrainer.from_bench_args(args, device, rank, world, probe=args.comm_probe)
     from cs744_pytorch_distributed_tutorial_amd.runtime.torch_trainer import TorchTrainer
     return TorchTrainer(args.model, args.batch_size, device, rank, world, sync=args.sync, comm=args.comm,
                         bucket_mb=args.bucket_mb, bucket_policy=args.bucket_policy, dtype=args.dtype,
@@ -115,10 +119,11 @@ def describe(args, trainer, world):
 
 def comm_kind(trainer, world: int) -> str:
     """The gradient transport the timed steps actually used."""
-    if world == 1:
-        return "none"
-    if getattr(trainer, "comm_kind", None):  # native engine
-        return trainer.comm_kind
+    kind = getattr(trainer, "comm_kind", None)  # native engine
+    if world == 1:  # a one-rank measurement communicator (--comm-probe) or none
+        return kind if kind and kind.startswith("probe") else "none"
+    if kind:
+        return kind
     net = getattr(trainer, "net", None)
     comm = getattr(net, "comm", None)  # framework DDP (TorchTrainer)
     return getattr(comm, "kind", "torch") if comm is not None else "torch"
@@ -193,6 +198,17 @@ def calibration(device) -> dict:
     return out
 
 
+def rccl_versions():
+    """{runtime, header} RCCL version codes: the library actually loaded (torch's) and the header the
+    native communicator was compiled against (they differ on this image: 2.26 vs 2.27)."""
+    try:
+        from cs744_pytorch_distributed_tutorial_amd.ops import native
+        rt, hdr = native.C().rccl_version()
+        return {"runtime": int(rt), "header": int(hdr)}
+    except Exception as e:  # noqa: BLE001
+        return {"error": str(e)[:120]}
+
+
 def _bench_comm(trainer):
     """The native DeviceComm the steps used (VGG engine, or the framework DDP's), or None."""
     native = getattr(trainer, "native_comm", None)
@@ -250,23 +266,30 @@ def main(argv=None) -> int:
     if args.seq_len == 0 and "8b" in args.model.lower():
         args.seq_len = 2048  # the round-1 measurements' context (the model's max_seq is 8192)
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
-    # one GPU per rank; the staged transport lets ranks share GPUs (local rank modulo the count:
-    # device_count() does not initialise HIP on this stack)
+    # one GPU per rank (local rank modulo the count — the identity on a full node; on a smaller box the
+    # staged transport, and the rccl fallback test, let ranks share GPUs; device_count() does not
+    # initialise HIP on this stack)
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dev_index = local % max(torch.cuda.device_count(), 1) if args.comm == "staged" else local
+    dev_index = local % max(torch.cuda.device_count(), 1)
     if args.engine == "native" and is_vgg(args.model):
         # before the process group or anything else creates streams: the native engine's side
         # stream must own a hardware queue (measured 4x slower steps when it shares one)
         from cs744_pytorch_distributed_tutorial_amd.ops import native
         torch.cuda.set_device(dev_index)
         native.C().reserve_streams()
+    native_vgg = args.engine == "native" and is_vgg(args.model)
     if world_env > 1:
-        D.init_process_group(backend="gloo" if args.comm == "staged" else "nccl")
+        # control plane only (barriers, the unique-id exchange, the max-over-ranks time): gloo whenever
+        # the gradients travel on a native communicator, so the native RcclComm is the ONLY RCCL
+        # communicator per rank — a ProcessGroupNCCL next to it would bring its own channels, CTAs and
+        # proxy threads for no traffic. The autograd trainers' DDP all-reduces through the process
+        # group itself, so they keep the nccl backend.
+        control_gloo = args.comm == "staged" or (native_vgg and args.comm == "rccl")
+        D.init_process_group(backend="gloo" if control_gloo else "nccl")
     rank, world = D.get_rank(), D.get_world_size()
     if world != args.gpus and rank == 0:
         print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
-    device = torch.device("cuda", dev_index) if args.comm == "staged" else (D.device() if world > 1
-                                                                             else torch.device("cuda", 0))
+    device = D.device() if world > 1 and D.get_backend() == "nccl" else torch.device("cuda", dev_index)
     torch.cuda.set_device(device)
     trainer = make_trainer(args, device, rank, world)
     # a dead peer leaves RCCL kernels spinning forever: the watchdog turns that into ncclCommAbort
@@ -340,6 +363,12 @@ def main(argv=None) -> int:
         out["vs_stock_torch_per_gpu"] = round(value / world / STOCK_TORCH_IMG_S_PER_GPU, 3)
     if getattr(trainer, "queue_shared", None) is not None:
         out["config"]["hw_queue_shared"] = trainer.queue_shared
+    if world > 1 or args.comm_probe:
+        out["config"]["control_plane"] = D.get_backend() if world > 1 else "none"
+        out["config"]["rccl_version"] = rccl_versions()
+    # a scaling run must never read a number from another transport as the native one: the
+    # fallback keeps its (valid, full-step) number, says so at the top level, and exits 0
+    out["comm_fallback"] = bool(world > 1 and args.comm in ("rccl", "staged") and comm_used != args.comm)
     if hasattr(trainer, "tile_table"):
         # which MFMA math the autotuner picked per conv GEMM: f32-input MFMA, or the fp32-accurate
         # split-bf16 x6 kernels (3 bf16 pieces per operand, 6 MFMAs; f64-checked like the f32 path)
@@ -367,12 +396,13 @@ def main(argv=None) -> int:
     if world > 1:
         D.barrier()
         D.destroy_process_group()
-    if world > 1 and args.comm == "rccl" and comm_used != "rccl":
-        # the number above ran on the fallback transport (torch.distributed over RCCL, collectives
-        # issued from Python), not the native communicator; the JSON's "comm" says which, and the
-        # measurement itself is a valid full step, so the exit status stays 0
-        print(f"[bench] warning: --comm rccl requested but the job ran on {comm_used!r} (native communicator "
-              "construction failed on some rank); see config.comm", file=sys.stderr, flush=True)
+    if out["comm_fallback"]:
+        # the number above ran on the fallback transport (torch.distributed, collectives issued from
+        # Python), not the native communicator: top-level "comm_fallback": true and config.comm say
+        # which; the measurement itself is a valid full step, so the exit status stays 0
+        print(f"[bench] warning: --comm {args.comm} requested but the job ran on {comm_used!r} (native "
+              "communicator construction failed on some rank); see comm_fallback / config.comm",
+              file=sys.stderr, flush=True)
     return 0
 
 

@@ -74,6 +74,7 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], *, 
                   gamma=fin["gamma"], beta=fin["beta"], running_mean=fin.get("running_mean"),
                   running_var=fin.get("running_var"), bnv=bnv, momentum=fin.get("momentum", BN_MOMENTUM),
                   eps=fin.get("eps", BN_EPS))
+    kw.update(_f3_amax(stage, x, w))
     rows = native.C().conv_gemm(FWD, x, w, None, bias, y, _ws(FWD, B, H, W, cin, cout, splits, x.device), st,
                                 B, H, W, cin, cout, w_oihw, bm, bn, splits, bk, stage, **kw)
     if bnv is not None:
@@ -89,7 +90,7 @@ def conv_dgrad(dz: torch.Tensor, w_ohwi: torch.Tensor, B: int, H: int, W: int, *
     cout, _, _, cin = w_ohwi.shape
     dx = torch.empty(B * H * W, cin, device=dz.device, dtype=torch.float32)
     native.C().conv_gemm(DGRAD, None, w_ohwi, dz, None, dx, _ws(DGRAD, B, H, W, cin, cout, splits, dz.device), None,
-                         B, H, W, cin, cout, False, bm, bn, splits, bk, stage)
+                         B, H, W, cin, cout, False, bm, bn, splits, bk, stage, **_f3_amax(stage, dz, w_ohwi))
     return dx
 
 
@@ -99,8 +100,21 @@ def conv_wgrad(dz: torch.Tensor, x: torch.Tensor, cout: int, *, w_oihw: bool = F
     B, H, W, cin = x.shape
     dw = torch.empty(cout * 27 if w_oihw else cout * 9 * cin, device=x.device, dtype=torch.float32)
     native.C().conv_gemm(WGRAD, x, None, dz, None, dw, _ws(WGRAD, B, H, W, cin, cout, splits, x.device), None,
-                         B, H, W, cin, cout, w_oihw, bm, bn, splits, bk, stage)
+                         B, H, W, cin, cout, w_oihw, bm, bn, splits, bk, stage, **_f3_amax(stage, dz, x))
     return dw.view(cout, 3, 3, 3) if w_oihw else dw.view(cout, 3, 3, cin)
+
+
+STAGE_F3 = 64  # launchers.h CS_STAGE_F3
+
+
+def _f3_amax(stage: int, a: torch.Tensor, b: torch.Tensor) -> dict:
+    """The F3 stage's operand bounds (conv_gemm.hip "F3"): |A|max and |B|max as one-float tensors
+    (the engine has them from the operands' producers; here torch computes them)."""
+    if not stage & STAGE_F3:
+        return {}
+    # CS_AMAX_SHARDS (8) floats each: the kernel takes the largest
+    return dict(amax_a=a.detach().abs().max().reshape(1).float().repeat(8),
+                amax_b=b.detach().abs().max().reshape(1).float().repeat(8))
 
 
 class BNState:

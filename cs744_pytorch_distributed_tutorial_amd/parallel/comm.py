@@ -145,7 +145,7 @@ def _all_ok(ok: bool, group) -> bool:
     return int(t.item()) == 1
 
 
-def _agreed(build, group, what: str, prepare=None, share=None) -> Comm:
+def _agreed(build, group, what: str, prepare=None, share=None, fallback_comm=None) -> Comm:
     """Build a native communicator on every rank, or on none, in two agreed phases (a rank that
     cannot join must not leave its peers waiting inside a collective):
 
@@ -153,16 +153,18 @@ def _agreed(build, group, what: str, prepare=None, share=None) -> Comm:
        the device); every rank reports success in one MIN all-reduce, and only if ALL succeeded
     2. ``share(ctx)`` — the collective exchange (the unique id's broadcast), then ``build(shared)``
        (``ncclCommInitRankConfig``), and a second MIN all-reduce on the outcome.
-    Any failure in either phase takes every rank to the torch.distributed communicator.
+    Any failure in either phase takes every rank to ``fallback_comm()`` (default: the
+    torch.distributed communicator).
     ``prepare``/``share`` default to no-ops, so ``build()`` alone gets the one-phase agreement."""
     import sys
 
     import torch.distributed as dist
 
     def fallback(err):
+        comm = fallback_comm() if fallback_comm is not None else TorchComm(group)
         print(f"[comm] native {what} communicator unavailable on some rank ({err!r} here); "
-              "every rank falls back to torch.distributed", file=sys.stderr, flush=True)
-        return TorchComm(group)
+              f"every rank falls back to {comm.kind}", file=sys.stderr, flush=True)
+        return comm
 
     ctx, err = None, None
     try:
@@ -209,9 +211,19 @@ def make_comm(kind: Optional[str] = None, group=None, max_ctas: Optional[int] = 
         return TorchComm(group)
     if kind == "rccl":
         from .rccl import RcclComm
+
+        def fallback_comm():
+            # over a gloo control plane (bench.py's default at --comm rccl) the device buffers travel
+            # through the staged communicator: the same C++ step, collectives host-staged over gloo
+            import torch.distributed as dist
+            if dist.is_initialized() and dist.get_backend(group) == "gloo" and torch.cuda.is_available():
+                from .staged import StagedComm
+                return StagedComm(group)
+            return TorchComm(group)
         ctas = comm_ctas() if max_ctas is None else max_ctas
         return _agreed(lambda uid: RcclComm.build(uid, group, ctas), group, "rccl",
-                       prepare=lambda: RcclComm.prepare(group), share=lambda uid: RcclComm.share_uid(uid, group))
+                       prepare=lambda: RcclComm.prepare(group), share=lambda uid: RcclComm.share_uid(uid, group),
+                       fallback_comm=fallback_comm)
     if kind == "staged":
         from .staged import StagedComm
         return StagedComm(group)

@@ -305,7 +305,7 @@ class NativeTrainer:
         if self.overlap_wgrad and os.environ.get("CS_QUEUE_CHECK", "1") != "0":
             comm_stream = self.native_comm.stream_ptr() if self.native_comm is not None else 0
             with torch.cuda.device(self.device):
-                self.queue_shared = list(C.queue_probe(comm_stream, 0.25))
+                self.queue_shared = list(C.queue_probe(comm_stream, 0.25, self.native_comm is not None))
             if self.queue_shared:
                 import sys
                 print(f"[engine] rank {rank}: streams share a hardware queue ({', '.join(self.queue_shared)}; "
@@ -321,11 +321,6 @@ class NativeTrainer:
         self.comm_defer = self._plan_defer(os.environ.get("CS_COMM_DEFER", "auto"),
                                            world > 1 or str(probe).startswith("xgmi"))
         self.engine.set_comm_defer(self.comm_defer)
-        # BatchNorm finalize: separate launches by default. The in-launch last-arriver finalize
-        # (bn_fin.h, CS_BN_FIN=1) removes one launch per block but measured 6-8 % slower with the
-        # side-stream weight gradients on one box (88.6 k vs 83.3 k img/s at 20/5, 90.3 k vs 83.7 k at
-        # 100/10; profiles/r4_ab_bn_fin.txt) and neutral on the serial step
-        self.engine.set_fin(os.environ.get("CS_BN_FIN", "0") == "1")
         self.engine.set_data(0, self.train_data, self.train_labels, self.aug_train)
         self.engine.set_data(1, self.test_data, self.test_labels, self.aug_test)
         self.idx_buf = self.engine.idx()
@@ -338,10 +333,6 @@ class NativeTrainer:
             self.engine.set_math(3)
         self.tune_us: Optional[List[float]] = None
         self.tile_source = "default"
-        # data-parallel steps (world > 1, or the one-GPU N>1 model) use the table tuned with the
-        # communicator's CTAs holding CUs (scripts/step_tune.py --probe), when one is shipped
-        self._dp_tiles = {"dp": True, "w1": False}.get(os.environ.get("CS_TILE_TABLE", ""),
-                                                        world > 1 or str(probe).startswith("xgmi"))
         if autotune:
             self._tune(model + ("" if dtype == "fp32" else "/bf16"), os.environ.get("CS744_TUNE_CACHE"))
         if graph == "auto":
@@ -389,13 +380,13 @@ class NativeTrainer:
             self._join_lag()
         for t in (self.params, self.mom, self.bufs, self.nbt):
             self.comm.broadcast(t, 0)
+        if getattr(self, "engine", None) is not None:
+            self.engine.params_changed()  # the F3 conv math re-measures the weights' bounds
 
     def _apply_tiles(self, ent: dict) -> bool:
         try:
             for t in ent["tiles"]:  # [block, mode, bm, bn, splits, bk(, stage)]
                 self.engine.set_tile(*t[:6], t[6] if len(t) > 6 else 0)
-            for l, on in enumerate(ent.get("dual", [])):
-                self.engine.set_block_dual(l, bool(on))
         except RuntimeError:  # a table from other kernels: retune
             return False
         self.tune_us = ent["us"]
@@ -418,9 +409,6 @@ class NativeTrainer:
         if os.environ.get("CS744_TUNE", "0") != "1" and os.path.exists(SHIPPED_TILES):
             with open(SHIPPED_TILES) as f:
                 shipped = json.load(f)
-            if self._dp_tiles and key + "/dp" in shipped and self._apply_tiles(shipped[key + "/dp"]):
-                self.tile_source = "shipped-dp"
-                return
             if key in shipped and self._apply_tiles(shipped[key]):
                 self.tile_source = "shipped"
                 return
@@ -429,8 +417,7 @@ class NativeTrainer:
         if cache and self.rank == 0:
             tiles = [[l, m] + list(self.engine.get_tile(l, m)) for l in range(self.layout.L) for m in range(3)
                      if not (l == 0 and m == 1)]
-            db[key] = {"tiles": tiles, "us": self.tune_us,
-                       "dual": [int(self.engine.block_dual(l)) for l in range(self.layout.L)]}
+            db[key] = {"tiles": tiles, "us": self.tune_us}
             with open(cache, "w") as f:
                 json.dump(db, f, indent=1)
 
@@ -556,6 +543,9 @@ class NativeTrainer:
 
     def _capture(self) -> None:
         B = self.B
+        # deferred buckets of an eager step (steps 0-1 run eagerly) are waited for here, outside the
+        # capture: a join inside it would have to cross into a stream that is not being captured
+        self._join_lag()
         self._pool = torch.cuda.graph_pool_handle()
         s = torch.cuda.Stream(device=self.device)
         s.wait_stream(torch.cuda.current_stream())
@@ -682,9 +672,8 @@ class NativeTrainer:
         return out
 
     def _join_lag(self) -> None:
-        """The current stream waits for weight gradients / SGD the engine deferred into the next
-        step (CS_WGRAD_LAG) and for deferred buckets' all-reduce + SGD (CS_COMM_DEFER): every host
-        read of the parameters goes through here."""
+        """The current stream waits for deferred buckets' all-reduce + SGD (CS_COMM_DEFER): every
+        host read of the parameters goes through here."""
         if self.engine is not None:
             self.engine.join_lag()
 
@@ -695,6 +684,7 @@ class NativeTrainer:
     def load_state_dict(self, sd: Dict[str, torch.Tensor]) -> None:
         self._join_lag()
         self.layout.pack(sd, self.params, self.bufs, self.nbt)
+        self.engine.params_changed()  # the F3 conv math re-measures the weights' bounds
 
     def optimizer_state_dict(self) -> dict:
         """torch.optim.SGD ``state_dict`` format (momentum_buffer per parameter index)."""
@@ -742,10 +732,10 @@ class NativeTrainer:
         return self.layout.unpack_grads(self.grads)
 
     @classmethod
-    def from_bench_args(cls, args, device, rank, world) -> "NativeTrainer":
+    def from_bench_args(cls, args, device, rank, world, probe: Optional[str] = None) -> "NativeTrainer":
         return cls(model=args.model, batch_size=args.batch_size, device=device, rank=rank, world=world,
                    sync=args.sync, comm=args.comm, bucket_mb=args.bucket_mb, dtype=args.dtype,
-                   graph="none" if args.no_graph else getattr(args, "graph", "auto"))
+                   graph="none" if args.no_graph else getattr(args, "graph", "auto"), probe=probe)
 
 
 def run_native(cfg, device, logger) -> dict:

@@ -32,7 +32,8 @@ int64_t conv_gemm(int64_t mode, c10::optional<torch::Tensor> x, c10::optional<to
                   int64_t stage, c10::optional<torch::Tensor> fin_cnt, c10::optional<torch::Tensor> fin_grp,
                   c10::optional<torch::Tensor> gamma, c10::optional<torch::Tensor> beta,
                   c10::optional<torch::Tensor> running_mean, c10::optional<torch::Tensor> running_var,
-                  c10::optional<torch::Tensor> bnv, double momentum, double eps) {
+                  c10::optional<torch::Tensor> bnv, double momentum, double eps, c10::optional<torch::Tensor> amax_a,
+                  c10::optional<torch::Tensor> amax_b) {
   TORCH_CHECK(mode >= 0 && mode <= 2, "conv_gemm: bad mode");
   TORCH_CHECK(pow2(H) && pow2(W) && pow2(Cin) && pow2(Cout) && Cin >= 4 && Cout >= 64 && B > 0,
               "conv_gemm: H, W, Cin, Cout must be powers of two (Cin>=4, Cout>=64)");
@@ -86,6 +87,11 @@ int64_t conv_gemm(int64_t mode, c10::optional<torch::Tensor> x, c10::optional<to
   DevGuard g(out.device());
   a.x = cptr(x); a.w = cptr(w); a.dz = cptr(dz); a.bias = cptr(bias);
   a.out = out.data_ptr<float>(); a.ws = mptr(ws); a.stats = mptr(stats);
+  // CS_STAGE_F3: GPU tensors of CS_AMAX_SHARDS floats whose maximum bounds |A| / |B| (the scales' source)
+  check_t(amax_a, CS_AMAX_SHARDS, "amax_a"); check_t(amax_b, CS_AMAX_SHARDS, "amax_b");
+  a.amax_a = cptr(amax_a); a.amax_b = cptr(amax_b);
+  TORCH_CHECK(!(stage & CS_STAGE_F3) || (a.amax_a != nullptr && a.amax_b != nullptr),
+              "conv_gemm: the F3 stage needs amax_a and amax_b");
   TORCH_CHECK(cs_conv_stage_ok((int)stage, (int)bm, (int)bn, (int)bk, w_oihw && mode == CS_CONV_FWD) &&
                   !(bk == 64 && w_oihw && mode == CS_CONV_FWD),
               "conv_gemm: no kernel for stage ", stage, " / ", bm, "x", bn, " / bk ", bk);
@@ -203,7 +209,7 @@ void register_conv_ops(pybind11::module& m) {
         py::arg("stage") = 0, py::arg("fin_cnt") = py::none(), py::arg("fin_grp") = py::none(),
         py::arg("gamma") = py::none(), py::arg("beta") = py::none(), py::arg("running_mean") = py::none(),
         py::arg("running_var") = py::none(), py::arg("bnv") = py::none(), py::arg("momentum") = 0.1,
-        py::arg("eps") = 1e-5);
+        py::arg("eps") = 1e-5, py::arg("amax_a") = py::none(), py::arg("amax_b") = py::none());
   m.def("bn_fin_sizes", [](int64_t T, int64_t C, int64_t nc) {
     return std::vector<int64_t>{cs_bn_fin_ints((int)T, (int)C, (int)nc), cs_bn_fin_grp_floats((int)T, (int)C, (int)nc)};
   }, "(ticket ints, group-partial floats) of an in-launch BN finalize over T row tiles, C channels, nc-wide column tiles");

@@ -48,26 +48,27 @@ void register_runtime(pybind11::module& m) {
   namespace py = pybind11;
   m.def(
       "queue_probe",
-      [](intptr_t comm_stream, double timeout_s) {
+      [](intptr_t comm_stream, double timeout_s, bool with_comm) {
         // pairs of {main = the current stream, side = the engine's side stream, comm} that share one
-        // hardware queue (device_comm.h streams_share_queue); comm_stream 0 = the reserved comm stream
+        // hardware queue (device_comm.h streams_share_queue); comm_stream 0 = the reserved comm stream.
+        // with_comm = false (no communicator: world 1): only main/side — the comm stream is never
+        // used then, and a shared queue there must not turn the overlap off
         hipStream_t main_s = cur_stream(), side = cs::reserved_side_stream();
         hipStream_t comm = comm_stream ? reinterpret_cast<hipStream_t>(comm_stream) : cs::reserved_comm_stream();
         std::vector<std::string> out;
         const std::pair<const char*, std::pair<hipStream_t, hipStream_t>> pairs[] = {
             {"main/side", {main_s, side}}, {"main/comm", {main_s, comm}}, {"side/comm", {side, comm}}};
-        for (const auto& pr : pairs)
+        for (const auto& pr : pairs) {
+          if (!with_comm && pr.second.second == comm) continue;
           if (cs::streams_share_queue(pr.second.first, pr.second.second, timeout_s)) out.emplace_back(pr.first);
+        }
         return out;
       },
-      py::arg("comm_stream") = 0, py::arg("timeout_s") = 0.25,
+      py::arg("comm_stream") = 0, py::arg("timeout_s") = 0.25, py::arg("with_comm") = true,
       "start-up check: which of the main / side / comm streams share a hardware queue");
   m.def("rccl_unique_id", []() { return py::bytes(cs::RcclComm::unique_id()); });
-  m.def("rccl_version", []() {
-    int v = 0;
-    ncclGetVersion(&v);
-    return v;
-  });
+  m.def("rccl_version", []() { return py::make_tuple(cs::RcclComm::runtime_version(), cs::RcclComm::header_version()); },
+        "(ncclGetVersion() of the loaded RCCL, NCCL_VERSION_CODE of the header built against)");
   // the engine's communicator interface (device_comm.h): RcclComm, StagedComm, ProbeComm
   py::class_<cs::DeviceComm>(m, "DeviceComm")
       .def_property_readonly("rank", &cs::DeviceComm::rank)
@@ -199,31 +200,26 @@ void register_runtime(pybind11::module& m) {
            py::arg("wd"), py::arg("dampening"))
       .def("set_sgd_first", &cs::VggEngine::set_sgd_first)
       .def("set_sgd_tail", &cs::VggEngine::set_sgd_tail)
-      .def("set_fin", &cs::VggEngine::set_fin)
       .def("set_debug_skip", &cs::VggEngine::set_debug_skip)
       .def("set_timing", &cs::VggEngine::set_timing)
       .def("set_math", &cs::VggEngine::set_math)
       .def("phase_times", &cs::VggEngine::phase_times)
       .def("link_error", &cs::VggEngine::link_error)
-      .def("set_stagger", &cs::VggEngine::set_stagger)
-      .def("set_lag", &cs::VggEngine::set_lag)
       .def("set_conv0_direct", &cs::VggEngine::set_conv0_direct)
       .def("set_conv0_bn_fold", &cs::VggEngine::set_conv0_bn_fold)
       .def("set_conv0_sgd_fold", &cs::VggEngine::set_conv0_sgd_fold)
       .def("set_conv0_batch_fold", &cs::VggEngine::set_conv0_batch_fold)
       .def("set_head_bn_fold", &cs::VggEngine::set_head_bn_fold)
       .def("set_side_sgd_tail", &cs::VggEngine::set_side_sgd_tail)
-      .def("set_head_tail", &cs::VggEngine::set_head_tail)
       .def("conv0_direct", &cs::VggEngine::conv0_direct)
       .def("join_lag", &cs::VggEngine::join_lag)
       .def("set_comm_defer", &cs::VggEngine::set_comm_defer)
+      .def("set_f3_probe", &cs::VggEngine::set_f3_probe)
+      .def("params_changed", &cs::VggEngine::params_changed)
+      .def("amax", &cs::VggEngine::amax)
       .def("comm_defer", &cs::VggEngine::comm_defer)
       .def("defer_pending", &cs::VggEngine::defer_pending)
-      .def("set_bn_fused_limits", &cs::VggEngine::set_bn_fused_limits, py::arg("fwd_t"), py::arg("bwd_p"))
-      .def("set_dual", &cs::VggEngine::set_dual)
       .def("set_bn_fused_rows", &cs::VggEngine::set_bn_fused_rows)
-      .def("block_dual", &cs::VggEngine::block_dual)
-      .def("set_block_dual", &cs::VggEngine::set_block_dual)
       .def("set_tile", &cs::VggEngine::set_tile, py::arg("block"), py::arg("mode"), py::arg("bm"), py::arg("bn"),
            py::arg("splits"), py::arg("bk") = 16, py::arg("stage") = 0)
       .def("get_tile", &cs::VggEngine::get_tile)

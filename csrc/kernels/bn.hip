@@ -176,12 +176,13 @@ __device__ __forceinline__ float4 bnrelu4(float4 y, float4 s, float4 t) {
 // one thread per (output position, 4 channels)
 __global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__ y, const float* __restrict__ scale,
                                                        const float* __restrict__ shift, float* __restrict__ out,
-                                                       int B, int H, int W, int C, int pool) {
+                                                       int B, int H, int W, int C, int pool, float* __restrict__ amax) {
   const int C4 = C >> 2;
   const int Ho = pool ? H >> 1 : H, Wo = pool ? W >> 1 : W;
   const int total = B * Ho * Wo * C4;
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= total) return;
+  const int t0 = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool live = t0 < total;
+  const int t = live ? t0 : 0;  // (every lane stays for the wave's bound)
   const int cq = t % C4, pos = t / C4;
   const float4 s = reinterpret_cast<const float4*>(scale)[cq];
   const float4 sh = reinterpret_cast<const float4*>(shift)[cq];
@@ -197,7 +198,9 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__
     r = make_float4(fmaxf(fmaxf(a0.x, a1.x), fmaxf(a2.x, a3.x)), fmaxf(fmaxf(a0.y, a1.y), fmaxf(a2.y, a3.y)),
                     fmaxf(fmaxf(a0.z, a1.z), fmaxf(a2.z, a3.z)), fmaxf(fmaxf(a0.w, a1.w), fmaxf(a2.w, a3.w)));
   }
-  reinterpret_cast<float4*>(out)[t] = r;
+  if (live) reinterpret_cast<float4*>(out)[t] = r;
+  // the output bound the next conv's F3 math scales by (ReLU output: non-negative)
+  if (amax != nullptr) cs::wave_amax_publish(live ? fmaxf(fmaxf(r.x, r.y), fmaxf(r.z, r.w)) : 0.f, amax);
 }
 
 template <bool APPLY, bool POOL>
@@ -206,7 +209,7 @@ __global__ __launch_bounds__(256) void bn_bwd_kernel(const float* __restrict__ y
                                                      const float* __restrict__ shift, const float* __restrict__ mean,
                                                      const float* __restrict__ invstd, const float* __restrict__ coef,
                                                      float* __restrict__ dz, float* __restrict__ part,
-                                                     unsigned long long* __restrict__ signal) {
+                                                     unsigned long long* __restrict__ signal, float* __restrict__ amax) {
   extern __shared__ __attribute__((aligned(16))) float red[];  // [rows][C][3] (reduce only)
   // a deferred stream-link signal (device_comm.h StreamLink::defer): this launch started, so the
   // kernels before it on the stream completed
@@ -222,11 +225,16 @@ __global__ __launch_bounds__(256) void bn_bwd_kernel(const float* __restrict__ y
   const int cq = threadIdx.x % C4, rl = threadIdx.x / C4;
   const int units = POOL ? B * (H >> 1) * (W >> 1) : B * H * W;
   float acc[3][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  float vm = 0.f;
   if (rl < rows) {
     for (int u = blockIdx.x * rows + rl; u < units; u += gridDim.x * rows)
-      bwd_visit<APPLY, POOL>(y, G, B, H, W, C, cq, u, scale, shift, mean, invstd, coef, dz, acc);
+      bwd_visit<APPLY, POOL>(y, G, B, H, W, C, cq, u, scale, shift, mean, invstd, coef, dz, acc, 0,
+                             APPLY && amax != nullptr ? &vm : nullptr);
   }
-  if (APPLY) return;
+  if (APPLY) {
+    if (amax != nullptr) cs::wave_amax_publish(vm, amax);  // the dZ bound (F3 conv math)
+    return;
+  }
   if (rl < rows) {
 #pragma unroll
     for (int k = 0; k < 3; ++k)
@@ -475,7 +483,8 @@ __global__ __launch_bounds__(256) void bn_fused_bwd_kernel(const float* __restri
                                                            const float* __restrict__ gamma, float* __restrict__ coef,
                                                            float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                            float* __restrict__ dbias, float* __restrict__ dz,
-                                                           unsigned long long* __restrict__ signal) {
+                                                           unsigned long long* __restrict__ signal,
+                                                           float* __restrict__ amax) {
   __shared__ float lds[4 * 4 * 3 * 4];
   __shared__ float coef_sh[3 * kFusedCh];  // this block's 16 channels' dZ coefficients
   // a deferred stream-link signal (device_comm.h StreamLink::defer): this launch started, so the
@@ -518,8 +527,11 @@ __global__ __launch_bounds__(256) void bn_fused_bwd_kernel(const float* __restri
   }
   __syncthreads();  // the apply pass reads the coefficients from LDS (no global round trip)
   float dummy[3][4];
+  float vm = 0.f;
   for (int u = rl; u < units; u += 64)
-    bwd_visit<true, POOL>(y, G, B, H, W, C, cqg, u, scale, shift, mean, invstd, coef_sh, dz, dummy, c0);
+    bwd_visit<true, POOL>(y, G, B, H, W, C, cqg, u, scale, shift, mean, invstd, coef_sh, dz, dummy, c0,
+                          amax != nullptr ? &vm : nullptr);
+  if (amax != nullptr) cs::wave_amax_publish(vm, amax);  // the dZ bound (F3 conv math)
 }
 
 // grid (C/16, row chunks): finalize the BN backward of this block's 16 channels from the P
@@ -634,32 +646,33 @@ hipError_t cs_bn_eval_coeffs(const float* gamma, const float* beta, const float*
 }
 
 hipError_t cs_bn_apply(const float* y, const float* scale, const float* shift, float* out, int B, int H, int W, int C,
-                       int pool, hipStream_t stream) {
+                       int pool, hipStream_t stream, float* amax) {
   if (C % 4 != 0 || (pool && ((H | W) & 1))) return hipErrorInvalidValue;
   const int total = B * (pool ? H / 2 : H) * (pool ? W / 2 : W) * (C / 4);
   if (total == 0) return hipSuccess;
   hipLaunchKernelGGL(bn_apply_kernel, dim3((total + 255) / 256), dim3(256), 0, stream, y, scale, shift, out, B, H, W,
-                     C, pool);
+                     C, pool, amax);
   return hipGetLastError();
 }
 
 hipError_t cs_bn_bwd(const float* y, const float* G, int B, int H, int W, int C, int pool, const float* scale,
                      const float* shift, const float* mean, const float* invstd, const float* gamma, float* part,
-                     float* coef, float* dgamma, float* dbeta, float* dbias, float* dz, hipStream_t stream) {
+                     float* coef, float* dgamma, float* dbeta, float* dbias, float* dz, hipStream_t stream,
+                     float* amax) {
   if (C % 4 != 0 || C > 1024 || (pool && ((H | W) & 1))) return hipErrorInvalidValue;
   const int P = cs_bn_bwd_blocks(B, H, W, C, pool);
   const int rows = 256 / (C / 4);
   const size_t lds = (size_t)rows * C * 3 * sizeof(float);
   if (pool) {
     hipLaunchKernelGGL((bn_bwd_kernel<false, true>), dim3(P), dim3(256), lds, stream, y, G, B, H, W, C, scale, shift,
-                       mean, invstd, nullptr, nullptr, part, nullptr);
+                       mean, invstd, nullptr, nullptr, part, nullptr, nullptr);
   } else {
     hipLaunchKernelGGL((bn_bwd_kernel<false, false>), dim3(P), dim3(256), lds, stream, y, G, B, H, W, C, scale, shift,
-                       mean, invstd, nullptr, nullptr, part, nullptr);
+                       mean, invstd, nullptr, nullptr, part, nullptr, nullptr);
   }
   if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
   return cs_bn_bwd_tail(y, G, B, H, W, C, pool, scale, shift, mean, invstd, gamma, part, P, coef, dgamma, dbeta,
-                        dbias, dz, stream);
+                        dbias, dz, stream, nullptr, amax);
 }
 
 hipError_t cs_bn_bwd_finalize(const float* part, int P, int C, int M, const float* gamma, const float* invstd,
@@ -674,7 +687,7 @@ hipError_t cs_bn_bwd_finalize(const float* part, int P, int C, int M, const floa
 hipError_t cs_bn_bwd_tail(const float* y, const float* G, int B, int H, int W, int C, int pool, const float* scale,
                           const float* shift, const float* mean, const float* invstd, const float* gamma,
                           const float* part, int P, float* coef, float* dgamma, float* dbeta, float* dbias, float* dz,
-                          hipStream_t stream, unsigned long long* signal) {
+                          hipStream_t stream, unsigned long long* signal, float* amax) {
   if (C % 4 != 0 || C > 1024 || (pool && ((H | W) & 1)) || P < 1) return hipErrorInvalidValue;
   const int M = B * H * W;
   const int rows = 256 / (C / 4);
@@ -686,10 +699,10 @@ hipError_t cs_bn_bwd_tail(const float* y, const float* G, int B, int H, int W, i
   if (blocks > 2048) blocks = 2048;
   if (pool) {
     hipLaunchKernelGGL((bn_bwd_kernel<true, true>), dim3(blocks), dim3(256), 0, stream, y, G, B, H, W, C, scale, shift,
-                       mean, invstd, coef, dz, nullptr, nullptr);
+                       mean, invstd, coef, dz, nullptr, nullptr, amax);
   } else {
     hipLaunchKernelGGL((bn_bwd_kernel<true, false>), dim3(blocks), dim3(256), 0, stream, y, G, B, H, W, C, scale,
-                       shift, mean, invstd, coef, dz, nullptr, nullptr);
+                       shift, mean, invstd, coef, dz, nullptr, nullptr, amax);
   }
   return hipGetLastError();
 }
@@ -704,10 +717,10 @@ hipError_t cs_bn_bwd_apply(const float* y, const float* G, int B, int H, int W, 
   if (blocks > 2048) blocks = 2048;
   if (pool)
     hipLaunchKernelGGL((bn_bwd_kernel<true, true>), dim3(blocks), dim3(256), 0, stream, y, G, B, H, W, C, scale, shift,
-                       mean, invstd, coef, dz, nullptr, signal);
+                       mean, invstd, coef, dz, nullptr, signal, nullptr);
   else
     hipLaunchKernelGGL((bn_bwd_kernel<true, false>), dim3(blocks), dim3(256), 0, stream, y, G, B, H, W, C, scale,
-                       shift, mean, invstd, coef, dz, nullptr, signal);
+                       shift, mean, invstd, coef, dz, nullptr, signal, nullptr);
   return hipGetLastError();
 }
 
@@ -747,13 +760,13 @@ hipError_t cs_bn_bwd_tail_fused(const float* y, const float* G, int B, int H, in
 
 hipError_t cs_bn_fused_bwd(const float* y, const float* G, int B, int H, int W, int C, int pool, const float* bnv,
                            const float* gamma, float* coef, float* dgamma, float* dbeta, float* dbias, float* dz,
-                           hipStream_t stream, unsigned long long* signal) {
+                           hipStream_t stream, unsigned long long* signal, float* amax) {
   if (C % kFusedCh != 0 || (pool && ((H | W) & 1))) return hipErrorInvalidValue;
   if (pool)
     hipLaunchKernelGGL((bn_fused_bwd_kernel<true>), dim3(C / kFusedCh), dim3(256), 0, stream, y, G, B, H, W, C, bnv,
-                       gamma, coef, dgamma, dbeta, dbias, dz, signal);
+                       gamma, coef, dgamma, dbeta, dbias, dz, signal, amax);
   else
     hipLaunchKernelGGL((bn_fused_bwd_kernel<false>), dim3(C / kFusedCh), dim3(256), 0, stream, y, G, B, H, W, C, bnv,
-                       gamma, coef, dgamma, dbeta, dbias, dz, signal);
+                       gamma, coef, dgamma, dbeta, dbias, dz, signal, amax);
   return hipGetLastError();
 }

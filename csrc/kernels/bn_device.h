@@ -19,7 +19,7 @@ template <bool APPLY, bool POOL>
 __device__ __forceinline__ void bwd_visit(const float* __restrict__ y, const float* __restrict__ G, int B, int H,
                                           int W, int C, int cq, int unit, const float* scale, const float* shift,
                                           const float* mean, const float* invstd, const float* coef, float* dz,
-                                          float (&acc)[3][4], int coef_c0 = 0) {
+                                          float (&acc)[3][4], int coef_c0 = 0, float* vmax = nullptr) {
   const int C4 = C >> 2;
   float sc[4], sh[4], mu[4], is[4], k1[4], k2[4], k3[4];
 #pragma unroll
@@ -80,6 +80,11 @@ __device__ __forceinline__ void bwd_visit(const float* __restrict__ y, const flo
 #pragma unroll
     for (int p = 0; p < NP; ++p)
       reinterpret_cast<float4*>(dz)[off[p]] = make_float4(out[p][0], out[p][1], out[p][2], out[p][3]);
+    if (vmax != nullptr)  // the dZ bound the F3 conv math scales by
+#pragma unroll
+      for (int p = 0; p < NP; ++p)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) *vmax = fmaxf(*vmax, fabsf(out[p][q]));
   }
 }
 

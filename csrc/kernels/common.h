@@ -50,6 +50,14 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
   return red[0];
 }
 
+// The F3 conv math's operand bounds (launchers.h CS_AMAX_SHARDS): every wave of a producer folds
+// |its values| into one atomic max on shard blockIdx % 8 (the float bits of a non-negative value
+// order like unsigned ints; a NaN, above +inf, wins). All 64 lanes must be active.
+__device__ __forceinline__ void wave_amax_publish(float v, float* amax) {
+  v = wave_max(v);
+  if ((threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<unsigned*>(amax) + (blockIdx.x & 7), __float_as_uint(v));
+}
+
 // XCD-aware bijective block remap (cdna_hip_programming.md §5, "XCD swizzle must be
 // bijective"): blocks b and b+8 share an XCD, so hand each XCD a contiguous range.
 __device__ __forceinline__ int xcd_remap(int orig, int nwg) {

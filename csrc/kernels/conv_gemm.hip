@@ -467,16 +467,83 @@ __device__ __forceinline__ bf16x4 round4(const float4 v) {
   return h;
 }
 
+// ---------------------------------------------------------------- F3: scaled fp16 hi/lo, 3 MFMAs
+// gfx950's f16 MFMA (v_mfma_f32_32x32x16_f16) runs at the bf16 rate with 11-bit significands, so
+// two fp16 pieces carry 22 bits where bf16 needs three: x*2^s = h + l, h = fp16(x*2^s) and
+// l = fp16(x*2^s - h) (the residual is exact in f32; |l| <= 2^-11 |x*2^s|, its rounding <= 2^-23).
+// fp16's range is the catch: each operand tensor gets one power-of-two scale 2^s from its absolute
+// maximum (CsConvArgs::amax_a / amax_b, written by the operand's producer) so that its largest
+// element lands in [2^14, 2^15) — nothing overflows, and the subnormal floor (2^-25 absolute) is
+// 2^-40 of the tensor's maximum. The product is hl + lh + hh (the dropped ll <= 2^-22 |a||b|),
+// accumulated in f32 by the MFMA, then scaled back by 2^-(sa+sb) in the epilogue (exact): a
+// 32x32x16 product costs 3 x 32 MFMA cycles (X6S: 6 x 32) and the LDS holds two planes, not three.
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+// 2^s for an operand whose absolute maximum is the largest of amax[0..CS_AMAX_SHARDS) (the
+// producers' per-XCD atomic-max shards): its largest element scales into [2^14, 2^15)
+__device__ __forceinline__ int f3_exp(const float* amax) {
+  if (amax == nullptr) return 0;
+  unsigned bits = 0;
+#pragma unroll
+  for (int i = 0; i < CS_AMAX_SHARDS; ++i) {  // as bit patterns: a NaN (above +inf) wins and gives s = 0
+    const unsigned u = __builtin_bit_cast(unsigned, amax[i]) & 0x7fffffffu;
+    bits = u > bits ? u : bits;
+  }
+  const int e = (int)(bits >> 23);
+  if (e == 0 || e == 255) return 0;  // zero / subnormal max, or inf / nan (propagates as is)
+  const int s = 14 - (e - 127);
+  return s < -100 ? -100 : (s > 100 ? 100 : s);
+}
+__device__ __forceinline__ float exp2i(int s) { return __builtin_bit_cast(float, (unsigned)(s + 127) << 23); }
+
+__device__ __forceinline__ void split2h(const float4 v, float sc, bf16x4& h, bf16x4& l) {
+  const float x[4] = {v.x * sc, v.y * sc, v.z * sc, v.w * sc};
+  f16x4 hv, lv;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const _Float16 hj = (_Float16)x[j];
+    hv[j] = hj;
+    lv[j] = (_Float16)(x[j] - (float)hj);
+  }
+  h = __builtin_bit_cast(bf16x4, hv);
+  l = __builtin_bit_cast(bf16x4, lv);
+}
+
+template <int RM, int RN>
+__device__ __forceinline__ void mma_f3(const bf16x8 (&ah)[RM], const bf16x8 (&al)[RM], const bf16x8 (&bh)[RN],
+                                       const bf16x8 (&bl)[RN], f32x16 (&acc)[RM][RN]) {
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j) {  // small terms first
+      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, ah[i]),
+                                                         __builtin_bit_cast(f16x8, bl[j]), acc[i][j], 0, 0, 0);
+      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, al[i]),
+                                                         __builtin_bit_cast(f16x8, bh[j]), acc[i][j], 0, 0, 0);
+      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, ah[i]),
+                                                         __builtin_bit_cast(f16x8, bh[j]), acc[i][j], 0, 0, 0);
+    }
+}
+
+// NP = 3: X6S split (h, m, l bf16); 2: F3 split (h, l fp16 of the scaled value, as 16-bit words);
+// 1: bf16 rounding
 template <int BM, int BN, int MODE, int BK, bool C4, int KG, int S, int NP = 3>
 __device__ __forceinline__ void store_xs(const Loader<BM, BN, MODE, BK, C4, false, KG>& ld, __bf16* As, __bf16* Bs,
                                          const int (&oa)[Tile<BM, BN, MODE, BK, false, KG>::AC],
-                                         const int (&ob)[Tile<BM, BN, MODE, BK, false, KG>::BC]) {
+                                         const int (&ob)[Tile<BM, BN, MODE, BK, false, KG>::BC], float sa = 1.f,
+                                         float sb = 1.f) {
   using T = Tile<BM, BN, MODE, BK, false, KG>;  // chunk counts depend on the block's thread count
   using X = TileXS<BM, BN, MODE, BK, NP>;
 #pragma unroll
   for (int i = 0; i < T::AC; ++i) {
     if constexpr (NP == 1) {
       *reinterpret_cast<bf16x4*>(As + oa[i]) = round4(ld.ra[S][i]);
+    } else if constexpr (NP == 2) {
+      bf16x4 h, l;
+      split2h(ld.ra[S][i], sa, h, l);
+      *reinterpret_cast<bf16x4*>(As + oa[i]) = h;
+      *reinterpret_cast<bf16x4*>(As + X::PLA + oa[i]) = l;
     } else {
       bf16x4 h, m, l;
       split4(ld.ra[S][i], h, m, l);
@@ -489,6 +556,11 @@ __device__ __forceinline__ void store_xs(const Loader<BM, BN, MODE, BK, C4, fals
   for (int i = 0; i < T::BC; ++i) {
     if constexpr (NP == 1) {
       *reinterpret_cast<bf16x4*>(Bs + ob[i]) = round4(ld.rb[S][i]);
+    } else if constexpr (NP == 2) {
+      bf16x4 h, l;
+      split2h(ld.rb[S][i], sb, h, l);
+      *reinterpret_cast<bf16x4*>(Bs + ob[i]) = h;
+      *reinterpret_cast<bf16x4*>(Bs + X::PLB + ob[i]) = l;
     } else {
       bf16x4 h, m, l;
       split4(ld.rb[S][i], h, m, l);
@@ -527,7 +599,8 @@ __device__ __forceinline__ void kstep_xs(Loader<BM, BN, MODE, BK, C4, false, KG>
                                          f32x16 (&acc)[Tile<BM, BN, MODE, BK>::RM][Tile<BM, BN, MODE, BK>::RN],
                                          int wm, int wn, int kg, int k_load,
                                          const int (&oa)[Tile<BM, BN, MODE, BK, false, KG>::AC],
-                                         const int (&ob)[Tile<BM, BN, MODE, BK, false, KG>::BC]) {
+                                         const int (&ob)[Tile<BM, BN, MODE, BK, false, KG>::BC], float sa,
+                                         float sb) {
   using T = Tile<BM, BN, MODE, BK>;
   using X = TileXS<BM, BN, MODE, BK, NP>;
   constexpr int NGK = T::NG / KG;
@@ -545,6 +618,11 @@ __device__ __forceinline__ void kstep_xs(Loader<BM, BN, MODE, BK, C4, false, KG>
 #pragma unroll
         for (int j = 0; j < T::RN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+    } else if constexpr (NP == 2) {
+      bf16x8 al[T::RM], bl[T::RN];
+      read_xs<T::RM, T::A_KC, X::PA, BK>(cur + X::PLA, wm * T::WM, g0 + gp, lane, al);
+      read_xs<T::RN, T::B_KC, X::PB, BK>(Bc + X::PLB, wn * T::WN, g0 + gp, lane, bl);
+      mma_f3<T::RM, T::RN>(ah, al, bh, bl, acc);
     } else {
       bf16x8 am[T::RM], al[T::RM], bm[T::RN], bl[T::RN];
       read_xs<T::RM, T::A_KC, X::PA, BK>(cur + X::PLA, wm * T::WM, g0 + gp, lane, am);
@@ -554,7 +632,7 @@ __device__ __forceinline__ void kstep_xs(Loader<BM, BN, MODE, BK, C4, false, KG>
       mma_x6f<T::RM, T::RN>(ah, am, al, bh, bm, bl, acc);
     }
     if (gp == 0) ld.template load<LS>(a, k_load);
-    if (gp == (NGK > 2 ? 2 : 0)) store_xs<BM, BN, MODE, BK, C4, KG, SS, NP>(ld, nxt, nxt + X::A16, oa, ob);
+    if (gp == (NGK > 2 ? 2 : 0)) store_xs<BM, BN, MODE, BK, C4, KG, SS, NP>(ld, nxt, nxt + X::A16, oa, ob, sa, sb);
   }
 }
 
@@ -624,7 +702,7 @@ __device__ __forceinline__ void kcompute_gl(const float* cur,
 // while tile t is multiplied, one raw s_barrier per K-step after a counted vmcnt (tile t
 // landed, newer tiles may still be in flight); no register stage, no ds_write.
 // One output tile (`tile`, already XCD-remapped) x one K split of a conv GEMM; the body of
-// both the single-GEMM kernel and the dual (wgrad + dgrad) kernel.
+// the GEMM kernel.
 template <int BM, int BN, int MODE, int BK, int SCHED, bool C4, int GL, int KG = 1>
 __device__ __forceinline__ void gemm_body(const CsConvArgs& a, const int tile, const int split, const int nsplit,
                                           float* smem) {
@@ -678,9 +756,12 @@ __device__ __forceinline__ void gemm_body(const CsConvArgs& a, const int tile, c
       cur = cur == NB - 1 ? 0 : cur + 1;
     }
     __syncthreads();  // every wave's fragment reads are done before the epilogue reuses LDS
-  } else if constexpr (SCHED == 3 || SCHED == 5) {
-    constexpr int NP = SCHED == 5 ? 1 : 3;  // SCHED 5: bf16 operands (h plane only)
+  } else if constexpr (SCHED == 3 || SCHED == 5 || SCHED == 6) {
+    // SCHED 5: bf16 operands (h plane only); SCHED 6: F3 (scaled fp16 h / l planes)
+    constexpr int NP = SCHED == 5 ? 1 : (SCHED == 6 ? 2 : 3);
     using X = TileXS<BM, BN, MODE, BK, NP>;
+    const int ea = SCHED == 6 ? f3_exp(a.amax_a) : 0, eb = SCHED == 6 ? f3_exp(a.amax_b) : 0;
+    const float sa = exp2i(ea), sb = exp2i(eb);
     Loader<BM, BN, MODE, BK, C4, false, KG> ld;
     ld.init(a, m0, n0);
     using TK = Tile<BM, BN, MODE, BK, false, KG>;
@@ -694,15 +775,26 @@ __device__ __forceinline__ void gemm_body(const CsConvArgs& a, const int tile, c
     if (nks > 0) {
       ld.template load<0>(a, ks_begin * BK);
       if (nks > 1) ld.template load<1>(a, (ks_begin + 1) * BK);
-      store_xs<BM, BN, MODE, BK, C4, KG, 0, NP>(ld, l0, l0 + X::A16, oa, ob);
+      store_xs<BM, BN, MODE, BK, C4, KG, 0, NP>(ld, l0, l0 + X::A16, oa, ob, sa, sb);
     }
     __syncthreads();
     for (int t = 0; t < nks; t += 2) {
-      kstep_xs<BM, BN, MODE, BK, 0, 1, C4, KG, NP>(ld, a, l0, l1, acc, wm, wn, kg, (ks_begin + t + 2) * BK, oa, ob);
+      kstep_xs<BM, BN, MODE, BK, 0, 1, C4, KG, NP>(ld, a, l0, l1, acc, wm, wn, kg, (ks_begin + t + 2) * BK, oa, ob,
+                                                   sa, sb);
       __syncthreads();
       if (t + 1 >= nks) break;
-      kstep_xs<BM, BN, MODE, BK, 1, 0, C4, KG, NP>(ld, a, l1, l0, acc, wm, wn, kg, (ks_begin + t + 3) * BK, oa, ob);
+      kstep_xs<BM, BN, MODE, BK, 1, 0, C4, KG, NP>(ld, a, l1, l0, acc, wm, wn, kg, (ks_begin + t + 3) * BK, oa, ob,
+                                                   sa, sb);
       __syncthreads();
+    }
+    if constexpr (SCHED == 6) {  // back to the operands' scale (a power of two: exact)
+      const float un = exp2i(-(ea + eb));
+#pragma unroll
+      for (int i = 0; i < T::RM; ++i)
+#pragma unroll
+        for (int j = 0; j < T::RN; ++j)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) acc[i][j][e] *= un;
     }
   } else {
   Loader<BM, BN, MODE, BK, C4, false, KG> ld;
@@ -742,34 +834,11 @@ __global__ __launch_bounds__(256 * KG) void conv_gemm_kernel(CsConvArgs a) {
   // dispatched them), then sgd.P blocks of an independent SGD update that run in the GEMM's tail
   const int nsplit = (a.total_ksteps + a.ksteps_per_split - 1) / a.ksteps_per_split;
   const int ng = ntiles * nsplit, lin = blockIdx.x;
-  if (a.start_sig != nullptr && lin == 0 && threadIdx.x == 0)
-    __hip_atomic_fetch_add(a.start_sig, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (lin >= ng + a.sgd.P) {  // the classifier's column pass: one piece per wave
-    const int hb = (lin - ng - a.sgd.P) * KG * 4 + (int)(threadIdx.x >> 6);
-    if (hb < a.head.P) cs_head::cols_wave(a.head, hb, threadIdx.x & 63);
-    return;
-  }
   if (lin >= ng) {
     cs_sgd::tail_body(a.sgd, lin - ng, a.sgd.P);
     return;
   }
   gemm_body<BM, BN, MODE, BK, SCHED, C4, GL, KG>(a, cs::xcd_remap(lin % ntiles, ntiles), lin / ntiles, nsplit, smem);
-}
-
-// Horizontal fusion of one block's two independent backward GEMMs: blocks [0, nb1) run the
-// weight gradient (64x64 tiles, K-step BK1, s1 splits), the rest the data gradient (64x64,
-// BK2, s2 splits) — one launch, one ramp and one tail instead of two.
-template <int BK1, int BK2, int SCHED = 0, int KG = 1>
-__global__ __launch_bounds__(256 * KG) void conv_dual_kernel(CsConvArgs wg, CsConvArgs dg, int nb1, int s1, int s2) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int b = blockIdx.x;
-  if (b < nb1) {
-    const int nt = ((wg.M + 63) / 64) * ((wg.N + 63) / 64);
-    gemm_body<64, 64, CS_CONV_WGRAD, BK1, SCHED, false, 0, KG>(wg, cs::xcd_remap(b % nt, nt), b / nt, s1, smem);
-  } else {
-    const int nt = ((dg.M + 63) / 64) * ((dg.N + 63) / 64), c = b - nb1;
-    gemm_body<64, 64, CS_CONV_DGRAD, BK2, SCHED, false, 0, KG>(dg, cs::xcd_remap(c % nt, nt), c / nt, s2, smem);
-  }
 }
 
 // Deterministic split-K combine: out = sum_z ws[z] (+bias, +BN tile stats for FWD;
@@ -924,15 +993,6 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(CsConvArgs a, int mo
   splitk_reduce_body(a, mode, nslab, zstep, blockIdx.x, smem);
 }
 
-// both split-K combines of a dual launch in one grid
-__global__ __launch_bounds__(256) void splitk_reduce_dual_kernel(CsConvArgs a1, int mode1, int nslab1, int zstep1,
-                                                                 int nb1, CsConvArgs a2, int mode2, int nslab2,
-                                                                 int zstep2) {
-  __shared__ float smem[kRedLds];
-  if ((int)blockIdx.x < nb1) splitk_reduce_body(a1, mode1, nslab1, zstep1, blockIdx.x, smem);
-  else splitk_reduce_body(a2, mode2, nslab2, zstep2, blockIdx.x - nb1, smem);
-}
-
 int reduce_blocks(const CsConvArgs& a) { return ((a.M + kRedRows - 1) / kRedRows) * ((a.N + 63) / 64); }
 
 // fold pre-pass for large split counts; returns (nslab, zstep) for the combine
@@ -961,7 +1021,6 @@ template <int BM, int BN, int MODE, int BK, int SCHED, bool C4, int GL, int KG =
 hipError_t launch_k(dim3 grid, size_t lds, hipStream_t stream, const CsConvArgs& a) {
   size_t l = std::max(lds, (size_t)(1024 + 16) * sizeof(float));  // bn_fin.h's combine space
   if (MODE == CS_CONV_DGRAD && a.ered.part != nullptr) l = std::max(l, (size_t)BM * (BN + 4) * sizeof(float));
-  if (a.head.P > 0) grid.x += (a.head.P + 4 * KG - 1) / (4 * KG);  // the column pass: a piece per wave
   hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, MODE, BK, SCHED, C4, GL, KG>), grid, dim3(256 * KG), l, stream, a);
   return hipGetLastError();
 }
@@ -975,6 +1034,7 @@ hipError_t launch_gemm_m(const CsConvArgs& a, int splits, int stage, hipStream_t
   const int ntiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
   const size_t lds = MATH == 3   ? TileXS<BM, BN, MODE, BK>::BYTES
                      : MATH == 5 ? TileXS<BM, BN, MODE, BK, 1>::BYTES
+                     : MATH == 6 ? TileXS<BM, BN, MODE, BK, 2>::BYTES
                                  : 2 * T::STAGE * sizeof(float);
   const dim3 grid(ntiles * splits + a.sgd.P);
   constexpr bool deep_fits = (BM + BN) * BK * 4 * 5 < 160 * 1024;
@@ -982,7 +1042,7 @@ hipError_t launch_gemm_m(const CsConvArgs& a, int splits, int stage, hipStream_t
     if (MODE == CS_CONV_FWD && a.w_oihw)  // padded conv0: Cin = 4 < BK
       return launch_k<BM, BN, MODE, BK, 0, true, 0>(grid, lds, stream, a);
   }
-  if constexpr (BK == 32 && MATH != 3 && MATH != 5) {
+  if constexpr (BK == 32 && MATH != 3 && MATH != 5 && MATH != 6) {
     if (stage == CS_STAGE_LDS_DMA)
       return launch_k<BM, BN, MODE, BK, MATH, false, 3>(grid, 3 * TG::STAGE * sizeof(float), stream, a);
     if constexpr (deep_fits) {
@@ -991,20 +1051,23 @@ hipError_t launch_gemm_m(const CsConvArgs& a, int splits, int stage, hipStream_t
     }
   }
   // K-groups: the LDS tile ring must also hold the (KG-1) partial-accumulator images
-  if constexpr (BK >= 32 && BM * BK >= 2048 && BN * BK >= 2048 && (MATH != 3 || BK == 32 || (BM == 64 && BN == 64))) {
+  if constexpr (BK >= 32 && BM * BK >= 2048 && BN * BK >= 2048 && (MATH != 3 || BK == 32 || (BM == 64 && BN == 64)) &&
+                (MATH != 6 || BK == 32 || !(BM == 128 && BN == 128))) {
     if (stage == CS_STAGE_KG2) {
       const size_t red = (size_t)1 * 4 * (BM / 64) * (BN / 64) * 16 * 64 * sizeof(float);
       return launch_k<BM, BN, MODE, BK, MATH, false, 0, 2>(grid, std::max(lds, red), stream, a);
     }
   }
-  if constexpr (BK == 64 && BM * BK >= 4096 && BN * BK >= 4096 && (MATH != 3 || (BM == 64 && BN == 64))) {
+  if constexpr (BK == 64 && BM * BK >= 4096 && BN * BK >= 4096 && (MATH != 3 || (BM == 64 && BN == 64)) &&
+                (MATH != 6 || !(BM == 128 && BN == 128))) {
     if (stage == CS_STAGE_KG4) {
       const size_t red = (size_t)3 * 4 * (BM / 64) * (BN / 64) * 16 * 64 * sizeof(float);
       return launch_k<BM, BN, MODE, BK, MATH, false, 0, 4>(grid, std::max(lds, red), stream, a);
     }
   }
   if (stage != CS_STAGE_REGS) return hipErrorInvalidValue;
-  if constexpr ((MATH == 3 && BK == 64 && !(BM == 64 && BN == 64)) || (MATH == 5 && BK == 64 && BM == 128 && BN == 128)) {
+  if constexpr ((MATH == 3 && BK == 64 && !(BM == 64 && BN == 64)) ||
+                ((MATH == 5 || MATH == 6) && BK == 64 && BM == 128 && BN == 128)) {
     return hipErrorInvalidValue;  // bf16 planes of a wider bk-64 tile exceed the 160 KiB LDS
   } else if constexpr (MATH >= 2) {
     return launch_k<BM, BN, MODE, BK, MATH, false, 0>(grid, lds, stream, a);
@@ -1016,6 +1079,7 @@ hipError_t launch_gemm_m(const CsConvArgs& a, int splits, int stage, hipStream_t
 template <int BM, int BN, int MODE, int BK>
 hipError_t launch_gemm(const CsConvArgs& a, int splits, int stage, hipStream_t stream) {
   if (stage & CS_STAGE_BF16) return launch_gemm_m<BM, BN, MODE, BK, 5>(a, splits, stage & ~CS_STAGE_BF16, stream);
+  if (stage & CS_STAGE_F3) return launch_gemm_m<BM, BN, MODE, BK, 6>(a, splits, stage & ~CS_STAGE_F3, stream);
   if (stage & CS_STAGE_X6S) return launch_gemm_m<BM, BN, MODE, BK, 3>(a, splits, stage & ~CS_STAGE_X6S, stream);
   if (stage & CS_STAGE_X6) return launch_gemm_m<BM, BN, MODE, BK, 2>(a, splits, stage & ~CS_STAGE_X6, stream);
   return launch_gemm_m<BM, BN, MODE, BK, 0>(a, splits, stage, stream);
@@ -1033,7 +1097,8 @@ hipError_t launch_gemm(const CsConvArgs& a, int splits, int stage, hipStream_t s
   CS_K(BM_, BN_, MODE_, 16, 2, false, 0) CS_K(BM_, BN_, MODE_, 32, 2, false, 0) \
   CS_K(BM_, BN_, MODE_, 32, 2, false, 3)                                      \
   CS_K(BM_, BN_, MODE_, 16, 3, false, 0) CS_K(BM_, BN_, MODE_, 32, 3, false, 0)     \
-  CS_K(BM_, BN_, MODE_, 16, 5, false, 0) CS_K(BM_, BN_, MODE_, 32, 5, false, 0)
+  CS_K(BM_, BN_, MODE_, 16, 5, false, 0) CS_K(BM_, BN_, MODE_, 32, 5, false, 0)     \
+  CS_K(BM_, BN_, MODE_, 16, 6, false, 0) CS_K(BM_, BN_, MODE_, 32, 6, false, 0)
 #define CS_TILE(BM_, BN_)                                                                       \
   CS_MODE(BM_, BN_, CS_CONV_FWD) CS_MODE(BM_, BN_, CS_CONV_DGRAD) CS_MODE(BM_, BN_, CS_CONV_WGRAD) \
   CS_K(BM_, BN_, CS_CONV_FWD, 16, 0, true, 0) CS_K(BM_, BN_, CS_CONV_FWD, 32, 0, true, 0)
@@ -1059,6 +1124,13 @@ CS_K(64, 128, CS_CONV_WGRAD, 64, 5, false, 0)
 CS_K(64, 64, CS_CONV_FWD, 64, 3, false, 0)
 CS_K(64, 64, CS_CONV_DGRAD, 64, 3, false, 0)
 CS_K(64, 64, CS_CONV_WGRAD, 64, 3, false, 0)
+#define CS_F3_64(BM_, BN_) \
+  CS_K(BM_, BN_, CS_CONV_FWD, 64, 6, false, 0) CS_K(BM_, BN_, CS_CONV_DGRAD, 64, 6, false, 0) \
+  CS_K(BM_, BN_, CS_CONV_WGRAD, 64, 6, false, 0)
+CS_F3_64(64, 64)
+CS_F3_64(128, 64)
+CS_F3_64(64, 128)
+#undef CS_F3_64
 #undef CS_TILE64
 #undef CS_BK64
 #define CS_KG1(BM_, BN_, BK_, KG_, M_)                                                            \
@@ -1076,6 +1148,16 @@ CS_KG1(64, 128, 32, 2, 3)
 CS_KG1(128, 128, 32, 2, 3)
 CS_KG1(64, 64, 64, 2, 3)
 CS_KG1(64, 64, 64, 4, 3)
+CS_KG1(64, 64, 32, 2, 6)
+CS_KG1(128, 64, 32, 2, 6)
+CS_KG1(64, 128, 32, 2, 6)
+CS_KG1(128, 128, 32, 2, 6)
+CS_KG1(64, 64, 64, 2, 6)
+CS_KG1(128, 64, 64, 2, 6)
+CS_KG1(64, 128, 64, 2, 6)
+CS_KG1(64, 64, 64, 4, 6)
+CS_KG1(128, 64, 64, 4, 6)
+CS_KG1(64, 128, 64, 4, 6)
 CS_KG1(64, 64, 32, 2, 5)
 CS_KG1(128, 64, 32, 2, 5)
 CS_KG1(64, 128, 32, 2, 5)
@@ -1103,13 +1185,6 @@ CS_DEEP(64, 128)
 CS_DEEP(128, 64)
 #undef CS_DEEP
 #undef CS_DEEP1
-template __global__ void conv_dual_kernel<16, 16>(CsConvArgs, CsConvArgs, int, int, int);
-template __global__ void conv_dual_kernel<16, 32>(CsConvArgs, CsConvArgs, int, int, int);
-template __global__ void conv_dual_kernel<32, 16>(CsConvArgs, CsConvArgs, int, int, int);
-template __global__ void conv_dual_kernel<32, 32>(CsConvArgs, CsConvArgs, int, int, int);
-template __global__ void conv_dual_kernel<64, 64, 3, 4>(CsConvArgs, CsConvArgs, int, int, int);
-template __global__ void conv_dual_kernel<64, 64, 3, 2>(CsConvArgs, CsConvArgs, int, int, int);
-template __global__ void conv_dual_kernel<16, 16, 3, 1>(CsConvArgs, CsConvArgs, int, int, int);
 #undef CS_TILE
 #undef CS_MODE
 #undef CS_K
@@ -1150,8 +1225,14 @@ void cs_conv_fill_dims(CsConvArgs* a, int mode) {
 }
 
 bool cs_conv_stage_ok(int stage, int bm, int bn, int bk, bool conv0_fwd) {
-  const int maths = ((stage & CS_STAGE_X6) != 0) + ((stage & CS_STAGE_X6S) != 0) + ((stage & CS_STAGE_BF16) != 0);
+  const int maths = ((stage & CS_STAGE_X6) != 0) + ((stage & CS_STAGE_X6S) != 0) + ((stage & CS_STAGE_BF16) != 0) +
+                    ((stage & CS_STAGE_F3) != 0);
   if (maths > 1) return false;
+  if (stage & CS_STAGE_F3) {  // two fp16 planes: register staging / K-groups; bk 64 up to 128x64 tiles
+    stage &= ~CS_STAGE_F3;
+    if (conv0_fwd || (stage != CS_STAGE_REGS && stage != CS_STAGE_KG2 && stage != CS_STAGE_KG4)) return false;
+    if (bk == 64 && bm == 128 && bn == 128) return false;
+  }
   if (stage & CS_STAGE_BF16) {  // bf16 operands (one plane): register staging / K-groups
     stage &= ~CS_STAGE_BF16;
     if (conv0_fwd || (stage != CS_STAGE_REGS && stage != CS_STAGE_KG2 && stage != CS_STAGE_KG4)) return false;
@@ -1192,7 +1273,7 @@ int cs_conv_effective_splits(int K, int bk, int splits) {
 }
 
 namespace {
-// dims, K-step split and size checks shared by the single and dual launchers; -> effective splits or -1
+// dims, K-step split and size checks; -> effective splits or -1
 int prep_gemm(CsConvArgs& a, int mode, int bk, int splits) {
   if (bk != 16 && bk != 32 && bk != 64) return -1;
   if (bk == 64 && mode == CS_CONV_FWD && a.w_oihw) return -1;  // conv0's K = 36
@@ -1210,65 +1291,11 @@ int prep_gemm(CsConvArgs& a, int mode, int bk, int splits) {
 }
 }  // namespace
 
-hipError_t cs_conv_gemm_dual(CsConvArgs wg, int wbk, int wsplits, CsConvArgs dg, int dbk, int dsplits,
-                             hipStream_t stream, int stage) {
-  if (wg.sgd.n != 0 || dg.sgd.n != 0 || wg.head.P != 0 || dg.head.P != 0)
-    return hipErrorInvalidValue;  // no appended work in dual launches
-  if (wg.w_oihw) return hipErrorInvalidValue;  // conv0 has no data gradient
-  if (wg.fin.cnt != nullptr) return hipErrorInvalidValue;  // (the weight gradient has no BN statistics)
-  const int s1 = prep_gemm(wg, CS_CONV_WGRAD, wbk, wsplits), s2 = prep_gemm(dg, CS_CONV_DGRAD, dbk, dsplits);
-  if (s1 < 0 || s2 < 0) return hipErrorInvalidValue;
-  if (s1 > 1 && s2 > 1 && wg.ws == dg.ws) return hipErrorInvalidValue;  // slabs must not alias
-  const int nt1 = ((wg.M + 63) / 64) * ((wg.N + 63) / 64), nt2 = ((dg.M + 63) / 64) * ((dg.N + 63) / 64);
-  const int nb1 = nt1 * s1, nb = nb1 + nt2 * s2;
-  // (>= the 64 x 68 float tile image of the dgrad epilogue's BN partials, CsConvArgs::ered)
-  const size_t lds = std::max<size_t>(
-      2 * (size_t)std::max(Tile<64, 64, CS_CONV_WGRAD, 32>::STAGE, Tile<64, 64, CS_CONV_DGRAD, 32>::STAGE) * sizeof(float),
-      64 * 68 * sizeof(float));
-  if (stage == CS_STAGE_REGS) {
-#define CS_DUAL(B1, B2)                                                                                      \
-  if (wbk == B1 && dbk == B2)                                                                                \
-    hipLaunchKernelGGL((conv_dual_kernel<B1, B2>), dim3(nb), dim3(256), lds, stream, wg, dg, nb1, s1, s2);
-    CS_DUAL(16, 16)
-    CS_DUAL(16, 32)
-    CS_DUAL(32, 16)
-    CS_DUAL(32, 32)
-#undef CS_DUAL
-  } else {
-    // split-bf16 planes (X6S), both halves with the same K-step and K-group count
-    const size_t xs = std::max(TileXS<64, 64, CS_CONV_WGRAD, 64>::BYTES, TileXS<64, 64, CS_CONV_DGRAD, 64>::BYTES);
-    const size_t red = (size_t)3 * 4 * 16 * 64 * sizeof(float);
-    if (wbk != dbk) return hipErrorInvalidValue;
-    if (stage == (CS_STAGE_X6S | CS_STAGE_KG4) && wbk == 64)
-      hipLaunchKernelGGL((conv_dual_kernel<64, 64, 3, 4>), dim3(nb), dim3(1024), std::max(xs, red), stream, wg, dg,
-                         nb1, s1, s2);
-    else if (stage == (CS_STAGE_X6S | CS_STAGE_KG2) && wbk == 64)
-      hipLaunchKernelGGL((conv_dual_kernel<64, 64, 3, 2>), dim3(nb), dim3(512), xs, stream, wg, dg, nb1, s1, s2);
-    else if (stage == (CS_STAGE_X6S | CS_STAGE_REGS) && wbk == 16)
-      hipLaunchKernelGGL((conv_dual_kernel<16, 16, 3, 1>), dim3(nb), dim3(256),
-                         std::max(TileXS<64, 64, CS_CONV_WGRAD, 16>::BYTES, TileXS<64, 64, CS_CONV_DGRAD, 16>::BYTES),
-                         stream, wg, dg, nb1, s1, s2);
-    else
-      return hipErrorInvalidValue;
-  }
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess || (s1 == 1 && s2 == 1)) return e;
-  if (s1 > 1 && s2 > 1) {
-    int ns1, z1, ns2, z2;
-    fold_if_needed(wg, s1, stream, ns1, z1);
-    fold_if_needed(dg, s2, stream, ns2, z2);
-    const int r1 = reduce_blocks(wg);
-    hipLaunchKernelGGL(splitk_reduce_dual_kernel, dim3(r1 + reduce_blocks(dg)), dim3(256), 0, stream, wg,
-                       (int)CS_CONV_WGRAD, ns1, z1, r1, dg, (int)CS_CONV_DGRAD, ns2, z2);
-    return hipGetLastError();
-  }
-  return s1 > 1 ? launch_reduce(wg, CS_CONV_WGRAD, s1, stream) : launch_reduce(dg, CS_CONV_DGRAD, s2, stream);
-}
-
 hipError_t cs_conv_gemm(CsConvArgs a, int mode, int bm, int bn, int bk, int splits, hipStream_t stream, int stage) {
   if (!cs_conv_stage_ok(stage, bm, bn, bk, a.w_oihw && mode == CS_CONV_FWD)) return hipErrorInvalidValue;
   splits = prep_gemm(a, mode, bk, splits);
   if (splits < 0) return hipErrorInvalidValue;
+  if ((stage & CS_STAGE_F3) && (a.amax_a == nullptr || a.amax_b == nullptr)) return hipErrorInvalidValue;
   a.sgd.P = a.sgd.n > 0 ? (int)std::min<int64_t>(256, (a.sgd.n / 4 + 255) / 256) : 0;
   if (a.fin.cnt != nullptr) {  // last-arriver BN finalize: its statistics must exist in this launch pair
     if (mode == CS_CONV_WGRAD || (mode == CS_CONV_FWD && a.stats == nullptr) ||

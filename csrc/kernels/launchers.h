@@ -23,8 +23,10 @@ hipError_t cs_make_batch(const uint8_t* data, const int64_t* labels, const int64
 
 // optimizer
 // counter (optional): incremented once by the launch (the engine's device-side step cursor)
+// the absolute maximum of x[0, n) folded (atomic max) into CS_AMAX_SHARDS floats
+hipError_t cs_amax(const float* x, int64_t n, float* amax, hipStream_t stream);
 hipError_t cs_sgd_flat(float* p, const float* g, float* m, int64_t n, float lr, float mom, float wd, float damp,
-                       float scale, int first, hipStream_t stream, int64_t* counter = nullptr);
+                       float scale, int first, hipStream_t stream, int64_t* counter = nullptr, float* amax = nullptr);
 // faithful sync modes on flat gradients (flat_ops.hip): dst = mean over `rows` rows of src [rows][n];
 // g = g + t, then / div when div > 0
 hipError_t cs_rows_mean(float* src, int rows, int64_t n, float* dst, int bcast, hipStream_t stream);
@@ -38,9 +40,8 @@ hipError_t cs_sgd_multi(const CsTensorEntry* tab_dev, int ntens, const int64_t* 
 // bn (optional, part 0 / 1): the features are the last VGG block's BatchNorm + ReLU + 2x2 max-pool of
 // its pre-BN output y [B][2][2][K] (scale / shift per channel), computed in the row pass (bn_apply's
 // arithmetic and max order: the same bits) and written to feat for the column pass
-// the classifier's per-column pass (dW, db, loss, correct count) as data: run by its own launch or
-// carried as extra workgroups of a weight-gradient launch (CsConvArgs::head; P = C*ceil(K/64)+1
-// wave-sized pieces, 0 = none)
+// the classifier's per-column pass (dW, db, loss, correct count) as data (P = C*ceil(K/64)+1
+// wave-sized pieces)
 struct CsHeadCols {
   const float* feat;
   int B, K, C;
@@ -69,6 +70,10 @@ hipError_t cs_softmax_xent(const float* logits, const int64_t* labels, int B, in
 
 // ---------------------------------------------------------------- conv (implicit GEMM, fp32 MFMA)
 enum { CS_CONV_FWD = 0, CS_CONV_DGRAD = 1, CS_CONV_WGRAD = 2 };
+// operand absolute-maximum bounds (the F3 conv math's scales) are kept as this many shards, each the
+// atomic max of the workgroups with blockIdx % CS_AMAX_SHARDS == shard (one per XCD: no single hot
+// word); the bound is the largest shard
+#define CS_AMAX_SHARDS 8
 
 // One BN-backward partial-sum pass (bn.hip "reduce"): y, incoming gradient G, the forward's
 // scale/shift/mean/invstd, partials out part [P][C][3]. P == 0: none.
@@ -87,6 +92,9 @@ struct CsSgdTail {
   int64_t n;
   float lr, mom, wd, damp;
   int first, P;
+  // optional: CS_AMAX_SHARDS floats the updated parameters' absolute maximum is folded into (a
+  // running bound of the weights for the F3 conv math)
+  float* amax;
 };
 
 // BatchNorm finalize by the last-arriving block of the launch that produces the statistics
@@ -130,15 +138,14 @@ struct CsConvArgs {
   // an independent SGD update appended to the launch (the serial world-1 step: block l+1's
   // parameters, whose last reader has run, ride block l's weight-gradient GEMM)
   CsSgdTail sgd;
+  // CS_STAGE_F3: device pointers to CS_AMAX_SHARDS floats whose maximum bounds |A| / |B| (the
+  // GEMM's A operand: FWD x, DGRAD / WGRAD dz; B: FWD / DGRAD w, WGRAD x); each sets its operand's
+  // power-of-two scale
+  const float* amax_a;
+  const float* amax_b;
   // FWD (with stats) / DGRAD (with ered): the BN finalize by the launch's last-arriving block
   // (or the split-K combine's); fin.cnt == null: off
   CsBnFin fin;
-  // a deferred stream-link signal (device_comm.h StreamLink::defer) the launch's block 0 bumps when
-  // it starts — every kernel before it on its stream has completed (the engine's staggered fork:
-  // block l+1's side-stream weight gradient waits for block l's data gradient to be resident)
-  unsigned long long* start_sig;
-  // the classifier's per-column pass carried as extra workgroups (head.P == 0: none)
-  CsHeadCols head;
   // filled by the launcher:
   int lgH, lgW, lgCin, lgCout, M, N, K, ksteps_per_split, total_ksteps;
 };
@@ -196,26 +203,14 @@ hipError_t cs_conv0_wgrad_bn(const float* x, const float* y, const float* G, con
 // staging / K-groups only; bk 64 only with 64x64 tiles)
 // | CS_STAGE_BF16: operands rounded to bf16 at the LDS store, one bf16 MFMA, f32 accumulate
 // (reduced precision: only for the engine's opt-in bf16 mode, never picked by the f32 autotune)
+// | CS_STAGE_F3: fp32-class split into two fp16 planes of the power-of-two-scaled operand (scales
+// from CsConvArgs::amax_a / amax_b, required), 3 v_mfma_f32_32x32x16_f16 per product (conv_gemm.hip "F3")
 enum { CS_STAGE_REGS = 0, CS_STAGE_LDS_DMA = 1, CS_STAGE_LDS_DMA_DEEP = 2, CS_STAGE_KG2 = 3, CS_STAGE_KG4 = 4,
-       CS_STAGE_X6 = 8, CS_STAGE_X6S = 16, CS_STAGE_BF16 = 32 };
+       CS_STAGE_X6 = 8, CS_STAGE_X6S = 16, CS_STAGE_BF16 = 32, CS_STAGE_F3 = 64 };
 // whether a (stage, tile, bk) combination has a kernel
 bool cs_conv_stage_ok(int stage, int bm, int bn, int bk, bool conv0_fwd);
 hipError_t cs_conv_gemm(CsConvArgs a, int mode, int bm, int bn, int bk, int splits, hipStream_t stream,
                         int stage = CS_STAGE_REGS);
-// one launch for a block's weight gradient (wg) and data gradient (dg), both 64x64 tiles with
-// register staging (K-steps wbk / dbk in {16, 32}); split-K slabs combined by one launch
-// (their workspaces must differ)
-// stage CS_STAGE_REGS (f32, bk 16/32 each), or an X6S stage shared by both halves:
-// X6S|KG4 and X6S|KG2 with bk 64, X6S|REGS with bk 16
-hipError_t cs_conv_gemm_dual(CsConvArgs wg, int wbk, int wsplits, CsConvArgs dg, int dbk, int dsplits,
-                             hipStream_t stream, int stage = CS_STAGE_REGS);
-inline bool cs_conv_dual_ok(int wstage, int wbk, int dstage, int dbk) {
-  if (wstage != dstage) return false;
-  if (wstage == CS_STAGE_REGS) return (wbk == 16 || wbk == 32) && (dbk == 16 || dbk == 32);
-  if (wbk != dbk) return false;
-  return ((wstage == (CS_STAGE_X6S | CS_STAGE_KG4) || wstage == (CS_STAGE_X6S | CS_STAGE_KG2)) && wbk == 64) ||
-         (wstage == (CS_STAGE_X6S | CS_STAGE_REGS) && wbk == 16);
-}
 // deterministic split-K combine of `splits` fp32 slabs in a.ws (dims filled): sum in split order
 // (+bias and BN tile statistics of CS_SPLITK_STAT_ROWS rows for FWD; conv0's OIHW scatter for WGRAD)
 hipError_t cs_conv_splitk_reduce(const CsConvArgs& a, int mode, int splits, hipStream_t stream);
@@ -233,8 +228,10 @@ hipError_t cs_bn_finalize(const float* part, int T, int R, int M, int C, const f
                           float* scale, float* shift, float* save_mean, float* save_invstd, hipStream_t stream);
 hipError_t cs_bn_eval_coeffs(const float* gamma, const float* beta, const float* rm, const float* rv, int C, float eps,
                              float* scale, float* shift, hipStream_t stream);
+// amax (optional): CS_AMAX_SHARDS floats the output's absolute maximum is atomically folded into
+// (the F3 conv math's operand bound); the same for dz in the BN-backward launchers below
 hipError_t cs_bn_apply(const float* y, const float* scale, const float* shift, float* out, int B, int H, int W, int C,
-                       int pool, hipStream_t stream);
+                       int pool, hipStream_t stream, float* amax = nullptr);
 int cs_bn_bwd_blocks(int B, int H, int W, int C, int pool);
 // part: [cs_bn_bwd_blocks][C][3] scratch; coef: [C][3] scratch; dgamma/dbeta/dbias may be null.
 // LDS bytes the BN-backward reduce body needs (C channels)
@@ -246,7 +243,7 @@ inline size_t cs_bn_red_lds(int C) { return (size_t)(256 / (C / 4)) * C * 3 * si
 hipError_t cs_bn_bwd_tail(const float* y, const float* G, int B, int H, int W, int C, int pool, const float* scale,
                           const float* shift, const float* mean, const float* invstd, const float* gamma,
                           const float* part, int P, float* coef, float* dgamma, float* dbeta, float* dbias, float* dz,
-                          hipStream_t stream, unsigned long long* signal = nullptr);
+                          hipStream_t stream, unsigned long long* signal = nullptr, float* amax = nullptr);
 // the finalize half of cs_bn_bwd_tail alone (coef, dgamma / dbeta / dbias), for a consumer that
 // applies the backward itself (cs_conv0_wgrad_bn)
 hipError_t cs_bn_bwd_finalize(const float* part, int P, int C, int M, const float* gamma, const float* invstd,
@@ -254,7 +251,8 @@ hipError_t cs_bn_bwd_finalize(const float* part, int P, int C, int M, const floa
                               unsigned long long* signal = nullptr);
 hipError_t cs_bn_bwd(const float* y, const float* G, int B, int H, int W, int C, int pool, const float* scale,
                      const float* shift, const float* mean, const float* invstd, const float* gamma, float* part,
-                     float* coef, float* dgamma, float* dbeta, float* dbias, float* dz, hipStream_t stream);
+                     float* coef, float* dgamma, float* dbeta, float* dbias, float* dz, hipStream_t stream,
+                     float* amax = nullptr);
 
 // single-launch BN for small layers (one block per 16 channels owns all their rows):
 // forward = finalize (tile partials -> bnv [4][C] = scale, shift, mean, invstd + running stats)
@@ -264,7 +262,7 @@ hipError_t cs_bn_fused_fwd(const float* part, int T, int R, int M, int C, const 
                            float* bnv, const float* y, float* out, int B, int H, int W, int pool, hipStream_t stream);
 hipError_t cs_bn_fused_bwd(const float* y, const float* G, int B, int H, int W, int C, int pool, const float* bnv,
                            const float* gamma, float* coef, float* dgamma, float* dbeta, float* dbias, float* dz,
-                           hipStream_t stream, unsigned long long* signal = nullptr);
+                           hipStream_t stream, unsigned long long* signal = nullptr, float* amax = nullptr);
 // finalize + apply of the BN backward in ONE launch when the reduce already ran (the data-gradient
 // epilogue's P row-tile partials [P][C][3], CsConvArgs::ered): grid (C/16, row chunks), every block
 // finalizes its 16 channels from the P partials (the same fixed-order sum in every block), block row

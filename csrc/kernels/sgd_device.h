@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "common.h"
 #include "launchers.h"
 
 namespace cs_sgd {
@@ -21,9 +22,11 @@ __device__ __forceinline__ void step1(float& p, float g, float& m, float lr, flo
   p = p - lr * d;
 }
 
-// the update of [0, t.n) of t's range by block `blk` of `nblk` (grid-stride, float4 + scalar tail)
+// the update of [0, t.n) of t's range by block `blk` of `nblk` (grid-stride, float4 + scalar tail);
+// every lane of the calling block runs it (t.amax: a wave reduction at the end)
 __device__ __forceinline__ void tail_body(const CsSgdTail& t, int blk, int nblk) {
   const int64_t n4 = t.n >> 2, stride = (int64_t)nblk * blockDim.x;
+  float vm = 0.f;
   float4* p4 = reinterpret_cast<float4*>(t.p);
   const float4* g4 = reinterpret_cast<const float4*>(t.g);
   float4* m4 = reinterpret_cast<float4*>(t.m);
@@ -37,13 +40,16 @@ __device__ __forceinline__ void tail_body(const CsSgdTail& t, int blk, int nblk)
     step1(pv.w, gv.w, mv.w, t.lr, t.mom, t.wd, t.damp, 1.0f, t.first);
     p4[i] = pv;
     if (t.mom != 0.f) m4[i] = mv;
+    vm = fmaxf(vm, fmaxf(fmaxf(fabsf(pv.x), fabsf(pv.y)), fmaxf(fabsf(pv.z), fabsf(pv.w))));
   }
   for (int64_t i = (n4 << 2) + (int64_t)blk * blockDim.x + threadIdx.x; i < t.n; i += stride) {
     float pv = t.p[i], mv = t.first ? 0.f : t.m[i];
     step1(pv, t.g[i], mv, t.lr, t.mom, t.wd, t.damp, 1.0f, t.first);
     t.p[i] = pv;
     if (t.mom != 0.f) t.m[i] = mv;
+    vm = fmaxf(vm, fabsf(pv));
   }
+  if (t.amax != nullptr) cs::wave_amax_publish(vm, t.amax);
 }
 
 }  // namespace cs_sgd

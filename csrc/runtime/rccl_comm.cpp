@@ -23,7 +23,24 @@ std::string RcclComm::unique_id() {
   return std::string(reinterpret_cast<const char*>(&id), sizeof(id));
 }
 
+int RcclComm::runtime_version() {
+  int v = 0;
+  nccl_ok(ncclGetVersion(&v), "ncclGetVersion");
+  return v;
+}
+
 namespace {
+// ncclConfig_t as this file fills it: `size` first (the library copies min(size, its own sizeof)),
+// blocking (2.14), minCTAs / maxCTAs (2.17). A runtime older than that, or of another major line,
+// would read the struct with a different layout: refuse it instead of passing garbage CTA budgets.
+void check_runtime_layout() {
+  const int v = RcclComm::runtime_version();
+  if (v / 10000 != NCCL_MAJOR || v < NCCL_VERSION(2, 17, 0))
+    throw std::runtime_error("RcclComm: RCCL runtime " + std::to_string(v) + " vs header " +
+                             std::to_string(NCCL_VERSION_CODE) +
+                             ": ncclConfig_t minCTAs/maxCTAs need a 2.x runtime >= 2.17");
+}
+
 // fork/join events only order two streams of this device: no system-scope fence needed (round 1
 // measured the three flag variants within 2 %: 72.3k / 73.7k / 72.4k img/s)
 unsigned comm_event_flags() { return hipEventDisableTiming | hipEventDisableSystemFence; }
@@ -33,6 +50,7 @@ RcclComm::RcclComm(const std::string& uid, int rank, int world, int device, bool
     : bridge_(comm_event_flags()), rank_(rank), world_(world), device_(device), max_ctas_(max_ctas) {
   if (uid.size() != sizeof(ncclUniqueId)) throw std::runtime_error("RcclComm: unique id must be 128 bytes");
   if (rank < 0 || rank >= world) throw std::runtime_error("RcclComm: bad rank");
+  check_runtime_layout();
   hip_ok(hipSetDevice(device), "hipSetDevice");
   if (high_priority) {  // the process-wide reserved comm stream: its own hardware queue (device_comm.h)
     stream_ = reserved_comm_stream();
@@ -46,6 +64,7 @@ RcclComm::RcclComm(const std::string& uid, int rank, int world, int device, bool
   std::memcpy(&id, uid.data(), sizeof(id));
   // ncclCommInitRankConfig: the header is ROCm 7.2's RCCL 2.27, the runtime torch's 2.26 — the
   // library copies min(config.size, its own sizeof) bytes, and every field set here predates both
+  // (checked above against the loaded library: check_runtime_layout)
   ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
   cfg.blocking = 1;
   if (max_ctas > 0) {

@@ -23,6 +23,9 @@ namespace cs {
 class RcclComm final : public DeviceComm {
  public:
   static std::string unique_id();  // 128 raw bytes (NCCL_UNIQUE_ID_BYTES)
+  // ncclGetVersion() of the RCCL library actually loaded (torch's, not necessarily the header's)
+  static int runtime_version();
+  static int header_version() { return NCCL_VERSION_CODE; }
 
   // max_ctas > 0: RCCL compute budget (ncclConfig_t maxCTAs, minCTAs <= it) so the bucketed
   // all-reduces overlapping the backward take at most that many CUs from the conv GEMMs

@@ -97,7 +97,7 @@ VggEngine::VggEngine(int64_t Bmax, std::vector<int64_t> desc, std::vector<int64_
   TORCH_CHECK(nbt_.is_cuda() && nbt_.scalar_type() == at::kLong && nbt_.numel() == L, "VggEngine: nbt int64 [L]");
   const auto fo = params_.options();
   const int64_t P = params_.numel();
-  int64_t gmax = 0, dzmax = 0, partmax = 0, cmax = 0, fin_ints = 0, grpmax = 4;
+  int64_t gmax = 0, dzmax = 0, partmax = 0, cmax = 0;
   blocks_.resize(L);
   for (int64_t l = 0; l < L; ++l) {
     VggBlock& b = blocks_[l];
@@ -135,19 +135,8 @@ VggEngine::VggEngine(int64_t Bmax, std::vector<int64_t> desc, std::vector<int64_
     gmax = std::max(gmax, Bmax * ho * ho * b.cout);
     dzmax = std::max(dzmax, pix * b.cout);
     partmax = std::max<int64_t>(partmax, (int64_t)cs_bn_bwd_blocks(Bmax, b.H, b.H, b.cout, b.pool) * b.cout * 3);
-    // in-launch finalize state, sized for the finest partials (16-row tiles, 64-wide column tiles):
-    // forward over this block's statistics, backward over block l-1's (carried by this dgrad)
-    const int64_t tf = cdiv(pix, CS_SPLITK_STAT_ROWS);
-    b.fin_fwd = fin_ints;
-    fin_ints += cs_bn_fin_ints((int)tf, b.cout, 64);
-    grpmax = std::max<int64_t>(grpmax, cs_bn_fin_grp_floats((int)tf, b.cout, 64));
-    if (l > 0) {
-      // block l-1's BN-backward partials out of block l's data gradient: [row tiles][cin][4]
-      partmax = std::max<int64_t>(partmax, tf * b.cin * 4);
-      b.fin_bwd = fin_ints;
-      fin_ints += cs_bn_fin_ints((int)tf, b.cin, 64);
-      grpmax = std::max<int64_t>(grpmax, cs_bn_fin_grp_floats((int)tf, b.cin, 64));
-    }
+    // block l-1's BN-backward partials out of block l's data gradient: [row tiles][cin][3]
+    if (l > 0) partmax = std::max<int64_t>(partmax, cdiv(pix, CS_SPLITK_STAT_ROWS) * b.cin * 3);
     cmax = std::max<int64_t>(cmax, b.cout);
     for (int m = 0; m < 3; ++m) b.tile[m] = default_tile(b, m, Bmax);
   }
@@ -172,14 +161,26 @@ VggEngine::VggEngine(int64_t Bmax, std::vector<int64_t> desc, std::vector<int64_
   ws_elems_ = kWsElems;
   ws_ = torch::zeros({ws_elems_}, fo);
   ws_w_ = torch::zeros({ws_elems_}, fo);
-  // zeroed once; every in-launch finalize leaves its tickets zeroed (bn_fin.h)
-  fin_cnt_ = torch::zeros({std::max<int64_t>(fin_ints, 1)}, fo.dtype(at::kInt));
-  fin_grp_ = torch::zeros({grpmax}, fo);
   side_ = reserved_side_stream();  // process-wide, created early (device_comm.h)
   dz_link_ = std::make_unique<StreamLink>();
   wg_link_ = std::make_unique<StreamLink>();
   for (const VggBlock& b : blocks_) dz_blk_.push_back(torch::zeros({Bmax * b.H * b.H * b.cout}, fo));
   if (const char* e = getenv("CS_OVERLAP_WGRAD")) overlap_ = atoi(e) != 0;
+  // CS_ENGINE_OFF: comma list of default-on schedule features to turn off for a cross-process A/B
+  // (one switch instead of one per feature): conv0_direct, conv0_bn_fold, conv0_sgd_fold,
+  // conv0_batch_fold, head_bn_fold, side_sgd_tail, sgd_tail, bn_fused
+  if (const char* e = getenv("CS_ENGINE_OFF")) {
+    const std::string off = std::string(",") + e + ",";
+    auto has = [&](const char* n) { return off.find(std::string(",") + n + ",") != std::string::npos; };
+    if (has("conv0_direct")) conv0_direct_ = false;
+    if (has("conv0_bn_fold")) conv0_bn_fold_ = false;
+    if (has("conv0_sgd_fold")) conv0_sgd_fold_ = false;
+    if (has("conv0_batch_fold")) conv0_batch_fold_ = false;
+    if (has("head_bn_fold")) head_bn_fold_ = false;
+    if (has("side_sgd_tail")) side_sgd_tail_ = false;
+    if (has("sgd_tail")) sgd_tail_on_ = false;
+    if (has("bn_fused")) bn_fused_rows_ = 0;
+  }
   // per-block parameter ranges for the per-block SGD: the backward-ready layout puts fc first,
   // then blocks L-1..0, each {w, bias, gamma, beta} inside [w_off, next block's w_off)
   {
@@ -196,22 +197,10 @@ VggEngine::VggEngine(int64_t Bmax, std::vector<int64_t> desc, std::vector<int64_
     }
     if (!contiguous) blk_range_.clear();
   }
-  if (const char* e = getenv("CS_CONV_DUAL")) dual_ = atoi(e) != 0;
-  if (const char* e = getenv("CS_BN_FUSED_ROWS")) bn_fused_rows_ = atoll(e);
   if (const char* e = getenv("CS_CONV_MATH")) math_ = atoi(e);
   if (const char* e = getenv("CS_DEBUG_SKIP")) debug_skip_ = atoi(e);
-  if (const char* e = getenv("CS_BN_FWD_FUSED_T")) fwd_fused_t_ = atoi(e);
-  if (const char* e = getenv("CS_WGRAD_STAGGER")) stagger_ = atoi(e) != 0;
-  if (const char* e = getenv("CS_WGRAD_LAG")) set_lag(atoi(e));
-  if (const char* e = getenv("CS_CONV0_DIRECT")) conv0_direct_ = atoi(e) != 0;
-  if (const char* e = getenv("CS_CONV0_BN_FOLD")) conv0_bn_fold_ = atoi(e) != 0;
-  if (const char* e = getenv("CS_CONV0_SGD_FOLD")) conv0_sgd_fold_ = atoi(e) != 0;
-  if (const char* e = getenv("CS_CONV0_BATCH_FOLD")) conv0_batch_fold_ = atoi(e) != 0;
-  if (const char* e = getenv("CS_HEAD_BN_FOLD")) head_bn_fold_ = atoi(e) != 0;
-  if (const char* e = getenv("CS_SIDE_SGD_TAIL")) side_sgd_tail_ = atoi(e) != 0;
-  if (const char* e = getenv("CS_HEAD_TAIL")) head_tail_ = atoi(e) != 0;
-  if (const char* e = getenv("CS_SIDE_JOIN_ONCE")) side_join_once_ = atoi(e) != 0;
-  if (const char* e = getenv("CS_BN_BWD_FUSED_P")) bwd_fused_p_ = atoi(e);
+  amax_ = torch::zeros({3 * L * CS_AMAX_SHARDS}, fo);
+  for (int64_t l = 0; l < L; ++l) wslot_.push_back((int)l);
   bn_part_ = torch::zeros({partmax}, fo);
   bn_coef_ = torch::zeros({cmax * 3}, fo);
   bn_eval_ = torch::zeros({2, cmax}, fo);
@@ -266,21 +255,27 @@ CsConvArgs VggEngine::conv_args(int l, int mode, int B, bool with_stats, float* 
     a.bias = P(b.b_off);
     a.out = b.y.data_ptr<float>();
     a.stats = with_stats ? b.stats.data_ptr<float>() : nullptr;
+    a.amax_a = amax_x(l);
+    a.amax_b = amax_w(l);
   } else if (mode == CS_CONV_DGRAD) {
     TORCH_CHECK(l > 0, "VggEngine: no dgrad for block 0");
     a.dz = dz;
     a.w = P(b.w_off);
     a.out = gbuf_[(L - l) % 2].data_ptr<float>();
+    a.amax_a = amax_dz(l);
+    a.amax_b = amax_w(l);
   } else {
     a.x = b.x.data_ptr<float>();
     a.dz = dz;
     a.out = G(b.w_off);
+    a.amax_a = amax_dz(l);
+    a.amax_b = amax_x(l);
   }
   return a;
 }
 
 void VggEngine::conv(int l, int mode, int B, const ConvTile& t, hipStream_t s, bool with_stats, float* ws,
-                     float* dz, const CsBnRed* ered, const CsSgdTail* sgd, const CsBnFin* fin) {
+                     float* dz, const CsBnRed* ered, const CsSgdTail* sgd) {
   VggBlock& b = blocks_[l];
   CsConvArgs a = conv_args(l, mode, B, with_stats, ws, dz);
   if (ered != nullptr) {
@@ -288,13 +283,6 @@ void VggEngine::conv(int l, int mode, int B, const ConvTile& t, hipStream_t s, b
     a.ered = *ered;
   }
   if (sgd != nullptr) a.sgd = *sgd;
-  if (fin != nullptr) a.fin = *fin;
-  if (head_next_.P > 0 && mode == CS_CONV_WGRAD && s == side_ && l + 1 == (int)blocks_.size()) {
-    a.head = head_next_;  // the classifier's column pass (forward_train) rides this launch
-    head_next_.P = 0;
-  }
-  a.start_sig = start_sig_;  // the staggered fork's deferred signal rides this launch (once)
-  start_sig_ = nullptr;
   const Dims d = dims(b, mode, B);
   const int sp = eff_splits(d.K, t.splits, t.bk);
   TORCH_CHECK(sp == 1 || (int64_t)sp * d.M * d.N <= ws_elems_, "VggEngine: split-K workspace too small");
@@ -304,23 +292,6 @@ void VggEngine::conv(int l, int mode, int B, const ConvTile& t, hipStream_t s, b
 bool VggEngine::bn_fused(int l, int64_t B) const {
   const VggBlock& b = blocks_[l];
   return B * b.H * b.H <= bn_fused_rows_ && b.cout % 16 == 0;
-}
-
-bool VggEngine::dual_ok(int l) const {
-  if (!dual_ || l == 0 || !blocks_[l].use_dual) return false;
-  const ConvTile& w = blocks_[l].tile[CS_CONV_WGRAD];
-  const ConvTile& d = blocks_[l].tile[CS_CONV_DGRAD];
-  return w.bm == 64 && w.bn == 64 && d.bm == 64 && d.bn == 64 && cs_conv_dual_ok(w.stage, w.bk, d.stage, d.bk);
-}
-
-void VggEngine::conv_dual(int l, int B, hipStream_t s, float* dz, const CsBnRed* ered, const CsBnFin* fin) {
-  const ConvTile& w = blocks_[l].tile[CS_CONV_WGRAD];
-  const ConvTile& d = blocks_[l].tile[CS_CONV_DGRAD];
-  CsConvArgs wa = conv_args(l, CS_CONV_WGRAD, B, false, ws_w_.data_ptr<float>(), dz);
-  CsConvArgs da = conv_args(l, CS_CONV_DGRAD, B, false, nullptr, dz);
-  if (ered != nullptr) da.ered = *ered;
-  if (fin != nullptr) da.fin = *fin;
-  ok(cs_conv_gemm_dual(wa, w.bk, w.splits, da, d.bk, d.splits, s, w.stage), "conv_gemm_dual");
 }
 
 CsSgdTail VggEngine::sgd_tail_args(int64_t block) {
@@ -336,7 +307,35 @@ CsSgdTail VggEngine::sgd_tail_args(int64_t block) {
   t.wd = (float)hp_[2];
   t.damp = (float)hp_[3];
   t.first = sgd_first_ ? 1 : 0;
+  t.amax = sgd_amax(off, n);
   return t;
+}
+
+float* VggEngine::sgd_amax(int64_t off, int64_t n) {
+  if (!f3_used_ || f3_probe_) return nullptr;
+  int lo = -1;
+  for (int l = 0; l < (int)blocks_.size(); ++l)
+    if (blocks_[l].w_off >= off && blocks_[l].w_off < off + n) lo = lo < 0 ? l : std::min(lo, l);
+  if (lo < 0) return nullptr;
+  for (int l = 0; l < (int)blocks_.size(); ++l)
+    if (blocks_[l].w_off >= off && blocks_[l].w_off < off + n) wslot_[l] = lo;
+  return amax_slot(lo);
+}
+
+void VggEngine::f3_refresh(hipStream_t s) {
+  if (!f3_used_ || f3_probe_) return;
+  const int L = (int)blocks_.size();
+  if (w_dirty_) {
+    ok(hipMemsetAsync(amax_slot(0), 0, (size_t)L * CS_AMAX_SHARDS * sizeof(float), s), "amax(w) reset");
+    for (int l = 1; l < L; ++l) {
+      const VggBlock& b = blocks_[l];
+      ok(cs_amax(P(b.w_off), (int64_t)b.cout * 9 * b.cin, amax_slot(l), s), "amax(w)");
+      wslot_[l] = l;
+    }
+    w_dirty_ = false;
+  }
+  // x / dz bounds are per step: folded in by this step's BN apply / backward launches
+  ok(hipMemsetAsync(amax_x(0), 0, (size_t)2 * L * CS_AMAX_SHARDS * sizeof(float), s), "amax(x, dz) reset");
 }
 
 CsBnRed VggEngine::ered_args(int l, int B) {
@@ -361,49 +360,6 @@ CsBnRed VggEngine::ered_args(int l, int B) {
   return r;
 }
 
-CsBnFin VggEngine::fin_fwd_args(int l, int B) {
-  VggBlock& b = blocks_[l];
-  const ConvTile& t = b.tile[CS_CONV_FWD];
-  const Dims d = dims(b, CS_CONV_FWD, B);
-  const int R = cs_conv_stat_rows((int)d.K, t.bm, t.bk, t.splits);
-  CsBnFin f{};
-  f.cnt = fin_cnt_.data_ptr<int>() + b.fin_fwd;
-  f.grp = fin_grp_.data_ptr<float>();
-  f.R = R;
-  f.M = (int)d.M;
-  f.T = (int)cdiv(d.M, R);
-  f.gamma = P(b.g_off);
-  f.beta = P(b.be_off);
-  f.rmean = bufs_.data_ptr<float>() + b.rm_off;
-  f.rvar = bufs_.data_ptr<float>() + b.rv_off;
-  f.nbt = nbt_.data_ptr<int64_t>() + l;
-  f.momentum = kBnMomentum;
-  f.eps = kBnEps;
-  f.bnv = b.bn.data_ptr<float>();
-  return f;
-}
-
-CsBnFin VggEngine::fin_bwd_args(int l, int B) {
-  VggBlock& c = blocks_[l - 1];
-  const ConvTile& t = blocks_[l].tile[CS_CONV_DGRAD];
-  const Dims d = dims(blocks_[l], CS_CONV_DGRAD, B);
-  const int R = cs_conv_ered_rows((int)d.K, t.bm, t.bk, t.splits);
-  CsBnFin f{};
-  f.cnt = fin_cnt_.data_ptr<int>() + blocks_[l].fin_bwd;
-  f.grp = fin_grp_.data_ptr<float>();
-  f.R = R;
-  f.M = (int)d.M;
-  f.T = (int)cdiv(d.M, R);
-  f.count = B * c.H * c.H;
-  f.gamma = P(c.g_off);
-  f.invstd = c.bn.data_ptr<float>() + 3 * c.cout;
-  f.coef = bn_coef_.data_ptr<float>();
-  f.dgamma = G(c.g_off);
-  f.dbeta = G(c.be_off);
-  f.dbias = G(c.b_off);
-  return f;
-}
-
 bool VggEngine::side_ok(hipStream_t s) const { return overlap_ && side_ != nullptr && !stream_capturing(s); }
 
 void VggEngine::flush_signal(hipStream_t s) {
@@ -416,20 +372,12 @@ void VggEngine::flush_side_sgd() {
   // the SGD of the last block whose weight gradient forked, not yet carried by a later one
   if (side_sgd_pending_ < 0) return;
   sgd_on(side_, blk_range_[side_sgd_pending_].first, blk_range_[side_sgd_pending_].second, false);
-  if (side_join_once_)
-    side_dirty_ = true;
-  else
-    wg_link_->signal(side_);
+  wg_link_->signal(side_);
   side_sgd_pending_ = -1;
 }
 
 void VggEngine::join_side(hipStream_t s) {
-  TORCH_CHECK(head_next_.P == 0, "VggEngine: the classifier column pass was never launched");
   flush_side_sgd();
-  if (side_dirty_) {  // one join signal for everything forked since the last join (side_join_once_)
-    wg_link_->signal(side_);
-    side_dirty_ = false;
-  }
   flush_signal(s);  // the side stream may be waiting for it: never wait on side before it is out
   wg_link_->wait(s);
 }
@@ -441,6 +389,7 @@ void VggEngine::forward_train(int64_t B) {
   const int L = (int)blocks_.size();
   red_pending_ = -1;
   flush_signal(s);
+  f3_refresh(s);
   // one launch: sampler index (device cursor into the epoch permutation, or idx_ when no
   // permutation is set), label gather, crop/flip/normalize into block 0's NHWC input
   const bool use_perm = perm_len_ > 0;
@@ -467,11 +416,7 @@ void VggEngine::forward_train(int64_t B) {
     float* bn = b.bn.data_ptr<float>();
     if (l == defer_block_) join_deferred(s);  // the previous step's deferred buckets wrote these weights
     float* out = (l + 1 < L) ? blocks_[l + 1].x.data_ptr<float>() : feats_.data_ptr<float>();
-    if (fin_on_ && !(l == 0 && conv0_direct_ok(B))) {
-      // conv [+ split-K combine]: its last-arriving block finalizes the batch statistics
-      const CsBnFin f = fin_fwd_args(l, (int)B);
-      conv(l, CS_CONV_FWD, (int)B, t, s, true, nullptr, nullptr, nullptr, nullptr, &f);
-    } else if (!(debug_skip_ & 8)) {
+    if (!(debug_skip_ & 8)) {
       const int64_t M = B * b.H * b.H;
       int rows;
       if (l == 0 && conv0_direct_ok(B)) {
@@ -484,19 +429,6 @@ void VggEngine::forward_train(int64_t B) {
         rows = cs_conv_stat_rows(9 * b.cin, t.bm, t.bk, t.splits);
       }
       const int T = (int)cdiv(M, rows);
-      if (T <= fwd_fused_t_ && b.cout % 16 == 0) {
-        if (lag_pending_ && l + 1 >= L - lag_blocks_) {
-          lag_out_->wait(s);
-          lag_pending_ = false;
-        }
-        // finalize + normalize/ReLU(/pool) in one launch: each block re-combines its 16 channels'
-        // T tile partials (the same fixed order in every block) instead of waiting on a finalize
-        ok(cs_bn_fused_fwd(b.stats.data_ptr<float>(), T, rows, (int)M, b.cout, P(b.g_off), P(b.be_off),
-                           bufs + b.rm_off, bufs + b.rv_off, nbt_.data_ptr<int64_t>() + l, kBnMomentum, kBnEps, bn,
-                           b.y.data_ptr<float>(), out, (int)B, b.H, b.H, b.pool, s),
-           "bn_fused_fwd");
-        continue;
-      }
       ok(cs_bn_finalize(b.stats.data_ptr<float>(), T, rows, (int)M, b.cout, P(b.g_off),
                         P(b.be_off), bufs + b.rm_off, bufs + b.rv_off, nbt_.data_ptr<int64_t>() + l, kBnMomentum,
                         kBnEps, bn, bn + b.cout, bn + 2 * b.cout, bn + 3 * b.cout, s),
@@ -504,19 +436,15 @@ void VggEngine::forward_train(int64_t B) {
     } else {
       conv(l, CS_CONV_FWD, (int)B, t, s, true);
     }
-    if (lag_pending_ && l + 1 >= L - lag_blocks_) {
-      // the deferred weight gradients read this block's output activation (the next block's input)
-      // and the lagged blocks' parameters: wait for them before overwriting / reading either
-      lag_out_->wait(s);
-      lag_pending_ = false;
-    }
     if (l + 1 == L && head_bn_fold_ && b.pool && b.H == 2 && b.cout == feat_ && !(debug_skip_ & 4)) {
       // the last block's normalize/ReLU/pool runs inside the classifier's row pass (below)
       head_bn = CsHeadBn{b.y.data_ptr<float>(), bn, bn + b.cout};
       continue;
     }
     if (!(debug_skip_ & 4))
-    ok(cs_bn_apply(b.y.data_ptr<float>(), bn, bn + b.cout, out, (int)B, b.H, b.H, b.cout, b.pool, s), "bn_apply");
+    ok(cs_bn_apply(b.y.data_ptr<float>(), bn, bn + b.cout, out, (int)B, b.H, b.H, b.cout, b.pool, s,
+                   l + 1 < L ? x_amax_out(l + 1) : nullptr),
+       "bn_apply");
   }
   // classifier + loss: dfeat -> gbuf_[0]. Inside the overlapped step the per-column pass (dW, db,
   // loss, accuracy: only the SGD and the host read them) forks to the side stream, off the
@@ -527,23 +455,14 @@ void VggEngine::forward_train(int64_t B) {
                     G(fc_w_), G(fc_b_), gbuf_[0].data_ptr<float>(), pred_.data_ptr<int64_t>(), head_ws_.data_ptr<float>(), s,
                     fork ? 1 : 0, head_bn.y != nullptr ? &head_bn : nullptr),
      "linear_xent");
-  if (fork && head_tail_ && !stagger_ && lag_blocks_ == 0 && !(debug_skip_ & 32)) {
-    // the column pass rides the top block's weight-gradient launch on the side stream (extra
-    // workgroups; that launch forks after the top block's data gradient, long after this row pass)
-    head_next_ = CsHeadCols{feats_.data_ptr<float>(), (int)B, (int)feat_, (int)ncls_, head_ws_.data_ptr<float>(),
-                            G(fc_w_), G(fc_b_), loss_.data_ptr<float>(), correct_.data_ptr<int>(),
-                            cs_head_cols_pieces((int)feat_, (int)ncls_)};
-  } else if (fork) {
+  if (fork) {
     pending_sig_ = dz_link_->defer();  // rides the top block's BN backward launch
     dz_link_->wait(side_);
     ok(cs_linear_xent(feats_.data_ptr<float>(), P(fc_w_), P(fc_b_), ylab_.data_ptr<int64_t>(), (int)B, (int)feat_,
                       (int)ncls_, 1.0f, loss_.data_ptr<float>(), correct_.data_ptr<int>(), logits_.data_ptr<float>(),
                       G(fc_w_), G(fc_b_), nullptr, pred_.data_ptr<int64_t>(), head_ws_.data_ptr<float>(), side_, 2),
        "linear_xent(cols)");
-    if (side_join_once_)
-      side_dirty_ = true;
-    else
-      wg_link_->signal(side_);
+    wg_link_->signal(side_);
   }
 }
 
@@ -563,8 +482,7 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
     // l+1's fork rides its first launch)
     if (debug_skip_ & 16) {
       flush_signal(s);
-    } else if (red_pending_ == l && l == 0 && !fin_on_ && conv0_bn_fold_ && b.pool && conv0_direct_ok(B) &&
-               !(red_P_ <= bwd_fused_p_ && b.cout % 16 == 0)) {
+    } else if (red_pending_ == l && l == 0 && conv0_bn_fold_ && b.pool && conv0_direct_ok(B)) {
       // block 0: only the finalize here; the apply runs inside the weight gradient (conv0_wgrad)
       ok(cs_bn_bwd_finalize(bn_part_.data_ptr<float>(), red_P_, b.cout, (int)(B * b.H * b.H), P(b.g_off),
                             bn + 3 * b.cout, bn_coef_.data_ptr<float>(), G(b.g_off), G(b.be_off), G(b.b_off), s,
@@ -573,79 +491,47 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
       pending_sig_ = nullptr;
       conv0_bn_G_ = Gin;
     } else if (red_pending_ == l) {
-      // the partial sums (and, with fin, the finalize) ran inside block l+1's data-gradient launch
-      if (fin_on_)
-        ok(cs_bn_bwd_apply(b.y.data_ptr<float>(), Gin, (int)B, b.H, b.H, b.cout, b.pool, bn, bn + b.cout,
-                           bn + 2 * b.cout, bn + 3 * b.cout, bn_coef_.data_ptr<float>(), dz, s, pending_sig_),
-           "bn_bwd_apply");
-      else if (red_P_ <= bwd_fused_p_ && b.cout % 16 == 0)
-        // finalize + apply in one launch (cs_bn_fused_fwd's backward twin)
-        ok(cs_bn_bwd_tail_fused(b.y.data_ptr<float>(), Gin, (int)B, b.H, b.H, b.cout, b.pool, bn, P(b.g_off),
-                                bn_part_.data_ptr<float>(), red_P_, bn_coef_.data_ptr<float>(), G(b.g_off),
-                                G(b.be_off), G(b.b_off), dz, s, pending_sig_),
-           "bn_bwd_tail_fused");
-      else
-        ok(cs_bn_bwd_tail(b.y.data_ptr<float>(), Gin, (int)B, b.H, b.H, b.cout, b.pool, bn, bn + b.cout,
-                          bn + 2 * b.cout, bn + 3 * b.cout, P(b.g_off), bn_part_.data_ptr<float>(), red_P_,
-                          bn_coef_.data_ptr<float>(), G(b.g_off), G(b.be_off), G(b.b_off), dz, s, pending_sig_),
-           "bn_bwd_tail");
+      // the partial sums ran inside block l+1's data-gradient launch: finalize + apply
+      ok(cs_bn_bwd_tail(b.y.data_ptr<float>(), Gin, (int)B, b.H, b.H, b.cout, b.pool, bn, bn + b.cout,
+                        bn + 2 * b.cout, bn + 3 * b.cout, P(b.g_off), bn_part_.data_ptr<float>(), red_P_,
+                        bn_coef_.data_ptr<float>(), G(b.g_off), G(b.be_off), G(b.b_off), dz, s, pending_sig_,
+                        dz_amax_out(l)),
+         "bn_bwd_tail");
       pending_sig_ = nullptr;
     } else if (bn_fused(l, B)) {  // reduce + finalize + apply in one launch (the top block)
       ok(cs_bn_fused_bwd(b.y.data_ptr<float>(), Gin, (int)B, b.H, b.H, b.cout, b.pool, bn, P(b.g_off),
-                         bn_coef_.data_ptr<float>(), G(b.g_off), G(b.be_off), G(b.b_off), dz, s, pending_sig_),
+                         bn_coef_.data_ptr<float>(), G(b.g_off), G(b.be_off), G(b.b_off), dz, s, pending_sig_,
+                         dz_amax_out(l)),
          "bn_fused_bwd");
       pending_sig_ = nullptr;
     } else {
       flush_signal(s);
       ok(cs_bn_bwd(b.y.data_ptr<float>(), Gin, (int)B, b.H, b.H, b.cout, b.pool, bn, bn + b.cout,
                    bn + 2 * b.cout, bn + 3 * b.cout, P(b.g_off), bn_part_.data_ptr<float>(),
-                   bn_coef_.data_ptr<float>(), G(b.g_off), G(b.be_off), G(b.b_off), dz, s),
+                   bn_coef_.data_ptr<float>(), G(b.g_off), G(b.be_off), G(b.b_off), dz, s, dz_amax_out(l)),
          "bn_bwd");
     }
     red_pending_ = -1;
-    // ---- weight and data gradients of block l; block l-1's BN-backward partials (and their
-    // finalize) ride the data gradient
-    // (measured against the BN backward's own reduce pass next to the side stream: +0.2-0.7 %,
-    // profiles/r4_ab_bn_epi_red.txt)
+    // ---- weight and data gradients of block l; block l-1's BN-backward partials ride the data
+    // gradient (measured against the BN backward's own reduce pass next to the side stream:
+    // +0.2-0.7 %, profiles/r4_ab_bn_epi_red.txt)
     const bool er = l > 0;
     CsBnRed erv{};
-    CsBnFin fin{};
-    if (er) {
-      erv = ered_args(l, (int)B);
-      if (fin_on_) fin = fin_bwd_args(l, (int)B);
-    }
-    const CsBnFin* fp = er && fin_on_ ? &fin : nullptr;
+    if (er) erv = ered_args(l, (int)B);
     if (ovl) {
       if (l > 0) {
         // the data gradient keeps the whole chip on the critical chain; the weight gradient forks
         // to the side stream after it and fills the chip while the main stream runs the
-        // latency-bound BN kernels (and the split-K combine) of the block below.
-        // Staggered (stagger_): block l+1's weight gradient, held back one block, forks when THIS
-        // data gradient starts (its launch carries the signal), so the data gradient's blocks take
-        // the CUs first and the side GEMM fills its tail and the BN gaps after it, instead of
-        // holding LDS that keeps data-gradient blocks off their CUs
-        if (side_pending_ >= 0) start_sig_ = dz_link_->defer();
-        conv(l, CS_CONV_DGRAD, (int)B, b.tile[CS_CONV_DGRAD], s, false, nullptr, dz, &erv, nullptr, fp);
-        if (side_pending_ >= 0) fork_wgrad(side_pending_, B, false);
-        if (lag_on(s) && l >= L - lag_blocks_) {
-          lag_list_.push_back(l);  // weight gradient + SGD deferred to the lag stream (step end)
-        } else if (stagger_) {
-          side_pending_ = l;
-        } else {
-          pending_sig_ = dz_link_->defer();
-          fork_wgrad(l, B, true);
-        }
+        // latency-bound BN kernels (and the split-K combine) of the block below
+        conv(l, CS_CONV_DGRAD, (int)B, b.tile[CS_CONV_DGRAD], s, false, nullptr, dz, &erv);
+        pending_sig_ = dz_link_->defer();
+        fork_wgrad(l, B);
       } else {
         // block 0's weight gradient is the step's last GEMM: nothing left to overlap it with, so it
         // runs here (the main split-K workspace is free: no data gradient for block 0)
-        if (side_pending_ >= 0) start_sig_ = dz_link_->defer();
         const bool sgd_done = conv0_wgrad(B, s, dz, bwd_sgd_);
-        if (side_pending_ >= 0) fork_wgrad(side_pending_, B, false);
         if (bwd_sgd_ && !sgd_done) sgd_on(s, blk_range_[0].first, blk_range_[0].second, true);
       }
-    } else if (dual_ok(l)) {  // wgrad + dgrad in one launch (no appended SGD blocks: the update runs first)
-      if (sgd_tail_ && l + 1 < L) sgd_on(s, blk_range_[l + 1].first, blk_range_[l + 1].second, false);
-      conv_dual(l, (int)B, s, dz, &erv, fp);
     } else {
       // block l+1's SGD rides this weight-gradient launch (its BN backward and data gradient ran)
       CsSgdTail tail{};
@@ -660,37 +546,16 @@ void VggEngine::backward(int64_t hi, int64_t lo, int64_t B, bool join) {
         conv(l, CS_CONV_WGRAD, (int)B, b.tile[CS_CONV_WGRAD], s, false, ws_w_.data_ptr<float>(), dz, nullptr,
              tail.n > 0 ? &tail : nullptr);
       }
-      if (l > 0)
-        conv(l, CS_CONV_DGRAD, (int)B, b.tile[CS_CONV_DGRAD], s, false, nullptr, dz, &erv, nullptr, fp);
+      if (l > 0) conv(l, CS_CONV_DGRAD, (int)B, b.tile[CS_CONV_DGRAD], s, false, nullptr, dz, &erv);
     }
     if (er) {
       red_pending_ = l - 1;
       red_P_ = erv.P;
     }
   }
-  // a weight gradient still held back at the end of this range (a bucket boundary): fork it now,
-  // behind the next main-stream launch as the unstaggered fork does, so the bucket's all-reduce
-  // (forked from the side stream next) covers it
-  if (side_pending_ >= 0) {
-    flush_signal(s);
-    pending_sig_ = dz_link_->defer();
-    fork_wgrad(side_pending_, B, false);
-  }
   if (join) {
     flush_signal(s);
     if (ovl) join_side(s);
-  }
-}
-
-void VggEngine::set_lag(int64_t n) {
-  join_lag();  // work deferred under the old setting is waited for where the new one expects none
-  lag_blocks_ = (int)n;
-  // the stream and its links are made here, never inside a step: creating either synchronises the
-  // device, which would wait on a side-stream link whose signal rides a launch not yet enqueued
-  if (lag_blocks_ > 0 && lag_ == nullptr) {
-    lag_ = reserved_lag_stream();
-    lag_in_ = std::make_unique<StreamLink>();
-    lag_out_ = std::make_unique<StreamLink>();
   }
 }
 
@@ -716,10 +581,6 @@ bool VggEngine::conv0_wgrad(int64_t B, hipStream_t s, float* dz, bool with_sgd) 
     counter = perm_len_ > 0 ? cursor_.data_ptr<int64_t>() : nullptr;
   }
   const CsSgdTail* sp = sgd.n > 0 ? &sgd : nullptr;
-  if (start_sig_ != nullptr) {  // the deferred fork signal this launch would have carried
-    ok(cs_link_signal(start_sig_, s), "link signal");
-    start_sig_ = nullptr;
-  }
   if (conv0_bn_G_ != nullptr) {  // block 0's BN-backward apply folded in (dz is not written)
     const float* bn = b.bn.data_ptr<float>();
     const float* Gin = conv0_bn_G_;
@@ -736,17 +597,7 @@ bool VggEngine::conv0_wgrad(int64_t B, hipStream_t s, float* dz, bool with_sgd) 
   return sp != nullptr;
 }
 
-bool VggEngine::lag_on(hipStream_t s) const {
-  const int L = (int)blocks_.size();
-  return lag_blocks_ > 0 && lag_blocks_ <= L - 2 && in_step_ && bwd_sgd_ && side_ok(s) && lag_ != nullptr;
-}
-
-void VggEngine::join_lag() {
-  join_deferred(cur_stream());
-  if (!lag_pending_) return;
-  lag_out_->wait(cur_stream());
-  lag_pending_ = false;
-}
+void VggEngine::join_lag() { join_deferred(cur_stream()); }
 
 void VggEngine::join_deferred(hipStream_t s) {
   if (defer_comm_ == nullptr) return;
@@ -755,7 +606,7 @@ void VggEngine::join_deferred(hipStream_t s) {
   defer_block_ = -1;
 }
 
-void VggEngine::fork_wgrad(int l, int64_t B, bool current) {
+void VggEngine::fork_wgrad(int l, int64_t B) {
   // the side stream waits for the deferred signal just issued (it rides a main-stream launch), then
   // block l's weight gradient into its own dz buffer's consumer, its SGD, and the join signal
   VggBlock& b = blocks_[l];
@@ -777,11 +628,7 @@ void VggEngine::fork_wgrad(int l, int64_t B, bool current) {
     sgd_on(side_, tail.p - P(0), tail.n, false);
   }
   if (bwd_sgd_) side_sgd_pending_ = l;
-  if (side_join_once_)
-    side_dirty_ = true;
-  else
-    wg_link_->signal(side_);
-  if (!current) side_pending_ = -1;
+  wg_link_->signal(side_);
 }
 
 std::string VggEngine::link_error() const {
@@ -798,7 +645,7 @@ void VggEngine::sgd_on(hipStream_t st, int64_t off, int64_t n, bool cursor) {
   if (n == 0) return;
   ok(cs_sgd_flat(P(off), G(off), mom_.data_ptr<float>() + off, n, (float)hp_[0], (float)hp_[1], (float)hp_[2],
                  (float)hp_[3], 1.0f, sgd_first_ ? 1 : 0, st,
-                 cursor && perm_len_ > 0 ? cursor_.data_ptr<int64_t>() : nullptr),
+                 cursor && perm_len_ > 0 ? cursor_.data_ptr<int64_t>() : nullptr, sgd_amax(off, n)),
      "sgd_flat(block)");
 }
 
@@ -810,7 +657,7 @@ void VggEngine::sgd(double lr, double momentum, double wd, double dampening, int
   // device-side batch cursor
   ok(cs_sgd_flat(P(off), G(off), mom_.data_ptr<float>() + off, n, (float)lr, (float)momentum, (float)wd,
                  (float)dampening, 1.0f, sgd_first_ ? 1 : 0, cur_stream(),
-                 perm_len_ > 0 ? cursor_.data_ptr<int64_t>() : nullptr),
+                 perm_len_ > 0 ? cursor_.data_ptr<int64_t>() : nullptr, sgd_amax(off, n)),
      "sgd_flat");
   sgd_first_ = false;
 }
@@ -869,6 +716,7 @@ void VggEngine::forward_eval(int64_t B) {
   join_lag();
   hipStream_t s = cur_stream();
   const int L = (int)blocks_.size();
+  f3_refresh(s);
   ok(cs_gather_labels(labels_[1].data_ptr<int64_t>(), idx_.data_ptr<int64_t>(), ylab_.data_ptr<int64_t>(), (int)B, s),
      "gather_labels");
   ok(cs_augment(data_[1].data_ptr<uint8_t>(), idx_.data_ptr<int64_t>(), aug_[1].data_ptr<int32_t>(),
@@ -888,7 +736,9 @@ void VggEngine::forward_eval(int64_t B) {
     ok(cs_bn_eval_coeffs(P(b.g_off), P(b.be_off), bufs + b.rm_off, bufs + b.rv_off, b.cout, kBnEps, sc, sh, s),
        "bn_eval_coeffs");
     float* out = (l + 1 < L) ? blocks_[l + 1].x.data_ptr<float>() : feats_.data_ptr<float>();
-    ok(cs_bn_apply(b.y.data_ptr<float>(), sc, sh, out, (int)B, b.H, b.H, b.cout, b.pool, s), "bn_apply");
+    ok(cs_bn_apply(b.y.data_ptr<float>(), sc, sh, out, (int)B, b.H, b.H, b.cout, b.pool, s,
+                   l + 1 < L ? x_amax_out(l + 1) : nullptr),
+       "bn_apply");
   }
   ok(cs_linear_xent(feats_.data_ptr<float>(), P(fc_w_), P(fc_b_), ylab_.data_ptr<int64_t>(), (int)B, (int)feat_,
                     (int)ncls_, 1.0f, loss_.data_ptr<float>(), correct_.data_ptr<int>(), logits_.data_ptr<float>(),
@@ -928,7 +778,11 @@ void VggEngine::step_impl(int64_t B, DeviceComm* comm, const std::vector<int64_t
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
   ok(hipStreamIsCapturing(s, &cap), "hipStreamIsCapturing");
   const bool capturing = cap != hipStreamCaptureStatusNone;
-  if (defer_comm_ != nullptr && (capturing || defer_comm_ != comm)) join_deferred(s);
+  // a join inside a capture would wait on a stream that is not captured (the dependency could be
+  // dropped): the caller joins before capturing (NativeTrainer._capture -> join_lag)
+  TORCH_CHECK(!(capturing && defer_comm_ != nullptr),
+              "VggEngine::step: deferred buckets pending while capturing a graph; call join_lag() first");
+  if (defer_comm_ != nullptr && defer_comm_ != comm) join_deferred(s);
   std::vector<size_t> deferred;
   tn_ = 0;
   Range step_range("cs.step");
@@ -1028,24 +882,6 @@ void VggEngine::step_impl(int64_t B, DeviceComm* comm, const std::vector<int64_t
       defer_comm_ = comm;
     }
   }
-  if (!lag_list_.empty()) {
-    // deferred weight gradients: the lag stream starts once the step's main stream (joined with
-    // the side stream: the head's column pass wrote the fc gradient the top block's SGD reads) is
-    // done — an explicit signal kernel, so nothing waits on a launch that may never come
-    Range r("cs.lag.fork");
-    flush_signal(s);
-    lag_in_->signal(s);
-    lag_in_->wait(lag_);
-    for (int l : lag_list_) {
-      if (!(debug_skip_ & 32))
-        conv(l, CS_CONV_WGRAD, (int)B, blocks_[l].tile[CS_CONV_WGRAD], lag_, false, ws_w_.data_ptr<float>(),
-             dz_blk_[l].data_ptr<float>());
-      sgd_on(lag_, blk_range_[l].first, blk_range_[l].second, false);
-    }
-    lag_out_->signal(lag_);
-    lag_pending_ = true;
-    lag_list_.clear();
-  }
   mark("allreduce_wait");
   {
     Range r("cs.sgd");
@@ -1063,6 +899,11 @@ void VggEngine::step_impl(int64_t B, DeviceComm* comm, const std::vector<int64_t
   mark("sgd");
 }
 
+void VggEngine::set_f3_probe(bool on) {
+  f3_probe_ = on;
+  if (on) amax_.fill_(1.0f);
+}
+
 void VggEngine::set_tile(int64_t block, int64_t mode, int64_t bm, int64_t bn, int64_t splits, int64_t bk,
                          int64_t stage) {
   TORCH_CHECK(block >= 0 && block < (int64_t)blocks_.size() && mode >= 0 && mode <= 2, "set_tile: index");
@@ -1072,9 +913,15 @@ void VggEngine::set_tile(int64_t block, int64_t mode, int64_t bm, int64_t bn, in
   TORCH_CHECK((bk == 16 || bk == 32 || bk == 64) && cs_conv_stage_ok((int)stage, (int)bm, (int)bn, (int)bk, conv0_fwd) &&
                   !(conv0_fwd && bk == 64),
               "set_tile: no kernel for stage ", stage, " with a ", bm, "x", bn, " tile and bk ", bk);
+  // block 0's input has no producer-written bound (make_batch / the conv0 batch fold)
+  TORCH_CHECK(!(stage & CS_STAGE_F3) || block > 0, "set_tile: the F3 conv math is for blocks >= 1");
   const int sp = eff_splits(d.K, (int)splits, (int)bk);
   TORCH_CHECK(sp == 1 || (int64_t)sp * d.M * d.N <= ws_elems_, "set_tile: split-K workspace too small");
   ConvTile& t = blocks_[block].tile[mode];
+  if ((stage & CS_STAGE_F3) && !f3_used_) {
+    f3_used_ = true;
+    w_dirty_ = true;
+  }
   t.bm = (int)bm;
   t.bn = (int)bn;
   t.splits = (int)splits;
@@ -1104,8 +951,6 @@ std::vector<double> VggEngine::autotune(int64_t B, int64_t iters) {
   ok(hipEventCreate(&e1), "event");
   std::vector<double> best_us;
   const int split_opts[] = {1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 64, 128, 256};
-  ConvTile best64[3];
-  float best64_t[3] = {1e30f, 1e30f, 1e30f};
   for (int l = 0; l < (int)blocks_.size(); ++l) {
     for (int mode = 0; mode < 3; ++mode) {
       if (l == 0 && mode == CS_CONV_DGRAD) {
@@ -1115,8 +960,6 @@ std::vector<double> VggEngine::autotune(int64_t B, int64_t iters) {
       const Dims d = dims(blocks_[l], mode, B);
       ConvTile best = blocks_[l].tile[mode];
       float best_t = 1e30f;
-      best64[mode] = best;
-      best64_t[mode] = 1e30f;
       std::vector<std::vector<int>> seen;
       const bool conv0_fwd = l == 0 && mode == CS_CONV_FWD && blocks_[0].cin == 4;
       for (int stage : {(int)CS_STAGE_REGS, (int)CS_STAGE_LDS_DMA, (int)CS_STAGE_LDS_DMA_DEEP, (int)CS_STAGE_KG2,
@@ -1164,11 +1007,6 @@ std::vector<double> VggEngine::autotune(int64_t B, int64_t iters) {
                 best_t = us;
                 best = t;
               }
-              if (bm == 64 && bn == 64 && stage == CS_STAGE_REGS && us < best64_t[mode]) {
-                best64_t[mode] = us;
-                best64[mode] = t;
-                best64[mode].us = us;
-              }
             }
           }
         }
@@ -1176,48 +1014,6 @@ std::vector<double> VggEngine::autotune(int64_t B, int64_t iters) {
       best.us = best_t;
       blocks_[l].tile[mode] = best;
       best_us.push_back(best_t);
-    }
-    // joint choice for the backward pair: one dual launch (wgrad + dgrad blocks in one grid)
-    // with the separately tuned tiles when they are dual-compatible (64x64, same staging), or
-    // with the best 64x64 f32 register-staged tiles, or the two separate launches — fastest wins
-    VggBlock& b = blocks_[l];
-    b.use_dual = false;
-    if (dual_ && l > 0) {
-      const ConvTile keep_w = b.tile[CS_CONV_WGRAD], keep_d = b.tile[CS_CONV_DGRAD];
-      float best_t = keep_w.us + keep_d.us;
-      ConvTile win_w = keep_w, win_d = keep_d;
-      std::vector<std::pair<ConvTile, ConvTile>> cands;
-      cands.emplace_back(keep_w, keep_d);
-      if (best64_t[CS_CONV_WGRAD] < 1e29f && best64_t[CS_CONV_DGRAD] < 1e29f)
-        cands.emplace_back(best64[CS_CONV_WGRAD], best64[CS_CONV_DGRAD]);
-      float* dz = dz_[l & 1].data_ptr<float>();
-      for (const auto& c : cands) {
-        b.tile[CS_CONV_WGRAD] = c.first;
-        b.tile[CS_CONV_DGRAD] = c.second;
-        b.use_dual = true;
-        if (!dual_ok(l)) continue;
-        conv_dual(l, (int)B, s, dz);  // warm
-        ok(hipEventRecord(e0, s), "record");
-        for (int64_t i = 0; i < iters; ++i) conv_dual(l, (int)B, s, dz);
-        ok(hipEventRecord(e1, s), "record");
-        ok(hipEventSynchronize(e1), "sync");
-        float ms = 0.f;
-        ok(hipEventElapsedTime(&ms, e0, e1), "elapsed");
-        const float dual_us = 1000.f * ms / (float)iters;
-        if (dual_us < best_t) {
-          best_t = dual_us;
-          win_w = c.first;
-          win_d = c.second;
-          const float tw = std::max(c.first.us, 1e-3f), td = std::max(c.second.us, 1e-3f);
-          win_w.us = dual_us * tw / (tw + td);
-          win_d.us = dual_us * td / (tw + td);
-        }
-      }
-      b.tile[CS_CONV_WGRAD] = win_w;
-      b.tile[CS_CONV_DGRAD] = win_d;
-      b.use_dual = best_t < keep_w.us + keep_d.us;
-      best_us[3 * l + CS_CONV_WGRAD] = win_w.us;
-      best_us[3 * l + CS_CONV_DGRAD] = win_d.us;
     }
   }
   hipEventDestroy(e0);

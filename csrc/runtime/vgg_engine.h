@@ -18,11 +18,10 @@
 // Every method enqueues on the caller's current HIP stream and never syncs the
 // host, so a whole step (or any bucket segment of it) can be captured as a graph.
 //
-// Kernel boundaries of one training step (round 4): the BatchNorm finalize of every block —
-// forward (batch statistics -> scale/shift, running stats) and backward (dgamma, dbeta, dbias,
-// dZ coefficients) — runs as the last-arriving block of the launch that produced its partial
-// sums (bn_fin.h: the conv GEMM epilogue, or its split-K combine), so a block's forward is
-// conv [+ combine] + apply and its backward apply + the two GEMMs (one launch when dual).
+// Kernel boundaries of one training step: a block's forward is conv [+ split-K combine] (BN tile
+// statistics from the epilogue) + BN finalize + apply (ReLU, pool); its backward is BN finalize +
+// apply (the partial sums come from the data-gradient epilogue of the block above) + data
+// gradient on the main stream, and the weight gradient + SGD on the side stream.
 #pragma once
 #include <torch/extension.h>
 
@@ -44,12 +43,10 @@ struct VggBlock {
   int cin = 0, cout = 0, H = 0, pool = 0;  // cin = 4 for the padded conv0
   int64_t w_off = 0, b_off = 0, g_off = 0, be_off = 0, rm_off = 0, rv_off = 0;
   ConvTile tile[3];
-  bool use_dual = true;  // backward wgrad + dgrad as one launch (if both tiles allow; autotuned)
   torch::Tensor x;      // [Bmax, H, H, cin]
   torch::Tensor y;      // [Bmax*H*H, cout]
   torch::Tensor stats;  // [ceil(Bmax*H*H/16), cout, 2] BN (mean, M2) partials per row tile
   torch::Tensor bn;     // [4, cout]: scale, shift, mean, invstd
-  int64_t fin_fwd = 0, fin_bwd = 0;  // this block's ticket ranges in fin_cnt_ (forward / backward finalize)
 };
 
 class VggEngine {
@@ -87,12 +84,7 @@ class VggEngine {
   void set_overlap(bool on) { overlap_ = on; }
   // SGD (momentum, weight decay, dampening) on [off, off+n) of the flat buffers
   void sgd(double lr, double momentum, double wd, double dampening, int64_t off, int64_t n);
-  void set_dual(bool on) { dual_ = on; }
   void set_bn_fused_rows(int64_t r) { bn_fused_rows_ = r; }
-  // in-launch BN finalize (bn_fin.h; default on): off = the separate finalize launches (tests)
-  void set_fin(bool on) { fin_on_ = on; }
-  bool block_dual(int64_t l) const { return blocks_.at(l).use_dual; }
-  void set_block_dual(int64_t l, bool on) { blocks_.at(l).use_dual = on; }
   // torch.optim.SGD's first step sets buf = d (no dampening): the next step's SGD launches
   // use first = 1 (only matters with dampening != 0); cleared once that step's SGD is enqueued
   void set_sgd_first(bool on) { sgd_first_ = on; }
@@ -107,55 +99,43 @@ class VggEngine {
   // 64 the next forward skips its wait for deferred buckets (ordering-test control).
   // CS_DEBUG_SKIP sets the mask at construction.
   void set_debug_skip(int64_t mask) { debug_skip_ = (int)mask; }
-  void set_stagger(bool on) { stagger_ = on; }
+  // Default-on schedule features, each a setter for the bitwise tests and one name in
+  // CS_ENGINE_OFF (constructor) for cross-process A/Bs:
   // block 0's convolution (3 -> 64) as the direct conv0.hip kernels instead of the implicit GEMM
-  // (forward + BN tile statistics, weight gradient); CS_CONV0_DIRECT=0 restores the GEMM
+  // (forward + BN tile statistics, weight gradient): conv0_direct
   void set_conv0_direct(bool on) { conv0_direct_ = on; }
   // with the direct kernels, block 0's BN-backward apply folded into its weight gradient (dZ of
-  // block 0 never written; CS_CONV0_BN_FOLD=0 keeps the separate apply launch)
+  // block 0 never written): conv0_bn_fold
   void set_conv0_bn_fold(bool on) { conv0_bn_fold_ = on; }
   // ... and block 0's SGD step (+ batch cursor) into the weight gradient's final sum (world 1,
-  // overlapped backward; CS_CONV0_SGD_FOLD=0 keeps the separate optimizer launch)
+  // overlapped backward): conv0_sgd_fold
   void set_conv0_sgd_fold(bool on) { conv0_sgd_fold_ = on; }
-  // ... and the training batch (make_batch) into the conv0 forward's input halo
+  // ... and the training batch (make_batch) into the conv0 forward's input halo: conv0_batch_fold
   void set_conv0_batch_fold(bool on) { conv0_batch_fold_ = on; }
-  // the last block's BN + ReLU + max-pool inside the classifier's row pass (no bn_apply launch at the
-  // forward's end; CS_HEAD_BN_FOLD=0 keeps it)
+  // the last block's BN + ReLU + max-pool inside the classifier's row pass: head_bn_fold
   void set_head_bn_fold(bool on) { head_bn_fold_ = on; }
-  // side stream: block l+1's SGD as extra workgroups of block l's weight-gradient launch (one SGD
-  // launch per block fewer; CS_SIDE_SGD_TAIL=0 launches each block's SGD behind its weight gradient)
+  // side stream: block l+1's SGD as extra workgroups of block l's weight-gradient launch: side_sgd_tail
   void set_side_sgd_tail(bool on) { side_sgd_tail_ = on; }
-  // the classifier's column pass as extra workgroups of the top block's side-stream weight-gradient
-  // launch instead of its own fork (CS_HEAD_TAIL=1; default: own launch behind a link wait)
-  void set_head_tail(bool on) { head_tail_ = on; }
-  // one side-stream join signal per join instead of one per fork (CS_SIDE_JOIN_ONCE=1; measured
-  // 2.4 % slower in-process: profiles/r5_ab_side_join_once.txt)
-  void set_side_join_once(bool on) { side_join_once_ = on; }
   bool conv0_direct(int64_t B) const { return conv0_direct_ok(B); }
-  // Deferred weight gradients (world 1, overlapped step): the top `n` blocks' weight gradients and
-  // SGD run on a lag stream that starts at the end of the step and overlaps the NEXT step's forward
-  // (whose BatchNorm gaps leave CUs idle) instead of the backward's data-gradient GEMMs; the forward
-  // waits for them before it overwrites their input activation (the apply of block L-n-1). Exact:
-  // every parameter is updated before its next use, so the numbers are bit-identical. 0 = off
-  // (CS_WGRAD_LAG). join_lag(): the current stream waits for deferred work (before reading params).
-  void set_lag(int64_t n);
+  // the current stream waits for deferred buckets' all-reduce + SGD (set_comm_defer, below): every
+  // host read of the parameters goes through here
   void join_lag();
   // Data-parallel steps: the buckets listed (bucket indices, never the last one) have their
   // all-reduce + SGD enqueued on the comm stream AFTER the last bucket's, and the step's closing
   // join covers only the others; the next step's forward waits for them right before the conv of
   // their lowest block. The bottom blocks' buckets — produced last by the backward, needed first by
   // the next forward — then no longer queue behind a large top bucket, whose collective instead
-  // overlaps the next forward's lower blocks. join_lag() waits for them too (eval, host reads).
+  // overlaps the next forward's lower blocks. join_lag() waits for them (eval, host reads).
   void set_comm_defer(std::vector<int64_t> buckets) { comm_defer_ = std::move(buckets); }
   std::vector<int64_t> comm_defer() const { return comm_defer_; }
   bool defer_pending() const { return defer_comm_ != nullptr; }
-  // single-launch BatchNorm (finalize folded into the apply pass, every block re-combining its 16
-  // channels' partials): forward for layers with <= fwd_t statistics partials, backward for <= bwd_p
-  // (0 = the separate finalize launch). CS_BN_FWD_FUSED_T / CS_BN_BWD_FUSED_P override.
-  void set_bn_fused_limits(int64_t fwd_t, int64_t bwd_p) {
-    fwd_fused_t_ = (int)fwd_t;
-    bwd_fused_p_ = (int)bwd_p;
-  }
+  // measurement only (WRONG numbers): every operand bound of the F3 conv math reads 1.0 and no
+  // producer writes one — prices the F3 GEMMs in the step before the bounds are produced
+  void set_f3_probe(bool on);
+  // the parameters were rewritten outside the engine's SGD (load, broadcast, init): the next step
+  // re-measures the weights' bounds for the F3 conv math
+  void params_changed() { w_dirty_ = true; }
+  torch::Tensor amax() const { return amax_; }
   // conv autotune candidates (CS_CONV_MATH): 0 f32, 1 x6, 2 f32 + x6 (default), 3 bf16 operands
   void set_math(int64_t m) {
     TORCH_CHECK(m >= 0 && m <= 3, "set_math: 0..3");
@@ -204,22 +184,16 @@ class VggEngine {
 
  private:
   void conv(int l, int mode, int B, const ConvTile& t, hipStream_t s, bool with_stats, float* ws = nullptr,
-            float* dz = nullptr, const CsBnRed* ered = nullptr, const CsSgdTail* sgd = nullptr,
-            const CsBnFin* fin = nullptr);
+            float* dz = nullptr, const CsBnRed* ered = nullptr, const CsSgdTail* sgd = nullptr);
   CsConvArgs conv_args(int l, int mode, int B, bool with_stats, float* ws, float* dz);
-  // block l's wgrad + dgrad as one launch (both 64x64 register-staged tiles)
-  bool dual_ok(int l) const;
   // single-launch BN backward (reduce + finalize + apply) for the top block when it has at most
   // bn_fused_rows_ rows (B*H*W)
   bool bn_fused(int l, int64_t B) const;
-  void conv_dual(int l, int B, hipStream_t s, float* dz, const CsBnRed* ered = nullptr, const CsBnFin* fin = nullptr);
   // Block l-1's BN-backward partial sums are computed where block l's data gradient is finished
-  // (the dgrad GEMM's epilogue, or its split-K combine: CsConvArgs::ered), and finalized by that
-  // launch's last-arriving block (fin): the BN backward of block l-1 is then the apply pass alone.
+  // (the dgrad GEMM's epilogue, or its split-K combine: CsConvArgs::ered): the BN backward of
+  // block l-1 is then finalize + apply.
   CsBnRed ered_args(int l, int B);
-  CsBnFin fin_fwd_args(int l, int B);
-  CsBnFin fin_bwd_args(int l, int B);  // block l-1's finalize, carried by block l's data gradient
-  int red_pending_ = -1;  // block whose BN-backward partials (fin: coefficients) are already in place
+  int red_pending_ = -1;  // block whose BN-backward partials are already in place
   int red_P_ = 0;         // ... as red_P_ row-tile partials (bn_part_; the separate finalize reads them)
   // ---- side-stream weight gradients (overlap_): kernel stream links (device_comm.h) main -> side
   // "dz(l) ready" and side -> main "weight gradients done", one dz buffer per block (the side
@@ -247,26 +221,38 @@ class VggEngine {
   torch::Tensor perm_, cursor_;
   int64_t perm_len_ = 0;
   // gbuf_: gradient ping-pong; ws_ / ws_w_: split-K slabs of the data / weight gradient (distinct:
-  // a dual launch runs both); bn_part_: BN-backward partials; fin_cnt_ / fin_grp_: bn_fin.h state
-  torch::Tensor gbuf_[2], dz_[2], ws_, ws_w_, bn_part_, bn_coef_, bn_eval_, head_ws_, fin_cnt_, fin_grp_;
+  // the side stream's weight gradient runs beside the next data gradient); bn_part_: BN-backward partials
+  torch::Tensor gbuf_[2], dz_[2], ws_, ws_w_, bn_part_, bn_coef_, bn_eval_, head_ws_;
+  // F3 operand bounds, CS_AMAX_SHARDS floats per slot: x of block l (slot l), dz of block l (L + l),
+  // weights of block l (2L + l)
+  torch::Tensor amax_;
+  bool f3_probe_ = false;
+  float* amax_x(int l) { return amax_.data_ptr<float>() + (int64_t)l * CS_AMAX_SHARDS; }
+  float* amax_dz(int l) { return amax_.data_ptr<float>() + (int64_t)(blocks_.size() + l) * CS_AMAX_SHARDS; }
+  // the weights' bound is a running maximum folded in by every SGD launch that rewrites them, kept
+  // per SGD range (a block at world 1, a bucket at world > 1, the whole buffer for sgd()): wslot_[l]
+  // is the slot of the range that last updated block l (an upper bound of its weights)
+  std::vector<int> wslot_;
+  float* amax_slot(int slot) { return amax_.data_ptr<float>() + (int64_t)(2 * blocks_.size() + slot) * CS_AMAX_SHARDS; }
+  float* amax_w(int l) { return amax_slot(wslot_[l]); }
+  bool f3_used_ = false;  // some conv tile runs the F3 math: the producers publish the bounds
+  bool w_dirty_ = true;   // the weights changed outside an SGD launch: re-measure their bounds
+  float* x_amax_out(int l) { return f3_used_ && !f3_probe_ ? amax_x(l) : nullptr; }
+  float* dz_amax_out(int l) { return f3_used_ && !f3_probe_ ? amax_dz(l) : nullptr; }
+  void f3_refresh(hipStream_t s);  // the step's / eval's entry: weight bounds if dirty, x / dz bounds zeroed
+  float* sgd_amax(int64_t off, int64_t n);  // the slot an SGD launch over [off, off + n) folds into
   int64_t ws_elems_ = 0;
-  bool fin_on_ = true;
-  bool dual_ = true;
   int math_ = 2;  // conv autotune candidates: 0 f32 MFMA, 1 split-bf16 X6, 2 both (CS_CONV_MATH)
-  // CS_BN_FUSED_ROWS; 0 disables. Measured on MI355X at B=64 (img/s): 0 -> 71.46k, 256 (blocks 6-7)
+  // 0 disables (CS_ENGINE_OFF=bn_fused). Measured on MI355X at B=64 (img/s): 0 -> 71.46k, 256 (blocks 6-7)
   // -> 71.64k, 1024 -> 69.85k, 4096 -> 63.07k: one block per 16 channels serialises too many rows
   int64_t bn_fused_rows_ = 256;
   bool sgd_tail_on_ = true;
   bool sgd_tail_ = false;  // set by step() for the step in flight (world 1)
   bool sgd_first_ = false;
   int debug_skip_ = 0;
-  // staggered side-stream fork (backward): block l's weight gradient forks when block l-1's data
-  // gradient starts instead of right after its own data gradient (CS_WGRAD_STAGGER)
-  bool stagger_ = false;
-  int side_pending_ = -1;                      // block whose weight-gradient fork is held back
-  unsigned long long* start_sig_ = nullptr;    // deferred signal the next conv launch carries
-  void fork_wgrad(int l, int64_t B, bool current);
-  int lag_blocks_ = 0;
+  // block l's weight gradient (+ the previous fork's SGD as tail workgroups) on the side stream,
+  // behind the deferred signal the next main-stream launch carries
+  void fork_wgrad(int l, int64_t B);
   bool conv0_direct_ = true;
   bool conv0_direct_ok(int64_t B) const;
   // with_sgd: block 0's SGD step (+ the batch cursor) rides the weight gradient's final sum when the
@@ -280,22 +266,12 @@ class VggEngine {
   bool conv0_batch_fold_ = true;
   bool head_bn_fold_ = true;
   bool side_sgd_tail_ = true;
-  bool side_join_once_ = false;
-  bool side_dirty_ = false;  // side-stream work since the last join signal (side_join_once_)
-  bool head_tail_ = false;  // measured neutral (profiles/r5_ab_head_tail.txt): opt-in
-  CsHeadCols head_next_{};  // P > 0: the column pass waiting for the top block's weight-gradient launch
   int side_sgd_pending_ = -1;  // block whose side-stream SGD has not been enqueued yet
   void flush_side_sgd();
-  hipStream_t lag_ = nullptr;
-  std::unique_ptr<StreamLink> lag_in_, lag_out_;  // main -> lag (step end), lag -> main (deferred work done)
-  std::vector<int> lag_list_;                      // blocks whose weight gradient this step defers
   std::vector<int64_t> comm_defer_;
   DeviceComm* defer_comm_ = nullptr;  // deferred buckets enqueued on this communicator, not waited for
   int defer_block_ = -1;              // the next forward waits before this block's conv
   void join_deferred(hipStream_t s);
-  bool lag_pending_ = false;                       // deferred work enqueued, not yet waited for
-  bool lag_on(hipStream_t s) const;
-  int fwd_fused_t_ = 0, bwd_fused_p_ = 0;
   double hp_[4] = {0, 0, 0, 0};  // lr, momentum, wd, dampening of the step in flight
   std::vector<std::pair<int64_t, int64_t>> blk_range_;  // block l's [off, off + n) (block L-1 from 0: fc)
   CsSgdTail sgd_tail_args(int64_t block);

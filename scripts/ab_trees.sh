@@ -2,7 +2,7 @@
 # Same-box A/B of source trees (each with its own built _C.so), interleaved:
 #   bash scripts/ab_trees.sh ROUNDS TREE[:VAR=VAL[,VAR=VAL]]... [-- bench.py args]
 # e.g. TREE = .ab/r2 (a `git worktree add .ab/r2 <commit>` built in place), . (the working tree), or
-# .:CS_BN_FIN=0 (the working tree with an environment override). One bench.py process per run,
+# .:CS_ENGINE_OFF=side_sgd_tail (the working tree with an environment override). One bench.py process per run,
 # the variants alternating ROUNDS times, so clock and thermal drift on the box hit every variant
 # alike. Prints one line per run and a median per variant.
 set -o pipefail

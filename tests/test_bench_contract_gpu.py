@@ -59,3 +59,45 @@ def test_bench_two_ranks_staged_json_line():
     bw = d["busbw_GBps"]
     assert bw and all(v > 0 for v in bw.values()), bw
     assert "9.00MiB" in bw or any(k.endswith("MiB") for k in bw)
+
+
+def test_bench_one_rank_rccl_probe_fields():
+    """World 1 with a one-rank native RCCL communicator (--comm-probe 1): the data-parallel step's
+    collectives run on the real RcclComm, and the JSON names the RCCL runtime actually loaded next
+    to the header the communicator was built against, and its CTA budget."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    r = subprocess.run([sys.executable, "bench.py", "--steps", "4", "--warmup", "2", "--comm-probe", "1"], cwd=ROOT,
+                       capture_output=True, text=True, timeout=240, env=dict(os.environ, CS744_BENCH_CALIBRATE="0"))
+    assert r.returncode == 0, r.stderr[-1500:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    c = d["config"]
+    assert c["comm"] == "probe:1" and d["comm_fallback"] is False
+    v = c["rccl_version"]
+    assert v["runtime"] >= 21700 and v["header"] >= 21700 and v["runtime"] // 10000 == v["header"] // 10000 == 2, v
+    assert c["comm_ctas"] is not None
+
+
+def test_bench_two_ranks_rccl_gloo_control_plane_fallback():
+    """`--comm rccl` at N = 2 exactly as the driver launches it, on the 1-GPU box: the control plane
+    is a gloo process group (no ProcessGroupNCCL next to the native communicator), both ranks build
+    the native RcclComm on the same device, RCCL refuses the duplicate GPU on every rank, the agreed
+    fallback takes both ranks to the staged communicator (the same C++ step over the gloo group), and
+    the line says so at the top level."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from conftest import torchrun_cmd
+    cmd = torchrun_cmd(2) + ["bench.py", "--gpus", "2", "--comm", "rccl", "--steps", "3", "--warmup", "2",
+                             "--busbw-iters", "0"]
+    # both ranks on cuda:0 (LOCAL_RANK 1 has no device of its own here)
+    env = dict(os.environ, CS744_BENCH_CALIBRATE="0", HIP_VISIBLE_DEVICES="0")
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    c = d["config"]
+    assert c["control_plane"] == "gloo" and c["parallelism"] == "dp2"
+    assert "runtime" in c["rccl_version"]
+    if c["comm"] == "rccl":  # a stack that lets two ranks share a device
+        assert d["comm_fallback"] is False
+    else:
+        assert d["comm_fallback"] is True and c["comm"] == "staged", c

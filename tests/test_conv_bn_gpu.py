@@ -35,6 +35,8 @@ TILES = [(64, 64, 1, 16), (128, 64, 1, 16), (64, 128, 3, 16), (128, 128, 2, 16),
 VARIANTS = [0, 1, 2, 3, 4, 8, 9, 10, 11, 12, 16, 19, 20]
 # +32 = bf16 operands, f32 accumulation (the engine's opt-in bf16 mode): bf16-level tolerance
 VARIANTS += [32, 35, 36]
+# +64 = F3: two fp16 planes of the power-of-two-scaled operand, 3 f16 MFMAs: held to the f64 tolerance
+VARIANTS += [64, 67, 68]
 
 
 def _tol(stage, f32=2e-5):
@@ -45,8 +47,14 @@ def _stage_ok(stage, bm, bn, bk, conv0_fwd=False):
     """Python mirror of cs_conv_stage_ok (conv_gemm.hip) — used at collection time so the test
     matrix holds only combinations that have a kernel (a skip then always means a gap);
     test_stage_table_mirrors_kernel checks the mirror against the C++ function."""
-    if sum(bool(stage & m) for m in (8, 16, 32)) > 1:
+    if sum(bool(stage & m) for m in (8, 16, 32, 64)) > 1:
         return False
+    if stage & 64:
+        stage &= ~64
+        if conv0_fwd or stage not in (0, 3, 4):
+            return False
+        if bk == 64 and bm == 128 and bn == 128:
+            return False
     if stage & 32:
         stage &= ~32
         if conv0_fwd or stage not in (0, 3, 4):
@@ -90,7 +98,7 @@ def _skip_stage(stage, bk, bm, bn, conv0_fwd=False):
 def test_stage_table_mirrors_kernel(dev):
     from cs744_pytorch_distributed_tutorial_amd.ops import native
     C = native.C()
-    for st in range(64):
+    for st in range(128):
         for bm in (64, 128):
             for bn in (64, 128):
                 for bk in (16, 32, 64):

@@ -141,7 +141,7 @@ def test_sync_modes_agree(gpu):
         torch.testing.assert_close(out[0]["params"], ref, rtol=1e-5, atol=1e-6, msg=mode)
 
 
-def _probe_run(probe, steps=6, skip=0, spin_us=40.0, defer=None):
+def _probe_run(probe, steps=6, skip=0, spin_us=40.0, defer=None, graph="none"):
     from cs744_pytorch_distributed_tutorial_amd.runtime.engine import NativeTrainer
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -149,7 +149,7 @@ def _probe_run(probe, steps=6, skip=0, spin_us=40.0, defer=None):
     if defer is not None:
         os.environ["CS_COMM_DEFER"] = defer
     try:
-        tr = NativeTrainer(batch_size=32, device=dev, bucket_mb=1.0, graph="none", train_size=512, test_size=32,
+        tr = NativeTrainer(batch_size=32, device=dev, bucket_mb=1.0, graph=graph, train_size=512, test_size=32,
                            autotune=False, probe=probe, probe_spin_us=spin_us)
     finally:
         if old is None:
@@ -202,6 +202,18 @@ def test_probe_comm_deferred_buckets_bitwise(gpu, probe, defer):
     assert calls > 6
     for k in base:
         assert torch.equal(base[k], probed[k]), (probe, defer, k)
+
+
+def test_full_graph_after_deferred_eager_steps_bitwise(gpu):
+    """graph='full' with a communicator and deferred buckets: steps 0-1 run eagerly and step 1 leaves
+    a deferred all-reduce + SGD on the comm stream; the capture at step 2 must wait for it first
+    (NativeTrainer._capture -> join_lag; VggEngine::step refuses a pending deferral inside a
+    capture). Bitwise equal to the world-1 run over the one-rank RCCL communicator."""
+    base, _ = _probe_run("0")
+    graphed, calls = _probe_run("1", defer="-2", graph="full")
+    assert calls > 6
+    for k in base:
+        assert torch.equal(base[k], graphed[k]), k
 
 
 def test_probe_comm_deferred_buckets_negative_control(gpu):

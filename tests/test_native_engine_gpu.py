@@ -176,30 +176,6 @@ def test_rccl_comm_world1_and_graph_capture(dev):
     assert c.native.async_error() == ""
 
 
-@pytest.mark.parametrize("stage,bkw,bkd", [(0, 32, 16), (16 | 4, 64, 64), (16 | 3, 64, 64), (16, 16, 16)])
-def test_dual_backward_launch_is_bitwise_equal(dev, stage, bkw, bkd):
-    # wgrad + dgrad horizontally fused into one launch (and one split-K combine) computes every
-    # tile with the same K-split and summation order as two launches: bit-equal training
-    # (f32 register staging, and the X6S split-bf16 K-group / register variants)
-    a = _trainer(dev, batch_size=32, train_size=256)
-    b = _trainer(dev, batch_size=32, train_size=256)
-    a.engine.set_dual(False)
-    b.engine.set_dual(True)
-    for l in range(a.layout.L):  # force split-K on both GEMMs so the dual combine path runs
-        for m in (1, 2):
-            if l == 0 and m == 1:
-                continue
-            for t in (a, b):
-                t.engine.set_tile(l, m, 64, 64, 4, bkw if m == 2 else bkd, stage)
-        if l > 0:
-            b.engine.set_block_dual(l, True)
-    for _ in range(3):
-        a.step()
-        b.step()
-    torch.cuda.synchronize()
-    assert torch.equal(a.params, b.params) and torch.equal(a.mom, b.mom)
-
-
 def test_debug_sync_mode_runs(dev):
     # CS_DEBUG_SYNC=1 (read once per process): every engine launch is followed by a stream sync +
     # error check outside graph capture; run it in a child process
@@ -283,9 +259,9 @@ def test_bf16_mode_tracks_fp32(dev):
 
 
 def _set_tiles(t, tiles):
-    """Tile tables exercising every in-launch finalize / apply site: split-K fwd / dgrad (statistics,
-    partials and apply in the combine), epilogue partials with 64x64 / 128x64 / 64x128 tiles at 256 /
-    1024 threads, and one wgrad + dgrad launch."""
+    """Tile tables exercising every BN statistics / partials site: split-K fwd / dgrad (statistics
+    and partials in the combine), epilogue partials with 64x64 / 128x64 / 64x128 tiles at 256 /
+    1024 threads."""
     if tiles in ("shipped", "default"):
         return
     for l in range(t.layout.L):
@@ -297,40 +273,6 @@ def _set_tiles(t, tiles):
             t.engine.set_tile(l, 0, 64, 128 if l % 2 else 64, 1, 32, 0)
             if l > 0:
                 t.engine.set_tile(l, 1, 64 if l % 2 else 128, 64, 1, 64 if l % 2 else 32, (16 | 4) if l % 2 else 0)
-        elif l > 0:  # one wgrad + dgrad launch, split-K on every other dgrad
-            t.engine.set_tile(l, 1, 64, 64, 1 + (l % 2), 16, 0)
-            t.engine.set_tile(l, 2, 64, 64, 2, 16, 0)
-            t.engine.set_block_dual(l, True)
-
-
-@pytest.mark.parametrize("tiles", ["shipped", "split", "nosplit", "dual"])
-def test_in_launch_bn_finalize_matches_finalize_launches(dev, tiles):
-    """Every BatchNorm finalize as the last-arriving block of the launch that produced its partial
-    sums (bn_fin.h: forward in the conv epilogue / split-K combine, backward in the data
-    gradient's epilogue / combine; set_fin(True), opt-in) vs the separate bn_finalize (default) /
-    bn_bwd_finalize launches: same partials, a different fixed combine order -> a norm bound after
-    two steps at B=64 and identical num_batches_tracked; run to run bitwise (the combine order
-    does not depend on which block arrives last)."""
-    out = []
-    for fin in (False, True, True):
-        t = _trainer(dev, batch_size=64, train_size=256, autotune=tiles == "shipped")
-        t.engine.set_fin(fin)
-        _set_tiles(t, tiles)
-        for _ in range(2):
-            t.step()
-        torch.cuda.synchronize()
-        out.append((t.params.clone(), t.mom.clone(), t.bufs.clone(), t.nbt.clone(), t.last_loss()))
-    a, b, c = out
-    assert abs(a[4] - b[4]) < 1e-4 * max(1.0, abs(a[4]))
-    # (a reordered fp32 combine: after two SGD steps the BN backward has amplified it to 1e-3 -
-    # 8.5e-3 of the momentum (measured: the dual-launch tiles are the most sensitive); the absolute
-    # accuracy of both orders is checked against fp64 in test_bench_config_b64_matches_fp64)
-    for name, x, y in zip(("params", "mom", "bufs"), a[:3], b[:3]):
-        d = (y.double() - x.double()).norm() / x.double().norm()
-        assert d.item() < 1e-2, (name, d.item())
-    assert torch.equal(a[3], b[3])
-    for x, y in zip(b[:4], c[:4]):
-        assert torch.equal(x, y)
 
 
 @pytest.mark.parametrize("tiles", ["shipped", "default"])
@@ -441,21 +383,17 @@ def _force_x6s(tr):
     return n
 
 
-@pytest.mark.parametrize("variant", ["autotuned", "x6s_everywhere", "f32_only", "split", "nosplit", "dual", "in_launch",
-                                     "bn_fused"])
+@pytest.mark.parametrize("variant", ["autotuned", "x6s_everywhere", "f32_only", "split", "nosplit", "bn_fused"])
 def test_bench_config_b64_matches_fp64(dev, variant):
     """The benchmarked configuration (B=64; tuned tiles = 22 of 23 GEMMs on X6S split-bf16
-    maths), every X6S GEMM, f32-MFMA-only tiles, the tile tables that put split-K combines,
-    64x128 / 128x64 epilogues and dual launches at every site, and the opt-in in-launch BN finalize
-    (CS_BN_FIN=1, bn_fin.h) vs the decision-aligned fp64 model: every gradient tensor within 1e-4
-    relative (max-abs normalised)."""
-    tr = _trainer(dev, batch_size=64, train_size=1024, autotune=variant in ("autotuned", "in_launch", "bn_fused"))
-    if variant in ("split", "nosplit", "dual"):
+    maths), every X6S GEMM, f32-MFMA-only tiles, the tile tables that put split-K combines and
+    64x128 / 128x64 epilogues at every site, and the single-launch BN backward at every layer vs the
+    decision-aligned fp64 model: every gradient tensor within 1e-4 relative (max-abs normalised)."""
+    tr = _trainer(dev, batch_size=64, train_size=1024, autotune=variant in ("autotuned", "bn_fused"))
+    if variant in ("split", "nosplit"):
         _set_tiles(tr, variant)
-    if variant == "in_launch":
-        tr.engine.set_fin(True)
-    if variant == "bn_fused":  # single-launch BN at every layer, forward and backward
-        tr.engine.set_bn_fused_limits(1 << 30, 1 << 30)
+    if variant == "bn_fused":  # single-launch BN backward (reduce + finalize + apply) at every layer
+        tr.engine.set_bn_fused_rows(1 << 30)
     if variant == "x6s_everywhere":
         tr.engine.set_conv0_direct(False)  # block 0's weight gradient on its X6S GEMM tile too
         assert _force_x6s(tr) == 22
@@ -484,12 +422,9 @@ def test_side_stream_wgrad_bitwise_and_graph(dev):
     each weight gradient) compute exactly what the serial backward does (SGD in the weight-gradient
     tails); a full-step graph (captured: serial) replays the same bits."""
     runs = []
-    for ovl, graph, stagger, lag in ((False, "none", False, 0), (True, "none", False, 0), (True, "full", False, 0),
-                                     (True, "none", True, 0), (True, "none", False, 3), (True, "none", True, 2)):
+    for ovl, graph in ((False, "none"), (True, "none"), (True, "full")):
         t = _trainer(dev, batch_size=32, train_size=256, graph=graph)
         t.engine.set_overlap(ovl)
-        t.engine.set_stagger(stagger)  # block l's weight gradient forks at block l-1's data gradient
-        t.engine.set_lag(lag)  # the top `lag` blocks' weight gradients + SGD run into the next forward
         for _ in range(5):
             t.step()
         torch.cuda.synchronize()
@@ -503,14 +438,11 @@ def test_side_stream_wgrad_bitwise_and_graph(dev):
 
 def test_long_run_no_syncs_deterministic(dev):
     """30 back-to-back steps (the host far ahead of the GPU, an epoch boundary crossed): side-stream
-    weight gradients == the serial backward, bit for bit, run to run (the in-launch finalizes'
-    arrival order changes, their combine order does not; the tickets stay zeroed)."""
+    weight gradients == the serial backward, bit for bit, run to run."""
     out = []
-    for ovl, stagger, lag in ((False, False, 0), (True, False, 0), (True, False, 0), (True, True, 0), (True, False, 3)):
+    for ovl in (False, True, True):
         t = _trainer(dev, batch_size=32, train_size=640)
         t.engine.set_overlap(ovl)
-        t.engine.set_stagger(stagger)
-        t.engine.set_lag(lag)
         for _ in range(30):
             t.step()
         torch.cuda.synchronize()
