@@ -105,6 +105,7 @@ def conv_wgrad(dz: torch.Tensor, x: torch.Tensor, cout: int, *, w_oihw: bool = F
 
 
 STAGE_F3 = 64  # launchers.h CS_STAGE_F3
+AMAX_SLOT = 64 * 32  # launchers.h CS_AMAX_SLOT
 
 
 def _f3_amax(stage: int, a: torch.Tensor, b: torch.Tensor) -> dict:
@@ -112,9 +113,9 @@ def _f3_amax(stage: int, a: torch.Tensor, b: torch.Tensor) -> dict:
     (the engine has them from the operands' producers; here torch computes them)."""
     if not stage & STAGE_F3:
         return {}
-    # CS_AMAX_SHARDS (8) floats each: the kernel takes the largest
-    return dict(amax_a=a.detach().abs().max().reshape(1).float().repeat(8),
-                amax_b=b.detach().abs().max().reshape(1).float().repeat(8))
+    # one slot of CS_AMAX_SLOT (64 shards x 32) floats each: the kernel takes the largest shard
+    return dict(amax_a=a.detach().abs().max().reshape(1).float().repeat(AMAX_SLOT),
+                amax_b=b.detach().abs().max().reshape(1).float().repeat(AMAX_SLOT))
 
 
 class BNState:

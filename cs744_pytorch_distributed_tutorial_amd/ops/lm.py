@@ -149,6 +149,12 @@ def gemm_operands_ok(a: torch.Tensor, b: torch.Tensor) -> bool:
         return False
     if (lda < K if a_kmajor else lda < M) or (ldb < K if b_kmajor else ldb < N):
         return False
+    # 32-bit buffer offsets: a K-major operand addresses 256 rows (kTile), an M-major one 64 k rows
+    # (kBK) per tile; and the tile count fits an int (cs_gemm_bf16's own checks, mirrored)
+    if (256 if a_kmajor else 64) * lda * 2 >= 0x7fffffff or (256 if b_kmajor else 64) * ldb * 2 >= 0x7fffffff:
+        return False
+    if ((M + 255) // 256) * ((N + 255) // 256) > 0x7fffffff:
+        return False
     return (a.data_ptr() | b.data_ptr()) % 16 == 0
 
 

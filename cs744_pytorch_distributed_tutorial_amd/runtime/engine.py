@@ -177,7 +177,7 @@ class FlatLayout:
 _STAGE_NAMES = {0: "regs", 1: "lds_dma", 2: "lds_dma_deep", 3: "kgroups2", 4: "kgroups4"}
 # conv tile tables tuned on MI355X, keyed "<model>[/bf16]/B<batch>/gfx950/<version>"; bump the
 # version whenever the conv kernel variants change (stale entries then fall back to an autotune)
-TILE_TABLE_VERSION = "v2"
+TILE_TABLE_VERSION = "v3"
 SHIPPED_TILES = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tiles_gfx950.json")
 
 
@@ -437,7 +437,8 @@ class NativeTrainer:
                     continue
                 out.append({"block": l, "op": names[m], "bm": bm, "bn": bn, "bk": bk, "splits": sp,
                             "stage": _STAGE_NAMES.get(st & 7, str(st & 7)),
-                            "math": "bf16" if st & 32 else ("x6s" if st & 16 else ("x6" if st & 8 else "f32")),
+                            "math": "f3" if st & 64 else ("bf16" if st & 32 else ("x6s" if st & 16 else
+                                                                                    ("x6" if st & 8 else "f32"))),
                             "us": us})
         return out
 

@@ -87,8 +87,8 @@ int64_t conv_gemm(int64_t mode, c10::optional<torch::Tensor> x, c10::optional<to
   DevGuard g(out.device());
   a.x = cptr(x); a.w = cptr(w); a.dz = cptr(dz); a.bias = cptr(bias);
   a.out = out.data_ptr<float>(); a.ws = mptr(ws); a.stats = mptr(stats);
-  // CS_STAGE_F3: GPU tensors of CS_AMAX_SHARDS floats whose maximum bounds |A| / |B| (the scales' source)
-  check_t(amax_a, CS_AMAX_SHARDS, "amax_a"); check_t(amax_b, CS_AMAX_SHARDS, "amax_b");
+  // CS_STAGE_F3: GPU tensors of CS_AMAX_SLOT floats whose shards bound |A| / |B| (the scales' source)
+  check_t(amax_a, CS_AMAX_SLOT, "amax_a"); check_t(amax_b, CS_AMAX_SLOT, "amax_b");
   a.amax_a = cptr(amax_a); a.amax_b = cptr(amax_b);
   TORCH_CHECK(!(stage & CS_STAGE_F3) || (a.amax_a != nullptr && a.amax_b != nullptr),
               "conv_gemm: the F3 stage needs amax_a and amax_b");

@@ -104,6 +104,31 @@ void register_runtime(pybind11::module& m) {
   m.def("link_timeout", &cs::link_timeout);
   m.def("abort_links", &cs::abort_links, "release every waiting stream-link kernel with an error (watchdog path)");
   m.def("reset_link_abort", &cs::reset_link_abort);
+  // diagnostic shader-clock sampler (clock_probe.hip, scripts/ramp_clock.py)
+  m.def(
+      "clock_sampler",
+      [](torch::Tensor out, torch::Tensor stop, intptr_t stream) {
+        check_gpu(out, "out");
+        check_gpu(stop, "stop");
+        TORCH_CHECK(out.scalar_type() == at::kLong && stop.scalar_type() == at::kInt && stop.numel() >= 1,
+                    "clock_sampler: int64 out, int32 stop");
+        const int64_t n = out.numel() / 2 - 1;
+        TORCH_CHECK(n >= 1 && n < (1 << 30), "clock_sampler: out must hold >= 2 pairs");
+        TORCH_CHECK(stream != 0, "clock_sampler: give it a stream of its own");
+        CS_LAUNCH(cs_clock_sampler(reinterpret_cast<unsigned long long*>(out.data_ptr()), static_cast<int>(n),
+                                       stop.data_ptr<int>(), reinterpret_cast<hipStream_t>(stream)));
+      },
+      "start the sampler on `stream`: (s_memrealtime, s_memtime) pairs into out until stop is set");
+  m.def("clock_stamp", [](torch::Tensor slots, int i) {
+    check_gpu(slots, "slots");
+    TORCH_CHECK(slots.scalar_type() == at::kLong && i >= 0 && i < slots.numel(), "clock_stamp: index out of range");
+    CS_LAUNCH(cs_clock_stamp(reinterpret_cast<unsigned long long*>(slots.data_ptr()), i, cur_stream()));
+  });
+  m.def("clock_stop", [](torch::Tensor stop) {
+    check_gpu(stop, "stop");
+    TORCH_CHECK(stop.scalar_type() == at::kInt, "clock_stop: int32 stop");
+    CS_LAUNCH(cs_clock_stop(stop.data_ptr<int>(), cur_stream()));
+  });
   py::class_<cs::StagedComm, cs::DeviceComm>(m, "StagedComm")
       .def(py::init<const std::string&, int>(), py::arg("group_name"), py::arg("device"));
   py::class_<cs::ProbeComm, cs::DeviceComm>(m, "ProbeComm")

@@ -200,7 +200,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__
   }
   if (live) reinterpret_cast<float4*>(out)[t] = r;
   // the output bound the next conv's F3 math scales by (ReLU output: non-negative)
-  if (amax != nullptr) cs::wave_amax_publish(live ? fmaxf(fmaxf(r.x, r.y), fmaxf(r.z, r.w)) : 0.f, amax);
+  if (amax != nullptr) cs::block_amax_publish(live ? fmaxf(fmaxf(r.x, r.y), fmaxf(r.z, r.w)) : 0.f, amax);
 }
 
 template <bool APPLY, bool POOL>
@@ -232,7 +232,7 @@ __global__ __launch_bounds__(256) void bn_bwd_kernel(const float* __restrict__ y
                              APPLY && amax != nullptr ? &vm : nullptr);
   }
   if (APPLY) {
-    if (amax != nullptr) cs::wave_amax_publish(vm, amax);  // the dZ bound (F3 conv math)
+    if (amax != nullptr) cs::block_amax_publish(vm, amax);  // the dZ bound (F3 conv math)
     return;
   }
   if (rl < rows) {
@@ -531,7 +531,7 @@ __global__ __launch_bounds__(256) void bn_fused_bwd_kernel(const float* __restri
   for (int u = rl; u < units; u += 64)
     bwd_visit<true, POOL>(y, G, B, H, W, C, cqg, u, scale, shift, mean, invstd, coef_sh, dz, dummy, c0,
                           amax != nullptr ? &vm : nullptr);
-  if (amax != nullptr) cs::wave_amax_publish(vm, amax);  // the dZ bound (F3 conv math)
+  if (amax != nullptr) cs::block_amax_publish(vm, amax);  // the dZ bound (F3 conv math)
 }
 
 // grid (C/16, row chunks): finalize the BN backward of this block's 16 channels from the P

@@ -50,12 +50,38 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
   return red[0];
 }
 
-// The F3 conv math's operand bounds (launchers.h CS_AMAX_SHARDS): every wave of a producer folds
-// |its values| into one atomic max on shard blockIdx % 8 (the float bits of a non-negative value
-// order like unsigned ints; a NaN, above +inf, wins). All 64 lanes must be active.
-__device__ __forceinline__ void wave_amax_publish(float v, float* amax) {
+// The F3 conv math's operand bounds (launchers.h CS_AMAX_*): a producer workgroup folds |its values|
+// into ONE atomic max on shard blockIdx % 64 (the float bits of a non-negative value order like
+// unsigned ints; a NaN, above +inf, wins). Every thread of the block calls it (a barrier inside).
+__device__ __forceinline__ void block_amax_publish(float v, float* amax) {
+  __shared__ float red[16];
   v = wave_max(v);
-  if ((threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<unsigned*>(amax) + (blockIdx.x & 7), __float_as_uint(v));
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < nw; ++w) v = fmaxf(v, red[w]);
+    atomicMax(reinterpret_cast<unsigned*>(amax) + (blockIdx.x & 63) * 32, __float_as_uint(v));
+  }
+}
+
+// Several bounds at once (the SGD's per-block weight bounds): v[k] folded into amax[k] (k < n,
+// n <= 16; null amax[k] skipped). Every thread of the block calls it (a barrier inside).
+__device__ __forceinline__ void block_amax_publish_n(const float (&v)[16], float* const (&amax)[16], int n) {
+  __shared__ float red[16][16];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    if (k >= n) break;
+    const float w = wave_max(v[k]);
+    if (lane == 0) red[wid][k] = w;
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < n && amax[threadIdx.x] != nullptr) {
+    float m = 0.f;
+    for (int i = 0; i < nw; ++i) m = fmaxf(m, red[i][threadIdx.x]);
+    atomicMax(reinterpret_cast<unsigned*>(amax[threadIdx.x]) + (blockIdx.x & 63) * 32, __float_as_uint(m));
+  }
 }
 
 // XCD-aware bijective block remap (cdna_hip_programming.md §5, "XCD swizzle must be

@@ -91,7 +91,22 @@ __host__ __device__ constexpr int win_off(int k) { return (k / 9) * kPlane + ((k
 template <bool BATCH>
 __global__ __launch_bounds__(256) void conv0_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                         const float* __restrict__ bias, float* __restrict__ y,
-                                                        float* __restrict__ stats, int H, CsBatchSrc src) {
+                                                        float* __restrict__ stats, int H, CsBatchSrc src,
+                                                        float* __restrict__ zero_bounds, int zero_slots,
+                                                        float* __restrict__ rot_cur, float* __restrict__ rot_next,
+                                                        unsigned rot_mask) {
+  // the step's first launch also resets the F3 conv math's per-step operand bounds (one word per
+  // shard, launchers.h CS_AMAX_*), which this step's BN launches then fold into, and makes the
+  // weight bounds the last step's SGD launches produced current (cs_amax_rotate)
+  {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    const size_t o = (size_t)(i / CS_AMAX_SHARDS) * CS_AMAX_SLOT + (i % CS_AMAX_SHARDS) * CS_AMAX_STRIDE;
+    if (zero_bounds != nullptr && i < zero_slots * CS_AMAX_SHARDS) zero_bounds[o] = 0.f;
+    if (rot_cur != nullptr && i < 32 * CS_AMAX_SHARDS && ((rot_mask >> (i / CS_AMAX_SHARDS)) & 1u)) {
+      rot_cur[o] = rot_next[o];
+      rot_next[o] = 0.f;
+    }
+  }
   __shared__ float xs[3 * kPlane];
   __shared__ float red[4][kCo];
   __shared__ float mean_sh[kCo];
@@ -378,17 +393,21 @@ size_t cs_conv0_wgrad_part_floats(int B, int H, int W) {
 }
 
 hipError_t cs_conv0_fwd(const float* x, const float* w, const float* bias, float* y, float* stats, int B, int H,
-                        int W, int Cout, hipStream_t stream, const CsBatchSrc* batch) {
+                        int W, int Cout, hipStream_t stream, const CsBatchSrc* batch, float* zero_bounds,
+                        int zero_slots, float* rot_cur, float* rot_next, unsigned rot_mask) {
   if (W != 32 || Cout != kCo || (H * W) % kPix != 0) return hipErrorInvalidValue;
+  if ((zero_bounds != nullptr && (int64_t)zero_slots * CS_AMAX_SHARDS > (int64_t)(B * H * W) / kPix * 256) ||
+      (rot_cur != nullptr && 32 * CS_AMAX_SHARDS > (int64_t)(B * H * W) / kPix * 256))
+    return hipErrorInvalidValue;
   if (batch != nullptr) {
     if (H != 32 || (batch->perm == nullptr) == (batch->idx_in == nullptr) ||
         (batch->perm != nullptr && batch->cursor == nullptr))
       return hipErrorInvalidValue;
     hipLaunchKernelGGL(conv0_fwd_kernel<true>, dim3((B * H * W) / kPix), dim3(256), 0, stream, nullptr, w, bias, y,
-                       stats, H, *batch);
+                       stats, H, *batch, zero_bounds, zero_slots, rot_cur, rot_next, rot_mask);
   } else {
     hipLaunchKernelGGL(conv0_fwd_kernel<false>, dim3((B * H * W) / kPix), dim3(256), 0, stream, x, w, bias, y, stats,
-                       H, CsBatchSrc{});
+                       H, CsBatchSrc{}, zero_bounds, zero_slots, rot_cur, rot_next, rot_mask);
   }
   return hipGetLastError();
 }

@@ -480,15 +480,17 @@ __device__ __forceinline__ bf16x4 round4(const float4 v) {
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
-// 2^s for an operand whose absolute maximum is the largest of amax[0..CS_AMAX_SHARDS) (the
-// producers' per-XCD atomic-max shards): its largest element scales into [2^14, 2^15)
+// 2^s for an operand whose absolute maximum is the largest of its CS_AMAX_SHARDS shards (the
+// producers' atomic-max shards, launchers.h): its largest element scales into [2^14, 2^15). Lane i
+// of every wave reads shard i; the wave's max is every lane's (all 64 lanes active).
 __device__ __forceinline__ int f3_exp(const float* amax) {
   if (amax == nullptr) return 0;
-  unsigned bits = 0;
+  static_assert(CS_AMAX_SHARDS == 64, "one shard per lane");
+  unsigned bits = __builtin_bit_cast(unsigned, amax[(threadIdx.x & 63) * CS_AMAX_STRIDE]) & 0x7fffffffu;
 #pragma unroll
-  for (int i = 0; i < CS_AMAX_SHARDS; ++i) {  // as bit patterns: a NaN (above +inf) wins and gives s = 0
-    const unsigned u = __builtin_bit_cast(unsigned, amax[i]) & 0x7fffffffu;
-    bits = u > bits ? u : bits;
+  for (int off = 32; off > 0; off >>= 1) {  // as bit patterns: a NaN (above +inf) wins and gives s = 0
+    const unsigned o = (unsigned)__shfl_xor((int)bits, off, 64);
+    bits = o > bits ? o : bits;
   }
   const int e = (int)(bits >> 23);
   if (e == 0 || e == 255) return 0;  // zero / subnormal max, or inf / nan (propagates as is)

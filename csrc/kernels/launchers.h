@@ -23,10 +23,24 @@ hipError_t cs_make_batch(const uint8_t* data, const int64_t* labels, const int64
 
 // optimizer
 // counter (optional): incremented once by the launch (the engine's device-side step cursor)
-// the absolute maximum of x[0, n) folded (atomic max) into CS_AMAX_SHARDS floats
+// The F3 conv math's weight bounds, produced by the SGD launch that writes the weights: up to
+// CS_WB_MAX conv-weight intervals [lo, hi) (element offsets relative to the launch's range start),
+// each with the CS_AMAX_SLOT bound the absolute maximum of its updated elements is folded into. Each
+// element counts for the interval that holds it, so the bounds are exact per weight tensor whatever
+// the SGD launch's range (a block, a bucket, the whole buffer). n == 0: none.
+#define CS_WB_MAX 16
+struct CsWeightBounds {
+  int64_t lo[CS_WB_MAX], hi[CS_WB_MAX];
+  float* amax[CS_WB_MAX];
+  int n;
+};
+// the absolute maximum of x[0, n) folded (atomic max) into one CS_AMAX_SLOT bound
 hipError_t cs_amax(const float* x, int64_t n, float* amax, hipStream_t stream);
+// F3 weight bounds of the blocks in `mask`: cur = next, next = 0 (CS_AMAX_SLOT slots, block l at l)
+hipError_t cs_amax_rotate(float* cur, float* next, unsigned mask, int L, hipStream_t stream);
 hipError_t cs_sgd_flat(float* p, const float* g, float* m, int64_t n, float lr, float mom, float wd, float damp,
-                       float scale, int first, hipStream_t stream, int64_t* counter = nullptr, float* amax = nullptr);
+                       float scale, int first, hipStream_t stream, int64_t* counter = nullptr,
+                       const CsWeightBounds* wb = nullptr);
 // faithful sync modes on flat gradients (flat_ops.hip): dst = mean over `rows` rows of src [rows][n];
 // g = g + t, then / div when div > 0
 hipError_t cs_rows_mean(float* src, int rows, int64_t n, float* dst, int bcast, hipStream_t stream);
@@ -70,10 +84,13 @@ hipError_t cs_softmax_xent(const float* logits, const int64_t* labels, int B, in
 
 // ---------------------------------------------------------------- conv (implicit GEMM, fp32 MFMA)
 enum { CS_CONV_FWD = 0, CS_CONV_DGRAD = 1, CS_CONV_WGRAD = 2 };
-// operand absolute-maximum bounds (the F3 conv math's scales) are kept as this many shards, each the
-// atomic max of the workgroups with blockIdx % CS_AMAX_SHARDS == shard (one per XCD: no single hot
-// word); the bound is the largest shard
-#define CS_AMAX_SHARDS 8
+// operand absolute-maximum bounds (the F3 conv math's scales) are kept as CS_AMAX_SHARDS shards,
+// each the atomic max of the producer workgroups with blockIdx % CS_AMAX_SHARDS == shard (one atomic
+// per workgroup, shards CS_AMAX_STRIDE floats = one 128-byte line apart: no hot word or line), and
+// the bound is the largest shard; a slot is CS_AMAX_SLOT floats
+#define CS_AMAX_SHARDS 64
+#define CS_AMAX_STRIDE 32
+#define CS_AMAX_SLOT (CS_AMAX_SHARDS * CS_AMAX_STRIDE)
 
 // One BN-backward partial-sum pass (bn.hip "reduce"): y, incoming gradient G, the forward's
 // scale/shift/mean/invstd, partials out part [P][C][3]. P == 0: none.
@@ -92,9 +109,7 @@ struct CsSgdTail {
   int64_t n;
   float lr, mom, wd, damp;
   int first, P;
-  // optional: CS_AMAX_SHARDS floats the updated parameters' absolute maximum is folded into (a
-  // running bound of the weights for the F3 conv math)
-  float* amax;
+  CsWeightBounds wb;  // optional (wb.n == 0): the weights' bounds for the F3 conv math
 };
 
 // BatchNorm finalize by the last-arriving block of the launch that produces the statistics
@@ -138,7 +153,7 @@ struct CsConvArgs {
   // an independent SGD update appended to the launch (the serial world-1 step: block l+1's
   // parameters, whose last reader has run, ride block l's weight-gradient GEMM)
   CsSgdTail sgd;
-  // CS_STAGE_F3: device pointers to CS_AMAX_SHARDS floats whose maximum bounds |A| / |B| (the
+  // CS_STAGE_F3: device pointers to CS_AMAX_SLOT bounds (largest shard) of |A| / |B| (the
   // GEMM's A operand: FWD x, DGRAD / WGRAD dz; B: FWD / DGRAD w, WGRAD x); each sets its operand's
   // power-of-two scale
   const float* amax_a;
@@ -175,8 +190,12 @@ struct CsBatchSrc {
 };
 int cs_conv0_tile_rows();
 size_t cs_conv0_wgrad_part_floats(int B, int H, int W);
+// zero_bounds (optional): zero_slots F3 operand bounds (CS_AMAX_SLOT apart) this launch resets;
+// rot_cur / rot_next / rot_mask (optional): the weight-bound rotation of cs_amax_rotate, folded in
 hipError_t cs_conv0_fwd(const float* x, const float* w, const float* bias, float* y, float* stats, int B, int H,
-                        int W, int Cout, hipStream_t stream, const CsBatchSrc* batch = nullptr);
+                        int W, int Cout, hipStream_t stream, const CsBatchSrc* batch = nullptr,
+                        float* zero_bounds = nullptr, int zero_slots = 0, float* rot_cur = nullptr,
+                        float* rot_next = nullptr, unsigned rot_mask = 0);
 // sgd (optional): block 0's parameter range, whose SGD step then rides the fixed-order sum (dW at
 // w_rel within the range; the range's other gradients must be final; counter: the batch cursor)
 hipError_t cs_conv0_wgrad(const float* x, const float* dz, float* part, float* dw, int B, int H, int W, int Cout,
@@ -228,7 +247,7 @@ hipError_t cs_bn_finalize(const float* part, int T, int R, int M, int C, const f
                           float* scale, float* shift, float* save_mean, float* save_invstd, hipStream_t stream);
 hipError_t cs_bn_eval_coeffs(const float* gamma, const float* beta, const float* rm, const float* rv, int C, float eps,
                              float* scale, float* shift, hipStream_t stream);
-// amax (optional): CS_AMAX_SHARDS floats the output's absolute maximum is atomically folded into
+// amax (optional): a CS_AMAX_SLOT bound the output's absolute maximum is atomically folded into
 // (the F3 conv math's operand bound); the same for dz in the BN-backward launchers below
 hipError_t cs_bn_apply(const float* y, const float* scale, const float* shift, float* out, int B, int H, int W, int C,
                        int pool, hipStream_t stream, float* amax = nullptr);
@@ -294,6 +313,13 @@ hipError_t cs_comm_scramble(void* buf, int64_t n, int kind, int inverse, hipStre
 hipError_t cs_link_signal(unsigned long long* count, hipStream_t stream);
 hipError_t cs_link_wait(const unsigned long long* count, unsigned long long* expect, int* err, const int* abort,
                         double timeout_s, hipStream_t stream, unsigned long long delta = 1);
+
+// Diagnostic shader-clock sampler (clock_probe.hip; scripts/ramp_clock.py): out holds
+// max_samples + 1 pairs (s_memrealtime, s_memtime), 0-terminated when stopped early; stop and
+// slots: device memory, zeroed. Not used by the engine.
+hipError_t cs_clock_sampler(unsigned long long* out, int max_samples, int* stop, hipStream_t stream);
+hipError_t cs_clock_stamp(unsigned long long* slots, int i, hipStream_t stream);
+hipError_t cs_clock_stop(int* stop, hipStream_t stream);
 
 // ---------------------------------------------------------------- decoder-LM elementwise ops (lm.hip)
 enum { CS_F32 = 0, CS_BF16 = 1 };

@@ -26,9 +26,9 @@ __device__ __forceinline__ void sgd1(float& p, float g, float& m, const SgdArgs&
 
 __global__ __launch_bounds__(256) void sgd_flat_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                        float* __restrict__ m, int64_t n, SgdArgs a,
-                                                       int64_t* __restrict__ counter, float* __restrict__ amax) {
+                                                       int64_t* __restrict__ counter, CsWeightBounds wb) {
   if (counter != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *counter += 1;
-  float vm = 0.f;  // running bound of the updated parameters (F3 conv math), when amax is given
+  float vm[CS_WB_MAX] = {};  // the weight bounds (F3 conv math), wb.n > 0
   const int64_t n4 = n >> 2;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   float4* p4 = reinterpret_cast<float4*>(p);
@@ -43,23 +43,33 @@ __global__ __launch_bounds__(256) void sgd_flat_kernel(float* __restrict__ p, co
     sgd1(pv.w, gv.w, mv.w, a);
     p4[i] = pv;
     if (a.mom != 0.f) m4[i] = mv;
-    vm = fmaxf(vm, fmaxf(fmaxf(fabsf(pv.x), fabsf(pv.y)), fmaxf(fabsf(pv.z), fabsf(pv.w))));
+    if (wb.n > 0) cs_sgd::wb_fold(wb, i << 2, fmaxf(fmaxf(fabsf(pv.x), fabsf(pv.y)), fmaxf(fabsf(pv.z), fabsf(pv.w))), vm);
   }
   for (int64_t i = (n4 << 2) + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     float pv = p[i], mv = a.first ? 0.f : m[i];
     sgd1(pv, g[i], mv, a);
     p[i] = pv;
     if (a.mom != 0.f) m[i] = mv;
-    vm = fmaxf(vm, fabsf(pv));
+    if (wb.n > 0) cs_sgd::wb_fold(wb, i, fabsf(pv), vm);
   }
-  if (amax != nullptr) cs::wave_amax_publish(vm, amax);
+  if (wb.n > 0) cs::block_amax_publish_n(vm, wb.amax, wb.n);
+}
+
+__global__ __launch_bounds__(256) void amax_rotate_kernel(float* __restrict__ cur, float* __restrict__ next,
+                                                          unsigned mask, int L) {
+  const int i = blockIdx.x * 256 + threadIdx.x, l = i / CS_AMAX_SHARDS;
+  if (l < L && ((mask >> l) & 1u)) {
+    const size_t o = (size_t)l * CS_AMAX_SLOT + (i % CS_AMAX_SHARDS) * CS_AMAX_STRIDE;
+    cur[o] = next[o];
+    next[o] = 0.f;
+  }
 }
 
 __global__ __launch_bounds__(256) void amax_kernel(const float* __restrict__ x, int64_t n, float* __restrict__ amax) {
   float vm = 0.f;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) vm = fmaxf(vm, fabsf(x[i]));
-  cs::wave_amax_publish(vm, amax);
+  cs::block_amax_publish(vm, amax);
 }
 
 // Multi-tensor form: table of {p, g, m, n}; each block walks chunks of 4096 elements.
@@ -92,13 +102,21 @@ __global__ __launch_bounds__(256) void sgd_multi_kernel(const CsTensorEntry* __r
 }  // namespace
 
 hipError_t cs_sgd_flat(float* p, const float* g, float* m, int64_t n, float lr, float mom, float wd, float damp,
-                       float scale, int first, hipStream_t stream, int64_t* counter, float* amax) {
+                       float scale, int first, hipStream_t stream, int64_t* counter, const CsWeightBounds* wb) {
   if (n <= 0) return hipSuccess;
   SgdArgs a{lr, mom, wd, damp, scale, first};
   const int64_t work = (n + 3) / 4;
   int blocks = (int)((work + 255) / 256);
   if (blocks > 2048) blocks = 2048;
-  hipLaunchKernelGGL(sgd_flat_kernel, dim3(blocks), dim3(256), 0, stream, p, g, m, n, a, counter, amax);
+  hipLaunchKernelGGL(sgd_flat_kernel, dim3(blocks), dim3(256), 0, stream, p, g, m, n, a, counter,
+                     wb != nullptr ? *wb : CsWeightBounds{});
+  return hipGetLastError();
+}
+
+hipError_t cs_amax_rotate(float* cur, float* next, unsigned mask, int L, hipStream_t stream) {
+  if (mask == 0 || L <= 0) return hipSuccess;
+  hipLaunchKernelGGL(amax_rotate_kernel, dim3((L * CS_AMAX_SHARDS + 255) / 256), dim3(256), 0, stream, cur, next, mask,
+                     L);
   return hipGetLastError();
 }
 

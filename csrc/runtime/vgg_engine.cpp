@@ -1,6 +1,7 @@
 #include "runtime/vgg_engine.h"
 
 #include "runtime/markers.h"
+#include "runtime/vgg_engine_util.h"
 
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 
@@ -13,72 +14,7 @@
 
 namespace cs {
 
-namespace {
-
-const float kMean[3] = {125.3f / 255.f, 123.0f / 255.f, 113.9f / 255.f};  // master/part1/part1.py:66-67
-const float kStd[3] = {63.0f / 255.f, 62.1f / 255.f, 66.7f / 255.f};
-constexpr float kBnMomentum = 0.1f, kBnEps = 1e-5f;
-constexpr int64_t kWsElems = 16ll << 20;  // 64 MiB split-K workspace
-
-hipStream_t cur_stream() { return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
-
-// CS_DEBUG_SYNC=1: race/fault isolation mode — every launch is followed by a
-// stream sync + error check (skipped while a hipGraph is being captured), so an async fault
-// is reported at the kernel that caused it instead of at a later sync.
-bool debug_sync() {
-  static const bool on = [] {
-    const char* e = getenv("CS_DEBUG_SYNC");
-    return e != nullptr && atoi(e) != 0;
-  }();
-  return on;
-}
-
-void ok(hipError_t e, const char* what) {
-  if (e != hipSuccess) throw std::runtime_error(std::string("VggEngine: ") + what + ": " + hipGetErrorString(e));
-  if (debug_sync()) {
-    hipStream_t s = cur_stream();
-    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(s, &st) == hipSuccess && st == hipStreamCaptureStatusNone) {
-      hipError_t e2 = hipStreamSynchronize(s);
-      if (e2 == hipSuccess) e2 = hipGetLastError();
-      if (e2 != hipSuccess)
-        throw std::runtime_error(std::string("VggEngine [debug sync] after ") + what + ": " + hipGetErrorString(e2));
-    }
-  }
-}
-
-int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
-
-struct Dims {
-  int64_t M, N, K;
-};
-
-Dims dims(const VggBlock& b, int mode, int64_t B) {
-  const int64_t pix = B * b.H * b.H;
-  if (mode == CS_CONV_FWD) return {pix, b.cout, 9ll * b.cin};
-  if (mode == CS_CONV_DGRAD) return {pix, b.cin, 9ll * b.cout};
-  return {b.cout, 9ll * b.cin, pix};
-}
-
-// the split count cs_conv_gemm will actually use (it re-balances K-steps per split)
-int eff_splits(int64_t K, int splits, int bk) { return cs_conv_effective_splits((int)K, bk, splits); }
-
-// default tile before autotune: ~2 waves of 256 CUs, >= 8 K-steps per split
-ConvTile default_tile(const VggBlock& b, int mode, int64_t B) {
-  const Dims d = dims(b, mode, B);
-  ConvTile t;
-  t.bm = 64;
-  t.bn = 64;
-  const int64_t tiles = cdiv(d.M, 64) * cdiv(d.N, 64);
-  const int64_t ks = cdiv(d.K, 16);
-  int s = 1;
-  while (tiles * s < 512 && ks / (2 * s) >= 8 && (2 * s) * d.M * d.N <= kWsElems) s *= 2;
-  t.bk = 16;
-  t.splits = s;
-  return t;
-}
-
-}  // namespace
+using namespace vgg;
 
 VggEngine::VggEngine(int64_t Bmax, std::vector<int64_t> desc, std::vector<int64_t> offs,
                      std::vector<int64_t> buf_offs, int64_t feat, int64_t ncls, torch::Tensor params,
@@ -199,8 +135,8 @@ VggEngine::VggEngine(int64_t Bmax, std::vector<int64_t> desc, std::vector<int64_
   }
   if (const char* e = getenv("CS_CONV_MATH")) math_ = atoi(e);
   if (const char* e = getenv("CS_DEBUG_SKIP")) debug_skip_ = atoi(e);
-  amax_ = torch::zeros({3 * L * CS_AMAX_SHARDS}, fo);
-  for (int64_t l = 0; l < L; ++l) wslot_.push_back((int)l);
+  TORCH_CHECK(L <= 32 && L <= CS_WB_MAX + 1, "VggEngine: at most ", CS_WB_MAX + 1, " blocks (F3 weight-bound tables)");
+  amax_ = torch::zeros({4 * L * CS_AMAX_SLOT}, fo);
   bn_part_ = torch::zeros({partmax}, fo);
   bn_coef_ = torch::zeros({cmax * 3}, fo);
   bn_eval_ = torch::zeros({2, cmax}, fo);
@@ -307,35 +243,8 @@ CsSgdTail VggEngine::sgd_tail_args(int64_t block) {
   t.wd = (float)hp_[2];
   t.damp = (float)hp_[3];
   t.first = sgd_first_ ? 1 : 0;
-  t.amax = sgd_amax(off, n);
+  t.wb = sgd_wb(off, n);
   return t;
-}
-
-float* VggEngine::sgd_amax(int64_t off, int64_t n) {
-  if (!f3_used_ || f3_probe_) return nullptr;
-  int lo = -1;
-  for (int l = 0; l < (int)blocks_.size(); ++l)
-    if (blocks_[l].w_off >= off && blocks_[l].w_off < off + n) lo = lo < 0 ? l : std::min(lo, l);
-  if (lo < 0) return nullptr;
-  for (int l = 0; l < (int)blocks_.size(); ++l)
-    if (blocks_[l].w_off >= off && blocks_[l].w_off < off + n) wslot_[l] = lo;
-  return amax_slot(lo);
-}
-
-void VggEngine::f3_refresh(hipStream_t s) {
-  if (!f3_used_ || f3_probe_) return;
-  const int L = (int)blocks_.size();
-  if (w_dirty_) {
-    ok(hipMemsetAsync(amax_slot(0), 0, (size_t)L * CS_AMAX_SHARDS * sizeof(float), s), "amax(w) reset");
-    for (int l = 1; l < L; ++l) {
-      const VggBlock& b = blocks_[l];
-      ok(cs_amax(P(b.w_off), (int64_t)b.cout * 9 * b.cin, amax_slot(l), s), "amax(w)");
-      wslot_[l] = l;
-    }
-    w_dirty_ = false;
-  }
-  // x / dz bounds are per step: folded in by this step's BN apply / backward launches
-  ok(hipMemsetAsync(amax_x(0), 0, (size_t)2 * L * CS_AMAX_SHARDS * sizeof(float), s), "amax(x, dz) reset");
 }
 
 CsBnRed VggEngine::ered_args(int l, int B) {
@@ -389,7 +298,9 @@ void VggEngine::forward_train(int64_t B) {
   const int L = (int)blocks_.size();
   red_pending_ = -1;
   flush_signal(s);
-  f3_refresh(s);
+  // the per-step bounds are reset by the conv0 forward launch when it runs first (no extra launch)
+  const bool zero_in_conv0 = conv0_direct_ok(B) && !(debug_skip_ & 8);
+  f3_refresh(s, zero_in_conv0);
   // one launch: sampler index (device cursor into the epoch permutation, or idx_ when no
   // permutation is set), label gather, crop/flip/normalize into block 0's NHWC input
   const bool use_perm = perm_len_ > 0;
@@ -415,13 +326,18 @@ void VggEngine::forward_train(int64_t B) {
     const ConvTile& t = b.tile[CS_CONV_FWD];
     float* bn = b.bn.data_ptr<float>();
     if (l == defer_block_) join_deferred(s);  // the previous step's deferred buckets wrote these weights
+    if ((w_deferred_ >> l) & 1u) {  // ... and their bounds (the join above, or an earlier join_lag)
+      join_deferred(s);
+      rotate_w(s, w_deferred_);
+    }
     float* out = (l + 1 < L) ? blocks_[l + 1].x.data_ptr<float>() : feats_.data_ptr<float>();
     if (!(debug_skip_ & 8)) {
       const int64_t M = B * b.H * b.H;
       int rows;
       if (l == 0 && conv0_direct_ok(B)) {
         ok(cs_conv0_fwd(b.x.data_ptr<float>(), P(b.w_off), P(b.b_off), b.y.data_ptr<float>(), b.stats.data_ptr<float>(),
-                        (int)B, b.H, b.H, b.cout, s, batch_fold ? &bsrc : nullptr),
+                        (int)B, b.H, b.H, b.cout, s, batch_fold ? &bsrc : nullptr, bounds_to_zero(), 2 * L,
+                        rot_mask_ ? amax_w(0) : nullptr, amax_wnext(0), rot_mask_),
            "conv0_fwd");
         rows = cs_conv0_tile_rows();
       } else {
@@ -643,21 +559,23 @@ VggEngine::~VggEngine() {
 
 void VggEngine::sgd_on(hipStream_t st, int64_t off, int64_t n, bool cursor) {
   if (n == 0) return;
+  const CsWeightBounds wb = sgd_wb(off, n);
   ok(cs_sgd_flat(P(off), G(off), mom_.data_ptr<float>() + off, n, (float)hp_[0], (float)hp_[1], (float)hp_[2],
                  (float)hp_[3], 1.0f, sgd_first_ ? 1 : 0, st,
-                 cursor && perm_len_ > 0 ? cursor_.data_ptr<int64_t>() : nullptr, sgd_amax(off, n)),
+                 cursor && perm_len_ > 0 ? cursor_.data_ptr<int64_t>() : nullptr, &wb),
      "sgd_flat(block)");
 }
 
 void VggEngine::sgd(double lr, double momentum, double wd, double dampening, int64_t off, int64_t n) {
   TORCH_CHECK(off >= 0 && n >= 0 && off + n <= params_.numel(), "sgd: range");
   if (n == 0) return;
+  const CsWeightBounds wb = sgd_wb(off, n);
   // first step (set_sgd_first): buf = d, torch's clone — with dampening 0 bit-equal to the
   // 0*mom + (1-damp)*d of later steps. The step's one optimizer launch also advances the
   // device-side batch cursor
   ok(cs_sgd_flat(P(off), G(off), mom_.data_ptr<float>() + off, n, (float)lr, (float)momentum, (float)wd,
                  (float)dampening, 1.0f, sgd_first_ ? 1 : 0, cur_stream(),
-                 perm_len_ > 0 ? cursor_.data_ptr<int64_t>() : nullptr, sgd_amax(off, n)),
+                 perm_len_ > 0 ? cursor_.data_ptr<int64_t>() : nullptr, &wb),
      "sgd_flat");
   sgd_first_ = false;
 }
@@ -875,7 +793,9 @@ void VggEngine::step_impl(int64_t B, DeviceComm* comm, const std::vector<int64_t
       // from here, behind the last bucket on the comm stream; the next forward joins them
       for (size_t k : deferred) {
         comm->all_reduce(G(bucket_ranges[2 * k]), bucket_ranges[2 * k + 1], ncclFloat32, ncclAvg, s, /*fork=*/true);
+        sgd_deferring_ = true;
         sgd_on(comm->stream(), bucket_ranges[2 * k], bucket_ranges[2 * k + 1], false);
+        sgd_deferring_ = false;
         const int lo = (int)bucket_blocks[k];
         defer_block_ = defer_block_ < 0 ? lo : std::min(defer_block_, lo);
       }
@@ -897,128 +817,6 @@ void VggEngine::step_impl(int64_t B, DeviceComm* comm, const std::vector<int64_t
     in_step_ = false;
   }
   mark("sgd");
-}
-
-void VggEngine::set_f3_probe(bool on) {
-  f3_probe_ = on;
-  if (on) amax_.fill_(1.0f);
-}
-
-void VggEngine::set_tile(int64_t block, int64_t mode, int64_t bm, int64_t bn, int64_t splits, int64_t bk,
-                         int64_t stage) {
-  TORCH_CHECK(block >= 0 && block < (int64_t)blocks_.size() && mode >= 0 && mode <= 2, "set_tile: index");
-  TORCH_CHECK((bm == 64 || bm == 128) && (bn == 64 || bn == 128) && splits >= 1 && splits <= 1024, "set_tile: tile");
-  const Dims d = dims(blocks_[block], (int)mode, Bmax_);
-  const bool conv0_fwd = block == 0 && mode == CS_CONV_FWD && blocks_[0].cin == 4;
-  TORCH_CHECK((bk == 16 || bk == 32 || bk == 64) && cs_conv_stage_ok((int)stage, (int)bm, (int)bn, (int)bk, conv0_fwd) &&
-                  !(conv0_fwd && bk == 64),
-              "set_tile: no kernel for stage ", stage, " with a ", bm, "x", bn, " tile and bk ", bk);
-  // block 0's input has no producer-written bound (make_batch / the conv0 batch fold)
-  TORCH_CHECK(!(stage & CS_STAGE_F3) || block > 0, "set_tile: the F3 conv math is for blocks >= 1");
-  const int sp = eff_splits(d.K, (int)splits, (int)bk);
-  TORCH_CHECK(sp == 1 || (int64_t)sp * d.M * d.N <= ws_elems_, "set_tile: split-K workspace too small");
-  ConvTile& t = blocks_[block].tile[mode];
-  if ((stage & CS_STAGE_F3) && !f3_used_) {
-    f3_used_ = true;
-    w_dirty_ = true;
-  }
-  t.bm = (int)bm;
-  t.bn = (int)bn;
-  t.splits = (int)splits;
-  t.bk = (int)bk;
-  t.stage = (int)stage;
-  t.us = -1.f;
-}
-
-std::vector<int64_t> VggEngine::get_tile(int64_t block, int64_t mode) const {
-  TORCH_CHECK(block >= 0 && block < (int64_t)blocks_.size() && mode >= 0 && mode <= 2, "get_tile: index");
-  const ConvTile& t = blocks_[block].tile[mode];
-  return {t.bm, t.bn, t.splits, t.bk, t.stage};
-}
-
-void VggEngine::run_conv(int64_t block, int64_t mode, int64_t B) {
-  TORCH_CHECK(block >= 0 && block < (int64_t)blocks_.size() && mode >= 0 && mode <= 2, "run_conv: index");
-  TORCH_CHECK(!(block == 0 && mode == CS_CONV_DGRAD), "run_conv: no dgrad for block 0");
-  TORCH_CHECK(B > 0 && B <= Bmax_, "run_conv: B");
-  conv((int)block, (int)mode, (int)B, blocks_[block].tile[mode], cur_stream(), mode == CS_CONV_FWD);
-}
-
-std::vector<double> VggEngine::autotune(int64_t B, int64_t iters) {
-  TORCH_CHECK(B > 0 && B <= Bmax_ && iters >= 1, "autotune: args");
-  hipStream_t s = cur_stream();
-  hipEvent_t e0, e1;
-  ok(hipEventCreate(&e0), "event");
-  ok(hipEventCreate(&e1), "event");
-  std::vector<double> best_us;
-  const int split_opts[] = {1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 64, 128, 256};
-  for (int l = 0; l < (int)blocks_.size(); ++l) {
-    for (int mode = 0; mode < 3; ++mode) {
-      if (l == 0 && mode == CS_CONV_DGRAD) {
-        best_us.push_back(0.0);
-        continue;
-      }
-      const Dims d = dims(blocks_[l], mode, B);
-      ConvTile best = blocks_[l].tile[mode];
-      float best_t = 1e30f;
-      std::vector<std::vector<int>> seen;
-      const bool conv0_fwd = l == 0 && mode == CS_CONV_FWD && blocks_[0].cin == 4;
-      for (int stage : {(int)CS_STAGE_REGS, (int)CS_STAGE_LDS_DMA, (int)CS_STAGE_LDS_DMA_DEEP, (int)CS_STAGE_KG2,
-                        (int)CS_STAGE_KG4, CS_STAGE_X6 | CS_STAGE_REGS, CS_STAGE_X6 | CS_STAGE_LDS_DMA,
-                        CS_STAGE_X6 | CS_STAGE_LDS_DMA_DEEP, CS_STAGE_X6 | CS_STAGE_KG2, CS_STAGE_X6 | CS_STAGE_KG4,
-                        CS_STAGE_X6S | CS_STAGE_REGS, CS_STAGE_X6S | CS_STAGE_KG2, CS_STAGE_X6S | CS_STAGE_KG4,
-                        CS_STAGE_BF16 | CS_STAGE_REGS, CS_STAGE_BF16 | CS_STAGE_KG2, CS_STAGE_BF16 | CS_STAGE_KG4})
-      for (int bk : {16, 32, 64}) {
-        // CS_CONV_MATH: 0 = f32 MFMA kernels only, 1 = split-bf16 (X6) only, 2 = both (default),
-        // 3 = bf16 operands (reduced precision, opt-in; the padded conv0 forward stays f32)
-        const bool x6 = (stage & (CS_STAGE_X6 | CS_STAGE_X6S)) != 0;
-        const bool bf = (stage & CS_STAGE_BF16) != 0;
-        if (math_ == 3) {
-          if (!bf && !(conv0_fwd && stage == CS_STAGE_REGS)) continue;
-        } else if (bf || (x6 && math_ == 0) || (!x6 && math_ == 1)) {
-          continue;
-        }
-        if (bk == 64 && conv0_fwd) continue;
-        const int64_t ks = cdiv(d.K, bk);
-        for (int bm : {64, 128}) {
-          for (int bn : {64, 128}) {
-            if (!cs_conv_stage_ok(stage, bm, bn, bk, conv0_fwd)) continue;
-            for (int sp : split_opts) {
-              if (sp > 1 && ks / sp < 2) continue;
-              const int e = eff_splits(d.K, sp, bk);
-              if (e > 1 && (int64_t)e * d.M * d.N > ws_elems_) continue;
-              std::vector<int> key = {bm, bn, bk, e, stage};
-              if (std::find(seen.begin(), seen.end(), key) != seen.end()) continue;
-              seen.push_back(key);
-              ConvTile t;
-              t.bm = bm;
-              t.bn = bn;
-              t.bk = bk;
-              t.splits = sp;
-              t.stage = stage;
-              conv(l, mode, (int)B, t, s, mode == CS_CONV_FWD);  // warm
-              ok(hipEventRecord(e0, s), "record");
-              for (int64_t i = 0; i < iters; ++i) conv(l, mode, (int)B, t, s, mode == CS_CONV_FWD);
-              ok(hipEventRecord(e1, s), "record");
-              ok(hipEventSynchronize(e1), "sync");
-              float ms = 0.f;
-              ok(hipEventElapsedTime(&ms, e0, e1), "elapsed");
-              const float us = 1000.f * ms / (float)iters;
-              if (us < best_t) {
-                best_t = us;
-                best = t;
-              }
-            }
-          }
-        }
-      }
-      best.us = best_t;
-      blocks_[l].tile[mode] = best;
-      best_us.push_back(best_t);
-    }
-  }
-  hipEventDestroy(e0);
-  hipEventDestroy(e1);
-  return best_us;
 }
 
 }  // namespace cs

@@ -223,24 +223,34 @@ class VggEngine {
   // gbuf_: gradient ping-pong; ws_ / ws_w_: split-K slabs of the data / weight gradient (distinct:
   // the side stream's weight gradient runs beside the next data gradient); bn_part_: BN-backward partials
   torch::Tensor gbuf_[2], dz_[2], ws_, ws_w_, bn_part_, bn_coef_, bn_eval_, head_ws_;
-  // F3 operand bounds, CS_AMAX_SHARDS floats per slot: x of block l (slot l), dz of block l (L + l),
+  // F3 operand bounds, CS_AMAX_SLOT floats per slot: x of block l (slot l), dz of block l (L + l),
   // weights of block l (2L + l)
   torch::Tensor amax_;
   bool f3_probe_ = false;
-  float* amax_x(int l) { return amax_.data_ptr<float>() + (int64_t)l * CS_AMAX_SHARDS; }
-  float* amax_dz(int l) { return amax_.data_ptr<float>() + (int64_t)(blocks_.size() + l) * CS_AMAX_SHARDS; }
-  // the weights' bound is a running maximum folded in by every SGD launch that rewrites them, kept
-  // per SGD range (a block at world 1, a bucket at world > 1, the whole buffer for sgd()): wslot_[l]
-  // is the slot of the range that last updated block l (an upper bound of its weights)
-  std::vector<int> wslot_;
-  float* amax_slot(int slot) { return amax_.data_ptr<float>() + (int64_t)(2 * blocks_.size() + slot) * CS_AMAX_SHARDS; }
-  float* amax_w(int l) { return amax_slot(wslot_[l]); }
+  float* amax_x(int l) { return amax_.data_ptr<float>() + (int64_t)l * CS_AMAX_SLOT; }
+  float* amax_dz(int l) { return amax_.data_ptr<float>() + (int64_t)(blocks_.size() + l) * CS_AMAX_SLOT; }
+  // weight bounds, exact per conv weight tensor: the GEMMs read the current slot (2L + l); every
+  // SGD launch that rewrites block l's weights folds their new absolute maximum into the next slot
+  // (3L + l), whatever its range (CsWeightBounds); the step's first launch makes next current
+  // (cs_amax_rotate, folded into the conv0 forward) — for deferred buckets right before their block
+  float* amax_w(int l) { return amax_.data_ptr<float>() + (int64_t)(2 * blocks_.size() + l) * CS_AMAX_SLOT; }
+  float* amax_wnext(int l) { return amax_.data_ptr<float>() + (int64_t)(3 * blocks_.size() + l) * CS_AMAX_SLOT; }
+  unsigned w_pending_ = 0;     // blocks whose next weight bound an enqueued SGD launch is producing
+  unsigned w_deferred_ = 0;    // ... of those, the deferred buckets' (rotated after their join)
+  bool sgd_deferring_ = false; // step(): the SGD launches being enqueued belong to deferred buckets
+  void rotate_w(hipStream_t s, unsigned mask);
   bool f3_used_ = false;  // some conv tile runs the F3 math: the producers publish the bounds
+  void update_f3_used();
   bool w_dirty_ = true;   // the weights changed outside an SGD launch: re-measure their bounds
   float* x_amax_out(int l) { return f3_used_ && !f3_probe_ ? amax_x(l) : nullptr; }
   float* dz_amax_out(int l) { return f3_used_ && !f3_probe_ ? amax_dz(l) : nullptr; }
-  void f3_refresh(hipStream_t s);  // the step's / eval's entry: weight bounds if dirty, x / dz bounds zeroed
-  float* sgd_amax(int64_t off, int64_t n);  // the slot an SGD launch over [off, off + n) folds into
+  // the step's / eval's entry: weight bounds re-measured if dirty, else the last step's rotated in
+  // (all but deferred buckets'); x / dz bounds zeroed — or, zero_later, both by the conv0 forward,
+  // whose launch then takes bounds_to_zero() / rot_mask_
+  void f3_refresh(hipStream_t s, bool zero_later = false);
+  float* bounds_to_zero() { return f3_used_ && !f3_probe_ ? amax_x(0) : nullptr; }
+  unsigned rot_mask_ = 0;  // the weight-bound rotation the conv0 forward folds in (zero_later)
+  CsWeightBounds sgd_wb(int64_t off, int64_t n);  // the weight bounds an SGD launch over [off, off + n) produces
   int64_t ws_elems_ = 0;
   int math_ = 2;  // conv autotune candidates: 0 f32 MFMA, 1 split-bf16 X6, 2 both (CS_CONV_MATH)
   // 0 disables (CS_ENGINE_OFF=bn_fused). Measured on MI355X at B=64 (img/s): 0 -> 71.46k, 256 (blocks 6-7)

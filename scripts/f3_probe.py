@@ -42,7 +42,11 @@ def to_f3(tr) -> int:
 
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--arm", choices=["base", "f3probe", "f3"], default="base")
+    p.add_argument("--arm", default="base",
+                   help="base (the shipped table) | x6s (the v2 X6S table) | f3probe | f3 (X6S tiles on F3) | "
+                        "tuned (the tile table in --table, key --key)")
+    p.add_argument("--table", default="gpurun_out/tiles_tuned.json")
+    p.add_argument("--key", default="VGG11/B64/gfx950/tuned")
     p.add_argument("--steps", type=int, default=100)
     p.add_argument("--warmup", type=int, default=20)
     args = p.parse_args()
@@ -51,7 +55,16 @@ def main():
     torch.cuda.set_device(dev)
     tr = NativeTrainer(batch_size=64, device=dev)
     n = 0
-    if args.arm != "base":
+    if args.arm == "x6s":  # the round-5 v2 table (X6S maths)
+        args.arm, args.table, args.key = "tuned", os.path.join(ROOT, "cs744_pytorch_distributed_tutorial_amd", "runtime",
+                                                               "tiles_gfx950.json"), "VGG11/B64/gfx950/v2"
+    if args.arm == "tuned":
+        with open(args.table) as f:
+            ent = json.load(f)[args.key]
+        for t in ent["tiles"]:
+            tr.engine.set_tile(*t[:6], t[6] if len(t) > 6 else 0)
+        n = sum(1 for t in ent["tiles"] if len(t) > 6 and t[6] & F3)
+    elif args.arm != "base":
         n = to_f3(tr)
         if args.arm == "f3probe":
             tr.engine.set_f3_probe(True)

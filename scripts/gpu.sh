@@ -16,6 +16,9 @@
 #                              never combined with other trace domains) -> scripts/pmc_summary.py
 #   extras                     part1 batch (B=256), stock PyTorch-ROCm baseline, ResNet-50, Llama-3-8B
 #   projection                 N>1 projection with the RCCL CTA budget priced (a model)
+#   ramp [STEPS]               start-up ramp per kernel: kernel trace + one GRBM/SQ counter pass
+#   ahead TAG [args]           kernel-trace timeline of steps enqueued behind a device sleep, so the
+#                              profiler's per-dispatch host cost does not open gaps (step_trace_ahead.py)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}" || exit 1
 mkdir -p gpurun_out
@@ -74,6 +77,32 @@ case "$what" in
     python3 scripts/pmc_summary.py gpurun_out/$TAG > gpurun_out/${TAG}_summary.txt 2>&1
     head -40 gpurun_out/${TAG}_summary.txt
     ;;
+  ramp)
+    # start-up ramp, kernel by kernel: one long run under a kernel trace (scripts/ramp_table.py),
+    # then one counter pass (GRBM_GUI_ACTIVE, SQ_BUSY_CYCLES; kernel trace only) over the same run
+    # (scripts/ramp_pmc.py)
+    N=${1:-230}
+    page_in
+    (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace -d $R/gpurun_out/ramp -o run -- \
+      python3 $R/scripts/ramp_run.py --steps $N > $R/gpurun_out/ramp.log 2>&1)
+    rc=$?; echo "trace rc=$rc"; [ $rc -eq 0 ] || exit $rc
+    python3 scripts/ramp_table.py gpurun_out/ramp > gpurun_out/ramp_table.txt 2>&1; head -30 gpurun_out/ramp_table.txt
+    (cd /tmp && timeout -s KILL 240 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_BUSY_CYCLES --kernel-trace --output-format csv \
+      -d $R/gpurun_out/ramp_pmc -o run -- python3 $R/scripts/ramp_run.py --steps $N > $R/gpurun_out/ramp_pmc.log 2>&1)
+    rc=$?; echo "pmc rc=$rc"; [ $rc -eq 0 ] || exit $rc
+    python3 scripts/ramp_pmc.py gpurun_out/ramp_pmc --steps $N > gpurun_out/ramp_pmc.txt 2>&1; head -30 gpurun_out/ramp_pmc.txt
+    ;;
+  ahead)
+    TAG=${1:-ahead}; shift || true
+    page_in
+    (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace -d $R/gpurun_out/$TAG -o run -- \
+      python3 $R/scripts/step_trace_ahead.py "$@" > $R/gpurun_out/$TAG.log 2>&1)
+    rc=$?; echo "rocprofv3 rc=$rc"; grep '^{' gpurun_out/$TAG.log || true
+    [ $rc -eq 0 ] || exit $rc
+    python3 scripts/step_timeline.py gpurun_out/$TAG --last 10 > gpurun_out/${TAG}_timeline.txt 2>&1
+    head -14 gpurun_out/${TAG}_timeline.txt
+    grep -E "^## queue|^# queue|^# main" gpurun_out/${TAG}_timeline.txt || true
+    ;;
   extras)
     # end-of-round side measurements (each its own bench.py process, JSON lines appended to
     # gpurun_out/extras.jsonl): the tutorial's part1 batch (B=256, master/part1/part1.py:17), the
@@ -93,6 +122,6 @@ case "$what" in
     cut -c1-220 gpurun_out/projection.jsonl
     ;;
   *)
-    echo "usage: bash scripts/gpu.sh suite|tests|bench|trace|pmc|extras|projection ..."; exit 2
+    echo "usage: bash scripts/gpu.sh suite|tests|bench|trace|ahead|pmc|ramp|extras|projection ..."; exit 2
     ;;
 esac

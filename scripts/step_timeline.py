@@ -3,7 +3,9 @@
 start / end offset from the step's first kernel, plus per-queue busy time and the critical
 (main-queue) idle gaps. A step = [the second-to-last step-head dispatch, the last one): make_batch, or
 the conv0 forward when the batch is built inside it (round 5's fold).
-Usage: python scripts/step_timeline.py <rocprofv3 out dir> [--names 48]"""
+With --last K, first a per-step table of the last K steps (span, main-queue busy and idle); run
+under scripts/step_trace_ahead.py for steps whose gaps are the schedule's, not the profiled host's.
+Usage: python scripts/step_timeline.py <rocprofv3 out dir> [--names 48] [--last 10]"""
 import argparse
 import collections
 import glob
@@ -34,6 +36,7 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("path")
     p.add_argument("--names", type=int, default=56)
+    p.add_argument("--last", type=int, default=0)
     a = p.parse_args()
     rows = load(a.path)
     mb = [i for i, r in enumerate(rows) if "make_batch" in r["name"]]
@@ -42,6 +45,21 @@ def main():
     if len(mb) < 2:
         print("need two make_batch dispatches")
         return
+    if a.last:
+        print(f"# last {a.last} steps: span / main-queue busy / main-queue idle between its dispatches (us)")
+        tot = [0.0, 0.0, 0.0]
+        sel = list(zip(mb, mb[1:]))[-a.last:]
+        for i0, i1 in sel:
+            st = rows[i0:i1]
+            mq = [r for r in st if r["q"] == st[0]["q"]]
+            span = (rows[i1]["start"] - st[0]["start"]) / 1e3
+            busy = sum(r["end"] - r["start"] for r in mq) / 1e3
+            idle = sum(max(0, b["start"] - e["end"]) for e, b in zip(mq, mq[1:])) / 1e3
+            idle += max(0, rows[i1]["start"] - mq[-1]["end"]) / 1e3
+            tot = [tot[0] + span, tot[1] + busy, tot[2] + idle]
+            print(f"  {span:8.1f} {busy:8.1f} {idle:8.1f}")
+        n = len(sel)
+        print(f"# mean  {tot[0] / n:8.1f} {tot[1] / n:8.1f} {tot[2] / n:8.1f}\n")
     step = rows[mb[-2]:mb[-1]]
     t0 = step[0]["start"]
     span = (rows[mb[-1]]["start"] - t0) / 1e3

@@ -100,7 +100,7 @@ def test_cpp_ddp_step_multi_rank_staged_bench_config(gpu):
     steps = 4
     nat = run_world(_train, 2, "ddp", "none", steps, "staged", 64, True)
     ref = run_world(_train, 2, "ddp", "segments", steps, "torch", 64, True)
-    assert nat[0]["tiles"] in ("shipped", "shipped-dp") and "x6s" in nat[0]["maths"], (nat[0]["tiles"], nat[0]["maths"])
+    assert nat[0]["tiles"] == "shipped" and "f3" in nat[0]["maths"], (nat[0]["tiles"], nat[0]["maths"])
     assert nat[0]["kind"] == "staged"
     for k in ("params", "mom", "bufs", "nbt"):
         assert torch.equal(nat[1][k], nat[0][k]), k
