@@ -52,6 +52,21 @@ def main():
         conf = v.get("SQ_LDS_BANK_CONFLICT", 0) / lds if lds else float("nan")
         print(f"{short(k):60s} {ndisp.get(k,0):4d} {mfma:6.1f} {100*v.get('SQ_WAIT_ANY',0)/wc:6.1f} "
               f"{100*v.get('SQ_WAIT_INST_ANY',0)/wc:6.1f} {100*v.get('SQ_ACTIVE_INST_ANY',0)/wc:7.1f} {conf:11.2f} {l2:6.1f}")
+    mix = [(k, v) for k, v in rows if v.get("SQ_INSTS_MFMA", 0) > 0]
+    if mix:
+        # instruction mix per MFMA (F3 issues 3 MFMAs per 32x32x16 product step, X6S 6: compare the
+        # per-dispatch VALU count too, not only the ratio)
+        print()
+        print(f"{'kernel':60s} {'n':>4s} {'mfma%':>6s} {'valu/mfma':>9s} {'lds/mfma':>8s} {'vmem/mfma':>9s} "
+              f"{'waitLDS%':>8s} {'kVALU/disp':>10s} {'kMFMA/disp':>10s}")
+        for k, v in mix:
+            mf = v["SQ_INSTS_MFMA"]
+            gui = v.get("GRBM_GUI_ACTIVE", 0)
+            util = 100.0 * v.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) / (gui * 128) if gui else float("nan")
+            wc = v.get("SQ_WAVE_CYCLES", 0) or 1
+            print(f"{short(k):60s} {ndisp.get(k, 0):4d} {util:6.1f} {v.get('SQ_INSTS_VALU', 0) / mf:9.2f} "
+                  f"{v.get('SQ_INSTS_LDS', 0) / mf:8.2f} {v.get('SQ_INSTS_VMEM_RD', 0) / mf:9.2f} "
+                  f"{100 * v.get('SQ_WAIT_INST_LDS', 0) / wc:8.1f} {v.get('SQ_INSTS_VALU', 0) / 1e3:10.1f} {mf / 1e3:10.1f}")
     print()
     print("raw per-dispatch averages:")
     for k, v in rows[:12]:

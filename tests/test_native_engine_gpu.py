@@ -520,3 +520,30 @@ def test_conv0_folds_bitwise(dev):
     for combo, r in zip(combos[1:], runs[1:]):
         for k, (a, b) in enumerate(zip(runs[0], r)):
             assert torch.equal(a.cpu(), b.cpu()), (combo, k)
+
+
+def test_f3_operand_bounds_are_the_exact_maxima(dev):
+    """The F3 GEMMs scale each operand by a power of two taken from the bound its producer
+    published (csrc/runtime/vgg_bounds.cpp): after real steps at the bench batch, every bound the
+    engine holds is exactly the absolute maximum of the tensor it stands for — activations (the
+    block inputs, from BN apply / pool), dZ (from the BN backward) and the updated conv weights
+    (from SGD, the slot the next step makes current)."""
+    tr = _trainer(dev, batch_size=64, train_size=512, autotune=True)  # the shipped v3 table
+    assert sum(t["math"] == "f3" for t in tr.tile_table()) >= 18
+    for _ in range(3):
+        tr.step()
+    torch.cuda.synchronize()
+    L, B = tr.layout.L, 64
+    bound = tr.engine.amax().view(-1, 64, 32)[:, :, 0].max(dim=1).values.cpu()  # slot -> max over shards
+    for l in range(1, L):
+        s = tr.layout.specs[l]
+        x = tr.engine.tensor(l, "x").reshape(-1)[: B * s.hw * s.hw * s.cin]
+        assert bound[l].item() == x.abs().max().item(), ("x", l)
+        w = tr.layout.view(tr.params, f"layers.{s.conv_idx}.weight")
+        assert bound[3 * L + l].item() == w.abs().max().item(), ("w", l)
+    # the dZ ping-pong buffers end the backward holding blocks 1 and 2 (block 0's dZ is never written)
+    for l in (1, 2):
+        s = tr.layout.specs[l]
+        dz = tr.engine.tensor(l, "dz").reshape(-1)[: B * s.hw * s.hw * s.cout]
+        assert bound[L + l].item() == dz.abs().max().item() > 0, ("dz", l)
+    tr.close()
