@@ -780,12 +780,20 @@ __device__ __forceinline__ void gemm_body(const CsConvArgs& a, const int tile, c
       store_xs<BM, BN, MODE, BK, C4, KG, 0, NP>(ld, l0, l0 + X::A16, oa, ob, sa, sb);
     }
     __syncthreads();
-    for (int t = 0; t < nks; t += 2) {
+    // one exit: an odd last K-step is peeled after the loop instead of a break between the
+    // halves (with two exits hipcc kept the accumulator in different registers at each and
+    // copied it inside the loop, behind an MFMA-result stall)
+    int t = 0;
+    for (; t + 1 < nks; t += 2) {
       kstep_xs<BM, BN, MODE, BK, 0, 1, C4, KG, NP>(ld, a, l0, l1, acc, wm, wn, kg, (ks_begin + t + 2) * BK, oa, ob,
                                                    sa, sb);
       __syncthreads();
-      if (t + 1 >= nks) break;
       kstep_xs<BM, BN, MODE, BK, 1, 0, C4, KG, NP>(ld, a, l1, l0, acc, wm, wn, kg, (ks_begin + t + 3) * BK, oa, ob,
+                                                   sa, sb);
+      __syncthreads();
+    }
+    if (t < nks) {
+      kstep_xs<BM, BN, MODE, BK, 0, 1, C4, KG, NP>(ld, a, l0, l1, acc, wm, wn, kg, (ks_begin + t + 2) * BK, oa, ob,
                                                    sa, sb);
       __syncthreads();
     }
@@ -809,18 +817,26 @@ __device__ __forceinline__ void gemm_body(const CsConvArgs& a, const int tile, c
     ld.template store<0>(lds0, lds0 + T::A_ELEMS);
   }
   __syncthreads();
-  // even step t: tile t in lds0, tile t+1 in registers[1] -> lds1, tile t+2 -> registers[0]
-  for (int t = 0; t < nks; t += 2) {
+  // even step t: tile t in lds0, tile t+1 in registers[1] -> lds1, tile t+2 -> registers[0];
+  // one loop exit, an odd last step peeled (as in the split-operand loop above)
+  int t = 0;
+  for (; t + 1 < nks; t += 2) {
     if constexpr (SCHED == 2)
       kstep_x6<BM, BN, MODE, BK, 0, 1, C4, KG>(ld, a, lds0, lds1, acc, wm, wn, r, hh, kg, (ks_begin + t + 2) * BK);
     else
       kstep<BM, BN, MODE, BK, SCHED, 0, 1, C4, KG>(ld, a, lds0, lds1, acc, wm, wn, r, hh, kg, (ks_begin + t + 2) * BK);
     __syncthreads();
-    if (t + 1 >= nks) break;
     if constexpr (SCHED == 2)
       kstep_x6<BM, BN, MODE, BK, 1, 0, C4, KG>(ld, a, lds1, lds0, acc, wm, wn, r, hh, kg, (ks_begin + t + 3) * BK);
     else
       kstep<BM, BN, MODE, BK, SCHED, 1, 0, C4, KG>(ld, a, lds1, lds0, acc, wm, wn, r, hh, kg, (ks_begin + t + 3) * BK);
+    __syncthreads();
+  }
+  if (t < nks) {
+    if constexpr (SCHED == 2)
+      kstep_x6<BM, BN, MODE, BK, 0, 1, C4, KG>(ld, a, lds0, lds1, acc, wm, wn, r, hh, kg, (ks_begin + t + 2) * BK);
+    else
+      kstep<BM, BN, MODE, BK, SCHED, 0, 1, C4, KG>(ld, a, lds0, lds1, acc, wm, wn, r, hh, kg, (ks_begin + t + 2) * BK);
     __syncthreads();
   }
   }

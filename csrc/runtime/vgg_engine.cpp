@@ -149,6 +149,7 @@ torch::Tensor VggEngine::tensor(int64_t block, const std::string& name) const {
   if (name == "g1") return gbuf_[1];
   if (name == "dz") return dz_[block & 1];
   TORCH_CHECK(block >= 0 && block < (int64_t)blocks_.size(), "tensor: block index");
+  if (name == "dz_blk") return dz_blk_[block];  // the overlapped backward's per-block dZ
   const VggBlock& b = blocks_[block];
   if (name == "x") return b.x;
   if (name == "y") return b.y;
