@@ -499,17 +499,28 @@ __device__ __forceinline__ int f3_exp(const float* amax) {
 }
 __device__ __forceinline__ float exp2i(int s) { return __builtin_bit_cast(float, (unsigned)(s + 127) << 23); }
 
+// One packed pair of the split: h = (fp16(x0*sc), fp16(x1*sc)) and l = (fp16(x0*sc - h0),
+// fp16(x1*sc - h1)), four v_fma_mix (f32 x and sc, f16 h picked by op_sel; mixlo / mixhi write
+// the low / high half). Each rounds the exact value once (x*sc is exact: sc is a power of two),
+// so the pieces are the ones the plain casts give. Left to itself hipcc mixes v_pk_mul /
+// v_cvt_pk / unpack / re-pack sequences and element shuffles (6-7 VALU per pair, not 4).
+// Pure VALU on register operands: no memory, no hazard inside the statement.
+__device__ __forceinline__ void split_pair(float x0, float x1, float sc, unsigned& h, unsigned& l) {
+  asm("v_fma_mixlo_f16 %0, %2, %4, 0\n\t"
+      "v_fma_mixhi_f16 %0, %3, %4, 0\n\t"
+      "v_fma_mixlo_f16 %1, %2, %4, -%0 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %1, %3, %4, -%0 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+      : "=&v"(h), "=&v"(l)
+      : "v"(x0), "v"(x1), "v"(sc));
+}
+
 __device__ __forceinline__ void split2h(const float4 v, float sc, bf16x4& h, bf16x4& l) {
-  const float x[4] = {v.x * sc, v.y * sc, v.z * sc, v.w * sc};
-  f16x4 hv, lv;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const _Float16 hj = (_Float16)x[j];
-    hv[j] = hj;
-    lv[j] = (_Float16)(x[j] - (float)hj);
-  }
-  h = __builtin_bit_cast(bf16x4, hv);
-  l = __builtin_bit_cast(bf16x4, lv);
+  typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+  unsigned h0, h1, l0, l1;
+  split_pair(v.x, v.y, sc, h0, l0);
+  split_pair(v.z, v.w, sc, h1, l1);
+  h = __builtin_bit_cast(bf16x4, u32x2{h0, h1});
+  l = __builtin_bit_cast(bf16x4, u32x2{l0, l1});
 }
 
 template <int RM, int RN>
