@@ -65,6 +65,7 @@ void VggEngine::f3_refresh(hipStream_t s, bool zero_later) {
 }
 
 void VggEngine::set_f3_probe(bool on) {
+  if (!on && f3_probe_) w_dirty_ = true;  // the real weight bounds were not kept: re-measure them
   f3_probe_ = on;
   if (on) amax_.fill_(1.0f);
 }

@@ -61,6 +61,11 @@ def main():
         n = len(sel)
         print(f"# mean  {tot[0] / n:8.1f} {tot[1] / n:8.1f} {tot[2] / n:8.1f}\n")
     step = rows[mb[-2]:mb[-1]]
+    if a.last:  # the detail: the step of the window whose main queue idled least
+        i0, i1 = min(list(zip(mb, mb[1:]))[-a.last:], key=lambda p: (rows[p[1]]["start"] - rows[p[0]]["start"]) - sum(
+            r["end"] - r["start"] for r in rows[p[0]:p[1]] if r["q"] == rows[p[0]]["q"]))
+        step = rows[i0:i1]
+        mb = [i0, i1]
     t0 = step[0]["start"]
     span = (rows[mb[-1]]["start"] - t0) / 1e3
     byq = collections.defaultdict(list)
